@@ -1,0 +1,392 @@
+// C-ABI entry points (include/diffopt_mi355x.h).  Every function catches the
+// engine's exceptions and maps them onto the header's return-code contract.
+#include <chrono>
+#include <cstring>
+
+#include "dopt_internal.h"
+
+using dopt::DevBuf;
+using dopt::Error;
+using dopt::Handle;
+
+struct dopt_handle : public Handle {};
+
+namespace {
+
+template <class F>
+int guarded(dopt_handle* h, F&& f) {
+  if (!h) return -1;
+  try {
+    h->err.clear();
+    DOPT_CHECK_HIP(hipSetDevice(h->device));
+    return f();
+  } catch (const Error& e) {
+    h->err = e.msg;
+    return e.code;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return -3;
+  }
+}
+
+// Host mode: copy `count` doubles of `src` into `buf`; device mode: borrow.
+const double* stage_in(Handle& h, DevBuf& buf, const double* src, size_t count) {
+  if (!src) return nullptr;
+  if (h.mem == DOPT_MEM_DEVICE) return src;
+  buf.ensure(count * sizeof(double));
+  if (count)
+    DOPT_CHECK_HIP(hipMemcpyAsync(buf.p, src, count * sizeof(double), hipMemcpyHostToDevice, h.stream));
+  return buf.as<double>();
+}
+
+double* out_ptr(Handle& h, DevBuf& buf, double* dst, size_t count) {
+  if (!dst) return nullptr;
+  if (h.mem == DOPT_MEM_DEVICE) return dst;
+  buf.ensure(count * sizeof(double));
+  return buf.as<double>();
+}
+
+void copy_out(Handle& h, double* dst, const double* dev, size_t count) {
+  if (!dst || h.mem == DOPT_MEM_DEVICE || !count) return;
+  DOPT_CHECK_HIP(hipMemcpyAsync(dst, dev, count * sizeof(double), hipMemcpyDeviceToHost, h.stream));
+}
+
+int first_info(Handle& h) {
+  std::vector<dopt::QPMeta> meta(h.batch);
+  DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h.meta.p, h.batch * sizeof(dopt::QPMeta),
+                                hipMemcpyDeviceToHost, h.stream));
+  DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+  for (auto& mm : meta)
+    if (!mm.iterative && mm.info > 0) return mm.info;
+  return 0;
+}
+
+struct Timer {
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  double s() const {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int dopt_abi_version(void) { return DOPT_ABI_VERSION; }
+
+int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t m,
+                int32_t p, int32_t kind) {
+  if (!out) return -1;
+  *out = nullptr;
+  if (batch < 0 || n < 0 || m < 0 || p < 0 || (kind != DOPT_KIND_QP && kind != DOPT_KIND_CONIC))
+    return -1;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -4;
+  if (device < 0 || device >= ndev) return -1;
+  auto* h = new dopt_handle();
+  h->device = device;
+  h->batch = batch;
+  h->n = n;
+  h->m = m;
+  h->p = p;
+  h->kind = kind;
+  int rc = guarded(h, [&]() {
+    DOPT_CHECK_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    h->own_stream = true;
+    if (kind == DOPT_KIND_QP) {
+      h->nmax = n + m + p;
+      h->ld = (int32_t)dopt::round_up(std::max(h->nmax, 1), 8);
+      h->K.ensure((size_t)batch * h->nmax * h->ld * sizeof(double));
+      h->ipiv.ensure((size_t)batch * std::max(h->nmax, 1) * sizeof(int32_t));
+      h->s.ensure((size_t)batch * std::max(m, 1) * sizeof(double));
+      h->kidx.ensure((size_t)2 * batch * std::max(m, 1) * sizeof(int32_t));
+      h->meta.ensure((size_t)std::max<int64_t>(batch, 1) * sizeof(dopt::QPMeta));
+      h->rhs.ensure((size_t)2 * batch * std::max(h->nmax, 1) * sizeof(double));
+      h->x.ensure((size_t)batch * std::max(h->nmax, 1) * sizeof(double));
+    }
+    return 0;
+  });
+  if (rc != 0) {
+    dopt_destroy(h);
+    return rc;
+  }
+  *out = h;
+  return 0;
+}
+
+int dopt_destroy(dopt_handle* h) {
+  if (!h) return 0;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  DevBuf* bufs[] = {&h->K, &h->ipiv, &h->s, &h->kidx, &h->meta, &h->rhs, &h->x, &h->cone_dev,
+                    &h->vp, &h->dpi, &h->M, &h->cwork, &h->cinfo};
+  for (auto* b : bufs) b->release();
+  for (auto& b : h->own_in) b.release();
+  for (auto& b : h->own_cin) b.release();
+  for (auto& b : h->tin) b.release();
+  for (auto& b : h->tout) b.release();
+  if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return 0;
+}
+
+const char* dopt_last_error(const dopt_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+int dopt_set_stream(dopt_handle* h, void* stream) {
+  return guarded(h, [&]() {
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    if (h->own_stream && h->stream) DOPT_CHECK_HIP(hipStreamDestroy(h->stream));
+    h->own_stream = false;
+    h->stream = static_cast<hipStream_t>(stream);  // NULL = legacy default stream
+    return 0;
+  });
+}
+
+int dopt_set_memory(dopt_handle* h, int32_t mem) {
+  return guarded(h, [&]() {
+    if (mem != DOPT_MEM_HOST && mem != DOPT_MEM_DEVICE) throw Error(-1, "bad memory mode");
+    h->mem = mem;
+    return 0;
+  });
+}
+
+int dopt_qp_set(dopt_handle* h, const double* Q, const double* G, const double* hv,
+                const double* A, const double* z, const double* lam, const double* nu) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_set on a non-QP handle");
+    const size_t B = h->batch, n = h->n, m = h->m, p = h->p;
+    if (!Q || !z) throw Error(-1, "Q and z are required");
+    if (m && (!G || !hv || !lam)) throw Error(-1, "G, h and lam are required when m > 0");
+    if (p && (!A || !nu)) throw Error(-1, "A and nu are required when p > 0");
+    h->Q = stage_in(*h, h->own_in[0], Q, B * n * n);
+    h->G = m ? stage_in(*h, h->own_in[1], G, B * m * n) : nullptr;
+    h->hv = m ? stage_in(*h, h->own_in[2], hv, B * m) : nullptr;
+    h->A = p ? stage_in(*h, h->own_in[3], A, B * p * n) : nullptr;
+    h->z = stage_in(*h, h->own_in[4], z, B * n);
+    h->lam = m ? stage_in(*h, h->own_in[5], lam, B * m) : nullptr;
+    h->nu = p ? stage_in(*h, h->own_in[6], nu, B * p) : nullptr;
+    h->set = true;
+    h->factored = false;
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  });
+}
+
+int dopt_qp_factor(dopt_handle* h) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_factor on a non-QP handle");
+    dopt::qp_factor(*h);
+    return first_info(*h);
+  });
+}
+
+int dopt_qp_reverse(dopt_handle* h, const double* dl_dz, double* out) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_reverse on a non-QP handle");
+    if (!dl_dz || !out) throw Error(-1, "dl_dz and out are required");
+    Timer tm;
+    const size_t B = h->batch, n = h->n, L = h->n + h->m + h->p;
+    const double* d = stage_in(*h, h->tin[0], dl_dz, B * n);
+    double* o = out_ptr(*h, h->tout[0], out, B * L);
+    dopt::qp_reverse(*h, d, o);
+    copy_out(*h, out, o, B * L);
+    const int rc = first_info(*h);
+    h->last_time = tm.s();
+    return rc;
+  });
+}
+
+int dopt_qp_forward(dopt_handle* h, const double* dQ, const double* dq, const double* dG,
+                    const double* dh, const double* dA, const double* db, double* out) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_forward on a non-QP handle");
+    if (!out) throw Error(-1, "out is required");
+    Timer tm;
+    const size_t B = h->batch, n = h->n, m = h->m, p = h->p, L = n + m + p;
+    const double* a = stage_in(*h, h->tin[1], dQ, B * n * n);
+    const double* b = stage_in(*h, h->tin[2], dq, B * n);
+    const double* c = stage_in(*h, h->tin[3], dG, B * m * n);
+    const double* d = stage_in(*h, h->tin[4], dh, B * m);
+    const double* e = stage_in(*h, h->tin[5], dA, B * p * n);
+    const double* f = stage_in(*h, h->tin[6], db, B * p);
+    double* o = out_ptr(*h, h->tout[1], out, B * L);
+    dopt::qp_forward(*h, a, b, c, d, e, f, o);
+    copy_out(*h, out, o, B * L);
+    const int rc = first_info(*h);
+    h->last_time = tm.s();
+    return rc;
+  });
+}
+
+int dopt_qp_forward_reverse(dopt_handle* h, const double* dl_dz, const double* dQ,
+                            const double* dq, const double* dG, const double* dh,
+                            const double* dA, const double* db, double* out_rev,
+                            double* out_fwd) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_forward_reverse on a non-QP handle");
+    if (!dl_dz || !out_rev || !out_fwd) throw Error(-1, "dl_dz, out_rev and out_fwd are required");
+    Timer tm;
+    const size_t B = h->batch, n = h->n, m = h->m, p = h->p, L = n + m + p;
+    const double* r = stage_in(*h, h->tin[0], dl_dz, B * n);
+    const double* a = stage_in(*h, h->tin[1], dQ, B * n * n);
+    const double* b = stage_in(*h, h->tin[2], dq, B * n);
+    const double* c = stage_in(*h, h->tin[3], dG, B * m * n);
+    const double* d = stage_in(*h, h->tin[4], dh, B * m);
+    const double* e = stage_in(*h, h->tin[5], dA, B * p * n);
+    const double* f = stage_in(*h, h->tin[6], db, B * p);
+    double* o1 = out_ptr(*h, h->tout[0], out_rev, B * L);
+    double* o2 = out_ptr(*h, h->tout[1], out_fwd, B * L);
+    h->factored = false;  // the fused path always re-factorises (one solve = factor + fwd + rev)
+    dopt::qp_forward_reverse(*h, r, a, b, c, d, e, f, o1, o2);
+    copy_out(*h, out_rev, o1, B * L);
+    copy_out(*h, out_fwd, o2, B * L);
+    const int rc = first_info(*h);
+    h->last_time = tm.s();
+    return rc;
+  });
+}
+
+int dopt_get_info(dopt_handle* h, int32_t* info) {
+  return guarded(h, [&]() {
+    if (!info) throw Error(-1, "info is required");
+    if (h->kind == DOPT_KIND_QP) {
+      std::vector<dopt::QPMeta> meta(h->batch);
+      DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h->meta.p, h->batch * sizeof(dopt::QPMeta),
+                                    hipMemcpyDeviceToHost, h->stream));
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+      for (int64_t i = 0; i < h->batch; ++i) info[i] = meta[i].iterative ? 0 : meta[i].info;
+    } else {
+      if (!h->cinfo.p) throw Error(-1, "no conic solve has run");
+      DOPT_CHECK_HIP(hipMemcpyAsync(info, h->cinfo.p, h->batch * sizeof(int32_t),
+                                    hipMemcpyDeviceToHost, h->stream));
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    }
+    return 0;
+  });
+}
+
+int dopt_get_iterative(dopt_handle* h, int8_t* flags) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "QP only");
+    if (!flags) throw Error(-1, "flags is required");
+    std::vector<dopt::QPMeta> meta(h->batch);
+    DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h->meta.p, h->batch * sizeof(dopt::QPMeta),
+                                  hipMemcpyDeviceToHost, h->stream));
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    for (int64_t i = 0; i < h->batch; ++i) flags[i] = (int8_t)meta[i].iterative;
+    return 0;
+  });
+}
+
+int dopt_get_system_size(dopt_handle* h, int32_t* sizes) {
+  return guarded(h, [&]() {
+    if (!sizes) throw Error(-1, "sizes is required");
+    if (h->kind == DOPT_KIND_QP) {
+      std::vector<dopt::QPMeta> meta(h->batch);
+      DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h->meta.p, h->batch * sizeof(dopt::QPMeta),
+                                    hipMemcpyDeviceToHost, h->stream));
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+      for (int64_t i = 0; i < h->batch; ++i) sizes[i] = meta[i].nsys;
+    } else {
+      if (!h->cinfo.p) throw Error(-1, "no conic solve has run");
+      DOPT_CHECK_HIP(hipMemcpyAsync(sizes, h->cinfo.as<int32_t>() + h->batch,
+                                    h->batch * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    }
+    return 0;
+  });
+}
+
+double dopt_last_time(const dopt_handle* h) { return h ? h->last_time : -1.0; }
+
+// ---- conic -----------------------------------------------------------------
+int dopt_conic_set(dopt_handle* h, const double* A, const double* b, const double* c,
+                   const double* x, const double* s, const double* y,
+                   const int32_t* cone_desc, int32_t ncones) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_CONIC) throw Error(-1, "dopt_conic_set on a non-conic handle");
+    const size_t B = h->batch, n = h->n, m = h->m;
+    if (!A || !b || !c || !x || !s || !y) throw Error(-1, "A, b, c, x, s, y are required");
+    if (ncones < 0 || (ncones > 0 && !cone_desc)) throw Error(-1, "bad cone table");
+    int64_t rows = 0;
+    for (int k = 0; k < ncones; ++k) {
+      const int code = cone_desc[2 * k], dim = cone_desc[2 * k + 1];
+      if (code < 0 || code > DOPT_CONE_PSD_TRI || dim < 0) throw Error(-1, "bad cone code/dimension");
+      if (code == DOPT_CONE_SOC && dim < 1) throw Error(-1, "SecondOrderCone dimension must be >= 1");
+      if (code == DOPT_CONE_PSD_TRI) {
+        int d = 0;
+        while (d * (d + 1) / 2 < dim) ++d;
+        if (d * (d + 1) / 2 != dim) throw Error(-1, "PSD triangle dimension is not triangular");
+        if (d > 64) throw Error(-1, "PSD cones larger than 64×64 are not supported");
+      }
+      rows += dim;
+    }
+    if (rows != (int64_t)m) throw Error(-1, "cone dimensions do not add up to m");
+    h->cones.assign(cone_desc, cone_desc + 2 * ncones);
+    h->cA = stage_in(*h, h->own_cin[0], A, B * m * n);
+    h->cb = stage_in(*h, h->own_cin[1], b, B * m);
+    h->cc = stage_in(*h, h->own_cin[2], c, B * n);
+    h->cx = stage_in(*h, h->own_cin[3], x, B * n);
+    h->cs = stage_in(*h, h->own_cin[4], s, B * m);
+    h->cy = stage_in(*h, h->own_cin[5], y, B * m);
+    h->cset = true;
+    h->cfactored = false;
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  });
+}
+
+int dopt_conic_factor(dopt_handle* h) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_CONIC) throw Error(-1, "dopt_conic_factor on a non-conic handle");
+    dopt::conic_factor(*h);
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  });
+}
+
+int dopt_conic_forward(dopt_handle* h, const double* dA, const double* db, const double* dc,
+                       double* out, double* out_dx) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_CONIC) throw Error(-1, "dopt_conic_forward on a non-conic handle");
+    if (!out) throw Error(-1, "out is required");
+    Timer tm;
+    const size_t B = h->batch, n = h->n, m = h->m, N = n + m + 1;
+    const double* a = stage_in(*h, h->tin[1], dA, B * m * n);
+    const double* b = stage_in(*h, h->tin[2], db, B * m);
+    const double* c = stage_in(*h, h->tin[3], dc, B * n);
+    double* o = out_ptr(*h, h->tout[0], out, B * N);
+    double* ox = out_ptr(*h, h->tout[1], out_dx, B * n);
+    dopt::conic_forward(*h, a, b, c, o, ox);
+    copy_out(*h, out, o, B * N);
+    copy_out(*h, out_dx, ox, B * n);
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    h->last_time = tm.s();
+    return 0;
+  });
+}
+
+int dopt_conic_reverse(dopt_handle* h, const double* dx, double* out_g, double* out_dA,
+                       double* out_db, double* out_dc) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_CONIC) throw Error(-1, "dopt_conic_reverse on a non-conic handle");
+    if (!dx || !out_g) throw Error(-1, "dx and out_g are required");
+    Timer tm;
+    const size_t B = h->batch, n = h->n, m = h->m, N = n + m + 1;
+    const double* d = stage_in(*h, h->tin[0], dx, B * n);
+    double* og = out_ptr(*h, h->tout[2], out_g, B * N);
+    double* oA = out_ptr(*h, h->tout[3], out_dA, B * m * n);
+    double* ob = out_ptr(*h, h->tout[4], out_db, B * m);
+    double* oc = out_ptr(*h, h->tout[5], out_dc, B * n);
+    dopt::conic_reverse(*h, d, og, oA, ob, oc);
+    copy_out(*h, out_g, og, B * N);
+    copy_out(*h, out_dA, oA, B * m * n);
+    copy_out(*h, out_db, ob, B * m);
+    copy_out(*h, out_dc, oc, B * n);
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    h->last_time = tm.s();
+    return 0;
+  });
+}
+
+}  // extern "C"

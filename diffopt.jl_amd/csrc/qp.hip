@@ -1,0 +1,918 @@
+// QP sensitivity path: KKT assembly, batched blocked LU (FP64 MFMA trailing
+// update), forward/transposed triangular solves, dense batched LSQR for the
+// `norm(Q) == 0` branch, and output recovery.  gfx950 (CDNA4) only.
+//
+// Reference: src/QuadraticProgram/QuadraticProgram.jl
+//   create_LHS_matrix :256-282   reverse_differentiate! :316-351
+//   forward_differentiate! :357-446   solve_system :486-496
+//
+// Layout in HBM (per problem b, fixed stride so every problem is independent):
+//   K     : nmax × ld doubles, ROW-major (row swaps are contiguous), ld % 8 == 0
+//   ipiv  : nmax int32 (absolute row index chosen for each column)
+//   s     : m doubles  (G z − h, Julia sparse-matvec summation order)
+//   kidx  : m int32 (kept inequality rows, ascending)  rpos: m int32 (row → kk | -1)
+//   meta  : QPMeta {nk, nsys, iterative, info}
+#include "dopt_internal.h"
+
+namespace dopt {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int TPB = 256;   // threads per workgroup (4 waves)
+constexpr int NB = 32;     // LU panel width
+constexpr int CW = 64;     // trailing-update column chunk
+constexpr int SMALL_LU_MAX = 512;  // max system size for the LDS-panel LU
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// block-wide sum; `red` = LDS scratch of >= 4 doubles; all threads get result
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  double r = red[0] + red[1] + red[2] + red[3];
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// 1. prepare: iterative flag, s = Gz − h, row classification + compaction.
+// One workgroup per problem.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(TPB) void qp_prepare_kernel(
+    const double* __restrict__ Q, const double* __restrict__ G,
+    const double* __restrict__ hv, const double* __restrict__ z,
+    const double* __restrict__ lam, int n, int m, int p,
+    double* __restrict__ s_out, int32_t* __restrict__ kidx_out,
+    int32_t* __restrict__ rpos_out, QPMeta* __restrict__ meta) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int wave_cnt[4];
+  __shared__ int base;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const double* Qb = Q + (size_t)b * n * n;
+  // `iterative = norm(Q) ≈ 0` (QuadraticProgram.jl:333): ≈ 0 is == 0; NaN → false
+  int nz = 0;
+  for (size_t i = t; i < (size_t)n * n; i += TPB) nz |= (Qb[i] != 0.0);
+  const int iterative = !__syncthreads_or(nz);
+  double* zs = smem;
+  for (int j = t; j < n; j += TPB) zs[j] = z[(size_t)b * n + j];
+  if (t == 0) base = 0;
+  __syncthreads();
+  const double* Gb = G + (size_t)b * m * n;
+  const int lane = t & 63, wv = t >> 6;
+  for (int i0 = 0; i0 < m; i0 += TPB) {
+    const int i = i0 + t;
+    int keep = 0;
+    if (i < m) {
+      // `G * z - h` as Julia's SparseMatrixCSC mul!: column-ordered, unfused.
+      double acc = 0.0;
+      for (int j = 0; j < n; ++j) acc = __dadd_rn(acc, __dmul_rn(Gb[i + (size_t)j * m], zs[j]));
+      const double si = __dsub_rn(acc, hv[(size_t)b * m + i]);
+      s_out[(size_t)b * m + i] = si;
+      const double li = lam[(size_t)b * m + i];
+      // exact elimination: λ_i == 0 and s_i != 0 decouples dλ_i
+      keep = iterative ? 1 : !(li == 0.0 && si != 0.0);
+    }
+    const unsigned long long ball = __ballot(keep);
+    const int prefix = __popcll(ball & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_cnt[wv] = __popcll(ball);
+    __syncthreads();
+    int off = base;
+    for (int w = 0; w < wv; ++w) off += wave_cnt[w];
+    if (i < m) {
+      if (keep) kidx_out[(size_t)b * m + off + prefix] = i;
+      rpos_out[(size_t)b * m + i] = keep ? off + prefix : -1;
+    }
+    __syncthreads();
+    if (t == 0) base += wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
+    __syncthreads();
+  }
+  if (t == 0) {
+    meta[b].nk = base;
+    meta[b].nsys = n + base + p;
+    meta[b].iterative = iterative;
+    meta[b].info = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 2. assemble the (reduced) KKT matrix, row-major, 32×32 tiles through LDS so
+// both the column-major sources and the row-major destination are coalesced.
+//   K = [Q, G_kᵀD(λ_k), Aᵀ; G_k, D(s_k), 0; A, 0, 0]   (QuadraticProgram.jl:276-280)
+// ---------------------------------------------------------------------------
+struct KKTSrc {
+  const double *Q, *G, *A, *lam, *s;
+  const int32_t* kidx;
+  int n, m, p, nk;
+};
+
+__device__ __forceinline__ double kkt_elem(const KKTSrc& S, int r, int c) {
+  const int n = S.n, nk = S.nk;
+  if (r < n) {
+    if (c < n) return S.Q[r + (size_t)c * n];
+    if (c < n + nk) {
+      const int i = S.kidx[c - n];
+      return S.G[i + (size_t)r * S.m] * S.lam[i];
+    }
+    return S.A[(c - n - nk) + (size_t)r * S.p];
+  }
+  if (r < n + nk) {
+    const int i = S.kidx[r - n];
+    if (c < n) return S.G[i + (size_t)c * S.m];
+    return (c == r) ? S.s[i] : 0.0;
+  }
+  if (c < n) return S.A[(r - n - nk) + (size_t)c * S.p];
+  return 0.0;
+}
+
+__global__ __launch_bounds__(TPB) void qp_assemble_kernel(
+    const double* __restrict__ Q, const double* __restrict__ G,
+    const double* __restrict__ A, const double* __restrict__ lam,
+    const double* __restrict__ s, const int32_t* __restrict__ kidx,
+    const QPMeta* __restrict__ meta, int n, int m, int p, int nmax, int ld,
+    int tiles_1d, double* __restrict__ K) {
+  __shared__ double tile[32][33];
+  const int b = blockIdx.y;
+  const int tr = blockIdx.x / tiles_1d, tc = blockIdx.x % tiles_1d;
+  const int N = meta[b].nsys;
+  const int r0 = tr * 32, c0 = tc * 32;
+  if (r0 >= N || c0 >= N) return;
+  KKTSrc S;
+  S.Q = Q + (size_t)b * n * n;
+  S.G = G + (size_t)b * m * n;
+  S.A = A + (size_t)b * p * n;
+  S.lam = lam + (size_t)b * m;
+  S.s = s + (size_t)b * m;
+  S.kidx = kidx + (size_t)b * m;
+  S.n = n; S.m = m; S.p = p; S.nk = meta[b].nk;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  // columns < n: sources are contiguous along the row index
+  for (int cc = ty; cc < 32; cc += 8) {
+    const int r = r0 + tx, c = c0 + cc;
+    if (c < n && r < N && c < N) tile[cc][tx] = kkt_elem(S, r, c);
+  }
+  // columns >= n: sources are contiguous along the column index
+  for (int rr = ty; rr < 32; rr += 8) {
+    const int r = r0 + rr, c = c0 + tx;
+    if (c >= n && r < N && c < N) tile[tx][rr] = kkt_elem(S, r, c);
+  }
+  __syncthreads();
+  double* Kb = K + (size_t)b * nmax * ld;
+  for (int rr = ty; rr < 32; rr += 8) {
+    const int r = r0 + rr, c = c0 + tx;
+    if (r < N && c < N) Kb[(size_t)r * ld + c] = tile[tx][rr];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 3. blocked right-looking LU with partial pivoting, one workgroup per problem.
+// Panel (N−c0)×32 factorised in LDS; L11⁻¹ formed in LDS; U12 = L11⁻¹A12 and
+// A22 −= L21·U12 on v_mfma_f64_16x16x4f64 in 64-column chunks.  Row swaps are
+// applied to trailing columns only ("lazy" left part): the solves interleave
+// the swaps per panel, K = P₁⁻¹M₁P₂⁻¹M₂…U.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(TPB) void qp_lu_small_kernel(
+    double* __restrict__ K, int32_t* __restrict__ ipiv, QPMeta* __restrict__ meta,
+    int nmax, int ld) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int lane = t & 63, wv = t >> 6;
+  if (meta[b].iterative) return;
+  const int N = meta[b].nsys;
+  if (N > SMALL_LU_MAX) return;  // handled by the generic kernel
+  double* Kb = K + (size_t)b * nmax * ld;
+  int32_t* piv = ipiv + (size_t)b * nmax;
+  const int Np = (N + 15) & ~15;
+  constexpr int PS = NB + 1;       // panel row stride (odd: conflict-free columns)
+  double* P = smem;                // Np × PS
+  double* UC = P + Np * PS;        // NB × CW
+  double* Li = UC + NB * CW;       // NB × NB  (L11⁻¹, row-major)
+  double* redv = Li + NB * NB;     // 4
+  int* redi = reinterpret_cast<int*>(redv + 4);  // 4 + pivots(NB)
+  int* pvs = redi + 4;
+  int info = 0;
+
+  for (int c0 = 0; c0 < N; c0 += NB) {
+    const int w = min(NB, N - c0);
+    const int R = N - c0;
+    const int Rp = (R + 15) & ~15;
+    // ---- load panel
+    {
+      const int cx = t & 31, ry = t >> 5;
+      for (int r = ry; r < Rp; r += 8)
+        P[r * PS + cx] = (r < R && cx < w) ? Kb[(size_t)(c0 + r) * ld + c0 + cx] : 0.0;
+    }
+    __syncthreads();
+    // ---- unblocked LU of the panel
+    for (int j = 0; j < w; ++j) {
+      double best = -1.0;
+      int bi = 0x7fffffff;
+      for (int r = j + t; r < R; r += TPB) {
+        const double v = fabs(P[r * PS + j]);
+        if (v > best) { best = v; bi = r; }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bi, o);
+        if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+      }
+      if (lane == 0) { redv[wv] = best; redi[wv] = bi; }
+      __syncthreads();
+      double pb = redv[0];
+      int pi = redi[0];
+      for (int k = 1; k < 4; ++k) {
+        if (redv[k] > pb || (redv[k] == pb && redi[k] < pi)) { pb = redv[k]; pi = redi[k]; }
+      }
+      if (pi == 0x7fffffff) pi = j;
+      if (pi != j && t < NB) {
+        const double a = P[j * PS + t], c = P[pi * PS + t];
+        P[j * PS + t] = c;
+        P[pi * PS + t] = a;
+      }
+      if (t == 0) pvs[j] = c0 + pi;
+      __syncthreads();
+      const double pv = P[j * PS + j];
+      if (pv == 0.0) {
+        if (info == 0) info = c0 + j + 1;
+      } else {
+        for (int r = j + 1 + t; r < R; r += TPB) {
+          const double l = P[r * PS + j] / pv;
+          P[r * PS + j] = l;
+          for (int c = j + 1; c < w; ++c) P[r * PS + c] = fma(-l, P[j * PS + c], P[r * PS + c]);
+        }
+      }
+      __syncthreads();
+    }
+    // ---- write panel back, save pivots
+    {
+      const int cx = t & 31, ry = t >> 5;
+      for (int r = ry; r < R; r += 8)
+        if (cx < w) Kb[(size_t)(c0 + r) * ld + c0 + cx] = P[r * PS + cx];
+      if (t < w) piv[c0 + t] = pvs[t];
+    }
+    if (c0 + w >= N) break;
+    // ---- L11⁻¹ (unit lower) into Li, one column per thread
+    if (t < NB) {
+      const int c = t;
+      for (int j = 0; j < NB; ++j) Li[j * NB + c] = 0.0;
+      if (c < w) {
+        Li[c * NB + c] = 1.0;
+        for (int j = c + 1; j < w; ++j) {
+          double acc = 0.0;
+          for (int i = c; i < j; ++i) acc = fma(P[j * PS + i], Li[i * NB + c], acc);
+          Li[j * NB + c] = -acc;
+        }
+      }
+    }
+    // ---- apply the panel's row swaps to trailing columns
+    for (int col = c0 + w + t; col < N; col += TPB) {
+      for (int j = 0; j < w; ++j) {
+        const int pr = pvs[j];
+        if (pr != c0 + j) {
+          const double a = Kb[(size_t)(c0 + j) * ld + col];
+          Kb[(size_t)(c0 + j) * ld + col] = Kb[(size_t)pr * ld + col];
+          Kb[(size_t)pr * ld + col] = a;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- trailing update in column chunks
+    for (int cc0 = c0 + w; cc0 < N; cc0 += CW) {
+      const int cw = min(CW, N - cc0);
+      // A12 chunk → registers, U12 = Li · A12 via MFMA (wave wv: column tile wv)
+      {
+        // stage A12 into UC
+        const int cx = t & 63, ry = t >> 6;
+        for (int r = ry; r < NB; r += 4)
+          UC[r * CW + cx] = (r < w && cx < cw) ? Kb[(size_t)(c0 + r) * ld + cc0 + cx] : 0.0;
+      }
+      __syncthreads();
+      {
+        // wave wv computes U12[:, 16wv:16wv+16] (two 16-row tiles)
+        d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+        const int col = wv * 16 + (lane & 15);
+#pragma unroll
+        for (int k = 0; k < NB / 4; ++k) {
+          const int kk = k * 4 + (lane >> 4);
+          const double bv = UC[kk * CW + col];
+          acc0 = mfma4(Li[(lane & 15) * NB + kk], bv, acc0);
+          acc1 = mfma4(Li[(16 + (lane & 15)) * NB + kk], bv, acc1);
+        }
+        __syncthreads();  // everyone finished reading UC
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row0 = (lane >> 4) + 4 * r;
+          UC[row0 * CW + col] = acc0[r];
+          UC[(16 + row0) * CW + col] = acc1[r];
+        }
+      }
+      __syncthreads();
+      // write U12 rows back to K
+      {
+        const int cx = t & 63, ry = t >> 6;
+        for (int r = ry; r < w; r += 4)
+          if (cx < cw) Kb[(size_t)(c0 + r) * ld + cc0 + cx] = UC[r * CW + cx];
+      }
+      // A22 −= L21 · U12: row tiles of 16 over the waves, 4 column tiles each
+      const int nrt = (R - w + 15) >> 4;
+      for (int rt = wv; rt < nrt; rt += 4) {
+        const int rbase = w + rt * 16;   // panel-relative row
+        d4 acc[4];
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int prow = rbase + (lane >> 4) + 4 * r;
+            const int gcol = cc0 + ct * 16 + (lane & 15);
+            acc[ct][r] = (prow < R && gcol < N) ? Kb[(size_t)(c0 + prow) * ld + gcol] : 0.0;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < NB / 4; ++k) {
+          const int kk = k * 4 + (lane >> 4);
+          const double a = -P[(rbase + (lane & 15)) * PS + kk];
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) acc[ct] = mfma4(a, UC[kk * CW + ct * 16 + (lane & 15)], acc[ct]);
+        }
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int prow = rbase + (lane >> 4) + 4 * r;
+            const int gcol = cc0 + ct * 16 + (lane & 15);
+            if (prow < R && gcol < N) Kb[(size_t)(c0 + prow) * ld + gcol] = acc[ct][r];
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (t == 0) meta[b].info = info;
+}
+
+// Generic fallback LU (any N): unblocked right-looking on global memory,
+// one workgroup per problem.  Used for systems larger than SMALL_LU_MAX.
+__global__ __launch_bounds__(TPB) void qp_lu_generic_kernel(
+    double* __restrict__ K, int32_t* __restrict__ ipiv, QPMeta* __restrict__ meta,
+    int nmax, int ld) {
+  __shared__ double redv[4];
+  __shared__ int redi[4];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int lane = t & 63, wv = t >> 6;
+  if (meta[b].iterative) return;
+  const int N = meta[b].nsys;
+  if (N <= SMALL_LU_MAX) return;
+  double* Kb = K + (size_t)b * nmax * ld;
+  int32_t* piv = ipiv + (size_t)b * nmax;
+  int info = 0;
+  for (int j = 0; j < N; ++j) {
+    double best = -1.0;
+    int bi = 0x7fffffff;
+    for (int r = j + t; r < N; r += TPB) {
+      const double v = fabs(Kb[(size_t)r * ld + j]);
+      if (v > best) { best = v; bi = r; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(best, o);
+      const int oi = __shfl_xor(bi, o);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    if (lane == 0) { redv[wv] = best; redi[wv] = bi; }
+    __syncthreads();
+    double pb = redv[0];
+    int pi = redi[0];
+    for (int k = 1; k < 4; ++k)
+      if (redv[k] > pb || (redv[k] == pb && redi[k] < pi)) { pb = redv[k]; pi = redi[k]; }
+    if (pi == 0x7fffffff) pi = j;
+    __syncthreads();
+    // swap only the trailing part (columns j..N): lazy left part, panel width 1
+    if (pi != j)
+      for (int c = j + t; c < N; c += TPB) {
+        const double a = Kb[(size_t)j * ld + c];
+        Kb[(size_t)j * ld + c] = Kb[(size_t)pi * ld + c];
+        Kb[(size_t)pi * ld + c] = a;
+      }
+    if (t == 0) piv[j] = pi;
+    __syncthreads();
+    const double pv = Kb[(size_t)j * ld + j];
+    if (pv == 0.0) {
+      if (info == 0) info = j + 1;
+      __syncthreads();
+      continue;
+    }
+    // rank-1 update: wave per row, lanes over columns
+    for (int r = j + 1 + wv; r < N; r += 4) {
+      const double l = Kb[(size_t)r * ld + j] / pv;
+      for (int c = j + 1 + lane; c < N; c += 64)
+        Kb[(size_t)r * ld + c] = fma(-l, Kb[(size_t)j * ld + c], Kb[(size_t)r * ld + c]);
+      if (lane == 0) Kb[(size_t)r * ld + j] = l;
+    }
+    __syncthreads();
+  }
+  if (t == 0) meta[b].info = info;
+}
+
+// ---------------------------------------------------------------------------
+// 4. triangular solves with the lazily-pivoted factors (panel width `nb`).
+//   trans = 0:  K x = r      x = U⁻¹ M_K⁻¹ P_K … M_1⁻¹ P_1 r
+//   trans = 1:  Kᵀ x = r     x = P_1⁻¹ M_1⁻ᵀ … P_K⁻¹ M_K⁻ᵀ U⁻ᵀ r
+// One workgroup per problem, vector in LDS.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(TPB) void qp_solve_kernel(
+    const double* __restrict__ K, const int32_t* __restrict__ ipiv,
+    const QPMeta* __restrict__ meta, int nmax, int ld, int trans,
+    const double* __restrict__ rhs, double* __restrict__ xout) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ double part[8][33];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int lane = t & 63, wv = t >> 6;
+  if (meta[b].iterative) return;
+  const int N = meta[b].nsys;
+  // panel width used by the factorisation of this problem
+  const int nb = (N <= SMALL_LU_MAX) ? NB : 1;
+  const double* Kb = K + (size_t)b * nmax * ld;
+  const int32_t* piv = ipiv + (size_t)b * nmax;
+  double* y = smem;
+  for (int i = t; i < N; i += TPB) y[i] = rhs[(size_t)b * nmax + i];
+  __syncthreads();
+  if (!trans) {
+    // ---- L part, panels forward
+    for (int c0 = 0; c0 < N; c0 += nb) {
+      const int w = min(nb, N - c0);
+      if (t == 0)
+        for (int j = 0; j < w; ++j) {
+          const int pr = piv[c0 + j];
+          if (pr != c0 + j) { const double a = y[c0 + j]; y[c0 + j] = y[pr]; y[pr] = a; }
+        }
+      __syncthreads();
+      if (wv == 0 && w > 1) {
+        double yj = (lane < w) ? y[c0 + lane] : 0.0;
+        for (int i = 0; i < w - 1; ++i) {
+          const double yi = __shfl(yj, i);
+          if (lane > i && lane < w) yj = fma(-Kb[(size_t)(c0 + lane) * ld + c0 + i], yi, yj);
+        }
+        if (lane < w) y[c0 + lane] = yj;
+      }
+      __syncthreads();
+      for (int r = c0 + w + t; r < N; r += TPB) {
+        const double* row = Kb + (size_t)r * ld + c0;
+        double acc = y[r];
+        for (int j = 0; j < w; ++j) acc = fma(-row[j], y[c0 + j], acc);
+        y[r] = acc;
+      }
+      __syncthreads();
+    }
+    // ---- U part, blocks backward (block width NB for the GEMV)
+    const int last = ((N - 1) / NB) * NB;
+    for (int i0 = last; i0 >= 0; i0 -= NB) {
+      const int w = min(NB, N - i0);
+      for (int r = wv; r < w; r += 4) {
+        const double* row = Kb + (size_t)(i0 + r) * ld;
+        double acc = 0.0;
+        for (int c = i0 + w + lane; c < N; c += 64) acc = fma(row[c], y[c], acc);
+        acc = wave_sum(acc);
+        if (lane == 0) y[i0 + r] -= acc;
+      }
+      __syncthreads();
+      if (wv == 0) {
+        double yj = (lane < w) ? y[i0 + lane] : 0.0;
+        for (int i = w - 1; i >= 0; --i) {
+          if (lane == i) yj = yj / Kb[(size_t)(i0 + i) * ld + i0 + i];
+          const double yi = __shfl(yj, i);
+          if (lane < i) yj = fma(-Kb[(size_t)(i0 + lane) * ld + i0 + i], yi, yj);
+        }
+        if (lane < w) y[i0 + lane] = yj;
+      }
+      __syncthreads();
+    }
+  } else {
+    // ---- Uᵀ part, blocks forward
+    for (int i0 = 0; i0 < N; i0 += NB) {
+      const int w = min(NB, N - i0);
+      if (wv == 0) {
+        double yj = (lane < w) ? y[i0 + lane] : 0.0;
+        for (int i = 0; i < w; ++i) {
+          if (lane == i) yj = yj / Kb[(size_t)(i0 + i) * ld + i0 + i];
+          const double yi = __shfl(yj, i);
+          if (lane > i && lane < w) yj = fma(-Kb[(size_t)(i0 + i) * ld + i0 + lane], yi, yj);
+        }
+        if (lane < w) y[i0 + lane] = yj;
+      }
+      __syncthreads();
+      for (int c = i0 + w + t; c < N; c += TPB) {
+        double acc = y[c];
+        for (int j = 0; j < w; ++j) acc = fma(-Kb[(size_t)(i0 + j) * ld + c], y[i0 + j], acc);
+        y[c] = acc;
+      }
+      __syncthreads();
+    }
+    // ---- Lᵀ part, panels backward
+    const int lastp = ((N - 1) / nb) * nb;
+    for (int c0 = lastp; c0 >= 0; c0 -= nb) {
+      const int w = min(nb, N - c0);
+      if (c0 + w < N) {
+        // y[c0+j] −= Σ_r L[r][c0+j] y[r], r ∈ [c0+w, N)
+        const int jx = t & 31, rg = t >> 5;
+        double acc = 0.0;
+        if (jx < w)
+          for (int r = c0 + w + rg; r < N; r += 8) acc = fma(Kb[(size_t)r * ld + c0 + jx], y[r], acc);
+        part[rg][jx] = acc;
+        __syncthreads();
+        if (t < w) {
+          double sacc = 0.0;
+          for (int g = 0; g < 8; ++g) sacc += part[g][t];
+          y[c0 + t] -= sacc;
+        }
+        __syncthreads();
+      }
+      if (wv == 0 && w > 1) {
+        double yj = (lane < w) ? y[c0 + lane] : 0.0;
+        for (int i = w - 1; i > 0; --i) {
+          const double yi = __shfl(yj, i);
+          if (lane < i) yj = fma(-Kb[(size_t)(c0 + i) * ld + c0 + lane], yi, yj);
+        }
+        if (lane < w) y[c0 + lane] = yj;
+      }
+      __syncthreads();
+      if (t == 0)
+        for (int j = w - 1; j >= 0; --j) {
+          const int pr = piv[c0 + j];
+          if (pr != c0 + j) { const double a = y[c0 + j]; y[c0 + j] = y[pr]; y[pr] = a; }
+        }
+      __syncthreads();
+    }
+  }
+  for (int i = t; i < N; i += TPB) xout[(size_t)b * nmax + i] = y[i];
+}
+
+// ---------------------------------------------------------------------------
+// 5. dense batched LSQR for the `iterative` branch (QuadraticProgram.jl:488):
+// IterativeSolvers.lsqr(LHS or LHSᵀ, RHS) on the FULL (unreduced) KKT matrix,
+// restating oracle/lsqr.py operation for operation.  One workgroup/problem.
+// ---------------------------------------------------------------------------
+__device__ void dense_matvec(const double* __restrict__ Kb, int ld, int N, int trans,
+                             const double* __restrict__ v, double* __restrict__ out) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (!trans) {
+    for (int r = wv; r < N; r += 4) {
+      const double* row = Kb + (size_t)r * ld;
+      double acc = 0.0;
+      for (int c = lane; c < N; c += 64) acc = fma(row[c], v[c], acc);
+      acc = wave_sum(acc);
+      if (lane == 0) out[r] = acc;
+    }
+  } else {
+    for (int c = t; c < N; c += TPB) {
+      double acc = 0.0;
+      for (int r = 0; r < N; ++r) acc = fma(Kb[(size_t)r * ld + c], v[r], acc);
+      out[c] = acc;
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(TPB) void qp_lsqr_kernel(
+    const double* __restrict__ K, const QPMeta* __restrict__ meta, int nmax,
+    int ld, int trans, const double* __restrict__ rhs, double* __restrict__ xout,
+    int32_t* __restrict__ iters) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ double red[4];
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (!meta[b].iterative) return;
+  const int N = meta[b].nsys;
+  const double* Kb = K + (size_t)b * nmax * ld;
+  double* x = smem;
+  double* u = x + N;
+  double* v = u + N;
+  double* w = v + N;
+  double* tmp = w + N;
+  double bb = 0.0;
+  for (int i = t; i < N; i += TPB) {
+    const double r = rhs[(size_t)b * nmax + i];
+    u[i] = r;
+    x[i] = 0.0;
+    bb = fma(r, r, bb);
+  }
+  double beta = sqrt(block_sum(bb, red));
+  int it = 0;
+  if (beta > 0.0) {
+    for (int i = t; i < N; i += TPB) u[i] /= beta;
+    __syncthreads();
+    dense_matvec(Kb, ld, N, !trans, u, v);   // v = Aᵀu
+    double aa = 0.0;
+    for (int i = t; i < N; i += TPB) aa = fma(v[i], v[i], aa);
+    double alpha = sqrt(block_sum(aa, red));
+    if (alpha > 0.0) {
+      for (int i = t; i < N; i += TPB) { v[i] /= alpha; w[i] = v[i]; }
+      __syncthreads();
+      const double eps = 2.220446049250313e-16;
+      const double atol = sqrt(eps), btol = sqrt(eps), ctol = sqrt(eps);
+      double anorm = 0.0, ddnorm = 0.0, res2 = 0.0, xxnorm = 0.0, zz = 0.0;
+      double sn2 = 0.0, cs2 = -1.0, rhobar = alpha, phibar = beta;
+      const double bnorm = beta;
+      const int maxiter = N;
+      while (it < maxiter) {
+        ++it;
+        dense_matvec(Kb, ld, N, trans, v, tmp);   // tmp = A v
+        double su = 0.0;
+        for (int i = t; i < N; i += TPB) { const double ui = tmp[i] - alpha * u[i]; u[i] = ui; su = fma(ui, ui, su); }
+        beta = sqrt(block_sum(su, red));
+        if (beta > 0.0) {
+          for (int i = t; i < N; i += TPB) u[i] /= beta;
+          __syncthreads();
+          anorm = sqrt(anorm * anorm + alpha * alpha + beta * beta);
+          dense_matvec(Kb, ld, N, !trans, u, tmp);  // tmp = Aᵀu
+          double sv = 0.0;
+          for (int i = t; i < N; i += TPB) { const double vi = tmp[i] - beta * v[i]; v[i] = vi; sv = fma(vi, vi, sv); }
+          alpha = sqrt(block_sum(sv, red));
+          if (alpha > 0.0) for (int i = t; i < N; i += TPB) v[i] /= alpha;
+          __syncthreads();
+        }
+        const double rhobar1 = rhobar;
+        const double rho = hypot(rhobar1, beta);
+        const double cs = rhobar1 / rho, sn = beta / rho;
+        const double theta = sn * alpha;
+        rhobar = -cs * alpha;
+        const double phi = cs * phibar;
+        phibar = sn * phibar;
+        const double tau = sn * phi;
+        const double t1 = phi / rho, t2 = -theta / rho;
+        double sw = 0.0;
+        for (int i = t; i < N; i += TPB) {
+          const double wi = w[i];
+          sw = fma(wi, wi, sw);
+          x[i] = x[i] + t1 * wi;
+          w[i] = v[i] + t2 * wi;
+        }
+        ddnorm += block_sum(sw, red) / (rho * rho);
+        const double delta = sn2 * rho, gambar = -cs2 * rho;
+        const double rhs_ = phi - delta * zz;
+        const double zbar = rhs_ / gambar;
+        const double xnorm = sqrt(xxnorm + zbar * zbar);
+        const double gamma = hypot(gambar, theta);
+        cs2 = gambar / gamma;
+        sn2 = theta / gamma;
+        zz = rhs_ / gamma;
+        xxnorm += zz * zz;
+        const double acond = anorm * sqrt(ddnorm);
+        const double rnorm = sqrt(phibar * phibar + res2);
+        const double arnorm = alpha * fabs(tau);
+        const double test1 = rnorm / bnorm;
+        const double test2 = (anorm * rnorm != 0.0) ? arnorm / (anorm * rnorm) : 0.0;
+        const double test3 = (acond != 0.0) ? 1.0 / acond : 0.0;
+        const double t1r = test1 / (1.0 + anorm * xnorm / bnorm);
+        const double rtol = btol + atol * anorm * xnorm / bnorm;
+        int istop = 0;
+        if (it >= maxiter) istop = 7;
+        if (1.0 + test3 <= 1.0) istop = 6;
+        if (1.0 + test2 <= 1.0) istop = 5;
+        if (1.0 + t1r <= 1.0) istop = 4;
+        if (test3 <= ctol) istop = 3;
+        if (test2 <= atol) istop = 2;
+        if (test1 <= rtol) istop = 1;
+        __syncthreads();
+        if (istop) break;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < N; i += TPB) xout[(size_t)b * nmax + i] = x[i];
+  if (t == 0 && iters) iters[b] = it;
+}
+
+// ---------------------------------------------------------------------------
+// 6. right-hand sides and outputs
+// ---------------------------------------------------------------------------
+// reverse RHS: [dl_dz; 0] reduced (QuadraticProgram.jl:329)
+__global__ __launch_bounds__(TPB) void qp_rev_rhs_kernel(
+    const double* __restrict__ dl_dz, const QPMeta* __restrict__ meta, int n,
+    int nmax, double* __restrict__ rhs) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int N = meta[b].nsys;
+  for (int i = t; i < N; i += TPB) rhs[(size_t)b * nmax + i] = (i < n) ? dl_dz[(size_t)b * n + i] : 0.0;
+}
+
+// forward RHS (QuadraticProgram.jl:429-433):
+//   [dQ z + dq + dGᵀλ + dAᵀν; λ.*(dG z) − λ.*dh; dA z − db]
+// full-length copy in `full` (n+m+p per problem, stride nmax) and reduced copy in rhs.
+__global__ __launch_bounds__(TPB) void qp_fwd_rhs_kernel(
+    const double* __restrict__ dQ, const double* __restrict__ dq,
+    const double* __restrict__ dG, const double* __restrict__ dh,
+    const double* __restrict__ dA, const double* __restrict__ db,
+    const double* __restrict__ z, const double* __restrict__ lam,
+    const double* __restrict__ nu, const int32_t* __restrict__ rpos,
+    const QPMeta* __restrict__ meta, int n, int m, int p, int nmax,
+    double* __restrict__ full, double* __restrict__ rhs) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  double* zs = smem;            // n
+  double* ls = zs + n;          // m
+  double* ns = ls + m;          // p
+  double* r = ns + p;           // n + m + p
+  for (int i = t; i < n; i += TPB) zs[i] = z[(size_t)b * n + i];
+  for (int i = t; i < m; i += TPB) ls[i] = lam[(size_t)b * m + i];
+  for (int i = t; i < p; i += TPB) ns[i] = nu[(size_t)b * p + i];
+  __syncthreads();
+  // r1 = dQ z + dq
+  for (int i = t; i < n; i += TPB) {
+    double acc = 0.0;
+    if (dQ) {
+      const double* Qb = dQ + (size_t)b * n * n;
+      for (int j = 0; j < n; ++j) acc = fma(Qb[i + (size_t)j * n], zs[j], acc);
+    }
+    if (dq) acc += dq[(size_t)b * n + i];
+    r[i] = acc;
+  }
+  __syncthreads();
+  // r1 += dGᵀλ ; r1 += dAᵀν  (wave per column, lanes over rows)
+  if (dG && m > 0) {
+    const double* Gb = dG + (size_t)b * m * n;
+    for (int i = wv; i < n; i += 4) {
+      double acc = 0.0;
+      for (int l = lane; l < m; l += 64) acc = fma(Gb[l + (size_t)i * m], ls[l], acc);
+      acc = wave_sum(acc);
+      if (lane == 0) r[i] += acc;
+    }
+  }
+  __syncthreads();
+  if (dA && p > 0) {
+    const double* Ab = dA + (size_t)b * p * n;
+    for (int i = wv; i < n; i += 4) {
+      double acc = 0.0;
+      for (int l = lane; l < p; l += 64) acc = fma(Ab[l + (size_t)i * p], ns[l], acc);
+      acc = wave_sum(acc);
+      if (lane == 0) r[i] += acc;
+    }
+  }
+  // r2 = λ.*(dG z) − λ.*dh
+  for (int l = t; l < m; l += TPB) {
+    double gz = 0.0;
+    if (dG) {
+      const double* Gb = dG + (size_t)b * m * n;
+      for (int j = 0; j < n; ++j) gz = fma(Gb[l + (size_t)j * m], zs[j], gz);
+    }
+    const double hh = dh ? dh[(size_t)b * m + l] : 0.0;
+    r[n + l] = ls[l] * gz - ls[l] * hh;
+  }
+  // r3 = dA z − db
+  for (int e = t; e < p; e += TPB) {
+    double az = 0.0;
+    if (dA) {
+      const double* Ab = dA + (size_t)b * p * n;
+      for (int j = 0; j < n; ++j) az = fma(Ab[e + (size_t)j * p], zs[j], az);
+    }
+    r[n + m + e] = az - (db ? db[(size_t)b * p + e] : 0.0);
+  }
+  __syncthreads();
+  const int nk = meta[b].nk;
+  double* fb = full + (size_t)b * nmax;
+  double* rb = rhs + (size_t)b * nmax;
+  for (int i = t; i < n + m + p; i += TPB) fb[i] = r[i];
+  for (int i = t; i < n; i += TPB) rb[i] = r[i];
+  for (int l = t; l < m; l += TPB) {
+    const int kk = rpos[(size_t)b * m + l];
+    if (kk >= 0) rb[n + kk] = r[n + l];
+  }
+  for (int e = t; e < p; e += TPB) rb[n + nk + e] = r[n + m + e];
+}
+
+// outputs: out = −[x_z | x_λ (scattered to all m rows) | x_ν]
+//   eliminated rows (λ_i == 0, s_i != 0):
+//     reverse:  x_λi = (0 − G_i·x_z)/s_i          (row n+i of LHS)
+//     forward:  x_λi = r_i / s_i                   (row n+i of LHSᵀ)
+__global__ __launch_bounds__(TPB) void qp_output_kernel(
+    const double* __restrict__ x, const double* __restrict__ G,
+    const double* __restrict__ s, const int32_t* __restrict__ rpos,
+    const QPMeta* __restrict__ meta, const double* __restrict__ full, int n,
+    int m, int p, int nmax, int trans, double* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int nk = meta[b].nk;
+  const double* xb = x + (size_t)b * nmax;
+  double* ob = out + (size_t)b * (n + m + p);
+  double* xz = smem;
+  for (int i = t; i < n; i += TPB) { xz[i] = xb[i]; ob[i] = -xb[i]; }
+  for (int e = t; e < p; e += TPB) ob[n + m + e] = -xb[n + nk + e];
+  __syncthreads();
+  const double* Gb = G + (size_t)b * m * n;
+  for (int l = t; l < m; l += TPB) {
+    const int kk = rpos[(size_t)b * m + l];
+    double xl;
+    if (kk >= 0) {
+      xl = xb[n + kk];
+    } else if (!trans) {
+      double acc = 0.0;
+      for (int j = 0; j < n; ++j) acc = fma(Gb[l + (size_t)j * m], xz[j], acc);
+      xl = (0.0 - acc) / s[(size_t)b * m + l];
+    } else {
+      xl = full[(size_t)b * nmax + n + l] / s[(size_t)b * m + l];
+    }
+    ob[n + l] = -xl;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static void check_launch() { DOPT_CHECK_HIP(hipGetLastError()); }
+
+static size_t lu_small_lds(int nmax) {
+  const int Np = ((std::min(nmax, SMALL_LU_MAX) + 15) / 16) * 16;
+  return ((size_t)Np * (NB + 1) + NB * CW + NB * NB + 4) * sizeof(double) + (4 + NB) * sizeof(int);
+}
+
+void qp_factor(Handle& h) {
+  if (!h.set) throw Error(-1, "dopt_qp_factor: dopt_qp_set has not been called");
+  const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
+  const int nmax = h.nmax, ld = h.ld;
+  QPMeta* meta = h.meta.as<QPMeta>();
+  static const double dummy = 0.0;
+  const double* G = h.G ? h.G : &dummy;
+  const double* A = h.A ? h.A : &dummy;
+  hipLaunchKernelGGL(qp_prepare_kernel, dim3(B), dim3(TPB), n * sizeof(double), h.stream,
+                     h.Q, m ? h.G : nullptr, m ? h.hv : nullptr, h.z, m ? h.lam : nullptr,
+                     n, m, p, h.s.as<double>(), h.kidx.as<int32_t>(),
+                     h.kidx.as<int32_t>() + (size_t)B * m, meta);
+  check_launch();
+  const int tiles_1d = (nmax + 31) / 32;
+  hipLaunchKernelGGL(qp_assemble_kernel, dim3(tiles_1d * tiles_1d, B), dim3(TPB), 0, h.stream,
+                     h.Q, G, A, m ? h.lam : &dummy, h.s.as<double>(), h.kidx.as<int32_t>(), meta,
+                     n, m, p, nmax, ld, tiles_1d, h.K.as<double>());
+  check_launch();
+  if (nmax > 0) {
+    hipLaunchKernelGGL(qp_lu_small_kernel, dim3(B), dim3(TPB), lu_small_lds(nmax), h.stream,
+                       h.K.as<double>(), h.ipiv.as<int32_t>(), meta, nmax, ld);
+    check_launch();
+    if (nmax > SMALL_LU_MAX) {
+      hipLaunchKernelGGL(qp_lu_generic_kernel, dim3(B), dim3(TPB), 0, h.stream,
+                         h.K.as<double>(), h.ipiv.as<int32_t>(), meta, nmax, ld);
+      check_launch();
+    }
+  }
+  h.factored = true;
+}
+
+static void qp_solve_and_output(Handle& h, int trans, double* out) {
+  const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
+  const int nmax = h.nmax, ld = h.ld;
+  QPMeta* meta = h.meta.as<QPMeta>();
+  double* rhs = h.rhs.as<double>();
+  double* full = rhs + (size_t)B * nmax;
+  double* x = h.x.as<double>();
+  hipLaunchKernelGGL(qp_solve_kernel, dim3(B), dim3(TPB), (size_t)nmax * sizeof(double), h.stream,
+                     h.K.as<double>(), h.ipiv.as<int32_t>(), meta, nmax, ld, trans, rhs, x);
+  check_launch();
+  hipLaunchKernelGGL(qp_lsqr_kernel, dim3(B), dim3(TPB), (size_t)5 * nmax * sizeof(double), h.stream,
+                     h.K.as<double>(), meta, nmax, ld, trans, rhs, x, (int32_t*)nullptr);
+  check_launch();
+  static const double dummy = 0.0;
+  hipLaunchKernelGGL(qp_output_kernel, dim3(B), dim3(TPB), (size_t)n * sizeof(double), h.stream,
+                     x, m ? h.G : &dummy, h.s.as<double>(), h.kidx.as<int32_t>() + (size_t)B * m,
+                     meta, full, n, m, p, nmax, trans, out);
+  check_launch();
+}
+
+void qp_reverse(Handle& h, const double* dl_dz, double* out) {
+  if (!h.factored) qp_factor(h);
+  hipLaunchKernelGGL(qp_rev_rhs_kernel, dim3(h.batch), dim3(TPB), 0, h.stream, dl_dz,
+                     h.meta.as<QPMeta>(), h.n, h.nmax, h.rhs.as<double>());
+  check_launch();
+  qp_solve_and_output(h, 0, out);
+}
+
+void qp_forward(Handle& h, const double* dQ, const double* dq, const double* dG,
+                const double* dh, const double* dA, const double* db, double* out) {
+  if (!h.factored) qp_factor(h);
+  const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
+  double* rhs = h.rhs.as<double>();
+  double* full = rhs + (size_t)B * h.nmax;
+  static const double dummy = 0.0;
+  hipLaunchKernelGGL(qp_fwd_rhs_kernel, dim3(B), dim3(TPB), (size_t)(2 * n + 2 * m + 2 * p) * sizeof(double),
+                     h.stream, dQ, dq, m ? dG : nullptr, m ? dh : nullptr, p ? dA : nullptr,
+                     p ? db : nullptr, h.z, m ? h.lam : &dummy, p ? h.nu : &dummy,
+                     h.kidx.as<int32_t>() + (size_t)B * m, h.meta.as<QPMeta>(), n, m, p, h.nmax, full, rhs);
+  check_launch();
+  qp_solve_and_output(h, 1, out);
+}
+
+void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
+                        const double* dq, const double* dG, const double* dh,
+                        const double* dA, const double* db, double* out_rev,
+                        double* out_fwd) {
+  if (!h.factored) qp_factor(h);
+  qp_reverse(h, dl_dz, out_rev);
+  qp_forward(h, dQ, dq, dG, dh, dA, db, out_fwd);
+}
+
+}  // namespace dopt

@@ -1,0 +1,308 @@
+"""QuadraticProgram back-end on the MI355X engine.
+
+Mirrors ``DiffOpt.QuadraticProgram`` (reference
+``src/QuadraticProgram/QuadraticProgram.jl``):
+
+* ``QPBatch`` — the batched C-ABI handle (one KKT system per problem, all
+  problems of one shape).  Accepts numpy arrays (host memory, copied into HBM)
+  or torch CUDA tensors (device memory, zero-copy, inputs resident in HBM).
+* ``Model`` — a single-problem model with the reference's plugin-interface
+  vocabulary: ``VariablePrimalStart``/``ConstraintDualStart`` setters with the
+  dual sign flip (:164-180), ``ReverseVariablePrimal`` inputs,
+  ``reverse_differentiate`` (:316-351), ``forward_differentiate`` (:357-446),
+  ``ForwardVariablePrimal`` (:299-305), ``ReverseObjectiveFunction``
+  (:448-458), ``ReverseConstraintFunction`` (``_get_dA``/``_get_db``
+  :307-314, :461-473) and ``DifferentiateTimeSec``.
+"""
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._arrays import Staged, colmajor, vector
+
+LE, EQ = "LessThan", "EqualTo"
+
+
+class QPBatch:
+    """Batched QP sensitivity engine (C-ABI handle wrapper)."""
+
+    def __init__(self, batch, n, m, p=0, device=0):
+        self.lib = _lib.load()
+        self.batch, self.n, self.m, self.p = int(batch), int(n), int(m), int(p)
+        self.device = device
+        h = ctypes.c_void_p()
+        rc = self.lib.dopt_create(ctypes.byref(h), device, self.batch, self.n, self.m,
+                                  self.p, _lib.DOPT_KIND_QP)
+        if rc != 0:
+            raise _lib.EngineError(rc, "dopt_create failed (no HIP device?)")
+        self.h = h
+        self._mem = None
+        self._keep = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.dopt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    # ---- memory mode -------------------------------------------------------
+    def _stage(self, arrays):
+        st = Staged(arrays)
+        if self._mem != st.mem:
+            _lib.check(self.lib.dopt_set_memory(self.h, st.mem), self.h)
+            self._mem = st.mem
+        if st.set_stream and st.stream != getattr(self, "_stream", -1):
+            _lib.check(self.lib.dopt_set_stream(self.h, st.stream), self.h)
+            self._stream = st.stream
+        return st
+
+    @property
+    def L(self):
+        return self.n + self.m + self.p
+
+    def set(self, Q, G=None, h=None, A=None, z=None, lam=None, nu=None):
+        """Problem data and primal–dual point (λ, ν in OptNet sign)."""
+        B, n, m, p = self.batch, self.n, self.m, self.p
+        st = self._stage([Q, G, h, A, z, lam, nu])
+        Qc = colmajor(Q, (B, n, n))
+        Gc = colmajor(G, (B, m, n)) if m else None
+        Ac = colmajor(A, (B, p, n)) if p else None
+        args = [Qc, Gc, vector(h, (B, m)) if m else None, Ac, vector(z, (B, n)),
+                vector(lam, (B, m)) if m else None, vector(nu, (B, p)) if p else None]
+        self._keep = args  # device mode borrows: keep the staged tensors alive
+        rc = self.lib.dopt_qp_set(self.h, *[st.ptr(a) for a in args])
+        _lib.check(rc, self.h)
+
+    def factor(self, singular_ok=False):
+        return _lib.check(self.lib.dopt_qp_factor(self.h), self.h, singular_ok)
+
+    def _out(self, like_device):
+        return Staged.empty((self.batch, self.L), like_device)
+
+    def reverse(self, dl_dz, singular_ok=False):
+        """Returns (B, n+m+p) = [dz | dλ | dν]."""
+        st = self._stage([dl_dz])
+        d = vector(dl_dz, (self.batch, self.n))
+        out = self._out(st.mem == _lib.DOPT_MEM_DEVICE)
+        rc = self.lib.dopt_qp_reverse(self.h, st.ptr(d), st.ptr(out))
+        _lib.check(rc, self.h, singular_ok)
+        return out
+
+    def forward(self, dQ=None, dq=None, dG=None, dh=None, dA=None, db=None,
+                singular_ok=False):
+        B, n, m, p = self.batch, self.n, self.m, self.p
+        st = self._stage([dQ, dq, dG, dh, dA, db])
+        args = [colmajor(dQ, (B, n, n)) if dQ is not None else None,
+                vector(dq, (B, n)) if dq is not None else None,
+                colmajor(dG, (B, m, n)) if (dG is not None and m) else None,
+                vector(dh, (B, m)) if (dh is not None and m) else None,
+                colmajor(dA, (B, p, n)) if (dA is not None and p) else None,
+                vector(db, (B, p)) if (db is not None and p) else None]
+        out = self._out(st.mem == _lib.DOPT_MEM_DEVICE)
+        rc = self.lib.dopt_qp_forward(self.h, *[st.ptr(a) for a in args], st.ptr(out))
+        _lib.check(rc, self.h, singular_ok)
+        return out
+
+    def forward_reverse(self, dl_dz, dQ=None, dq=None, dG=None, dh=None, dA=None,
+                        db=None, out_rev=None, out_fwd=None, singular_ok=False):
+        """One full sensitivity solve per problem: factor + reverse + forward."""
+        B, n, m, p = self.batch, self.n, self.m, self.p
+        st = self._stage([dl_dz, dQ, dq, dG, dh, dA, db])
+        dev = st.mem == _lib.DOPT_MEM_DEVICE
+        args = [vector(dl_dz, (B, n)),
+                colmajor(dQ, (B, n, n)) if dQ is not None else None,
+                vector(dq, (B, n)) if dq is not None else None,
+                colmajor(dG, (B, m, n)) if (dG is not None and m) else None,
+                vector(dh, (B, m)) if (dh is not None and m) else None,
+                colmajor(dA, (B, p, n)) if (dA is not None and p) else None,
+                vector(db, (B, p)) if (db is not None and p) else None]
+        o1 = out_rev if out_rev is not None else self._out(dev)
+        o2 = out_fwd if out_fwd is not None else self._out(dev)
+        rc = self.lib.dopt_qp_forward_reverse(self.h, *[st.ptr(a) for a in args],
+                                              st.ptr(o1), st.ptr(o2))
+        _lib.check(rc, self.h, singular_ok)
+        return o1, o2
+
+    # ---- introspection -----------------------------------------------------
+    def info(self):
+        buf = np.zeros(self.batch, dtype=np.int32)
+        _lib.check(self.lib.dopt_get_info(self.h, buf.ctypes.data), self.h)
+        return buf
+
+    def iterative(self):
+        buf = np.zeros(self.batch, dtype=np.int8)
+        _lib.check(self.lib.dopt_get_iterative(self.h, buf.ctypes.data), self.h)
+        return buf.astype(bool)
+
+    def system_size(self):
+        buf = np.zeros(self.batch, dtype=np.int32)
+        _lib.check(self.lib.dopt_get_system_size(self.h, buf.ctypes.data), self.h)
+        return buf
+
+    def last_time(self):
+        return self.lib.dopt_last_time(self.h)
+
+    def split(self, out):
+        n, m = self.n, self.m
+        return out[:, :n], out[:, n:n + m], out[:, n + m:]
+
+
+class Model:
+    """Single-problem ``DiffOpt.QuadraticProgram.Model`` on the engine.
+
+    Problem data is given in the matrix form the reference builds from MOI
+    (``_gradient_cache``, :182-213): ``Q`` (symmetric Hessian), ``q``, ``G``,
+    ``h`` (LessThan rows), ``A``, ``b`` (EqualTo rows).  Tangent sign handling
+    of ``_fill`` (diff_opt.jl:594-656) happens in the setters below.
+    """
+
+    def __init__(self, device=0):
+        self.device = device
+        self.empty()
+
+    # MOI.empty! (:126-137)
+    def empty(self):
+        self.Q = self.q = self.G = self.h = self.A = self.b = None
+        self.x = None
+        self.lam = None
+        self.nu = None
+        self._engine = None
+        self.forw_grad_cache = None
+        self.back_grad_cache = None
+        self.diff_time = float("nan")
+        self.input_dx = {}
+        self.input_objective = None      # (dQ, dq)
+        self.input_le = {}               # row -> (coeffs, constant)
+        self.input_eq = {}
+
+    def set_problem(self, Q, q, G=None, h=None, A=None, b=None):
+        n = np.asarray(q).shape[0]
+        self.Q = np.asarray(Q, dtype=np.float64).reshape(n, n)
+        self.q = np.asarray(q, dtype=np.float64)
+        self.G = np.zeros((0, n)) if G is None else np.asarray(G, float).reshape(-1, n)
+        self.h = np.zeros(0) if h is None else np.asarray(h, float).ravel()
+        self.A = np.zeros((0, n)) if A is None else np.asarray(A, float).reshape(-1, n)
+        self.b = np.zeros(0) if b is None else np.asarray(b, float).ravel()
+        self._engine = None
+
+    @property
+    def n(self):
+        return self.q.shape[0]
+
+    # ---- starts (diff_opt.jl:362-370, QuadraticProgram.jl:164-180) ---------
+    def set_variable_primal_start(self, x):
+        self.x = np.asarray(x, dtype=np.float64).copy()
+        self._engine = None
+
+    def set_constraint_dual_start(self, kind, duals):
+        """MOI ``ConstraintDual`` values; stored with the OptNet sign flip."""
+        d = -np.asarray(duals, dtype=np.float64)
+        if kind == LE:
+            self.lam = d
+        elif kind == EQ:
+            self.nu = d
+        else:
+            raise ValueError(kind)
+        self._engine = None
+
+    # ---- sensitivity inputs -------------------------------------------------
+    def set_reverse_variable_primal(self, i, value):
+        self.input_dx[int(i)] = float(value)
+
+    def set_forward_objective_function(self, dQ=None, dq=None):
+        self.input_objective = (dQ, dq)
+
+    def set_forward_constraint_function(self, kind, row, coeffs, constant):
+        """Tangent of the constraint function ``coeffsᵀx + constant`` of row
+        ``row`` (``func``-in-``set``).  ``_fill``: the constant is negated for
+        both EqualTo and LessThan (it is the tangent of the set constant)."""
+        tgt = self.input_le if kind == LE else self.input_eq
+        tgt[int(row)] = (np.asarray(coeffs, dtype=np.float64), float(constant))
+
+    def empty_input_sensitivities(self):
+        self.input_dx = {}
+        self.input_objective = None
+        self.input_le = {}
+        self.input_eq = {}
+
+    # ---- engine ------------------------------------------------------------
+    def _ensure(self):
+        n, m, p = self.n, self.G.shape[0], self.A.shape[0]
+        if self.x is None or len(self.x) < n or np.any(np.isnan(self.x)):
+            raise ValueError("VariablePrimalStart missing")
+        lam = np.zeros(m) if self.lam is None else self.lam
+        nu = np.zeros(p) if self.nu is None else self.nu
+        if self._engine is None:
+            e = QPBatch(1, n, m, p, self.device)
+            e.set(self.Q[None], self.G[None], self.h[None], self.A[None], self.x[None],
+                  lam[None], nu[None])
+            self._engine = e
+            self._lam, self._nu = lam, nu
+        return self._engine
+
+    def reverse_differentiate(self):
+        import time
+        t0 = time.perf_counter()
+        e = self._ensure()
+        dl = np.zeros(self.n)
+        for i, v in self.input_dx.items():
+            dl[i] = v
+        out = np.asarray(e.reverse(dl[None]))[0]
+        n, m = self.n, self.G.shape[0]
+        self.back_grad_cache = (out[:n], out[n:n + m], out[n + m:])
+        self.diff_time = time.perf_counter() - t0
+
+    def forward_differentiate(self):
+        import time
+        t0 = time.perf_counter()
+        e = self._ensure()
+        n, m, p = self.n, self.G.shape[0], self.A.shape[0]
+        dQ, dq = (None, None) if self.input_objective is None else self.input_objective
+        dG = np.zeros((m, n))
+        dh = np.zeros(m)
+        for r, (c, k) in self.input_le.items():
+            dG[r] = c
+            dh[r] = -k
+        dA = np.zeros((p, n))
+        db = np.zeros(p)
+        for r, (c, k) in self.input_eq.items():
+            dA[r] = c
+            db[r] = -k
+        out = np.asarray(e.forward(
+            None if dQ is None else np.asarray(dQ, float)[None],
+            None if dq is None else np.asarray(dq, float)[None],
+            dG[None] if m else None, dh[None] if m else None,
+            dA[None] if p else None, db[None] if p else None))[0]
+        self.forw_grad_cache = (out[:n], out[n:n + m], out[n + m:])
+        self.diff_time = time.perf_counter() - t0
+
+    # ---- outputs -----------------------------------------------------------
+    def forward_variable_primal(self, i):
+        """``ForwardVariablePrimal`` (:299-305)."""
+        return self.forw_grad_cache[0][i]
+
+    def reverse_objective_function(self):
+        """``ReverseObjectiveFunction`` (:448-458): (dq, dQ) with
+        ``dq = ∇z`` and ``dQ = (∇z zᵀ + z ∇zᵀ)/2`` (materialised)."""
+        dz = self.back_grad_cache[0]
+        z = self.x
+        return dz.copy(), 0.5 * (np.outer(dz, z) + np.outer(z, dz))
+
+    def reverse_constraint_function(self, kind, row):
+        """``ReverseConstraintFunction`` (diff_opt.jl:475-481): (coefficients,
+        constant) from ``_get_dA``/``_get_db`` (:307-314, :461-473)."""
+        dz, dlam, dnu = self.back_grad_cache
+        z = self.x
+        if kind == LE:
+            l = self._lam[row]
+            return l * dlam[row] * z + l * dz, l * dlam[row]
+        if kind == EQ:
+            return dnu[row] * z + self._nu[row] * dz, dnu[row]
+        raise ValueError(kind)
+
+    def differentiate_time_sec(self):
+        return self.diff_time

@@ -1,0 +1,163 @@
+"""Seeded synthetic instances with a KKT point by construction.
+
+QP (OptNet sign):  Q = LLᵀ/n + 0.1 I,  G, A ~ N(0,1)/√n,  z ~ N(0,1);
+a seeded permutation makes ⌊φ·m⌋ rows active (s_i = 0, λ_i ~ U(0.5,1.5)), the
+others inactive (λ_i = 0, s_i ~ −U(0.5,1.5)); ν ~ N(0,1); h = Gz − s; b = Az;
+q = −(Qz + Gᵀλ + Aᵀν).  Reverse seed dl/dz ~ N(0,1); forward tangents
+dq, dh, db ~ N(0,1) (dQ = dG = dA = 0 unless `dense_tangents`).
+Seeds: 20250307 + config index.  No solver is needed: (z, λ, ν) is the exact
+primal–dual optimum of the generated problem.
+"""
+
+import math
+
+import numpy as np
+
+SEED0 = 20250307
+
+# BASELINE.json configs (index → shape); p = 0 assumed where unspecified
+QP_CONFIGS = {
+    1: dict(n=50, m=80, p=30, phi=0.2, batch=1),
+    2: dict(n=200, m=300, p=0, phi=0.3, batch=1024),
+    3: dict(n=1000, m=1500, p=0, phi=0.3, batch=8192),
+}
+CONIC_CONFIGS = {
+    4: dict(n=500, cones=[(3, 25)] * 20, batch=512),
+    5: dict(n=500, cones=[(4, 1275)] * 10, batch=64),
+}
+
+
+def qp_numpy(batch, n, m, p, phi, seed, dense_tangents=False):
+    rng = np.random.default_rng(seed)
+    out = {k: [] for k in ["Q", "q", "G", "h", "A", "b", "z", "lam", "nu", "dl_dz",
+                           "dq", "dh", "db", "dQ", "dG", "dA"]}
+    k_act = int(math.floor(phi * m))
+    for _ in range(batch):
+        L = rng.standard_normal((n, n))
+        Q = L @ L.T / n + 0.1 * np.eye(n)
+        G = rng.standard_normal((m, n)) / math.sqrt(n)
+        A = rng.standard_normal((p, n)) / math.sqrt(n)
+        z = rng.standard_normal(n)
+        perm = rng.permutation(m)
+        lam = np.zeros(m)
+        s = np.zeros(m)
+        act, ina = perm[:k_act], perm[k_act:]
+        lam[act] = rng.uniform(0.5, 1.5, size=k_act)
+        s[ina] = -rng.uniform(0.5, 1.5, size=m - k_act)
+        nu = rng.standard_normal(p)
+        h = G @ z - s
+        b = A @ z
+        q = -(Q @ z + G.T @ lam + A.T @ nu)
+        out["Q"].append(Q); out["q"].append(q); out["G"].append(G); out["h"].append(h)
+        out["A"].append(A); out["b"].append(b); out["z"].append(z); out["lam"].append(lam)
+        out["nu"].append(nu)
+        out["dl_dz"].append(rng.standard_normal(n))
+        out["dq"].append(rng.standard_normal(n))
+        out["dh"].append(rng.standard_normal(m))
+        out["db"].append(rng.standard_normal(p))
+        if dense_tangents:
+            S = rng.standard_normal((n, n))
+            out["dQ"].append((S + S.T) / 2)
+            out["dG"].append(rng.standard_normal((m, n)))
+            out["dA"].append(rng.standard_normal((p, n)))
+    res = {k: np.stack(v) for k, v in out.items() if v}
+    return res
+
+
+def qp_config_numpy(cfg, batch=None, **kw):
+    c = QP_CONFIGS[cfg]
+    return qp_numpy(batch or c["batch"], c["n"], c["m"], c["p"], c["phi"], SEED0 + cfg, **kw)
+
+
+def qp_torch(batch, n, m, p, phi, seed, device="cuda", rank_offset=0):
+    """Same construction on the GPU with torch (for bench-sized batches).
+    `rank_offset` shifts the seed so every rank gets distinct problems."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed * 1000003 + rank_offset)
+    f64 = dict(dtype=torch.float64, device=device)
+    L = torch.randn(batch, n, n, generator=g, **f64)
+    Q = L @ L.transpose(1, 2) / n + 0.1 * torch.eye(n, **f64)
+    del L
+    G = torch.randn(batch, m, n, generator=g, **f64) / math.sqrt(n)
+    A = torch.randn(batch, p, n, generator=g, **f64) / math.sqrt(n)
+    z = torch.randn(batch, n, generator=g, **f64)
+    k_act = int(math.floor(phi * m))
+    keys = torch.rand(batch, m, generator=g, device=device)
+    perm = torch.argsort(keys, dim=1)
+    act = torch.zeros(batch, m, dtype=torch.bool, device=device)
+    act.scatter_(1, perm[:, :k_act], True)
+    lam = torch.where(act, 0.5 + torch.rand(batch, m, generator=g, **f64), torch.zeros((), **f64))
+    s = torch.where(act, torch.zeros((), **f64), -(0.5 + torch.rand(batch, m, generator=g, **f64)))
+    nu = torch.randn(batch, p, generator=g, **f64)
+    h = torch.einsum("bmn,bn->bm", G, z) - s
+    b = torch.einsum("bpn,bn->bp", A, z)
+    q = -(torch.einsum("bij,bj->bi", Q, z) + torch.einsum("bmn,bm->bn", G, lam)
+          + torch.einsum("bpn,bp->bn", A, nu))
+    return dict(Q=Q, q=q, G=G, h=h, A=A, b=b, z=z, lam=lam, nu=nu,
+                dl_dz=torch.randn(batch, n, generator=g, **f64),
+                dq=torch.randn(batch, n, generator=g, **f64),
+                dh=torch.randn(batch, m, generator=g, **f64),
+                db=torch.randn(batch, p, generator=g, **f64))
+
+
+# ---------------------------------------------------------------------------
+# conic: optimal (x, s, y) by construction, complementary boundary pairs
+# ---------------------------------------------------------------------------
+def _tri(X):
+    d = X.shape[0]
+    return np.array([X[i, j] for j in range(d) for i in range(j + 1)])
+
+
+def conic_numpy(batch, n, cones, seed, guard=1e-3):
+    """Geometric form A_moi x + b_moi ∈ K with primal slack s ∈ K, dual y ∈ K*,
+    ⟨s, y⟩ = 0 per cone (MOI set_dot), dual feasibility c = A_moiᵀ W y with
+    W the set_dot weights (2 on PSD off-diagonal triangle entries)."""
+    rng = np.random.default_rng(seed)
+    m = sum(d for _, d in cones)
+    out = {k: [] for k in ["A", "b", "c", "x", "s", "y", "dx", "dA", "db", "dc"]}
+    for _ in range(batch):
+        s = np.zeros(m)
+        y = np.zeros(m)
+        wts = np.ones(m)
+        o = 0
+        for code, dim in cones:
+            if code == 0:       # Zeros: s = 0, y free
+                y[o:o + dim] = rng.standard_normal(dim)
+            elif code in (1, 2):  # Nonneg / Nonpos: complementary, guard band
+                sg = 1.0 if code == 1 else -1.0
+                act = rng.random(dim) < 0.5
+                mag_s = rng.uniform(0.5, 1.5, dim)
+                mag_y = rng.uniform(0.5, 1.5, dim)
+                s[o:o + dim] = np.where(act, 0.0, sg * mag_s)
+                y[o:o + dim] = np.where(act, sg * mag_y, 0.0)
+            elif code == 3:     # SOC: s = α(‖u‖, u), y = β(‖u‖, −u)
+                u = rng.standard_normal(dim - 1)
+                nu_ = np.linalg.norm(u)
+                al, be = rng.uniform(0.5, 1.5), rng.uniform(0.5, 1.5)
+                s[o] = al * nu_
+                s[o + 1:o + dim] = al * u
+                y[o] = be * nu_
+                y[o + 1:o + dim] = -be * u
+            elif code == 4:     # PSD: S = V diag(σ) Vᵀ, Y = V diag(ω) Vᵀ, σ∘ω = 0
+                d = int((math.isqrt(8 * dim + 1) - 1) // 2)
+                V, _ = np.linalg.qr(rng.standard_normal((d, d)))
+                r = d // 2
+                sig = np.concatenate([rng.uniform(0.5, 1.5, r), np.zeros(d - r)])
+                om = np.concatenate([np.zeros(r), rng.uniform(0.5, 1.5, d - r)])
+                s[o:o + dim] = _tri((V * sig) @ V.T)
+                y[o:o + dim] = _tri((V * om) @ V.T)
+                wts[o:o + dim] = np.array([1.0 if i == j else 2.0
+                                           for j in range(d) for i in range(j + 1)])
+            o += dim
+        A = rng.standard_normal((m, n)) / math.sqrt(n)
+        x = rng.standard_normal(n)
+        b = s - A @ x                      # A x + b = s ∈ K
+        c = A.T @ (wts * y)                # c − A_moiᵀ W y = 0 (MOI dual feasibility)
+        out["A"].append(A); out["b"].append(b); out["c"].append(c); out["x"].append(x)
+        out["s"].append(s); out["y"].append(y)
+        out["dx"].append(rng.standard_normal(n))
+        out["dA"].append(rng.standard_normal((m, n)))
+        out["db"].append(rng.standard_normal(m))
+        out["dc"].append(rng.standard_normal(n))
+    return {k: np.stack(v) for k, v in out.items()}

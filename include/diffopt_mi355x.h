@@ -1,0 +1,157 @@
+/*
+ * diffopt_mi355x.h — C ABI of the MI355X-native DiffOpt sensitivity-solve engine.
+ *
+ * Drop-in boundary for DiffOpt.jl's differentiation back-ends (the
+ * `DiffOpt.AbstractModel` plugin layer, reference src/diff_opt.jl:274):
+ *   - QuadraticProgram back-end  (src/QuadraticProgram/QuadraticProgram.jl)
+ *   - ConicProgram back-end      (src/ConicProgram/ConicProgram.jl)
+ * A Julia `ccall` shim (diffopt.jl_amd/julia/DiffOptMI355X.jl)
+ * and the Python ctypes host (diffopt.jl_amd/diffopt_amd) bind exactly these
+ * symbols.  Plain C types only: no torch/HIP types cross the boundary except an
+ * opaque `void*` stream.
+ *
+ * Conventions
+ *   - Float64 everywhere; dense arrays are COLUMN-MAJOR (Julia order) and
+ *     BATCH-MAJOR: problem b's n×n `Q` starts at Q + b*n*n, its m×n `G` at
+ *     G + b*m*n, its vectors at v + b*len.
+ *   - QP duals are in OptNet sign (λ = −MOI dual of LessThan, ν = −MOI dual of
+ *     EqualTo: QuadraticProgram.jl:164-180); the caller applies the flip.
+ *   - Memory mode (dopt_set_memory): DOPT_MEM_HOST (default) — every pointer is a
+ *     host pointer, inputs are copied into engine-owned HBM and outputs copied
+ *     back before return.  DOPT_MEM_DEVICE — every pointer is a device pointer on
+ *     the handle's device; inputs given to dopt_*_set are BORROWED (not copied)
+ *     and must stay alive and unchanged until the next dopt_*_set or
+ *     dopt_destroy; outputs are written in place.
+ *   - Errors: return 0 on success; > 0 = LAPACK-style info of the FIRST
+ *     problem whose KKT factor is exactly singular (the Julia shim raises
+ *     LinearAlgebra.SingularException(info), matching `LHS \ RHS`);
+ *     < 0 = argument/device error, message in dopt_last_error(h).
+ *     Per-problem info: dopt_get_info().
+ *   - Threading: a handle is used by one host thread at a time (the reference
+ *     models are not thread-safe either).  Work runs on the handle's HIP stream;
+ *     every call is synchronous at return.
+ */
+#ifndef DIFFOPT_MI355X_H
+#define DIFFOPT_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DOPT_KIND_QP 0
+#define DOPT_KIND_CONIC 1
+
+#define DOPT_MEM_HOST 0
+#define DOPT_MEM_DEVICE 1
+
+/* cone codes for dopt_conic_set (MOI set → code); see oracle/cones.py */
+#define DOPT_CONE_ZEROS 0        /* MOI.Zeros           (dual: Reals)        */
+#define DOPT_CONE_NONNEG 1       /* MOI.Nonnegatives                          */
+#define DOPT_CONE_NONPOS 2       /* MOI.Nonpositives                          */
+#define DOPT_CONE_SOC 3          /* MOI.SecondOrderCone                       */
+#define DOPT_CONE_PSD_TRI 4      /* MOI.PositiveSemidefiniteConeTriangle      */
+
+#define DOPT_ABI_VERSION 1
+
+typedef struct dopt_handle dopt_handle;
+
+/* Create a batched model: `batch` independent problems of identical shape.
+ * QP:    n variables, m LessThan rows (G z ≤ h), p EqualTo rows (A z = b).
+ * CONIC: n variables, m conic rows (A x + b ∈ K), p ignored.
+ * Replaces: `MOI.instantiate(QuadraticProgram.Model)` / `ConicProgram.Model()`
+ * (reference moi_wrapper.jl:605-617; QuadraticProgram.jl:107-120;
+ * ConicProgram.jl:99-111). */
+int dopt_create(dopt_handle** h, int device, int64_t batch, int32_t n,
+                int32_t m, int32_t p, int32_t kind);
+int dopt_destroy(dopt_handle* h);
+const char* dopt_last_error(const dopt_handle* h);
+int dopt_abi_version(void);
+/* hipStream_t as void*; NULL = the legacy default (null) stream.  Until this
+ * is called the handle uses a private non-blocking stream.  A caller that
+ * produces device-mode inputs on stream S passes S here (PyTorch: the current
+ * stream) so the engine's kernels are ordered after that work. */
+int dopt_set_stream(dopt_handle* h, void* stream);
+int dopt_set_memory(dopt_handle* h, int32_t mem);
+
+/* ---- QuadraticProgram ------------------------------------------------------
+ * Problem data + primal-dual point.  Replaces `_gradient_cache`'s inputs
+ * (QuadraticProgram.jl:182-213: A, G, h, Q from MOI matrix form) and the
+ * `VariablePrimalStart` / `ConstraintDualStart` setters
+ * (diff_opt.jl:362-370, QuadraticProgram.jl:164-180).
+ * Q: n×n Hessian (symmetrised, utils.jl:46-69); G: m×n; h: m; A: p×n;
+ * z: n; lam: m; nu: p.  G/h/lam may be NULL iff m == 0; A/nu iff p == 0. */
+int dopt_qp_set(dopt_handle* h, const double* Q, const double* G,
+                const double* hvec, const double* A, const double* z,
+                const double* lam, const double* nu);
+/* Assemble the KKT matrix (create_LHS_matrix, QuadraticProgram.jl:256-282),
+ * select the solve branch per problem (`iterative = norm(Q) ≈ 0`, :333/:436)
+ * and LU-factorise it ONCE (the reference re-factorises per call, :490).
+ * Rows with λ_i == 0 and (Gz−h)_i != 0 are eliminated exactly (their
+ * unknowns decouple).  Optional: dopt_qp_reverse/forward factor on demand. */
+int dopt_qp_factor(dopt_handle* h);
+/* reverse_differentiate! (QuadraticProgram.jl:316-351):
+ * out[b] = [dz (n) | dλ (m) | dν (p)] = −LHS \ [dl_dz; 0; 0]. */
+int dopt_qp_reverse(dopt_handle* h, const double* dl_dz, double* out);
+/* forward_differentiate! (QuadraticProgram.jl:357-446):
+ * out[b] = [dz | dλ | dν] = −LHSᵀ \ [dQ z + dq + dGᵀλ + dAᵀν;
+ *                                    λ∘(dG z) − λ∘dh; dA z − db].
+ * Any tangent pointer may be NULL (= zero tangent).  dQ: n×n, dq: n,
+ * dG: m×n, dh: m, dA: p×n, db: p (user tangents of Q, q, G, h, A, b — the
+ * `_fill` sign handling of diff_opt.jl:594-656 is the caller's). */
+int dopt_qp_forward(dopt_handle* h, const double* dQ, const double* dq,
+                    const double* dG, const double* dh, const double* dA,
+                    const double* db, double* out);
+/* Fused forward + reverse for one factorisation (the batched throughput path;
+ * results identical to dopt_qp_reverse + dopt_qp_forward). */
+int dopt_qp_forward_reverse(dopt_handle* h, const double* dl_dz,
+                            const double* dQ, const double* dq,
+                            const double* dG, const double* dh,
+                            const double* dA, const double* db,
+                            double* out_rev, double* out_fwd);
+
+/* ---- ConicProgram ----------------------------------------------------------
+ * A: m×n MOI coefficients (A_moi x + b ∈ K; the diffcp sign flip of
+ * ConicProgram.jl:179-183 is applied inside), b: m MOI constants, c: n
+ * objective (already negated by the caller for MAX_SENSE, :206-208),
+ * x: n, s: m (ConstraintPrimalStart), y: m (ConstraintDualStart).
+ * cone_desc: 2*ncones int32 pairs (code, dimension) in row order (the
+ * ProductOfSets layout, product_of_sets.jl:15-74); identical for every
+ * problem of the batch. */
+int dopt_conic_set(dopt_handle* h, const double* A, const double* b,
+                   const double* c, const double* x, const double* s,
+                   const double* y, const int32_t* cone_desc, int32_t ncones);
+/* _gradient_cache (ConicProgram.jl:172-255): v = y − s, Dπ(v), π(v), M. */
+int dopt_conic_factor(dopt_handle* h);
+/* forward_differentiate! (ConicProgram.jl:257-334): out[b] = [du | dv | dw]
+ * (n+m+1) = lsqr(M, [dAᵀvp + dc; −dA x + db; −dc·x − db·vp]) (0 if the RHS is
+ * exactly zero, :320).  out_dx (optional, n per problem) receives
+ * ForwardVariablePrimal = −(du − x·dw) (:403-412).  dA/db/dc may be NULL. */
+int dopt_conic_forward(dopt_handle* h, const double* dA, const double* db,
+                       const double* dc, double* out, double* out_dx);
+/* reverse_differentiate! (ConicProgram.jl:336-394), dy = ds = 0:
+ * out_g[b] = lsqr(M, [dx; 0; −xᵀdx]) (0 if its norm ≤ 1e-4, :369-370).
+ * Optional outputs (any may be NULL): out_dA (m×n col-major) =
+ * g_v xᵀ − vp g_xᵀ, out_db (m) = g_v − g_end·vp, out_dc (n) = g_x − g_end·x
+ * (getters :396-443). */
+int dopt_conic_reverse(dopt_handle* h, const double* dx, double* out_g,
+                       double* out_dA, double* out_db, double* out_dc);
+
+/* ---- introspection ---------------------------------------------------------*/
+/* per-problem status of the last factor/solve: QP: 0 ok, k>0 zero pivot at
+ * column k of the (reduced) KKT; CONIC: LSQR istop of the last solve. */
+int dopt_get_info(dopt_handle* h, int32_t* info);
+/* per-problem `iterative` branch flags (QP; 1 = LSQR branch). */
+int dopt_get_iterative(dopt_handle* h, int8_t* flags);
+/* per-problem size of the factorised (reduced) KKT system (QP) or LSQR
+ * iteration count of the last solve (CONIC). */
+int dopt_get_system_size(dopt_handle* h, int32_t* sizes);
+/* wall time (s) of the last forward/reverse call, incl. any factorisation it
+ * triggered — the DifferentiateTimeSec analogue (diff_opt.jl:256-266). */
+double dopt_last_time(const dopt_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DIFFOPT_MI355X_H */

@@ -1,0 +1,230 @@
+"""QP path on the MI355X: HIP engine vs the CPU oracle and the reference's
+golden fixtures.  Parity bar (BASELINE.json north_star): 1e-6 relative
+Frobenius in Float64 on (dz, dλ, dν) forward and reverse; bit-exact discrete
+selections (iterative branch, eliminated-row set)."""
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import qp as oqp
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+RTOL = 1e-6   # relative Frobenius, north_star
+
+
+def relfro(a, b):
+    a = np.asarray(a, dtype=float)
+    b = np.asarray(b, dtype=float)
+    nb = np.linalg.norm(b)
+    return np.linalg.norm(a - b) / (nb if nb > 0 else 1.0)
+
+
+@pytest.fixture(scope="module")
+def QPBatch():
+    from diffopt_amd.qp import QPBatch
+    return QPBatch
+
+
+def _fixtures():
+    out = []
+    for f in ["qp_fixtures.json", "lp_fixtures.json"]:
+        with open(os.path.join(HERE, "golden", f)) as fh:
+            out += json.load(fh)
+    return out
+
+
+FX = _fixtures()
+
+
+def _arr(fx):
+    a = {k: np.array(v, dtype=float) for k, v in fx.items() if isinstance(v, list)}
+    n = a["Q"].shape[0]
+    a["G"] = a["G"].reshape(-1, n)
+    a["A"] = a["A"].reshape(-1, n)
+    fw = {k: np.array(v, dtype=float) for k, v in fx["fwd"].items()}
+    if "dG" in fw:
+        fw["dG"] = fw["dG"].reshape(a["G"].shape)
+    if "dA" in fw:
+        fw["dA"] = fw["dA"].reshape(a["A"].shape)
+    return a, fw
+
+
+def _engine_solve(QPBatch, a, fw):
+    n, m, p = a["Q"].shape[0], a["G"].shape[0], a["A"].shape[0]
+    e = QPBatch(1, n, m, p)
+    e.set(a["Q"][None], a["G"][None], a["h"][None], a["A"][None], a["z"][None],
+          a["lam"][None], a["nu"][None])
+    rev = e.reverse(a["dzb"][None])[0]
+    kw = {k: v[None] for k, v in fw.items() if v.size}
+    fwd = e.forward(**kw)[0]
+    it = bool(e.iterative()[0])
+    return (rev[:n], rev[n:n + m], rev[n + m:]), (fwd[:n], fwd[n:n + m], fwd[n + m:]), it
+
+
+@pytest.mark.parametrize("fx", FX, ids=[f["name"] for f in FX])
+def test_engine_matches_reference_fixture_and_oracle(QPBatch, fx):
+    from test_oracle_golden import qp_outputs
+    a, fw = _arr(fx)
+    (dz, dl, dn), (fz, fl, fn), it = _engine_solve(QPBatch, a, fw)
+    assert it == oqp.is_iterative(a["Q"])            # bit-exact branch selection
+    got = qp_outputs(a, fw, solve_rev=lambda: (dz, dl, dn), solve_fwd=lambda: fz)
+    for k, v in fx["expect"].items():                 # the reference's own values
+        exp = np.array(v, dtype=float).reshape(np.shape(got[k]))
+        np.testing.assert_allclose(got[k], exp, atol=fx["atol"], rtol=fx["rtol"], err_msg=k)
+    Q, G, h, A, z, lam, nu = (a[k] for k in ["Q", "G", "h", "A", "z", "lam", "nu"])
+    rz, rl, rn = oqp.reverse_differentiate(Q, G, h, A, z, lam, nu, a["dzb"])
+    oz, ol, on = oqp.forward_differentiate(Q, G, h, A, z, lam, nu, **fw)
+    # relative Frobenius per direction on the stacked [dz|dλ|dν] (a block whose
+    # exact value is 0 — e.g. dλ of eliminated rows — is measured on that scale)
+    for g, r in [((dz, dl, dn), (rz, rl, rn)), ((fz, fl, fn), (oz, ol, on))]:
+        assert relfro(np.concatenate(g), np.concatenate(r)) <= RTOL
+
+
+def _synthetic(batch, n, m, p, phi, seed, dense=False):
+    from diffopt_amd.synthetic import qp_numpy
+    return qp_numpy(batch, n, m, p, phi, seed, dense_tangents=dense)
+
+
+def _check_batch(QPBatch, d, dense=False):
+    B, n = d["z"].shape
+    m = d["lam"].shape[1]
+    p = d["nu"].shape[1]
+    e = QPBatch(B, n, m, p)
+    e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    fkw = dict(dq=d["dq"], dh=d["dh"], db=d["db"])
+    if dense:
+        fkw.update(dQ=d["dQ"], dG=d["dG"], dA=d["dA"])
+    rev, fwd = e.forward_reverse(d["dl_dz"], **fkw)
+    sizes = e.system_size()
+    worst = 0.0
+    for b in range(B):
+        args = [d[k][b] for k in ["Q", "G", "h", "A", "z", "lam", "nu"]]
+        rz, rl, rn = oqp.reverse_differentiate(*args, d["dl_dz"][b])
+        fk = {k: v[b] for k, v in fkw.items()}
+        oz, ol, on = oqp.forward_differentiate(*args, **fk)
+        worst = max(worst, relfro(rev[b], np.concatenate([rz, rl, rn])),
+                    relfro(fwd[b], np.concatenate([oz, ol, on])))
+        # bit-exact elimination set: λ == 0 and (Gz − h) != 0 (Julia summation order)
+        s = oqp.gz_minus_h(d["G"][b], d["z"][b], d["h"][b])
+        kept = np.count_nonzero(~((d["lam"][b] == 0) & (s != 0)))
+        assert sizes[b] == n + kept + p
+    assert worst <= RTOL, worst
+    return e
+
+
+def test_cfg1_shape_batch(QPBatch):
+    _check_batch(QPBatch, _synthetic(4, 50, 80, 30, 0.2, 20250308))
+
+
+def test_cfg2_shape_small_batch(QPBatch):
+    _check_batch(QPBatch, _synthetic(6, 200, 300, 0, 0.3, 20250309))
+
+
+def test_dense_tangents(QPBatch):
+    _check_batch(QPBatch, _synthetic(3, 40, 60, 10, 0.5, 7, dense=True), dense=True)
+
+
+def test_generic_large_system_path(QPBatch):
+    """Reduced system > 512 unknowns takes the generic LU kernel."""
+    _check_batch(QPBatch, _synthetic(2, 300, 400, 20, 0.6, 11))
+
+
+def test_ragged_shapes(QPBatch):
+    for (n, m, p) in [(1, 1, 0), (3, 0, 0), (5, 0, 2), (7, 3, 0), (33, 31, 1), (64, 1, 63)]:
+        _check_batch(QPBatch, _synthetic(2, n, m, p, 0.5, 100 + n))
+
+
+def test_reverse_forward_separately_equal_fused(QPBatch):
+    d = _synthetic(5, 30, 40, 5, 0.4, 3)
+    B, n = d["z"].shape
+    e = QPBatch(B, n, 40, 5)
+    e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    r1, f1 = e.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
+    e.factor()
+    r2 = e.reverse(d["dl_dz"])
+    f2 = e.forward(dq=d["dq"], dh=d["dh"], db=d["db"])
+    np.testing.assert_array_equal(r1, r2)
+    np.testing.assert_array_equal(f1, f2)
+
+
+def test_singular_kkt_raises(QPBatch):
+    """λ_i == 0 and s_i == 0 → zero row/column in LHS → SingularException."""
+    from diffopt_amd import SingularException
+    Q = np.eye(2)[None]
+    G = np.array([[[1.0, 0.0]]])
+    z = np.array([[1.0, 2.0]])
+    h = np.array([1.0])[None]           # s = Gz − h = 0
+    lam = np.zeros((1, 1))
+    e = QPBatch(1, 2, 1, 0)
+    e.set(Q, G, h, np.zeros((1, 0, 2)), z, lam, np.zeros((1, 0)))
+    with pytest.raises(SingularException):
+        e.reverse(np.ones((1, 2)))
+    assert e.info()[0] > 0
+
+
+def test_lp_iterative_batch_mixed_with_qp(QPBatch):
+    """A batch mixing Q == 0 (LSQR branch) and Q != 0 (LU branch)."""
+    with open(os.path.join(HERE, "golden", "lp_fixtures.json")) as fh:
+        lp = json.load(fh)
+    fx = [f for f in lp if f["name"] == "lp_simplex"][0]
+    a, fw = _arr(fx)
+    n, m = a["Q"].shape[0], a["G"].shape[0]
+    Qs = np.stack([a["Q"], np.eye(n)])
+    e = QPBatch(2, n, m, 0)
+    e.set(Qs, np.stack([a["G"]] * 2), np.stack([a["h"]] * 2), np.zeros((2, 0, n)),
+          np.stack([a["z"]] * 2), np.stack([a["lam"]] * 2), np.zeros((2, 0)))
+    rev = e.reverse(np.stack([a["dzb"]] * 2))
+    assert list(e.iterative()) == [True, False]
+    for b in range(2):
+        rz, rl, rn = oqp.reverse_differentiate(Qs[b], a["G"], a["h"], np.zeros((0, n)),
+                                               a["z"], a["lam"], np.zeros(0), a["dzb"])
+        assert relfro(rev[b], np.concatenate([rz, rl, rn])) <= RTOL
+
+
+def test_device_mode_matches_host_mode(QPBatch):
+    import torch
+    d = _synthetic(3, 20, 30, 4, 0.3, 5)
+    B, n = d["z"].shape
+    e = QPBatch(B, n, 30, 4)
+    e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    r1, f1 = e.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
+    t = {k: torch.tensor(v, device="cuda") for k, v in d.items()}
+    e2 = QPBatch(B, n, 30, 4)
+    e2.set(t["Q"], t["G"], t["h"], t["A"], t["z"], t["lam"], t["nu"])
+    r2, f2 = e2.forward_reverse(t["dl_dz"], dq=t["dq"], dh=t["dh"], db=t["db"])
+    np.testing.assert_array_equal(r1, r2.cpu().numpy())
+    np.testing.assert_array_equal(f1, f2.cpu().numpy())
+
+
+def test_full_cfg2_kkt_residual_property(QPBatch):
+    """BASELINE config 2 at full batch (1024 × n=200, m=300): size-independent
+    check — every solution satisfies its KKT system (reverse: LHS x = rhs,
+    forward: LHSᵀ x = rhs) to 1e-9 relative, computed in fp64 on the GPU."""
+    import torch
+    from diffopt_amd.synthetic import qp_torch
+    n, m, p = 200, 300, 0
+    d = qp_torch(1024, n, m, p, 0.3, 20250309)
+    e = QPBatch(1024, n, m, p)
+    e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    rev, fwd = e.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
+    torch.cuda.synchronize()
+    Q, G, z, lam = d["Q"], d["G"], d["z"], d["lam"]
+    s = torch.einsum("bmn,bn->bm", G, z) - d["h"]
+    # reverse: −x = rev ; LHS x = [dl; 0]
+    xz, xl = -rev[:, :n], -rev[:, n:]
+    r1 = torch.einsum("bij,bj->bi", Q, xz) + torch.einsum("bmn,bm->bn", G, lam * xl) - d["dl_dz"]
+    r2 = torch.einsum("bmn,bn->bm", G, xz) + s * xl
+    res = torch.sqrt((r1 ** 2).sum(1) + (r2 ** 2).sum(1)) / torch.linalg.norm(d["dl_dz"], dim=1)
+    assert float(res.max()) < 1e-9
+    # forward: LHSᵀ y = [dq; −λ dh]
+    yz, yl = -fwd[:, :n], -fwd[:, n:]
+    f1 = torch.einsum("bji,bj->bi", Q, yz) + torch.einsum("bmn,bm->bn", G, yl) - d["dq"]
+    f2 = lam * torch.einsum("bmn,bn->bm", G, yz) + s * yl - (-lam * d["dh"])
+    nrm = torch.sqrt((d["dq"] ** 2).sum(1) + ((lam * d["dh"]) ** 2).sum(1))
+    res = torch.sqrt((f1 ** 2).sum(1) + (f2 ** 2).sum(1)) / nrm
+    assert float(res.max()) < 1e-9
+    assert (e.info() == 0).all()
