@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""bench.py — KKT sensitivity solves/sec (forward + reverse) on batched dense QPs.
+
+Workload (BASELINE.json configs[1] = config 2): per GPU a batch of 1024 dense
+QPs, n = 200 variables, m = 300 inequalities (p = 0), 30 % active, synthetic
+(seeded, KKT point by construction — SURVEY.md §8(d)), inputs resident in HBM
+before the timed region.  One step = for every problem of the batch: KKT
+assembly + LU factorisation + reverse solve (dl/dz → dz, dλ, dν) + forward
+solve (dq, dh → dz, dλ, dν) — the reference refactorises per call; the engine
+factors once per step and reuses it for both directions.  N > 1: one process
+per GPU, problems sharded (weak scaling: 1024 per rank), plus one RCCL
+all-gather of the packed sensitivities per step (§8(e)).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (driver, N > 1)
+
+Prints ONE JSON line on rank 0 (the driver's contract), with `roofline`
+(dominant kernel, timed live with HIP events on the engine's stream) and
+`cpu_baseline` (the oracle restatement timed on the host's cores).
+"""
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "diffopt.jl_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+PEAK_FP64_TFLOPS = 78.6     # MI355X FP64 matrix/vector dense (spec; probe measured 75.4)
+PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+QP_CFG = {2: dict(n=200, m=300, p=0, phi=0.3, batch=1024),
+          3: dict(n=1000, m=1500, p=0, phi=0.3, batch=1024)}
+
+
+# --------------------------------------------------------------------------
+# CPU baseline: the oracle restatement of the reference algorithm (sparse LU of
+# the full KKT via SuperLU, re-factorised for reverse and for forward exactly
+# as QuadraticProgram.jl:490 does), one process per core.
+# --------------------------------------------------------------------------
+def _cpu_worker(args):
+    cfg, seed, seconds = args
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"
+    from diffopt_amd.synthetic import qp_numpy
+    from oracle import qp as oqp
+    d = qp_numpy(1, cfg["n"], cfg["m"], cfg["p"], cfg["phi"], seed)
+    a = [d[k][0] for k in ["Q", "G", "h", "A", "z", "lam", "nu"]]
+    n_done = 0
+    t0 = time.perf_counter()
+    while True:
+        oqp.reverse_differentiate(*a, d["dl_dz"][0], sparse=True)
+        oqp.forward_differentiate(*a, dq=d["dq"][0], dh=d["dh"][0], sparse=True)
+        n_done += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    return n_done, time.perf_counter() - t0
+
+
+def cpu_baseline(cfg, seconds, workers):
+    import multiprocessing as mp
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        res = pool.map(_cpu_worker, [(cfg, 1000 + i, seconds) for i in range(workers)])
+    wall = time.perf_counter() - t0
+    solves = sum(r[0] for r in res)
+    rate = sum(r[0] / r[1] for r in res)
+    return dict(value=round(rate, 2), unit="solves/s", cores=workers, kind="port",
+                sample=(f"{solves} config-2 QP solves (n={cfg['n']}, m={cfg['m']}, fwd+rev, "
+                        f"SuperLU re-factorised per direction) on {workers} processes "
+                        f"× {seconds:.0f} s (wall {wall:.1f} s)"))
+
+
+def _load_pmc(kernel):
+    """HBM bytes/launch for `kernel` from the committed rocprofv3 --pmc summary
+    (tools/pmc_summary.py → profiles/pmc_latest.json), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(path) as f:
+            return json.load(f)["kernels"][kernel]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(QP_CFG))
+    ap.add_argument("--batch", type=int, default=None, help="problems per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-workers", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-allgather", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    cfg = dict(QP_CFG[args.config])
+    if args.batch:
+        cfg["batch"] = args.batch
+    B, n, m, p = cfg["batch"], cfg["n"], cfg["m"], cfg["p"]
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        workers = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
+        cpu = cpu_baseline(cfg, args.cpu_seconds, workers)
+
+    import torch
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local_rank))
+    from diffopt_amd.qp import QPBatch
+    from diffopt_amd.synthetic import SEED0, qp_torch
+
+    d = qp_torch(B, n, m, p, cfg["phi"], SEED0 + args.config, rank_offset=rank)
+    eng = QPBatch(B, n, m, p, device=local_rank)
+    eng.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    L = n + m + p
+    out_rev = torch.empty(B, L, dtype=torch.float64, device="cuda")
+    out_fwd = torch.empty(B, L, dtype=torch.float64, device="cuda")
+    gathered = None
+    if world > 1 and not args.no_allgather:
+        gathered = torch.empty(world, B, 2 * L, dtype=torch.float64, device="cuda")
+        packed = torch.empty(B, 2 * L, dtype=torch.float64, device="cuda")
+
+    def step():
+        eng.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"] if p else None,
+                            out_rev=out_rev, out_fwd=out_fwd)
+        if gathered is not None:
+            packed[:, :L].copy_(out_rev)
+            packed[:, L:].copy_(out_fwd)
+            dist.all_gather_into_tensor(gathered.view(-1), packed.view(-1))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    sizes = eng.system_size()
+    eng.phase_times()                      # reset accumulators
+    eng.set_profiling(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    eng.set_profiling(False)
+    phases = eng.phase_times()
+    elapsed = t1 - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    if (eng.info() != 0).any():
+        raise RuntimeError("singular KKT in the benchmark batch")
+
+    if rank == 0:
+        # dominant kernel and its roofline (algorithmic work per launch ÷ avg
+        # launch time measured with HIP events on the engine's stream)
+        name, (ms_tot, cnt) = max(phases.items(), key=lambda kv: kv[1][0])
+        avg_s = ms_tot / cnt / 1e3
+        Ns = sizes.astype("float64")
+        if name == "qp_lu":
+            work = float((2.0 / 3.0 * Ns ** 3).sum())          # reduced-KKT LU flops
+            achieved = work / avg_s / 1e12
+            roof = dict(bound="mfma", achieved=round(achieved, 3), peak=PEAK_FP64_TFLOPS,
+                        unit="TFLOP/s", frac=round(achieved / PEAK_FP64_TFLOPS, 4))
+        else:
+            if name == "qp_solve":
+                work = float((8.0 * Ns ** 2).sum())               # one read of the LU factors
+            elif name == "qp_assemble":
+                work = float(B * 8.0 * (n * n + 2 * m * n) + (8.0 * Ns ** 2).sum())
+            elif name == "qp_prepare":
+                work = float(B * 8.0 * (n * n + m * n + 3 * m + n))
+            else:
+                work = float(B * 8.0 * (m * n + 2 * L))
+            achieved = work / avg_s / 1e9
+            roof = dict(bound="hbm", achieved=round(achieved, 1), peak=PEAK_HBM_GBS,
+                        unit="GB/s", frac=round(achieved / PEAK_HBM_GBS, 4))
+        roof["kernel"] = name
+        roof["traffic"] = _load_pmc(name)
+        roof["avg_launch_ms"] = round(avg_s * 1e3, 4)
+        roof["phases_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in sorted(phases.items())}
+        value = world * B * args.steps / elapsed
+        line = {
+            "metric": "KKT sensitivity solves/sec (fwd+rev) on batched QPs",
+            "value": round(value, 1),
+            "unit": "solves/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded KKT point by construction, SURVEY.md §8(d))",
+            "config": {"workload": f"config {args.config}: dense QP batch, fwd+rev sensitivities",
+                       "problems_per_gpu": B, "n": n, "m_ineq": m, "p_eq": p,
+                       "active_fraction": cfg["phi"],
+                       "reduced_kkt_size_mean": round(float(Ns.mean()), 1),
+                       "parallelism": f"batch-sharded x{world}" + (" + RCCL all-gather" if gathered is not None else "")},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -125,6 +125,11 @@ int dopt_destroy(dopt_handle* h) {
   for (auto& b : h->own_cin) b.release();
   for (auto& b : h->tin) b.release();
   for (auto& b : h->tout) b.release();
+  for (auto& pe : h->ev_pending) {
+    (void)hipEventDestroy(pe.second.first);
+    (void)hipEventDestroy(pe.second.second);
+  }
+  for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -298,6 +303,37 @@ int dopt_get_system_size(dopt_handle* h, int32_t* sizes) {
 }
 
 double dopt_last_time(const dopt_handle* h) { return h ? h->last_time : -1.0; }
+
+int dopt_set_profiling(dopt_handle* h, int32_t on) {
+  return guarded(h, [&]() {
+    h->collect_phases();
+    h->prof = on != 0;
+    return 0;
+  });
+}
+
+int dopt_get_phase_times(dopt_handle* h, double* ms, int32_t* counts, int32_t nphases) {
+  return guarded(h, [&]() {
+    if (nphases < 0 || nphases > DOPT_NUM_PHASES) throw Error(-1, "bad nphases");
+    h->collect_phases();
+    for (int i = 0; i < nphases; ++i) {
+      if (ms) ms[i] = h->phase_ms[i];
+      if (counts) counts[i] = h->phase_cnt[i];
+    }
+    for (int i = 0; i < DOPT_NUM_PHASES; ++i) {
+      h->phase_ms[i] = 0.0;
+      h->phase_cnt[i] = 0;
+    }
+    return 0;
+  });
+}
+
+const char* dopt_phase_name(int32_t phase) {
+  static const char* names[DOPT_NUM_PHASES] = {
+      "qp_prepare", "qp_assemble", "qp_lu", "qp_rhs", "qp_solve", "qp_lsqr", "qp_output",
+      "conic_cone", "conic_rhs", "conic_lsqr", "conic_output"};
+  return (phase >= 0 && phase < DOPT_NUM_PHASES) ? names[phase] : "unknown";
+}
 
 // ---- conic -----------------------------------------------------------------
 int dopt_conic_set(dopt_handle* h, const double* A, const double* b, const double* c,

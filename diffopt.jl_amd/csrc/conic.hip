@@ -1,11 +1,733 @@
-// Conic sensitivity path (ConicProgram.jl) — implemented in a follow-up commit.
+// Conic sensitivity path (ConicProgram.jl) on gfx950: cone projections and
+// their derivatives (MathOptSetDistances semantics on the dual cones,
+// diff_opt.jl:491-519), and a matrix-free batched LSQR on
+//   M = [0, AᵀDπ, c; −A, I−Dπ, b; −cᵀ, −bᵀDπ, 0]     (ConicProgram.jl:243-247)
+// with A = −A_moi (diffcp sign), never materialised: every M·z / Mᵀ·r is one
+// A_moi·(·) GEMV, one A_moiᵀ·(·) GEMV and a structured Dπ apply.
+//
+// Structured Dπ per cone (stored per problem in `params`):
+//   Zeros        : identity                        (no storage)
+//   Nonneg/Nonpos: diagonal                         (k doubles)
+//   SOC          : [case, t, ‖x‖] + x from v        (4 doubles)
+//   PSD triangle : U (d×d eigenvectors, row-major) and the Daleckii–Krein
+//                  weight matrix B (d×d) → Dπ w = S² J (S⁻² w),
+//                  Dπᵀ w = J w, J w = tri(U (B ∘ (Uᵀ smat(w) U)) Uᵀ)
+//                  (Dπ = S²JS⁻² = Jᵀ: the convention pinned by the reference's
+//                  PSD fixtures, oracle/cones.py)
 #include "dopt_internal.h"
+
 namespace dopt {
-void conic_factor(Handle&) { throw Error(-5, "conic path not built yet"); }
-void conic_forward(Handle&, const double*, const double*, const double*, double*, double*) {
-  throw Error(-5, "conic path not built yet");
+
+constexpr int CTPB = 256;
+constexpr int PSD_MAX = 64;
+
+struct ConeDesc {
+  int32_t code, dim, row, poff;  // poff: offset into the per-problem param block
+};
+
+__device__ __forceinline__ double cwave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
 }
-void conic_reverse(Handle&, const double*, double*, double*, double*, double*) {
-  throw Error(-5, "conic path not built yet");
+
+__device__ __forceinline__ double cblock_sum(double v, double* red) {
+  v = cwave_sum(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
 }
+
+__device__ __forceinline__ int psd_side(int dim) {
+  int d = 0;
+  while ((d + 1) * (d + 2) / 2 <= dim) ++d;
+  return d;
+}
+
+// triangle index (i ≤ j) in MOI column-wise upper-triangle order
+__device__ __forceinline__ int tri_idx(int i, int j) { return j * (j + 1) / 2 + i; }
+
+// ---------------------------------------------------------------------------
+// cone kernel: v = y − s; vp = π(v); structured Dπ parameters.
+// grid (ncones, batch); one workgroup per cone.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(CTPB) void conic_cone_kernel(
+    const ConeDesc* __restrict__ cones, int ncones, const double* __restrict__ y,
+    const double* __restrict__ s, int m, int plen, double* __restrict__ v_out,
+    double* __restrict__ vp_out, double* __restrict__ params) {
+  __shared__ double X[PSD_MAX][PSD_MAX + 1];
+  __shared__ double V[PSD_MAX][PSD_MAX + 1];
+  __shared__ double red[8];
+  __shared__ double rot_c[PSD_MAX / 2], rot_s[PSD_MAX / 2];
+  __shared__ int pp[PSD_MAX / 2], qq[PSD_MAX / 2];
+  __shared__ int perm[PSD_MAX];
+  const int k = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const ConeDesc cd = cones[k];
+  const double* yb = y + (size_t)b * m + cd.row;
+  const double* sb = s + (size_t)b * m + cd.row;
+  double* vb = v_out + (size_t)b * m + cd.row;
+  double* vpb = vp_out + (size_t)b * m + cd.row;
+  double* P = params + (size_t)b * plen + cd.poff;
+  const int dim = cd.dim;
+  for (int i = t; i < dim; i += CTPB) vb[i] = yb[i] - sb[i];
+  __syncthreads();
+  if (cd.code == DOPT_CONE_ZEROS) {
+    for (int i = t; i < dim; i += CTPB) vpb[i] = vb[i];
+  } else if (cd.code == DOPT_CONE_NONNEG || cd.code == DOPT_CONE_NONPOS) {
+    const bool pos = cd.code == DOPT_CONE_NONNEG;
+    for (int i = t; i < dim; i += CTPB) {
+      const double x = vb[i];
+      const double sg = (x > 0.0) ? 1.0 : ((x < 0.0) ? -1.0 : 0.0);
+      vpb[i] = pos ? fmax(x, 0.0) : fmin(x, 0.0);
+      P[i] = pos ? (sg + 1.0) / 2.0 : (1.0 - sg) / 2.0;
+    }
+  } else if (cd.code == DOPT_CONE_SOC) {
+    double ss = 0.0;
+    for (int i = 1 + t; i < dim; i += CTPB) ss = fma(vb[i], vb[i], ss);
+    const double nx = sqrt(cblock_sum(ss, red));
+    const double tt = vb[0];
+    int cs;
+    if (nx <= tt) cs = 0;           // interior: π = v, Dπ = I
+    else if (nx <= -tt) cs = 1;     // polar: π = 0, Dπ = 0
+    else cs = 2;
+    for (int i = t; i < dim; i += CTPB) {
+      double pv;
+      if (cs == 0) pv = vb[i];
+      else if (cs == 1) pv = 0.0;
+      else pv = ((nx + tt) / 2.0) * (i == 0 ? 1.0 : vb[i] / nx);
+      vpb[i] = pv;
+    }
+    if (t == 0) { P[0] = cs; P[1] = tt; P[2] = nx; P[3] = 0.0; }
+  } else if (cd.code == DOPT_CONE_PSD_TRI) {
+    const int d = psd_side(dim);
+    // X = smat(v) (unscaled), V = I
+    for (int e = t; e < d * d; e += CTPB) {
+      const int i = e / d, j = e % d;
+      X[i][j] = (i <= j) ? vb[tri_idx(i, j)] : vb[tri_idx(j, i)];
+      V[i][j] = (i == j) ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    // parallel cyclic Jacobi (round-robin pairing), d padded to even
+    const int de = d + (d & 1);
+    double fro = 0.0;
+    for (int e = t; e < d * d; e += CTPB) fro = fma(X[e / d][e % d], X[e / d][e % d], fro);
+    const double nrm2 = cblock_sum(fro, red);
+    for (int sweep = 0; sweep < 40; ++sweep) {
+      double off = 0.0;
+      for (int e = t; e < d * d; e += CTPB) {
+        const int i = e / d, j = e % d;
+        if (i != j) off = fma(X[i][j], X[i][j], off);
+      }
+      off = cblock_sum(off, red);
+      if (off <= 1e-32 * nrm2 || off == 0.0) break;
+      for (int step = 0; step < de - 1; ++step) {
+        // round-robin pairs: position 0 fixed, others rotate
+        if (t < de / 2) {
+          auto at = [&](int pos) { return pos == 0 ? 0 : 1 + ((pos - 1 + step) % (de - 1)); };
+          int a = at(t), c = at(de - 1 - t);
+          if (a > c) { const int tmp = a; a = c; c = tmp; }
+          pp[t] = a;
+          qq[t] = c;
+          double cth = 1.0, sth = 0.0;
+          if (c < d) {
+            const double apq = X[a][c];
+            if (apq != 0.0) {
+              const double app = X[a][a], aqq = X[c][c];
+              const double tau = (aqq - app) / (2.0 * apq);
+              const double tn = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+              cth = 1.0 / sqrt(1.0 + tn * tn);
+              sth = tn * cth;
+            }
+          }
+          rot_c[t] = cth;
+          rot_s[t] = sth;
+        }
+        __syncthreads();
+        // rows: X ← Jᵀ X
+        for (int e = t; e < (de / 2) * d; e += CTPB) {
+          const int r = e / d, col = e % d;
+          const int a = pp[r], c = qq[r];
+          if (c < d) {
+            const double cth = rot_c[r], sth = rot_s[r];
+            const double xa = X[a][col], xc = X[c][col];
+            X[a][col] = cth * xa - sth * xc;
+            X[c][col] = sth * xa + cth * xc;
+          }
+        }
+        __syncthreads();
+        // columns: X ← X J ; V ← V J
+        for (int e = t; e < (de / 2) * d; e += CTPB) {
+          const int r = e / d, row = e % d;
+          const int a = pp[r], c = qq[r];
+          if (c < d) {
+            const double cth = rot_c[r], sth = rot_s[r];
+            const double xa = X[row][a], xc = X[row][c];
+            X[row][a] = cth * xa - sth * xc;
+            X[row][c] = sth * xa + cth * xc;
+            const double va = V[row][a], vc = V[row][c];
+            V[row][a] = cth * va - sth * vc;
+            V[row][c] = sth * va + cth * vc;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // sort eigenpairs ascending (as LAPACK) — selection sort by one thread
+    if (t == 0) {
+      for (int i = 0; i < d; ++i) perm[i] = i;
+      for (int i = 0; i < d; ++i) {
+        int mi = i;
+        for (int j = i + 1; j < d; ++j)
+          if (X[perm[j]][perm[j]] < X[perm[mi]][perm[mi]]) mi = j;
+        const int tmp = perm[i]; perm[i] = perm[mi]; perm[mi] = tmp;
+      }
+    }
+    __syncthreads();
+    // params: U (row-major, columns = eigenvectors) then B, then flag
+    double* U = P;
+    double* Bm = P + d * d;
+    for (int e = t; e < d * d; e += CTPB) {
+      const int i = e / d, j = e % d;
+      U[i * d + j] = V[i][perm[j]];
+    }
+    int allpos = 1;
+    for (int i = 0; i < d; ++i) allpos &= (X[perm[i]][perm[i]] >= 0.0);
+    for (int e = t; e < d * d; e += CTPB) {
+      const int i = e / d, j = e % d;
+      const double li = X[perm[i]][perm[i]], lj = X[perm[j]][perm[j]];
+      double w;
+      if (li == lj) w = (li > 0.0) ? 1.0 : 0.0;
+      else w = (fmax(li, 0.0) - fmax(lj, 0.0)) / (li - lj);
+      Bm[i * d + j] = allpos ? 1.0 : w;
+    }
+    if (t == 0) P[2 * d * d] = allpos;
+    // vp = tri(U max(Λ,0) Uᵀ)
+    __syncthreads();
+    for (int e = t; e < dim; e += CTPB) {
+      int j = 0;
+      while ((j + 1) * (j + 2) / 2 <= e) ++j;
+      const int i = e - j * (j + 1) / 2;
+      double acc = 0.0;
+      for (int q = 0; q < d; ++q) acc = fma(V[i][perm[q]] * fmax(X[perm[q]][perm[q]], 0.0), V[j][perm[q]], acc);
+      vpb[e] = acc;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// structured Dπ apply inside a workgroup (all threads call).
+//   trans = 0: out = Dπ in ;  trans = 1: out = Dπᵀ in.   in/out: m vectors.
+// PSD scratch in LDS (`lds`, ≥ 3·PSD_MAX·(PSD_MAX+1) doubles).
+// ---------------------------------------------------------------------------
+__device__ void dpi_apply(const ConeDesc* cones, int ncones, const double* __restrict__ v,
+                          const double* __restrict__ P, const double* in, double* out,
+                          int trans, double* lds, double* red) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // diagonal / identity cones: elementwise; SOC: one wave per cone
+  for (int k = 0; k < ncones; ++k) {
+    const ConeDesc cd = cones[k];
+    if (cd.code == DOPT_CONE_ZEROS) {
+      for (int i = t; i < cd.dim; i += CTPB) out[cd.row + i] = in[cd.row + i];
+    } else if (cd.code == DOPT_CONE_NONNEG || cd.code == DOPT_CONE_NONPOS) {
+      const double* dg = P + cd.poff;
+      for (int i = t; i < cd.dim; i += CTPB) out[cd.row + i] = dg[i] * in[cd.row + i];
+    }
+  }
+  int soc_i = 0;
+  for (int k = 0; k < ncones; ++k) {
+    const ConeDesc cd = cones[k];
+    if (cd.code != DOPT_CONE_SOC) continue;
+    if ((soc_i++ & 3) != wv) continue;
+    const double* pr = P + cd.poff;
+    const int cs = (int)pr[0];
+    const double tt = pr[1], nx = pr[2];
+    const double* xv = v + cd.row + 1;   // x part of v
+    const double* w = in + cd.row;
+    double* o = out + cd.row;
+    if (cs == 0) {
+      for (int i = lane; i < cd.dim; i += 64) o[i] = w[i];
+    } else if (cs == 1) {
+      for (int i = lane; i < cd.dim; i += 64) o[i] = 0.0;
+    } else {
+      // Dπ = (1/(2‖x‖)) [‖x‖, xᵀ; x, (‖x‖+t)I − (t/‖x‖²) x xᵀ]  (symmetric)
+      double dotxw = 0.0;
+      for (int i = lane; i < cd.dim - 1; i += 64) dotxw = fma(xv[i], w[1 + i], dotxw);
+      dotxw = cwave_sum(dotxw);
+      const double w0 = w[0];
+      const double inv2 = 1.0 / (2.0 * nx);
+      if (lane == 0) o[0] = (nx * w0 + dotxw) * inv2;
+      for (int i = lane; i < cd.dim - 1; i += 64)
+        o[1 + i] = (xv[i] * w0 + (nx + tt) * w[1 + i] - (tt / (nx * nx)) * xv[i] * dotxw) * inv2;
+    }
+  }
+  __syncthreads();
+  // PSD cones: whole workgroup per cone
+  double* Xs = lds;                                  // d × (d+1)
+  double* Ys = lds + PSD_MAX * (PSD_MAX + 1);
+  double* Us = lds + 2 * PSD_MAX * (PSD_MAX + 1);
+  for (int k = 0; k < ncones; ++k) {
+    const ConeDesc cd = cones[k];
+    if (cd.code != DOPT_CONE_PSD_TRI) continue;
+    const int d = psd_side(cd.dim);
+    const int ld = d + 1;
+    const double* U = P + cd.poff;
+    const double* Bm = U + d * d;
+    const bool ident = U[2 * d * d] != 0.0;
+    const double* w = in + cd.row;
+    double* o = out + cd.row;
+    if (ident) {
+      for (int i = t; i < cd.dim; i += CTPB) o[i] = w[i];
+      continue;
+    }
+    // X = smat(S^{-2} w) for Dπ (=Jᵀ = S²JS⁻²), smat(w) for Dπᵀ (= J)
+    for (int e = t; e < d * d; e += CTPB) {
+      const int i = e / d, j = e % d;
+      const int a = i <= j ? i : j, c = i <= j ? j : i;
+      double val = w[tri_idx(a, c)];
+      if (!trans && a != c) val *= 0.5;
+      Xs[i * ld + j] = val;
+      Us[i * ld + j] = U[i * d + j];
+    }
+    __syncthreads();
+    // Y = Uᵀ X
+    for (int e = t; e < d * d; e += CTPB) {
+      const int i = e / d, j = e % d;
+      double acc = 0.0;
+      for (int q = 0; q < d; ++q) acc = fma(Us[q * ld + i], Xs[q * ld + j], acc);
+      Ys[i * ld + j] = acc;
+    }
+    __syncthreads();
+    // X = (Y U) ∘ B
+    for (int e = t; e < d * d; e += CTPB) {
+      const int i = e / d, j = e % d;
+      double acc = 0.0;
+      for (int q = 0; q < d; ++q) acc = fma(Ys[i * ld + q], Us[q * ld + j], acc);
+      Xs[i * ld + j] = acc * Bm[i * d + j];
+    }
+    __syncthreads();
+    // Y = U X
+    for (int e = t; e < d * d; e += CTPB) {
+      const int i = e / d, j = e % d;
+      double acc = 0.0;
+      for (int q = 0; q < d; ++q) acc = fma(Us[i * ld + q], Xs[q * ld + j], acc);
+      Ys[i * ld + j] = acc;
+    }
+    __syncthreads();
+    // out = tri(Y Uᵀ), times S² for Dπ
+    for (int e = t; e < cd.dim; e += CTPB) {
+      int j = 0;
+      while ((j + 1) * (j + 2) / 2 <= e) ++j;
+      const int i = e - j * (j + 1) / 2;
+      double acc = 0.0;
+      for (int q = 0; q < d; ++q) acc = fma(Ys[i * ld + q], Us[j * ld + q], acc);
+      o[e] = (!trans && i != j) ? 2.0 * acc : acc;
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+}
+
+// y[0:m] = A_moi · x   (A_moi col-major m×n); thread per row, coalesced
+__device__ void gemv_n(const double* __restrict__ A, int m, int n, const double* x, double* y) {
+  for (int i = threadIdx.x; i < m; i += CTPB) {
+    double acc = 0.0;
+    for (int j = 0; j < n; ++j) acc = fma(A[i + (size_t)j * m], x[j], acc);
+    y[i] = acc;
+  }
+}
+
+// g[0:n] = A_moiᵀ · w ; wave per column, lanes over rows
+__device__ void gemv_t(const double* __restrict__ A, int m, int n, const double* w, double* g) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int j = wv; j < n; j += CTPB / 64) {
+    const double* col = A + (size_t)j * m;
+    double acc = 0.0;
+    for (int i = lane; i < m; i += 64) acc = fma(col[i], w[i], acc);
+    acc = cwave_sum(acc);
+    if (lane == 0) g[j] = acc;
+  }
+}
+
+struct ConicProblem {
+  const double *A, *b, *c, *v, *P;
+  int m, n;
+};
+
+// out = M z   (z, out: N = n+m+1; scratch: Dv (m), Au (m), g (n))
+__device__ void M_apply(const ConicProblem& pr, const ConeDesc* cones, int ncones,
+                        const double* z, double* out, double* Dv, double* Au, double* g,
+                        double* lds, double* red) {
+  const int n = pr.n, m = pr.m, t = threadIdx.x;
+  dpi_apply(cones, ncones, pr.v, pr.P, z + n, Dv, 0, lds, red);
+  gemv_n(pr.A, m, n, z, Au);        // A_moi u  (= −A u)
+  gemv_t(pr.A, m, n, Dv, g);        // A_moiᵀ Dv (= −AᵀDv)
+  __syncthreads();
+  const double w = z[n + m];
+  double cu = 0.0, bd = 0.0;
+  for (int j = t; j < n; j += CTPB) {
+    out[j] = -g[j] + pr.c[j] * w;
+    cu = fma(pr.c[j], z[j], cu);
+  }
+  for (int i = t; i < m; i += CTPB) {
+    out[n + i] = Au[i] + z[n + i] - Dv[i] + pr.b[i] * w;
+    bd = fma(pr.b[i], Dv[i], bd);
+  }
+  const double s = cblock_sum(-cu - bd, red);
+  if (t == 0) out[n + m] = s;
+  __syncthreads();
+}
+
+// out = Mᵀ r
+__device__ void MT_apply(const ConicProblem& pr, const ConeDesc* cones, int ncones,
+                         const double* r, double* out, double* tmpm, double* Ap, double* g,
+                         double* lds, double* red) {
+  const int n = pr.n, m = pr.m, t = threadIdx.x;
+  gemv_n(pr.A, m, n, r, Ap);          // A_moi p  (A p = −A_moi p)
+  gemv_t(pr.A, m, n, r + n, g);       // A_moiᵀ q (−Aᵀ q = A_moiᵀ q)
+  __syncthreads();
+  const double tw = r[n + m];
+  for (int i = t; i < m; i += CTPB) tmpm[i] = -Ap[i] - r[n + i] - pr.b[i] * tw;
+  __syncthreads();
+  dpi_apply(cones, ncones, pr.v, pr.P, tmpm, out + n, 1, lds, red);
+  double cp = 0.0, bq = 0.0;
+  for (int j = t; j < n; j += CTPB) {
+    out[j] = g[j] - pr.c[j] * tw;
+    cp = fma(pr.c[j], r[j], cp);
+  }
+  for (int i = t; i < m; i += CTPB) {
+    out[n + i] += r[n + i];
+    bq = fma(pr.b[i], r[n + i], bq);
+  }
+  const double s = cblock_sum(cp + bq, red);
+  if (t == 0) out[n + m] = s;
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// LSQR (IterativeSolvers 0.9 defaults, oracle/lsqr.py) on M, one workgroup per
+// problem; vectors in a per-problem global workspace (L2-resident).
+// mode 0: forward (rhs built from tangents); mode 1: reverse.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
+    const ConeDesc* __restrict__ cones_g, int ncones, const double* __restrict__ A,
+    const double* __restrict__ b, const double* __restrict__ c,
+    const double* __restrict__ v, const double* __restrict__ P, int plen, int m, int n,
+    const double* __restrict__ rhs, double rhs_zero_tol, double* __restrict__ work,
+    double* __restrict__ xout, int32_t* __restrict__ info) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ double red[4];
+  __shared__ ConeDesc cones[128];
+  const int bidx = blockIdx.x, t = threadIdx.x;
+  const int N = n + m + 1;
+  const ConeDesc* cn = cones_g;
+  if (ncones <= 128) {
+    for (int k = t; k < ncones; k += CTPB) cones[k] = cones_g[k];
+    cn = cones;
+  }
+  ConicProblem pr;
+  pr.A = A + (size_t)bidx * m * n;
+  pr.b = b + (size_t)bidx * m;
+  pr.c = c + (size_t)bidx * n;
+  pr.v = v + (size_t)bidx * m;
+  pr.P = P + (size_t)bidx * plen;
+  pr.m = m;
+  pr.n = n;
+  const size_t wl = (size_t)5 * N + 3 * (size_t)m + n;
+  double* x = work + (size_t)bidx * wl;
+  double* u = x + N;
+  double* vv = u + N;
+  double* w = vv + N;
+  double* tmp = w + N;
+  double* s1 = tmp + N;   // m
+  double* s2 = s1 + m;    // m
+  double* s3 = s2 + m;    // m
+  double* s4 = s3 + m;    // n
+  const double* rb = rhs + (size_t)bidx * N;
+  double bb = 0.0;
+  for (int i = t; i < N; i += CTPB) {
+    const double r = rb[i];
+    u[i] = r;
+    x[i] = 0.0;
+    bb = fma(r, r, bb);
+  }
+  double beta = sqrt(cblock_sum(bb, red));
+  int it = 0, istop = 0;
+  if (beta > rhs_zero_tol) {
+    for (int i = t; i < N; i += CTPB) u[i] /= beta;
+    __syncthreads();
+    MT_apply(pr, cn, ncones, u, vv, s1, s2, s4, lds, red);
+    double aa = 0.0;
+    for (int i = t; i < N; i += CTPB) aa = fma(vv[i], vv[i], aa);
+    double alpha = sqrt(cblock_sum(aa, red));
+    if (alpha > 0.0) {
+      for (int i = t; i < N; i += CTPB) { vv[i] /= alpha; w[i] = vv[i]; }
+      __syncthreads();
+      const double eps = 2.220446049250313e-16;
+      const double atol = sqrt(eps), btol = sqrt(eps), ctol = sqrt(eps);
+      double anorm = 0.0, ddnorm = 0.0, res2 = 0.0, xxnorm = 0.0, zz = 0.0;
+      double sn2 = 0.0, cs2 = -1.0, rhobar = alpha, phibar = beta;
+      const double bnorm = beta;
+      const int maxiter = N;
+      while (it < maxiter) {
+        ++it;
+        M_apply(pr, cn, ncones, vv, tmp, s1, s2, s4, lds, red);
+        double su = 0.0;
+        for (int i = t; i < N; i += CTPB) { const double ui = tmp[i] - alpha * u[i]; u[i] = ui; su = fma(ui, ui, su); }
+        beta = sqrt(cblock_sum(su, red));
+        if (beta > 0.0) {
+          for (int i = t; i < N; i += CTPB) u[i] /= beta;
+          __syncthreads();
+          anorm = sqrt(anorm * anorm + alpha * alpha + beta * beta);
+          MT_apply(pr, cn, ncones, u, tmp, s1, s2, s4, lds, red);
+          double sv = 0.0;
+          for (int i = t; i < N; i += CTPB) { const double vi = tmp[i] - beta * vv[i]; vv[i] = vi; sv = fma(vi, vi, sv); }
+          alpha = sqrt(cblock_sum(sv, red));
+          if (alpha > 0.0) for (int i = t; i < N; i += CTPB) vv[i] /= alpha;
+          __syncthreads();
+        }
+        const double rhobar1 = rhobar;
+        const double rho = hypot(rhobar1, beta);
+        const double cs = rhobar1 / rho, sn = beta / rho;
+        const double theta = sn * alpha;
+        rhobar = -cs * alpha;
+        const double phi = cs * phibar;
+        phibar = sn * phibar;
+        const double tau = sn * phi;
+        const double t1 = phi / rho, t2 = -theta / rho;
+        double sw = 0.0;
+        for (int i = t; i < N; i += CTPB) {
+          const double wi = w[i];
+          sw = fma(wi, wi, sw);
+          x[i] = x[i] + t1 * wi;
+          w[i] = vv[i] + t2 * wi;
+        }
+        ddnorm += cblock_sum(sw, red) / (rho * rho);
+        const double delta = sn2 * rho, gambar = -cs2 * rho;
+        const double rhs_ = phi - delta * zz;
+        const double zbar = rhs_ / gambar;
+        const double xnorm = sqrt(xxnorm + zbar * zbar);
+        const double gamma = hypot(gambar, theta);
+        cs2 = gambar / gamma;
+        sn2 = theta / gamma;
+        zz = rhs_ / gamma;
+        xxnorm += zz * zz;
+        const double acond = anorm * sqrt(ddnorm);
+        const double rnorm = sqrt(phibar * phibar + res2);
+        const double arnorm = alpha * fabs(tau);
+        const double test1 = rnorm / bnorm;
+        const double test2 = (anorm * rnorm != 0.0) ? arnorm / (anorm * rnorm) : 0.0;
+        const double test3 = (acond != 0.0) ? 1.0 / acond : 0.0;
+        const double t1r = test1 / (1.0 + anorm * xnorm / bnorm);
+        const double rtol = btol + atol * anorm * xnorm / bnorm;
+        istop = 0;
+        if (it >= maxiter) istop = 7;
+        if (1.0 + test3 <= 1.0) istop = 6;
+        if (1.0 + test2 <= 1.0) istop = 5;
+        if (1.0 + t1r <= 1.0) istop = 4;
+        if (test3 <= ctol) istop = 3;
+        if (test2 <= atol) istop = 2;
+        if (test1 <= rtol) istop = 1;
+        __syncthreads();
+        if (istop) break;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < N; i += CTPB) xout[(size_t)bidx * N + i] = x[i];
+  if (t == 0 && info) {
+    info[bidx] = istop;
+    info[gridDim.x + bidx] = it;
+  }
+}
+
+// forward RHS: [dA_moiᵀ vp + dc; −dA_moi x + db; −dc·x − db·vp]  (ConicProgram.jl:314-318)
+__global__ __launch_bounds__(CTPB) void conic_fwd_rhs_kernel(
+    const double* __restrict__ dA, const double* __restrict__ db, const double* __restrict__ dc,
+    const double* __restrict__ x, const double* __restrict__ vp, int m, int n,
+    double* __restrict__ rhs) {
+  __shared__ double red[4];
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int N = n + m + 1;
+  const double* xb = x + (size_t)b * n;
+  const double* vpb = vp + (size_t)b * m;
+  double* r = rhs + (size_t)b * N;
+  const double* Ab = dA ? dA + (size_t)b * m * n : nullptr;
+  for (int j = wv; j < n; j += CTPB / 64) {
+    double acc = 0.0;
+    if (Ab)
+      for (int i = lane; i < m; i += 64) acc = fma(Ab[i + (size_t)j * m], vpb[i], acc);
+    acc = cwave_sum(acc);
+    if (lane == 0) r[j] = acc + (dc ? dc[(size_t)b * n + j] : 0.0);
+  }
+  for (int i = t; i < m; i += CTPB) {
+    double acc = 0.0;
+    if (Ab)
+      for (int j = 0; j < n; ++j) acc = fma(Ab[i + (size_t)j * m], xb[j], acc);
+    r[n + i] = -acc + (db ? db[(size_t)b * m + i] : 0.0);
+  }
+  double cu = 0.0, bv = 0.0;
+  if (dc) for (int j = t; j < n; j += CTPB) cu = fma(dc[(size_t)b * n + j], xb[j], cu);
+  if (db) for (int i = t; i < m; i += CTPB) bv = fma(db[(size_t)b * m + i], vpb[i], bv);
+  const double s = cblock_sum(cu, red);
+  const double s2 = cblock_sum(bv, red);
+  if (t == 0) r[n + m] = -s - s2;
+}
+
+// reverse RHS: [dx; 0; −xᵀdx]  (ConicProgram.jl:363-367 with dy = ds = 0)
+__global__ __launch_bounds__(CTPB) void conic_rev_rhs_kernel(
+    const double* __restrict__ dx, const double* __restrict__ x, int m, int n,
+    double* __restrict__ rhs) {
+  __shared__ double red[4];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int N = n + m + 1;
+  double* r = rhs + (size_t)b * N;
+  double acc = 0.0;
+  for (int j = t; j < n; j += CTPB) {
+    const double d = dx[(size_t)b * n + j];
+    r[j] = d;
+    acc = fma(x[(size_t)b * n + j], d, acc);
+  }
+  for (int i = t; i < m; i += CTPB) r[n + i] = 0.0;
+  const double s = cblock_sum(acc, red);
+  if (t == 0) r[n + m] = -s;
+}
+
+// outputs
+__global__ __launch_bounds__(CTPB) void conic_fwd_out_kernel(
+    const double* __restrict__ z, const double* __restrict__ x, int m, int n,
+    double* __restrict__ out_dx) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int N = n + m + 1;
+  const double* zb = z + (size_t)b * N;
+  const double dw = zb[N - 1];
+  for (int j = t; j < n; j += CTPB) out_dx[(size_t)b * n + j] = -(zb[j] - x[(size_t)b * n + j] * dw);
+}
+
+__global__ __launch_bounds__(CTPB) void conic_rev_out_kernel(
+    const double* __restrict__ g, const double* __restrict__ x, const double* __restrict__ vp,
+    int m, int n, double* __restrict__ dA, double* __restrict__ db, double* __restrict__ dc) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int N = n + m + 1;
+  const double* gb = g + (size_t)b * N;
+  const double ge = gb[N - 1];
+  const double* xb = x + (size_t)b * n;
+  const double* vpb = vp + (size_t)b * m;
+  if (dc) for (int j = t; j < n; j += CTPB) dc[(size_t)b * n + j] = gb[j] - ge * xb[j];
+  if (db) for (int i = t; i < m; i += CTPB) db[(size_t)b * m + i] = gb[n + i] - ge * vpb[i];
+  if (dA) {
+    double* Ab = dA + (size_t)b * m * n;
+    for (int j = 0; j < n; ++j)
+      for (int i = t; i < m; i += CTPB) Ab[i + (size_t)j * m] = gb[n + i] * xb[j] - vpb[i] * gb[j];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static void ccheck() { DOPT_CHECK_HIP(hipGetLastError()); }
+
+static size_t dpi_lds_bytes(const std::vector<int32_t>& cones) {
+  for (size_t k = 0; k < cones.size() / 2; ++k)
+    if (cones[2 * k] == DOPT_CONE_PSD_TRI) return (size_t)3 * PSD_MAX * (PSD_MAX + 1) * sizeof(double);
+  return 16;
+}
+
+void conic_factor(Handle& h) {
+  if (!h.cset) throw Error(-1, "dopt_conic_factor: dopt_conic_set has not been called");
+  const int B = (int)h.batch, m = h.m;
+  const int nc = (int)h.cones.size() / 2;
+  std::vector<ConeDesc> cd(nc);
+  int row = 0, poff = 0;
+  for (int k = 0; k < nc; ++k) {
+    const int code = h.cones[2 * k], dim = h.cones[2 * k + 1];
+    cd[k] = {code, dim, row, poff};
+    row += dim;
+    if (code == DOPT_CONE_NONNEG || code == DOPT_CONE_NONPOS) poff += dim;
+    else if (code == DOPT_CONE_SOC) poff += 4;
+    else if (code == DOPT_CONE_PSD_TRI) {
+      int d = 0;
+      while ((d + 1) * (d + 2) / 2 <= dim) ++d;
+      poff += 2 * d * d + 2;
+    }
+  }
+  h.dpi_len = std::max(poff, 1);
+  h.cone_dev.ensure(std::max<size_t>(nc, 1) * sizeof(ConeDesc));
+  if (nc)
+    DOPT_CHECK_HIP(hipMemcpyAsync(h.cone_dev.p, cd.data(), nc * sizeof(ConeDesc), hipMemcpyHostToDevice, h.stream));
+  h.vp.ensure((size_t)2 * B * std::max(m, 1) * sizeof(double));  // v then vp
+  h.dpi.ensure((size_t)B * h.dpi_len * sizeof(double));
+  {
+    PhaseTimer pt(h, DOPT_PHASE_CONIC_CONE);
+    if (nc && B) {
+      hipLaunchKernelGGL(conic_cone_kernel, dim3(nc, B), dim3(CTPB), 0, h.stream,
+                         h.cone_dev.as<ConeDesc>(), nc, h.cy, h.cs, m, h.dpi_len,
+                         h.vp.as<double>(), h.vp.as<double>() + (size_t)B * m, h.dpi.as<double>());
+      ccheck();
+    }
+  }
+  h.cfactored = true;
+}
+
+static void conic_lsqr(Handle& h, double tol, double* out) {
+  const int B = (int)h.batch, m = h.m, n = h.n;
+  const int nc = (int)h.cones.size() / 2;
+  const size_t N = (size_t)n + m + 1;
+  const size_t wl = 5 * N + 3 * (size_t)m + n;
+  h.cwork.ensure((size_t)B * (wl + N) * sizeof(double));
+  h.cinfo.ensure((size_t)2 * std::max(B, 1) * sizeof(int32_t));
+  double* rhs = h.cwork.as<double>() + (size_t)B * wl;
+  PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
+  hipLaunchKernelGGL(conic_lsqr_kernel, dim3(B), dim3(CTPB), dpi_lds_bytes(h.cones), h.stream,
+                     h.cone_dev.as<ConeDesc>(), nc, h.cA, h.cb, h.cc, h.vp.as<double>(),
+                     h.dpi.as<double>(), h.dpi_len, m, n, rhs, tol, h.cwork.as<double>(), out,
+                     h.cinfo.as<int32_t>());
+  ccheck();
+}
+
+void conic_forward(Handle& h, const double* dA, const double* db, const double* dc,
+                   double* out, double* out_dx) {
+  if (!h.cfactored) conic_factor(h);
+  const int B = (int)h.batch, m = h.m, n = h.n;
+  const size_t N = (size_t)n + m + 1;
+  const size_t wl = 5 * N + 3 * (size_t)m + n;
+  h.cwork.ensure((size_t)B * (wl + N) * sizeof(double));
+  double* rhs = h.cwork.as<double>() + (size_t)B * wl;
+  {
+    PhaseTimer pt(h, DOPT_PHASE_CONIC_RHS);
+    hipLaunchKernelGGL(conic_fwd_rhs_kernel, dim3(B), dim3(CTPB), 0, h.stream, dA, db, dc, h.cx,
+                       h.vp.as<double>() + (size_t)B * m, m, n, rhs);
+    ccheck();
+  }
+  conic_lsqr(h, 0.0, out);   // `norm(RHS) <= 1e-400` ≡ RHS == 0 (ConicProgram.jl:320)
+  if (out_dx) {
+    PhaseTimer pt(h, DOPT_PHASE_CONIC_OUTPUT);
+    hipLaunchKernelGGL(conic_fwd_out_kernel, dim3(B), dim3(CTPB), 0, h.stream, out, h.cx, m, n, out_dx);
+    ccheck();
+  }
+}
+
+void conic_reverse(Handle& h, const double* dx, double* out_g, double* out_dA, double* out_db,
+                   double* out_dc) {
+  if (!h.cfactored) conic_factor(h);
+  const int B = (int)h.batch, m = h.m, n = h.n;
+  const size_t N = (size_t)n + m + 1;
+  const size_t wl = 5 * N + 3 * (size_t)m + n;
+  h.cwork.ensure((size_t)B * (wl + N) * sizeof(double));
+  double* rhs = h.cwork.as<double>() + (size_t)B * wl;
+  {
+    PhaseTimer pt(h, DOPT_PHASE_CONIC_RHS);
+    hipLaunchKernelGGL(conic_rev_rhs_kernel, dim3(B), dim3(CTPB), 0, h.stream, dx, h.cx, m, n, rhs);
+    ccheck();
+  }
+  conic_lsqr(h, 1e-4, out_g);  // `norm(dz) <= 1e-4` → g = 0 (ConicProgram.jl:369-370)
+  if (out_dA || out_db || out_dc) {
+    PhaseTimer pt(h, DOPT_PHASE_CONIC_OUTPUT);
+    hipLaunchKernelGGL(conic_rev_out_kernel, dim3(B), dim3(CTPB), 0, h.stream, out_g, h.cx,
+                       h.vp.as<double>() + (size_t)B * m, m, n, out_dA, out_db, out_dc);
+    ccheck();
+  }
+}
+
 }  // namespace dopt

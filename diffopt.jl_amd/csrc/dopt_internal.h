@@ -84,6 +84,55 @@ struct Handle {
 
   // scratch for host-mode tangents / outputs
   DevBuf tin[8], tout[6];
+
+  // per-phase GPU timing (HIP events on the handle's stream)
+  bool prof = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_pending;
+  double phase_ms[DOPT_NUM_PHASES] = {0};
+  int32_t phase_cnt[DOPT_NUM_PHASES] = {0};
+
+  hipEvent_t take_event() {
+    if (!ev_pool.empty()) {
+      hipEvent_t e = ev_pool.back();
+      ev_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    DOPT_CHECK_HIP(hipEventCreate(&e));
+    return e;
+  }
+  void collect_phases() {
+    if (ev_pending.empty()) return;
+    DOPT_CHECK_HIP(hipStreamSynchronize(stream));
+    for (auto& pe : ev_pending) {
+      float ms = 0.f;
+      DOPT_CHECK_HIP(hipEventElapsedTime(&ms, pe.second.first, pe.second.second));
+      phase_ms[pe.first] += ms;
+      phase_cnt[pe.first] += 1;
+      ev_pool.push_back(pe.second.first);
+      ev_pool.push_back(pe.second.second);
+    }
+    ev_pending.clear();
+  }
+};
+
+// RAII phase bracket: records a start/stop event pair around the kernels
+// launched in its scope when profiling is enabled.
+struct PhaseTimer {
+  Handle& h;
+  int phase;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  PhaseTimer(Handle& hh, int ph) : h(hh), phase(ph) {
+    if (!h.prof) return;
+    e0 = h.take_event();
+    e1 = h.take_event();
+    DOPT_CHECK_HIP(hipEventRecord(e0, h.stream));
+  }
+  ~PhaseTimer() {
+    if (!h.prof) return;
+    if (hipEventRecord(e1, h.stream) == hipSuccess) h.ev_pending.push_back({phase, {e0, e1}});
+  }
 };
 
 // Launch helpers (defined in qp.hip / conic.hip)

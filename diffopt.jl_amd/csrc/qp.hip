@@ -840,17 +840,20 @@ void qp_factor(Handle& h) {
   static const double dummy = 0.0;
   const double* G = h.G ? h.G : &dummy;
   const double* A = h.A ? h.A : &dummy;
+  { PhaseTimer pt(h, DOPT_PHASE_QP_PREPARE);
   hipLaunchKernelGGL(qp_prepare_kernel, dim3(B), dim3(TPB), n * sizeof(double), h.stream,
                      h.Q, m ? h.G : nullptr, m ? h.hv : nullptr, h.z, m ? h.lam : nullptr,
                      n, m, p, h.s.as<double>(), h.kidx.as<int32_t>(),
                      h.kidx.as<int32_t>() + (size_t)B * m, meta);
-  check_launch();
+  check_launch(); }
   const int tiles_1d = (nmax + 31) / 32;
+  { PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
   hipLaunchKernelGGL(qp_assemble_kernel, dim3(tiles_1d * tiles_1d, B), dim3(TPB), 0, h.stream,
                      h.Q, G, A, m ? h.lam : &dummy, h.s.as<double>(), h.kidx.as<int32_t>(), meta,
                      n, m, p, nmax, ld, tiles_1d, h.K.as<double>());
-  check_launch();
+  check_launch(); }
   if (nmax > 0) {
+    PhaseTimer pt(h, DOPT_PHASE_QP_LU);
     hipLaunchKernelGGL(qp_lu_small_kernel, dim3(B), dim3(TPB), lu_small_lds(nmax), h.stream,
                        h.K.as<double>(), h.ipiv.as<int32_t>(), meta, nmax, ld);
     check_launch();
@@ -870,13 +873,16 @@ static void qp_solve_and_output(Handle& h, int trans, double* out) {
   double* rhs = h.rhs.as<double>();
   double* full = rhs + (size_t)B * nmax;
   double* x = h.x.as<double>();
+  { PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
   hipLaunchKernelGGL(qp_solve_kernel, dim3(B), dim3(TPB), (size_t)nmax * sizeof(double), h.stream,
                      h.K.as<double>(), h.ipiv.as<int32_t>(), meta, nmax, ld, trans, rhs, x);
-  check_launch();
+  check_launch(); }
+  { PhaseTimer pt(h, DOPT_PHASE_QP_LSQR);
   hipLaunchKernelGGL(qp_lsqr_kernel, dim3(B), dim3(TPB), (size_t)5 * nmax * sizeof(double), h.stream,
                      h.K.as<double>(), meta, nmax, ld, trans, rhs, x, (int32_t*)nullptr);
-  check_launch();
+  check_launch(); }
   static const double dummy = 0.0;
+  PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
   hipLaunchKernelGGL(qp_output_kernel, dim3(B), dim3(TPB), (size_t)n * sizeof(double), h.stream,
                      x, m ? h.G : &dummy, h.s.as<double>(), h.kidx.as<int32_t>() + (size_t)B * m,
                      meta, full, n, m, p, nmax, trans, out);
@@ -885,9 +891,10 @@ static void qp_solve_and_output(Handle& h, int trans, double* out) {
 
 void qp_reverse(Handle& h, const double* dl_dz, double* out) {
   if (!h.factored) qp_factor(h);
+  { PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
   hipLaunchKernelGGL(qp_rev_rhs_kernel, dim3(h.batch), dim3(TPB), 0, h.stream, dl_dz,
                      h.meta.as<QPMeta>(), h.n, h.nmax, h.rhs.as<double>());
-  check_launch();
+  check_launch(); }
   qp_solve_and_output(h, 0, out);
 }
 
@@ -898,11 +905,12 @@ void qp_forward(Handle& h, const double* dQ, const double* dq, const double* dG,
   double* rhs = h.rhs.as<double>();
   double* full = rhs + (size_t)B * h.nmax;
   static const double dummy = 0.0;
+  { PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
   hipLaunchKernelGGL(qp_fwd_rhs_kernel, dim3(B), dim3(TPB), (size_t)(2 * n + 2 * m + 2 * p) * sizeof(double),
                      h.stream, dQ, dq, m ? dG : nullptr, m ? dh : nullptr, p ? dA : nullptr,
                      p ? db : nullptr, h.z, m ? h.lam : &dummy, p ? h.nu : &dummy,
                      h.kidx.as<int32_t>() + (size_t)B * m, h.meta.as<QPMeta>(), n, m, p, h.nmax, full, rhs);
-  check_launch();
+  check_launch(); }
   qp_solve_and_output(h, 1, out);
 }
 

@@ -46,7 +46,11 @@ SIGNATURES = {
     "dopt_get_iterative": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_get_system_size": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_last_time": (ctypes.c_double, [_h]),
+    "dopt_set_profiling": (ctypes.c_int, [_h, ctypes.c_int32]),
+    "dopt_get_phase_times": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]),
+    "dopt_phase_name": (ctypes.c_char_p, [ctypes.c_int32]),
 }
+NUM_PHASES = 11
 
 
 class EngineUnavailable(RuntimeError):
@@ -94,6 +98,15 @@ def load():
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def phase_times(lib, handle):
+    import numpy as np
+    ms = np.zeros(NUM_PHASES, dtype=np.float64)
+    cnt = np.zeros(NUM_PHASES, dtype=np.int32)
+    check(lib.dopt_get_phase_times(handle, ms.ctypes.data, cnt.ctypes.data, NUM_PHASES), handle)
+    return {lib.dopt_phase_name(i).decode(): (float(ms[i]), int(cnt[i]))
+            for i in range(NUM_PHASES) if cnt[i]}
 
 
 def check(rc, handle=None, singular_ok=False):

@@ -146,6 +146,14 @@ class QPBatch:
     def last_time(self):
         return self.lib.dopt_last_time(self.h)
 
+    def set_profiling(self, on=True):
+        _lib.check(self.lib.dopt_set_profiling(self.h, int(bool(on))), self.h)
+
+    def phase_times(self):
+        """{phase name: (total ms, launches)} since the last call (HIP events
+        on the handle's stream)."""
+        return _lib.phase_times(self.lib, self.h)
+
     def split(self, out):
         n, m = self.n, self.m
         return out[:, :n], out[:, n:n + m], out[:, n + m:]

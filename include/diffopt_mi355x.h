@@ -147,6 +147,26 @@ int dopt_get_iterative(dopt_handle* h, int8_t* flags);
 /* per-problem size of the factorised (reduced) KKT system (QP) or LSQR
  * iteration count of the last solve (CONIC). */
 int dopt_get_system_size(dopt_handle* h, int32_t* sizes);
+/* Per-phase GPU time, measured with HIP events on the handle's stream around
+ * each phase's kernels while profiling is on (off by default). */
+#define DOPT_PHASE_QP_PREPARE 0   /* branch flag, s = Gz − h, row elimination   */
+#define DOPT_PHASE_QP_ASSEMBLE 1  /* KKT matrix assembly                         */
+#define DOPT_PHASE_QP_LU 2        /* blocked LU (MFMA trailing update)           */
+#define DOPT_PHASE_QP_RHS 3       /* forward/reverse right-hand sides            */
+#define DOPT_PHASE_QP_SOLVE 4     /* triangular solves                           */
+#define DOPT_PHASE_QP_LSQR 5      /* LSQR (norm(Q) == 0 branch)                  */
+#define DOPT_PHASE_QP_OUTPUT 6    /* output recovery / scatter                   */
+#define DOPT_PHASE_CONIC_CONE 7   /* π(v), Dπ(v) per cone                        */
+#define DOPT_PHASE_CONIC_RHS 8    /* conic right-hand sides                      */
+#define DOPT_PHASE_CONIC_LSQR 9   /* conic LSQR on M                             */
+#define DOPT_PHASE_CONIC_OUTPUT 10
+#define DOPT_NUM_PHASES 11
+int dopt_set_profiling(dopt_handle* h, int32_t on);
+/* Accumulated milliseconds and launch counts per phase since the last call
+ * (arrays of length nphases ≤ DOPT_NUM_PHASES); resets the accumulators. */
+int dopt_get_phase_times(dopt_handle* h, double* ms, int32_t* counts,
+                         int32_t nphases);
+const char* dopt_phase_name(int32_t phase);
 /* wall time (s) of the last forward/reverse call, incl. any factorisation it
  * triggered — the DifferentiateTimeSec analogue (diff_opt.jl:256-266). */
 double dopt_last_time(const dopt_handle* h);
