@@ -1,6 +1,7 @@
 // C-ABI entry points (include/diffopt_mi355x.h).  Every function catches the
 // engine's exceptions and maps them onto the header's return-code contract.
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 #include "dopt_internal.h"
@@ -93,9 +94,17 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
   int rc = guarded(h, [&]() {
     DOPT_CHECK_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     h->own_stream = true;
+    if (const char* e = getenv("DOPT_STAMPS")) {
+      if (e[0] == '1') {
+        h->stamps.ensure(8 * sizeof(unsigned long long));
+        DOPT_CHECK_HIP(hipMemset(h->stamps.p, 0, 8 * sizeof(unsigned long long)));
+      }
+    }
     if (kind == DOPT_KIND_QP) {
-      h->nmax = n + m + p;
-      h->ld = (int32_t)dopt::round_up(std::max(h->nmax, 1), 8);
+      // Systems are identity-padded to whole 32-column LU panels (qp_fast.hip),
+      // so the per-problem stride / row stride are rounded up to 32.
+      h->nmax = (int32_t)dopt::round_up(std::max(n + m + p, 1), 32);
+      h->ld = h->nmax;
       h->K.ensure((size_t)batch * h->nmax * h->ld * sizeof(double));
       h->ipiv.ensure((size_t)batch * std::max(h->nmax, 1) * sizeof(int32_t));
       h->s.ensure((size_t)batch * std::max(m, 1) * sizeof(double));
@@ -118,7 +127,7 @@ int dopt_destroy(dopt_handle* h) {
   if (!h) return 0;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  DevBuf* bufs[] = {&h->K, &h->ipiv, &h->s, &h->kidx, &h->meta, &h->rhs, &h->x, &h->cone_dev,
+  DevBuf* bufs[] = {&h->dinv, &h->stamps, &h->ws, &h->K, &h->ipiv, &h->s, &h->kidx, &h->meta, &h->rhs, &h->x, &h->cone_dev,
                     &h->vp, &h->dpi, &h->M, &h->cwork, &h->cinfo};
   for (auto* b : bufs) b->release();
   for (auto& b : h->own_in) b.release();
@@ -304,6 +313,18 @@ int dopt_get_system_size(dopt_handle* h, int32_t* sizes) {
 
 double dopt_last_time(const dopt_handle* h) { return h ? h->last_time : -1.0; }
 
+int dopt_debug_stamps(dopt_handle* h, int64_t* out, int32_t n) {
+  return guarded(h, [&]() {
+    if (!h->stamps.p) return 0;
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    unsigned long long buf[8] = {0};
+    DOPT_CHECK_HIP(hipMemcpy(buf, h->stamps.p, sizeof(buf), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n && i < 8; ++i) out[i] = (int64_t)buf[i];
+    DOPT_CHECK_HIP(hipMemset(h->stamps.p, 0, sizeof(buf)));
+    return 8;
+  });
+}
+
 int dopt_set_profiling(dopt_handle* h, int32_t on) {
   return guarded(h, [&]() {
     h->collect_phases();
@@ -331,7 +352,7 @@ int dopt_get_phase_times(dopt_handle* h, double* ms, int32_t* counts, int32_t np
 const char* dopt_phase_name(int32_t phase) {
   static const char* names[DOPT_NUM_PHASES] = {
       "qp_prepare", "qp_assemble", "qp_lu", "qp_rhs", "qp_solve", "qp_lsqr", "qp_output",
-      "conic_cone", "conic_rhs", "conic_lsqr", "conic_output"};
+      "conic_cone", "conic_rhs", "conic_lsqr", "conic_output", "qp_fused"};
   return (phase >= 0 && phase < DOPT_NUM_PHASES) ? names[phase] : "unknown";
 }
 

@@ -221,7 +221,7 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
 //   trans = 0: out = Dπ in ;  trans = 1: out = Dπᵀ in.   in/out: m vectors.
 // PSD scratch in LDS (`lds`, ≥ 3·PSD_MAX·(PSD_MAX+1) doubles).
 // ---------------------------------------------------------------------------
-__device__ void dpi_apply(const ConeDesc* cones, int ncones, const double* __restrict__ v,
+__device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, const double* __restrict__ v,
                           const double* __restrict__ P, const double* in, double* out,
                           int trans, double* lds, double* red) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -330,7 +330,7 @@ __device__ void dpi_apply(const ConeDesc* cones, int ncones, const double* __res
 }
 
 // y[0:m] = A_moi · x   (A_moi col-major m×n); thread per row, coalesced
-__device__ void gemv_n(const double* __restrict__ A, int m, int n, const double* x, double* y) {
+__device__ __forceinline__ void gemv_n(const double* __restrict__ A, int m, int n, const double* x, double* y) {
   for (int i = threadIdx.x; i < m; i += CTPB) {
     double acc = 0.0;
     for (int j = 0; j < n; ++j) acc = fma(A[i + (size_t)j * m], x[j], acc);
@@ -339,7 +339,7 @@ __device__ void gemv_n(const double* __restrict__ A, int m, int n, const double*
 }
 
 // g[0:n] = A_moiᵀ · w ; wave per column, lanes over rows
-__device__ void gemv_t(const double* __restrict__ A, int m, int n, const double* w, double* g) {
+__device__ __forceinline__ void gemv_t(const double* __restrict__ A, int m, int n, const double* w, double* g) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int j = wv; j < n; j += CTPB / 64) {
     const double* col = A + (size_t)j * m;
@@ -356,7 +356,7 @@ struct ConicProblem {
 };
 
 // out = M z   (z, out: N = n+m+1; scratch: Dv (m), Au (m), g (n))
-__device__ void M_apply(const ConicProblem& pr, const ConeDesc* cones, int ncones,
+__device__ __forceinline__ void M_apply(const ConicProblem& pr, const ConeDesc* cones, int ncones,
                         const double* z, double* out, double* Dv, double* Au, double* g,
                         double* lds, double* red) {
   const int n = pr.n, m = pr.m, t = threadIdx.x;
@@ -380,7 +380,7 @@ __device__ void M_apply(const ConicProblem& pr, const ConeDesc* cones, int ncone
 }
 
 // out = Mᵀ r
-__device__ void MT_apply(const ConicProblem& pr, const ConeDesc* cones, int ncones,
+__device__ __forceinline__ void MT_apply(const ConicProblem& pr, const ConeDesc* cones, int ncones,
                          const double* r, double* out, double* tmpm, double* Ap, double* g,
                          double* lds, double* red) {
   const int n = pr.n, m = pr.m, t = threadIdx.x;

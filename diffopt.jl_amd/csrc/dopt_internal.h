@@ -54,6 +54,19 @@ struct QPMeta {
   int32_t info;      // 0 ok, k>0 zero pivot at column k
 };
 
+// Workgroup size of the fast QP kernels (qp_fast.hip); the launch sites in
+// qp.hip must use exactly this (the kernels' thread mappings assume it).
+constexpr int FAST_THREADS = 512;
+
+// QP problem inputs / forward tangents as seen by the kernels (device pointers)
+struct QPIn {
+  const double *Q, *G, *h, *A, *z, *lam, *nu;
+  int n, m, p;
+};
+struct FwdTangents {
+  const double *dQ, *dq, *dG, *dh, *dA, *db;
+};
+
 struct Handle {
   int device = 0;
   int64_t batch = 0;
@@ -70,6 +83,10 @@ struct Handle {
   DevBuf own_in[7];          // host-mode copies of the 7 QP inputs
   int32_t nmax = 0, ld = 0;  // max system size, K row stride (doubles)
   DevBuf K, ipiv, s, kidx, meta, rhs, x;
+  DevBuf ws;                 // per-workgroup KKT workspace of the fused kernel
+  DevBuf dinv;               // per-problem diagonal-block inverses (split path)
+  DevBuf stamps;             // diagnostic in-kernel cycle stamps (env DOPT_STAMPS=1)
+  int32_t wg_per_cu = 2;     // persistent-grid occupancy of the fast kernels
   bool set = false, factored = false;
 
   // ---- CONIC ----

@@ -6,8 +6,12 @@
 //   create_LHS_matrix :256-282   reverse_differentiate! :316-351
 //   forward_differentiate! :357-446   solve_system :486-496
 //
+// This file: the fallback kernels (generic LU for reduced systems > 512,
+// lazy-swap solves, dense LSQR for the iterative branch, their RHS/outputs)
+// and the host-side orchestration.  The fast path lives in qp_fast.hip.
+//
 // Layout in HBM (per problem b, fixed stride so every problem is independent):
-//   K     : nmax × ld doubles, ROW-major (row swaps are contiguous), ld % 8 == 0
+//   K     : nmax × ld doubles, ROW-major (row swaps are contiguous), ld = nmax = round_up(n+m+p, 32)
 //   ipiv  : nmax int32 (absolute row index chosen for each column)
 //   s     : m doubles  (G z − h, Julia sparse-matvec summation order)
 //   kidx  : m int32 (kept inequality rows, ascending)  rpos: m int32 (row → kk | -1)
@@ -20,7 +24,6 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int TPB = 256;   // threads per workgroup (4 waves)
 constexpr int NB = 32;     // LU panel width
-constexpr int CW = 64;     // trailing-update column chunk
 constexpr int SMALL_LU_MAX = 512;  // max system size for the LDS-panel LU
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -41,327 +44,11 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 }
 
 // ---------------------------------------------------------------------------
-// 1. prepare: iterative flag, s = Gz − h, row classification + compaction.
-// One workgroup per problem.
+// 3. generic fallback LU (reduced systems larger than the fast path's 512):
+// unblocked right-looking on global memory, panel width 1, trailing-only
+// ("lazy") row swaps: K = P₁⁻¹M₁P₂⁻¹M₂…U, undone by qp_solve_kernel.
+// Problem data was assembled into the per-problem K buffer by qp_fast.hip.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(TPB) void qp_prepare_kernel(
-    const double* __restrict__ Q, const double* __restrict__ G,
-    const double* __restrict__ hv, const double* __restrict__ z,
-    const double* __restrict__ lam, int n, int m, int p,
-    double* __restrict__ s_out, int32_t* __restrict__ kidx_out,
-    int32_t* __restrict__ rpos_out, QPMeta* __restrict__ meta) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int wave_cnt[4];
-  __shared__ int base;
-  const int b = blockIdx.x, t = threadIdx.x;
-  const double* Qb = Q + (size_t)b * n * n;
-  // `iterative = norm(Q) ≈ 0` (QuadraticProgram.jl:333): ≈ 0 is == 0; NaN → false
-  int nz = 0;
-  for (size_t i = t; i < (size_t)n * n; i += TPB) nz |= (Qb[i] != 0.0);
-  const int iterative = !__syncthreads_or(nz);
-  double* zs = smem;
-  for (int j = t; j < n; j += TPB) zs[j] = z[(size_t)b * n + j];
-  if (t == 0) base = 0;
-  __syncthreads();
-  const double* Gb = G + (size_t)b * m * n;
-  const int lane = t & 63, wv = t >> 6;
-  for (int i0 = 0; i0 < m; i0 += TPB) {
-    const int i = i0 + t;
-    int keep = 0;
-    if (i < m) {
-      // `G * z - h` as Julia's SparseMatrixCSC mul!: column-ordered, unfused.
-      double acc = 0.0;
-      for (int j = 0; j < n; ++j) acc = __dadd_rn(acc, __dmul_rn(Gb[i + (size_t)j * m], zs[j]));
-      const double si = __dsub_rn(acc, hv[(size_t)b * m + i]);
-      s_out[(size_t)b * m + i] = si;
-      const double li = lam[(size_t)b * m + i];
-      // exact elimination: λ_i == 0 and s_i != 0 decouples dλ_i
-      keep = iterative ? 1 : !(li == 0.0 && si != 0.0);
-    }
-    const unsigned long long ball = __ballot(keep);
-    const int prefix = __popcll(ball & ((1ull << lane) - 1ull));
-    if (lane == 0) wave_cnt[wv] = __popcll(ball);
-    __syncthreads();
-    int off = base;
-    for (int w = 0; w < wv; ++w) off += wave_cnt[w];
-    if (i < m) {
-      if (keep) kidx_out[(size_t)b * m + off + prefix] = i;
-      rpos_out[(size_t)b * m + i] = keep ? off + prefix : -1;
-    }
-    __syncthreads();
-    if (t == 0) base += wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
-    __syncthreads();
-  }
-  if (t == 0) {
-    meta[b].nk = base;
-    meta[b].nsys = n + base + p;
-    meta[b].iterative = iterative;
-    meta[b].info = 0;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// 2. assemble the (reduced) KKT matrix, row-major, 32×32 tiles through LDS so
-// both the column-major sources and the row-major destination are coalesced.
-//   K = [Q, G_kᵀD(λ_k), Aᵀ; G_k, D(s_k), 0; A, 0, 0]   (QuadraticProgram.jl:276-280)
-// ---------------------------------------------------------------------------
-struct KKTSrc {
-  const double *Q, *G, *A, *lam, *s;
-  const int32_t* kidx;
-  int n, m, p, nk;
-};
-
-__device__ __forceinline__ double kkt_elem(const KKTSrc& S, int r, int c) {
-  const int n = S.n, nk = S.nk;
-  if (r < n) {
-    if (c < n) return S.Q[r + (size_t)c * n];
-    if (c < n + nk) {
-      const int i = S.kidx[c - n];
-      return S.G[i + (size_t)r * S.m] * S.lam[i];
-    }
-    return S.A[(c - n - nk) + (size_t)r * S.p];
-  }
-  if (r < n + nk) {
-    const int i = S.kidx[r - n];
-    if (c < n) return S.G[i + (size_t)c * S.m];
-    return (c == r) ? S.s[i] : 0.0;
-  }
-  if (c < n) return S.A[(r - n - nk) + (size_t)c * S.p];
-  return 0.0;
-}
-
-__global__ __launch_bounds__(TPB) void qp_assemble_kernel(
-    const double* __restrict__ Q, const double* __restrict__ G,
-    const double* __restrict__ A, const double* __restrict__ lam,
-    const double* __restrict__ s, const int32_t* __restrict__ kidx,
-    const QPMeta* __restrict__ meta, int n, int m, int p, int nmax, int ld,
-    int tiles_1d, double* __restrict__ K) {
-  __shared__ double tile[32][33];
-  const int b = blockIdx.y;
-  const int tr = blockIdx.x / tiles_1d, tc = blockIdx.x % tiles_1d;
-  const int N = meta[b].nsys;
-  const int r0 = tr * 32, c0 = tc * 32;
-  if (r0 >= N || c0 >= N) return;
-  KKTSrc S;
-  S.Q = Q + (size_t)b * n * n;
-  S.G = G + (size_t)b * m * n;
-  S.A = A + (size_t)b * p * n;
-  S.lam = lam + (size_t)b * m;
-  S.s = s + (size_t)b * m;
-  S.kidx = kidx + (size_t)b * m;
-  S.n = n; S.m = m; S.p = p; S.nk = meta[b].nk;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  // columns < n: sources are contiguous along the row index
-  for (int cc = ty; cc < 32; cc += 8) {
-    const int r = r0 + tx, c = c0 + cc;
-    if (c < n && r < N && c < N) tile[cc][tx] = kkt_elem(S, r, c);
-  }
-  // columns >= n: sources are contiguous along the column index
-  for (int rr = ty; rr < 32; rr += 8) {
-    const int r = r0 + rr, c = c0 + tx;
-    if (c >= n && r < N && c < N) tile[tx][rr] = kkt_elem(S, r, c);
-  }
-  __syncthreads();
-  double* Kb = K + (size_t)b * nmax * ld;
-  for (int rr = ty; rr < 32; rr += 8) {
-    const int r = r0 + rr, c = c0 + tx;
-    if (r < N && c < N) Kb[(size_t)r * ld + c] = tile[tx][rr];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// 3. blocked right-looking LU with partial pivoting, one workgroup per problem.
-// Panel (N−c0)×32 factorised in LDS; L11⁻¹ formed in LDS; U12 = L11⁻¹A12 and
-// A22 −= L21·U12 on v_mfma_f64_16x16x4f64 in 64-column chunks.  Row swaps are
-// applied to trailing columns only ("lazy" left part): the solves interleave
-// the swaps per panel, K = P₁⁻¹M₁P₂⁻¹M₂…U.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
-  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
-
-__global__ __launch_bounds__(TPB) void qp_lu_small_kernel(
-    double* __restrict__ K, int32_t* __restrict__ ipiv, QPMeta* __restrict__ meta,
-    int nmax, int ld) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int b = blockIdx.x, t = threadIdx.x;
-  const int lane = t & 63, wv = t >> 6;
-  if (meta[b].iterative) return;
-  const int N = meta[b].nsys;
-  if (N > SMALL_LU_MAX) return;  // handled by the generic kernel
-  double* Kb = K + (size_t)b * nmax * ld;
-  int32_t* piv = ipiv + (size_t)b * nmax;
-  const int Np = (N + 15) & ~15;
-  constexpr int PS = NB + 1;       // panel row stride (odd: conflict-free columns)
-  double* P = smem;                // Np × PS
-  double* UC = P + Np * PS;        // NB × CW
-  double* Li = UC + NB * CW;       // NB × NB  (L11⁻¹, row-major)
-  double* redv = Li + NB * NB;     // 4
-  int* redi = reinterpret_cast<int*>(redv + 4);  // 4 + pivots(NB)
-  int* pvs = redi + 4;
-  int info = 0;
-
-  for (int c0 = 0; c0 < N; c0 += NB) {
-    const int w = min(NB, N - c0);
-    const int R = N - c0;
-    const int Rp = (R + 15) & ~15;
-    // ---- load panel
-    {
-      const int cx = t & 31, ry = t >> 5;
-      for (int r = ry; r < Rp; r += 8)
-        P[r * PS + cx] = (r < R && cx < w) ? Kb[(size_t)(c0 + r) * ld + c0 + cx] : 0.0;
-    }
-    __syncthreads();
-    // ---- unblocked LU of the panel
-    for (int j = 0; j < w; ++j) {
-      double best = -1.0;
-      int bi = 0x7fffffff;
-      for (int r = j + t; r < R; r += TPB) {
-        const double v = fabs(P[r * PS + j]);
-        if (v > best) { best = v; bi = r; }
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const double ov = __shfl_xor(best, o);
-        const int oi = __shfl_xor(bi, o);
-        if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
-      }
-      if (lane == 0) { redv[wv] = best; redi[wv] = bi; }
-      __syncthreads();
-      double pb = redv[0];
-      int pi = redi[0];
-      for (int k = 1; k < 4; ++k) {
-        if (redv[k] > pb || (redv[k] == pb && redi[k] < pi)) { pb = redv[k]; pi = redi[k]; }
-      }
-      if (pi == 0x7fffffff) pi = j;
-      if (pi != j && t < NB) {
-        const double a = P[j * PS + t], c = P[pi * PS + t];
-        P[j * PS + t] = c;
-        P[pi * PS + t] = a;
-      }
-      if (t == 0) pvs[j] = c0 + pi;
-      __syncthreads();
-      const double pv = P[j * PS + j];
-      if (pv == 0.0) {
-        if (info == 0) info = c0 + j + 1;
-      } else {
-        for (int r = j + 1 + t; r < R; r += TPB) {
-          const double l = P[r * PS + j] / pv;
-          P[r * PS + j] = l;
-          for (int c = j + 1; c < w; ++c) P[r * PS + c] = fma(-l, P[j * PS + c], P[r * PS + c]);
-        }
-      }
-      __syncthreads();
-    }
-    // ---- write panel back, save pivots
-    {
-      const int cx = t & 31, ry = t >> 5;
-      for (int r = ry; r < R; r += 8)
-        if (cx < w) Kb[(size_t)(c0 + r) * ld + c0 + cx] = P[r * PS + cx];
-      if (t < w) piv[c0 + t] = pvs[t];
-    }
-    if (c0 + w >= N) break;
-    // ---- L11⁻¹ (unit lower) into Li, one column per thread
-    if (t < NB) {
-      const int c = t;
-      for (int j = 0; j < NB; ++j) Li[j * NB + c] = 0.0;
-      if (c < w) {
-        Li[c * NB + c] = 1.0;
-        for (int j = c + 1; j < w; ++j) {
-          double acc = 0.0;
-          for (int i = c; i < j; ++i) acc = fma(P[j * PS + i], Li[i * NB + c], acc);
-          Li[j * NB + c] = -acc;
-        }
-      }
-    }
-    // ---- apply the panel's row swaps to trailing columns
-    for (int col = c0 + w + t; col < N; col += TPB) {
-      for (int j = 0; j < w; ++j) {
-        const int pr = pvs[j];
-        if (pr != c0 + j) {
-          const double a = Kb[(size_t)(c0 + j) * ld + col];
-          Kb[(size_t)(c0 + j) * ld + col] = Kb[(size_t)pr * ld + col];
-          Kb[(size_t)pr * ld + col] = a;
-        }
-      }
-    }
-    __syncthreads();
-    // ---- trailing update in column chunks
-    for (int cc0 = c0 + w; cc0 < N; cc0 += CW) {
-      const int cw = min(CW, N - cc0);
-      // A12 chunk → registers, U12 = Li · A12 via MFMA (wave wv: column tile wv)
-      {
-        // stage A12 into UC
-        const int cx = t & 63, ry = t >> 6;
-        for (int r = ry; r < NB; r += 4)
-          UC[r * CW + cx] = (r < w && cx < cw) ? Kb[(size_t)(c0 + r) * ld + cc0 + cx] : 0.0;
-      }
-      __syncthreads();
-      {
-        // wave wv computes U12[:, 16wv:16wv+16] (two 16-row tiles)
-        d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
-        const int col = wv * 16 + (lane & 15);
-#pragma unroll
-        for (int k = 0; k < NB / 4; ++k) {
-          const int kk = k * 4 + (lane >> 4);
-          const double bv = UC[kk * CW + col];
-          acc0 = mfma4(Li[(lane & 15) * NB + kk], bv, acc0);
-          acc1 = mfma4(Li[(16 + (lane & 15)) * NB + kk], bv, acc1);
-        }
-        __syncthreads();  // everyone finished reading UC
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row0 = (lane >> 4) + 4 * r;
-          UC[row0 * CW + col] = acc0[r];
-          UC[(16 + row0) * CW + col] = acc1[r];
-        }
-      }
-      __syncthreads();
-      // write U12 rows back to K
-      {
-        const int cx = t & 63, ry = t >> 6;
-        for (int r = ry; r < w; r += 4)
-          if (cx < cw) Kb[(size_t)(c0 + r) * ld + cc0 + cx] = UC[r * CW + cx];
-      }
-      // A22 −= L21 · U12: row tiles of 16 over the waves, 4 column tiles each
-      const int nrt = (R - w + 15) >> 4;
-      for (int rt = wv; rt < nrt; rt += 4) {
-        const int rbase = w + rt * 16;   // panel-relative row
-        d4 acc[4];
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int prow = rbase + (lane >> 4) + 4 * r;
-            const int gcol = cc0 + ct * 16 + (lane & 15);
-            acc[ct][r] = (prow < R && gcol < N) ? Kb[(size_t)(c0 + prow) * ld + gcol] : 0.0;
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < NB / 4; ++k) {
-          const int kk = k * 4 + (lane >> 4);
-          const double a = -P[(rbase + (lane & 15)) * PS + kk];
-#pragma unroll
-          for (int ct = 0; ct < 4; ++ct) acc[ct] = mfma4(a, UC[kk * CW + ct * 16 + (lane & 15)], acc[ct]);
-        }
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int prow = rbase + (lane >> 4) + 4 * r;
-            const int gcol = cc0 + ct * 16 + (lane & 15);
-            if (prow < R && gcol < N) Kb[(size_t)(c0 + prow) * ld + gcol] = acc[ct][r];
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  if (t == 0) meta[b].info = info;
-}
-
-// Generic fallback LU (any N): unblocked right-looking on global memory,
-// one workgroup per problem.  Used for systems larger than SMALL_LU_MAX.
 __global__ __launch_bounds__(TPB) void qp_lu_generic_kernel(
     double* __restrict__ K, int32_t* __restrict__ ipiv, QPMeta* __restrict__ meta,
     int nmax, int ld) {
@@ -439,8 +126,8 @@ __global__ __launch_bounds__(TPB) void qp_solve_kernel(
   const int lane = t & 63, wv = t >> 6;
   if (meta[b].iterative) return;
   const int N = meta[b].nsys;
-  // panel width used by the factorisation of this problem
-  const int nb = (N <= SMALL_LU_MAX) ? NB : 1;
+  if (N <= SMALL_LU_MAX) return;   // fast path (qp_fast.hip) owns these
+  const int nb = 1;                // generic LU: panel width 1, lazy swaps
   const double* Kb = K + (size_t)b * nmax * ld;
   const int32_t* piv = ipiv + (size_t)b * nmax;
   double* y = smem;
@@ -561,7 +248,7 @@ __global__ __launch_bounds__(TPB) void qp_solve_kernel(
 // IterativeSolvers.lsqr(LHS or LHSᵀ, RHS) on the FULL (unreduced) KKT matrix,
 // restating oracle/lsqr.py operation for operation.  One workgroup/problem.
 // ---------------------------------------------------------------------------
-__device__ void dense_matvec(const double* __restrict__ Kb, int ld, int N, int trans,
+__device__ __forceinline__ void dense_matvec(const double* __restrict__ Kb, int ld, int N, int trans,
                              const double* __restrict__ v, double* __restrict__ out) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   if (!trans) {
@@ -700,6 +387,7 @@ __global__ __launch_bounds__(TPB) void qp_rev_rhs_kernel(
     int nmax, double* __restrict__ rhs) {
   const int b = blockIdx.x, t = threadIdx.x;
   const int N = meta[b].nsys;
+  if (!meta[b].iterative && N <= SMALL_LU_MAX) return;
   for (int i = t; i < N; i += TPB) rhs[(size_t)b * nmax + i] = (i < n) ? dl_dz[(size_t)b * n + i] : 0.0;
 }
 
@@ -716,6 +404,7 @@ __global__ __launch_bounds__(TPB) void qp_fwd_rhs_kernel(
     double* __restrict__ full, double* __restrict__ rhs) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (!meta[b].iterative && meta[b].nsys <= SMALL_LU_MAX) return;
   double* zs = smem;            // n
   double* ls = zs + n;          // m
   double* ns = ls + m;          // p
@@ -798,6 +487,7 @@ __global__ __launch_bounds__(TPB) void qp_output_kernel(
     int m, int p, int nmax, int trans, double* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x, t = threadIdx.x;
+  if (!meta[b].iterative && meta[b].nsys <= SMALL_LU_MAX) return;
   const int nk = meta[b].nk;
   const double* xb = x + (size_t)b * nmax;
   double* ob = out + (size_t)b * (n + m + p);
@@ -827,100 +517,190 @@ __global__ __launch_bounds__(TPB) void qp_output_kernel(
 // ---------------------------------------------------------------------------
 static void check_launch() { DOPT_CHECK_HIP(hipGetLastError()); }
 
-static size_t lu_small_lds(int nmax) {
-  const int Np = ((std::min(nmax, SMALL_LU_MAX) + 15) / 16) * 16;
-  return ((size_t)Np * (NB + 1) + NB * CW + NB * NB + 4) * sizeof(double) + (4 + NB) * sizeof(int);
+// fast path (qp_fast.hip)
+__global__ void qp_fused_kernel(QPIn, FwdTangents, const double*, int, double*, size_t, double*, int,
+                                int, double*, int32_t*, int32_t*, QPMeta*, double*, double*,
+                                double*, int, int, unsigned long long*);
+__global__ void qp_factor_fast_kernel(QPIn, int, double*, int, int, double*, int32_t*, int32_t*,
+                                      int32_t*, double*, QPMeta*);
+__global__ void qp_solve_fast_kernel(QPIn, FwdTangents, const double*, int, const double*, int, int,
+                                     const double*, const int32_t*, const int32_t*, const double*,
+                                     const QPMeta*, double*, int, double*);
+size_t fast_dyn_lds(int n);
+size_t fast_ws_stride();
+size_t fast_dinv_stride(int nmax);
+
+static double* dinv_of(Handle& h) {
+  h.dinv.ensure((size_t)h.batch * fast_dinv_stride(h.nmax) * sizeof(double));
+  return h.dinv.as<double>();
 }
+
+static QPIn qp_inputs(Handle& h) {
+  static const double dummy = 0.0;
+  QPIn P;
+  P.Q = h.Q;
+  P.G = h.m ? h.G : &dummy;
+  P.h = h.m ? h.hv : &dummy;
+  P.A = h.p ? h.A : &dummy;
+  P.z = h.z;
+  P.lam = h.m ? h.lam : &dummy;
+  P.nu = h.p ? h.nu : &dummy;
+  P.n = h.n;
+  P.m = h.m;
+  P.p = h.p;
+  return P;
+}
+
+static int fast_grid(Handle& h) {
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h.device);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(h.batch, (int64_t)cus * h.wg_per_cu));
+}
+
+static int32_t* rpos_of(Handle& h) { return h.kidx.as<int32_t>() + (size_t)h.batch * h.m; }
+static int32_t* perm_of(Handle& h) { return h.ipiv.as<int32_t>(); }
 
 void qp_factor(Handle& h) {
   if (!h.set) throw Error(-1, "dopt_qp_factor: dopt_qp_set has not been called");
-  const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
-  const int nmax = h.nmax, ld = h.ld;
+  const int B = (int)h.batch;
   QPMeta* meta = h.meta.as<QPMeta>();
-  static const double dummy = 0.0;
-  const double* G = h.G ? h.G : &dummy;
-  const double* A = h.A ? h.A : &dummy;
-  { PhaseTimer pt(h, DOPT_PHASE_QP_PREPARE);
-  hipLaunchKernelGGL(qp_prepare_kernel, dim3(B), dim3(TPB), n * sizeof(double), h.stream,
-                     h.Q, m ? h.G : nullptr, m ? h.hv : nullptr, h.z, m ? h.lam : nullptr,
-                     n, m, p, h.s.as<double>(), h.kidx.as<int32_t>(),
-                     h.kidx.as<int32_t>() + (size_t)B * m, meta);
-  check_launch(); }
-  const int tiles_1d = (nmax + 31) / 32;
-  { PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
-  hipLaunchKernelGGL(qp_assemble_kernel, dim3(tiles_1d * tiles_1d, B), dim3(TPB), 0, h.stream,
-                     h.Q, G, A, m ? h.lam : &dummy, h.s.as<double>(), h.kidx.as<int32_t>(), meta,
-                     n, m, p, nmax, ld, tiles_1d, h.K.as<double>());
-  check_launch(); }
-  if (nmax > 0) {
+  {
     PhaseTimer pt(h, DOPT_PHASE_QP_LU);
-    hipLaunchKernelGGL(qp_lu_small_kernel, dim3(B), dim3(TPB), lu_small_lds(nmax), h.stream,
-                       h.K.as<double>(), h.ipiv.as<int32_t>(), meta, nmax, ld);
+    hipLaunchKernelGGL(qp_factor_fast_kernel, dim3(fast_grid(h)), dim3(FAST_THREADS), fast_dyn_lds(h.n), h.stream,
+                       qp_inputs(h), B, h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(),
+                       h.kidx.as<int32_t>(), rpos_of(h), perm_of(h), dinv_of(h), meta);
     check_launch();
-    if (nmax > SMALL_LU_MAX) {
-      hipLaunchKernelGGL(qp_lu_generic_kernel, dim3(B), dim3(TPB), 0, h.stream,
-                         h.K.as<double>(), h.ipiv.as<int32_t>(), meta, nmax, ld);
+    if (h.nmax > SMALL_LU_MAX) {
+      hipLaunchKernelGGL(qp_lu_generic_kernel, dim3(B), dim3(TPB), 0, h.stream, h.K.as<double>(),
+                         h.ipiv.as<int32_t>(), meta, h.nmax, h.ld);
       check_launch();
     }
   }
   h.factored = true;
 }
 
-static void qp_solve_and_output(Handle& h, int trans, double* out) {
+// fallback problems (iterative branch, or reduced size > FAST_MAX)
+static void fallback_solve_and_output(Handle& h, int trans, double* out) {
   const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
   const int nmax = h.nmax, ld = h.ld;
   QPMeta* meta = h.meta.as<QPMeta>();
   double* rhs = h.rhs.as<double>();
   double* full = rhs + (size_t)B * nmax;
   double* x = h.x.as<double>();
-  { PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
-  hipLaunchKernelGGL(qp_solve_kernel, dim3(B), dim3(TPB), (size_t)nmax * sizeof(double), h.stream,
-                     h.K.as<double>(), h.ipiv.as<int32_t>(), meta, nmax, ld, trans, rhs, x);
-  check_launch(); }
-  { PhaseTimer pt(h, DOPT_PHASE_QP_LSQR);
-  hipLaunchKernelGGL(qp_lsqr_kernel, dim3(B), dim3(TPB), (size_t)5 * nmax * sizeof(double), h.stream,
-                     h.K.as<double>(), meta, nmax, ld, trans, rhs, x, (int32_t*)nullptr);
-  check_launch(); }
+  if (nmax > SMALL_LU_MAX) {
+    PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
+    hipLaunchKernelGGL(qp_solve_kernel, dim3(B), dim3(TPB), (size_t)nmax * sizeof(double), h.stream,
+                       h.K.as<double>(), h.ipiv.as<int32_t>(), meta, nmax, ld, trans, rhs, x);
+    check_launch();
+  }
+  {
+    PhaseTimer pt(h, DOPT_PHASE_QP_LSQR);
+    hipLaunchKernelGGL(qp_lsqr_kernel, dim3(B), dim3(TPB), (size_t)5 * nmax * sizeof(double), h.stream,
+                       h.K.as<double>(), meta, nmax, ld, trans, rhs, x, (int32_t*)nullptr);
+    check_launch();
+  }
   static const double dummy = 0.0;
   PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
   hipLaunchKernelGGL(qp_output_kernel, dim3(B), dim3(TPB), (size_t)n * sizeof(double), h.stream,
-                     x, m ? h.G : &dummy, h.s.as<double>(), h.kidx.as<int32_t>() + (size_t)B * m,
-                     meta, full, n, m, p, nmax, trans, out);
+                     x, m ? h.G : &dummy, h.s.as<double>(), rpos_of(h), meta, full, n, m, p, nmax,
+                     trans, out);
   check_launch();
+}
+
+static void fallback_rev_rhs(Handle& h, const double* dl_dz) {
+  PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
+  hipLaunchKernelGGL(qp_rev_rhs_kernel, dim3(h.batch), dim3(TPB), 0, h.stream, dl_dz,
+                     h.meta.as<QPMeta>(), h.n, h.nmax, h.rhs.as<double>());
+  check_launch();
+}
+
+static void fallback_fwd_rhs(Handle& h, const FwdTangents& T) {
+  const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
+  double* rhs = h.rhs.as<double>();
+  double* full = rhs + (size_t)B * h.nmax;
+  static const double dummy = 0.0;
+  PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
+  hipLaunchKernelGGL(qp_fwd_rhs_kernel, dim3(B), dim3(TPB), (size_t)(2 * n + 2 * m + 2 * p) * sizeof(double),
+                     h.stream, T.dQ, T.dq, T.dG, T.dh, T.dA, T.db, h.z, m ? h.lam : &dummy,
+                     p ? h.nu : &dummy, rpos_of(h), h.meta.as<QPMeta>(), n, m, p, h.nmax, full, rhs);
+  check_launch();
+}
+
+static FwdTangents tangents(Handle& h, const double* dQ, const double* dq, const double* dG,
+                            const double* dh, const double* dA, const double* db) {
+  FwdTangents T;
+  T.dQ = dQ;
+  T.dq = dq;
+  T.dG = h.m ? dG : nullptr;
+  T.dh = h.m ? dh : nullptr;
+  T.dA = h.p ? dA : nullptr;
+  T.db = h.p ? db : nullptr;
+  return T;
 }
 
 void qp_reverse(Handle& h, const double* dl_dz, double* out) {
   if (!h.factored) qp_factor(h);
-  { PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
-  hipLaunchKernelGGL(qp_rev_rhs_kernel, dim3(h.batch), dim3(TPB), 0, h.stream, dl_dz,
-                     h.meta.as<QPMeta>(), h.n, h.nmax, h.rhs.as<double>());
-  check_launch(); }
-  qp_solve_and_output(h, 0, out);
+  const int B = (int)h.batch;
+  double* full = h.rhs.as<double>() + (size_t)B * h.nmax;
+  {
+    PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
+    hipLaunchKernelGGL(qp_solve_fast_kernel, dim3(fast_grid(h)), dim3(FAST_THREADS), 0, h.stream, qp_inputs(h),
+                       tangents(h, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr), dl_dz, B,
+                       h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(), rpos_of(h), perm_of(h),
+                       dinv_of(h), h.meta.as<QPMeta>(), full, 0, out);
+    check_launch();
+  }
+  fallback_rev_rhs(h, dl_dz);
+  fallback_solve_and_output(h, 0, out);
 }
 
 void qp_forward(Handle& h, const double* dQ, const double* dq, const double* dG,
                 const double* dh, const double* dA, const double* db, double* out) {
   if (!h.factored) qp_factor(h);
-  const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
-  double* rhs = h.rhs.as<double>();
-  double* full = rhs + (size_t)B * h.nmax;
-  static const double dummy = 0.0;
-  { PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
-  hipLaunchKernelGGL(qp_fwd_rhs_kernel, dim3(B), dim3(TPB), (size_t)(2 * n + 2 * m + 2 * p) * sizeof(double),
-                     h.stream, dQ, dq, m ? dG : nullptr, m ? dh : nullptr, p ? dA : nullptr,
-                     p ? db : nullptr, h.z, m ? h.lam : &dummy, p ? h.nu : &dummy,
-                     h.kidx.as<int32_t>() + (size_t)B * m, h.meta.as<QPMeta>(), n, m, p, h.nmax, full, rhs);
-  check_launch(); }
-  qp_solve_and_output(h, 1, out);
+  const int B = (int)h.batch;
+  double* full = h.rhs.as<double>() + (size_t)B * h.nmax;
+  const FwdTangents T = tangents(h, dQ, dq, dG, dh, dA, db);
+  {
+    PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
+    hipLaunchKernelGGL(qp_solve_fast_kernel, dim3(fast_grid(h)), dim3(FAST_THREADS), 0, h.stream, qp_inputs(h),
+                       T, (const double*)nullptr, B, h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(),
+                       rpos_of(h), perm_of(h), dinv_of(h), h.meta.as<QPMeta>(), full, 1, out);
+    check_launch();
+  }
+  fallback_fwd_rhs(h, T);
+  fallback_solve_and_output(h, 1, out);
 }
 
 void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
                         const double* dq, const double* dG, const double* dh,
                         const double* dA, const double* db, double* out_rev,
                         double* out_fwd) {
-  if (!h.factored) qp_factor(h);
-  qp_reverse(h, dl_dz, out_rev);
-  qp_forward(h, dQ, dq, dG, dh, dA, db, out_fwd);
+  const int B = (int)h.batch;
+  const int grid = fast_grid(h);
+  const size_t ws_stride = fast_ws_stride();
+  h.ws.ensure((size_t)grid * ws_stride * sizeof(double));
+  double* full = h.rhs.as<double>() + (size_t)B * h.nmax;
+  const FwdTangents T = tangents(h, dQ, dq, dG, dh, dA, db);
+  {
+    PhaseTimer pt(h, DOPT_PHASE_QP_FUSED);
+    hipLaunchKernelGGL(qp_fused_kernel, dim3(grid), dim3(FAST_THREADS), fast_dyn_lds(h.n), h.stream,
+                       qp_inputs(h), T, dl_dz, B, h.ws.as<double>(), ws_stride, h.K.as<double>(), h.ld,
+                       h.nmax, h.s.as<double>(), h.kidx.as<int32_t>(), rpos_of(h), h.meta.as<QPMeta>(),
+                       full, out_rev, out_fwd, 1, 1, h.stamps.as<unsigned long long>());
+    check_launch();
+  }
+  // fallback problems were prepared + assembled by the fused kernel
+  if (h.nmax > SMALL_LU_MAX) {
+    PhaseTimer pt(h, DOPT_PHASE_QP_LU);
+    hipLaunchKernelGGL(qp_lu_generic_kernel, dim3(B), dim3(TPB), 0, h.stream, h.K.as<double>(),
+                       h.ipiv.as<int32_t>(), h.meta.as<QPMeta>(), h.nmax, h.ld);
+    check_launch();
+  }
+  fallback_rev_rhs(h, dl_dz);
+  fallback_solve_and_output(h, 0, out_rev);
+  fallback_fwd_rhs(h, T);
+  fallback_solve_and_output(h, 1, out_fwd);
+  h.factored = false;   // the fused path leaves no reusable factorisation
 }
 
 }  // namespace dopt

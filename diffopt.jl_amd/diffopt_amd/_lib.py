@@ -49,8 +49,9 @@ SIGNATURES = {
     "dopt_set_profiling": (ctypes.c_int, [_h, ctypes.c_int32]),
     "dopt_get_phase_times": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]),
     "dopt_phase_name": (ctypes.c_char_p, [ctypes.c_int32]),
+    "dopt_debug_stamps": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_int32]),
 }
-NUM_PHASES = 11
+NUM_PHASES = 12
 
 
 class EngineUnavailable(RuntimeError):

@@ -160,13 +160,19 @@ int dopt_get_system_size(dopt_handle* h, int32_t* sizes);
 #define DOPT_PHASE_CONIC_RHS 8    /* conic right-hand sides                      */
 #define DOPT_PHASE_CONIC_LSQR 9   /* conic LSQR on M                             */
 #define DOPT_PHASE_CONIC_OUTPUT 10
-#define DOPT_NUM_PHASES 11
+#define DOPT_PHASE_QP_FUSED 11    /* fused prepare+assemble+LU+both solves      */
+#define DOPT_NUM_PHASES 12
 int dopt_set_profiling(dopt_handle* h, int32_t on);
 /* Accumulated milliseconds and launch counts per phase since the last call
  * (arrays of length nphases ≤ DOPT_NUM_PHASES); resets the accumulators. */
 int dopt_get_phase_times(dopt_handle* h, double* ms, int32_t* counts,
                          int32_t nphases);
 const char* dopt_phase_name(int32_t phase);
+/* Diagnostic: in-kernel cycle stamps of the fused QP kernel, summed over
+ * workgroups, when the process runs with DOPT_STAMPS=1 (slots: prepare,
+ * assemble, LU panel, LU L11⁻¹, LU trailing update, reverse, forward).
+ * Returns the number of slots written (0 if stamps are off); resets them. */
+int dopt_debug_stamps(dopt_handle* h, int64_t* out, int32_t n);
 /* wall time (s) of the last forward/reverse call, incl. any factorisation it
  * triggered — the DifferentiateTimeSec analogue (diff_opt.jl:256-266). */
 double dopt_last_time(const dopt_handle* h);
