@@ -173,11 +173,19 @@ def main():
         name, (ms_tot, cnt) = max(phases.items(), key=lambda kv: kv[1][0])
         avg_s = ms_tot / cnt / 1e3
         Ns = sizes.astype("float64")
-        if name == "qp_lu":
-            work = float((2.0 / 3.0 * Ns ** 3).sum())          # reduced-KKT LU flops
+        # algorithmic HBM bytes of one fused step: read Q, G, h, z, λ (+A, ν) and
+        # the tangents, write both sensitivity vectors
+        io_bytes = float(B * 8.0 * (n * n + (m + p) * n + 2 * m + 2 * p + 3 * n + m + 2 * L))
+        if name in ("qp_lu", "qp_fused"):
+            # reduced-KKT LU flops (+ the two triangular-solve pairs when fused)
+            work = float((2.0 / 3.0 * Ns ** 3).sum())
+            if name == "qp_fused":
+                work += float((4.0 * Ns ** 2).sum())
             achieved = work / avg_s / 1e12
             roof = dict(bound="mfma", achieved=round(achieved, 3), peak=PEAK_FP64_TFLOPS,
                         unit="TFLOP/s", frac=round(achieved / PEAK_FP64_TFLOPS, 4))
+            if name == "qp_fused":
+                roof["io_GBs"] = round(io_bytes / avg_s / 1e9, 1)
         else:
             if name == "qp_solve":
                 work = float((8.0 * Ns ** 2).sum())               # one read of the LU factors

@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Summarise two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; separate runs
+because they do not fit one TCC pass on gfx950) into profiles/pmc_latest.json:
+HBM bytes per launch per engine kernel.
+
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports ½ of the
+bytes of wide coalesced reads → doubled here; WRITE_SIZE is taken as is.
+FETCH_SIZE/WRITE_SIZE are in KB (rocprofv3 derived counters) → ×1024.
+
+  python tools/pmc_summary.py <fetch_dir> <write_dir> <out.json>
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+# rocprof kernel-name fragment → engine phase name (bench.py roofline keys)
+KERNEL_PHASE = {
+    "qp_fused_kernel": "qp_fused",
+    "qp_factor_fast_kernel": "qp_lu",
+    "qp_solve_fast_kernel": "qp_solve",
+    "conic_lsqr_kernel": "conic_lsqr",
+    "conic_cone_kernel": "conic_cone",
+}
+
+
+def per_launch(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    acc = defaultdict(lambda: defaultdict(float))   # phase → dispatch → value
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                kn = row.get("Kernel_Name", "")
+                for frag, ph in KERNEL_PHASE.items():
+                    if frag in kn:
+                        acc[ph][row.get("Dispatch_Id")] += float(row["Counter_Value"])
+    return {ph: sum(v.values()) / len(v) for ph, v in acc.items() if v}
+
+
+def main():
+    fdir, wdir, out = sys.argv[1:4]
+    fetch = per_launch(fdir, "FETCH_SIZE")
+    write = per_launch(wdir, "WRITE_SIZE")
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes",
+           "correction": "FETCH_SIZE x2 (gfx950 wide-read halving), KB x1024",
+           "kernels": {}}
+    for ph in sorted(set(fetch) | set(write)):
+        rb = fetch.get(ph, 0.0) * 2 * 1024
+        wb = write.get(ph, 0.0) * 1024
+        res["kernels"][ph] = {"read_bytes_per_launch": rb, "write_bytes_per_launch": wb,
+                              "hbm_bytes_per_launch": rb + wb}
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
