@@ -130,16 +130,18 @@ def main():
     out_fwd = torch.empty(B, L, dtype=torch.float64, device="cuda")
     gathered = None
     if world > 1 and not args.no_allgather:
-        gathered = torch.empty(world, B, 2 * L, dtype=torch.float64, device="cuda")
+        from diffopt_amd import parallel
+        gathered = True
         packed = torch.empty(B, 2 * L, dtype=torch.float64, device="cuda")
 
     def step():
         eng.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"] if p else None,
                             out_rev=out_rev, out_fwd=out_fwd)
         if gathered is not None:
-            packed[:, :L].copy_(out_rev)
-            packed[:, L:].copy_(out_fwd)
-            dist.all_gather_into_tensor(gathered.view(-1), packed.view(-1))
+            # weak scaling: every rank owns B problems of the world·B batch;
+            # one RCCL all-gather of the packed [rev | fwd] sensitivities
+            parallel.pack(out_rev, out_fwd, into=packed)
+            parallel.all_gather_rows(packed, world * B)
 
     for _ in range(args.warmup):
         step()
