@@ -30,10 +30,17 @@ constexpr int FAST_MAX = FT;       // max reduced system size (one panel row per
 constexpr int LP = FNB + 1;        // padded LDS row of a 32×32 block
 constexpr int DINV_STRIDE = 2 * FNB * FNB;   // doubles per panel in `dinv` (L11⁻¹, U11⁻¹)
 
+constexpr int UCH = 12;            // U12 column tiles staged in LDS per chunk
+
+struct alignas(16) PivotCand {
+  long long key;   // bits of |a| (monotone for a ≥ 0), −1: no candidate
+  int pos;         // logical position of the candidate row
+  int wave;
+};
+
 struct FastLDS {
-  double slot[2][NW][FNB];       // per-wave argmax row, double buffered
-  double sval[2][NW];
-  int sidx[2][NW];
+  PivotCand cand[NW];            // per-wave pivot candidate of the current column
+  double prow[FNB];              // broadcast pivot row (rotated, masked)
   int info;
   int pad[3];
   double Lt[FNB * LP];           // diagonal block staging (L11 | U11)
@@ -44,6 +51,7 @@ struct FastLDS {
   double tmp[FAST_MAX];
   double part[(FT / 32) * LP];
   double atile[NW][16 * 17];     // per-wave transpose tiles (assembly)
+  double u12[UCH * 8 * 64];      // U12 tiles in MFMA B-operand order
 };
 
 // Diagnostic cycle stamps (s_memtime, thread 0): active only when the kernel
@@ -76,69 +84,134 @@ __device__ __forceinline__ double fwave_sum(double v) {
 }
 
 // ---------------------------------------------------------------------------
-// LU of the N×N row-major matrix K (row stride ld), N ≤ FAST_MAX.  Writes
-// L11⁻¹ / U11⁻¹ of every diagonal block to dinv.  Returns LAPACK-style info.
+// Wave argmax of (key, idx): max key, ties → smallest idx (LAPACK idamax:
+// first maximum in the current order).  key = bit pattern of |a| (monotone
+// for non-negative doubles) or −1 for non-candidates.  Four DPP steps reduce
+// each 16-lane row, two row_bcast steps fold the rows into lane 63.
 // ---------------------------------------------------------------------------
-// N: padded size (multiple of 32, rows/columns ≥ Nt are an identity block);
-// Nt: true size (trailing updates never touch the decoupled padding).
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void amax_step(long long& key, int& idx) {
+  const int lo = (int)(unsigned long long)key, hi = (int)((unsigned long long)key >> 32);
+  const int olo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROWMASK, 0xF, false);
+  const int ohi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROWMASK, 0xF, false);
+  const int oi = __builtin_amdgcn_update_dpp(idx, idx, CTRL, ROWMASK, 0xF, false);
+  const long long ok = (long long)(((unsigned long long)(unsigned)ohi << 32) | (unsigned)olo);
+  const bool take = ok > key || (ok == key && oi < idx);
+  key = take ? ok : key;
+  idx = take ? oi : idx;
+}
+
+// same fold carrying the candidate's wave id along
+template <int CTRL>
+__device__ __forceinline__ void amax3_step(long long& key, int& idx, int& w) {
+  const int lo = (int)(unsigned long long)key, hi = (int)((unsigned long long)key >> 32);
+  const int olo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, 0xF, 0xF, false);
+  const int ohi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, 0xF, 0xF, false);
+  const int oi = __builtin_amdgcn_update_dpp(idx, idx, CTRL, 0xF, 0xF, false);
+  const int ow = __builtin_amdgcn_update_dpp(w, w, CTRL, 0xF, 0xF, false);
+  const long long ok = (long long)(((unsigned long long)(unsigned)ohi << 32) | (unsigned)olo);
+  const bool take = ok > key || (ok == key && oi < idx);
+  key = take ? ok : key;
+  idx = take ? oi : idx;
+  w = take ? ow : w;
+}
+
+__device__ __forceinline__ void wave_argmax(long long& key, int& idx) {
+  amax_step<0xB1, 0xF>(key, idx);    // quad_perm [1,0,3,2]
+  amax_step<0x4E, 0xF>(key, idx);    // quad_perm [2,3,0,1]
+  amax_step<0x141, 0xF>(key, idx);   // row_half_mirror
+  amax_step<0x140, 0xF>(key, idx);   // row_mirror
+  amax_step<0x142, 0xA>(key, idx);   // row_bcast:15 → rows 1, 3
+  amax_step<0x143, 0xC>(key, idx);   // row_bcast:31 → rows 2, 3
+  const int lo = __builtin_amdgcn_readlane((int)(unsigned long long)key, 63);
+  const int hi = __builtin_amdgcn_readlane((int)((unsigned long long)key >> 32), 63);
+  idx = __builtin_amdgcn_readlane(idx, 63);
+  key = (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// ---------------------------------------------------------------------------
+// LU of the row-major matrix K (row stride ld).  N: padded size (multiple of
+// 32; rows/columns ≥ Nt are an identity block, exact because they decouple);
+// Nt: true size (trailing updates never touch the padding).  Writes L11⁻¹ /
+// U11⁻¹ of every diagonal block to dinv.  Returns LAPACK-style info.
+//
+// Panel: thread t owns the panel segment of logical row c0+t (physical row
+// `phys`) in a ROTATING register window — at column step j, r[c] holds panel
+// column (j+c) mod 32 — so the column loop stays rolled (small code, static
+// register indices); the elimination of step j writes the shifted window.
+// Pivoting only relabels logical positions (`pos`); no row data moves.
+// Trailing update: U12 = L11⁻¹·A12 per 16-column tile (wave-split, MFMA),
+// staged in LDS in B-operand order; then waves stream (row tile, 4 column
+// tiles) items with the L21 fragment in registers.
+// ---------------------------------------------------------------------------
 __device__ __forceinline__ int lu_fast(double* __restrict__ K, int ld, int N, int Nt,
                                        double* __restrict__ dinv, FastLDS& S, Stamp& st) {
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
   for (int i = t; i < N; i += FT) S.perm[i] = i;
-  if (t == 0) S.info = 0;
+  int info = 0;   // uniform: every thread sees the same pivots
   __syncthreads();
   for (int c0 = 0; c0 < N; c0 += FNB) {
     const int R = N - c0;
-    // Thread t owns the panel segment of logical row c0+t (physical row
-    // `phys`) for the whole panel; pivoting only relabels logical positions
-    // (`pos`), so no row data moves between threads.  LAPACK getf2 order:
-    // pivot = first max |a| in the current (logical) order.
     const bool own = t < R;
     const int phys = S.perm[c0 + (own ? t : 0)];
     int pos = own ? t : -1;
-    double pr[FNB];
+    double r[FNB];
     {
-      const double* src = K + (size_t)phys * ld + c0;
+      const double* src = K + (size_t)phys * ld + c0;   // valid row for every thread
 #pragma unroll
-      for (int c = 0; c < FNB; ++c) pr[c] = own ? src[c] : 0.0;
+      for (int c = 0; c < FNB; ++c) {
+        const double v = src[c];
+        r[c] = own ? v : 0.0;
+      }
     }
-#pragma clang loop unroll(full)
+    const bool wact = wv * 64 < R;   // wave owns at least one panel row (uniform)
+    // Per column: (1) wave argmax → one 16-B (key, pos, wave) entry per wave;
+    // barrier; (2) active waves fold the 8 entries (one ds_read_b128 + 3 DPP
+    // steps), the single winning lane publishes its row; barrier; (3) active
+    // waves eliminate with the broadcast pivot row.  LDS traffic per column
+    // is one row write and one row read per active wave (the step is
+    // LDS-throughput-bound, not barrier-bound).
+#pragma unroll 1
     for (int j = 0; j < FNB; ++j) {
-      const int buf = j & 1;
-      const bool cand = own && pos >= j;
-      double best = cand ? fabs(pr[j]) : -1.0;
-      int bi = cand ? pos : 0x7fffffff;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const double ov = __shfl_xor(best, o);
-        const int oi = __shfl_xor(bi, o);
-        if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+      if (wact) {
+        const bool cand = own && pos >= j;
+        long long key = cand ? __double_as_longlong(fabs(r[0])) : -1LL;
+        int bi = cand ? pos : 0x7fffffff;
+        wave_argmax(key, bi);
+        if (lane == 0) S.cand[wv] = PivotCand{key, bi, wv};
+      } else if (lane == 0) {
+        S.cand[wv] = PivotCand{-1LL, 0x7fffffff, wv};
       }
-      if (pos == bi) {
-#pragma unroll
-        for (int c = 0; c < FNB; ++c) S.slot[buf][wv][c] = pr[c];
-      }
-      if (lane == 0) { S.sval[buf][wv] = best; S.sidx[buf][wv] = bi; }
       __syncthreads();
-      double pb = S.sval[buf][0];
-      int pi = S.sidx[buf][0], ww = 0;
+      if (wact) {
+        const PivotCand pc = S.cand[lane & (NW - 1)];
+        long long key = pc.key;
+        int bi = pc.pos, bw = pc.wave;
+        amax3_step<0xB1>(key, bi, bw);    // quad_perm [1,0,3,2]
+        amax3_step<0x4E>(key, bi, bw);    // quad_perm [2,3,0,1]
+        amax3_step<0x141>(key, bi, bw);   // row_half_mirror: folds the 8 entries
+        bi = __builtin_amdgcn_readfirstlane(bi);
+        bw = __builtin_amdgcn_readfirstlane(bw);
+        if (wv == bw && pos == bi) {
+          // columns < j (rotated to the tail) are published as 0 so the
+          // elimination needs no masking
 #pragma unroll
-      for (int k = 1; k < NW; ++k) {
-        const double vk = S.sval[buf][k];
-        const int ik = S.sidx[buf][k];
-        if (vk > pb || (vk == pb && ik < pi)) { pb = vk; pi = ik; ww = k; }
+          for (int c = 0; c < FNB; ++c) S.prow[c] = (c < FNB - j) ? r[c] : 0.0;
+        }
+        if (pos == bi) pos = j;            // pivot row takes position j
+        else if (pos == j) pos = bi;       // row at j takes the pivot's old place
       }
-      const double* prow = S.slot[buf][ww];
-      const double pv = prow[j];
-      if (pos == pi) pos = j;            // pivot row takes position j
-      else if (pos == j) pos = pi;       // row at j takes the pivot's old place
-      if (pv == 0.0) {
-        if (t == 0 && S.info == 0) S.info = c0 + j + 1;
-      } else if (own && pos > j) {
-        const double l = pr[j] / pv;
-        pr[j] = l;
+      __syncthreads();
+      const double pv = S.prow[0];
+      info = (pv == 0.0 && info == 0) ? c0 + j + 1 : info;
+      if (wact) {
+        const bool below = own && pos > j && pv != 0.0;
+        const double r0 = r[0];
+        const double l = r0 / pv;
+        const double le = below ? l : 0.0;   // 0: row unchanged (fma(−0, p, v) = v)
 #pragma unroll
-        for (int c = j + 1; c < FNB; ++c) pr[c] = fma(-l, prow[c], pr[c]);
+        for (int c = 0; c < FNB - 1; ++c) r[c] = fma(-le, S.prow[c + 1], r[c + 1]);
+        r[FNB - 1] = below ? l : r0;
       }
     }
     st.mark(2);
@@ -147,13 +220,13 @@ __device__ __forceinline__ int lu_fast(double* __restrict__ K, int ld, int N, in
     if (own) {
       double* dst = K + (size_t)phys * ld + c0;
 #pragma unroll
-      for (int c = 0; c < FNB; ++c) dst[c] = pr[c];
+      for (int c = 0; c < FNB; ++c) dst[c] = r[c];
     }
     __syncthreads();   // every thread has read its old perm entry
     if (own) S.perm[c0 + pos] = phys;
     if (own && pos < FNB) {
 #pragma unroll
-      for (int c = 0; c < FNB; ++c) S.Lt[pos * LP + c] = pr[c];
+      for (int c = 0; c < FNB; ++c) S.Lt[pos * LP + c] = r[c];
     }
     __syncthreads();
     // ---- L11⁻¹ (wave 0) and U11⁻¹ (wave 1), one column per lane
@@ -171,9 +244,7 @@ __device__ __forceinline__ int lu_fast(double* __restrict__ K, int ld, int N, in
         if (jj > c) x[jj] = -acc;
       }
 #pragma unroll
-      for (int jj = 0; jj < FNB; ++jj) {
-        S.Linv[jj * LP + c] = x[jj];
-      }
+      for (int jj = 0; jj < FNB; ++jj) S.Linv[jj * LP + c] = x[jj];
     } else if (wv == 1 && lane < FNB) {
       const int c = lane;
       double x[FNB];
@@ -194,60 +265,81 @@ __device__ __forceinline__ int lu_fast(double* __restrict__ K, int ld, int N, in
       Db[i] = ((i < FNB * FNB) ? S.Linv : S.Uinv)[(e >> 5) * LP + (e & 31)];
     }
     st.mark(3);
-    const int Rt = Nt - c0;   // true rows/columns from c0 on
-    if (Rt <= FNB) break;     // no (true) trailing matrix
-    // ---- trailing update: wave-owned 16-column tiles, true extent only
-    const int nct = (Rt - FNB + 15) >> 4;
-    const int nrt = nct;
-    for (int ct = wv; ct < nct; ct += NW) {
-      const int colL = c0 + FNB + ct * 16 + (lane & 15);
-      const bool cok = colL < Nt;
-      d4f u0 = {0, 0, 0, 0}, u1 = {0, 0, 0, 0};
+    // Trailing update over the full padded extent: the identity padding
+    // contributes exact zeros (L21 padding rows and U12 padding columns are
+    // 0), so no tile needs a bounds predicate.
+    if (R <= FNB) break;             // last panel: no trailing matrix
+    const int nct = (R - FNB) >> 4;  // 16-wide tiles of the trailing matrix
+    for (int ch0 = 0; ch0 < nct; ch0 += UCH) {
+      const int chn = min(UCH, nct - ch0);
+      // ---- U12 = L11⁻¹·A12 for this chunk's column tiles (wave-split)
+      for (int q = wv; q < chn; q += NW) {
+        const int colL = c0 + FNB + (ch0 + q) * 16 + l16;
+        double bv[FNB / 4];
 #pragma unroll
-      for (int s = 0; s < FNB / 4; ++s) {
-        const int k = 4 * s + g;
-        const double bv = cok ? K[(size_t)S.perm[c0 + k] * ld + colL] : 0.0;
-        u0 = fmfma(S.Linv[(lane & 15) * LP + k], bv, u0);
-        u1 = fmfma(S.Linv[(16 + (lane & 15)) * LP + k], bv, u1);
-      }
-      if (cok) {
+        for (int s = 0; s < FNB / 4; ++s) bv[s] = K[(size_t)S.perm[c0 + 4 * s + g] * ld + colL];
+        d4f u0 = {0, 0, 0, 0}, u1 = {0, 0, 0, 0};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          K[(size_t)S.perm[c0 + g + 4 * r] * ld + colL] = u0[r];
-          K[(size_t)S.perm[c0 + 16 + g + 4 * r] * ld + colL] = u1[r];
+        for (int s = 0; s < FNB / 4; ++s) {
+          u0 = fmfma(S.Linv[l16 * LP + 4 * s + g], bv[s], u0);
+          u1 = fmfma(S.Linv[(16 + l16) * LP + 4 * s + g], bv[s], u1);
+        }
+        double* ub = S.u12 + q * 512;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          ub[rr * 64 + lane] = u0[rr];
+          ub[(4 + rr) * 64 + lane] = u1[rr];
+          K[(size_t)S.perm[c0 + g + 4 * rr] * ld + colL] = u0[rr];
+          K[(size_t)S.perm[c0 + 16 + g + 4 * rr] * ld + colL] = u1[rr];
         }
       }
-#pragma unroll 2
-      for (int rt = 0; rt < nrt; ++rt) {
-        const int rA = FNB + rt * 16 + (lane & 15);
-        const double* arow = K + (size_t)S.perm[c0 + (rA < Rt ? rA : 0)] * ld + c0;
+      __syncthreads();
+      // ---- A22 −= L21·U12: items (row tile, group of ≤ 4 column tiles).
+      // Every load is unconditional (clamped duplicate columns are loaded but
+      // never stored), so one item's 24 loads are in flight together.
+      const int ngr = (chn + 3) >> 2;
+      const int nitems = nct * ngr;
+      for (int it = wv; it < nitems; it += NW) {
+        const int rt = it / ngr, q0 = (it - rt * ngr) * 4;
+        const int nq = min(4, chn - q0);
+        const int col = c0 + FNB + (ch0 + q0) * 16 + l16;
+        const double* arow = K + (size_t)S.perm[c0 + FNB + rt * 16 + l16] * ld + c0;
         double a[FNB / 4];
 #pragma unroll
-        for (int s = 0; s < FNB / 4; ++s) a[s] = (rA < Rt) ? -arow[4 * s + g] : 0.0;
-        size_t cidx[4];
-        bool cv[4];
-        d4f acc;
+        for (int s = 0; s < FNB / 4; ++s) a[s] = -arow[4 * s + g];
+        int ro[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int cr = FNB + rt * 16 + g + 4 * r;
-          cv[r] = cok && cr < Rt;
-          cidx[r] = (size_t)S.perm[c0 + (cr < Rt ? cr : 0)] * ld + colL;
-          acc[r] = cv[r] ? K[cidx[r]] : 0.0;
+        for (int rr = 0; rr < 4; ++rr) ro[rr] = S.perm[c0 + FNB + rt * 16 + g + 4 * rr] * ld;
+        d4f acc[4];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int cq = col + 16 * min(qq, nq - 1);
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) acc[qq][rr] = K[ro[rr] + cq];
+        }
+        const double* ub = S.u12 + q0 * 512 + lane;
+#pragma unroll
+        for (int s = 0; s < FNB / 4; ++s) {
+          double b[4];
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) b[qq] = ub[min(qq, nq - 1) * 512 + s * 64];
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) acc[qq] = fmfma(a[s], b[qq], acc[qq]);
         }
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc = fmfma(a[s], u0[s], acc);
+        for (int qq = 0; qq < 4; ++qq) {
+          if (qq < nq) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc = fmfma(a[4 + s], u1[s], acc);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (cv[r]) K[cidx[r]] = acc[r];
+            for (int rr = 0; rr < 4; ++rr) K[ro[rr] + col + 16 * qq] = acc[qq][rr];
+          }
+        }
       }
+      __syncthreads();
     }
-    __syncthreads();
     st.mark(4);
   }
   __syncthreads();
-  return S.info;
+  return info;
 }
 
 // ---------------------------------------------------------------------------
@@ -260,105 +352,80 @@ __device__ __forceinline__ int lu_fast(double* __restrict__ K, int ld, int N, in
 __device__ __forceinline__ void lu_solve_fast(const double* __restrict__ K, int ld, int N,
                                               const double* __restrict__ dinv, FastLDS& S,
                                               int trans) {
+  // Four right-looking block sweeps share one shape: per 32-block k,
+  //   (a) wave 0, lanes 0..31: x_k = D_k · v_k (D_k = a stored diagonal-block
+  //       inverse or its transpose), 
+  //   (b) every other entry e of the sweep: v_e −= Σ_j F(e, j) · x_k[j]
+  //       with F a 32-wide slice of L or U (a row segment when trans = 0, a
+  //       column segment when trans = 1).
+  // Both operand sets are loaded before the block's first barrier, so the
+  // global-load latency overlaps the diagonal GEMV.
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   double* y = S.y;
   double* v = S.tmp;
   const int nblk = N / FNB;   // N padded to a multiple of 32
-  constexpr int w = FNB;
   if (!trans) {
     for (int i = t; i < N; i += FT) v[i] = y[S.perm[i]];
-    __syncthreads();
-    for (int bk = 0; bk < nblk; ++bk) {           // L: forward
-      const int i0 = bk * FNB;
-      if (wv == 0 && lane < w) {
-        const double* Li = dinv + (size_t)bk * DINV_STRIDE + lane * FNB;
-        double acc = 0.0;
-#pragma unroll 8
-        for (int c = 0; c < w; ++c) acc = fma(Li[c], v[i0 + c], acc);
-        v[i0 + lane] = acc;
-      }
-      __syncthreads();
-      for (int r = i0 + w + t; r < N; r += FT) {
-        const double* row = K + (size_t)S.perm[r] * ld + i0;
-        double acc = v[r];
-#pragma unroll 8
-        for (int j = 0; j < w; ++j) acc = fma(-row[j], v[i0 + j], acc);
-        v[r] = acc;
-      }
-      __syncthreads();
-    }
-    for (int bk = nblk - 1; bk >= 0; --bk) {      // U: backward
-      const int i0 = bk * FNB;
-      if (i0 + w < N) {
-        for (int r = wv; r < w; r += NW) {
-          const double* row = K + (size_t)S.perm[i0 + r] * ld;
-          double acc = 0.0;
-          for (int c = i0 + w + lane; c < N; c += 64) acc = fma(row[c], v[c], acc);
-          acc = fwave_sum(acc);
-          if (lane == 0) v[i0 + r] -= acc;
-        }
-        __syncthreads();
-      }
-      if (wv == 0 && lane < w) {
-        const double* Ui = dinv + (size_t)bk * DINV_STRIDE + FNB * FNB + lane * FNB;
-        double acc = 0.0;
-#pragma unroll 8
-        for (int c = 0; c < w; ++c) acc = fma(Ui[c], v[i0 + c], acc);
-        v[i0 + lane] = acc;
-      }
-      __syncthreads();
-    }
-    for (int i = t; i < N; i += FT) y[i] = v[i];
-    __syncthreads();
   } else {
     for (int i = t; i < N; i += FT) v[i] = y[i];
-    __syncthreads();
-    for (int bk = 0; bk < nblk; ++bk) {           // Uᵀ: forward
+  }
+  __syncthreads();
+  for (int sweep = 0; sweep < 2; ++sweep) {
+    // trans = 0: sweep 0 = L (forward), sweep 1 = U (backward)
+    // trans = 1: sweep 0 = Uᵀ (forward), sweep 1 = Lᵀ (backward)
+    const bool fwd = sweep == 0;
+    const bool useU = (sweep == 1) != (trans != 0);   // which factor's inverse
+    for (int s = 0; s < nblk; ++s) {
+      const int bk = fwd ? s : nblk - 1 - s;
       const int i0 = bk * FNB;
-      if (wv == 0 && lane < w) {
-        const double* Ui = dinv + (size_t)bk * DINV_STRIDE + FNB * FNB + lane;
-        double acc = 0.0;
-#pragma unroll 8
-        for (int c = 0; c < w; ++c) acc = fma(Ui[c * FNB], v[i0 + c], acc);
-        v[i0 + lane] = acc;
-      }
-      __syncthreads();
-      for (int c = i0 + w + t; c < N; c += FT) {
-        double acc = v[c];
-        for (int j = 0; j < w; ++j) acc = fma(-K[(size_t)S.perm[i0 + j] * ld + c], v[i0 + j], acc);
-        v[c] = acc;
-      }
-      __syncthreads();
-    }
-    for (int bk = nblk - 1; bk >= 0; --bk) {      // Lᵀ: backward
-      const int i0 = bk * FNB;
-      if (i0 + w < N) {
-        const int jx = t & 31, rg = t >> 5;
-        double acc = 0.0;
-        if (jx < w)
-          for (int r = i0 + w + rg; r < N; r += FT / 32) acc = fma(K[(size_t)S.perm[r] * ld + i0 + jx], v[r], acc);
-        S.part[rg * LP + jx] = acc;
-        __syncthreads();
-        if (t < w) {
-          double s = 0.0;
+      // (b) operand: entry e of this thread (rows/columns after the block for
+      // the forward sweep, before it for the backward sweep)
+      const int e = fwd ? i0 + FNB + t : t;
+      const bool has = fwd ? e < N : e < i0;
+      const int ec = has ? e : i0;           // clamped, never used when !has
+      double f[FNB];
+      if (!trans) {
+        const double* row = K + (size_t)S.perm[ec] * ld + i0;
 #pragma unroll
-          for (int gg = 0; gg < FT / 32; ++gg) s += S.part[gg * LP + t];
-          v[i0 + t] -= s;
-        }
-        __syncthreads();
+        for (int j = 0; j < FNB; ++j) f[j] = row[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < FNB; ++j) f[j] = K[(size_t)S.perm[i0 + j] * ld + ec];
       }
-      if (wv == 0 && lane < w) {
-        const double* Li = dinv + (size_t)bk * DINV_STRIDE + lane;
+      // (a) diagonal block
+      if (wv == 0 && lane < FNB) {
+        const double* Dk = dinv + (size_t)bk * DINV_STRIDE + (useU ? FNB * FNB : 0);
+        double d[FNB];
+        if (!trans) {
+#pragma unroll
+          for (int j = 0; j < FNB; ++j) d[j] = Dk[lane * FNB + j];     // row `lane`
+        } else {
+#pragma unroll
+          for (int j = 0; j < FNB; ++j) d[j] = Dk[j * FNB + lane];     // column `lane`
+        }
         double acc = 0.0;
-#pragma unroll 8
-        for (int c = 0; c < w; ++c) acc = fma(Li[c * FNB], v[i0 + c], acc);
-        v[i0 + lane] = acc;
+#pragma unroll
+        for (int j = 0; j < FNB; ++j) acc = fma(d[j], v[i0 + j], acc);
+        S.part[lane] = acc;
+      }
+      __syncthreads();
+      if (wv == 0 && lane < FNB) v[i0 + lane] = S.part[lane];
+      if (has) {   // e lies outside block k: no thread reads v[e] in this step
+        double acc = v[e];
+#pragma unroll
+        for (int j = 0; j < FNB; ++j) acc = fma(-f[j], S.part[j], acc);
+        v[e] = acc;
       }
       __syncthreads();
     }
-    for (int i = t; i < N; i += FT) y[S.perm[i]] = v[i];
     __syncthreads();
   }
+  if (!trans) {
+    for (int i = t; i < N; i += FT) y[i] = v[i];
+  } else {
+    for (int i = t; i < N; i += FT) y[S.perm[i]] = v[i];
+  }
+  __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
@@ -370,9 +437,24 @@ __device__ __forceinline__ int prepare_wg(const QPIn& P, int b, double* s_out, i
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n = P.n, m = P.m, p = P.p;
   const double* Qb = P.Q + (size_t)b * n * n;
-  int nz = 0;
-  for (size_t i = t; i < (size_t)n * n; i += FT) nz |= (Qb[i] != 0.0);
-  const int iterative = !__syncthreads_or(nz);
+  // branch flag: norm(Q) ≈ 0 ⇔ Q == 0 (exact zero test); batched loads with
+  // a workgroup early exit once a nonzero is seen (dense QPs: first batch)
+  int iterative = 1;
+  {
+    const size_t nn = (size_t)n * n;
+    for (size_t i0 = 0; i0 < nn; i0 += (size_t)8 * FT) {
+      int nz = 0;
+      double q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const size_t i = i0 + (size_t)u * FT + t;
+        q[u] = Qb[i < nn ? i : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) nz |= (q[u] != 0.0);
+      if (__syncthreads_or(nz)) { iterative = 0; break; }
+    }
+  }
   for (int j = t; j < n; j += FT) zs[j] = P.z[(size_t)b * n + j];
   if (t == 0) cnt[NW] = 0;
   __syncthreads();
@@ -383,12 +465,12 @@ __device__ __forceinline__ int prepare_wg(const QPIn& P, int b, double* s_out, i
     if (i < m) {
       double acc = 0.0;
       int j = 0;
-      for (; j + 8 <= n; j += 8) {
-        double gv[8];
+      for (; j + 16 <= n; j += 16) {
+        double gv[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) gv[u] = Gb[i + (size_t)(j + u) * m];
+        for (int u = 0; u < 16; ++u) gv[u] = Gb[i + (size_t)(j + u) * m];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc = __dadd_rn(acc, __dmul_rn(gv[u], zs[j + u]));
+        for (int u = 0; u < 16; ++u) acc = __dadd_rn(acc, __dmul_rn(gv[u], zs[j + u]));
       }
       for (; j < n; ++j) acc = __dadd_rn(acc, __dmul_rn(Gb[i + (size_t)j * m], zs[j]));
       const double si = __dsub_rn(acc, P.h[(size_t)b * m + i]);
@@ -425,18 +507,13 @@ __device__ __forceinline__ int prepare_wg(const QPIn& P, int b, double* s_out, i
   return iterative;
 }
 
-// K (row-major, stride ld) = [Q, G_kᵀD(λ_k), Aᵀ; G_k, D(s_k), 0; A, 0, 0]
-// 16×16 tiles owned by waves (no workgroup barriers); column-major sources
-// are transposed through a wave-private LDS tile.
-__device__ __forceinline__ double kkt_src_colmajor(const QPIn& P, const double* Qb,
-                                                   const double* Gb, const double* Ab,
-                                                   const int32_t* kb, int nk, int r, int c) {
-  // rows r, columns c < n: contiguous along r in the sources
-  if (r < P.n) return Qb[r + (size_t)c * P.n];
-  if (r < P.n + nk) return Gb[kb[r - P.n] + (size_t)c * P.m];
-  return Ab[(r - P.n - nk) + (size_t)c * P.p];
-}
-
+// K (row-major, stride ld) = [Q, G_kᵀD(λ_k), Aᵀ; G_k, D(s_k), 0; A, 0, 0],
+// identity-padded to Np = round_up(N, 32).  16×16 tiles owned by waves (no
+// workgroup barriers inside the tile loop); column-major sources (c < n) are
+// transposed through a wave-private LDS tile.  Every global load is
+// unconditional (a select picks the source address, out-of-block elements
+// read a dummy and are discarded), so a tile's loads are in flight together.
+// kidx, λ_k and s_k are staged in LDS (perm / y / tmp are free here).
 __device__ __forceinline__ void assemble_wg(const QPIn& P, int b, const double* s,
                                             const int32_t* kidx, int nk, double* K, int ld,
                                             FastLDS& S) {
@@ -449,45 +526,67 @@ __device__ __forceinline__ void assemble_wg(const QPIn& P, int b, const double* 
   const double* lb = P.lam + (size_t)b * m;
   const double* sb = s + (size_t)b * m;
   const int32_t* kb = kidx + (size_t)b * m;
+  int* kid = S.perm;
+  double* lamk = S.y;
+  double* sk = S.tmp;
+  for (int i = t; i < nk; i += FT) {
+    const int k = kb[i];
+    kid[i] = k;
+    lamk[i] = lb[k];
+    sk[i] = sb[k];
+  }
+  __syncthreads();
   double* tl = S.atile[wv];
-  const int Np = (N + 31) & ~31;      // identity-padded to full 32-wide panels
+  const int Np = (N + 31) & ~31;
   const int T = Np >> 4;
   const int lr = lane & 15, lg = lane >> 4;
   for (int tile = wv; tile < T * T; tile += NW) {
     const int r0 = (tile / T) * 16, c0 = (tile % T) * 16;
     if (c0 < n) {
       // transpose stage: lane reads source rows r0+lr, columns c0+lg+4q
+      const int r = r0 + lr;
+      const double* base;
+      size_t cstride;
+      if (r < n) { base = Qb + r; cstride = n; }
+      else if (r < n + nk) { base = Gb + kid[r - n]; cstride = m; }
+      else if (r < N) { base = Ab + (r - n - nk); cstride = p; }
+      else { base = Qb; cstride = 0; }
+      double v[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int r = r0 + lr, c = c0 + lg + 4 * q;
-        tl[(lg + 4 * q) * 17 + lr] = (r < N && c < n) ? kkt_src_colmajor(P, Qb, Gb, Ab, kb, nk, r, c) : 0.0;
+        const int c = c0 + lg + 4 * q;
+        const bool ok = r < N && c < n;
+        v[q] = base[(size_t)(ok ? c : 0) * cstride];
+        v[q] = ok ? v[q] : 0.0;
       }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) tl[(lg + 4 * q) * 17 + lr] = v[q];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    // direct stage: lane writes K rows r0+lg+4q, column c0+lr
+    const int c = c0 + lr;
+    const bool cG = c >= n && c < n + nk, cA = c >= n + nk && c < N;
+    const int ci = cG ? c - n : 0;
+    const double* cbase = cG ? Gb + kid[ci] : (cA ? Ab + (c - n - nk) : Qb);
+    const size_t rstride = cG ? (size_t)m : (cA ? (size_t)p : 0);
+    const double mul = cG ? lamk[ci] : 1.0;
+    double v[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int r = r0 + lg + 4 * q, c = c0 + lr;
-      {
-        double val;
-        if (r >= N || c >= N) {
-          val = (r == c) ? 1.0 : 0.0;
-        } else if (c < n) {
-          val = tl[lr * 17 + lg + 4 * q];
-        } else if (r < n) {
-          if (c < n + nk) {
-            const int i = kb[c - n];
-            val = Gb[i + (size_t)r * m] * lb[i];
-          } else {
-            val = Ab[(c - n - nk) + (size_t)r * p];
-          }
-        } else {
-          val = (c == r && r < n + nk) ? sb[kb[r - n]] : 0.0;
-        }
-        K[(size_t)r * ld + c] = val;
-      }
+      const int r = r0 + lg + 4 * q;
+      const bool ld_ok = r < n && (cG || cA);
+      v[q] = cbase[(size_t)(ld_ok ? r : 0) * rstride];
+      double val;
+      if (c < n) val = tl[lr * 17 + lg + 4 * q];
+      else if (ld_ok) val = v[q] * mul;
+      else if (r == c) val = (r >= N) ? 1.0 : ((r >= n && r < n + nk) ? sk[max(r - n, 0)] : 0.0);
+      else val = 0.0;
+      v[q] = val;
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) K[(size_t)(r0 + lg + 4 * q) * ld + c] = v[q];
     __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
@@ -580,8 +679,18 @@ __device__ __forceinline__ void output_wg(const QPIn& P, int b, const double* x,
     if (kk >= 0) {
       xl = x[n + kk];
     } else if (!trans) {
+      // eliminated row: x_λ = (0 − G_l·x_z)/s_l; column-major G is coalesced
+      // across l, loads batched 16 deep
       double acc = 0.0;
-      for (int j = 0; j < n; ++j) acc = fma(Gb[l + (size_t)j * m], x[j], acc);
+      int j = 0;
+      for (; j + 16 <= n; j += 16) {
+        double gv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) gv[u] = Gb[l + (size_t)(j + u) * m];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc = fma(gv[u], x[j + u], acc);
+      }
+      for (; j < n; ++j) acc = fma(Gb[l + (size_t)j * m], x[j], acc);
       xl = (0.0 - acc) / s[(size_t)b * m + l];
     } else {
       xl = full[(size_t)b * (n + m + p) + n + l] / s[(size_t)b * m + l];
