@@ -100,6 +100,9 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
         DOPT_CHECK_HIP(hipMemset(h->stamps.p, 0, 8 * sizeof(unsigned long long)));
       }
     }
+    if (const char* e = getenv("DOPT_FAST_MAX")) {
+      h->fast_max = std::max(0, std::min(atoi(e), dopt::FAST_MAX_N));
+    }
     if (kind == DOPT_KIND_QP) {
       // Systems are identity-padded to whole 32-column LU panels (qp_fast.hip),
       // so the per-problem stride / row stride are rounded up to 32.
@@ -160,6 +163,15 @@ int dopt_set_memory(dopt_handle* h, int32_t mem) {
   return guarded(h, [&]() {
     if (mem != DOPT_MEM_HOST && mem != DOPT_MEM_DEVICE) throw Error(-1, "bad memory mode");
     h->mem = mem;
+    return 0;
+  });
+}
+
+int dopt_set_qp_fast_max(dopt_handle* h, int32_t fast_max) {
+  return guarded(h, [&]() {
+    if (fast_max < 0 || fast_max > dopt::FAST_MAX_N) throw Error(-1, "fast_max must be in [0, 512]");
+    h->fast_max = fast_max;
+    h->factored = false;
     return 0;
   });
 }

@@ -57,6 +57,18 @@ struct QPMeta {
 // Workgroup size of the fast QP kernels (qp_fast.hip); the launch sites in
 // qp.hip must use exactly this (the kernels' thread mappings assume it).
 constexpr int FAST_THREADS = 512;
+constexpr int FAST_MAX_N = 512;      // largest reduced system of the fused one-WG path
+constexpr int BLOCKED_MAX = 1536;    // largest reduced system of the blocked step path
+
+// Which factorisation path a problem takes (decided per problem on the
+// device from its reduced size; fast_max ≤ FAST_MAX_N is a handle setting).
+enum QPRoute { ROUTE_LSQR = 0, ROUTE_FAST = 1, ROUTE_BLOCKED = 2, ROUTE_GENERIC = 3 };
+__host__ __device__ inline int qp_route(int iterative, int nsys, int fast_max) {
+  if (iterative) return ROUTE_LSQR;
+  if (nsys <= fast_max) return ROUTE_FAST;
+  if (nsys <= BLOCKED_MAX) return ROUTE_BLOCKED;
+  return ROUTE_GENERIC;
+}
 
 // QP problem inputs / forward tangents as seen by the kernels (device pointers)
 struct QPIn {
@@ -87,6 +99,9 @@ struct Handle {
   DevBuf dinv;               // per-problem diagonal-block inverses (split path)
   DevBuf stamps;             // diagnostic in-kernel cycle stamps (env DOPT_STAMPS=1)
   int32_t wg_per_cu = 2;     // persistent-grid occupancy of the fast kernels
+  int32_t fast_max = FAST_MAX_N;   // reduced sizes above this take the blocked path (env DOPT_FAST_MAX)
+  int32_t blocked_npmax = 0;       // largest padded blocked system of the current factorisation
+  bool has_generic = true;         // some problem exceeds BLOCKED_MAX (set by the read-back)
   bool set = false, factored = false;
 
   // ---- CONIC ----
@@ -161,6 +176,10 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
                         const double* dq, const double* dG, const double* dh,
                         const double* dA, const double* db, double* out_rev,
                         double* out_fwd);
+// blocked step path (qp_blocked.hip) for ROUTE_BLOCKED problems, on the
+// per-problem K / perm (ipiv) / dinv buffers the assembly filled
+void qp_blocked_factor(Handle& h, double* dinv);
+void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rhs, double* x);
 void conic_factor(Handle& h);
 void conic_forward(Handle& h, const double* dA, const double* db, const double* dc,
                    double* out, double* out_dx);

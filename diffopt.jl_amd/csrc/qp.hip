@@ -24,7 +24,6 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int TPB = 256;   // threads per workgroup (4 waves)
 constexpr int NB = 32;     // LU panel width
-constexpr int SMALL_LU_MAX = 512;  // max system size for the LDS-panel LU
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -58,7 +57,7 @@ __global__ __launch_bounds__(TPB) void qp_lu_generic_kernel(
   const int lane = t & 63, wv = t >> 6;
   if (meta[b].iterative) return;
   const int N = meta[b].nsys;
-  if (N <= SMALL_LU_MAX) return;
+  if (N <= BLOCKED_MAX) return;   // fused / blocked paths own these
   double* Kb = K + (size_t)b * nmax * ld;
   int32_t* piv = ipiv + (size_t)b * nmax;
   int info = 0;
@@ -126,7 +125,7 @@ __global__ __launch_bounds__(TPB) void qp_solve_kernel(
   const int lane = t & 63, wv = t >> 6;
   if (meta[b].iterative) return;
   const int N = meta[b].nsys;
-  if (N <= SMALL_LU_MAX) return;   // fast path (qp_fast.hip) owns these
+  if (N <= BLOCKED_MAX) return;   // fused / blocked paths own these
   const int nb = 1;                // generic LU: panel width 1, lazy swaps
   const double* Kb = K + (size_t)b * nmax * ld;
   const int32_t* piv = ipiv + (size_t)b * nmax;
@@ -384,10 +383,10 @@ __global__ __launch_bounds__(TPB) void qp_lsqr_kernel(
 // reverse RHS: [dl_dz; 0] reduced (QuadraticProgram.jl:329)
 __global__ __launch_bounds__(TPB) void qp_rev_rhs_kernel(
     const double* __restrict__ dl_dz, const QPMeta* __restrict__ meta, int n,
-    int nmax, double* __restrict__ rhs) {
+    int nmax, int fast_max, double* __restrict__ rhs) {
   const int b = blockIdx.x, t = threadIdx.x;
   const int N = meta[b].nsys;
-  if (!meta[b].iterative && N <= SMALL_LU_MAX) return;
+  if (qp_route(meta[b].iterative, N, fast_max) == ROUTE_FAST) return;
   for (int i = t; i < N; i += TPB) rhs[(size_t)b * nmax + i] = (i < n) ? dl_dz[(size_t)b * n + i] : 0.0;
 }
 
@@ -400,11 +399,11 @@ __global__ __launch_bounds__(TPB) void qp_fwd_rhs_kernel(
     const double* __restrict__ dA, const double* __restrict__ db,
     const double* __restrict__ z, const double* __restrict__ lam,
     const double* __restrict__ nu, const int32_t* __restrict__ rpos,
-    const QPMeta* __restrict__ meta, int n, int m, int p, int nmax,
+    const QPMeta* __restrict__ meta, int n, int m, int p, int nmax, int fast_max,
     double* __restrict__ full, double* __restrict__ rhs) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  if (!meta[b].iterative && meta[b].nsys <= SMALL_LU_MAX) return;
+  if (qp_route(meta[b].iterative, meta[b].nsys, fast_max) == ROUTE_FAST) return;
   double* zs = smem;            // n
   double* ls = zs + n;          // m
   double* ns = ls + m;          // p
@@ -484,10 +483,10 @@ __global__ __launch_bounds__(TPB) void qp_output_kernel(
     const double* __restrict__ x, const double* __restrict__ G,
     const double* __restrict__ s, const int32_t* __restrict__ rpos,
     const QPMeta* __restrict__ meta, const double* __restrict__ full, int n,
-    int m, int p, int nmax, int trans, double* __restrict__ out) {
+    int m, int p, int nmax, int fast_max, int trans, double* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x, t = threadIdx.x;
-  if (!meta[b].iterative && meta[b].nsys <= SMALL_LU_MAX) return;
+  if (qp_route(meta[b].iterative, meta[b].nsys, fast_max) == ROUTE_FAST) return;
   const int nk = meta[b].nk;
   const double* xb = x + (size_t)b * nmax;
   double* ob = out + (size_t)b * (n + m + p);
@@ -520,12 +519,12 @@ static void check_launch() { DOPT_CHECK_HIP(hipGetLastError()); }
 // fast path (qp_fast.hip)
 __global__ void qp_fused_kernel(QPIn, FwdTangents, const double*, int, double*, size_t, double*, int,
                                 int, double*, int32_t*, int32_t*, QPMeta*, double*, double*,
-                                double*, int, int, unsigned long long*);
+                                double*, int, int, unsigned long long*, int);
 __global__ void qp_factor_fast_kernel(QPIn, int, double*, int, int, double*, int32_t*, int32_t*,
-                                      int32_t*, double*, QPMeta*);
+                                      int32_t*, double*, QPMeta*, int);
 __global__ void qp_solve_fast_kernel(QPIn, FwdTangents, const double*, int, const double*, int, int,
                                      const double*, const int32_t*, const int32_t*, const double*,
-                                     const QPMeta*, double*, int, double*);
+                                     const QPMeta*, double*, int, double*, int);
 size_t fast_dyn_lds(int n);
 size_t fast_ws_stride();
 size_t fast_dinv_stride(int nmax);
@@ -568,9 +567,10 @@ void qp_factor(Handle& h) {
     PhaseTimer pt(h, DOPT_PHASE_QP_LU);
     hipLaunchKernelGGL(qp_factor_fast_kernel, dim3(fast_grid(h)), dim3(FAST_THREADS), fast_dyn_lds(h.n), h.stream,
                        qp_inputs(h), B, h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(),
-                       h.kidx.as<int32_t>(), rpos_of(h), perm_of(h), dinv_of(h), meta);
+                       h.kidx.as<int32_t>(), rpos_of(h), perm_of(h), dinv_of(h), meta, h.fast_max);
     check_launch();
-    if (h.nmax > SMALL_LU_MAX) {
+    if (h.nmax > h.fast_max) qp_blocked_factor(h, dinv_of(h));
+    if (h.nmax > BLOCKED_MAX && h.has_generic) {
       hipLaunchKernelGGL(qp_lu_generic_kernel, dim3(B), dim3(TPB), 0, h.stream, h.K.as<double>(),
                          h.ipiv.as<int32_t>(), meta, h.nmax, h.ld);
       check_launch();
@@ -587,7 +587,11 @@ static void fallback_solve_and_output(Handle& h, int trans, double* out) {
   double* rhs = h.rhs.as<double>();
   double* full = rhs + (size_t)B * nmax;
   double* x = h.x.as<double>();
-  if (nmax > SMALL_LU_MAX) {
+  if (nmax > h.fast_max) {
+    PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
+    qp_blocked_solve(h, dinv_of(h), trans, rhs, x);
+  }
+  if (nmax > BLOCKED_MAX && h.has_generic) {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     hipLaunchKernelGGL(qp_solve_kernel, dim3(B), dim3(TPB), (size_t)nmax * sizeof(double), h.stream,
                        h.K.as<double>(), h.ipiv.as<int32_t>(), meta, nmax, ld, trans, rhs, x);
@@ -603,14 +607,14 @@ static void fallback_solve_and_output(Handle& h, int trans, double* out) {
   PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
   hipLaunchKernelGGL(qp_output_kernel, dim3(B), dim3(TPB), (size_t)n * sizeof(double), h.stream,
                      x, m ? h.G : &dummy, h.s.as<double>(), rpos_of(h), meta, full, n, m, p, nmax,
-                     trans, out);
+                     h.fast_max, trans, out);
   check_launch();
 }
 
 static void fallback_rev_rhs(Handle& h, const double* dl_dz) {
   PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
   hipLaunchKernelGGL(qp_rev_rhs_kernel, dim3(h.batch), dim3(TPB), 0, h.stream, dl_dz,
-                     h.meta.as<QPMeta>(), h.n, h.nmax, h.rhs.as<double>());
+                     h.meta.as<QPMeta>(), h.n, h.nmax, h.fast_max, h.rhs.as<double>());
   check_launch();
 }
 
@@ -622,7 +626,8 @@ static void fallback_fwd_rhs(Handle& h, const FwdTangents& T) {
   PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
   hipLaunchKernelGGL(qp_fwd_rhs_kernel, dim3(B), dim3(TPB), (size_t)(2 * n + 2 * m + 2 * p) * sizeof(double),
                      h.stream, T.dQ, T.dq, T.dG, T.dh, T.dA, T.db, h.z, m ? h.lam : &dummy,
-                     p ? h.nu : &dummy, rpos_of(h), h.meta.as<QPMeta>(), n, m, p, h.nmax, full, rhs);
+                     p ? h.nu : &dummy, rpos_of(h), h.meta.as<QPMeta>(), n, m, p, h.nmax, h.fast_max,
+                     full, rhs);
   check_launch();
 }
 
@@ -647,7 +652,7 @@ void qp_reverse(Handle& h, const double* dl_dz, double* out) {
     hipLaunchKernelGGL(qp_solve_fast_kernel, dim3(fast_grid(h)), dim3(FAST_THREADS), 0, h.stream, qp_inputs(h),
                        tangents(h, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr), dl_dz, B,
                        h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(), rpos_of(h), perm_of(h),
-                       dinv_of(h), h.meta.as<QPMeta>(), full, 0, out);
+                       dinv_of(h), h.meta.as<QPMeta>(), full, 0, out, h.fast_max);
     check_launch();
   }
   fallback_rev_rhs(h, dl_dz);
@@ -664,7 +669,8 @@ void qp_forward(Handle& h, const double* dQ, const double* dq, const double* dG,
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     hipLaunchKernelGGL(qp_solve_fast_kernel, dim3(fast_grid(h)), dim3(FAST_THREADS), 0, h.stream, qp_inputs(h),
                        T, (const double*)nullptr, B, h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(),
-                       rpos_of(h), perm_of(h), dinv_of(h), h.meta.as<QPMeta>(), full, 1, out);
+                       rpos_of(h), perm_of(h), dinv_of(h), h.meta.as<QPMeta>(), full, 1, out,
+                       h.fast_max);
     check_launch();
   }
   fallback_fwd_rhs(h, T);
@@ -686,11 +692,15 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
     hipLaunchKernelGGL(qp_fused_kernel, dim3(grid), dim3(FAST_THREADS), fast_dyn_lds(h.n), h.stream,
                        qp_inputs(h), T, dl_dz, B, h.ws.as<double>(), ws_stride, h.K.as<double>(), h.ld,
                        h.nmax, h.s.as<double>(), h.kidx.as<int32_t>(), rpos_of(h), h.meta.as<QPMeta>(),
-                       full, out_rev, out_fwd, 1, 1, h.stamps.as<unsigned long long>());
+                       full, out_rev, out_fwd, 1, 1, h.stamps.as<unsigned long long>(), h.fast_max);
     check_launch();
   }
   // fallback problems were prepared + assembled by the fused kernel
-  if (h.nmax > SMALL_LU_MAX) {
+  if (h.nmax > h.fast_max) {
+    PhaseTimer pt(h, DOPT_PHASE_QP_LU);
+    qp_blocked_factor(h, dinv_of(h));
+  }
+  if (h.nmax > BLOCKED_MAX && h.has_generic) {
     PhaseTimer pt(h, DOPT_PHASE_QP_LU);
     hipLaunchKernelGGL(qp_lu_generic_kernel, dim3(B), dim3(TPB), 0, h.stream, h.K.as<double>(),
                        h.ipiv.as<int32_t>(), h.meta.as<QPMeta>(), h.nmax, h.ld);

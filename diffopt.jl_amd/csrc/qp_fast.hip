@@ -712,7 +712,7 @@ __global__ __launch_bounds__(FT) void qp_fused_kernel(
     size_t ws_stride, double* __restrict__ Kper, int ld_per, int nmax, double* __restrict__ s,
     int32_t* __restrict__ kidx, int32_t* __restrict__ rpos, QPMeta* __restrict__ meta,
     double* __restrict__ full, double* __restrict__ out_rev, double* __restrict__ out_fwd,
-    int do_rev, int do_fwd, unsigned long long* __restrict__ stamps) {
+    int do_rev, int do_fwd, unsigned long long* __restrict__ stamps, int fast_max) {
   __shared__ FastLDS S;
   extern __shared__ __attribute__((aligned(16))) double zsm[];
   __shared__ int cnt[NW + 1];
@@ -729,7 +729,7 @@ __global__ __launch_bounds__(FT) void qp_fused_kernel(
     st.mark(0);
     const int nk = meta[b].nk;
     const int N = P.n + nk + P.p;
-    if (it || N > FAST_MAX) {
+    if (it || N > fast_max) {
       assemble_wg(P, b, s, kidx, nk, Kper + (size_t)b * nmax * ld_per, ld_per, S);
       continue;
     }
@@ -761,7 +761,7 @@ __global__ __launch_bounds__(FT) void qp_fused_kernel(
 __global__ __launch_bounds__(FT) void qp_factor_fast_kernel(
     QPIn P, int B, double* __restrict__ Kper, int ld_per, int nmax, double* __restrict__ s,
     int32_t* __restrict__ kidx, int32_t* __restrict__ rpos, int32_t* __restrict__ perm_out,
-    double* __restrict__ dinv, QPMeta* __restrict__ meta) {
+    double* __restrict__ dinv, QPMeta* __restrict__ meta, int fast_max) {
   __shared__ FastLDS S;
   extern __shared__ __attribute__((aligned(16))) double zsm[];
   __shared__ int cnt[NW + 1];
@@ -772,7 +772,7 @@ __global__ __launch_bounds__(FT) void qp_factor_fast_kernel(
     const int N = P.n + nk + P.p;
     double* Kb = Kper + (size_t)b * nmax * ld_per;
     assemble_wg(P, b, s, kidx, nk, Kb, ld_per, S);
-    if (it || N > FAST_MAX) continue;
+    if (it || N > fast_max) continue;
     Stamp st;
     st.acc = nullptr;
     const int Np = (N + FNB - 1) & ~(FNB - 1);
@@ -788,13 +788,13 @@ __global__ __launch_bounds__(FT) void qp_solve_fast_kernel(
     const double* __restrict__ Kper, int ld_per, int nmax, const double* __restrict__ s,
     const int32_t* __restrict__ rpos, const int32_t* __restrict__ perm_in,
     const double* __restrict__ dinv, const QPMeta* __restrict__ meta, double* __restrict__ full,
-    int trans, double* __restrict__ out) {
+    int trans, double* __restrict__ out, int fast_max) {
   __shared__ FastLDS S;
   const size_t dstride = (size_t)((nmax + FNB - 1) / FNB) * DINV_STRIDE;
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
     const int nk = meta[b].nk;
     const int N = P.n + nk + P.p;
-    if (meta[b].iterative || N > FAST_MAX) continue;
+    if (meta[b].iterative || N > fast_max) continue;
     const double* Kb = Kper + (size_t)b * nmax * ld_per;
     const int Np = (N + FNB - 1) & ~(FNB - 1);
     for (int i = threadIdx.x; i < Np; i += FT) S.perm[i] = perm_in[(size_t)b * nmax + i];

@@ -33,6 +33,7 @@ SIGNATURES = {
     "dopt_last_error": (ctypes.c_char_p, [_h]),
     "dopt_set_stream": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_set_memory": (ctypes.c_int, [_h, ctypes.c_int32]),
+    "dopt_set_qp_fast_max": (ctypes.c_int, [_h, ctypes.c_int32]),
     "dopt_qp_set": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 7),
     "dopt_qp_factor": (ctypes.c_int, [_h]),
     "dopt_qp_reverse": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_void_p]),

@@ -146,6 +146,11 @@ class QPBatch:
     def last_time(self):
         return self.lib.dopt_last_time(self.h)
 
+    def set_fast_max(self, fast_max):
+        """Reduced KKT sizes ≤ fast_max (0..512) use the fused per-problem
+        kernel, larger ones the blocked step path (dopt_set_qp_fast_max)."""
+        _lib.check(self.lib.dopt_set_qp_fast_max(self.h, int(fast_max)), self.h)
+
     def set_profiling(self, on=True):
         _lib.check(self.lib.dopt_set_profiling(self.h, int(bool(on))), self.h)
 

@@ -74,6 +74,13 @@ int dopt_abi_version(void);
  * stream) so the engine's kernels are ordered after that work. */
 int dopt_set_stream(dopt_handle* h, void* stream);
 int dopt_set_memory(dopt_handle* h, int32_t mem);
+/* QP factorisation path threshold: problems whose reduced KKT size is
+ * ≤ fast_max (0..512, default 512, env DOPT_FAST_MAX) use the fused
+ * one-workgroup-per-problem kernel; larger ones (≤ 1536) the blocked step
+ * path that spreads each LU over the whole GPU; beyond that a generic kernel.
+ * Results agree to rounding; this is a performance setting (no reference
+ * counterpart — the reference always calls UMFPACK, QuadraticProgram.jl:490). */
+int dopt_set_qp_fast_max(dopt_handle* h, int32_t fast_max);
 
 /* ---- QuadraticProgram ------------------------------------------------------
  * Problem data + primal-dual point.  Replaces `_gradient_cache`'s inputs

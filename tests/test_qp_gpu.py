@@ -89,11 +89,13 @@ def _synthetic(batch, n, m, p, phi, seed, dense=False):
     return qp_numpy(batch, n, m, p, phi, seed, dense_tangents=dense)
 
 
-def _check_batch(QPBatch, d, dense=False):
+def _check_batch(QPBatch, d, dense=False, fast_max=None):
     B, n = d["z"].shape
     m = d["lam"].shape[1]
     p = d["nu"].shape[1]
     e = QPBatch(B, n, m, p)
+    if fast_max is not None:
+        e.set_fast_max(fast_max)
     e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
     fkw = dict(dq=d["dq"], dh=d["dh"], db=d["db"])
     if dense:
@@ -128,9 +130,52 @@ def test_dense_tangents(QPBatch):
     _check_batch(QPBatch, _synthetic(3, 40, 60, 10, 0.5, 7, dense=True), dense=True)
 
 
-def test_generic_large_system_path(QPBatch):
-    """Reduced system > 512 unknowns takes the generic LU kernel."""
+def test_blocked_path_mid_size(QPBatch):
+    """Reduced system 512 < N' ≤ 1536 (here 560) takes the blocked step path
+    (panel / U12 / MFMA trailing-update launches over the whole batch)."""
     _check_batch(QPBatch, _synthetic(2, 300, 400, 20, 0.6, 11))
+
+
+def test_blocked_path_cfg3_shape(QPBatch):
+    """BASELINE config 3 shape (n=1000, m=1500, 30 % active ⇒ N' = 1450, three
+    panel rows per thread) at batch 2."""
+    _check_batch(QPBatch, _synthetic(2, 1000, 1500, 0, 0.3, 20250310))
+
+
+def test_blocked_path_forced_small_and_ragged(QPBatch):
+    """fast_max = 0 forces every LU problem onto the blocked path: config-1/2
+    shapes and ragged sizes (p = 0, m = 0, N' not a multiple of 32)."""
+    _check_batch(QPBatch, _synthetic(3, 200, 300, 0, 0.3, 20250309), fast_max=0)
+    _check_batch(QPBatch, _synthetic(3, 50, 80, 30, 0.2, 20250308), fast_max=0)
+    for (n, m, p) in [(1, 1, 0), (3, 0, 0), (7, 3, 0), (33, 31, 1), (64, 1, 63)]:
+        _check_batch(QPBatch, _synthetic(2, n, m, p, 0.5, 100 + n), fast_max=0)
+
+
+def test_blocked_matches_fused_and_split(QPBatch):
+    """Same batch through the fused kernel and the blocked path: agreement to
+    rounding (different accumulation order only); blocked split calls
+    (factor → reverse → forward) bit-equal to the blocked fused call."""
+    d = _synthetic(4, 120, 200, 10, 0.4, 21)
+    B, n = d["z"].shape
+    e1 = QPBatch(B, n, 200, 10)
+    e1.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    r1, f1 = e1.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
+    e2 = QPBatch(B, n, 200, 10)
+    e2.set_fast_max(0)
+    e2.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    r2, f2 = e2.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
+    for a, b in ((r1, r2), (f1, f2)):
+        assert max(relfro(a[i], b[i]) for i in range(B)) <= 1e-11
+    e2.factor()
+    r3 = e2.reverse(d["dl_dz"])
+    f3 = e2.forward(dq=d["dq"], dh=d["dh"], db=d["db"])
+    np.testing.assert_array_equal(r2, r3)
+    np.testing.assert_array_equal(f2, f3)
+
+
+def test_generic_large_system_path(QPBatch):
+    """Reduced system > 1536 unknowns takes the generic LU kernel."""
+    _check_batch(QPBatch, _synthetic(2, 1200, 700, 0, 0.6, 12))
 
 
 def test_ragged_shapes(QPBatch):
@@ -151,8 +196,10 @@ def test_reverse_forward_separately_equal_fused(QPBatch):
     np.testing.assert_array_equal(f1, f2)
 
 
-def test_singular_kkt_raises(QPBatch):
-    """λ_i == 0 and s_i == 0 → zero row/column in LHS → SingularException."""
+@pytest.mark.parametrize("fast_max", [512, 0])
+def test_singular_kkt_raises(QPBatch, fast_max):
+    """λ_i == 0 and s_i == 0 → zero row/column in LHS → SingularException
+    (fused path and blocked path)."""
     from diffopt_amd import SingularException
     Q = np.eye(2)[None]
     G = np.array([[[1.0, 0.0]]])
@@ -160,6 +207,7 @@ def test_singular_kkt_raises(QPBatch):
     h = np.array([1.0])[None]           # s = Gz − h = 0
     lam = np.zeros((1, 1))
     e = QPBatch(1, 2, 1, 0)
+    e.set_fast_max(fast_max)
     e.set(Q, G, h, np.zeros((1, 0, 2)), z, lam, np.zeros((1, 0)))
     with pytest.raises(SingularException):
         e.reverse(np.ones((1, 2)))
