@@ -180,6 +180,8 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
 // per-problem K / perm (ipiv) / dinv buffers the assembly filled
 void qp_blocked_factor(Handle& h, double* dinv);
 void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rhs, double* x);
+void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, const double* rhs_fwd,
+                       double* x_rev, double* x_fwd);
 void conic_factor(Handle& h);
 void conic_forward(Handle& h, const double* dA, const double* db, const double* dc,
                    double* out, double* out_dx);

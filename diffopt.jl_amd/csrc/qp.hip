@@ -579,18 +579,24 @@ void qp_factor(Handle& h) {
   h.factored = true;
 }
 
-// fallback problems (iterative branch, or reduced size > FAST_MAX)
-static void fallback_solve_and_output(Handle& h, int trans, double* out) {
+// Per-direction work buffers of the non-fused problems (trans 0 = reverse,
+// 1 = forward): reduced RHS, solution, and the full-length forward RHS.
+static double* rhs_of(Handle& h, int trans) {
+  return h.rhs.as<double>() + (size_t)(trans ? 2 : 0) * h.batch * h.nmax;
+}
+static double* full_of(Handle& h) { return h.rhs.as<double>() + (size_t)h.batch * h.nmax; }
+static double* x_of(Handle& h, int trans) {
+  return h.x.as<double>() + (size_t)(trans ? 1 : 0) * h.batch * h.nmax;
+}
+
+// generic solves, LSQR and output recovery of the non-fused problems for one
+// direction (the blocked solves are launched by the callers)
+static void fallback_finish(Handle& h, int trans, double* out) {
   const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
   const int nmax = h.nmax, ld = h.ld;
   QPMeta* meta = h.meta.as<QPMeta>();
-  double* rhs = h.rhs.as<double>();
-  double* full = rhs + (size_t)B * nmax;
-  double* x = h.x.as<double>();
-  if (nmax > h.fast_max) {
-    PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
-    qp_blocked_solve(h, dinv_of(h), trans, rhs, x);
-  }
+  double* rhs = rhs_of(h, trans);
+  double* x = x_of(h, trans);
   if (nmax > BLOCKED_MAX && h.has_generic) {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     hipLaunchKernelGGL(qp_solve_kernel, dim3(B), dim3(TPB), (size_t)nmax * sizeof(double), h.stream,
@@ -606,29 +612,33 @@ static void fallback_solve_and_output(Handle& h, int trans, double* out) {
   static const double dummy = 0.0;
   PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
   hipLaunchKernelGGL(qp_output_kernel, dim3(B), dim3(TPB), (size_t)n * sizeof(double), h.stream,
-                     x, m ? h.G : &dummy, h.s.as<double>(), rpos_of(h), meta, full, n, m, p, nmax,
-                     h.fast_max, trans, out);
+                     x, m ? h.G : &dummy, h.s.as<double>(), rpos_of(h), meta, full_of(h), n, m, p,
+                     nmax, h.fast_max, trans, out);
   check_launch();
 }
 
 static void fallback_rev_rhs(Handle& h, const double* dl_dz) {
   PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
   hipLaunchKernelGGL(qp_rev_rhs_kernel, dim3(h.batch), dim3(TPB), 0, h.stream, dl_dz,
-                     h.meta.as<QPMeta>(), h.n, h.nmax, h.fast_max, h.rhs.as<double>());
+                     h.meta.as<QPMeta>(), h.n, h.nmax, h.fast_max, rhs_of(h, 0));
   check_launch();
 }
 
 static void fallback_fwd_rhs(Handle& h, const FwdTangents& T) {
   const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
-  double* rhs = h.rhs.as<double>();
-  double* full = rhs + (size_t)B * h.nmax;
   static const double dummy = 0.0;
   PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
   hipLaunchKernelGGL(qp_fwd_rhs_kernel, dim3(B), dim3(TPB), (size_t)(2 * n + 2 * m + 2 * p) * sizeof(double),
                      h.stream, T.dQ, T.dq, T.dG, T.dh, T.dA, T.db, h.z, m ? h.lam : &dummy,
                      p ? h.nu : &dummy, rpos_of(h), h.meta.as<QPMeta>(), n, m, p, h.nmax, h.fast_max,
-                     full, rhs);
+                     full_of(h), rhs_of(h, 1));
   check_launch();
+}
+
+static void blocked_solve(Handle& h, int trans) {
+  if (h.nmax <= h.fast_max) return;
+  PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
+  qp_blocked_solve(h, dinv_of(h), trans, rhs_of(h, trans), x_of(h, trans));
 }
 
 static FwdTangents tangents(Handle& h, const double* dQ, const double* dq, const double* dG,
@@ -646,7 +656,7 @@ static FwdTangents tangents(Handle& h, const double* dQ, const double* dq, const
 void qp_reverse(Handle& h, const double* dl_dz, double* out) {
   if (!h.factored) qp_factor(h);
   const int B = (int)h.batch;
-  double* full = h.rhs.as<double>() + (size_t)B * h.nmax;
+  double* full = full_of(h);
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     hipLaunchKernelGGL(qp_solve_fast_kernel, dim3(fast_grid(h)), dim3(FAST_THREADS), 0, h.stream, qp_inputs(h),
@@ -656,14 +666,15 @@ void qp_reverse(Handle& h, const double* dl_dz, double* out) {
     check_launch();
   }
   fallback_rev_rhs(h, dl_dz);
-  fallback_solve_and_output(h, 0, out);
+  blocked_solve(h, 0);
+  fallback_finish(h, 0, out);
 }
 
 void qp_forward(Handle& h, const double* dQ, const double* dq, const double* dG,
                 const double* dh, const double* dA, const double* db, double* out) {
   if (!h.factored) qp_factor(h);
   const int B = (int)h.batch;
-  double* full = h.rhs.as<double>() + (size_t)B * h.nmax;
+  double* full = full_of(h);
   const FwdTangents T = tangents(h, dQ, dq, dG, dh, dA, db);
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
@@ -674,7 +685,8 @@ void qp_forward(Handle& h, const double* dQ, const double* dq, const double* dG,
     check_launch();
   }
   fallback_fwd_rhs(h, T);
-  fallback_solve_and_output(h, 1, out);
+  blocked_solve(h, 1);
+  fallback_finish(h, 1, out);
 }
 
 void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
@@ -685,7 +697,7 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
   const int grid = fast_grid(h);
   const size_t ws_stride = fast_ws_stride();
   h.ws.ensure((size_t)grid * ws_stride * sizeof(double));
-  double* full = h.rhs.as<double>() + (size_t)B * h.nmax;
+  double* full = full_of(h);
   const FwdTangents T = tangents(h, dQ, dq, dG, dh, dA, db);
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_FUSED);
@@ -707,9 +719,13 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
     check_launch();
   }
   fallback_rev_rhs(h, dl_dz);
-  fallback_solve_and_output(h, 0, out_rev);
   fallback_fwd_rhs(h, T);
-  fallback_solve_and_output(h, 1, out_fwd);
+  if (h.nmax > h.fast_max) {   // both directions of the blocked problems in one pass
+    PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
+    qp_blocked_solve2(h, dinv_of(h), rhs_of(h, 0), rhs_of(h, 1), x_of(h, 0), x_of(h, 1));
+  }
+  fallback_finish(h, 0, out_rev);
+  fallback_finish(h, 1, out_fwd);
   h.factored = false;   // the fused path leaves no reusable factorisation
 }
 

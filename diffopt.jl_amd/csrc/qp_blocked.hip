@@ -6,8 +6,8 @@
 //
 //   panel   (1 WG / problem)        partial-pivot LU of the R × 32 panel held in
 //                                   registers (RPT rows per thread), pivoting by
-//                                   relabelling (perm), L11⁻¹ / U11⁻¹ → dinv
-//   u12     (WG per 64 columns)     U12 = L11⁻¹ · A12 on v_mfma_f64_16x16x4f64
+//                                   relabelling (perm), L11⁻¹ / U11⁻¹ → dinv,
+//                                   then U12 = L11⁻¹ · A12 on v_mfma_f64_16x16x4f64
 //   update  (WG per 64×64 tile)     A22 −= L21 · U12 (MFMA; U12 tile staged in
 //                                   LDS), XCD-aware tile order so one problem's
 //                                   tiles share an L2
@@ -32,37 +32,54 @@ typedef double d4b __attribute__((ext_vector_type(4)));
 constexpr int BNB = 32;                  // panel width
 constexpr int BLP = BNB + 1;             // padded LDS row of a 32×32 block
 constexpr int BDINV = 2 * BNB * BNB;     // doubles per panel in dinv (L11⁻¹ | U11⁻¹)
-constexpr int PT = 512;                  // panel / solve workgroup size
-constexpr int PNW = PT / 64;
+constexpr int PT = 512;                  // solve workgroup size
 
 __device__ __forceinline__ d4b bmfma(double a, double b, d4b c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// wave argmax of (key, idx): max key, ties → smallest idx (LAPACK idamax)
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ void bamax_step(long long& key, int& idx) {
-  const int lo = (int)(unsigned long long)key, hi = (int)((unsigned long long)key >> 32);
-  const int olo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROWMASK, 0xF, false);
-  const int ohi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROWMASK, 0xF, false);
-  const int oi = __builtin_amdgcn_update_dpp(idx, idx, CTRL, ROWMASK, 0xF, false);
-  const long long ok = (long long)(((unsigned long long)(unsigned)ohi << 32) | (unsigned)olo);
-  const bool take = ok > key || (ok == key && oi < idx);
-  key = take ? ok : key;
-  idx = take ? oi : idx;
-}
+// diagnostic phase stamps (thread 0, s_memtime), accumulated per slot when
+// `stamps` is non-null (env DOPT_STAMPS=1, read with dopt_debug_stamps)
+struct BStamp {
+  unsigned long long* acc;
+  unsigned long long last;
+  __device__ __forceinline__ void start() {
+    if (acc && threadIdx.x == 0) last = __builtin_amdgcn_s_memtime();
+  }
+  __device__ __forceinline__ void mark(int k) {
+    if (acc && threadIdx.x == 0) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      atomicAdd(&acc[k], now - last);
+      last = now;
+    }
+  }
+};
 
-__device__ __forceinline__ void bwave_argmax(long long& key, int& idx) {
-  bamax_step<0xB1, 0xF>(key, idx);    // quad_perm [1,0,3,2]
-  bamax_step<0x4E, 0xF>(key, idx);    // quad_perm [2,3,0,1]
-  bamax_step<0x141, 0xF>(key, idx);   // row_half_mirror
-  bamax_step<0x140, 0xF>(key, idx);   // row_mirror
-  bamax_step<0x142, 0xA>(key, idx);   // row_bcast:15
-  bamax_step<0x143, 0xC>(key, idx);   // row_bcast:31
-  const int lo = __builtin_amdgcn_readlane((int)(unsigned long long)key, 63);
-  const int hi = __builtin_amdgcn_readlane((int)((unsigned long long)key >> 32), 63);
-  idx = __builtin_amdgcn_readlane(idx, 63);
-  key = (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+// wave max of a double (DPP butterfly within rows, row_bcast across rows,
+// result broadcast from lane 63)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp((int)b, (int)b, CTRL, ROWMASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), CTRL, ROWMASK, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double wave_max_f64(double v) {
+  v = fmax(v, dpp_f64<0xB1, 0xF>(v));    // quad_perm [1,0,3,2]
+  v = fmax(v, dpp_f64<0x4E, 0xF>(v));    // quad_perm [2,3,0,1]
+  v = fmax(v, dpp_f64<0x141, 0xF>(v));   // row_half_mirror
+  v = fmax(v, dpp_f64<0x140, 0xF>(v));   // row_mirror
+  v = fmax(v, dpp_f64<0x142, 0xA>(v));   // row_bcast:15
+  v = fmax(v, dpp_f64<0x143, 0xC>(v));   // row_bcast:31
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, 63);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ int wave_min_i32(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+  return v;
 }
 
 __device__ __forceinline__ int blocked_np(const QPMeta& mm, int fast_max) {
@@ -72,20 +89,23 @@ __device__ __forceinline__ int blocked_np(const QPMeta& mm, int fast_max) {
 
 // ---------------------------------------------------------------------------
 // Panel: logical rows c0 .. Np−1, columns c0 .. c0+31.  Thread t owns local
-// rows t + PT·q (q < RPT) in a rotating register window (r[q][c] holds panel
+// rows t + TPB·q (q < RPT) in a rotating register window (r[q][c] holds panel
 // column (j + c) mod 32 at column step j), exactly the scheme of qp_fast.hip's
 // lu_fast, generalised to several rows per thread.  Two barriers per column.
 // ---------------------------------------------------------------------------
-template <int RPT>
-__global__ __launch_bounds__(PT) void blu_panel_kernel(double* __restrict__ K, int ld, int nmax,
+template <int TPB, int RPT>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void blu_panel_kernel(double* __restrict__ K, int ld, int nmax,
                                                        int32_t* __restrict__ perm,
                                                        double* __restrict__ dinv, size_t dstride,
                                                        QPMeta* __restrict__ meta, int c0,
-                                                       int fast_max) {
-  __shared__ long long ckey[PNW];
-  __shared__ int cpos[PNW];
-  __shared__ double prow[BNB];
+                                                       int fast_max, int corr,
+                                                       unsigned long long* __restrict__ stamps) {
+  constexpr int TW = TPB / 64;   // waves
+  __shared__ double slot_val[2][TW];
+  __shared__ int slot_pos[2][TW];
+  __shared__ __attribute__((aligned(16))) double slot_row[2][TW][BNB];
   __shared__ double Lt[BNB * BLP], Linv[BNB * BLP], Uinv[BNB * BLP];
+  __shared__ int ptop[BNB];
   const int b = blockIdx.x;
   const QPMeta mm = meta[b];
   const int Np = blocked_np(mm, fast_max);
@@ -94,12 +114,15 @@ __global__ __launch_bounds__(PT) void blu_panel_kernel(double* __restrict__ K, i
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   double* Kb = K + (size_t)b * nmax * ld;
   int32_t* pb = perm + (size_t)b * nmax;
+  BStamp st;
+  st.acc = stamps;
+  st.start();
 
   int phys[RPT], pos[RPT];
   double r[RPT][BNB];
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
-    const int li = t + PT * q;
+    const int li = t + TPB * q;
     const bool own = li < R;
     phys[q] = own ? (c0 == 0 ? li : pb[c0 + li]) : 0;
     pos[q] = own ? li : -1;
@@ -114,57 +137,107 @@ __global__ __launch_bounds__(PT) void blu_panel_kernel(double* __restrict__ K, i
     }
   }
   int info = 0;
+  if (stamps) {
+    __syncthreads();   // diagnostic: attribute the panel load to slot 0
+    st.mark(0);
+  }
+  // One barrier per column: every wave publishes its best candidate (|a| as a
+  // double, logical position, and the candidate's rotated row) to a
+  // double-buffered slot; after the barrier every thread folds the TW slots
+  // and reads the winner's row.  A wave runs at most one column ahead of the
+  // slowest (the next barrier), so two buffers suffice.
+  // Pivot rule (LAPACK idamax): max |a|, ties → smallest logical position.
 #pragma unroll 1
   for (int j = 0; j < BNB; ++j) {
-    long long key = -1LL;
-    int bi = 0x7fffffff;
+    const int buf = j & 1;
+    double av = -1.0;    // −1: no candidate
+    int ap = 0x7fffffff;
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
-      const long long k = pos[q] >= j ? __double_as_longlong(fabs(r[q][0])) : -1LL;
-      const bool take = k > key || (k == key && pos[q] < bi);
-      key = take ? k : key;
-      bi = take ? pos[q] : bi;
+      const double a = pos[q] >= j ? fabs(r[q][0]) : -1.0;
+      const bool take = a > av || (a == av && pos[q] < ap);
+      av = take ? a : av;
+      ap = take ? pos[q] : ap;
     }
-    bwave_argmax(key, bi);
+    const double wmax = wave_max_f64(av);
+    const unsigned long long tied = __ballot(av == wmax);
+    int wpos;
+    if (__popcll(tied) == 1) {
+      wpos = __builtin_amdgcn_readlane(ap, __ffsll((long long)tied) - 1);
+    } else {   // exact tie in |a| (or no candidate at all): smallest position
+      wpos = wave_min_i32(av == wmax ? ap : 0x7fffffff);
+    }
     if (lane == 0) {
-      ckey[wv] = key;
-      cpos[wv] = bi;
-    }
-    __syncthreads();
-    key = ckey[0];
-    bi = cpos[0];
-#pragma unroll
-    for (int w = 1; w < PNW; ++w) {
-      const long long k = ckey[w];
-      const int p = cpos[w];
-      const bool take = k > key || (k == key && p < bi);
-      key = take ? k : key;
-      bi = take ? p : bi;
+      slot_val[buf][wv] = wmax;
+      slot_pos[buf][wv] = wpos;
     }
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
-      if (pos[q] == bi) {
-        // columns < j (rotated to the tail) are published as 0: no masking below
+      if (pos[q] == wpos) {
+        double* dst = slot_row[buf][wv];
 #pragma unroll
-        for (int c = 0; c < BNB; ++c) prow[c] = (c < BNB - j) ? r[q][c] : 0.0;
+        for (int c = 0; c < BNB; ++c) dst[c] = r[q][c];
       }
-      pos[q] = (pos[q] == bi) ? j : ((pos[q] == j) ? bi : pos[q]);
     }
+    // columns < j sit rotated at the tail [32−j, 32): publish them as 0 so the
+    // elimination below needs no masking (same wave ⇒ ordered after the row)
+    if (wpos != 0x7fffffff && lane >= BNB - j && lane < BNB) slot_row[buf][wv][lane] = 0.0;
     __syncthreads();
+    double sv[TW];
+    int sp[TW];
+#pragma unroll
+    for (int w = 0; w < TW; ++w) {   // all slot reads issued before the fold
+      sv[w] = slot_val[buf][w];
+      sp[w] = slot_pos[buf][w];
+    }
+    double bv = sv[0];
+    int bi = sp[0];
+    int ww = 0;
+#pragma unroll
+    for (int w = 1; w < TW; ++w) {
+      const bool take = (sv[w] > bv) | ((sv[w] == bv) & (sp[w] < bi));
+      bv = take ? sv[w] : bv;
+      bi = take ? sp[w] : bi;
+      ww = take ? w : ww;
+    }
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) pos[q] = (pos[q] == bi) ? j : ((pos[q] == j) ? bi : pos[q]);
+    const double* prow = slot_row[buf][ww];
     const double pv = prow[0];
     info = (pv == 0.0 && info == 0) ? c0 + j + 1 : info;
+    // LAPACK dgetf2: scale by the reciprocal unless |pivot| < sfmin
+    const bool use_rcp = fabs(pv) >= 2.2250738585072014e-308;
+    const double rcp = 1.0 / pv;
+    double le[RPT], r0[RPT];
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       const bool below = pos[q] > j && pv != 0.0;
-      const double r0 = r[q][0];
-      const double l = r0 / pv;
-      const double le = below ? l : 0.0;   // 0: row unchanged (fma(−0, p, v) = v)
-#pragma unroll
-      for (int c = 0; c < BNB - 1; ++c) r[q][c] = fma(-le, prow[c + 1], r[q][c + 1]);
-      r[q][BNB - 1] = below ? l : r0;
+      r0[q] = r[q][0];
+      const double l = use_rcp ? r0[q] * rcp : r0[q] / pv;
+      le[q] = below ? -l : 0.0;    // 0: row unchanged (fma(−0, p, v) = v)
+      r0[q] = below ? l : r0[q];   // rotated-in tail: multiplier (below) or the old entry
     }
+    // pivot row consumed in chunks of 8 columns; the compiler barrier keeps the
+    // LDS reads of later chunks from being hoisted (register pressure: the
+    // rows, not the pivot row, must own the VGPRs)
+#pragma unroll
+    for (int c8 = 0; c8 < BNB; c8 += 8) {
+      double pr[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) pr[u] = (c8 + u + 1 < BNB) ? prow[c8 + u + 1] : 0.0;
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (c8 + u < BNB - 1) r[q][c8 + u] = fma(le[q], pr[u], r[q][c8 + u + 1]);
+      }
+      asm volatile("" ::: "memory");
+    }
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) r[q][BNB - 1] = r0[q];
   }
   __syncthreads();   // every thread has read its perm entries
+  st.mark(1);
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
     if (pos[q] >= 0) {
@@ -173,124 +246,177 @@ __global__ __launch_bounds__(PT) void blu_panel_kernel(double* __restrict__ K, i
       for (int c = 0; c < BNB; ++c) dst[c] = r[q][c];
       pb[c0 + pos[q]] = phys[q];
       if (pos[q] < BNB) {
+        ptop[pos[q]] = phys[q];
 #pragma unroll
         for (int c = 0; c < BNB; ++c) Lt[pos[q] * BLP + c] = r[q][c];
       }
     }
   }
   __syncthreads();
-  if (wv == 0 && lane < BNB) {            // L11⁻¹ (unit lower), one column per lane
+  st.mark(2);
+  // U12 = L11⁻¹·A12 over 16-column tiles of the trailing columns, wave-strided;
+  // the first tile's A12 strip is loaded before the inverses so its latency
+  // overlaps them.  Each wave overwrites only the strip it read.
+  const int g = lane >> 4, l16 = lane & 15;
+  const int ntile = (R - BNB) >> 4;
+  size_t ro[BNB / 4];
+#pragma unroll
+  for (int s = 0; s < BNB / 4; ++s) ro[s] = (size_t)ptop[4 * s + g] * ld;
+  double bv[BNB / 4];
+  if (wv < ntile) {
+#pragma unroll
+    for (int s = 0; s < BNB / 4; ++s) bv[s] = Kb[ro[s] + c0 + BNB + 16 * wv + l16];
+  }
+  // L11⁻¹ (wave 0) and U11⁻¹ (wave 1), one column per lane, right-looking so
+  // the dependency chain is one update deep per column
+  if (wv == 0 && lane < BNB) {
     const int c = lane;
     double x[BNB];
 #pragma unroll
     for (int jj = 0; jj < BNB; ++jj) x[jj] = (jj == c) ? 1.0 : 0.0;
 #pragma unroll
-    for (int jj = 1; jj < BNB; ++jj) {
-      double acc = 0.0;
+    for (int i = 0; i < BNB - 1; ++i) {
 #pragma unroll
-      for (int i = 0; i < jj; ++i) acc = fma(Lt[jj * BLP + i], x[i], acc);
-      if (jj > c) x[jj] = -acc;
+      for (int jj = i + 1; jj < BNB; ++jj) x[jj] = fma(-Lt[jj * BLP + i], x[i], x[jj]);
     }
 #pragma unroll
     for (int jj = 0; jj < BNB; ++jj) Linv[jj * BLP + c] = x[jj];
-  } else if (wv == 1 && lane < BNB) {     // U11⁻¹
+  } else if (wv == 1 && lane < BNB) {
     const int c = lane;
     double x[BNB];
 #pragma unroll
-    for (int jj = BNB - 1; jj >= 0; --jj) {
-      double acc = (jj == c) ? 1.0 : 0.0;
+    for (int jj = 0; jj < BNB; ++jj) x[jj] = (jj == c) ? 1.0 : 0.0;
 #pragma unroll
-      for (int i = jj + 1; i < BNB; ++i) acc = fma(-Lt[jj * BLP + i], x[i], acc);
-      x[jj] = acc / Lt[jj * BLP + jj];
+    for (int jj = BNB - 1; jj >= 0; --jj) {
+      x[jj] = x[jj] / Lt[jj * BLP + jj];
+#pragma unroll
+      for (int i = 0; i < jj; ++i) x[i] = fma(-Lt[i * BLP + jj], x[jj], x[i]);
     }
 #pragma unroll
     for (int jj = 0; jj < BNB; ++jj) Uinv[jj * BLP + c] = x[jj];
   }
   __syncthreads();
+  st.mark(3);
   double* Db = dinv + (size_t)b * dstride + (size_t)(c0 / BNB) * BDINV;
-  for (int i = t; i < BDINV; i += PT) {
+  for (int i = t; i < BDINV; i += TPB) {
     const int e = i & (BNB * BNB - 1);
     Db[i] = ((i < BNB * BNB) ? Linv : Uinv)[(e >> 5) * BLP + (e & 31)];
   }
   if (t == 0 && info != 0 && mm.info == 0) meta[b].info = info;
+  st.mark(4);
+  if (wv >= ntile) return;
+  double a0[BNB / 4], a1[BNB / 4];
+#pragma unroll
+  for (int s = 0; s < BNB / 4; ++s) {
+    a0[s] = Linv[l16 * BLP + 4 * s + g];
+    a1[s] = Linv[(16 + l16) * BLP + 4 * s + g];
+  }
+  int rw[4];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) rw[rr] = ptop[g + 4 * rr];
+  int rw2[4];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) rw2[rr] = ptop[16 + g + 4 * rr];
+  // corr: second panel of a pair — the previous panel's rank-32 update of this
+  // panel's pivot rows in the trailing columns is still pending (the pair's
+  // update is applied to rows ≥ c0+32 only):  A12 −= L21prev(ptop) · U12prev.
+  //   A operand: L21prev rows ptop[l16] / ptop[16+l16], k = columns c0−32+4s+g
+  //   B operand: U12prev rows perm[c0−32+4s+g]
+  double lp0[BNB / 4], lp1[BNB / 4];
+  size_t rp[BNB / 4];
+  if (corr) {
+#pragma unroll
+    for (int s = 0; s < BNB / 4; ++s) {
+      lp0[s] = -Kb[(size_t)ptop[l16] * ld + c0 - BNB + 4 * s + g];
+      lp1[s] = -Kb[(size_t)ptop[16 + l16] * ld + c0 - BNB + 4 * s + g];
+      rp[s] = (size_t)pb[c0 - BNB + 4 * s + g] * ld;
+    }
+  }
+  for (int q = wv; q < ntile; q += TW) {
+    const int colL = c0 + BNB + 16 * q + l16;
+    if (corr) {
+      // A12 rows 4s+g (B layout) = C layout of two 16-row tiles: rows g+4rr
+      // (s = rr) and 16+g+4rr (s = rr+4)
+      double up[BNB / 4];
+#pragma unroll
+      for (int s = 0; s < BNB / 4; ++s) up[s] = Kb[rp[s] + colL];
+      d4b c0v = {bv[0], bv[1], bv[2], bv[3]}, c1v = {bv[4], bv[5], bv[6], bv[7]};
+#pragma unroll
+      for (int s = 0; s < BNB / 4; ++s) {
+        c0v = bmfma(lp0[s], up[s], c0v);
+        c1v = bmfma(lp1[s], up[s], c1v);
+      }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        bv[rr] = c0v[rr];
+        bv[4 + rr] = c1v[rr];
+      }
+    }
+    d4b u0 = {0, 0, 0, 0}, u1 = {0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < BNB / 4; ++s) {
+      u0 = bmfma(a0[s], bv[s], u0);
+      u1 = bmfma(a1[s], bv[s], u1);
+    }
+    const int qn = q + TW;
+    if (qn < ntile) {   // prefetch the next strip before storing this one
+#pragma unroll
+      for (int s = 0; s < BNB / 4; ++s) bv[s] = Kb[ro[s] + c0 + BNB + 16 * qn + l16];
+    }
+    // C layout: row g + 4·rr, column l16 (row k of U12 = logical pivot row c0+k)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      Kb[(size_t)rw[rr] * ld + colL] = u0[rr];
+      Kb[(size_t)rw2[rr] * ld + colL] = u1[rr];
+    }
+  }
+  if (stamps) {
+    __builtin_amdgcn_s_waitcnt(0);
+    st.mark(5);
+  }
 }
 
 // ---------------------------------------------------------------------------
-// U12 = L11⁻¹ · A12 for the pivot rows (logical c0 .. c0+31), 64 columns per
-// workgroup, 16 per wave.  A operand: L11⁻¹ rows from dinv; B operand: the
-// A12 column strip.  Each wave overwrites only the strip it read.
+// Trailing update C −= L·U with inner width KW (32: one panel, 64: a pair of
+// panels — half the C traffic): k = logical columns c0 .. c0+KW−1, rows and
+// columns from c0+KW, columns limited to `cols_max` (the narrow update of the
+// pair's second panel uses 32).  64×64 tiles: wave w owns tile rows
+// 16w..16w+15 × 64 columns (4 MFMA tiles); the KW×64 U tile is staged once in
+// LDS.  1-D grid of nrt·nct·B tiles with an XCD-aware remap: logical tiles of
+// one problem are consecutive, so they run on one XCD and share its L2 for
+// the L and U operands.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void blu_u12_kernel(double* __restrict__ K, int ld, int nmax,
-                                                      const int32_t* __restrict__ perm,
-                                                      const double* __restrict__ dinv,
-                                                      size_t dstride, const QPMeta* __restrict__ meta,
-                                                      int c0, int fast_max) {
-  const int b = blockIdx.y;
-  const int Np = blocked_np(meta[b], fast_max);
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
-  const int col0 = c0 + BNB + blockIdx.x * 64 + 16 * wv;
-  if (col0 >= Np) return;   // wave-uniform; no barriers in this kernel
-  double* Kb = K + (size_t)b * nmax * ld;
-  const int32_t* pb = perm + (size_t)b * nmax;
-  const double* Li = dinv + (size_t)b * dstride + (size_t)(c0 / BNB) * BDINV;
-  const int colL = col0 + l16;
-  size_t ro[BNB / 4];
-#pragma unroll
-  for (int s = 0; s < BNB / 4; ++s) ro[s] = (size_t)pb[c0 + 4 * s + g] * ld;
-  double bv[BNB / 4], a0[BNB / 4], a1[BNB / 4];
-#pragma unroll
-  for (int s = 0; s < BNB / 4; ++s) {
-    bv[s] = Kb[ro[s] + colL];
-    a0[s] = Li[l16 * BNB + 4 * s + g];
-    a1[s] = Li[(16 + l16) * BNB + 4 * s + g];
-  }
-  d4b u0 = {0, 0, 0, 0}, u1 = {0, 0, 0, 0};
-#pragma unroll
-  for (int s = 0; s < BNB / 4; ++s) {
-    u0 = bmfma(a0[s], bv[s], u0);
-    u1 = bmfma(a1[s], bv[s], u1);
-  }
-  // C layout: row g + 4·rr, column l16 (row k of U12 = logical pivot row c0+k)
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    Kb[(size_t)pb[c0 + g + 4 * rr] * ld + colL] = u0[rr];
-    Kb[(size_t)pb[c0 + 16 + g + 4 * rr] * ld + colL] = u1[rr];
-  }
-}
+constexpr int ULD = 64 + 16;   // LDS row stride (doubles) of the staged U tile
 
-// ---------------------------------------------------------------------------
-// A22 −= L21 · U12 over 64×64 tiles of the trailing matrix (logical rows and
-// columns c0+32 .. Np−1).  Wave w owns tile rows 16w..16w+15 × 64 columns
-// (4 MFMA tiles); the U12 32×64 tile is staged once in LDS.  1-D grid of
-// nt²·B tiles with an XCD-aware remap: logical tiles of one problem are
-// consecutive, so they run on one XCD and share its L2 for L21 / U12.
-// ---------------------------------------------------------------------------
-constexpr int ULD = 64 + 16;   // LDS row stride (doubles) of the staged U12 tile
-
+template <int KW>
 __global__ __launch_bounds__(256) void blu_update_kernel(double* __restrict__ K, int ld, int nmax,
                                                          const int32_t* __restrict__ perm,
                                                          const QPMeta* __restrict__ meta, int c0,
-                                                         int fast_max, int nt, int total) {
-  __shared__ double U[BNB * ULD];
+                                                         int fast_max, int cols_max, int nrt,
+                                                         int nct, int total) {
+  __shared__ double U[KW * ULD];
   // bijective XCD remap (blocks L and L+8 share an XCD)
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
   const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
-  const int tiles = nt * nt;
+  const int tiles = nrt * nct;
   const int b = logical / tiles;
   const int tile = logical - b * tiles;
-  const int rt = tile / nt, ct = tile - rt * nt;
+  const int rt = tile / nct, ct = tile - rt * nct;
   const int Np = blocked_np(meta[b], fast_max);
-  const int R2 = Np - c0 - BNB;   // trailing extent (multiple of 32, may be ≤ 0)
-  if (rt * 64 >= R2 || ct * 64 >= R2) return;   // workgroup-uniform
+  const int R2 = Np - c0 - KW;          // trailing rows (multiple of 32, may be ≤ 0)
+  const int C2 = min(R2, cols_max);     // trailing columns updated by this launch
+  if (rt * 64 >= R2 || ct * 64 >= C2) return;   // workgroup-uniform
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
   double* Kb = K + (size_t)b * nmax * ld;
   const int32_t* pb = perm + (size_t)b * nmax;
-  const int cbase = c0 + BNB + ct * 64;
-  {
-    // stage U12[k][cbase .. cbase+63]: thread → (row k, 8 contiguous columns)
-    const int k = t >> 3, c8 = (t & 7) * 8;
-    const bool ok = cbase + c8 < Np;   // 32-aligned halves: all-or-nothing
+  const int cbase = c0 + KW + ct * 64;
+  const int cend = c0 + KW + C2;
+#pragma unroll
+  for (int h = 0; h < KW / 32; ++h) {
+    // stage U[k][cbase .. cbase+63]: thread → (row k, 8 contiguous columns)
+    const int k = 32 * h + (t >> 3), c8 = (t & 7) * 8;
+    const bool ok = cbase + c8 < cend;   // 32-aligned halves: all-or-nothing
     const double* src = Kb + (size_t)pb[c0 + k] * ld + (ok ? cbase + c8 : 0);
     double v[8];
 #pragma unroll
@@ -298,16 +424,16 @@ __global__ __launch_bounds__(256) void blu_update_kernel(double* __restrict__ K,
 #pragma unroll
     for (int u = 0; u < 8; ++u) U[k * ULD + c8 + u] = ok ? v[u] : 0.0;
   }
-  const int rbase = c0 + BNB + rt * 64 + 16 * wv;
+  const int rbase = c0 + KW + rt * 64 + 16 * wv;
   const bool wact = rt * 64 + 16 * wv < R2;   // wave-uniform
-  const int nq = min(4, (R2 - ct * 64) >> 4);
-  double a[BNB / 4];
+  const int nq = min(4, (C2 - ct * 64) >> 4);
+  double a[KW / 4];
   d4b acc[4];
   size_t ro[4];
   if (wact) {
     const double* arow = Kb + (size_t)pb[rbase + l16] * ld + c0;
 #pragma unroll
-    for (int s = 0; s < BNB / 4; ++s) a[s] = -arow[4 * s + g];
+    for (int s = 0; s < KW / 4; ++s) a[s] = -arow[4 * s + g];
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) ro[rr] = (size_t)pb[rbase + g + 4 * rr] * ld;
 #pragma unroll
@@ -320,7 +446,7 @@ __global__ __launch_bounds__(256) void blu_update_kernel(double* __restrict__ K,
   __syncthreads();
   if (!wact) return;
 #pragma unroll
-  for (int s = 0; s < BNB / 4; ++s) {
+  for (int s = 0; s < KW / 4; ++s) {
     double bq[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) bq[q] = U[(4 * s + g) * ULD + 16 * q + l16];
@@ -432,6 +558,100 @@ __global__ __launch_bounds__(PT) void blu_solve_kernel(const double* __restrict_
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// trans = 0 (K x = b): the slices are 32-wide ROW segments, so 8 lanes share
+// a row (4 contiguous doubles each, two 16-B loads) — one wave load touches 8
+// rows' lines instead of 64 — and the 8 partial dots are folded with lane
+// shuffles.  64 rows per pass; up to 8 passes of loads are issued before the
+// block's barrier (taller systems load the remaining passes after it).
+// ---------------------------------------------------------------------------
+constexpr int RPASS = PT / 8;   // rows per pass
+constexpr int RCH = 8;          // passes per load chunk
+
+__global__ __launch_bounds__(PT) void blu_solve_rows_kernel(const double* __restrict__ K, int ld,
+                                                            int nmax,
+                                                            const int32_t* __restrict__ perm,
+                                                            const double* __restrict__ dinv,
+                                                            size_t dstride,
+                                                            const QPMeta* __restrict__ meta,
+                                                            int fast_max,
+                                                            const double* __restrict__ rhs,
+                                                            double* __restrict__ xout) {
+  __shared__ double v[BLOCKED_MAX];
+  __shared__ int ps[BLOCKED_MAX];
+  __shared__ double part[BNB];
+  const int b = blockIdx.x;
+  const QPMeta mm = meta[b];
+  const int Np = blocked_np(mm, fast_max);
+  if (Np == 0) return;
+  const int N = mm.nsys;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int g8 = t & 7, rid = t >> 3;
+  const double* Kb = K + (size_t)b * nmax * ld;
+  const double* Dbase = dinv + (size_t)b * dstride;
+  const double* rb = rhs + (size_t)b * nmax;
+  for (int i = t; i < Np; i += PT) ps[i] = perm[(size_t)b * nmax + i];
+  __syncthreads();
+  for (int i = t; i < Np; i += PT) {
+    const int pr = ps[i];
+    v[i] = pr < N ? rb[pr] : 0.0;   // P b
+  }
+  __syncthreads();
+  const int nblk = Np / BNB;
+  for (int sweep = 0; sweep < 2; ++sweep) {
+    const bool fwd = sweep == 0;
+    for (int s = 0; s < nblk; ++s) {
+      const int bk = fwd ? s : nblk - 1 - s;
+      const int i0 = bk * BNB;
+      const int e0 = fwd ? i0 + BNB : 0;
+      const int ecnt = fwd ? Np - e0 : i0;
+      const int npass = (ecnt + RPASS - 1) / RPASS;
+      double f[RCH][4];
+      auto load_chunk = [&](int c) {
+#pragma unroll
+        for (int p = 0; p < RCH; ++p) {
+          const int li = (c * RCH + p) * RPASS + rid;
+          const int ec = li < ecnt ? e0 + li : i0;   // clamped: a valid row, result unused
+          const double* row = Kb + (size_t)ps[ec] * ld + i0 + 4 * g8;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) f[p][u] = row[u];
+        }
+      };
+      if (npass > 0) load_chunk(0);
+      if (wv == 0 && lane < BNB) {   // x_k = L11⁻¹ v_k (forward) / U11⁻¹ v_k (backward)
+        const double* Dk = Dbase + (size_t)bk * BDINV + (fwd ? 0 : BNB * BNB) + lane * BNB;
+        double acc = 0.0;
+#pragma unroll 8
+        for (int j = 0; j < BNB; ++j) acc = fma(Dk[j], v[i0 + j], acc);
+        part[lane] = acc;
+      }
+      __syncthreads();
+      if (wv == 0 && lane < BNB) v[i0 + lane] = part[lane];
+      double xk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xk[u] = part[4 * g8 + u];
+      for (int c = 0; c * RCH < npass; ++c) {
+        if (c > 0) load_chunk(c);
+#pragma unroll
+        for (int p = 0; p < RCH; ++p) {
+          double d = f[p][0] * xk[0];
+#pragma unroll
+          for (int u = 1; u < 4; ++u) d = fma(f[p][u], xk[u], d);
+          d += __shfl_xor(d, 1);
+          d += __shfl_xor(d, 2);
+          d += __shfl_xor(d, 4);
+          const int li = (c * RCH + p) * RPASS + rid;
+          if (g8 == 0 && li < ecnt) v[e0 + li] -= d;   // rows outside block k only
+        }
+      }
+      __syncthreads();
+    }
+  }
+  double* xb = xout + (size_t)b * nmax;
+  for (int i = t; i < N; i += PT) xb[i] = v[i];
+}
+
 }  // namespace
 
 size_t fast_dinv_stride(int nmax);
@@ -463,30 +683,49 @@ void qp_blocked_factor(Handle& h, double* dinv) {
   double* K = h.K.as<double>();
   int32_t* perm = h.ipiv.as<int32_t>();
   QPMeta* meta = h.meta.as<QPMeta>();
-  for (int c0 = 0; c0 < npmax; c0 += BNB) {
+  // Panels go in pairs (c0, c0+32): panel A; narrow rank-32 update of panel
+  // B's columns; panel B (with the pending rank-32 correction of its pivot
+  // rows' trailing columns); one rank-64 update of everything right of and
+  // below the pair — half the trailing-matrix traffic of rank-32 steps.
+  unsigned long long* st = h.stamps.as<unsigned long long>();
+  auto panel = [&](int c0, int corr) {
+    // workgroup shape by panel height: the per-column pivot overhead (argmax,
+    // publish, fold, reciprocal) is paid once per wave, so short panels use
+    // few waves with several rows per thread (two waves up to 384 rows, four
+    // workgroups per CU), tall panels 8 waves with 2–3 rows per thread
     const int R = npmax - c0;
-    const int rpt = (R + PT - 1) / PT;
-    if (rpt <= 1)
-      hipLaunchKernelGGL(blu_panel_kernel<1>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
-                         dinv, dstride, meta, c0, h.fast_max);
-    else if (rpt == 2)
-      hipLaunchKernelGGL(blu_panel_kernel<2>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
-                         dinv, dstride, meta, c0, h.fast_max);
-    else
-      hipLaunchKernelGGL(blu_panel_kernel<3>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
-                         dinv, dstride, meta, c0, h.fast_max);
+#define DOPT_PANEL(T, Q)                                                                     \
+  hipLaunchKernelGGL((blu_panel_kernel<T, Q>), dim3(B), dim3(T), 0, h.stream, K, h.ld, h.nmax, \
+                     perm, dinv, dstride, meta, c0, h.fast_max, corr, st)
+    if (R <= 128) DOPT_PANEL(128, 1);
+    else if (R <= 256) DOPT_PANEL(128, 2);
+    else if (R <= 384) DOPT_PANEL(128, 3);
+    else if (R <= 512) DOPT_PANEL(256, 2);
+    else if (R <= 1024) DOPT_PANEL(512, 2);
+    else DOPT_PANEL(512, 3);
+#undef DOPT_PANEL
     DOPT_CHECK_HIP(hipGetLastError());
-    const int R2 = R - BNB;
-    if (R2 <= 0) break;
-    const int nt = (R2 + 63) / 64;
-    hipLaunchKernelGGL(blu_u12_kernel, dim3(nt, B), dim3(256), 0, h.stream, K, h.ld, h.nmax, perm,
-                       dinv, dstride, meta, c0, h.fast_max);
-    DOPT_CHECK_HIP(hipGetLastError());
-    const long long total = (long long)nt * nt * B;
+  };
+  auto update = [&](int c0, int kw, int cols_max) {
+    const int R2 = npmax - c0 - kw;
+    if (R2 <= 0) return;
+    const int nrt = (R2 + 63) / 64, nct = (std::min(R2, cols_max) + 63) / 64;
+    const long long total = (long long)nrt * nct * B;
     if (total > 0x7fffffffLL) throw Error(-1, "blocked LU: trailing-update grid too large");
-    hipLaunchKernelGGL(blu_update_kernel, dim3((unsigned)total), dim3(256), 0, h.stream, K, h.ld,
-                       h.nmax, perm, meta, c0, h.fast_max, nt, (int)total);
+    if (kw == 64)
+      hipLaunchKernelGGL(blu_update_kernel<64>, dim3((unsigned)total), dim3(256), 0, h.stream, K,
+                         h.ld, h.nmax, perm, meta, c0, h.fast_max, cols_max, nrt, nct, (int)total);
+    else
+      hipLaunchKernelGGL(blu_update_kernel<32>, dim3((unsigned)total), dim3(256), 0, h.stream, K,
+                         h.ld, h.nmax, perm, meta, c0, h.fast_max, cols_max, nrt, nct, (int)total);
     DOPT_CHECK_HIP(hipGetLastError());
+  };
+  for (int c0 = 0; c0 < npmax; c0 += 2 * BNB) {
+    panel(c0, 0);
+    if (npmax - c0 <= BNB) break;
+    update(c0, BNB, BNB);          // panel B's 32 columns, all rows below panel A
+    panel(c0 + BNB, 1);
+    update(c0, 2 * BNB, 1 << 30);  // rank 64, rows and columns from c0+64
   }
 }
 
@@ -495,20 +734,33 @@ void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rh
   if (npmax == 0) return;
   const int B = (int)h.batch;
   const size_t dstride = fast_dinv_stride(h.nmax);
-  const int ent = (npmax + PT - 1) / PT;
   const double* K = h.K.as<double>();
   const int32_t* perm = h.ipiv.as<int32_t>();
   const QPMeta* meta = h.meta.as<QPMeta>();
-  if (ent <= 1)
-    hipLaunchKernelGGL(blu_solve_kernel<1>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
-                       dinv, dstride, meta, h.fast_max, trans, rhs, x);
-  else if (ent == 2)
-    hipLaunchKernelGGL(blu_solve_kernel<2>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
-                       dinv, dstride, meta, h.fast_max, trans, rhs, x);
-  else
-    hipLaunchKernelGGL(blu_solve_kernel<3>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
-                       dinv, dstride, meta, h.fast_max, trans, rhs, x);
+  if (!trans) {
+    hipLaunchKernelGGL(blu_solve_rows_kernel, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
+                       dinv, dstride, meta, h.fast_max, rhs, x);
+  } else {
+    // Kᵀ x = b: the slices are column segments, contiguous across entries, so
+    // one entry per thread is already coalesced
+    const int ent = (npmax + PT - 1) / PT;
+    if (ent <= 1)
+      hipLaunchKernelGGL(blu_solve_kernel<1>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
+                         dinv, dstride, meta, h.fast_max, trans, rhs, x);
+    else if (ent == 2)
+      hipLaunchKernelGGL(blu_solve_kernel<2>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
+                         dinv, dstride, meta, h.fast_max, trans, rhs, x);
+    else
+      hipLaunchKernelGGL(blu_solve_kernel<3>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
+                         dinv, dstride, meta, h.fast_max, trans, rhs, x);
+  }
   DOPT_CHECK_HIP(hipGetLastError());
+}
+
+void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, const double* rhs_fwd,
+                       double* x_rev, double* x_fwd) {
+  qp_blocked_solve(h, dinv, 0, rhs_rev, x_rev);
+  qp_blocked_solve(h, dinv, 1, rhs_fwd, x_fwd);
 }
 
 }  // namespace dopt

@@ -597,15 +597,16 @@ __device__ __forceinline__ void rev_rhs_wg(const double* dl_dz, int b, int n, in
   __syncthreads();
 }
 
-// forward RHS → S.y (reduced) and `full` (n+m+p, global) for eliminated rows
+// forward RHS → S.y (reduced) and `full` (n+m+p entries at per-problem stride
+// nmax, shared with the fallback kernels) for eliminated rows
 __device__ __forceinline__ void fwd_rhs_wg(const QPIn& P, const FwdTangents& T, int b, const int32_t* rpos, int nk,
-                           int Np, FastLDS& S, double* full) {
+                           int Np, FastLDS& S, double* full, int nmax) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n = P.n, m = P.m, p = P.p;
   const double* zb = P.z + (size_t)b * n;
   const double* lb = P.lam + (size_t)b * m;
   const double* nb = P.nu + (size_t)b * p;
-  double* r = full + (size_t)b * (n + m + p);
+  double* r = full + (size_t)b * nmax;
   for (int i = t; i < n; i += FT) {
     double acc = 0.0;
     if (T.dQ) {
@@ -665,7 +666,7 @@ __device__ __forceinline__ void fwd_rhs_wg(const QPIn& P, const FwdTangents& T, 
 
 // out = −[x_z | x_λ (all m rows) | x_ν]; eliminated rows recovered exactly.
 __device__ __forceinline__ void output_wg(const QPIn& P, int b, const double* x, const double* s,
-                          const int32_t* rpos, int nk, const double* full, int trans,
+                          const int32_t* rpos, int nk, const double* full, int nmax, int trans,
                           double* out) {
   const int t = threadIdx.x;
   const int n = P.n, m = P.m, p = P.p;
@@ -693,7 +694,7 @@ __device__ __forceinline__ void output_wg(const QPIn& P, int b, const double* x,
       for (; j < n; ++j) acc = fma(Gb[l + (size_t)j * m], x[j], acc);
       xl = (0.0 - acc) / s[(size_t)b * m + l];
     } else {
-      xl = full[(size_t)b * (n + m + p) + n + l] / s[(size_t)b * m + l];
+      xl = full[(size_t)b * nmax + n + l] / s[(size_t)b * m + l];
     }
     ob[n + l] = -xl;
   }
@@ -742,13 +743,13 @@ __global__ __launch_bounds__(FT) void qp_fused_kernel(
     if (do_rev) {
       rev_rhs_wg(dl_dz, b, P.n, Np, S);
       lu_solve_fast(W, ld, Np, Dw, S, 0);
-      output_wg(P, b, S.y, s, rpos, nk, full, 0, out_rev);
+      output_wg(P, b, S.y, s, rpos, nk, full, nmax, 0, out_rev);
       st.mark(5);
     }
     if (do_fwd) {
-      fwd_rhs_wg(P, T, b, rpos, nk, Np, S, full);
+      fwd_rhs_wg(P, T, b, rpos, nk, Np, S, full, nmax);
       lu_solve_fast(W, ld, Np, Dw, S, 1);
-      output_wg(P, b, S.y, s, rpos, nk, full, 1, out_fwd);
+      output_wg(P, b, S.y, s, rpos, nk, full, nmax, 1, out_fwd);
       st.mark(6);
     }
     __syncthreads();
@@ -799,9 +800,9 @@ __global__ __launch_bounds__(FT) void qp_solve_fast_kernel(
     const int Np = (N + FNB - 1) & ~(FNB - 1);
     for (int i = threadIdx.x; i < Np; i += FT) S.perm[i] = perm_in[(size_t)b * nmax + i];
     if (!trans) rev_rhs_wg(dl_dz, b, P.n, Np, S);
-    else fwd_rhs_wg(P, T, b, rpos, nk, Np, S, full);
+    else fwd_rhs_wg(P, T, b, rpos, nk, Np, S, full, nmax);
     lu_solve_fast(Kb, ld_per, Np, dinv + (size_t)b * dstride, S, trans);
-    output_wg(P, b, S.y, s, rpos, nk, full, trans, out);
+    output_wg(P, b, S.y, s, rpos, nk, full, nmax, trans, out);
   }
 }
 

@@ -173,6 +173,17 @@ def test_blocked_matches_fused_and_split(QPBatch):
     np.testing.assert_array_equal(f2, f3)
 
 
+def test_mixed_routes_in_one_batch(QPBatch):
+    """One batch whose problems take different paths — fused (N' ≤ fast_max)
+    and blocked (N' > fast_max), interleaved — with forward tangents that
+    reach eliminated rows (the `full` RHS buffer both paths share).  The LSQR
+    branch in a mixed batch: test_lp_iterative_batch_mixed_with_qp."""
+    lo = _synthetic(3, 60, 80, 4, 0.2, 31)    # N' = 60 + 16 + 4 = 80
+    hi = _synthetic(3, 60, 80, 4, 0.6, 32)    # N' = 60 + 48 + 4 = 112 (48 + 4 < n: LICQ)
+    d = {k: np.concatenate([np.stack([lo[k][i], hi[k][i]]) for i in range(3)]) for k in lo}
+    _check_batch(QPBatch, d, fast_max=100)
+
+
 def test_generic_large_system_path(QPBatch):
     """Reduced system > 1536 unknowns takes the generic LU kernel."""
     _check_batch(QPBatch, _synthetic(2, 1200, 700, 0, 0.6, 12))
