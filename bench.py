@@ -35,6 +35,9 @@ PEAK_FP64_TFLOPS = 78.6     # MI355X FP64 matrix/vector dense (spec; probe measu
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 QP_CFG = {2: dict(n=200, m=300, p=0, phi=0.3, batch=1024),
           3: dict(n=1000, m=1500, p=0, phi=0.3, batch=1024)}
+# conic configs (BASELINE.json configs[3], [4]); batch = problems per GPU
+# (config 5: 64 SDPs over 4 GPUs = 16 per GPU)
+CONIC_CFG = {4: dict(batch=512), 5: dict(batch=16)}
 
 
 # --------------------------------------------------------------------------
@@ -75,6 +78,174 @@ def cpu_baseline(cfg, seconds, workers):
                         f"× {seconds:.0f} s (wall {wall:.1f} s)"))
 
 
+def _conic_cpu_worker(args):
+    cfg, seed, seconds = args
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"
+    import numpy as np
+    from diffopt_amd.synthetic import CONIC_CONFIGS, conic_numpy
+    from oracle import conic as ocn
+    c = CONIC_CONFIGS[cfg]
+    d = conic_numpy(1, c["n"], c["cones"], seed)
+    t0 = time.perf_counter()
+    cache = ocn.Cache(d["A"][0], d["b"][0], d["c"][0], d["x"][0], d["s"][0], d["y"][0], c["cones"])
+    t_cache = time.perf_counter() - t0
+    if cfg == 4:
+        n_done = 0
+        t0 = time.perf_counter()
+        while True:
+            ocn.Cache(d["A"][0], d["b"][0], d["c"][0], d["x"][0], d["s"][0], d["y"][0], c["cones"])
+            ocn.forward_differentiate(cache, db=d["db"][0], dc=d["dc"][0])
+            ocn.reverse_differentiate(cache, d["dx"][0])
+            n_done += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        return n_done, time.perf_counter() - t0, None
+    # config 5: one full solve is minutes of CPU; time LSQR iterations (one
+    # matvec + one rmatvec each) for `seconds` and extrapolate with the
+    # iteration counts the engine reports
+    v = d["db"][0].copy()
+    z = np.concatenate([d["dc"][0], d["db"][0], [1.0]])
+    k = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        cache.rmatvec(cache.matvec(z))
+        k += 1
+    t_it = (time.perf_counter() - t0) / k
+    return k, t_cache, t_it
+
+
+def conic_cpu_baseline(cfg, seconds, workers, iters_per_solve):
+    import multiprocessing as mp
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        res = pool.map(_conic_cpu_worker, [(cfg, 1000 + i, seconds) for i in range(workers)])
+    wall = time.perf_counter() - t0
+    if cfg == 4:
+        solves = sum(r[0] for r in res)
+        rate = sum(r[0] / r[1] for r in res)
+        sample = (f"{solves} config-4 SOCP solves (n=500, 20 SOC(25), Dπ + fwd LSQR + rev LSQR, "
+                  f"IterativeSolvers defaults) on {workers} processes × {seconds:.0f} s "
+                  f"(wall {wall:.1f} s)")
+    else:
+        per = [r[1] + iters_per_solve * r[2] for r in res]
+        rate = sum(1.0 / t for t in per)
+        sample = (f"config-5 SDP (n=500, 10 PSD(50), m=12750): Dπ build timed once and "
+                  f"{sum(r[0] for r in res)} LSQR iterations (M·v + Mᵀ·u) timed for "
+                  f"{seconds:.0f} s per process on {workers} processes, extrapolated to the "
+                  f"engine's {iters_per_solve:.0f} fwd+rev iterations per solve (wall {wall:.1f} s)")
+    return dict(value=round(rate, 3), unit="solves/s", cores=workers, kind="port", sample=sample)
+
+
+def run_conic(args, world, rank, local_rank):
+    """Configs 4/5: batched conic sensitivities (cone Dπ + forward LSQR +
+    reverse LSQR per problem), roofline on the LSQR kernel's algorithmic HBM
+    bytes."""
+    import numpy as np
+    import torch
+    from diffopt_amd.conic import ConicBatch
+    from diffopt_amd.synthetic import CONIC_CONFIGS, SEED0, conic_numpy
+    c = CONIC_CONFIGS[args.config]
+    n, cones = c["n"], c["cones"]
+    B = args.batch or CONIC_CFG[args.config]["batch"]
+    m = sum(dim for _, dim in cones)
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local_rank))
+    d = conic_numpy(B, n, cones, SEED0 + args.config + 7919 * rank)
+    dev = {k: torch.from_numpy(d[k]).cuda() for k in ["A", "b", "c", "x", "s", "y", "dx", "db", "dc"]}
+    del d
+    eng = ConicBatch(B, n, cones, device=local_rank)
+    eng.set(dev["A"], dev["b"], dev["c"], dev["x"], dev["s"], dev["y"])
+    N = n + m + 1
+    packed = torch.empty(B, 2 * N, dtype=torch.float64, device="cuda") if world > 1 else None
+
+    def step():
+        eng.factor()                                   # v, π(v), Dπ per cone
+        fo, fdx = eng.forward(db=dev["db"], dc=dev["dc"])
+        g, _, rdb, rdc = eng.reverse(dev["dx"], want_dA=False)
+        if packed is not None:
+            from diffopt_amd import parallel
+            packed[:, :N].copy_(fo)
+            packed[:, N:].copy_(g)
+            parallel.all_gather_rows(packed, world * B)
+        return fo, g
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # iteration counts (deterministic for fixed inputs) for the byte count
+    eng.forward(db=dev["db"], dc=dev["dc"])
+    it_f = eng.iterations().astype(np.float64)
+    eng.reverse(dev["dx"], want_dA=False)
+    it_r = eng.iterations().astype(np.float64)
+    torch.cuda.synchronize()
+    eng.phase_times()
+    eng.set_profiling(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.set_profiling(False)
+    phases = eng.phase_times()
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline:
+            workers = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
+            cpu = conic_cpu_baseline(args.config, args.cpu_seconds, workers,
+                                     float(it_f.mean() + it_r.mean()))
+        plen = 0
+        for code, dim in cones:
+            if code in (1, 2):
+                plen += dim
+            elif code == 3:
+                plen += 4
+            elif code == 4:
+                dd = int((math.isqrt(8 * dim + 1) - 1) // 2)
+                plen += 2 * dd * dd + 2
+        # algorithmic HBM bytes per LSQR iteration: two passes over A (M·v and
+        # Mᵀ·u are sequentially dependent; each pass serves both A· and Aᵀ·),
+        # the structured Dπ parameters, and the N-vectors (SURVEY.md §8(d))
+        b_it = 16.0 * m * n + 8.0 * (plen + 4 * (n + m))
+        ms_tot, cnt = phases["conic_lsqr"]
+        avg_s = ms_tot / cnt / 1e3
+        per_launch = b_it * float(it_f.sum() + it_r.sum()) / 2.0
+        achieved = per_launch / avg_s / 1e9
+        roof = dict(bound="hbm", achieved=round(achieved, 1), peak=PEAK_HBM_GBS, unit="GB/s",
+                    frac=round(achieved / PEAK_HBM_GBS, 4), traffic=_load_pmc("conic_lsqr"),
+                    kernel="conic_lsqr", avg_launch_ms=round(avg_s * 1e3, 4),
+                    bytes_per_iteration=b_it,
+                    lsqr_iterations_mean={"forward": float(it_f.mean()), "reverse": float(it_r.mean())},
+                    phases_ms_per_step={k: round(v[0] / args.steps, 4) for k, v in sorted(phases.items())})
+        value = world * B * args.steps / elapsed
+        print(json.dumps({
+            "metric": "KKT sensitivity solves/sec (fwd+rev) on batched conic programs",
+            "value": round(value, 3), "unit": "solves/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded complementary cone pairs by construction, SURVEY.md §8(d))",
+            "config": {"workload": f"config {args.config}: " + ("SOCP batch, 20 SOC(25)" if args.config == 4
+                                                                  else "SDP batch, 10 PSD(50)"),
+                       "problems_per_gpu": B, "n": n, "m_rows": m,
+                       "parallelism": f"batch-sharded x{world}" + (" + RCCL all-gather" if world > 1 else "")},
+            "roofline": roof, "cpu_baseline": cpu}), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def _load_pmc(kernel):
     """HBM bytes/launch for `kernel` from the committed rocprofv3 --pmc summary
     (tools/pmc_summary.py → profiles/pmc_latest.json), or None."""
@@ -91,7 +262,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(QP_CFG))
+    ap.add_argument("--config", type=int, default=2, choices=sorted(QP_CFG) + sorted(CONIC_CFG))
     ap.add_argument("--batch", type=int, default=None, help="problems per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-workers", type=int, default=None)
@@ -102,6 +273,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.config in CONIC_CFG:
+        return run_conic(args, world, rank, local_rank)
     cfg = dict(QP_CFG[args.config])
     if args.batch:
         cfg["batch"] = args.batch

@@ -329,24 +329,82 @@ __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, con
   __syncthreads();
 }
 
-// y[0:m] = A_moi · x   (A_moi col-major m×n); thread per row, coalesced
-__device__ __forceinline__ void gemv_n(const double* __restrict__ A, int m, int n, const double* x, double* y) {
-  for (int i = threadIdx.x; i < m; i += CTPB) {
-    double acc = 0.0;
-    for (int j = 0; j < n; ++j) acc = fma(A[i + (size_t)j * m], x[j], acc);
-    y[i] = acc;
-  }
-}
+// One sweep over A_moi (col-major m×n) serving both products of an M / Mᵀ
+// apply:  y[0:m] = A_moi·x  and  g[0:n] = A_moiᵀ·w.
+// Rows go in blocks of PAIR_ROWS = 64·PAIR_K (lane ↔ row, PAIR_K rows per
+// lane, every load a coalesced 512-byte wave segment); wave wv owns columns
+// j ≡ wv (mod 4), so g[j] needs only an in-wave reduction and y's four
+// per-wave partials are summed through LDS (`ys`, 4·PAIR_ROWS doubles).
+// Two columns are in flight per wave (2·PAIR_K independent loads).
+constexpr int PAIR_K = 8;
+constexpr int PAIR_ROWS = 64 * PAIR_K;
 
-// g[0:n] = A_moiᵀ · w ; wave per column, lanes over rows
-__device__ __forceinline__ void gemv_t(const double* __restrict__ A, int m, int n, const double* w, double* g) {
+__device__ __forceinline__ void gemv_pair(const double* __restrict__ A, int m, int n,
+                                          const double* __restrict__ x, const double* __restrict__ w,
+                                          double* __restrict__ y, double* __restrict__ g,
+                                          double* __restrict__ ys) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int j = wv; j < n; j += CTPB / 64) {
-    const double* col = A + (size_t)j * m;
-    double acc = 0.0;
-    for (int i = lane; i < m; i += 64) acc = fma(col[i], w[i], acc);
-    acc = cwave_sum(acc);
-    if (lane == 0) g[j] = acc;
+  for (int r0 = 0; r0 < m; r0 += PAIR_ROWS) {
+    double wr[PAIR_K], ya[PAIR_K];
+    bool ok[PAIR_K];
+#pragma unroll
+    for (int k = 0; k < PAIR_K; ++k) {
+      const int i = r0 + lane + 64 * k;
+      ok[k] = i < m;
+      wr[k] = ok[k] ? w[i] : 0.0;
+      ya[k] = 0.0;
+    }
+    const double* Ar = A + r0 + lane;
+    int j = wv;
+    for (; j + 4 < n; j += 8) {
+      const double* c0 = Ar + (size_t)j * m;
+      const double* c1 = c0 + (size_t)4 * m;
+      double a0[PAIR_K], a1[PAIR_K];
+#pragma unroll
+      for (int k = 0; k < PAIR_K; ++k) {
+        a0[k] = ok[k] ? c0[64 * k] : 0.0;
+        a1[k] = ok[k] ? c1[64 * k] : 0.0;
+      }
+      const double x0 = x[j], x1 = x[j + 4];
+      double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+      for (int k = 0; k < PAIR_K; ++k) {
+        s0 = fma(a0[k], wr[k], s0);
+        s1 = fma(a1[k], wr[k], s1);
+        ya[k] = fma(a0[k], x0, ya[k]);
+        ya[k] = fma(a1[k], x1, ya[k]);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        s0 += __shfl_xor(s0, o);
+        s1 += __shfl_xor(s1, o);
+      }
+      if (lane == 0) {
+        g[j] = r0 ? g[j] + s0 : s0;
+        g[j + 4] = r0 ? g[j + 4] + s1 : s1;
+      }
+    }
+    for (; j < n; j += 4) {
+      const double* c0 = Ar + (size_t)j * m;
+      double a0[PAIR_K];
+#pragma unroll
+      for (int k = 0; k < PAIR_K; ++k) a0[k] = ok[k] ? c0[64 * k] : 0.0;
+      const double x0 = x[j];
+      double s0 = 0.0;
+#pragma unroll
+      for (int k = 0; k < PAIR_K; ++k) {
+        s0 = fma(a0[k], wr[k], s0);
+        ya[k] = fma(a0[k], x0, ya[k]);
+      }
+      s0 = cwave_sum(s0);
+      if (lane == 0) g[j] = r0 ? g[j] + s0 : s0;
+    }
+#pragma unroll
+    for (int k = 0; k < PAIR_K; ++k) ys[wv * PAIR_ROWS + lane + 64 * k] = ya[k];
+    __syncthreads();
+    for (int r = threadIdx.x; r < PAIR_ROWS && r0 + r < m; r += CTPB)
+      y[r0 + r] = (ys[r] + ys[PAIR_ROWS + r]) + (ys[2 * PAIR_ROWS + r] + ys[3 * PAIR_ROWS + r]);
+    __syncthreads();
   }
 }
 
@@ -358,12 +416,11 @@ struct ConicProblem {
 // out = M z   (z, out: N = n+m+1; scratch: Dv (m), Au (m), g (n))
 __device__ __forceinline__ void M_apply(const ConicProblem& pr, const ConeDesc* cones, int ncones,
                         const double* z, double* out, double* Dv, double* Au, double* g,
-                        double* lds, double* red) {
+                        double* lds, double* red, double* ys) {
   const int n = pr.n, m = pr.m, t = threadIdx.x;
   dpi_apply(cones, ncones, pr.v, pr.P, z + n, Dv, 0, lds, red);
-  gemv_n(pr.A, m, n, z, Au);        // A_moi u  (= −A u)
-  gemv_t(pr.A, m, n, Dv, g);        // A_moiᵀ Dv (= −AᵀDv)
-  __syncthreads();
+  // A_moi u (= −A u) and A_moiᵀ Dv (= −AᵀDv) in one sweep
+  gemv_pair(pr.A, m, n, z, Dv, Au, g, ys);
   const double w = z[n + m];
   double cu = 0.0, bd = 0.0;
   for (int j = t; j < n; j += CTPB) {
@@ -382,11 +439,10 @@ __device__ __forceinline__ void M_apply(const ConicProblem& pr, const ConeDesc* 
 // out = Mᵀ r
 __device__ __forceinline__ void MT_apply(const ConicProblem& pr, const ConeDesc* cones, int ncones,
                          const double* r, double* out, double* tmpm, double* Ap, double* g,
-                         double* lds, double* red) {
+                         double* lds, double* red, double* ys) {
   const int n = pr.n, m = pr.m, t = threadIdx.x;
-  gemv_n(pr.A, m, n, r, Ap);          // A_moi p  (A p = −A_moi p)
-  gemv_t(pr.A, m, n, r + n, g);       // A_moiᵀ q (−Aᵀ q = A_moiᵀ q)
-  __syncthreads();
+  // A_moi p (A p = −A_moi p) and A_moiᵀ q (−Aᵀ q = A_moiᵀ q) in one sweep
+  gemv_pair(pr.A, m, n, r, r + n, Ap, g, ys);
   const double tw = r[n + m];
   for (int i = t; i < m; i += CTPB) tmpm[i] = -Ap[i] - r[n + i] - pr.b[i] * tw;
   __syncthreads();
@@ -419,6 +475,7 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ double red[4];
   __shared__ ConeDesc cones[128];
+  __shared__ double ys[4 * PAIR_ROWS];
   const int bidx = blockIdx.x, t = threadIdx.x;
   const int N = n + m + 1;
   const ConeDesc* cn = cones_g;
@@ -457,7 +514,7 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
   if (beta > rhs_zero_tol) {
     for (int i = t; i < N; i += CTPB) u[i] /= beta;
     __syncthreads();
-    MT_apply(pr, cn, ncones, u, vv, s1, s2, s4, lds, red);
+    MT_apply(pr, cn, ncones, u, vv, s1, s2, s4, lds, red, ys);
     double aa = 0.0;
     for (int i = t; i < N; i += CTPB) aa = fma(vv[i], vv[i], aa);
     double alpha = sqrt(cblock_sum(aa, red));
@@ -472,7 +529,7 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
       const int maxiter = N;
       while (it < maxiter) {
         ++it;
-        M_apply(pr, cn, ncones, vv, tmp, s1, s2, s4, lds, red);
+        M_apply(pr, cn, ncones, vv, tmp, s1, s2, s4, lds, red, ys);
         double su = 0.0;
         for (int i = t; i < N; i += CTPB) { const double ui = tmp[i] - alpha * u[i]; u[i] = ui; su = fma(ui, ui, su); }
         beta = sqrt(cblock_sum(su, red));
@@ -480,7 +537,7 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
           for (int i = t; i < N; i += CTPB) u[i] /= beta;
           __syncthreads();
           anorm = sqrt(anorm * anorm + alpha * alpha + beta * beta);
-          MT_apply(pr, cn, ncones, u, tmp, s1, s2, s4, lds, red);
+          MT_apply(pr, cn, ncones, u, tmp, s1, s2, s4, lds, red, ys);
           double sv = 0.0;
           for (int i = t; i < N; i += CTPB) { const double vi = tmp[i] - beta * vv[i]; vv[i] = vi; sv = fma(vi, vi, sv); }
           alpha = sqrt(cblock_sum(sv, red));

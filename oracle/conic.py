@@ -38,29 +38,43 @@ class Cache:
         self.cones = list(cones)
         self.v = y - s                             # :222
         self.blocks = C.dpi_blocks(self.v, self.cones, psd_convention)  # :225
-        self.D = C.blockdiag(self.blocks)
+        self._off = C.cone_offsets(self.cones)
         self.vp = C.pi(self.v, self.cones)         # :249
         self.m, self.n = m, n
+
+    @property
+    def D(self):
+        """Dense ``Dπ`` (the reference's ``BlockDiagonal``, :225)."""
+        return C.blockdiag(self.blocks)
+
+    def _dpi(self, v, trans=False):
+        """``Dπ·v`` / ``Dπᵀ·v`` block by block, as ``BlockDiagonal`` multiplies."""
+        out = np.empty_like(v)
+        for k, blk in enumerate(self.blocks):
+            a, b = self._off[k], self._off[k + 1]
+            out[a:b] = (blk.T if trans else blk) @ v[a:b]
+        return out
 
     def M(self):
         """Dense ``M = [0, AᵀDπ, c; −A, I−Dπ, b; −cᵀ, −bᵀDπ, 0]`` (:243-247)."""
         m, n = self.m, self.n
         N = n + m + 1
         M = np.zeros((N, N))
-        M[:n, n:n + m] = self.A.T @ self.D
+        D = self.D
+        M[:n, n:n + m] = self.A.T @ D
         M[:n, -1] = self.c
         M[n:n + m, :n] = -self.A
-        M[n:n + m, n:n + m] = np.eye(m) - self.D
+        M[n:n + m, n:n + m] = np.eye(m) - D
         M[n:n + m, -1] = self.b
         M[-1, :n] = -self.c
-        M[-1, n:n + m] = -(self.b @ self.D)
+        M[-1, n:n + m] = -(self.b @ D)
         return M
 
     # matrix-free products, identical to multiplying by M() ---------------
     def matvec(self, z):
         n, m = self.n, self.m
         u, v, w = z[:n], z[n:n + m], z[-1]
-        Dv = self.D @ v
+        Dv = self._dpi(v)
         return np.concatenate([self.A.T @ Dv + self.c * w,
                                -self.A @ u + v - Dv + self.b * w,
                                [-(self.c @ u) - (self.b @ Dv)]])
@@ -70,7 +84,7 @@ class Cache:
         p, q, t = r[:n], r[n:n + m], r[-1]
         Ap = self.A @ p
         return np.concatenate([-(self.A.T @ q) - self.c * t,
-                               self.D.T @ (Ap - q - self.b * t) + q,
+                               self._dpi(Ap - q - self.b * t, trans=True) + q,
                                [self.c @ p + self.b @ q]])
 
 
