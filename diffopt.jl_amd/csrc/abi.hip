@@ -100,6 +100,9 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
         DOPT_CHECK_HIP(hipMemset(h->stamps.p, 0, 8 * sizeof(unsigned long long)));
       }
     }
+    if (const char* e = getenv("DOPT_CONIC_SPLIT")) {
+      if (e[0] == '0' || e[0] == '1') h->conic_split = e[0] - '0';
+    }
     if (const char* e = getenv("DOPT_FAST_MAX")) {
       h->fast_max = std::max(0, std::min(atoi(e), dopt::FAST_MAX_N));
     }

@@ -329,21 +329,30 @@ __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, con
   __syncthreads();
 }
 
-// One sweep over A_moi (col-major m×n) serving both products of an M / Mᵀ
+// One sweep over A_moi (col-major, leading dimension ld, m rows here) serving both products of an M / Mᵀ
 // apply:  y[0:m] = A_moi·x  and  g[0:n] = A_moiᵀ·w.
 // Rows go in blocks of PAIR_ROWS = 64·PAIR_K (lane ↔ row, PAIR_K rows per
 // lane, every load a coalesced 512-byte wave segment); wave wv owns columns
 // j ≡ wv (mod 4), so g[j] needs only an in-wave reduction and y's four
 // per-wave partials are summed through LDS (`ys`, 4·PAIR_ROWS doubles).
-// Two columns are in flight per wave (2·PAIR_K independent loads).
+// PAIR_NC columns are in flight per wave (PAIR_NC·PAIR_K independent loads).
 constexpr int PAIR_K = 8;
+#ifndef DOPT_PAIR_NC
+#define DOPT_PAIR_NC 4
+#endif
+constexpr int PAIR_NC = DOPT_PAIR_NC;   // columns in flight per wave
 constexpr int PAIR_ROWS = 64 * PAIR_K;
 
-__device__ __forceinline__ void gemv_pair(const double* __restrict__ A, int m, int n,
+__device__ __forceinline__ void gemv_pair(const double* __restrict__ A, int ld, int m, int n,
                                           const double* __restrict__ x, const double* __restrict__ w,
                                           double* __restrict__ y, double* __restrict__ g,
                                           double* __restrict__ ys) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (m <= 0) {
+    for (int j = threadIdx.x; j < n; j += CTPB) g[j] = 0.0;
+    __syncthreads();
+    return;
+  }
   for (int r0 = 0; r0 < m; r0 += PAIR_ROWS) {
     double wr[PAIR_K], ya[PAIR_K];
     bool ok[PAIR_K];
@@ -356,36 +365,38 @@ __device__ __forceinline__ void gemv_pair(const double* __restrict__ A, int m, i
     }
     const double* Ar = A + r0 + lane;
     int j = wv;
-    for (; j + 4 < n; j += 8) {
-      const double* c0 = Ar + (size_t)j * m;
-      const double* c1 = c0 + (size_t)4 * m;
-      double a0[PAIR_K], a1[PAIR_K];
+    for (; j + 4 * (PAIR_NC - 1) < n; j += 4 * PAIR_NC) {
+      double a[PAIR_NC][PAIR_K];
 #pragma unroll
-      for (int k = 0; k < PAIR_K; ++k) {
-        a0[k] = ok[k] ? c0[64 * k] : 0.0;
-        a1[k] = ok[k] ? c1[64 * k] : 0.0;
+      for (int c = 0; c < PAIR_NC; ++c) {
+        const double* cc = Ar + (size_t)(j + 4 * c) * ld;
+#pragma unroll
+        for (int k = 0; k < PAIR_K; ++k) a[c][k] = ok[k] ? cc[64 * k] : 0.0;
       }
-      const double x0 = x[j], x1 = x[j + 4];
-      double s0 = 0.0, s1 = 0.0;
+      double sc[PAIR_NC];
 #pragma unroll
-      for (int k = 0; k < PAIR_K; ++k) {
-        s0 = fma(a0[k], wr[k], s0);
-        s1 = fma(a1[k], wr[k], s1);
-        ya[k] = fma(a0[k], x0, ya[k]);
-        ya[k] = fma(a1[k], x1, ya[k]);
+      for (int c = 0; c < PAIR_NC; ++c) {
+        const double xc = x[j + 4 * c];
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < PAIR_K; ++k) {
+          acc = fma(a[c][k], wr[k], acc);
+          ya[k] = fma(a[c][k], xc, ya[k]);
+        }
+        sc[c] = acc;
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) {
-        s0 += __shfl_xor(s0, o);
-        s1 += __shfl_xor(s1, o);
+#pragma unroll
+        for (int c = 0; c < PAIR_NC; ++c) sc[c] += __shfl_xor(sc[c], o);
       }
       if (lane == 0) {
-        g[j] = r0 ? g[j] + s0 : s0;
-        g[j + 4] = r0 ? g[j + 4] + s1 : s1;
+#pragma unroll
+        for (int c = 0; c < PAIR_NC; ++c) g[j + 4 * c] = r0 ? g[j + 4 * c] + sc[c] : sc[c];
       }
     }
     for (; j < n; j += 4) {
-      const double* c0 = Ar + (size_t)j * m;
+      const double* c0 = Ar + (size_t)j * ld;
       double a0[PAIR_K];
 #pragma unroll
       for (int k = 0; k < PAIR_K; ++k) a0[k] = ok[k] ? c0[64 * k] : 0.0;
@@ -420,7 +431,7 @@ __device__ __forceinline__ void M_apply(const ConicProblem& pr, const ConeDesc* 
   const int n = pr.n, m = pr.m, t = threadIdx.x;
   dpi_apply(cones, ncones, pr.v, pr.P, z + n, Dv, 0, lds, red);
   // A_moi u (= −A u) and A_moiᵀ Dv (= −AᵀDv) in one sweep
-  gemv_pair(pr.A, m, n, z, Dv, Au, g, ys);
+  gemv_pair(pr.A, m, m, n, z, Dv, Au, g, ys);
   const double w = z[n + m];
   double cu = 0.0, bd = 0.0;
   for (int j = t; j < n; j += CTPB) {
@@ -442,7 +453,7 @@ __device__ __forceinline__ void MT_apply(const ConicProblem& pr, const ConeDesc*
                          double* lds, double* red, double* ys) {
   const int n = pr.n, m = pr.m, t = threadIdx.x;
   // A_moi p (A p = −A_moi p) and A_moiᵀ q (−Aᵀ q = A_moiᵀ q) in one sweep
-  gemv_pair(pr.A, m, n, r, r + n, Ap, g, ys);
+  gemv_pair(pr.A, m, m, n, r, r + n, Ap, g, ys);
   const double tw = r[n + m];
   for (int i = t; i < m; i += CTPB) tmpm[i] = -Ap[i] - r[n + i] - pr.b[i] * tw;
   __syncthreads();
@@ -681,6 +692,312 @@ __global__ __launch_bounds__(CTPB) void conic_rev_out_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Split LSQR: the same iteration as conic_lsqr_kernel, but each M / Mᵀ apply
+// is spread over a (row block × problem) grid so that a few large problems
+// (config 5: 16 SDPs per GPU, m = 12 750) still fill all 256 CUs.  One LSQR
+// iteration = 6 launches:
+//   dpi(0)  : Dv = Dπ·v_m                       grid (cones, B)
+//   passM   : rows of A·v_n, partial Aᵀ·Dv     grid (row blocks, B)
+//   upd_u   : finish M·v, u ← M·v − αu, β      grid (B)
+//   passT   : rows of A·u_n, partial Aᵀ·u_m    grid (row blocks, B)
+//   dpi(1)  : Dπᵀ·(…)                           grid (cones, B)
+//   upd_v   : finish Mᵀ·u, v ← Mᵀu − βv, α, the Givens recurrences, x, w,
+//             stopping tests                    grid (B)
+// Scalars live in a per-problem LsqrState; a finished problem sets `done`
+// and every later launch returns at once for it.  The host checks the count
+// of unfinished problems every SPLIT_CHUNK iterations.
+// ---------------------------------------------------------------------------
+constexpr int SPLIT_CHUNK = 8;
+
+struct LsqrState {
+  double alpha, beta, rhobar, phibar, anorm, ddnorm, xxnorm, zz, sn2, cs2, bnorm, pad;
+  int32_t it, istop, done, skipT;
+};
+
+struct SplitWS {
+  // per-problem vectors (stride N or m), partial Aᵀ products (RB·n)
+  double *x, *u, *v, *w, *out, *Dv, *tmpm, *yb, *gpart;
+  int N, m, n, RB;
+  __device__ double* vec(double* base, int b) const { return base + (size_t)b * N; }
+  __device__ double* mvec(double* base, int b) const { return base + (size_t)b * m; }
+};
+
+__device__ __forceinline__ void split_finish(int b, int32_t* active, LsqrState& st) {
+  st.done = 1;
+  if (threadIdx.x == 0) atomicSub(active, 1);
+}
+
+__global__ __launch_bounds__(CTPB) void conic_split_init_kernel(
+    const double* __restrict__ rhs, double tol, SplitWS ws, LsqrState* __restrict__ stv,
+    int32_t* __restrict__ active) {
+  __shared__ double red[4];
+  const int b = blockIdx.x, t = threadIdx.x, N = ws.N;
+  const double* rb = rhs + (size_t)b * N;
+  double* u = ws.vec(ws.u, b);
+  double* x = ws.vec(ws.x, b);
+  double bb = 0.0;
+  for (int i = t; i < N; i += CTPB) {
+    const double r = rb[i];
+    u[i] = r;
+    x[i] = 0.0;
+    bb = fma(r, r, bb);
+  }
+  const double beta = sqrt(cblock_sum(bb, red));
+  if (t == 0) {
+    LsqrState st = {};
+    st.beta = beta;
+    if (!(beta > tol)) split_finish(b, active, st);
+    stv[b] = st;
+  }
+  if (beta > tol)
+    for (int i = t; i < N; i += CTPB) u[i] /= beta;
+}
+
+// rows [r0, r0+rows) of the pair of products; `dir` 0: M·v (x = v_n, w = Dv),
+// 1: Mᵀ·u (x = u_n, w = u_m)
+__global__ __launch_bounds__(CTPB) void conic_split_pass_kernel(
+    int dir, const double* __restrict__ A, const double* __restrict__ bvec, SplitWS ws,
+    const LsqrState* __restrict__ stv) {
+  __shared__ double ys[4 * PAIR_ROWS];
+  const int rb = blockIdx.x, b = blockIdx.y;
+  const LsqrState& st = stv[b];
+  if (st.done || (dir == 1 && st.skipT)) return;
+  const int m = ws.m, n = ws.n, N = ws.N;
+  const int r0 = rb * PAIR_ROWS;
+  const int rows = min(PAIR_ROWS, m - r0);
+  const double* Ab = A + (size_t)b * m * n + r0;
+  const double* src = dir == 0 ? ws.vec(ws.v, b) : ws.vec(ws.u, b);
+  const double* wv = dir == 0 ? ws.mvec(ws.Dv, b) + r0 : src + n + r0;
+  double* yb = ws.mvec(ws.yb, b) + r0;
+  gemv_pair(Ab, m, rows, n, src, wv, yb, ws.gpart + ((size_t)b * ws.RB + rb) * n, ys);
+  const double last = src[N - 1];
+  const double* bb = bvec + (size_t)b * m + r0;
+  if (dir == 0) {
+    double* o = ws.vec(ws.out, b) + n + r0;
+    const double* vm = src + n + r0;
+    const double* Dv = ws.mvec(ws.Dv, b) + r0;
+    for (int i = threadIdx.x; i < rows; i += CTPB) o[i] = yb[i] + vm[i] - Dv[i] + bb[i] * last;
+  } else {
+    double* tm = ws.mvec(ws.tmpm, b) + r0;
+    const double* um = src + n + r0;
+    for (int i = threadIdx.x; i < rows; i += CTPB) tm[i] = -yb[i] - um[i] - bb[i] * last;
+  }
+}
+
+// Dπ (dir 0: Dv = Dπ v_m) or Dπᵀ (dir 1: out_m = Dπᵀ tmpm), one cone per WG
+__global__ __launch_bounds__(CTPB) void conic_split_dpi_kernel(
+    int dir, const ConeDesc* __restrict__ cones_g, const double* __restrict__ vcone,
+    const double* __restrict__ P, int plen, SplitWS ws, const LsqrState* __restrict__ stv) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ double red[4];
+  const int k = blockIdx.x, b = blockIdx.y;
+  const LsqrState& st = stv[b];
+  if (st.done || (dir == 1 && st.skipT)) return;
+  const ConeDesc cd = cones_g[k];
+  const double* pv = vcone + (size_t)b * ws.m;
+  const double* pp = P + (size_t)b * plen;
+  if (dir == 0)
+    dpi_apply(&cd, 1, pv, pp, ws.vec(ws.v, b) + ws.n, ws.mvec(ws.Dv, b), 0, lds, red);
+  else
+    dpi_apply(&cd, 1, pv, pp, ws.mvec(ws.tmpm, b), ws.vec(ws.out, b) + ws.n, 1, lds, red);
+}
+
+// out_n = −Σ_rb gpart + c·v_last, out_end = −c·v_n − b·Dv; then u ← out − αu
+__global__ __launch_bounds__(CTPB) void conic_split_upd_u_kernel(
+    const double* __restrict__ bvec, const double* __restrict__ cvec, SplitWS ws,
+    LsqrState* __restrict__ stv) {
+  __shared__ double red[4];
+  const int b = blockIdx.x, t = threadIdx.x;
+  LsqrState st = stv[b];
+  if (st.done) return;
+  const int n = ws.n, m = ws.m, N = ws.N;
+  const double* v = ws.vec(ws.v, b);
+  double* out = ws.vec(ws.out, b);
+  double* u = ws.vec(ws.u, b);
+  const double* c = cvec + (size_t)b * n;
+  const double* bb = bvec + (size_t)b * m;
+  const double* Dv = ws.mvec(ws.Dv, b);
+  const double* gp = ws.gpart + (size_t)b * ws.RB * n;
+  const double w = v[N - 1];
+  double cu = 0.0, bd = 0.0;
+  for (int j = t; j < n; j += CTPB) {
+    double g = 0.0;
+    for (int r = 0; r < ws.RB; ++r) g += gp[(size_t)r * n + j];
+    out[j] = -g + c[j] * w;
+    cu = fma(c[j], v[j], cu);
+  }
+  for (int i = t; i < m; i += CTPB) bd = fma(bb[i], Dv[i], bd);
+  const double se = cblock_sum(-cu - bd, red);
+  if (t == 0) out[N - 1] = se;
+  __syncthreads();
+  double su = 0.0;
+  for (int i = t; i < N; i += CTPB) {
+    const double ui = out[i] - st.alpha * u[i];
+    u[i] = ui;
+    su = fma(ui, ui, su);
+  }
+  const double beta = sqrt(cblock_sum(su, red));
+  if (beta > 0.0)
+    for (int i = t; i < N; i += CTPB) u[i] /= beta;
+  if (t == 0) {
+    st.it += 1;
+    st.beta = beta;
+    st.skipT = !(beta > 0.0);
+    if (beta > 0.0) st.anorm = sqrt(st.anorm * st.anorm + st.alpha * st.alpha + beta * beta);
+    stv[b] = st;
+  }
+}
+
+// finish Mᵀ·u into out: out_n = Σ_rb gpart − c·u_last, out_m += u_m,
+// out_end = c·u_n + b·u_m
+__device__ __forceinline__ void split_finish_T(const SplitWS& ws, int b, const double* bvec,
+                                               const double* cvec, double* red) {
+  const int t = threadIdx.x, n = ws.n, m = ws.m, N = ws.N;
+  const double* u = ws.vec(ws.u, b);
+  double* out = ws.vec(ws.out, b);
+  const double* c = cvec + (size_t)b * n;
+  const double* bb = bvec + (size_t)b * m;
+  const double* gp = ws.gpart + (size_t)b * ws.RB * n;
+  const double tw = u[N - 1];
+  double cp = 0.0, bq = 0.0;
+  for (int j = t; j < n; j += CTPB) {
+    double g = 0.0;
+    for (int r = 0; r < ws.RB; ++r) g += gp[(size_t)r * n + j];
+    out[j] = g - c[j] * tw;
+    cp = fma(c[j], u[j], cp);
+  }
+  for (int i = t; i < m; i += CTPB) {
+    out[n + i] += u[n + i];
+    bq = fma(bb[i], u[n + i], bq);
+  }
+  const double se = cblock_sum(cp + bq, red);
+  if (t == 0) out[N - 1] = se;
+  __syncthreads();
+}
+
+// first Mᵀ·u: v = Mᵀu/α, w = v, recurrence initial values
+__global__ __launch_bounds__(CTPB) void conic_split_init2_kernel(
+    const double* __restrict__ bvec, const double* __restrict__ cvec, SplitWS ws,
+    LsqrState* __restrict__ stv, int32_t* __restrict__ active) {
+  __shared__ double red[4];
+  const int b = blockIdx.x, t = threadIdx.x, N = ws.N;
+  LsqrState st = stv[b];
+  if (st.done) return;
+  split_finish_T(ws, b, bvec, cvec, red);
+  double* out = ws.vec(ws.out, b);
+  double* v = ws.vec(ws.v, b);
+  double* w = ws.vec(ws.w, b);
+  double aa = 0.0;
+  for (int i = t; i < N; i += CTPB) aa = fma(out[i], out[i], aa);
+  const double alpha = sqrt(cblock_sum(aa, red));
+  if (alpha > 0.0)
+    for (int i = t; i < N; i += CTPB) { const double vi = out[i] / alpha; v[i] = vi; w[i] = vi; }
+  if (t == 0) {
+    st.alpha = alpha;
+    st.anorm = st.ddnorm = st.xxnorm = st.zz = st.sn2 = 0.0;
+    st.cs2 = -1.0;
+    st.rhobar = alpha;
+    st.phibar = st.beta;
+    st.bnorm = st.beta;
+    st.it = 0;
+    st.istop = 0;
+    if (!(alpha > 0.0)) split_finish(b, active, st);
+    stv[b] = st;
+  }
+}
+
+__global__ __launch_bounds__(CTPB) void conic_split_upd_v_kernel(
+    const double* __restrict__ bvec, const double* __restrict__ cvec, SplitWS ws,
+    LsqrState* __restrict__ stv, int maxiter, int32_t* __restrict__ active) {
+  __shared__ double red[4];
+  const int b = blockIdx.x, t = threadIdx.x, N = ws.N;
+  LsqrState st = stv[b];
+  if (st.done) return;
+  double* v = ws.vec(ws.v, b);
+  double alpha = st.alpha;
+  const double beta = st.beta;
+  if (!st.skipT) {
+    split_finish_T(ws, b, bvec, cvec, red);
+    const double* out = ws.vec(ws.out, b);
+    double sv = 0.0;
+    for (int i = t; i < N; i += CTPB) { const double vi = out[i] - beta * v[i]; v[i] = vi; sv = fma(vi, vi, sv); }
+    alpha = sqrt(cblock_sum(sv, red));
+    if (alpha > 0.0) for (int i = t; i < N; i += CTPB) v[i] /= alpha;
+    __syncthreads();
+  }
+  const double rhobar1 = st.rhobar;
+  const double rho = hypot(rhobar1, beta);
+  const double cs = rhobar1 / rho, sn = beta / rho;
+  const double theta = sn * alpha;
+  const double rhobar = -cs * alpha;
+  const double phi = cs * st.phibar;
+  const double phibar = sn * st.phibar;
+  const double tau = sn * phi;
+  const double t1 = phi / rho, t2 = -theta / rho;
+  double* x = ws.vec(ws.x, b);
+  double* w = ws.vec(ws.w, b);
+  double sw = 0.0;
+  for (int i = t; i < N; i += CTPB) {
+    const double wi = w[i];
+    sw = fma(wi, wi, sw);
+    x[i] = x[i] + t1 * wi;
+    w[i] = v[i] + t2 * wi;
+  }
+  const double ddnorm = st.ddnorm + cblock_sum(sw, red) / (rho * rho);
+  if (t != 0) return;
+  const double eps = 2.220446049250313e-16;
+  const double atol = sqrt(eps), btol = sqrt(eps), ctol = sqrt(eps);
+  const double anorm = st.anorm, bnorm = st.bnorm;
+  const double delta = st.sn2 * rho, gambar = -st.cs2 * rho;
+  const double rhs_ = phi - delta * st.zz;
+  const double zbar = rhs_ / gambar;
+  const double xnorm = sqrt(st.xxnorm + zbar * zbar);
+  const double gamma = hypot(gambar, theta);
+  st.cs2 = gambar / gamma;
+  st.sn2 = theta / gamma;
+  st.zz = rhs_ / gamma;
+  st.xxnorm += st.zz * st.zz;
+  const double acond = anorm * sqrt(ddnorm);
+  const double rnorm = sqrt(phibar * phibar);
+  const double arnorm = alpha * fabs(tau);
+  const double test1 = rnorm / bnorm;
+  const double test2 = (anorm * rnorm != 0.0) ? arnorm / (anorm * rnorm) : 0.0;
+  const double test3 = (acond != 0.0) ? 1.0 / acond : 0.0;
+  const double t1r = test1 / (1.0 + anorm * xnorm / bnorm);
+  const double rtol = btol + atol * anorm * xnorm / bnorm;
+  int istop = 0;
+  if (st.it >= maxiter) istop = 7;
+  if (1.0 + test3 <= 1.0) istop = 6;
+  if (1.0 + test2 <= 1.0) istop = 5;
+  if (1.0 + t1r <= 1.0) istop = 4;
+  if (test3 <= ctol) istop = 3;
+  if (test2 <= atol) istop = 2;
+  if (test1 <= rtol) istop = 1;
+  st.alpha = alpha;
+  st.rhobar = rhobar;
+  st.phibar = phibar;
+  st.ddnorm = ddnorm;
+  st.istop = istop;
+  if (istop) {
+    st.done = 1;
+    atomicSub(active, 1);
+  }
+  stv[b] = st;
+}
+
+__global__ __launch_bounds__(CTPB) void conic_split_out_kernel(
+    SplitWS ws, const LsqrState* __restrict__ stv, double* __restrict__ xout,
+    int32_t* __restrict__ info) {
+  const int b = blockIdx.x, t = threadIdx.x, N = ws.N;
+  const double* x = ws.vec(ws.x, b);
+  for (int i = t; i < N; i += CTPB) xout[(size_t)b * N + i] = x[i];
+  if (t == 0 && info) {
+    info[b] = stv[b].istop;
+    info[gridDim.x + b] = stv[b].it;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 static void ccheck() { DOPT_CHECK_HIP(hipGetLastError()); }
@@ -727,6 +1044,79 @@ void conic_factor(Handle& h) {
   h.cfactored = true;
 }
 
+// Split-path LSQR (see conic_split_* above); rhs already in place.
+static void conic_lsqr_split(Handle& h, double tol, const double* rhs, double* out) {
+  const int B = (int)h.batch, m = h.m, n = h.n;
+  const int nc = (int)h.cones.size() / 2;
+  const int N = n + m + 1;
+  const int RB = std::max(1, (m + PAIR_ROWS - 1) / PAIR_ROWS);
+  const size_t per = (size_t)5 * N + 4 * (size_t)std::max(m, 1) + (size_t)RB * n;
+  h.csplit.ensure((size_t)B * per * sizeof(double) + (size_t)B * sizeof(LsqrState) + 64);
+  SplitWS ws;
+  double* base = h.csplit.as<double>();
+  ws.x = base;
+  ws.u = ws.x + (size_t)B * N;
+  ws.v = ws.u + (size_t)B * N;
+  ws.w = ws.v + (size_t)B * N;
+  ws.out = ws.w + (size_t)B * N;
+  ws.Dv = ws.out + (size_t)B * N;
+  ws.tmpm = ws.Dv + (size_t)B * std::max(m, 1);
+  ws.yb = ws.tmpm + (size_t)B * std::max(m, 1);
+  ws.gpart = ws.yb + (size_t)B * std::max(m, 1);
+  ws.N = N;
+  ws.m = m;
+  ws.n = n;
+  ws.RB = RB;
+  LsqrState* st = reinterpret_cast<LsqrState*>(base + (size_t)B * per);
+  int32_t* active = reinterpret_cast<int32_t*>(st + B);
+  const size_t dl = dpi_lds_bytes(h.cones);
+  const double* vcone = h.vp.as<double>();
+  const double* P = h.dpi.as<double>();
+  const ConeDesc* cd = h.cone_dev.as<ConeDesc>();
+  const int32_t nact = B;
+  DOPT_CHECK_HIP(hipMemcpyAsync(active, &nact, sizeof(int32_t), hipMemcpyHostToDevice, h.stream));
+  int32_t left = B;
+  PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
+  auto passT = [&]() {
+    hipLaunchKernelGGL(conic_split_pass_kernel, dim3(RB, B), dim3(CTPB), 0, h.stream, 1, h.cA,
+                       h.cb, ws, st);
+    if (nc)
+      hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, B), dim3(CTPB), dl, h.stream, 1, cd,
+                         vcone, P, h.dpi_len, ws, st);
+  };
+  hipLaunchKernelGGL(conic_split_init_kernel, dim3(B), dim3(CTPB), 0, h.stream, rhs, tol, ws, st,
+                     active);
+  passT();
+  hipLaunchKernelGGL(conic_split_init2_kernel, dim3(B), dim3(CTPB), 0, h.stream, h.cb, h.cc, ws,
+                     st, active);
+  ccheck();
+  for (int it = 0; it < N && left > 0;) {
+    for (int k = 0; k < SPLIT_CHUNK && it < N; ++k, ++it) {
+      if (nc)
+        hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, B), dim3(CTPB), dl, h.stream, 0, cd,
+                           vcone, P, h.dpi_len, ws, st);
+      hipLaunchKernelGGL(conic_split_pass_kernel, dim3(RB, B), dim3(CTPB), 0, h.stream, 0, h.cA,
+                         h.cb, ws, st);
+      hipLaunchKernelGGL(conic_split_upd_u_kernel, dim3(B), dim3(CTPB), 0, h.stream, h.cb, h.cc,
+                         ws, st);
+      passT();
+      hipLaunchKernelGGL(conic_split_upd_v_kernel, dim3(B), dim3(CTPB), 0, h.stream, h.cb, h.cc,
+                         ws, st, N, active);
+    }
+    ccheck();
+    DOPT_CHECK_HIP(hipMemcpyAsync(&left, active, sizeof(int32_t), hipMemcpyDeviceToHost, h.stream));
+    DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+  }
+  hipLaunchKernelGGL(conic_split_out_kernel, dim3(B), dim3(CTPB), 0, h.stream, ws, st, out,
+                     h.cinfo.as<int32_t>());
+  ccheck();
+}
+
+static bool use_split(const Handle& h) {
+  if (h.conic_split >= 0) return h.conic_split != 0;
+  return h.m > 2 * PAIR_ROWS;   // several row blocks per problem: spread them over CUs
+}
+
 static void conic_lsqr(Handle& h, double tol, double* out) {
   const int B = (int)h.batch, m = h.m, n = h.n;
   const int nc = (int)h.cones.size() / 2;
@@ -735,6 +1125,10 @@ static void conic_lsqr(Handle& h, double tol, double* out) {
   h.cwork.ensure((size_t)B * (wl + N) * sizeof(double));
   h.cinfo.ensure((size_t)2 * std::max(B, 1) * sizeof(int32_t));
   double* rhs = h.cwork.as<double>() + (size_t)B * wl;
+  if (use_split(h)) {
+    conic_lsqr_split(h, tol, rhs, out);
+    return;
+  }
   PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
   hipLaunchKernelGGL(conic_lsqr_kernel, dim3(B), dim3(CTPB), dpi_lds_bytes(h.cones), h.stream,
                      h.cone_dev.as<ConeDesc>(), nc, h.cA, h.cb, h.cc, h.vp.as<double>(),

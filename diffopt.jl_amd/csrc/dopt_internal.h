@@ -111,6 +111,8 @@ struct Handle {
   std::vector<int32_t> cones;   // (code, dim) pairs
   DevBuf cone_dev;              // device copy of cone table (+ offsets)
   DevBuf vp, dpi, M, cwork, cinfo;
+  DevBuf csplit;                // split-path LSQR vectors, partial products, state
+  int32_t conic_split = -1;     // -1 auto, 0 persistent kernel, 1 split (env DOPT_CONIC_SPLIT)
   int32_t dpi_len = 0;          // doubles per problem of packed Dπ blocks
   bool cset = false, cfactored = false;
 

@@ -10,6 +10,9 @@ import os
 
 LIB_NAME = "libdiffopt_mi355x.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+if os.environ.get("DOPT_LIB_VARIANT"):
+    # tuning builds (libdiffopt_mi355x.<variant>.so next to the product library)
+    LIB_PATH = LIB_PATH[:-3] + "." + os.environ["DOPT_LIB_VARIANT"] + ".so"
 
 DOPT_KIND_QP = 0
 DOPT_KIND_CONIC = 1

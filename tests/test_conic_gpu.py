@@ -189,3 +189,56 @@ def test_zero_rhs_gives_zero(ConicBatch):
     g, _, _, _ = e.reverse(np.full((2, 8), 1e-6))  # ‖dz‖ ≤ 1e-4 (:369-370)
     assert np.all(g == 0)
     e.close()
+
+
+# ---------------------------------------------------------------------------
+# split path (row-block × problem grids, conic_split_* kernels): forced with
+# DOPT_CONIC_SPLIT=1 on the shapes above, and taken automatically for
+# m > 1024 (several row blocks per problem, partial Aᵀ products reduced)
+# ---------------------------------------------------------------------------
+@pytest.fixture
+def SplitConicBatch(ConicBatch, monkeypatch):
+    monkeypatch.setenv("DOPT_CONIC_SPLIT", "1")
+    return ConicBatch
+
+
+def test_split_mixed_cones_batch(SplitConicBatch):
+    _synthetic_check(SplitConicBatch, 6, 30, [(0, 3), (1, 10), (3, 6), (2, 4), (4, 6)], 11)
+
+
+def test_split_well_posed_batch(SplitConicBatch):
+    w = _synthetic_check(SplitConicBatch, 2, 100, [(3, 10)] * 20, 21)
+    assert max(w.values()) <= 1e-5, w
+
+
+def test_split_psd_blocks_batch(SplitConicBatch):
+    _synthetic_check(SplitConicBatch, 3, 25, [(4, 10), (4, 15), (1, 5)], 13)
+
+
+def test_split_zero_rhs_gives_zero(SplitConicBatch):
+    test_zero_rhs_gives_zero(SplitConicBatch)
+
+
+def test_split_matches_persistent_kernel(ConicBatch, monkeypatch):
+    # same problems through both LSQR drivers: identical algorithm, different
+    # summation order of the A products → agreement to the oracle bar
+    from diffopt_amd.synthetic import conic_numpy
+    cones = [(3, 10)] * 20
+    d = conic_numpy(3, 100, cones, 21)
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DOPT_CONIC_SPLIT", mode)
+        e = ConicBatch(3, 100, cones)
+        e.set(d["A"], d["b"], d["c"], d["x"], d["s"], d["y"])
+        out, _ = e.forward(d["dA"], d["db"], d["dc"])
+        g = e.reverse(d["dx"])[0]
+        res[mode] = (np.asarray(out), np.asarray(g), e.iterations())
+        e.close()
+    assert relfro(res["1"][0], res["0"][0]) <= 1e-5
+    assert relfro(res["1"][1], res["0"][1]) <= 1e-5
+
+
+def test_config5_shape_multi_rowblock(ConicBatch):
+    # BASELINE config 5 structure (PSD(50) cones, m ≫ n) scaled to oracle
+    # speed: 3 PSD(50) → m = 3825 = 8 row blocks, auto split path
+    _synthetic_check(ConicBatch, 2, 100, [(4, 1275)] * 3, 16)
