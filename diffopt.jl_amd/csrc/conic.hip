@@ -221,6 +221,38 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
 //   trans = 0: out = Dπ in ;  trans = 1: out = Dπᵀ in.   in/out: m vectors.
 // PSD scratch in LDS (`lds`, ≥ 3·PSD_MAX·(PSD_MAX+1) doubles).
 // ---------------------------------------------------------------------------
+// C(i, j) = Σ_{q<d} a(i, q)·b(q, j) over a dp×dp grid of 4×4 register tiles
+// (one tile per thread per pass); `upper` skips tiles strictly below the
+// diagonal.  a, b read LDS; st(i, j, v) stores.
+template <class FA, class FB, class FS>
+__device__ __forceinline__ void psd_gemm4(int d, int dp, bool upper, FA a, FB b, FS st) {
+  const int nt = dp >> 2;
+  for (int tile = threadIdx.x; tile < nt * nt; tile += CTPB) {
+    const int ti = tile / nt, tj = tile % nt;
+    if (upper && tj < ti) continue;
+    double acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = 0.0;
+    for (int q = 0; q < d; ++q) {
+      double av[4], bv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) av[r] = a(4 * ti + r, q);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) bv[c] = b(q, 4 * tj + c);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = fma(av[r], bv[c], acc[r][c]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) st(4 * ti + r, 4 * tj + c, acc[r][c]);
+  }
+}
+
 __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, const double* __restrict__ v,
                           const double* __restrict__ P, const double* in, double* out,
                           int trans, double* lds, double* red) {
@@ -263,15 +295,19 @@ __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, con
     }
   }
   __syncthreads();
-  // PSD cones: whole workgroup per cone
-  double* Xs = lds;                                  // d × (d+1)
+  // PSD cones: whole workgroup per cone; the four d×d products run on 4×4
+  // register tiles (8 LDS reads per 16 FMAs) over the side padded to dp =
+  // round_up(d, 4); padded rows/columns are zero on load and the q-sums stop
+  // at d, so they never reach a kept entry.
+  double* Xs = lds;                                  // dp × (dp+1)
   double* Ys = lds + PSD_MAX * (PSD_MAX + 1);
   double* Us = lds + 2 * PSD_MAX * (PSD_MAX + 1);
   for (int k = 0; k < ncones; ++k) {
     const ConeDesc cd = cones[k];
     if (cd.code != DOPT_CONE_PSD_TRI) continue;
     const int d = psd_side(cd.dim);
-    const int ld = d + 1;
+    const int dp = (d + 3) & ~3;
+    const int ld = dp + 1;
     const double* U = P + cd.poff;
     const double* Bm = U + d * d;
     const bool ident = U[2 * d * d] != 0.0;
@@ -282,48 +318,40 @@ __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, con
       continue;
     }
     // X = smat(S^{-2} w) for Dπ (=Jᵀ = S²JS⁻²), smat(w) for Dπᵀ (= J)
-    for (int e = t; e < d * d; e += CTPB) {
-      const int i = e / d, j = e % d;
-      const int a = i <= j ? i : j, c = i <= j ? j : i;
-      double val = w[tri_idx(a, c)];
-      if (!trans && a != c) val *= 0.5;
+    for (int e = t; e < dp * dp; e += CTPB) {
+      const int i = e / dp, j = e % dp;
+      double val = 0.0, uv = 0.0;
+      if (i < d && j < d) {
+        const int a = i <= j ? i : j, c = i <= j ? j : i;
+        val = w[tri_idx(a, c)];
+        if (!trans && a != c) val *= 0.5;
+        uv = U[i * d + j];
+      }
       Xs[i * ld + j] = val;
-      Us[i * ld + j] = U[i * d + j];
+      Us[i * ld + j] = uv;
     }
     __syncthreads();
     // Y = Uᵀ X
-    for (int e = t; e < d * d; e += CTPB) {
-      const int i = e / d, j = e % d;
-      double acc = 0.0;
-      for (int q = 0; q < d; ++q) acc = fma(Us[q * ld + i], Xs[q * ld + j], acc);
-      Ys[i * ld + j] = acc;
-    }
+    psd_gemm4(d, dp, false, [&](int i, int q) { return Us[q * ld + i]; },
+              [&](int q, int j) { return Xs[q * ld + j]; },
+              [&](int i, int j, double v) { Ys[i * ld + j] = v; });
     __syncthreads();
     // X = (Y U) ∘ B
-    for (int e = t; e < d * d; e += CTPB) {
-      const int i = e / d, j = e % d;
-      double acc = 0.0;
-      for (int q = 0; q < d; ++q) acc = fma(Ys[i * ld + q], Us[q * ld + j], acc);
-      Xs[i * ld + j] = acc * Bm[i * d + j];
-    }
+    psd_gemm4(d, dp, false, [&](int i, int q) { return Ys[i * ld + q]; },
+              [&](int q, int j) { return Us[q * ld + j]; },
+              [&](int i, int j, double v) { Xs[i * ld + j] = (i < d && j < d) ? v * Bm[i * d + j] : 0.0; });
     __syncthreads();
     // Y = U X
-    for (int e = t; e < d * d; e += CTPB) {
-      const int i = e / d, j = e % d;
-      double acc = 0.0;
-      for (int q = 0; q < d; ++q) acc = fma(Us[i * ld + q], Xs[q * ld + j], acc);
-      Ys[i * ld + j] = acc;
-    }
+    psd_gemm4(d, dp, false, [&](int i, int q) { return Us[i * ld + q]; },
+              [&](int q, int j) { return Xs[q * ld + j]; },
+              [&](int i, int j, double v) { Ys[i * ld + j] = v; });
     __syncthreads();
-    // out = tri(Y Uᵀ), times S² for Dπ
-    for (int e = t; e < cd.dim; e += CTPB) {
-      int j = 0;
-      while ((j + 1) * (j + 2) / 2 <= e) ++j;
-      const int i = e - j * (j + 1) / 2;
-      double acc = 0.0;
-      for (int q = 0; q < d; ++q) acc = fma(Ys[i * ld + q], Us[j * ld + q], acc);
-      o[e] = (!trans && i != j) ? 2.0 * acc : acc;
-    }
+    // out = tri(Y Uᵀ) (upper-triangle tiles only), times S² for Dπ
+    psd_gemm4(d, dp, true, [&](int i, int q) { return Ys[i * ld + q]; },
+              [&](int q, int j) { return Us[j * ld + q]; },
+              [&](int i, int j, double v) {
+                if (i <= j && j < d) o[tri_idx(i, j)] = (!trans && i != j) ? 2.0 * v : v;
+              });
     __syncthreads();
   }
   __syncthreads();
@@ -338,11 +366,12 @@ __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, con
 // PAIR_NC columns are in flight per wave (PAIR_NC·PAIR_K independent loads).
 constexpr int PAIR_K = 8;
 #ifndef DOPT_PAIR_NC
-#define DOPT_PAIR_NC 4
+#define DOPT_PAIR_NC 2
 #endif
 constexpr int PAIR_NC = DOPT_PAIR_NC;   // columns in flight per wave
 constexpr int PAIR_ROWS = 64 * PAIR_K;
 
+template <int PK = PAIR_K>
 __device__ __forceinline__ void gemv_pair(const double* __restrict__ A, int ld, int m, int n,
                                           const double* __restrict__ x, const double* __restrict__ w,
                                           double* __restrict__ y, double* __restrict__ g,
@@ -353,11 +382,11 @@ __device__ __forceinline__ void gemv_pair(const double* __restrict__ A, int ld, 
     __syncthreads();
     return;
   }
-  for (int r0 = 0; r0 < m; r0 += PAIR_ROWS) {
-    double wr[PAIR_K], ya[PAIR_K];
-    bool ok[PAIR_K];
+  for (int r0 = 0; r0 < m; r0 += (64 * PK)) {
+    double wr[PK], ya[PK];
+    bool ok[PK];
 #pragma unroll
-    for (int k = 0; k < PAIR_K; ++k) {
+    for (int k = 0; k < PK; ++k) {
       const int i = r0 + lane + 64 * k;
       ok[k] = i < m;
       wr[k] = ok[k] ? w[i] : 0.0;
@@ -366,12 +395,12 @@ __device__ __forceinline__ void gemv_pair(const double* __restrict__ A, int ld, 
     const double* Ar = A + r0 + lane;
     int j = wv;
     for (; j + 4 * (PAIR_NC - 1) < n; j += 4 * PAIR_NC) {
-      double a[PAIR_NC][PAIR_K];
+      double a[PAIR_NC][PK];
 #pragma unroll
       for (int c = 0; c < PAIR_NC; ++c) {
         const double* cc = Ar + (size_t)(j + 4 * c) * ld;
 #pragma unroll
-        for (int k = 0; k < PAIR_K; ++k) a[c][k] = ok[k] ? cc[64 * k] : 0.0;
+        for (int k = 0; k < PK; ++k) a[c][k] = ok[k] ? cc[64 * k] : 0.0;
       }
       double sc[PAIR_NC];
 #pragma unroll
@@ -379,7 +408,7 @@ __device__ __forceinline__ void gemv_pair(const double* __restrict__ A, int ld, 
         const double xc = x[j + 4 * c];
         double acc = 0.0;
 #pragma unroll
-        for (int k = 0; k < PAIR_K; ++k) {
+        for (int k = 0; k < PK; ++k) {
           acc = fma(a[c][k], wr[k], acc);
           ya[k] = fma(a[c][k], xc, ya[k]);
         }
@@ -397,13 +426,13 @@ __device__ __forceinline__ void gemv_pair(const double* __restrict__ A, int ld, 
     }
     for (; j < n; j += 4) {
       const double* c0 = Ar + (size_t)j * ld;
-      double a0[PAIR_K];
+      double a0[PK];
 #pragma unroll
-      for (int k = 0; k < PAIR_K; ++k) a0[k] = ok[k] ? c0[64 * k] : 0.0;
+      for (int k = 0; k < PK; ++k) a0[k] = ok[k] ? c0[64 * k] : 0.0;
       const double x0 = x[j];
       double s0 = 0.0;
 #pragma unroll
-      for (int k = 0; k < PAIR_K; ++k) {
+      for (int k = 0; k < PK; ++k) {
         s0 = fma(a0[k], wr[k], s0);
         ya[k] = fma(a0[k], x0, ya[k]);
       }
@@ -411,10 +440,10 @@ __device__ __forceinline__ void gemv_pair(const double* __restrict__ A, int ld, 
       if (lane == 0) g[j] = r0 ? g[j] + s0 : s0;
     }
 #pragma unroll
-    for (int k = 0; k < PAIR_K; ++k) ys[wv * PAIR_ROWS + lane + 64 * k] = ya[k];
+    for (int k = 0; k < PK; ++k) ys[wv * (64 * PK) + lane + 64 * k] = ya[k];
     __syncthreads();
-    for (int r = threadIdx.x; r < PAIR_ROWS && r0 + r < m; r += CTPB)
-      y[r0 + r] = (ys[r] + ys[PAIR_ROWS + r]) + (ys[2 * PAIR_ROWS + r] + ys[3 * PAIR_ROWS + r]);
+    for (int r = threadIdx.x; r < (64 * PK) && r0 + r < m; r += CTPB)
+      y[r0 + r] = (ys[r] + ys[(64 * PK) + r]) + (ys[2 * (64 * PK) + r] + ys[3 * (64 * PK) + r]);
     __syncthreads();
   }
 }
@@ -708,6 +737,11 @@ __global__ __launch_bounds__(CTPB) void conic_rev_out_kernel(
 // of unfinished problems every SPLIT_CHUNK iterations.
 // ---------------------------------------------------------------------------
 constexpr int SPLIT_CHUNK = 8;
+#ifndef DOPT_SPLIT_K
+#define DOPT_SPLIT_K 8
+#endif
+constexpr int SPLIT_K = DOPT_SPLIT_K;            // rows per lane of a split row block
+constexpr int SPLIT_ROWS = 64 * SPLIT_K;
 
 struct LsqrState {
   double alpha, beta, rhobar, phibar, anorm, ddnorm, xxnorm, zz, sn2, cs2, bnorm, pad;
@@ -758,18 +792,18 @@ __global__ __launch_bounds__(CTPB) void conic_split_init_kernel(
 __global__ __launch_bounds__(CTPB) void conic_split_pass_kernel(
     int dir, const double* __restrict__ A, const double* __restrict__ bvec, SplitWS ws,
     const LsqrState* __restrict__ stv) {
-  __shared__ double ys[4 * PAIR_ROWS];
+  __shared__ double ys[4 * SPLIT_ROWS];
   const int rb = blockIdx.x, b = blockIdx.y;
   const LsqrState& st = stv[b];
   if (st.done || (dir == 1 && st.skipT)) return;
   const int m = ws.m, n = ws.n, N = ws.N;
-  const int r0 = rb * PAIR_ROWS;
-  const int rows = min(PAIR_ROWS, m - r0);
+  const int r0 = rb * SPLIT_ROWS;
+  const int rows = min(SPLIT_ROWS, m - r0);
   const double* Ab = A + (size_t)b * m * n + r0;
   const double* src = dir == 0 ? ws.vec(ws.v, b) : ws.vec(ws.u, b);
   const double* wv = dir == 0 ? ws.mvec(ws.Dv, b) + r0 : src + n + r0;
   double* yb = ws.mvec(ws.yb, b) + r0;
-  gemv_pair(Ab, m, rows, n, src, wv, yb, ws.gpart + ((size_t)b * ws.RB + rb) * n, ys);
+  gemv_pair<SPLIT_K>(Ab, m, rows, n, src, wv, yb, ws.gpart + ((size_t)b * ws.RB + rb) * n, ys);
   const double last = src[N - 1];
   const double* bb = bvec + (size_t)b * m + r0;
   if (dir == 0) {
@@ -802,11 +836,79 @@ __global__ __launch_bounds__(CTPB) void conic_split_dpi_kernel(
     dpi_apply(&cd, 1, pv, pp, ws.mvec(ws.tmpm, b), ws.vec(ws.out, b) + ws.n, 1, lds, red);
 }
 
+// The per-problem vector kernels below run 1024-thread workgroups and issue
+// VU independent loads per thread before using them (vectors of N = 13 251
+// doubles at config 5 would otherwise serialise on load latency).
+constexpr int VT = 1024;
+constexpr int VU = 4;
+
+__device__ __forceinline__ double vblock_sum(double v, double* red) {
+  v = cwave_sum(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < VT / 64; ++k) s += red[k];
+  return s;
+}
+
+// Σ_rb gpart[rb][j] (the row blocks' partial Aᵀ products) for j = threadIdx.x
+// + k·VT; four independent accumulators
+__device__ __forceinline__ double gpart_sum(const double* __restrict__ gp, int RB, int n, int j) {
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int r = 0;
+  for (; r + 3 < RB; r += 4) {
+    s0 += gp[(size_t)r * n + j];
+    s1 += gp[(size_t)(r + 1) * n + j];
+    s2 += gp[(size_t)(r + 2) * n + j];
+    s3 += gp[(size_t)(r + 3) * n + j];
+  }
+  for (; r < RB; ++r) s0 += gp[(size_t)r * n + j];
+  return (s0 + s1) + (s2 + s3);
+}
+
+// dst ← (src − coef·dst), returns Σ dst² (block-wide); all N entries
+__device__ __forceinline__ double axpy_norm2(double* __restrict__ dst, const double* __restrict__ src,
+                                             double coef, int N, double* red) {
+  const int t = threadIdx.x;
+  double acc = 0.0;
+  for (int i0 = t; i0 < N; i0 += VU * VT) {
+    double sv[VU], dv[VU];
+#pragma unroll
+    for (int k = 0; k < VU; ++k) {
+      const int i = i0 + k * VT;
+      sv[k] = i < N ? src[i] : 0.0;
+      dv[k] = i < N ? dst[i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < VU; ++k) {
+      const int i = i0 + k * VT;
+      const double r = sv[k] - coef * dv[k];
+      if (i < N) dst[i] = r;
+      acc = fma(r, r, acc);
+    }
+  }
+  return vblock_sum(acc, red);
+}
+
+__device__ __forceinline__ void vscale(double* __restrict__ v, int N, double div) {
+  const int t = threadIdx.x;
+  for (int i0 = t; i0 < N; i0 += VU * VT) {
+    double a[VU];
+#pragma unroll
+    for (int k = 0; k < VU; ++k) { const int i = i0 + k * VT; a[k] = i < N ? v[i] : 0.0; }
+#pragma unroll
+    for (int k = 0; k < VU; ++k) { const int i = i0 + k * VT; if (i < N) v[i] = a[k] / div; }
+  }
+}
+
 // out_n = −Σ_rb gpart + c·v_last, out_end = −c·v_n − b·Dv; then u ← out − αu
-__global__ __launch_bounds__(CTPB) void conic_split_upd_u_kernel(
+__global__ __launch_bounds__(VT) void conic_split_upd_u_kernel(
     const double* __restrict__ bvec, const double* __restrict__ cvec, SplitWS ws,
     LsqrState* __restrict__ stv) {
-  __shared__ double red[4];
+  __shared__ double red[VT / 64];
   const int b = blockIdx.x, t = threadIdx.x;
   LsqrState st = stv[b];
   if (st.done) return;
@@ -820,25 +922,26 @@ __global__ __launch_bounds__(CTPB) void conic_split_upd_u_kernel(
   const double* gp = ws.gpart + (size_t)b * ws.RB * n;
   const double w = v[N - 1];
   double cu = 0.0, bd = 0.0;
-  for (int j = t; j < n; j += CTPB) {
-    double g = 0.0;
-    for (int r = 0; r < ws.RB; ++r) g += gp[(size_t)r * n + j];
-    out[j] = -g + c[j] * w;
+  for (int j = t; j < n; j += VT) {
+    out[j] = -gpart_sum(gp, ws.RB, n, j) + c[j] * w;
     cu = fma(c[j], v[j], cu);
   }
-  for (int i = t; i < m; i += CTPB) bd = fma(bb[i], Dv[i], bd);
-  const double se = cblock_sum(-cu - bd, red);
+  for (int i0 = t; i0 < m; i0 += VU * VT) {
+    double x0[VU], x1[VU];
+#pragma unroll
+    for (int k = 0; k < VU; ++k) {
+      const int i = i0 + k * VT;
+      x0[k] = i < m ? bb[i] : 0.0;
+      x1[k] = i < m ? Dv[i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < VU; ++k) bd = fma(x0[k], x1[k], bd);
+  }
+  const double se = vblock_sum(-cu - bd, red);
   if (t == 0) out[N - 1] = se;
   __syncthreads();
-  double su = 0.0;
-  for (int i = t; i < N; i += CTPB) {
-    const double ui = out[i] - st.alpha * u[i];
-    u[i] = ui;
-    su = fma(ui, ui, su);
-  }
-  const double beta = sqrt(cblock_sum(su, red));
-  if (beta > 0.0)
-    for (int i = t; i < N; i += CTPB) u[i] /= beta;
+  const double beta = sqrt(axpy_norm2(u, out, st.alpha, N, red));
+  if (beta > 0.0) vscale(u, N, beta);
   if (t == 0) {
     st.it += 1;
     st.beta = beta;
@@ -860,26 +963,38 @@ __device__ __forceinline__ void split_finish_T(const SplitWS& ws, int b, const d
   const double* gp = ws.gpart + (size_t)b * ws.RB * n;
   const double tw = u[N - 1];
   double cp = 0.0, bq = 0.0;
-  for (int j = t; j < n; j += CTPB) {
-    double g = 0.0;
-    for (int r = 0; r < ws.RB; ++r) g += gp[(size_t)r * n + j];
-    out[j] = g - c[j] * tw;
+  for (int j = t; j < n; j += VT) {
+    out[j] = gpart_sum(gp, ws.RB, n, j) - c[j] * tw;
     cp = fma(c[j], u[j], cp);
   }
-  for (int i = t; i < m; i += CTPB) {
-    out[n + i] += u[n + i];
-    bq = fma(bb[i], u[n + i], bq);
+  const double* um = u + n;
+  double* om = out + n;
+  for (int i0 = t; i0 < m; i0 += VU * VT) {
+    double a[VU], q[VU], bv[VU];
+#pragma unroll
+    for (int k = 0; k < VU; ++k) {
+      const int i = i0 + k * VT;
+      a[k] = i < m ? om[i] : 0.0;
+      q[k] = i < m ? um[i] : 0.0;
+      bv[k] = i < m ? bb[i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < VU; ++k) {
+      const int i = i0 + k * VT;
+      if (i < m) om[i] = a[k] + q[k];
+      bq = fma(bv[k], q[k], bq);
+    }
   }
-  const double se = cblock_sum(cp + bq, red);
+  const double se = vblock_sum(cp + bq, red);
   if (t == 0) out[N - 1] = se;
   __syncthreads();
 }
 
 // first Mᵀ·u: v = Mᵀu/α, w = v, recurrence initial values
-__global__ __launch_bounds__(CTPB) void conic_split_init2_kernel(
+__global__ __launch_bounds__(VT) void conic_split_init2_kernel(
     const double* __restrict__ bvec, const double* __restrict__ cvec, SplitWS ws,
     LsqrState* __restrict__ stv, int32_t* __restrict__ active) {
-  __shared__ double red[4];
+  __shared__ double red[VT / 64];
   const int b = blockIdx.x, t = threadIdx.x, N = ws.N;
   LsqrState st = stv[b];
   if (st.done) return;
@@ -888,10 +1003,10 @@ __global__ __launch_bounds__(CTPB) void conic_split_init2_kernel(
   double* v = ws.vec(ws.v, b);
   double* w = ws.vec(ws.w, b);
   double aa = 0.0;
-  for (int i = t; i < N; i += CTPB) aa = fma(out[i], out[i], aa);
-  const double alpha = sqrt(cblock_sum(aa, red));
+  for (int i = t; i < N; i += VT) aa = fma(out[i], out[i], aa);
+  const double alpha = sqrt(vblock_sum(aa, red));
   if (alpha > 0.0)
-    for (int i = t; i < N; i += CTPB) { const double vi = out[i] / alpha; v[i] = vi; w[i] = vi; }
+    for (int i = t; i < N; i += VT) { const double vi = out[i] / alpha; v[i] = vi; w[i] = vi; }
   if (t == 0) {
     st.alpha = alpha;
     st.anorm = st.ddnorm = st.xxnorm = st.zz = st.sn2 = 0.0;
@@ -906,10 +1021,10 @@ __global__ __launch_bounds__(CTPB) void conic_split_init2_kernel(
   }
 }
 
-__global__ __launch_bounds__(CTPB) void conic_split_upd_v_kernel(
+__global__ __launch_bounds__(VT) void conic_split_upd_v_kernel(
     const double* __restrict__ bvec, const double* __restrict__ cvec, SplitWS ws,
     LsqrState* __restrict__ stv, int maxiter, int32_t* __restrict__ active) {
-  __shared__ double red[4];
+  __shared__ double red[VT / 64];
   const int b = blockIdx.x, t = threadIdx.x, N = ws.N;
   LsqrState st = stv[b];
   if (st.done) return;
@@ -918,11 +1033,8 @@ __global__ __launch_bounds__(CTPB) void conic_split_upd_v_kernel(
   const double beta = st.beta;
   if (!st.skipT) {
     split_finish_T(ws, b, bvec, cvec, red);
-    const double* out = ws.vec(ws.out, b);
-    double sv = 0.0;
-    for (int i = t; i < N; i += CTPB) { const double vi = out[i] - beta * v[i]; v[i] = vi; sv = fma(vi, vi, sv); }
-    alpha = sqrt(cblock_sum(sv, red));
-    if (alpha > 0.0) for (int i = t; i < N; i += CTPB) v[i] /= alpha;
+    alpha = sqrt(axpy_norm2(v, ws.vec(ws.out, b), beta, N, red));
+    if (alpha > 0.0) vscale(v, N, alpha);
     __syncthreads();
   }
   const double rhobar1 = st.rhobar;
@@ -937,13 +1049,26 @@ __global__ __launch_bounds__(CTPB) void conic_split_upd_v_kernel(
   double* x = ws.vec(ws.x, b);
   double* w = ws.vec(ws.w, b);
   double sw = 0.0;
-  for (int i = t; i < N; i += CTPB) {
-    const double wi = w[i];
-    sw = fma(wi, wi, sw);
-    x[i] = x[i] + t1 * wi;
-    w[i] = v[i] + t2 * wi;
+  for (int i0 = t; i0 < N; i0 += VU * VT) {
+    double wv[VU], xv[VU], vv[VU];
+#pragma unroll
+    for (int k = 0; k < VU; ++k) {
+      const int i = i0 + k * VT;
+      wv[k] = i < N ? w[i] : 0.0;
+      xv[k] = i < N ? x[i] : 0.0;
+      vv[k] = i < N ? v[i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < VU; ++k) {
+      const int i = i0 + k * VT;
+      sw = fma(wv[k], wv[k], sw);
+      if (i < N) {
+        x[i] = xv[k] + t1 * wv[k];
+        w[i] = vv[k] + t2 * wv[k];
+      }
+    }
   }
-  const double ddnorm = st.ddnorm + cblock_sum(sw, red) / (rho * rho);
+  const double ddnorm = st.ddnorm + vblock_sum(sw, red) / (rho * rho);
   if (t != 0) return;
   const double eps = 2.220446049250313e-16;
   const double atol = sqrt(eps), btol = sqrt(eps), ctol = sqrt(eps);
@@ -1049,7 +1174,7 @@ static void conic_lsqr_split(Handle& h, double tol, const double* rhs, double* o
   const int B = (int)h.batch, m = h.m, n = h.n;
   const int nc = (int)h.cones.size() / 2;
   const int N = n + m + 1;
-  const int RB = std::max(1, (m + PAIR_ROWS - 1) / PAIR_ROWS);
+  const int RB = std::max(1, (m + SPLIT_ROWS - 1) / SPLIT_ROWS);
   const size_t per = (size_t)5 * N + 4 * (size_t)std::max(m, 1) + (size_t)RB * n;
   h.csplit.ensure((size_t)B * per * sizeof(double) + (size_t)B * sizeof(LsqrState) + 64);
   SplitWS ws;
@@ -1087,7 +1212,7 @@ static void conic_lsqr_split(Handle& h, double tol, const double* rhs, double* o
   hipLaunchKernelGGL(conic_split_init_kernel, dim3(B), dim3(CTPB), 0, h.stream, rhs, tol, ws, st,
                      active);
   passT();
-  hipLaunchKernelGGL(conic_split_init2_kernel, dim3(B), dim3(CTPB), 0, h.stream, h.cb, h.cc, ws,
+  hipLaunchKernelGGL(conic_split_init2_kernel, dim3(B), dim3(VT), 0, h.stream, h.cb, h.cc, ws,
                      st, active);
   ccheck();
   for (int it = 0; it < N && left > 0;) {
@@ -1097,10 +1222,10 @@ static void conic_lsqr_split(Handle& h, double tol, const double* rhs, double* o
                            vcone, P, h.dpi_len, ws, st);
       hipLaunchKernelGGL(conic_split_pass_kernel, dim3(RB, B), dim3(CTPB), 0, h.stream, 0, h.cA,
                          h.cb, ws, st);
-      hipLaunchKernelGGL(conic_split_upd_u_kernel, dim3(B), dim3(CTPB), 0, h.stream, h.cb, h.cc,
+      hipLaunchKernelGGL(conic_split_upd_u_kernel, dim3(B), dim3(VT), 0, h.stream, h.cb, h.cc,
                          ws, st);
       passT();
-      hipLaunchKernelGGL(conic_split_upd_v_kernel, dim3(B), dim3(CTPB), 0, h.stream, h.cb, h.cc,
+      hipLaunchKernelGGL(conic_split_upd_v_kernel, dim3(B), dim3(VT), 0, h.stream, h.cb, h.cc,
                          ws, st, N, active);
     }
     ccheck();
