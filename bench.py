@@ -225,7 +225,8 @@ def run_conic(args, world, rank, local_rank):
         per_launch = b_it * float(it_f.sum() + it_r.sum()) / 2.0
         achieved = per_launch / avg_s / 1e9
         roof = dict(bound="hbm", achieved=round(achieved, 1), peak=PEAK_HBM_GBS, unit="GB/s",
-                    frac=round(achieved / PEAK_HBM_GBS, 4), traffic=_load_pmc("conic_lsqr"),
+                    frac=round(achieved / PEAK_HBM_GBS, 4),
+                    traffic=_load_pmc("conic_lsqr_split" if args.config == 5 else "conic_lsqr"),
                     kernel="conic_lsqr", avg_launch_ms=round(avg_s * 1e3, 4),
                     bytes_per_iteration=b_it,
                     lsqr_iterations_mean={"forward": float(it_f.mean()), "reverse": float(it_r.mean())},

@@ -7,7 +7,7 @@ gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports ½ of the
 bytes of wide coalesced reads → doubled here; WRITE_SIZE is taken as is.
 FETCH_SIZE/WRITE_SIZE are in KB (rocprofv3 derived counters) → ×1024.
 
-  python tools/pmc_summary.py <fetch_dir> <write_dir> <out.json>
+  python tools/pmc_summary.py <fetch_dir> <write_dir> <out.json>   (merges into out.json)
 """
 import csv
 import glob
@@ -23,7 +23,12 @@ KERNEL_PHASE = {
     "qp_solve_fast_kernel": "qp_solve",
     "conic_lsqr_kernel": "conic_lsqr",
     "conic_cone_kernel": "conic_cone",
+    "conic_split_pass_kernel": "conic_split_pass",
 }
+# split-path LSQR: every conic_split_* dispatch belongs to the LSQR call opened
+# by the preceding conic_split_init_kernel; reported per LSQR call under the
+# bench's phase name "conic_lsqr" (key "conic_lsqr_split")
+SPLIT_FRAG, SPLIT_OPEN = "conic_split_", "conic_split_init_kernel"
 
 
 def per_launch(d, counter):
@@ -40,7 +45,21 @@ def per_launch(d, counter):
                 for frag, ph in KERNEL_PHASE.items():
                     if frag in kn:
                         acc[ph][row.get("Dispatch_Id")] += float(row["Counter_Value"])
-    return {ph: sum(v.values()) / len(v) for ph, v in acc.items() if v}
+    res = {ph: sum(v.values()) / len(v) for ph, v in acc.items() if v}
+    tot, calls = 0.0, set()
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                kn = row.get("Kernel_Name", "")
+                if SPLIT_FRAG in kn:
+                    tot += float(row["Counter_Value"])
+                    if SPLIT_OPEN in kn:
+                        calls.add(row.get("Dispatch_Id"))
+    if calls:
+        res["conic_lsqr_split"] = tot / len(calls)
+    return res
 
 
 def main():
@@ -55,6 +74,11 @@ def main():
         wb = write.get(ph, 0.0) * 1024
         res["kernels"][ph] = {"read_bytes_per_launch": rb, "write_bytes_per_launch": wb,
                               "hbm_bytes_per_launch": rb + wb}
+    if os.path.exists(out):          # merge: other configs' kernels stay
+        with open(out) as f:
+            old = json.load(f).get("kernels", {})
+        old.update(res["kernels"])
+        res["kernels"] = old
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
