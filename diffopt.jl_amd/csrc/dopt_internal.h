@@ -99,7 +99,11 @@ struct Handle {
   DevBuf dinv;               // per-problem diagonal-block inverses (split path)
   DevBuf stamps;             // diagnostic in-kernel cycle stamps (env DOPT_STAMPS=1)
   int32_t wg_per_cu = 2;     // persistent-grid occupancy of the fast kernels
-  int32_t fast_max = FAST_MAX_N;   // reduced sizes above this take the blocked path (env DOPT_FAST_MAX)
+  // reduced sizes above this take the blocked path (env DOPT_FAST_MAX).  Default 0:
+  // the blocked step path is faster at every measured size and batch
+  // (tools/route_sweep.py, profiles/r01f_route_sweep.jsonl: 1.5–1.8× at batch
+  // 1024, ≥ parity at batch 128); the fused kernel stays as an opt-in route.
+  int32_t fast_max = 0;
   int32_t blocked_npmax = 0;       // largest padded blocked system of the current factorisation
   bool has_generic = true;         // some problem exceeds BLOCKED_MAX (set by the read-back)
   bool set = false, factored = false;

@@ -525,6 +525,9 @@ __global__ void qp_factor_fast_kernel(QPIn, int, double*, int, int, double*, int
 __global__ void qp_solve_fast_kernel(QPIn, FwdTangents, const double*, int, const double*, int, int,
                                      const double*, const int32_t*, const int32_t*, const double*,
                                      const QPMeta*, double*, int, double*, int);
+__global__ void qp_prep_asm_kernel(QPIn, double*, int, int, double*, int32_t*, int32_t*, QPMeta*, int);
+int prep_asm_cap(int n, int m);
+size_t prep_asm_lds(int n, int cap);
 size_t fast_dyn_lds(int n);
 size_t fast_ws_stride();
 size_t fast_dinv_stride(int nmax);
@@ -559,16 +562,30 @@ static int fast_grid(Handle& h) {
 static int32_t* rpos_of(Handle& h) { return h.kidx.as<int32_t>() + (size_t)h.batch * h.m; }
 static int32_t* perm_of(Handle& h) { return h.ipiv.as<int32_t>(); }
 
+// fast_max == 0: no problem takes the fused route, so prepare + assembly run in
+// the standalone high-occupancy kernel (one workgroup per problem)
+static void prep_assemble(Handle& h) {
+  const int cap = prep_asm_cap(h.n, h.m);
+  hipLaunchKernelGGL(qp_prep_asm_kernel, dim3(h.batch), dim3(FAST_THREADS), prep_asm_lds(h.n, cap),
+                     h.stream, qp_inputs(h), h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(),
+                     h.kidx.as<int32_t>(), rpos_of(h), h.meta.as<QPMeta>(), cap);
+  check_launch();
+}
+
 void qp_factor(Handle& h) {
   if (!h.set) throw Error(-1, "dopt_qp_factor: dopt_qp_set has not been called");
   const int B = (int)h.batch;
   QPMeta* meta = h.meta.as<QPMeta>();
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_LU);
-    hipLaunchKernelGGL(qp_factor_fast_kernel, dim3(fast_grid(h)), dim3(FAST_THREADS), fast_dyn_lds(h.n), h.stream,
-                       qp_inputs(h), B, h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(),
-                       h.kidx.as<int32_t>(), rpos_of(h), perm_of(h), dinv_of(h), meta, h.fast_max);
-    check_launch();
+    if (h.fast_max == 0) {
+      prep_assemble(h);
+    } else {
+      hipLaunchKernelGGL(qp_factor_fast_kernel, dim3(fast_grid(h)), dim3(FAST_THREADS), fast_dyn_lds(h.n),
+                         h.stream, qp_inputs(h), B, h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(),
+                         h.kidx.as<int32_t>(), rpos_of(h), perm_of(h), dinv_of(h), meta, h.fast_max);
+      check_launch();
+    }
     if (h.nmax > h.fast_max) qp_blocked_factor(h, dinv_of(h));
     if (h.nmax > BLOCKED_MAX && h.has_generic) {
       hipLaunchKernelGGL(qp_lu_generic_kernel, dim3(B), dim3(TPB), 0, h.stream, h.K.as<double>(),
@@ -696,10 +713,13 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
   const int B = (int)h.batch;
   const int grid = fast_grid(h);
   const size_t ws_stride = fast_ws_stride();
-  h.ws.ensure((size_t)grid * ws_stride * sizeof(double));
   double* full = full_of(h);
   const FwdTangents T = tangents(h, dQ, dq, dG, dh, dA, db);
-  {
+  if (h.fast_max == 0) {
+    PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
+    prep_assemble(h);
+  } else {
+    h.ws.ensure((size_t)grid * ws_stride * sizeof(double));
     PhaseTimer pt(h, DOPT_PHASE_QP_FUSED);
     hipLaunchKernelGGL(qp_fused_kernel, dim3(grid), dim3(FAST_THREADS), fast_dyn_lds(h.n), h.stream,
                        qp_inputs(h), T, dl_dz, B, h.ws.as<double>(), ws_stride, h.K.as<double>(), h.ld,

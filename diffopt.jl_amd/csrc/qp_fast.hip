@@ -513,10 +513,14 @@ __device__ __forceinline__ int prepare_wg(const QPIn& P, int b, double* s_out, i
 // transposed through a wave-private LDS tile.  Every global load is
 // unconditional (a select picks the source address, out-of-block elements
 // read a dummy and are discarded), so a tile's loads are in flight together.
-// kidx, λ_k and s_k are staged in LDS (perm / y / tmp are free here).
-__device__ __forceinline__ void assemble_wg(const QPIn& P, int b, const double* s,
-                                            const int32_t* kidx, int nk, double* K, int ld,
-                                            FastLDS& S) {
+// kidx, λ_k and s_k are staged in LDS (`kid`, `lamk`, `sk`, `cap` entries:
+// FastLDS's perm / y / tmp, free here, or the dynamic LDS of the standalone
+// assembly kernel); kept sets larger than `cap` are gathered from global
+// memory instead (`tiles` = one 16×17 transpose tile per wave).
+__device__ __forceinline__ void assemble_rows(const QPIn& P, int b, const double* s,
+                                              const int32_t* kidx, int nk, double* K, int ld,
+                                              int* kid_l, double* lamk_l, double* sk_l, int cap,
+                                              double (*tiles)[16 * 17]) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n = P.n, m = P.m, p = P.p;
   const int N = n + nk + p;
@@ -526,21 +530,23 @@ __device__ __forceinline__ void assemble_wg(const QPIn& P, int b, const double* 
   const double* lb = P.lam + (size_t)b * m;
   const double* sb = s + (size_t)b * m;
   const int32_t* kb = kidx + (size_t)b * m;
-  int* kid = S.perm;
-  double* lamk = S.y;
-  double* sk = S.tmp;
-  for (int i = t; i < nk; i += FT) {
-    const int k = kb[i];
-    kid[i] = k;
-    lamk[i] = lb[k];
-    sk[i] = sb[k];
+  const bool staged = nk <= cap;
+  if (staged) {
+    for (int i = t; i < nk; i += (int)blockDim.x) {
+      const int k = kb[i];
+      kid_l[i] = k;
+      lamk_l[i] = lb[k];
+      sk_l[i] = sb[k];
+    }
   }
   __syncthreads();
-  double* tl = S.atile[wv];
+  const int* kid = staged ? kid_l : kb;
+  double* tl = tiles[wv];
+  const int NWB = (int)blockDim.x >> 6;
   const int Np = (N + 31) & ~31;
   const int T = Np >> 4;
   const int lr = lane & 15, lg = lane >> 4;
-  for (int tile = wv; tile < T * T; tile += NW) {
+  for (int tile = wv; tile < T * T; tile += NWB) {
     const int r0 = (tile / T) * 16, c0 = (tile % T) * 16;
     if (c0 < n) {
       // transpose stage: lane reads source rows r0+lr, columns c0+lg+4q
@@ -571,7 +577,7 @@ __device__ __forceinline__ void assemble_wg(const QPIn& P, int b, const double* 
     const int ci = cG ? c - n : 0;
     const double* cbase = cG ? Gb + kid[ci] : (cA ? Ab + (c - n - nk) : Qb);
     const size_t rstride = cG ? (size_t)m : (cA ? (size_t)p : 0);
-    const double mul = cG ? lamk[ci] : 1.0;
+    const double mul = cG ? (staged ? lamk_l[ci] : lb[kid[ci]]) : 1.0;
     double v[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -581,7 +587,10 @@ __device__ __forceinline__ void assemble_wg(const QPIn& P, int b, const double* 
       double val;
       if (c < n) val = tl[lr * 17 + lg + 4 * q];
       else if (ld_ok) val = v[q] * mul;
-      else if (r == c) val = (r >= N) ? 1.0 : ((r >= n && r < n + nk) ? sk[max(r - n, 0)] : 0.0);
+      else if (r == c) {
+        const int ki = max(r - n, 0);
+        val = (r >= N) ? 1.0 : ((r >= n && r < n + nk) ? (staged ? sk_l[ki] : sb[kid[ki]]) : 0.0);
+      }
       else val = 0.0;
       v[q] = val;
     }
@@ -590,6 +599,12 @@ __device__ __forceinline__ void assemble_wg(const QPIn& P, int b, const double* 
     __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
+}
+
+__device__ __forceinline__ void assemble_wg(const QPIn& P, int b, const double* s,
+                                            const int32_t* kidx, int nk, double* K, int ld,
+                                            FastLDS& S) {
+  assemble_rows(P, b, s, kidx, nk, K, ld, S.perm, S.y, S.tmp, FAST_MAX, S.atile);
 }
 
 __device__ __forceinline__ void rev_rhs_wg(const double* dl_dz, int b, int n, int N, FastLDS& S) {
@@ -805,6 +820,37 @@ __global__ __launch_bounds__(FT) void qp_solve_fast_kernel(
     output_wg(P, b, S.y, s, rpos, nk, full, nmax, trans, out);
   }
 }
+
+// Standalone prepare + assembly for the blocked / generic / LSQR routes (the
+// default route: fast_max = 0).  One 512-thread workgroup per problem with a
+// slim LDS footprint (z, the kept-row staging, the transpose tiles), so
+// several problems share a CU, unlike the 256-VGPR fused kernel (one
+// workgroup per CU) that otherwise does this work.  Same per-problem code, so
+// s, the kept set and K are bit-identical to the fused kernel's.
+__global__ __launch_bounds__(FT) void qp_prep_asm_kernel(
+    QPIn P, double* __restrict__ Kper, int ld_per, int nmax, double* __restrict__ s,
+    int32_t* __restrict__ kidx, int32_t* __restrict__ rpos, QPMeta* __restrict__ meta, int cap) {
+  __shared__ double tiles[NW][16 * 17];
+  __shared__ int cnt[NW + 1];
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
+  double* zsm = dyn;                           // n
+  double* lamk = zsm + P.n;                    // cap
+  double* sk = lamk + cap;                     // cap
+  int* kid = (int*)(sk + cap);                 // cap
+  const int b = blockIdx.x;
+  prepare_wg(P, b, s, kidx, rpos, meta, zsm, cnt);
+  const int nk = meta[b].nk;
+  assemble_rows(P, b, s, kidx, nk, Kper + (size_t)b * nmax * ld_per, ld_per, kid, lamk, sk, cap,
+                tiles);
+}
+
+// kept-row staging capacity of qp_prep_asm_kernel (all of m while the dynamic
+// LDS stays ≤ 64 KB; beyond that the assembly gathers from global memory)
+int prep_asm_cap(int n, int m) {
+  const int avail = (64 * 1024 - std::max(n, 1) * 8) / 20;
+  return std::max(0, std::min(m, avail));
+}
+size_t prep_asm_lds(int n, int cap) { return (size_t)std::max(n, 1) * 8 + (size_t)cap * 20; }
 
 size_t fast_dyn_lds(int n) { return (size_t)std::max(n, 1) * sizeof(double); }
 size_t fast_ws_stride() { return (size_t)FAST_MAX * FAST_MAX + (size_t)(FAST_MAX / FNB) * DINV_STRIDE; }

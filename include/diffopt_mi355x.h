@@ -75,7 +75,7 @@ int dopt_abi_version(void);
 int dopt_set_stream(dopt_handle* h, void* stream);
 int dopt_set_memory(dopt_handle* h, int32_t mem);
 /* QP factorisation path threshold: problems whose reduced KKT size is
- * ≤ fast_max (0..512, default 512, env DOPT_FAST_MAX) use the fused
+ * ≤ fast_max (0..512, default 0, env DOPT_FAST_MAX) use the fused
  * one-workgroup-per-problem kernel; larger ones (≤ 1536) the blocked step
  * path that spreads each LU over the whole GPU; beyond that a generic kernel.
  * Results agree to rounding; this is a performance setting (no reference

@@ -142,6 +142,16 @@ def test_blocked_path_cfg3_shape(QPBatch):
     _check_batch(QPBatch, _synthetic(2, 1000, 1500, 0, 0.3, 20250310))
 
 
+def test_fused_path_small_and_ragged(QPBatch):
+    """fast_max = 512 routes every LU problem with N' ≤ 512 to the fused
+    one-workgroup-per-problem kernel (the default route is the blocked path)."""
+    _check_batch(QPBatch, _synthetic(3, 200, 300, 0, 0.3, 20250309), fast_max=512)
+    _check_batch(QPBatch, _synthetic(3, 50, 80, 30, 0.2, 20250308), fast_max=512)
+    _check_batch(QPBatch, _synthetic(3, 40, 60, 10, 0.5, 7, dense=True), dense=True, fast_max=512)
+    for (n, m, p) in [(1, 1, 0), (3, 0, 0), (5, 0, 2), (7, 3, 0), (33, 31, 1), (64, 1, 63)]:
+        _check_batch(QPBatch, _synthetic(2, n, m, p, 0.5, 100 + n), fast_max=512)
+
+
 def test_blocked_path_forced_small_and_ragged(QPBatch):
     """fast_max = 0 forces every LU problem onto the blocked path: config-1/2
     shapes and ragged sizes (p = 0, m = 0, N' not a multiple of 32)."""
@@ -158,6 +168,7 @@ def test_blocked_matches_fused_and_split(QPBatch):
     d = _synthetic(4, 120, 200, 10, 0.4, 21)
     B, n = d["z"].shape
     e1 = QPBatch(B, n, 200, 10)
+    e1.set_fast_max(512)
     e1.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
     r1, f1 = e1.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
     e2 = QPBatch(B, n, 200, 10)
