@@ -103,6 +103,9 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
     if (const char* e = getenv("DOPT_CONIC_SPLIT")) {
       if (e[0] == '0' || e[0] == '1') h->conic_split = e[0] - '0';
     }
+    if (const char* e = getenv("DOPT_LU_STREAMS")) {
+      h->lu_streams = std::max(1, std::min(atoi(e), DOPT_MAX_LU_STREAMS));
+    }
     if (const char* e = getenv("DOPT_FAST_MAX")) {
       h->fast_max = std::max(0, std::min(atoi(e), dopt::FAST_MAX_N));
     }
@@ -146,6 +149,14 @@ int dopt_destroy(dopt_handle* h) {
     (void)hipEventDestroy(pe.second.second);
   }
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
+  for (int k = 0; k < DOPT_MAX_LU_STREAMS; ++k) {
+    if (h->sub_stream[k]) {
+      (void)hipStreamSynchronize(h->sub_stream[k]);
+      (void)hipStreamDestroy(h->sub_stream[k]);
+    }
+    if (h->join_ev[k]) (void)hipEventDestroy(h->join_ev[k]);
+  }
+  if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;

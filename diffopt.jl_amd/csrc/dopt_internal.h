@@ -59,6 +59,7 @@ struct QPMeta {
 constexpr int FAST_THREADS = 512;
 constexpr int FAST_MAX_N = 512;      // largest reduced system of the fused one-WG path
 constexpr int BLOCKED_MAX = 1536;    // largest reduced system of the blocked step path
+#define DOPT_MAX_LU_STREAMS 4
 
 // Which factorisation path a problem takes (decided per problem on the
 // device from its reduced size; fast_max ≤ FAST_MAX_N is a handle setting).
@@ -104,6 +105,11 @@ struct Handle {
   // (tools/route_sweep.py, profiles/r01f_route_sweep.jsonl: 1.5–1.8× at batch
   // 1024, ≥ parity at batch 128); the fused kernel stays as an opt-in route.
   int32_t fast_max = 0;
+  // blocked LU: batch chunks stepped on concurrent streams (env DOPT_LU_STREAMS)
+  int32_t lu_streams = 1;   // 2–4 measured no faster on configs 2 and 3 (r01f)
+  hipStream_t sub_stream[DOPT_MAX_LU_STREAMS] = {};
+  hipEvent_t join_ev[DOPT_MAX_LU_STREAMS] = {};
+  hipEvent_t fork_ev = nullptr;
   int32_t blocked_npmax = 0;       // largest padded blocked system of the current factorisation
   bool has_generic = true;         // some problem exceeds BLOCKED_MAX (set by the read-back)
   bool set = false, factored = false;

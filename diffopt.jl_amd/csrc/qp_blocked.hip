@@ -99,14 +99,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void b
                                                        double* __restrict__ dinv, size_t dstride,
                                                        QPMeta* __restrict__ meta, int c0,
                                                        int fast_max, int corr,
-                                                       unsigned long long* __restrict__ stamps) {
+                                                       unsigned long long* __restrict__ stamps, int b0) {
   constexpr int TW = TPB / 64;   // waves
   __shared__ double slot_val[2][TW];
   __shared__ int slot_pos[2][TW];
   __shared__ __attribute__((aligned(16))) double slot_row[2][TW][BNB];
   __shared__ double Lt[BNB * BLP], Linv[BNB * BLP], Uinv[BNB * BLP];
   __shared__ int ptop[BNB];
-  const int b = blockIdx.x;
+  const int b = b0 + (int)blockIdx.x;
   const QPMeta mm = meta[b];
   const int Np = blocked_np(mm, fast_max);
   if (c0 >= Np) return;   // not a blocked problem, or already factored
@@ -393,15 +393,16 @@ __global__ __launch_bounds__(256) void blu_update_kernel(double* __restrict__ K,
                                                          const int32_t* __restrict__ perm,
                                                          const QPMeta* __restrict__ meta, int c0,
                                                          int fast_max, int cols_max, int nrt,
-                                                         int nct, int total) {
+                                                         int nct, int total, int b0) {
   __shared__ double U[KW * ULD];
   // bijective XCD remap (blocks L and L+8 share an XCD)
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
   const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
   const int tiles = nrt * nct;
-  const int b = logical / tiles;
-  const int tile = logical - b * tiles;
+  const int bl = logical / tiles;
+  const int tile = logical - bl * tiles;
+  const int b = b0 + bl;
   const int rt = tile / nct, ct = tile - rt * nct;
   const int Np = blocked_np(meta[b], fast_max);
   const int R2 = Np - c0 - KW;          // trailing rows (multiple of 32, may be ≤ 0)
@@ -688,6 +689,26 @@ void qp_blocked_factor(Handle& h, double* dinv) {
   // rows' trailing columns); one rank-64 update of everything right of and
   // below the pair — half the trailing-matrix traffic of rank-32 steps.
   unsigned long long* st = h.stamps.as<unsigned long long>();
+  // The batch is cut into `ns` contiguous chunks, each stepping through its
+  // panels on its own HIP stream: one chunk's latency-bound panel kernels
+  // overlap another chunk's MFMA trailing updates (env DOPT_LU_STREAMS).
+  const int ns = std::max(1, std::min<int>(h.lu_streams, std::min(B / 64, DOPT_MAX_LU_STREAMS)));
+  hipStream_t sts[DOPT_MAX_LU_STREAMS];
+  sts[0] = h.stream;
+  if (ns > 1) {
+    if (!h.fork_ev) DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.fork_ev, hipEventDisableTiming));
+    DOPT_CHECK_HIP(hipEventRecord(h.fork_ev, h.stream));
+    for (int k = 1; k < ns; ++k) {
+      if (!h.sub_stream[k]) {
+        DOPT_CHECK_HIP(hipStreamCreateWithFlags(&h.sub_stream[k], hipStreamNonBlocking));
+        DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.join_ev[k], hipEventDisableTiming));
+      }
+      sts[k] = h.sub_stream[k];
+      DOPT_CHECK_HIP(hipStreamWaitEvent(sts[k], h.fork_ev, 0));
+    }
+  }
+  int b0 = 0, bc = B;
+  hipStream_t stm = h.stream;
   auto panel = [&](int c0, int corr) {
     // workgroup shape by panel height: the per-column pivot overhead (argmax,
     // publish, fold, reciprocal) is paid once per wave, so short panels use
@@ -695,8 +716,8 @@ void qp_blocked_factor(Handle& h, double* dinv) {
     // workgroups per CU), tall panels 8 waves with 2–3 rows per thread
     const int R = npmax - c0;
 #define DOPT_PANEL(T, Q)                                                                     \
-  hipLaunchKernelGGL((blu_panel_kernel<T, Q>), dim3(B), dim3(T), 0, h.stream, K, h.ld, h.nmax, \
-                     perm, dinv, dstride, meta, c0, h.fast_max, corr, st)
+  hipLaunchKernelGGL((blu_panel_kernel<T, Q>), dim3(bc), dim3(T), 0, stm, K, h.ld, h.nmax, \
+                     perm, dinv, dstride, meta, c0, h.fast_max, corr, st, b0)
     if (R <= 128) DOPT_PANEL(128, 1);
     else if (R <= 256) DOPT_PANEL(128, 2);
     else if (R <= 384) DOPT_PANEL(128, 3);
@@ -710,22 +731,37 @@ void qp_blocked_factor(Handle& h, double* dinv) {
     const int R2 = npmax - c0 - kw;
     if (R2 <= 0) return;
     const int nrt = (R2 + 63) / 64, nct = (std::min(R2, cols_max) + 63) / 64;
-    const long long total = (long long)nrt * nct * B;
+    const long long total = (long long)nrt * nct * bc;
     if (total > 0x7fffffffLL) throw Error(-1, "blocked LU: trailing-update grid too large");
     if (kw == 64)
-      hipLaunchKernelGGL(blu_update_kernel<64>, dim3((unsigned)total), dim3(256), 0, h.stream, K,
-                         h.ld, h.nmax, perm, meta, c0, h.fast_max, cols_max, nrt, nct, (int)total);
+      hipLaunchKernelGGL(blu_update_kernel<64>, dim3((unsigned)total), dim3(256), 0, stm, K,
+                         h.ld, h.nmax, perm, meta, c0, h.fast_max, cols_max, nrt, nct, (int)total, b0);
     else
-      hipLaunchKernelGGL(blu_update_kernel<32>, dim3((unsigned)total), dim3(256), 0, h.stream, K,
-                         h.ld, h.nmax, perm, meta, c0, h.fast_max, cols_max, nrt, nct, (int)total);
+      hipLaunchKernelGGL(blu_update_kernel<32>, dim3((unsigned)total), dim3(256), 0, stm, K,
+                         h.ld, h.nmax, perm, meta, c0, h.fast_max, cols_max, nrt, nct, (int)total, b0);
     DOPT_CHECK_HIP(hipGetLastError());
   };
+  // chunks issued step-interleaved so every stream has work queued early
+  int cb0[DOPT_MAX_LU_STREAMS], cbc[DOPT_MAX_LU_STREAMS];
+  for (int k = 0; k < ns; ++k) {
+    cb0[k] = (int)((long long)B * k / ns);
+    cbc[k] = (int)((long long)B * (k + 1) / ns) - cb0[k];
+  }
   for (int c0 = 0; c0 < npmax; c0 += 2 * BNB) {
-    panel(c0, 0);
-    if (npmax - c0 <= BNB) break;
-    update(c0, BNB, BNB);          // panel B's 32 columns, all rows below panel A
-    panel(c0 + BNB, 1);
-    update(c0, 2 * BNB, 1 << 30);  // rank 64, rows and columns from c0+64
+    for (int k = 0; k < ns; ++k) {
+      b0 = cb0[k];
+      bc = cbc[k];
+      stm = sts[k];
+      panel(c0, 0);
+      if (npmax - c0 <= BNB) continue;
+      update(c0, BNB, BNB);          // panel B's 32 columns, all rows below panel A
+      panel(c0 + BNB, 1);
+      update(c0, 2 * BNB, 1 << 30);  // rank 64, rows and columns from c0+64
+    }
+  }
+  for (int k = 1; k < ns; ++k) {
+    DOPT_CHECK_HIP(hipEventRecord(h.join_ev[k], sts[k]));
+    DOPT_CHECK_HIP(hipStreamWaitEvent(h.stream, h.join_ev[k], 0));
   }
 }
 

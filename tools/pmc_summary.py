@@ -24,7 +24,15 @@ KERNEL_PHASE = {
     "conic_lsqr_kernel": "conic_lsqr",
     "conic_cone_kernel": "conic_cone",
     "conic_split_pass_kernel": "conic_split_pass",
+    "qp_prep_asm_kernel": "qp_assemble",
 }
+# blocked QP route: one bench phase = several launches (the panel / trailing-
+# update sequence of one factorisation, the two solve kernels of one step);
+# summed over the dispatches and divided by the number of steps, counted by
+# the per-step qp_prep_asm_kernel dispatch
+QP_GROUPS = {"qp_lu": ("blu_panel_kernel", "blu_update_kernel"),
+             "qp_solve": ("blu_solve_kernel", "blu_solve_rows_kernel")}
+QP_STEP = "qp_prep_asm_kernel"
 # split-path LSQR: every conic_split_* dispatch belongs to the LSQR call opened
 # by the preceding conic_split_init_kernel; reported per LSQR call under the
 # bench's phase name "conic_lsqr" (key "conic_lsqr_split")
@@ -59,6 +67,21 @@ def per_launch(d, counter):
                         calls.add(row.get("Dispatch_Id"))
     if calls:
         res["conic_lsqr_split"] = tot / len(calls)
+    gtot, steps = defaultdict(float), set()
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                kn = row.get("Kernel_Name", "")
+                if QP_STEP in kn:
+                    steps.add(row.get("Dispatch_Id"))
+                for ph, frags in QP_GROUPS.items():
+                    if any(fr in kn for fr in frags):
+                        gtot[ph] += float(row["Counter_Value"])
+    if steps:
+        for ph, v in gtot.items():
+            res[ph] = v / len(steps)
     return res
 
 
