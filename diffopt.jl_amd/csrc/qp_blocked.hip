@@ -474,18 +474,13 @@ __global__ __launch_bounds__(256) void blu_update_kernel(double* __restrict__ K,
 // rhs / x: per problem stride nmax, length nsys.
 // ---------------------------------------------------------------------------
 template <int ENT>
-__global__ __launch_bounds__(PT) void blu_solve_kernel(const double* __restrict__ K, int ld, int nmax,
-                                                       const int32_t* __restrict__ perm,
-                                                       const double* __restrict__ dinv,
-                                                       size_t dstride, const QPMeta* __restrict__ meta,
-                                                       int fast_max, int trans,
-                                                       const double* __restrict__ rhs,
-                                                       double* __restrict__ xout) {
-  __shared__ double v[BLOCKED_MAX];
-  __shared__ double y[BLOCKED_MAX];
-  __shared__ int ps[BLOCKED_MAX];
-  __shared__ double part[BNB];
-  const int b = blockIdx.x;
+__device__ __forceinline__ void solve_cols_body(int b, const double* __restrict__ K, int ld, int nmax,
+                                                const int32_t* __restrict__ perm,
+                                                const double* __restrict__ dinv, size_t dstride,
+                                                const QPMeta* __restrict__ meta, int fast_max, int trans,
+                                                const double* __restrict__ rhs,
+                                                double* __restrict__ xout, double* v, double* y, int* ps,
+                                                double* part) {
   const QPMeta mm = meta[b];
   const int Np = blocked_np(mm, fast_max);
   if (Np == 0) return;
@@ -559,6 +554,22 @@ __global__ __launch_bounds__(PT) void blu_solve_kernel(const double* __restrict_
   }
 }
 
+template <int ENT>
+__global__ __launch_bounds__(PT) void blu_solve_kernel(const double* __restrict__ K, int ld, int nmax,
+                                                       const int32_t* __restrict__ perm,
+                                                       const double* __restrict__ dinv,
+                                                       size_t dstride, const QPMeta* __restrict__ meta,
+                                                       int fast_max, int trans,
+                                                       const double* __restrict__ rhs,
+                                                       double* __restrict__ xout) {
+  __shared__ double v[BLOCKED_MAX];
+  __shared__ double y[BLOCKED_MAX];
+  __shared__ int ps[BLOCKED_MAX];
+  __shared__ double part[BNB];
+  solve_cols_body<ENT>(blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, fast_max, trans, rhs, xout,
+                       v, y, ps, part);
+}
+
 
 // ---------------------------------------------------------------------------
 // trans = 0 (K x = b): the slices are 32-wide ROW segments, so 8 lanes share
@@ -570,19 +581,13 @@ __global__ __launch_bounds__(PT) void blu_solve_kernel(const double* __restrict_
 constexpr int RPASS = PT / 8;   // rows per pass
 constexpr int RCH = 8;          // passes per load chunk
 
-__global__ __launch_bounds__(PT) void blu_solve_rows_kernel(const double* __restrict__ K, int ld,
-                                                            int nmax,
-                                                            const int32_t* __restrict__ perm,
-                                                            const double* __restrict__ dinv,
-                                                            size_t dstride,
-                                                            const QPMeta* __restrict__ meta,
-                                                            int fast_max,
-                                                            const double* __restrict__ rhs,
-                                                            double* __restrict__ xout) {
-  __shared__ double v[BLOCKED_MAX];
-  __shared__ int ps[BLOCKED_MAX];
-  __shared__ double part[BNB];
-  const int b = blockIdx.x;
+__device__ __forceinline__ void solve_rows_body(int b, const double* __restrict__ K, int ld, int nmax,
+                                                const int32_t* __restrict__ perm,
+                                                const double* __restrict__ dinv, size_t dstride,
+                                                const QPMeta* __restrict__ meta, int fast_max,
+                                                const double* __restrict__ rhs,
+                                                double* __restrict__ xout, double* v, int* ps,
+                                                double* part) {
   const QPMeta mm = meta[b];
   const int Np = blocked_np(mm, fast_max);
   if (Np == 0) return;
@@ -653,6 +658,49 @@ __global__ __launch_bounds__(PT) void blu_solve_rows_kernel(const double* __rest
   for (int i = t; i < N; i += PT) xb[i] = v[i];
 }
 
+__global__ __launch_bounds__(PT) void blu_solve_rows_kernel(const double* __restrict__ K, int ld,
+                                                            int nmax,
+                                                            const int32_t* __restrict__ perm,
+                                                            const double* __restrict__ dinv,
+                                                            size_t dstride,
+                                                            const QPMeta* __restrict__ meta,
+                                                            int fast_max,
+                                                            const double* __restrict__ rhs,
+                                                            double* __restrict__ xout) {
+  __shared__ double v[BLOCKED_MAX];
+  __shared__ int ps[BLOCKED_MAX];
+  __shared__ double part[BNB];
+  solve_rows_body(blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, fast_max, rhs, xout, v, ps, part);
+}
+
+// Both directions of one forward+reverse step in ONE launch (2B workgroups):
+// blocks [0, B) solve K x = b (row slices), [B, 2B) solve Kᵀ x = b (column
+// slices), so the two sweeps over each problem's factors run concurrently and
+// the second direction's reads hit L2 / MALL (blocks L and L+B share an XCD
+// when B is a multiple of 8).  Same per-problem code as the one-direction
+// kernels, hence bit-identical results.
+template <int ENT>
+__global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict__ K, int ld, int nmax,
+                                                        const int32_t* __restrict__ perm,
+                                                        const double* __restrict__ dinv,
+                                                        size_t dstride, const QPMeta* __restrict__ meta,
+                                                        int fast_max, int B,
+                                                        const double* __restrict__ rhs_rev,
+                                                        const double* __restrict__ rhs_fwd,
+                                                        double* __restrict__ x_rev,
+                                                        double* __restrict__ x_fwd) {
+  __shared__ double v[BLOCKED_MAX];
+  __shared__ double y[BLOCKED_MAX];
+  __shared__ int ps[BLOCKED_MAX];
+  __shared__ double part[BNB];
+  const int L = blockIdx.x;
+  if (L < B)
+    solve_rows_body(L, K, ld, nmax, perm, dinv, dstride, meta, fast_max, rhs_rev, x_rev, v, ps, part);
+  else
+    solve_cols_body<ENT>(L - B, K, ld, nmax, perm, dinv, dstride, meta, fast_max, 1, rhs_fwd, x_fwd, v,
+                         y, ps, part);
+}
+
 }  // namespace
 
 size_t fast_dinv_stride(int nmax);
@@ -718,7 +766,13 @@ void qp_blocked_factor(Handle& h, double* dinv) {
 #define DOPT_PANEL(T, Q)                                                                     \
   hipLaunchKernelGGL((blu_panel_kernel<T, Q>), dim3(bc), dim3(T), 0, stm, K, h.ld, h.nmax, \
                      perm, dinv, dstride, meta, c0, h.fast_max, corr, st, b0)
-    if (R <= 128) DOPT_PANEL(128, 1);
+#ifndef DOPT_PANEL_VARIANT
+#define DOPT_PANEL_VARIANT 0
+#endif
+    if (DOPT_PANEL_VARIANT == 1 && R > 128 && R <= 512) {   // tuning build: 4 waves, 1–2 rows/thread
+      if (R <= 256) DOPT_PANEL(256, 1);
+      else DOPT_PANEL(256, 2);
+    } else if (R <= 128) DOPT_PANEL(128, 1);
     else if (R <= 256) DOPT_PANEL(128, 2);
     else if (R <= 384) DOPT_PANEL(128, 3);
     else if (R <= 512) DOPT_PANEL(256, 2);
@@ -795,8 +849,23 @@ void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rh
 
 void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, const double* rhs_fwd,
                        double* x_rev, double* x_fwd) {
-  qp_blocked_solve(h, dinv, 0, rhs_rev, x_rev);
-  qp_blocked_solve(h, dinv, 1, rhs_fwd, x_fwd);
+  const int npmax = h.blocked_npmax;
+  if (npmax == 0) return;
+  const int B = (int)h.batch;
+  if (2LL * B > 0x7fffffffLL) throw Error(-1, "blocked solve: grid too large");
+  const size_t dstride = fast_dinv_stride(h.nmax);
+  const double* K = h.K.as<double>();
+  const int32_t* perm = h.ipiv.as<int32_t>();
+  const QPMeta* meta = h.meta.as<QPMeta>();
+  const int ent = (npmax + PT - 1) / PT;
+#define DOPT_SOLVE2(E)                                                                            \
+  hipLaunchKernelGGL(blu_solve2_kernel<E>, dim3(2 * B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm, \
+                     dinv, dstride, meta, h.fast_max, B, rhs_rev, rhs_fwd, x_rev, x_fwd)
+  if (ent <= 1) DOPT_SOLVE2(1);
+  else if (ent == 2) DOPT_SOLVE2(2);
+  else DOPT_SOLVE2(3);
+#undef DOPT_SOLVE2
+  DOPT_CHECK_HIP(hipGetLastError());
 }
 
 }  // namespace dopt
