@@ -33,8 +33,8 @@ for _p in (ROOT, os.path.join(ROOT, "diffopt.jl_amd")):
 
 PEAK_FP64_TFLOPS = 78.6     # MI355X FP64 matrix/vector dense (spec; probe measured 75.4)
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
-QP_CFG = {2: dict(n=200, m=300, p=0, phi=0.3, batch=1024),
-          3: dict(n=1000, m=1500, p=0, phi=0.3, batch=1024)}
+QP_CFG = {2: dict(id=2, n=200, m=300, p=0, phi=0.3, batch=1024),
+          3: dict(id=3, n=1000, m=1500, p=0, phi=0.3, batch=1024)}
 # conic configs (BASELINE.json configs[3], [4]); batch = problems per GPU
 # (config 5: 64 SDPs over 4 GPUs = 16 per GPU)
 CONIC_CFG = {4: dict(batch=512), 5: dict(batch=16)}
@@ -73,7 +73,7 @@ def cpu_baseline(cfg, seconds, workers):
     solves = sum(r[0] for r in res)
     rate = sum(r[0] / r[1] for r in res)
     return dict(value=round(rate, 2), unit="solves/s", cores=workers, kind="port",
-                sample=(f"{solves} config-2 QP solves (n={cfg['n']}, m={cfg['m']}, fwd+rev, "
+                sample=(f"{solves} config-{cfg.get('id', 2)} QP solves (n={cfg['n']}, m={cfg['m']}, fwd+rev, "
                         f"SuperLU re-factorised per direction) on {workers} processes "
                         f"× {seconds:.0f} s (wall {wall:.1f} s)"))
 
@@ -203,7 +203,7 @@ def run_conic(args, world, rank, local_rank):
         elapsed = float(tt.item())
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline:
             workers = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
             cpu = conic_cpu_baseline(args.config, args.cpu_seconds, workers,
                                      float(it_f.mean() + it_r.mean()))
@@ -282,7 +282,7 @@ def main():
     B, n, m, p = cfg["batch"], cfg["n"], cfg["m"], cfg["p"]
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         workers = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
         cpu = cpu_baseline(cfg, args.cpu_seconds, workers)
 
@@ -375,7 +375,7 @@ def main():
             roof = dict(bound="hbm", achieved=round(achieved, 1), peak=PEAK_HBM_GBS,
                         unit="GB/s", frac=round(achieved / PEAK_HBM_GBS, 4))
         roof["kernel"] = name
-        roof["traffic"] = _load_pmc(name)
+        roof["traffic"] = _load_pmc(name if args.config == 2 else f"{name}@cfg{args.config}")
         roof["avg_launch_ms"] = round(avg_s * 1e3, 4)
         roof["phases_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in sorted(phases.items())}
         value = world * B * args.steps / elapsed

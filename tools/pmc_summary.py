@@ -31,7 +31,7 @@ KERNEL_PHASE = {
 # summed over the dispatches and divided by the number of steps, counted by
 # the per-step qp_prep_asm_kernel dispatch
 QP_GROUPS = {"qp_lu": ("blu_panel_kernel", "blu_update_kernel"),
-             "qp_solve": ("blu_solve_kernel", "blu_solve_rows_kernel")}
+             "qp_solve": ("blu_solve_kernel", "blu_solve_rows_kernel", "blu_solve2_kernel")}
 QP_STEP = "qp_prep_asm_kernel"
 # split-path LSQR: every conic_split_* dispatch belongs to the LSQR call opened
 # by the preceding conic_split_init_kernel; reported per LSQR call under the
