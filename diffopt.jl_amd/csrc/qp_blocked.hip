@@ -1,5 +1,5 @@
-// Blocked step path for reduced KKT systems of FAST_MAX_N < N ≤ BLOCKED_MAX
-// (config 3: n = 1000, m = 1500 ⇒ N' ≈ 1450): the batched LU is a sequence of
+// Blocked step path — the default route for reduced KKT systems N ≤ BLOCKED_MAX
+// (config 2: N' = 290, config 3: N' ≈ 1450): the batched LU is a sequence of
 // launches per 32-column panel, each covering EVERY problem of the batch, so
 // the O(N³) trailing update is spread over all 256 CUs instead of one
 // workgroup per problem.
