@@ -103,6 +103,14 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
     if (const char* e = getenv("DOPT_CONIC_SPLIT")) {
       if (e[0] == '0' || e[0] == '1') h->conic_split = e[0] - '0';
     }
+    if (const char* e = getenv("DOPT_LU_GROUP")) {
+      const int gsz = atoi(e);
+      h->lu_group = gsz == 0 ? 0 : std::max(2, std::min(gsz, 4));
+    }
+    if (const char* e = getenv("DOPT_UPD_CT")) {
+      const int ct = atoi(e);
+      h->upd_ct = ct >= 4 ? 4 : (ct >= 2 ? 2 : 1);
+    }
     if (const char* e = getenv("DOPT_LU_STREAMS")) {
       h->lu_streams = std::max(1, std::min(atoi(e), DOPT_MAX_LU_STREAMS));
     }

@@ -106,6 +106,15 @@ struct Handle {
   // 1024, ≥ parity at batch 128); the fused kernel stays as an opt-in route.
   int32_t fast_max = 0;
   // blocked LU: batch chunks stepped on concurrent streams (env DOPT_LU_STREAMS)
+  // panels per trailing update of the blocked LU (env DOPT_LU_GROUP): 0 = the
+  // pair scheme with the in-panel correction (default); 2–4 = left-looking
+  // panel groups with a separate U12 kernel and one rank-32g update, measured
+  // 5–11 % slower on configs 2/3 (r01f: the rank-128 tile update is latency-
+  // bound at 2 WGs/CU and the U12 strips re-read the group's U rows)
+  int32_t lu_group = 0;
+  // column tiles per rank-64 update workgroup (env DOPT_UPD_CT: 1, 2, 4); the
+  // prefetching strip kernel measured within ±2 % of one tile per WG (r01f)
+  int32_t upd_ct = 1;
   int32_t lu_streams = 1;   // 2–4 measured no faster on configs 2 and 3 (r01f)
   hipStream_t sub_stream[DOPT_MAX_LU_STREAMS] = {};
   hipEvent_t join_ev[DOPT_MAX_LU_STREAMS] = {};

@@ -263,7 +263,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void b
 #pragma unroll
   for (int s = 0; s < BNB / 4; ++s) ro[s] = (size_t)ptop[4 * s + g] * ld;
   double bv[BNB / 4];
-  if (wv < ntile) {
+  if (corr >= 0 && wv < ntile) {
 #pragma unroll
     for (int s = 0; s < BNB / 4; ++s) bv[s] = Kb[ro[s] + c0 + BNB + 16 * wv + l16];
   }
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void b
   }
   if (t == 0 && info != 0 && mm.info == 0) meta[b].info = info;
   st.mark(4);
-  if (wv >= ntile) return;
+  if (corr < 0 || wv >= ntile) return;   // corr < 0: U12 left to blu_u12_kernel
   double a0[BNB / 4], a1[BNB / 4];
 #pragma unroll
   for (int s = 0; s < BNB / 4; ++s) {
@@ -460,6 +460,192 @@ __global__ __launch_bounds__(256) void blu_update_kernel(double* __restrict__ K,
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) Kb[ro[rr] + cbase + 16 * q + l16] = acc[q][rr];
     }
+  }
+}
+
+// Strip variant of the trailing update: one workgroup owns 64 rows × CT
+// column tiles.  The L operand (64 × KW) is loaded once per strip instead of
+// once per tile, and the next tile's C block and U rows are loaded into
+// registers while the current tile's MFMAs run (U re-staged through LDS
+// between two barriers).  Same arithmetic order per element as
+// blu_update_kernel, hence bit-identical factors.
+template <int KW, int CT>
+__global__ __launch_bounds__(256) void blu_update_strip_kernel(double* __restrict__ K, int ld, int nmax,
+                                                               const int32_t* __restrict__ perm,
+                                                               const QPMeta* __restrict__ meta, int c0,
+                                                               int fast_max, int cols_max, int nrt,
+                                                               int ncs, int total, int b0) {
+  __shared__ double U[KW * ULD];
+  const int L = blockIdx.x;
+  const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
+  const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
+  const int tiles = nrt * ncs;
+  const int bl = logical / tiles;
+  const int tile = logical - bl * tiles;
+  const int b = b0 + bl;
+  const int rt = tile / ncs, cs = tile - rt * ncs;
+  const int Np = blocked_np(meta[b], fast_max);
+  const int R2 = Np - c0 - KW;
+  const int C2 = min(R2, cols_max);
+  if (rt * 64 >= R2 || cs * CT * 64 >= C2) return;   // workgroup-uniform
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
+  double* Kb = K + (size_t)b * nmax * ld;
+  const int32_t* pb = perm + (size_t)b * nmax;
+  const int cend = c0 + KW + C2;
+  const int c8 = (t & 7) * 8;
+  size_t urow[KW / 32];
+#pragma unroll
+  for (int h = 0; h < KW / 32; ++h) urow[h] = (size_t)pb[c0 + 32 * h + (t >> 3)] * ld;
+  double uv[KW / 32][8];
+  auto load_u = [&](int cb) {
+    const bool ok = cb + c8 < cend;   // 32-aligned halves: all-or-nothing
+#pragma unroll
+    for (int h = 0; h < KW / 32; ++h) {
+      const double* src = Kb + urow[h] + (ok ? cb + c8 : 0);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) uv[h][u] = ok ? src[u] : 0.0;
+    }
+  };
+  auto store_u = [&]() {
+#pragma unroll
+    for (int h = 0; h < KW / 32; ++h) {
+      const int k = 32 * h + (t >> 3);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) U[k * ULD + c8 + u] = uv[h][u];
+    }
+  };
+  const int rbase = c0 + KW + rt * 64 + 16 * wv;
+  const bool wact = rt * 64 + 16 * wv < R2;   // wave-uniform
+  double a[KW / 4];
+  size_t ro[4];
+  d4b acc[4], accn[4];
+  int ct = cs * CT;
+  int cbase = c0 + KW + ct * 64;
+  load_u(cbase);
+  if (wact) {
+    const double* arow = Kb + (size_t)pb[rbase + l16] * ld + c0;
+#pragma unroll
+    for (int s = 0; s < KW / 4; ++s) a[s] = -arow[4 * s + g];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) ro[rr] = (size_t)pb[rbase + g + 4 * rr] * ld;
+    const int nq = min(4, (C2 - ct * 64) >> 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int cq = cbase + 16 * min(q, nq - 1) + l16;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) acc[q][rr] = Kb[ro[rr] + cq];
+    }
+  }
+  store_u();
+  __syncthreads();
+#pragma unroll 1
+  for (int j = 0; j < CT; ++j) {
+    const int nq = min(4, (C2 - ct * 64) >> 4);
+    const bool more = j + 1 < CT && (ct + 1) * 64 < C2;   // workgroup-uniform
+    if (more) {
+      load_u(cbase + 64);
+      if (wact) {
+        const int nqn = min(4, (C2 - (ct + 1) * 64) >> 4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int cq = cbase + 64 + 16 * min(q, nqn - 1) + l16;
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) accn[q][rr] = Kb[ro[rr] + cq];
+        }
+      }
+    }
+    if (wact) {
+#pragma unroll
+      for (int s = 0; s < KW / 4; ++s) {
+        double bq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bq[q] = U[(4 * s + g) * ULD + 16 * q + l16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = bmfma(a[s], bq[q], acc[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (q < nq) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) Kb[ro[rr] + cbase + 16 * q + l16] = acc[q][rr];
+        }
+      }
+    }
+    if (!more) break;
+    __syncthreads();   // every wave has read U of this tile
+    store_u();
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = accn[q];
+    ++ct;
+    cbase += 64;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// U12 of panel i of a panel group (group scheme, see qp_blocked_factor):
+//   A12 −= L[pivot rows, kc pending columns c0g .. c0g+kc) · U[those rows, trailing]
+//   U12  = L11⁻¹ · A12
+// for the 32 pivot rows of the panel at column ci over its trailing columns
+// ≥ ci+32.  One 256-thread workgroup per (problem, 64-column tile), one
+// 16-column MFMA strip per wave; the same operand layouts as the panel
+// kernel's in-kernel U12 (A operand −L / L11⁻¹ rows, B operand row-k strips).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void blu_u12_kernel(double* __restrict__ K, int ld, int nmax,
+                                                      const int32_t* __restrict__ perm,
+                                                      const double* __restrict__ dinv,
+                                                      size_t dstride, const QPMeta* __restrict__ meta,
+                                                      int c0g, int ci, int kc, int fast_max, int nct,
+                                                      int total, int b0) {
+  const int L = blockIdx.x;
+  const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
+  const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
+  const int bl = logical / nct;
+  const int ct = logical - bl * nct;
+  const int b = b0 + bl;
+  const int Np = blocked_np(meta[b], fast_max);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
+  const int ntile = (Np - ci - BNB) >> 4;   // 16-column strips right of the panel
+  const int q = ct * 4 + wv;
+  if (ci + BNB >= Np || q >= ntile) return;   // wave-uniform
+  double* Kb = K + (size_t)b * nmax * ld;
+  const int32_t* pb = perm + (size_t)b * nmax;
+  const double* Db = dinv + (size_t)b * dstride + (size_t)(ci / BNB) * BDINV;   // L11⁻¹, row-major
+  const int colL = ci + BNB + 16 * q + l16;
+  int ptop0 = pb[ci + l16], ptop1 = pb[ci + 16 + l16];
+  double bv[BNB / 4];
+#pragma unroll
+  for (int s = 0; s < BNB / 4; ++s) bv[s] = Kb[(size_t)pb[ci + 4 * s + g] * ld + colL];
+  d4b c0v = {bv[0], bv[1], bv[2], bv[3]}, c1v = {bv[4], bv[5], bv[6], bv[7]};
+  for (int kb = c0g; kb < c0g + kc; kb += BNB) {
+    double lp0[BNB / 4], lp1[BNB / 4], up[BNB / 4];
+#pragma unroll
+    for (int s = 0; s < BNB / 4; ++s) {
+      lp0[s] = -Kb[(size_t)ptop0 * ld + kb + 4 * s + g];
+      lp1[s] = -Kb[(size_t)ptop1 * ld + kb + 4 * s + g];
+      up[s] = Kb[(size_t)pb[kb + 4 * s + g] * ld + colL];
+    }
+#pragma unroll
+    for (int s = 0; s < BNB / 4; ++s) {
+      c0v = bmfma(lp0[s], up[s], c0v);
+      c1v = bmfma(lp1[s], up[s], c1v);
+    }
+  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    bv[rr] = c0v[rr];
+    bv[4 + rr] = c1v[rr];
+  }
+  d4b u0 = {0, 0, 0, 0}, u1 = {0, 0, 0, 0};
+#pragma unroll
+  for (int s = 0; s < BNB / 4; ++s) {
+    u0 = bmfma(Db[l16 * BNB + 4 * s + g], bv[s], u0);
+    u1 = bmfma(Db[(16 + l16) * BNB + 4 * s + g], bv[s], u1);
+  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    Kb[(size_t)pb[ci + g + 4 * rr] * ld + colL] = u0[rr];
+    Kb[(size_t)pb[ci + 16 + g + 4 * rr] * ld + colL] = u1[rr];
   }
 }
 
@@ -785,14 +971,32 @@ void qp_blocked_factor(Handle& h, double* dinv) {
     const int R2 = npmax - c0 - kw;
     if (R2 <= 0) return;
     const int nrt = (R2 + 63) / 64, nct = (std::min(R2, cols_max) + 63) / 64;
+    const int CT = h.upd_ct;
+    if (CT > 1 && nct > 1) {   // strip kernel: CT column tiles per workgroup
+      const int ncs = (nct + CT - 1) / CT;
+      const long long tot = (long long)nrt * ncs * bc;
+      if (tot > 0x7fffffffLL) throw Error(-1, "blocked LU: trailing-update grid too large");
+#define DOPT_STRIP(KW, C)                                                                           \
+  hipLaunchKernelGGL((blu_update_strip_kernel<KW, C>), dim3((unsigned)tot), dim3(256), 0, stm, K, h.ld, \
+                     h.nmax, perm, meta, c0, h.fast_max, cols_max, nrt, ncs, (int)tot, b0)
+      if (kw == 64) {
+        if (CT == 2) DOPT_STRIP(64, 2);
+        else DOPT_STRIP(64, 4);
+        DOPT_CHECK_HIP(hipGetLastError());
+        return;
+      }
+#undef DOPT_STRIP
+    }
     const long long total = (long long)nrt * nct * bc;
     if (total > 0x7fffffffLL) throw Error(-1, "blocked LU: trailing-update grid too large");
-    if (kw == 64)
-      hipLaunchKernelGGL(blu_update_kernel<64>, dim3((unsigned)total), dim3(256), 0, stm, K,
-                         h.ld, h.nmax, perm, meta, c0, h.fast_max, cols_max, nrt, nct, (int)total, b0);
-    else
-      hipLaunchKernelGGL(blu_update_kernel<32>, dim3((unsigned)total), dim3(256), 0, stm, K,
-                         h.ld, h.nmax, perm, meta, c0, h.fast_max, cols_max, nrt, nct, (int)total, b0);
+#define DOPT_UPDATE(KW)                                                                           \
+  hipLaunchKernelGGL(blu_update_kernel<KW>, dim3((unsigned)total), dim3(256), 0, stm, K, h.ld, h.nmax, \
+                     perm, meta, c0, h.fast_max, cols_max, nrt, nct, (int)total, b0)
+    if (kw == 128) DOPT_UPDATE(128);
+    else if (kw == 96) DOPT_UPDATE(96);
+    else if (kw == 64) DOPT_UPDATE(64);
+    else DOPT_UPDATE(32);
+#undef DOPT_UPDATE
     DOPT_CHECK_HIP(hipGetLastError());
   };
   // chunks issued step-interleaved so every stream has work queued early
@@ -801,16 +1005,43 @@ void qp_blocked_factor(Handle& h, double* dinv) {
     cb0[k] = (int)((long long)B * k / ns);
     cbc[k] = (int)((long long)B * (k + 1) / ns) - cb0[k];
   }
-  for (int c0 = 0; c0 < npmax; c0 += 2 * BNB) {
+  auto u12 = [&](int c0g, int ci, int kc) {
+    const int R = npmax - ci - BNB;
+    if (R <= 0) return;
+    const int nct = (R + 63) / 64;
+    const long long total = (long long)nct * bc;
+    if (total > 0x7fffffffLL) throw Error(-1, "blocked LU: U12 grid too large");
+    hipLaunchKernelGGL(blu_u12_kernel, dim3((unsigned)total), dim3(256), 0, stm, K, h.ld, h.nmax, perm,
+                       dinv, dstride, meta, c0g, ci, kc, h.fast_max, nct, (int)total, b0);
+    DOPT_CHECK_HIP(hipGetLastError());
+  };
+  const int G = h.lu_group;
+  for (int c0 = 0; c0 < npmax; c0 += (G ? G : 2) * BNB) {
     for (int k = 0; k < ns; ++k) {
       b0 = cb0[k];
       bc = cbc[k];
       stm = sts[k];
-      panel(c0, 0);
-      if (npmax - c0 <= BNB) continue;
-      update(c0, BNB, BNB);          // panel B's 32 columns, all rows below panel A
-      panel(c0 + BNB, 1);
-      update(c0, 2 * BNB, 1 << 30);  // rank 64, rows and columns from c0+64
+      if (G == 0) {   // panel pairs with the in-panel pending-rank-32 correction
+        panel(c0, 0);
+        if (npmax - c0 <= BNB) continue;
+        update(c0, BNB, BNB);          // panel B's 32 columns, all rows below panel A
+        panel(c0 + BNB, 1);
+        update(c0, 2 * BNB, 1 << 30);  // rank 64, rows and columns from c0+64
+        continue;
+      }
+      // Panel group of g ≤ G panels, left-looking inside the group: panel i's
+      // 32 columns get the group's pending rank-32i update (rows ≥ ci), then
+      // the panel factors, then its U12 strip applies the same pending update
+      // to its pivot rows and multiplies by L11⁻¹; one rank-32g update of
+      // everything right of and below the group ends it — C traffic ∝ 1/g.
+      const int g = std::min(G, (npmax - c0) / BNB);
+      for (int i = 0; i < g; ++i) {
+        const int ci = c0 + i * BNB;
+        if (i > 0) update(c0, i * BNB, BNB);
+        panel(ci, -1);
+        u12(c0, ci, i * BNB);
+      }
+      update(c0, g * BNB, 1 << 30);
     }
   }
   for (int k = 1; k < ns; ++k) {

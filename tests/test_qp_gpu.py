@@ -161,6 +161,40 @@ def test_blocked_path_forced_small_and_ragged(QPBatch):
         _check_batch(QPBatch, _synthetic(2, n, m, p, 0.5, 100 + n), fast_max=0)
 
 
+@pytest.mark.parametrize("group", ["2", "3", "4"])
+def test_blocked_panel_groups(QPBatch, monkeypatch, group):
+    """Left-looking panel groups (DOPT_LU_GROUP, read at handle creation):
+    separate U12 kernel with the group's pending update, rank-32g trailing
+    update; shapes whose panel count is not a multiple of the group."""
+    monkeypatch.setenv("DOPT_LU_GROUP", group)
+    _check_batch(QPBatch, _synthetic(3, 200, 300, 0, 0.3, 20250309))
+    _check_batch(QPBatch, _synthetic(2, 300, 400, 20, 0.6, 11))
+    for (n, m, p) in [(7, 3, 0), (33, 31, 1), (64, 1, 63)]:
+        _check_batch(QPBatch, _synthetic(2, n, m, p, 0.5, 100 + n))
+
+
+@pytest.mark.parametrize("ct", ["2", "4"])
+def test_blocked_update_strips(QPBatch, monkeypatch, ct):
+    """Strip trailing-update kernel (DOPT_UPD_CT column tiles per workgroup,
+    prefetched): bit-identical to the one-tile kernel, and oracle parity on
+    shapes with ragged column-tile counts."""
+    d = _synthetic(2, 300, 400, 20, 0.6, 11)
+    B, n = d["z"].shape
+    outs = []
+    for env in (None, ct):
+        if env is None:
+            monkeypatch.delenv("DOPT_UPD_CT", raising=False)
+        else:
+            monkeypatch.setenv("DOPT_UPD_CT", env)
+        e = QPBatch(B, n, 400, 20)
+        e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+        outs.append(e.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"]))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    _check_batch(QPBatch, _synthetic(2, 200, 300, 0, 0.3, 20250309))
+    _check_batch(QPBatch, _synthetic(2, 1000, 1500, 0, 0.3, 20250310))
+
+
 def test_blocked_matches_fused_and_split(QPBatch):
     """Same batch through the fused kernel and the blocked path: agreement to
     rounding (different accumulation order only); blocked split calls
