@@ -229,6 +229,25 @@ int dopt_qp_factor(dopt_handle* h) {
   });
 }
 
+int dopt_qp_reverse_grads(dopt_handle* h, const double* rev, double* dQ, double* dq, double* dG,
+                          double* g_const, double* dA, double* a_const) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_reverse_grads on a non-QP handle");
+    if (!rev) throw Error(-1, "rev is required");
+    const size_t B = h->batch, n = h->n, m = h->m, p = h->p, L = n + m + p;
+    const double* r = stage_in(*h, h->tin[0], rev, B * L);
+    double* outs[6] = {dQ, dq, dG, g_const, dA, a_const};
+    const size_t cnt[6] = {B * n * n, B * n, B * m * n, B * m, B * p * n, B * p};
+    double* dev[6];
+    for (int k = 0; k < 6; ++k) dev[k] = outs[k] ? out_ptr(*h, h->tout[k], outs[k], cnt[k]) : nullptr;
+    dopt::qp_reverse_grads(*h, r, dev[0], dev[1], dev[2], dev[3], dev[4], dev[5]);
+    for (int k = 0; k < 6; ++k)
+      if (outs[k]) copy_out(*h, outs[k], dev[k], cnt[k]);
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  });
+}
+
 int dopt_qp_reverse(dopt_handle* h, const double* dl_dz, double* out) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_reverse on a non-QP handle");

@@ -191,6 +191,8 @@ struct PhaseTimer {
 // Launch helpers (defined in qp.hip / conic.hip)
 void qp_factor(Handle& h);
 void qp_reverse(Handle& h, const double* dl_dz, double* out);
+void qp_reverse_grads(Handle& h, const double* rev, double* dQ, double* dq, double* dG, double* gc,
+                      double* dA, double* ac);
 void qp_forward(Handle& h, const double* dQ, const double* dq, const double* dG,
                 const double* dh, const double* dA, const double* db, double* out);
 void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,

@@ -512,6 +512,63 @@ __global__ __launch_bounds__(TPB) void qp_output_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Batched reverse-gradient materialisation (the reference's lazy getters,
+// materialised for every problem at once): from rev = [dz | dλ | dν]
+//   ReverseObjectiveFunction (QuadraticProgram.jl:448-458):
+//     dq = dz,  dQ = (dz zᵀ + z dzᵀ)/2
+//   ReverseConstraintFunction via _get_dA / _get_db (:307-314, :461-473,
+//   diff_opt.jl:475-481), MOI function coefficients and constants:
+//     LessThan row i:  dG_i = λ_i dλ_i z + λ_i dz,  g_const_i = λ_i dλ_i
+//     EqualTo  row i:  dA_i = dν_i z + ν_i dz,       a_const_i = dν_i
+// Matrices column-major per problem (Julia order), so consecutive threads
+// write consecutive rows of one column: pure streaming stores.  Any output
+// pointer may be null.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(TPB) void qp_reverse_grads_kernel(
+    const double* __restrict__ rev, const double* __restrict__ z, const double* __restrict__ lam,
+    const double* __restrict__ nu, int B, int n, int m, int p, double* __restrict__ dQ,
+    double* __restrict__ dq, double* __restrict__ dG, double* __restrict__ gc,
+    double* __restrict__ dA, double* __restrict__ ac) {
+  const int L = n + m + p;
+  const long long nn = (long long)n * n, mn = (long long)m * n, pn = (long long)p * n;
+  const long long per = nn + mn + pn + n + m + p;
+  for (int b = blockIdx.y; b < B; b += gridDim.y) {
+    const double* rb = rev + (size_t)b * L;
+    const double* zb = z + (size_t)b * n;
+    for (long long e = (long long)blockIdx.x * TPB + threadIdx.x; e < per;
+         e += (long long)gridDim.x * TPB) {
+      if (e < nn) {
+        if (!dQ) continue;
+        const int i = (int)(e % n), j = (int)(e / n);
+        dQ[(size_t)b * nn + e] = 0.5 * (rb[i] * zb[j] + zb[i] * rb[j]);
+      } else if (e < nn + mn) {
+        if (!dG) continue;
+        const long long f = e - nn;
+        const int i = (int)(f % m), j = (int)(f / m);
+        const double li = lam[(size_t)b * m + i];
+        dG[(size_t)b * mn + f] = li * rb[n + i] * zb[j] + li * rb[j];
+      } else if (e < nn + mn + pn) {
+        if (!dA) continue;
+        const long long f = e - nn - mn;
+        const int i = (int)(f % p), j = (int)(f / p);
+        dA[(size_t)b * pn + f] = rb[n + m + i] * zb[j] + nu[(size_t)b * p + i] * rb[j];
+      } else {
+        const int f = (int)(e - nn - mn - pn);
+        if (f < n) {
+          if (dq) dq[(size_t)b * n + f] = rb[f];
+        } else if (f < n + m) {
+          const int i = f - n;
+          if (gc) gc[(size_t)b * m + i] = lam[(size_t)b * m + i] * rb[n + i];
+        } else {
+          const int i = f - n - m;
+          if (ac) ac[(size_t)b * p + i] = rb[n + m + i];
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 static void check_launch() { DOPT_CHECK_HIP(hipGetLastError()); }
@@ -704,6 +761,19 @@ void qp_forward(Handle& h, const double* dQ, const double* dq, const double* dG,
   fallback_fwd_rhs(h, T);
   blocked_solve(h, 1);
   fallback_finish(h, 1, out);
+}
+
+void qp_reverse_grads(Handle& h, const double* rev, double* dQ, double* dq, double* dG, double* gc,
+                      double* dA, double* ac) {
+  if (!h.set) throw Error(-1, "dopt_qp_reverse_grads: dopt_qp_set has not been called");
+  static const double dummy = 0.0;
+  const long long per = (long long)h.n * h.n + (long long)(h.m + h.p) * h.n + h.n + h.m + h.p;
+  const int gx = (int)std::max<long long>(1, std::min<long long>((per + TPB - 1) / TPB, 64));
+  const int gy = (int)std::min<int64_t>(h.batch, 65535);
+  hipLaunchKernelGGL(qp_reverse_grads_kernel, dim3(gx, gy), dim3(TPB), 0, h.stream, rev, h.z,
+                     h.m ? h.lam : &dummy, h.p ? h.nu : &dummy, (int)h.batch, h.n, h.m, h.p, dQ, dq,
+                     h.m ? dG : nullptr, h.m ? gc : nullptr, h.p ? dA : nullptr, h.p ? ac : nullptr);
+  check_launch();
 }
 
 void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,

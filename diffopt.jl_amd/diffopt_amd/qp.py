@@ -21,6 +21,7 @@ import numpy as np
 
 from . import _lib
 from ._arrays import Staged, colmajor, vector
+from ._arrays import _is_torch as _is_t
 
 LE, EQ = "LessThan", "EqualTo"
 
@@ -126,6 +127,32 @@ class QPBatch:
                                               st.ptr(o1), st.ptr(o2))
         _lib.check(rc, self.h, singular_ok)
         return o1, o2
+
+    def reverse_grads(self, rev, dQ=True, dG=True, dA=True):
+        """Materialised reverse gradients of every problem from a reverse
+        output ``rev`` (B, n+m+p) — ``ReverseObjectiveFunction`` /
+        ``ReverseConstraintFunction`` (QuadraticProgram.jl:448-473, :307-314):
+        dict with dq (B, n), dQ (B, n, n), dG (B, m, n), g_const (B, m),
+        dA (B, p, n), a_const (B, p); the gradients w.r.t. h and b are
+        −g_const and −a_const.  Matrices are returned as (B, rows, cols)
+        views of the column-major buffers."""
+        B, n, m, p = self.batch, self.n, self.m, self.p
+        st = self._stage([rev])
+        dev = st.mem == _lib.DOPT_MEM_DEVICE
+        r = vector(rev, (B, n + m + p))
+        out = {"dq": Staged.empty((B, n), dev),
+               "dQ": Staged.empty((B, n, n), dev) if dQ else None,
+               "dG": Staged.empty((B, n, m), dev) if (dG and m) else None,
+               "g_const": Staged.empty((B, m), dev) if m else None,
+               "dA": Staged.empty((B, n, p), dev) if (dA and p) else None,
+               "a_const": Staged.empty((B, p), dev) if p else None}
+        rc = self.lib.dopt_qp_reverse_grads(
+            self.h, st.ptr(r), *[st.ptr(out[k]) for k in ["dQ", "dq", "dG", "g_const", "dA", "a_const"]])
+        _lib.check(rc, self.h)
+        for k in ("dQ", "dG", "dA"):   # column-major (B, cols, rows) → (B, rows, cols) view
+            if out[k] is not None:
+                out[k] = out[k].transpose(1, 2) if _is_t(out[k]) else np.swapaxes(out[k], 1, 2)
+        return out
 
     # ---- introspection -----------------------------------------------------
     def info(self):

@@ -141,6 +141,27 @@ function DiffOpt.reverse_differentiate!(m::QPModel)
     return
 end
 
+# Materialised reverse gradients of the last reverse pass (the lazy
+# ReverseObjectiveFunction / ReverseConstraintFunction getters of
+# QuadraticProgram.jl:448-473, :307-314 evaluated on the device for the whole
+# model): (dQ, dq, dG, g_const, dA, a_const); ∂h = −g_const, ∂b = −a_const.
+function reverse_gradients(m::QPModel)
+    h = _ensure!(m)
+    n, mi, p = h.n, h.m, h.p
+    dz, dl, dn = m.inner.back_grad_cache.dz, m.inner.back_grad_cache.dλ, m.inner.back_grad_cache.dν
+    rev = vcat(dz, dl, dn)
+    dQ, dq = Matrix{Float64}(undef, n, n), Vector{Float64}(undef, n)
+    dG, gc = Matrix{Float64}(undef, mi, n), Vector{Float64}(undef, mi)
+    dA, ac = Matrix{Float64}(undef, p, n), Vector{Float64}(undef, p)
+    GC.@preserve rev dQ dq dG gc dA ac begin
+        _check(ccall((:dopt_qp_reverse_grads, LIB), Cint,
+                     (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                      Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                     h.ptr, rev, dQ, dq, _ptr(dG), _ptr(gc), _ptr(dA), _ptr(ac)), h.ptr)
+    end
+    return (dQ = dQ, dq = dq, dG = dG, g_const = gc, dA = dA, a_const = ac)
+end
+
 # forward_differentiate! (QuadraticProgram.jl:357-446): tangents gathered with
 # the reference's own `_fill` sign rules (diff_opt.jl:594-656)
 function DiffOpt.forward_differentiate!(m::QPModel)

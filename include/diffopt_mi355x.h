@@ -110,6 +110,18 @@ int dopt_qp_reverse(dopt_handle* h, const double* dl_dz, double* out);
 int dopt_qp_forward(dopt_handle* h, const double* dQ, const double* dq,
                     const double* dG, const double* dh, const double* dA,
                     const double* db, double* out);
+/* Batched reverse gradients (the reference's lazy getters, materialised for
+ * every problem; QuadraticProgram.jl:448-473, :307-314, diff_opt.jl:475-481),
+ * from rev = the [dz | dλ | dν] output of dopt_qp_reverse /
+ * dopt_qp_forward_reverse and the handle's z, λ, ν:
+ *   ReverseObjectiveFunction:  dq = dz (n),  dQ = (dz zᵀ + z dzᵀ)/2 (n×n)
+ *   ReverseConstraintFunction, LessThan rows:  dG (m×n) row i = λ_i dλ_i z +
+ *     λ_i dz, g_const (m) = λ_i dλ_i   (the gradient w.r.t. h is −g_const)
+ *   EqualTo rows:  dA (p×n) row i = dν_i z + ν_i dz, a_const (p) = dν_i
+ *     (the gradient w.r.t. b is −a_const)
+ * Column-major per problem, batch-major.  Any output may be NULL. */
+int dopt_qp_reverse_grads(dopt_handle* h, const double* rev, double* dQ, double* dq,
+                          double* dG, double* g_const, double* dA, double* a_const);
 /* Fused forward + reverse for one factorisation (the batched throughput path;
  * results identical to dopt_qp_reverse + dopt_qp_forward). */
 int dopt_qp_forward_reverse(dopt_handle* h, const double* dl_dz,

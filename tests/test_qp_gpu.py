@@ -195,6 +195,35 @@ def test_blocked_update_strips(QPBatch, monkeypatch, ct):
     _check_batch(QPBatch, _synthetic(2, 1000, 1500, 0, 0.3, 20250310))
 
 
+def test_reverse_grads_materialised(QPBatch):
+    """dopt_qp_reverse_grads: ReverseObjectiveFunction / ReverseConstraintFunction
+    of every problem (QuadraticProgram.jl:448-473, :307-314) against the
+    oracle's getters, host mode and device mode (bit-identical)."""
+    import torch
+    d = _synthetic(3, 50, 80, 30, 0.2, 20250308)
+    B, n = d["z"].shape
+    m, p = d["lam"].shape[1], d["nu"].shape[1]
+    e = QPBatch(B, n, m, p)
+    e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    rev = np.asarray(e.reverse(d["dl_dz"]))
+    g = e.reverse_grads(rev)
+    for b in range(B):
+        dz, dl, dn = rev[b, :n], rev[b, n:n + m], rev[b, n + m:]
+        dq, dQ = oqp.reverse_objective(d["z"][b], dz)
+        dG, gc = oqp.reverse_constraint_le(d["z"][b], d["lam"][b], dz, dl)
+        dA, ac = oqp.reverse_constraint_eq(d["z"][b], d["nu"][b], dz, dn)
+        for got, ref in ((g["dq"][b], dq), (g["dQ"][b], dQ), (g["dG"][b], dG),
+                         (g["g_const"][b], gc), (g["dA"][b], dA), (g["a_const"][b], ac)):
+            np.testing.assert_allclose(got, ref, rtol=1e-14, atol=1e-15)
+    dev = {k: torch.as_tensor(v, device="cuda") for k, v in d.items()}
+    e2 = QPBatch(B, n, m, p)
+    e2.set(dev["Q"], dev["G"], dev["h"], dev["A"], dev["z"], dev["lam"], dev["nu"])
+    g2 = e2.reverse_grads(torch.as_tensor(rev, device="cuda"))
+    torch.cuda.synchronize()
+    for k in g:
+        np.testing.assert_array_equal(g2[k].cpu().numpy(), g[k])
+
+
 def test_blocked_matches_fused_and_split(QPBatch):
     """Same batch through the fused kernel and the blocked path: agreement to
     rounding (different accumulation order only); blocked split calls
