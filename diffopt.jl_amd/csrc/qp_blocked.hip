@@ -32,7 +32,10 @@ typedef double d4b __attribute__((ext_vector_type(4)));
 constexpr int BNB = 32;                  // panel width
 constexpr int BLP = BNB + 1;             // padded LDS row of a 32×32 block
 constexpr int BDINV = 2 * BNB * BNB;     // doubles per panel in dinv (L11⁻¹ | U11⁻¹)
-constexpr int PT = 512;                  // solve workgroup size
+#ifndef DOPT_SOLVE_PT
+#define DOPT_SOLVE_PT 512
+#endif
+constexpr int PT = DOPT_SOLVE_PT;        // solve workgroup size (tuning builds: -DDOPT_SOLVE_PT)
 
 __device__ __forceinline__ d4b bmfma(double a, double b, d4b c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
