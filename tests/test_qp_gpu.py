@@ -333,14 +333,19 @@ def test_device_mode_matches_host_mode(QPBatch):
     np.testing.assert_array_equal(f1, f2.cpu().numpy())
 
 
-def test_full_cfg2_kkt_residual_property(QPBatch):
-    """BASELINE config 2 at full batch (1024 × n=200, m=300): size-independent
-    check — every solution satisfies its KKT system (reverse: LHS x = rhs,
-    forward: LHSᵀ x = rhs) to 1e-9 relative, computed in fp64 on the GPU."""
+@pytest.mark.parametrize("cfg", [(200, 300, 20250309), (1000, 1500, 20250310)],
+                         ids=["config2", "config3"])
+def test_full_batch_kkt_residual_property(QPBatch, cfg):
+    """BASELINE configs 2 and 3 at full batch (1024 × n=200, m=300 and
+    1024 × n=1000, m=1500): size-independent check — every solution satisfies
+    its KKT system (reverse: LHS x = rhs, forward: LHSᵀ x = rhs) to 1e-9
+    relative, computed in fp64 on the GPU — plus bit-exact kept-set sizes
+    against a GPU recount of λ == 0 ∧ s ≠ 0."""
     import torch
     from diffopt_amd.synthetic import qp_torch
-    n, m, p = 200, 300, 0
-    d = qp_torch(1024, n, m, p, 0.3, 20250309)
+    n, m, seed = cfg
+    p = 0
+    d = qp_torch(1024, n, m, p, 0.3, seed)
     e = QPBatch(1024, n, m, p)
     e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
     rev, fwd = e.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
@@ -361,3 +366,10 @@ def test_full_cfg2_kkt_residual_property(QPBatch):
     res = torch.sqrt((f1 ** 2).sum(1) + (f2 ** 2).sum(1)) / nrm
     assert float(res.max()) < 1e-9
     assert (e.info() == 0).all()
+    # by construction inactive rows have s = −U(0.5, 1.5), far from 0, so the
+    # kept set is exactly the active set whatever the summation order
+    kept = (~((lam == 0) & (s != 0))).sum(1).cpu().numpy()
+    np.testing.assert_array_equal(e.system_size(), n + kept)
+    del d, rev, fwd, Q, G, z, lam, s
+    e.close()
+    torch.cuda.empty_cache()
