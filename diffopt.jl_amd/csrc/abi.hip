@@ -149,6 +149,9 @@ int dopt_destroy(dopt_handle* h) {
                     &h->vp, &h->dpi, &h->M, &h->cwork, &h->cinfo};
   for (auto* b : bufs) b->release();
   for (auto& b : h->own_in) b.release();
+  for (auto& b : h->csc_in) b.release();
+  for (auto& b : h->csc_in_val) b.release();
+  h->csc_err.release();
   for (auto& b : h->own_cin) b.release();
   for (auto& b : h->tin) b.release();
   for (auto& b : h->tout) b.release();
@@ -211,6 +214,68 @@ int dopt_qp_set(dopt_handle* h, const double* Q, const double* G, const double* 
     h->G = m ? stage_in(*h, h->own_in[1], G, B * m * n) : nullptr;
     h->hv = m ? stage_in(*h, h->own_in[2], hv, B * m) : nullptr;
     h->A = p ? stage_in(*h, h->own_in[3], A, B * p * n) : nullptr;
+    h->z = stage_in(*h, h->own_in[4], z, B * n);
+    h->lam = m ? stage_in(*h, h->own_in[5], lam, B * m) : nullptr;
+    h->nu = p ? stage_in(*h, h->own_in[6], nu, B * p) : nullptr;
+    h->set = true;
+    h->factored = false;
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  });
+}
+
+// Host mode: copy `count` int64 of `src` into `buf`; device mode: borrow.
+static const int64_t* stage_in_i64(Handle& h, DevBuf& buf, const int64_t* src, size_t count) {
+  if (!src) return nullptr;
+  if (h.mem == DOPT_MEM_DEVICE) return src;
+  buf.ensure(std::max<size_t>(count, 1) * sizeof(int64_t));
+  if (count)
+    DOPT_CHECK_HIP(hipMemcpyAsync(buf.p, src, count * sizeof(int64_t), hipMemcpyHostToDevice, h.stream));
+  return (const int64_t*)buf.p;
+}
+
+int dopt_qp_set_csc(dopt_handle* h,
+                    const int64_t* Q_colptr, const int64_t* Q_rowval, const double* Q_nzval, int64_t Q_nnz,
+                    const int64_t* G_colptr, const int64_t* G_rowval, const double* G_nzval, int64_t G_nnz,
+                    const int64_t* A_colptr, const int64_t* A_rowval, const double* A_nzval, int64_t A_nnz,
+                    const double* hv, const double* z, const double* lam, const double* nu) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_set_csc on a non-QP handle");
+    const size_t B = h->batch, n = h->n, m = h->m, p = h->p;
+    if (!Q_colptr || !z) throw Error(-1, "Q and z are required");
+    if (m && (!G_colptr || !hv || !lam)) throw Error(-1, "G, h and lam are required when m > 0");
+    if (p && (!A_colptr || !nu)) throw Error(-1, "A and nu are required when p > 0");
+    if (Q_nnz < 0 || G_nnz < 0 || A_nnz < 0) throw Error(-1, "nnz must be >= 0");
+    h->csc_err.ensure(sizeof(int));
+    DOPT_CHECK_HIP(hipMemsetAsync(h->csc_err.p, 0, sizeof(int), h->stream));
+    int* err = h->csc_err.as<int>();
+    struct Mat { const int64_t *cp, *rv; const double* nz; int64_t nnz; size_t rows; int slot; };
+    const Mat mats[3] = {{Q_colptr, Q_rowval, Q_nzval, Q_nnz, n, 0},
+                         {G_colptr, G_rowval, G_nzval, G_nnz, m, 1},
+                         {A_colptr, A_rowval, A_nzval, A_nnz, p, 3}};
+    const double* dense[3] = {nullptr, nullptr, nullptr};
+    for (int k = 0; k < 3; ++k) {
+      const Mat& M = mats[k];
+      if (M.rows == 0) continue;
+      if (M.nnz > 0 && (!M.rv || !M.nz)) throw Error(-1, "rowval and nzval are required when nnz > 0");
+      const int64_t* cp = stage_in_i64(*h, h->csc_in[3 * k], M.cp, B * (n + 1));
+      const int64_t* rv = stage_in_i64(*h, h->csc_in[3 * k + 1], M.rv, (size_t)M.nnz);
+      const double* nz = stage_in(*h, h->csc_in_val[k], M.nz, (size_t)M.nnz);
+      DevBuf& d = h->own_in[M.slot];
+      d.ensure(B * M.rows * n * sizeof(double));
+      dopt::csc_to_dense(*h, cp, rv ? rv : cp, nz ? nz : (const double*)d.p, M.nnz, (int)M.rows, (int)n,
+                         d.as<double>(), err);
+      dense[k] = d.as<double>();
+    }
+    int herr = 0;
+    DOPT_CHECK_HIP(hipMemcpyAsync(&herr, err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    if (herr) throw Error(-1, (herr & 1) ? "CSC colptr is not monotone / out of range"
+                                         : "CSC rowval out of range");
+    h->Q = dense[0];
+    h->G = m ? dense[1] : nullptr;
+    h->hv = m ? stage_in(*h, h->own_in[2], hv, B * m) : nullptr;
+    h->A = p ? dense[2] : nullptr;
     h->z = stage_in(*h, h->own_in[4], z, B * n);
     h->lam = m ? stage_in(*h, h->own_in[5], lam, B * m) : nullptr;
     h->nu = p ? stage_in(*h, h->own_in[6], nu, B * p) : nullptr;

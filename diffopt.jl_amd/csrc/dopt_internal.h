@@ -93,7 +93,8 @@ struct Handle {
   // ---- QP ----
   const double *Q = nullptr, *G = nullptr, *hv = nullptr, *A = nullptr;
   const double *z = nullptr, *lam = nullptr, *nu = nullptr;
-  DevBuf own_in[7];          // host-mode copies of the 7 QP inputs
+  DevBuf own_in[7];          // host-mode copies of the 7 QP inputs (Q, G, A: also the CSC densification)
+  DevBuf csc_in[9], csc_in_val[3], csc_err;   // host-mode copies of CSC colptr / rowval / nzval
   int32_t nmax = 0, ld = 0;  // max system size, K row stride (doubles)
   DevBuf K, ipiv, s, kidx, meta, rhs, x;
   DevBuf ws;                 // per-workgroup KKT workspace of the fused kernel
@@ -191,6 +192,8 @@ struct PhaseTimer {
 // Launch helpers (defined in qp.hip / conic.hip)
 void qp_factor(Handle& h);
 void qp_reverse(Handle& h, const double* dl_dz, double* out);
+void csc_to_dense(Handle& h, const int64_t* colptr, const int64_t* rowval, const double* nzval,
+                  int64_t nnz, int rows, int ncols, double* dense, int* err);
 void qp_reverse_grads(Handle& h, const double* rev, double* dQ, double* dq, double* dG, double* gc,
                       double* dA, double* ac);
 void qp_forward(Handle& h, const double* dQ, const double* dq, const double* dG,

@@ -569,6 +569,51 @@ __global__ __launch_bounds__(TPB) void qp_reverse_grads_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// CSC → dense staging (the MOI matrix form the reference's _gradient_cache
+// builds: QuadraticProgram.jl:182-213 / utils.jl:46-69 give SparseMatrixCSC
+// {Float64,Int64} with 1-based colptr/rowval).  Problem b's column j owns the
+// 1-based entries colptr[b·(ncols+1)+j] .. colptr[b·(ncols+1)+j+1]−1 of the
+// concatenated rowval / nzval.  The dense target (rows × ncols, column-major,
+// batch-major) is zero-filled beforehand; a malformed index sets *err.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(TPB) void csc_scatter_kernel(const int64_t* __restrict__ colptr,
+                                                          const int64_t* __restrict__ rowval,
+                                                          const double* __restrict__ nzval,
+                                                          int64_t nnz, int rows, int ncols, int B,
+                                                          double* __restrict__ dense,
+                                                          int* __restrict__ err) {
+  for (int b = blockIdx.y; b < B; b += gridDim.y) {
+    const int64_t* cp = colptr + (size_t)b * (ncols + 1);
+    double* db = dense + (size_t)b * rows * ncols;
+    for (int j = blockIdx.x; j < ncols; j += gridDim.x) {
+      const int64_t k0 = cp[j] - 1, k1 = cp[j + 1] - 1;
+      if (k0 < 0 || k1 < k0 || k1 > nnz) {
+        if (threadIdx.x == 0) atomicOr(err, 1);
+        continue;
+      }
+      for (int64_t k = k0 + threadIdx.x; k < k1; k += TPB) {
+        const int64_t r = rowval[k] - 1;
+        if (r < 0 || r >= rows) {
+          atomicOr(err, 2);
+          continue;
+        }
+        db[(size_t)j * rows + r] = nzval[k];
+      }
+    }
+  }
+}
+
+void csc_to_dense(Handle& h, const int64_t* colptr, const int64_t* rowval, const double* nzval,
+                  int64_t nnz, int rows, int ncols, double* dense, int* err) {
+  DOPT_CHECK_HIP(hipMemsetAsync(dense, 0, (size_t)h.batch * rows * ncols * sizeof(double), h.stream));
+  const int gx = std::max(1, std::min(ncols, 1024));
+  const int gy = (int)std::min<int64_t>(h.batch, 65535);
+  hipLaunchKernelGGL(csc_scatter_kernel, dim3(gx, gy), dim3(TPB), 0, h.stream, colptr, rowval, nzval,
+                     nnz, rows, ncols, (int)h.batch, dense, err);
+  DOPT_CHECK_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 static void check_launch() { DOPT_CHECK_HIP(hipGetLastError()); }

@@ -78,6 +78,43 @@ class QPBatch:
         rc = self.lib.dopt_qp_set(self.h, *[st.ptr(a) for a in args])
         _lib.check(rc, self.h)
 
+    def set_csc(self, Q, G=None, h=None, A=None, z=None, lam=None, nu=None):
+        """``set`` with Q, G, A as sparse matrices in the reference's MOI
+        matrix form (scipy.sparse, one per problem or one shared by all;
+        converted to Julia CSC arrays: Int64, 1-based) — dopt_qp_set_csc
+        densifies them on the device.  Host mode."""
+        B, n, m, p = self.batch, self.n, self.m, self.p
+
+        def csc(mats, rows):
+            import scipy.sparse as sp
+            if mats is None or rows == 0:
+                return None, None, None, 0
+            if sp.issparse(mats):
+                mats = [mats] * B
+            cps, rvs, nzs, off = [], [], [], 0
+            for M in mats:
+                M = sp.csc_matrix(M)
+                if M.shape != (rows, n):
+                    raise ValueError(f"sparse matrix of shape {M.shape}, expected {(rows, n)}")
+                cps.append(M.indptr.astype(np.int64) + off + 1)
+                rvs.append(M.indices.astype(np.int64) + 1)
+                nzs.append(M.data.astype(np.float64))
+                off += M.nnz
+            return (np.ascontiguousarray(np.concatenate(cps)), np.ascontiguousarray(np.concatenate(rvs)),
+                    np.ascontiguousarray(np.concatenate(nzs)), off)
+
+        st = self._stage([z, h, lam, nu])
+        if st.mem != _lib.DOPT_MEM_HOST:
+            raise TypeError("set_csc takes host (numpy / scipy) arrays")
+        mats = [csc(Q, n), csc(G, m), csc(A, p)]
+        vecs = [vector(h, (B, m)) if m else None, vector(z, (B, n)),
+                vector(lam, (B, m)) if m else None, vector(nu, (B, p)) if p else None]
+        args = []
+        for cp, rv, nz, nnz in mats:
+            args += [st.ptr(cp), st.ptr(rv if nnz else None), st.ptr(nz if nnz else None), nnz]
+        rc = self.lib.dopt_qp_set_csc(self.h, *args, *[st.ptr(v) for v in vecs])
+        _lib.check(rc, self.h)
+
     def factor(self, singular_ok=False):
         return _lib.check(self.lib.dopt_qp_factor(self.h), self.h, singular_ok)
 

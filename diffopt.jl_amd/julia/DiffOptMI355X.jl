@@ -88,18 +88,26 @@ MOI.get(m::QPModel, a::DiffOpt.ReverseObjectiveFunction) = MOI.get(m.inner, a)
 DiffOpt._get_dA(m::QPModel, ci::MOI.ConstraintIndex) = DiffOpt._get_dA(m.inner, ci)
 DiffOpt._get_db(m::QPModel, ci::MOI.ConstraintIndex) = DiffOpt._get_db(m.inner, ci)
 
-# dense problem data in the engine's layout (column-major, λ/ν OptNet sign)
+# problem data in the MOI matrix form the reference's _gradient_cache builds
+# (QuadraticProgram.jl:182-213): SparseMatrixCSC{Float64,Int64} — handed to the
+# engine as is (dopt_qp_set_csc: colptr / rowval 1-based Int64, densified on
+# the device), λ/ν in OptNet sign
 function _problem(m::QPModel)
     inner = m.inner
-    A = Matrix{Float64}(QP._equalities(inner).coefficients)
-    G = Matrix{Float64}(QP._inequalities(inner).coefficients)
+    A = SparseArrays.SparseMatrixCSC{Float64,Int64}(QP._equalities(inner).coefficients)
+    G = SparseArrays.SparseMatrixCSC{Float64,Int64}(QP._inequalities(inner).coefficients)
     h = Vector{Float64}(QP._inequalities(inner).constants.upper)
     n = length(inner.x)
     obj = MOI.get(inner.model,
                   MOI.ObjectiveFunction{MOI.ScalarQuadraticFunction{Float64}}())
-    Q = Matrix{Float64}(DiffOpt.sparse_array_representation(obj, n).quadratic_terms)
+    Q = SparseArrays.SparseMatrixCSC{Float64,Int64}(
+        DiffOpt.sparse_array_representation(obj, n).quadratic_terms)
     return Q, G, h, A
 end
+
+_csc(M::SparseArrays.SparseMatrixCSC{Float64,Int64}) =
+    (M.colptr, isempty(M.rowval) ? Ptr{Int64}(C_NULL) : pointer(M.rowval),
+     isempty(M.nzval) ? Ptr{Float64}(C_NULL) : pointer(M.nzval), Int64(length(M.nzval)))
 
 function _ensure!(m::QPModel)
     inner = m.inner
@@ -109,12 +117,16 @@ function _ensure!(m::QPModel)
         h = m.handle = Handle(n, mi, p; device = m.device)
     end
     Q, G, hv, A = _problem(m)
+    q, g, a = _csc(Q), _csc(G), _csc(A)
     GC.@preserve Q G hv A inner begin
-        _check(ccall((:dopt_qp_set, LIB), Cint,
-                     (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                      Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
-                     h.ptr, _ptr(Q), _ptr(G), _ptr(hv), _ptr(A), _ptr(inner.x),
-                     _ptr(inner.λ), _ptr(inner.ν)), h.ptr)
+        _check(ccall((:dopt_qp_set_csc, LIB), Cint,
+                     (Ptr{Cvoid},
+                      Ptr{Int64}, Ptr{Int64}, Ptr{Float64}, Int64,
+                      Ptr{Int64}, Ptr{Int64}, Ptr{Float64}, Int64,
+                      Ptr{Int64}, Ptr{Int64}, Ptr{Float64}, Int64,
+                      Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                     h.ptr, q..., g..., a...,
+                     _ptr(hv), _ptr(inner.x), _ptr(inner.λ), _ptr(inner.ν)), h.ptr)
     end
     return h
 end

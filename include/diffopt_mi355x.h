@@ -92,6 +92,20 @@ int dopt_set_qp_fast_max(dopt_handle* h, int32_t fast_max);
 int dopt_qp_set(dopt_handle* h, const double* Q, const double* G,
                 const double* hvec, const double* A, const double* z,
                 const double* lam, const double* nu);
+/* Same as dopt_qp_set, with Q, G, A given in the MOI matrix form the
+ * reference builds (`_gradient_cache`, QuadraticProgram.jl:182-213;
+ * `sparse_array_representation`, utils.jl:46-69): Julia SparseMatrixCSC
+ * {Float64,Int64} arrays, 1-based.  For a batch, problem b's colptr is the
+ * (ncols+1) entries at X_colptr + b·(n+1) and indexes (1-based) into the
+ * concatenated X_rowval / X_nzval of X_nnz entries; all three matrices have n
+ * columns (Q n×n symmetrised, G m×n, A p×n).  The library densifies on the
+ * device (zero fill + scatter); a malformed colptr / rowval returns −1.
+ * Host mode copies the CSC arrays, device mode borrows them. */
+int dopt_qp_set_csc(dopt_handle* h,
+                    const int64_t* Q_colptr, const int64_t* Q_rowval, const double* Q_nzval, int64_t Q_nnz,
+                    const int64_t* G_colptr, const int64_t* G_rowval, const double* G_nzval, int64_t G_nnz,
+                    const int64_t* A_colptr, const int64_t* A_rowval, const double* A_nzval, int64_t A_nnz,
+                    const double* hv, const double* z, const double* lam, const double* nu);
 /* Assemble the KKT matrix (create_LHS_matrix, QuadraticProgram.jl:256-282),
  * select the solve branch per problem (`iterative = norm(Q) ≈ 0`, :333/:436)
  * and LU-factorise it ONCE (the reference re-factorises per call, :490).

@@ -224,6 +224,35 @@ def test_reverse_grads_materialised(QPBatch):
         np.testing.assert_array_equal(g2[k].cpu().numpy(), g[k])
 
 
+def test_csc_staging_matches_dense(QPBatch):
+    """dopt_qp_set_csc (MOI matrix form: Julia CSC, Int64, 1-based) densified
+    on the device gives bit-identical sensitivities to dopt_qp_set with the
+    same dense matrices; sparse G/A with empty columns; malformed CSC raises."""
+    import scipy.sparse as sp
+    from diffopt_amd import EngineError
+    d = _synthetic(3, 40, 60, 10, 0.5, 77)
+    B, n = d["z"].shape
+    m, p = 60, 10
+    rng = np.random.default_rng(5)
+    G = d["G"] * (rng.random(d["G"].shape) < 0.3)
+    G[:, :, 3] = 0.0                      # an empty column
+    A = d["A"] * (rng.random(d["A"].shape) < 0.5)
+    h = np.einsum("bmn,bn->bm", G, d["z"]) - np.einsum("bmn,bn->bm", d["G"], d["z"]) + d["h"]
+    e1 = QPBatch(B, n, m, p)
+    e1.set(d["Q"], G, h, A, d["z"], d["lam"], d["nu"])
+    r1, f1 = e1.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
+    e2 = QPBatch(B, n, m, p)
+    e2.set_csc([sp.csc_matrix(q) for q in d["Q"]], [sp.csc_matrix(g) for g in G], h,
+               [sp.csc_matrix(a) for a in A], d["z"], d["lam"], d["nu"])
+    r2, f2 = e2.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
+    np.testing.assert_array_equal(r1, r2)
+    np.testing.assert_array_equal(f1, f2)
+    bad = sp.csc_matrix(G[0])
+    bad.indices[0] = 99                   # row index out of range
+    with pytest.raises(EngineError):
+        e2.set_csc(sp.csc_matrix(d["Q"][0]), bad, h, sp.csc_matrix(A[0]), d["z"], d["lam"], d["nu"])
+
+
 def test_blocked_matches_fused_and_split(QPBatch):
     """Same batch through the fused kernel and the blocked path: agreement to
     rounding (different accumulation order only); blocked split calls
