@@ -476,38 +476,76 @@ const char* dopt_phase_name(int32_t phase) {
 }
 
 // ---- conic -----------------------------------------------------------------
+// cone-table validation + staging shared by the dense and CSC setters; `A` is
+// already a device pointer
+static void conic_set_common(Handle* h, const double* A, const double* b, const double* c,
+                             const double* x, const double* s, const double* y,
+                             const int32_t* cone_desc, int32_t ncones) {
+  const size_t B = h->batch, n = h->n, m = h->m;
+  if (!b || !c || !x || !s || !y) throw Error(-1, "A, b, c, x, s, y are required");
+  if (ncones < 0 || (ncones > 0 && !cone_desc)) throw Error(-1, "bad cone table");
+  int64_t rows = 0;
+  for (int k = 0; k < ncones; ++k) {
+    const int code = cone_desc[2 * k], dim = cone_desc[2 * k + 1];
+    if (code < 0 || code > DOPT_CONE_PSD_TRI || dim < 0) throw Error(-1, "bad cone code/dimension");
+    if (code == DOPT_CONE_SOC && dim < 1) throw Error(-1, "SecondOrderCone dimension must be >= 1");
+    if (code == DOPT_CONE_PSD_TRI) {
+      int d = 0;
+      while (d * (d + 1) / 2 < dim) ++d;
+      if (d * (d + 1) / 2 != dim) throw Error(-1, "PSD triangle dimension is not triangular");
+      if (d > 64) throw Error(-1, "PSD cones larger than 64×64 are not supported");
+    }
+    rows += dim;
+  }
+  if (rows != (int64_t)m) throw Error(-1, "cone dimensions do not add up to m");
+  h->cones.assign(cone_desc, cone_desc + 2 * ncones);
+  h->cA = A;
+  h->cb = stage_in(*h, h->own_cin[1], b, B * m);
+  h->cc = stage_in(*h, h->own_cin[2], c, B * n);
+  h->cx = stage_in(*h, h->own_cin[3], x, B * n);
+  h->cs = stage_in(*h, h->own_cin[4], s, B * m);
+  h->cy = stage_in(*h, h->own_cin[5], y, B * m);
+  h->cset = true;
+  h->cfactored = false;
+  DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+}
+
 int dopt_conic_set(dopt_handle* h, const double* A, const double* b, const double* c,
                    const double* x, const double* s, const double* y,
                    const int32_t* cone_desc, int32_t ncones) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_CONIC) throw Error(-1, "dopt_conic_set on a non-conic handle");
+    if (!A) throw Error(-1, "A, b, c, x, s, y are required");
+    conic_set_common(h, stage_in(*h, h->own_cin[0], A, (size_t)h->batch * h->m * h->n), b, c, x, s, y,
+                     cone_desc, ncones);
+    return 0;
+  });
+}
+
+int dopt_conic_set_csc(dopt_handle* h, const int64_t* A_colptr, const int64_t* A_rowval,
+                       const double* A_nzval, int64_t A_nnz, const double* b, const double* c,
+                       const double* x, const double* s, const double* y,
+                       const int32_t* cone_desc, int32_t ncones) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_CONIC) throw Error(-1, "dopt_conic_set_csc on a non-conic handle");
     const size_t B = h->batch, n = h->n, m = h->m;
-    if (!A || !b || !c || !x || !s || !y) throw Error(-1, "A, b, c, x, s, y are required");
-    if (ncones < 0 || (ncones > 0 && !cone_desc)) throw Error(-1, "bad cone table");
-    int64_t rows = 0;
-    for (int k = 0; k < ncones; ++k) {
-      const int code = cone_desc[2 * k], dim = cone_desc[2 * k + 1];
-      if (code < 0 || code > DOPT_CONE_PSD_TRI || dim < 0) throw Error(-1, "bad cone code/dimension");
-      if (code == DOPT_CONE_SOC && dim < 1) throw Error(-1, "SecondOrderCone dimension must be >= 1");
-      if (code == DOPT_CONE_PSD_TRI) {
-        int d = 0;
-        while (d * (d + 1) / 2 < dim) ++d;
-        if (d * (d + 1) / 2 != dim) throw Error(-1, "PSD triangle dimension is not triangular");
-        if (d > 64) throw Error(-1, "PSD cones larger than 64×64 are not supported");
-      }
-      rows += dim;
-    }
-    if (rows != (int64_t)m) throw Error(-1, "cone dimensions do not add up to m");
-    h->cones.assign(cone_desc, cone_desc + 2 * ncones);
-    h->cA = stage_in(*h, h->own_cin[0], A, B * m * n);
-    h->cb = stage_in(*h, h->own_cin[1], b, B * m);
-    h->cc = stage_in(*h, h->own_cin[2], c, B * n);
-    h->cx = stage_in(*h, h->own_cin[3], x, B * n);
-    h->cs = stage_in(*h, h->own_cin[4], s, B * m);
-    h->cy = stage_in(*h, h->own_cin[5], y, B * m);
-    h->cset = true;
-    h->cfactored = false;
+    if (!A_colptr) throw Error(-1, "A, b, c, x, s, y are required");
+    if (A_nnz < 0 || (A_nnz > 0 && (!A_rowval || !A_nzval))) throw Error(-1, "bad CSC nnz / arrays");
+    h->csc_err.ensure(sizeof(int));
+    DOPT_CHECK_HIP(hipMemsetAsync(h->csc_err.p, 0, sizeof(int), h->stream));
+    const int64_t* cp = stage_in_i64(*h, h->csc_in[0], A_colptr, B * (n + 1));
+    const int64_t* rv = stage_in_i64(*h, h->csc_in[1], A_rowval, (size_t)A_nnz);
+    const double* nz = stage_in(*h, h->csc_in_val[0], A_nzval, (size_t)A_nnz);
+    DevBuf& d = h->own_cin[0];
+    d.ensure(std::max<size_t>(B * m * n, 1) * sizeof(double));
+    if (m) dopt::csc_to_dense(*h, cp, rv ? rv : cp, nz ? nz : d.as<double>(), A_nnz, (int)m, (int)n,
+                              d.as<double>(), h->csc_err.as<int>());
+    int herr = 0;
+    DOPT_CHECK_HIP(hipMemcpyAsync(&herr, h->csc_err.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
     DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    if (herr) throw Error(-1, (herr & 1) ? "CSC colptr is not monotone / out of range"
+                                         : "CSC rowval out of range");
+    conic_set_common(h, d.as<double>(), b, c, x, s, y, cone_desc, ncones);
     return 0;
   });
 }

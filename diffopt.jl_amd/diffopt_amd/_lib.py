@@ -41,6 +41,8 @@ SIGNATURES = {
     "dopt_qp_factor": (ctypes.c_int, [_h]),
     "dopt_qp_reverse": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_void_p]),
     "dopt_qp_reverse_grads": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 7),
+    "dopt_conic_set_csc": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_int64] + [ctypes.c_void_p] * 6 + [ctypes.c_int32]),
     "dopt_qp_set_csc": (ctypes.c_int, [_h] + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_int64] * 3 + [ctypes.c_void_p] * 4),
     "dopt_qp_forward": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 7),

@@ -73,6 +73,37 @@ class ConicBatch:
                                      desc.ctypes.data if desc.size else None, len(self.cones))
         _lib.check(rc, self.h)
 
+    def set_csc(self, A, b, c, x, s, y):
+        """``set`` with ``A`` (MOI coefficients, m × n) as scipy.sparse — one per
+        problem or one shared — passed as Julia CSC arrays (Int64, 1-based) to
+        dopt_conic_set_csc, which densifies on the device.  Host mode."""
+        import scipy.sparse as sp
+        B, n, m = self.batch, self.n, self.m
+        mats = [A] * B if sp.issparse(A) else list(A)
+        cps, rvs, nzs, off = [], [], [], 0
+        for M in mats:
+            M = sp.csc_matrix(M)
+            if M.shape != (m, n):
+                raise ValueError(f"sparse A of shape {M.shape}, expected {(m, n)}")
+            cps.append(M.indptr.astype(np.int64) + off + 1)
+            rvs.append(M.indices.astype(np.int64) + 1)
+            nzs.append(M.data.astype(np.float64))
+            off += M.nnz
+        cp = np.ascontiguousarray(np.concatenate(cps))
+        rv = np.ascontiguousarray(np.concatenate(rvs))
+        nz = np.ascontiguousarray(np.concatenate(nzs))
+        st = self._stage([b, c, x, s, y])
+        if st.mem != _lib.DOPT_MEM_HOST:
+            raise TypeError("set_csc takes host (numpy / scipy) arrays")
+        vecs = [vector(b, (B, m)), vector(c, (B, n)), vector(x, (B, n)), vector(s, (B, m)),
+                vector(y, (B, m))]
+        desc = np.array([v for cd in self.cones for v in cd], dtype=np.int32)
+        rc = self.lib.dopt_conic_set_csc(self.h, cp.ctypes.data, rv.ctypes.data if off else None,
+                                         nz.ctypes.data if off else None, off,
+                                         *[st.ptr(v) for v in vecs],
+                                         desc.ctypes.data if desc.size else None, len(self.cones))
+        _lib.check(rc, self.h)
+
     def factor(self):
         _lib.check(self.lib.dopt_conic_factor(self.h), self.h)
 

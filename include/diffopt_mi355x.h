@@ -155,6 +155,15 @@ int dopt_qp_forward_reverse(dopt_handle* h, const double* dl_dz,
 int dopt_conic_set(dopt_handle* h, const double* A, const double* b,
                    const double* c, const double* x, const double* s,
                    const double* y, const int32_t* cone_desc, int32_t ncones);
+/* dopt_conic_set with A_moi in the reference's MOI matrix form (ConicProgram.jl
+ * _gradient_cache :172-255 reads it from MatrixOfConstraints): Julia
+ * SparseMatrixCSC{Float64,Int64} arrays, 1-based, batch layout as in
+ * dopt_qp_set_csc (colptr at offset b·(n+1), indexes into the concatenated
+ * rowval / nzval); densified on the device, malformed indices return −1. */
+int dopt_conic_set_csc(dopt_handle* h, const int64_t* A_colptr, const int64_t* A_rowval,
+                       const double* A_nzval, int64_t A_nnz, const double* b, const double* c,
+                       const double* x, const double* s, const double* y,
+                       const int32_t* cone_desc, int32_t ncones);
 /* _gradient_cache (ConicProgram.jl:172-255): v = y − s, Dπ(v), π(v), M. */
 int dopt_conic_factor(dopt_handle* h);
 /* forward_differentiate! (ConicProgram.jl:257-334): out[b] = [du | dv | dw]

@@ -191,6 +191,38 @@ def test_zero_rhs_gives_zero(ConicBatch):
     e.close()
 
 
+def test_csc_staging_matches_dense(ConicBatch):
+    """dopt_conic_set_csc (A_moi as Julia CSC arrays, 1-based, densified on the
+    device) is bit-identical to dopt_conic_set with the same dense A; a
+    malformed colptr raises."""
+    import scipy.sparse as sp
+    from diffopt_amd import EngineError
+    from diffopt_amd.synthetic import conic_numpy
+    cones = [(0, 3), (1, 10), (3, 6), (4, 6)]
+    d = conic_numpy(3, 20, cones, 31)
+    A = d["A"].copy()
+    A[:, :, 2] = 0.0                      # an empty column
+    outs = []
+    for mode in ("dense", "csc"):
+        e = ConicBatch(3, 20, cones)
+        if mode == "dense":
+            e.set(A, d["b"], d["c"], d["x"], d["s"], d["y"])
+        else:
+            e.set_csc([sp.csc_matrix(a) for a in A], d["b"], d["c"], d["x"], d["s"], d["y"])
+        out, dx = e.forward(None, d["db"], d["dc"])
+        g = e.reverse(d["dx"])[0]
+        outs.append((np.asarray(out), np.asarray(dx), np.asarray(g)))
+        e.close()
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+    e = ConicBatch(1, 20, cones)
+    bad = sp.csc_matrix(A[0])
+    bad.indptr[5] = bad.indptr[4] - 1     # non-monotone colptr
+    with pytest.raises(EngineError):
+        e.set_csc(bad, d["b"][:1], d["c"][:1], d["x"][:1], d["s"][:1], d["y"][:1])
+    e.close()
+
+
 # ---------------------------------------------------------------------------
 # split path (row-block × problem grids, conic_split_* kernels): forced with
 # DOPT_CONIC_SPLIT=1 on the shapes above, and taken automatically for
