@@ -366,7 +366,7 @@ __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, con
 // PAIR_NC columns are in flight per wave (PAIR_NC·PAIR_K independent loads).
 constexpr int PAIR_K = 8;
 #ifndef DOPT_PAIR_NC
-#define DOPT_PAIR_NC 2
+#define DOPT_PAIR_NC 3   // r01f sweep on config 4: 1 → 458, 2 → 570, 3 → 587, 4 → 530 solves/s
 #endif
 constexpr int PAIR_NC = DOPT_PAIR_NC;   // columns in flight per wave
 constexpr int PAIR_ROWS = 64 * PAIR_K;
