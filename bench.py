@@ -269,6 +269,8 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--sync-allgather", action="store_true",
+                    help="N > 1: blocking all-gather per step instead of the overlapped pipeline")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -303,22 +305,33 @@ def main():
     out_rev = torch.empty(B, L, dtype=torch.float64, device="cuda")
     out_fwd = torch.empty(B, L, dtype=torch.float64, device="cuda")
     gathered = None
+    pipe = None
     if world > 1 and not args.no_allgather:
         from diffopt_amd import parallel
         gathered = True
         packed = torch.empty(B, 2 * L, dtype=torch.float64, device="cuda")
+        if not args.sync_allgather:
+            pipe = parallel.GatherPipeline(B, 2 * L, torch.float64, "cuda")
 
     def step():
         eng.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"] if p else None,
                             out_rev=out_rev, out_fwd=out_fwd)
         if gathered is not None:
             # weak scaling: every rank owns B problems of the world·B batch;
-            # one RCCL all-gather of the packed [rev | fwd] sensitivities
-            parallel.pack(out_rev, out_fwd, into=packed)
-            parallel.all_gather_rows(packed, world * B)
+            # one RCCL all-gather of the packed [rev | fwd] sensitivities per
+            # step, overlapped with the next step's kernels (GatherPipeline;
+            # every gather completes inside the timed region: drain() below)
+            if pipe is not None:
+                parallel.pack(out_rev, out_fwd, into=pipe.next_buffer())
+                pipe.submit()
+            else:
+                parallel.pack(out_rev, out_fwd, into=packed)
+                parallel.all_gather_rows(packed, world * B)
 
     for _ in range(args.warmup):
         step()
+    if pipe is not None:
+        pipe.drain()
     torch.cuda.synchronize()
     sizes = eng.system_size()
     eng.phase_times()                      # reset accumulators
@@ -329,6 +342,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if pipe is not None:
+        pipe.drain()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -396,7 +411,7 @@ def main():
                        "problems_per_gpu": B, "n": n, "m_ineq": m, "p_eq": p,
                        "active_fraction": cfg["phi"],
                        "reduced_kkt_size_mean": round(float(Ns.mean()), 1),
-                       "parallelism": f"batch-sharded x{world}" + (" + RCCL all-gather" if gathered is not None else "")},
+                       "parallelism": f"batch-sharded x{world}" + ((" + RCCL all-gather" + (" (overlapped)" if pipe is not None else "")) if gathered is not None else "")},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -58,6 +58,60 @@ def all_gather_rows(local, total, group=None):
     return torch.cat([buf[r * mx: r * mx + sizes[r]] for r in range(world)], dim=0)
 
 
+class GatherPipeline:
+    """All-gather of per-step packed sensitivities, overlapped with the next
+    step's compute (for streams of independent batches).
+
+    Two packed buffers alternate: `next_buffer()` returns the buffer to pack
+    step k into (first waiting for the gather that last read it, two steps
+    ago), `submit()` starts the asynchronous all-gather of it and returns at
+    once, `drain()` waits for every gather in flight.  With the ``nccl``
+    backend (RCCL) the waits order torch's current stream after the
+    collective without blocking the host, so step k's gather over xGMI runs
+    under step k+1's kernels.  Even shards only (every rank `rows` rows).
+    `result(k)` is the gathered (world·rows, width) tensor of step k once it
+    has completed (the two most recent steps are kept).
+    """
+
+    def __init__(self, rows, width, dtype, device, group=None):
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.bufs = [torch.empty(rows, width, dtype=dtype, device=device) for _ in range(2)]
+        self.outs = [torch.empty(self.world * rows, width, dtype=dtype, device=device)
+                     for _ in range(2)]
+        self.work = [None, None]
+        self.step = 0
+
+    def next_buffer(self):
+        i = self.step & 1
+        if self.work[i] is not None:
+            self.work[i].wait()
+            self.work[i] = None
+        return self.bufs[i]
+
+    def submit(self):
+        import torch.distributed as dist
+        i = self.step & 1
+        self.work[i] = dist.all_gather_into_tensor(self.outs[i], self.bufs[i], group=self.group,
+                                                   async_op=True)
+        self.step += 1
+
+    def drain(self):
+        for i in range(2):
+            if self.work[i] is not None:
+                self.work[i].wait()
+                self.work[i] = None
+
+    def result(self, k):
+        if k < self.step - 2 or k >= self.step:
+            raise IndexError(f"step {k} is not among the last two submitted")
+        if self.work[k & 1] is not None:
+            self.work[k & 1].wait()
+            self.work[k & 1] = None
+        return self.outs[k & 1]
+
+
 def sharded_forward_reverse(engine_factory, data, total, group=None):
     """Run one batch-sharded fwd+rev sensitivity solve.
 

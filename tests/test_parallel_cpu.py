@@ -94,3 +94,48 @@ def test_gloo_world2_even_split():
 
 def test_gloo_world3_ragged_split():
     _run(3, 7)
+
+
+def _pipeline_worker(rank, world, port, steps, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rows, width = 3, 5
+        pipe = parallel.GatherPipeline(rows, width, torch.float64, "cpu")
+        got = {}
+        for k in range(steps):
+            buf = pipe.next_buffer()
+            buf.copy_(torch.full((rows, width), 100.0 * k + rank, dtype=torch.float64)
+                      + torch.arange(rows * width, dtype=torch.float64).reshape(rows, width))
+            pipe.submit()
+            if k >= 1:      # the previous step's gather may complete under this step
+                got[k - 1] = pipe.result(k - 1).clone()
+        pipe.drain()
+        got[steps - 1] = pipe.result(steps - 1).clone()
+        q.put((rank, {k: v.numpy() for k, v in got.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_gather_pipeline_world2():
+    """GatherPipeline (bench.py's overlapped all-gather): every step's
+    gathered rows are exactly the ranks' packed rows in rank order, with two
+    gathers in flight and the buffers reused."""
+    world, steps = 2, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_pipeline_worker, args=(r, world, port, steps, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    base = np.arange(15, dtype=np.float64).reshape(3, 5)
+    for _, got in res:
+        assert sorted(got) == list(range(steps))
+        for k, v in got.items():
+            ref = np.concatenate([base + 100.0 * k + r for r in range(world)])
+            assert np.array_equal(v, ref)
