@@ -517,10 +517,14 @@ __device__ __forceinline__ int prepare_wg(const QPIn& P, int b, double* s_out, i
 // FastLDS's perm / y / tmp, free here, or the dynamic LDS of the standalone
 // assembly kernel); kept sets larger than `cap` are gathered from global
 // memory instead (`tiles` = one 16×17 transpose tile per wave).
+// G-pass tile (standalone assembly kernel): 64 kept rows × 64 columns of G
+constexpr int GP_R = 64, GP_C = 64, GP_LD = GP_C + 1;
+
+template <bool GPASS>
 __device__ __forceinline__ void assemble_rows(const QPIn& P, int b, const double* s,
                                               const int32_t* kidx, int nk, double* K, int ld,
                                               int* kid_l, double* lamk_l, double* sk_l, int cap,
-                                              double (*tiles)[16 * 17]) {
+                                              double (*tiles)[16 * 17], double* gtile = nullptr) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n = P.n, m = P.m, p = P.p;
   const int N = n + nk + p;
@@ -554,7 +558,10 @@ __device__ __forceinline__ void assemble_rows(const QPIn& P, int b, const double
       const double* base;
       size_t cstride;
       if (r < n) { base = Qb + r; cstride = n; }
-      else if (r < n + nk) { base = Gb + kid[r - n]; cstride = m; }
+      else if (r < n + nk) {   // G_k rows (GPASS: written by the G pass below)
+        base = GPASS ? Qb : Gb + kid[r - n];
+        cstride = GPASS ? 0 : m;
+      }
       else if (r < N) { base = Ab + (r - n - nk); cstride = p; }
       else { base = Qb; cstride = 0; }
       double v[4];
@@ -582,7 +589,7 @@ __device__ __forceinline__ void assemble_rows(const QPIn& P, int b, const double
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = r0 + lg + 4 * q;
-      const bool ld_ok = r < n && (cG || cA);
+      const bool ld_ok = r < n && ((!GPASS && cG) || cA);
       v[q] = cbase[(size_t)(ld_ok ? r : 0) * rstride];
       double val;
       if (c < n) val = tl[lr * 17 + lg + 4 * q];
@@ -595,8 +602,49 @@ __device__ __forceinline__ void assemble_rows(const QPIn& P, int b, const double
       v[q] = val;
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) K[(size_t)(r0 + lg + 4 * q) * ld + c] = v[q];
+    for (int q = 0; q < 4; ++q) {
+      const int r = r0 + lg + 4 * q;
+      if (!GPASS || !((r < n && cG) || (r >= n && r < n + nk && c < n)))
+        K[(size_t)r * ld + c] = v[q];
+    }
     __builtin_amdgcn_wave_barrier();
+  }
+  if constexpr (GPASS) {
+    __syncthreads();   // the G-pass tile aliases the transpose tiles
+    // G pass: 64 kept rows × 64 columns per step.  Wave w loads columns
+    // j0 + w + 8u (u < 8) of the 64 kept rows (lane ↔ kept row: sorted row
+    // indices, so a wave's loads cover the same lines a dense sweep would),
+    // writes G_kᵀΛ straight out (K row j, 64 consecutive columns n + ci) and
+    // stages the values in LDS; then the block writes the G_k rows out as
+    // 64-column (512 B) contiguous segments.
+    const int NT = (int)blockDim.x;
+    for (int ci0 = 0; ci0 < nk; ci0 += GP_R) {
+      const int ci = ci0 + lane;
+      const bool rok = ci < nk;
+      const int gi = rok ? kid[ci] : 0;
+      const double li = rok ? (staged ? lamk_l[ci] : lb[gi]) : 0.0;
+      for (int j0 = 0; j0 < n; j0 += GP_C) {
+        double gv[GP_C / 8];
+#pragma unroll
+        for (int u = 0; u < GP_C / 8; ++u) {
+          const int j = j0 + wv + 8 * u;
+          gv[u] = Gb[gi + (size_t)min(j, n - 1) * m];
+        }
+#pragma unroll
+        for (int u = 0; u < GP_C / 8; ++u) {
+          const int j = j0 + wv + 8 * u;
+          if (rok && j < n) K[(size_t)j * ld + n + ci] = gv[u] * li;
+          gtile[lane * GP_LD + wv + 8 * u] = gv[u];
+        }
+        __syncthreads();
+        for (int e = t; e < GP_R * GP_C; e += NT) {
+          const int rr = e / GP_C, cc = e - rr * GP_C;
+          if (ci0 + rr < nk && j0 + cc < n)
+            K[(size_t)(n + ci0 + rr) * ld + j0 + cc] = gtile[rr * GP_LD + cc];
+        }
+        __syncthreads();
+      }
+    }
   }
   __syncthreads();
 }
@@ -604,7 +652,7 @@ __device__ __forceinline__ void assemble_rows(const QPIn& P, int b, const double
 __device__ __forceinline__ void assemble_wg(const QPIn& P, int b, const double* s,
                                             const int32_t* kidx, int nk, double* K, int ld,
                                             FastLDS& S) {
-  assemble_rows(P, b, s, kidx, nk, K, ld, S.perm, S.y, S.tmp, FAST_MAX, S.atile);
+  assemble_rows<false>(P, b, s, kidx, nk, K, ld, S.perm, S.y, S.tmp, FAST_MAX, S.atile);
 }
 
 __device__ __forceinline__ void rev_rhs_wg(const double* dl_dz, int b, int n, int N, FastLDS& S) {
@@ -830,7 +878,10 @@ __global__ __launch_bounds__(FT) void qp_solve_fast_kernel(
 __global__ __launch_bounds__(FT) void qp_prep_asm_kernel(
     QPIn P, double* __restrict__ Kper, int ld_per, int nmax, double* __restrict__ s,
     int32_t* __restrict__ kidx, int32_t* __restrict__ rpos, QPMeta* __restrict__ meta, int cap) {
-  __shared__ double tiles[NW][16 * 17];
+  // the transpose tiles (tile loop) and the G-pass tile are never live together
+  __shared__ double tbuf[GP_R * GP_LD > NW * 16 * 17 ? GP_R * GP_LD : NW * 16 * 17];
+  double (*tiles)[16 * 17] = reinterpret_cast<double (*)[16 * 17]>(tbuf);
+  double* gtile = tbuf;
   __shared__ int cnt[NW + 1];
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   double* zsm = dyn;                           // n
@@ -840,8 +891,8 @@ __global__ __launch_bounds__(FT) void qp_prep_asm_kernel(
   const int b = blockIdx.x;
   prepare_wg(P, b, s, kidx, rpos, meta, zsm, cnt);
   const int nk = meta[b].nk;
-  assemble_rows(P, b, s, kidx, nk, Kper + (size_t)b * nmax * ld_per, ld_per, kid, lamk, sk, cap,
-                tiles);
+  assemble_rows<true>(P, b, s, kidx, nk, Kper + (size_t)b * nmax * ld_per, ld_per, kid, lamk, sk, cap,
+                      tiles, gtile);
 }
 
 // kept-row staging capacity of qp_prep_asm_kernel (all of m while the dynamic
