@@ -702,6 +702,7 @@ __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict_
         has[q] = fwd ? e < Np : e < i0;
         ev[q] = e;
         const int ec = has[q] ? e : i0;
+        if (!__any(has[q])) continue;   // the whole wave is past the entries: no loads
         if (!trans) {
           const double* row = Kb + (size_t)ps[ec] * ld + i0;
 #pragma unroll
@@ -806,6 +807,7 @@ __device__ __forceinline__ void solve_rows_body(int b, const double* __restrict_
       auto load_chunk = [&](int c) {
 #pragma unroll
         for (int p = 0; p < RCH; ++p) {
+          if ((c * RCH + p) * RPASS >= ecnt) break;   // pass wholly past the entries (uniform)
           const int li = (c * RCH + p) * RPASS + rid;
           const int ec = li < ecnt ? e0 + li : i0;   // clamped: a valid row, result unused
           const double* row = Kb + (size_t)ps[ec] * ld + i0 + 4 * g8;
@@ -830,6 +832,7 @@ __device__ __forceinline__ void solve_rows_body(int b, const double* __restrict_
         if (c > 0) load_chunk(c);
 #pragma unroll
         for (int p = 0; p < RCH; ++p) {
+          if ((c * RCH + p) * RPASS >= ecnt) break;
           double d = f[p][0] * xk[0];
 #pragma unroll
           for (int u = 1; u < 4; ++u) d = fma(f[p][u], xk[u], d);
