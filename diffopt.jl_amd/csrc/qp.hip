@@ -502,7 +502,15 @@ __global__ __launch_bounds__(TPB) void qp_output_kernel(
       xl = xb[n + kk];
     } else if (!trans) {
       double acc = 0.0;
-      for (int j = 0; j < n; ++j) acc = fma(Gb[l + (size_t)j * m], xz[j], acc);
+      int j = 0;
+      for (; j + 8 <= n; j += 8) {   // 8 loads in flight, same summation order
+        double gv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) gv[u] = Gb[l + (size_t)(j + u) * m];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = fma(gv[u], xz[j + u], acc);
+      }
+      for (; j < n; ++j) acc = fma(Gb[l + (size_t)j * m], xz[j], acc);
       xl = (0.0 - acc) / s[(size_t)b * m + l];
     } else {
       xl = full[(size_t)b * nmax + n + l] / s[(size_t)b * m + l];
