@@ -284,8 +284,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void b
     }
 #pragma unroll
     for (int jj = 0; jj < BNB; ++jj) Linv[jj * BLP + c] = x[jj];
-  } else if (wv == 1 && lane < BNB) {
-    const int c = lane;
+  } else if (TW > 1 ? (wv == 1 && lane < BNB) : (wv == 0 && lane >= BNB)) {
+    const int c = lane & (BNB - 1);   // single-wave panels: the upper 32 lanes
     double x[BNB];
 #pragma unroll
     for (int jj = 0; jj < BNB; ++jj) x[jj] = (jj == c) ? 1.0 : 0.0;
@@ -964,6 +964,8 @@ void qp_blocked_factor(Handle& h, double* dinv) {
     if (DOPT_PANEL_VARIANT == 1 && R > 128 && R <= 512) {   // tuning build: 4 waves, 1–2 rows/thread
       if (R <= 256) DOPT_PANEL(256, 1);
       else DOPT_PANEL(256, 2);
+    } else if (DOPT_PANEL_VARIANT == 2 && R <= 128) {   // tuning build: one wave, no cross-wave fold
+      DOPT_PANEL(64, 2);
     } else if (R <= 128) DOPT_PANEL(128, 1);
     else if (R <= 256) DOPT_PANEL(128, 2);
     else if (R <= 384) DOPT_PANEL(128, 3);
