@@ -111,6 +111,7 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
       const int ct = atoi(e);
       h->upd_ct = ct >= 4 ? 4 : (ct >= 2 ? 2 : 1);
     }
+    if (const char* e = getenv("DOPT_SOLVE_ILV")) h->solve_ilv = atoi(e) != 0;
     if (const char* e = getenv("DOPT_LU_STREAMS")) {
       h->lu_streams = std::max(1, std::min(atoi(e), DOPT_MAX_LU_STREAMS));
     }

@@ -117,6 +117,11 @@ struct Handle {
   // prefetching strip kernel measured within ±2 % of one tile per WG (r01f)
   int32_t upd_ct = 1;
   int32_t lu_streams = 1;   // 2–4 measured no faster on configs 2 and 3 (r01f)
+  // solve2 workgroup order (env DOPT_SOLVE_ILV): 0 = all row sweeps then all
+  // column sweeps; 1 = the two directions of each group of 8 problems
+  // adjacent in dispatch order, on the same XCD (r01j: config-2 solve phase
+  // 0.458 → 0.413 ms, config 3 unchanged)
+  int32_t solve_ilv = 1;
   hipStream_t sub_stream[DOPT_MAX_LU_STREAMS] = {};
   hipEvent_t join_ev[DOPT_MAX_LU_STREAMS] = {};
   hipEvent_t fork_ev = nullptr;

@@ -880,12 +880,16 @@ __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict
                                                         const double* __restrict__ rhs_rev,
                                                         const double* __restrict__ rhs_fwd,
                                                         double* __restrict__ x_rev,
-                                                        double* __restrict__ x_fwd) {
+                                                        double* __restrict__ x_fwd, int ilv) {
   __shared__ double v[BLOCKED_MAX];
   __shared__ double y[BLOCKED_MAX];
   __shared__ int ps[BLOCKED_MAX];
   __shared__ double part[BNB];
-  const int L = blockIdx.x;
+  int L = blockIdx.x;
+  if (ilv) {   // B % 8 == 0: workgroups 16g+j (rows) and 16g+8+j (columns) solve problem 8g+j
+    const int g = L >> 4, j = L & 7;
+    L = (L & 8) ? B + 8 * g + j : 8 * g + j;
+  }
   if (L < B)
     solve_rows_body(L, K, ld, nmax, perm, dinv, dstride, meta, fast_max, rhs_rev, x_rev, v, ps, part);
   else
@@ -1099,7 +1103,8 @@ void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, con
   const int ent = (npmax + PT - 1) / PT;
 #define DOPT_SOLVE2(E)                                                                            \
   hipLaunchKernelGGL(blu_solve2_kernel<E>, dim3(2 * B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm, \
-                     dinv, dstride, meta, h.fast_max, B, rhs_rev, rhs_fwd, x_rev, x_fwd)
+                     dinv, dstride, meta, h.fast_max, B, rhs_rev, rhs_fwd, x_rev, x_fwd, ilv)
+  const int ilv = h.solve_ilv && B % 8 == 0;
   if (ent <= 1) DOPT_SOLVE2(1);
   else if (ent == 2) DOPT_SOLVE2(2);
   else DOPT_SOLVE2(3);

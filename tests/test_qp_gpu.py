@@ -195,6 +195,26 @@ def test_blocked_update_strips(QPBatch, monkeypatch, ct):
     _check_batch(QPBatch, _synthetic(2, 1000, 1500, 0, 0.3, 20250310))
 
 
+@pytest.mark.parametrize("B", [16, 12])
+def test_solve2_interleaved_order(QPBatch, monkeypatch, B):
+    """Both-direction solve with the directions of each group of 8 problems
+    adjacent in dispatch order (DOPT_SOLVE_ILV=1, the default; B % 8 != 0
+    falls back to the split order): bit-identical to the split order, and
+    oracle parity."""
+    d = _synthetic(B, 120, 150, 10, 0.4, 20250311)
+    n = d["z"].shape[1]
+    outs = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("DOPT_SOLVE_ILV", env)
+        e = QPBatch(B, n, 150, 10)
+        e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+        outs.append(e.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"]))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    monkeypatch.delenv("DOPT_SOLVE_ILV")
+    _check_batch(QPBatch, d)
+
+
 def test_reverse_grads_materialised(QPBatch):
     """dopt_qp_reverse_grads: ReverseObjectiveFunction / ReverseConstraintFunction
     of every problem (QuadraticProgram.jl:448-473, :307-314) against the
