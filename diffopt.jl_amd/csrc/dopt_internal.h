@@ -119,8 +119,9 @@ struct Handle {
   int32_t lu_streams = 1;   // 2–4 measured no faster on configs 2 and 3 (r01f)
   // solve2 workgroup order (env DOPT_SOLVE_ILV): 0 = all row sweeps then all
   // column sweeps; 1 = the two directions of each group of 8 problems
-  // adjacent in dispatch order, on the same XCD (r01j: config-2 solve phase
-  // 0.458 → 0.413 ms, config 3 unchanged)
+  // adjacent in dispatch order, on the same XCD, so the launch does not end
+  // with only the longer column sweeps in flight (r01j: config-2 solve phase
+  // 0.458 → 0.413 ms, config 3 unchanged; HBM reads only 2 % lower)
   int32_t solve_ilv = 1;
   hipStream_t sub_stream[DOPT_MAX_LU_STREAMS] = {};
   hipEvent_t join_ev[DOPT_MAX_LU_STREAMS] = {};
