@@ -120,7 +120,7 @@ struct Handle {
   // solve2 workgroup order (env DOPT_SOLVE_ILV): 0 = all row sweeps then all
   // column sweeps; 1 = the two directions of each group of 8 problems
   // adjacent in dispatch order, on the same XCD, so the launch does not end
-  // with only the longer column sweeps in flight (r01j: config-2 solve phase
+  // with only column sweeps in flight (r01j: config-2 solve phase
   // 0.458 → 0.413 ms, config 3 unchanged; HBM reads only 2 % lower)
   int32_t solve_ilv = 1;
   hipStream_t sub_stream[DOPT_MAX_LU_STREAMS] = {};
