@@ -1,15 +1,18 @@
 #!/usr/bin/env python3
 """bench.py — KKT sensitivity solves/sec (forward + reverse) on batched dense QPs.
 
-Workload (BASELINE.json configs[1] = config 2): per GPU a batch of 1024 dense
-QPs, n = 200 variables, m = 300 inequalities (p = 0), 30 % active, synthetic
+Workload: N = 1 (no torchrun) — BASELINE.json configs[1] = config 2: a batch
+of 1024 dense QPs, n = 200 variables, m = 300 inequalities (p = 0), 30 %
+active.  N > 1 (torchrun) — configs[2] = config 3, the north_star headline:
+n = 1000, m = 1500, 1024 problems per rank (8192 on 8 GPUs).  Synthetic
 (seeded, KKT point by construction — SURVEY.md §8(d)), inputs resident in HBM
 before the timed region.  One step = for every problem of the batch: KKT
 assembly + LU factorisation + reverse solve (dl/dz → dz, dλ, dν) + forward
 solve (dq, dh → dz, dλ, dν) — the reference refactorises per call; the engine
 factors once per step and reuses it for both directions.  N > 1: one process
-per GPU, problems sharded (weak scaling: 1024 per rank), plus one RCCL
-all-gather of the packed sensitivities per step (§8(e)).
+per GPU, problems sharded (weak scaling), plus one RCCL all-gather of the
+packed sensitivities per step (§8(e)).  `--lam-eps 1e-9` gives the inactive
+rows tiny non-zero duals (interior-point-like: no exact elimination, N' = n+m).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...   (driver, N > 1)
@@ -50,7 +53,7 @@ def _cpu_worker(args):
     os.environ["OPENBLAS_NUM_THREADS"] = "1"
     from diffopt_amd.synthetic import qp_numpy
     from oracle import qp as oqp
-    d = qp_numpy(1, cfg["n"], cfg["m"], cfg["p"], cfg["phi"], seed)
+    d = qp_numpy(1, cfg["n"], cfg["m"], cfg["p"], cfg["phi"], seed, lam_eps=cfg.get("lam_eps", 0.0))
     a = [d[k][0] for k in ["Q", "G", "h", "A", "z", "lam", "nu"]]
     n_done = 0
     t0 = time.perf_counter()
@@ -114,13 +117,17 @@ def _conic_cpu_worker(args):
     return k, t_cache, t_it
 
 
-def conic_cpu_baseline(cfg, seconds, workers, iters_per_solve):
+def conic_cpu_samples(cfg, seconds, workers):
     import multiprocessing as mp
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
         res = pool.map(_conic_cpu_worker, [(cfg, 1000 + i, seconds) for i in range(workers)])
-    wall = time.perf_counter() - t0
+    return res, time.perf_counter() - t0, workers
+
+
+def conic_cpu_baseline(cfg, seconds, samples, iters_per_solve):
+    res, wall, workers = samples
     if cfg == 4:
         solves = sum(r[0] for r in res)
         rate = sum(r[0] / r[1] for r in res)
@@ -149,6 +156,13 @@ def run_conic(args, world, rank, local_rank):
     n, cones = c["n"], c["cones"]
     B = args.batch or CONIC_CFG[args.config]["batch"]
     m = sum(dim for _, dim in cones)
+    # the CPU baseline forks worker processes: run it before this process
+    # initialises HIP (config 5 extrapolates with the engine's iteration
+    # counts, a host computation done after the GPU run)
+    cpu_raw = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        workers = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
+        cpu_raw = conic_cpu_samples(args.config, args.cpu_seconds, workers)
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
@@ -203,9 +217,8 @@ def run_conic(args, world, rank, local_rank):
         elapsed = float(tt.item())
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            workers = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
-            cpu = conic_cpu_baseline(args.config, args.cpu_seconds, workers,
+        if cpu_raw is not None:
+            cpu = conic_cpu_baseline(args.config, args.cpu_seconds, cpu_raw,
                                      float(it_f.mean() + it_r.mean()))
         plen = 0
         for code, dim in cones:
@@ -263,7 +276,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(QP_CFG) + sorted(CONIC_CFG))
+    ap.add_argument("--config", type=int, default=None, choices=sorted(QP_CFG) + sorted(CONIC_CFG),
+                    help="default: 2 at N = 1, 3 (the north_star headline) under torchrun")
+    ap.add_argument("--lam-eps", type=float, default=0.0,
+                    help="QP: inactive rows get λ = LAM_EPS instead of 0 (no exact elimination)")
     ap.add_argument("--batch", type=int, default=None, help="problems per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-workers", type=int, default=None)
@@ -276,9 +292,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.config is None:
+        args.config = 3 if world > 1 else 2
     if args.config in CONIC_CFG:
         return run_conic(args, world, rank, local_rank)
     cfg = dict(QP_CFG[args.config])
+    cfg["lam_eps"] = args.lam_eps
     if args.batch:
         cfg["batch"] = args.batch
     B, n, m, p = cfg["batch"], cfg["n"], cfg["m"], cfg["p"]
@@ -298,7 +317,7 @@ def main():
     from diffopt_amd.qp import QPBatch
     from diffopt_amd.synthetic import SEED0, qp_torch
 
-    d = qp_torch(B, n, m, p, cfg["phi"], SEED0 + args.config, rank_offset=rank)
+    d = qp_torch(B, n, m, p, cfg["phi"], SEED0 + args.config, rank_offset=rank, lam_eps=args.lam_eps)
     eng = QPBatch(B, n, m, p, device=local_rank)
     eng.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
     L = n + m + p
@@ -334,6 +353,7 @@ def main():
         pipe.drain()
     torch.cuda.synchronize()
     sizes = eng.system_size()
+    kinds = eng.lu_kind()
     eng.phase_times()                      # reset accumulators
     eng.set_profiling(True)
     if dist:
@@ -364,26 +384,17 @@ def main():
         name, (ms_tot, cnt) = max(phases.items(), key=lambda kv: kv[1][0])
         avg_s = ms_tot / cnt / 1e3
         Ns = sizes.astype("float64")
-        # algorithmic HBM bytes of one fused step: read Q, G, h, z, λ (+A, ν) and
-        # the tangents, write both sensitivity vectors
-        io_bytes = float(B * 8.0 * (n * n + (m + p) * n + 2 * m + 2 * p + 3 * n + m + 2 * L))
-        if name in ("qp_lu", "qp_fused"):
-            # reduced-KKT LU flops (+ the two triangular-solve pairs when fused)
+        if name in ("qp_lu", "qp_lu_pivot"):
+            # algorithmic flops of the reduced-KKT LU, (2/3)·N'³ per problem
             work = float((2.0 / 3.0 * Ns ** 3).sum())
-            if name == "qp_fused":
-                work += float((4.0 * Ns ** 2).sum())
             achieved = work / avg_s / 1e12
             roof = dict(bound="mfma", achieved=round(achieved, 3), peak=PEAK_FP64_TFLOPS,
                         unit="TFLOP/s", frac=round(achieved / PEAK_FP64_TFLOPS, 4))
-            if name == "qp_fused":
-                roof["io_GBs"] = round(io_bytes / avg_s / 1e9, 1)
         else:
             if name == "qp_solve":
-                work = float((8.0 * Ns ** 2).sum())               # one read of the LU factors
+                work = float((16.0 * Ns ** 2).sum())              # both directions read the factors
             elif name == "qp_assemble":
                 work = float(B * 8.0 * (n * n + 2 * m * n) + (8.0 * Ns ** 2).sum())
-            elif name == "qp_prepare":
-                work = float(B * 8.0 * (n * n + m * n + 3 * m + n))
             else:
                 work = float(B * 8.0 * (m * n + 2 * L))
             achieved = work / avg_s / 1e9
@@ -411,6 +422,9 @@ def main():
                        "problems_per_gpu": B, "n": n, "m_ineq": m, "p_eq": p,
                        "active_fraction": cfg["phi"],
                        "reduced_kkt_size_mean": round(float(Ns.mean()), 1),
+                       "inactive_dual": args.lam_eps,
+                       "factorisation": {"no_pivot": int((kinds == 1).sum()),
+                                         "partial_pivoting": int((kinds == 2).sum())},
                        "parallelism": f"batch-sharded x{world}" + ((" + RCCL all-gather" + (" (overlapped)" if pipe is not None else "")) if gathered is not None else "")},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -94,32 +94,16 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
   int rc = guarded(h, [&]() {
     DOPT_CHECK_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     h->own_stream = true;
-    if (const char* e = getenv("DOPT_STAMPS")) {
-      if (e[0] == '1') {
-        h->stamps.ensure(8 * sizeof(unsigned long long));
-        DOPT_CHECK_HIP(hipMemset(h->stamps.p, 0, 8 * sizeof(unsigned long long)));
-      }
-    }
     if (const char* e = getenv("DOPT_CONIC_SPLIT")) {
       if (e[0] == '0' || e[0] == '1') h->conic_split = e[0] - '0';
     }
-    if (const char* e = getenv("DOPT_LU_GROUP")) {
-      const int gsz = atoi(e);
-      h->lu_group = gsz == 0 ? 0 : std::max(2, std::min(gsz, 4));
-    }
-    if (const char* e = getenv("DOPT_UPD_CT")) {
-      const int ct = atoi(e);
-      h->upd_ct = ct >= 4 ? 4 : (ct >= 2 ? 2 : 1);
-    }
-    if (const char* e = getenv("DOPT_SOLVE_ILV")) h->solve_ilv = atoi(e) != 0;
-    if (const char* e = getenv("DOPT_LU_STREAMS")) {
-      h->lu_streams = std::max(1, std::min(atoi(e), DOPT_MAX_LU_STREAMS));
-    }
-    if (const char* e = getenv("DOPT_FAST_MAX")) {
-      h->fast_max = std::max(0, std::min(atoi(e), dopt::FAST_MAX_N));
-    }
+    if (const char* e = getenv("DOPT_LU")) h->lu_mode = atoi(e) != 0;
     if (kind == DOPT_KIND_QP) {
-      // Systems are identity-padded to whole 32-column LU panels (qp_fast.hip),
+      // largest supported system: the generic solve stages an nmax vector in
+      // LDS (64 KB), the blocked path is limited to BLOCKED_MAX unknowns
+      if ((int64_t)n + m + p > 8192)
+        throw Error(-1, "QP systems with n + m + p > 8192 are not supported");
+      // Systems are identity-padded to whole 32-column blocks (qp_assemble.hip),
       // so the per-problem stride / row stride are rounded up to 32.
       h->nmax = (int32_t)dopt::round_up(std::max(n + m + p, 1), 32);
       h->ld = h->nmax;
@@ -146,8 +130,8 @@ int dopt_destroy(dopt_handle* h) {
   if (!h) return 0;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  DevBuf* bufs[] = {&h->dinv, &h->stamps, &h->ws, &h->K, &h->ipiv, &h->s, &h->kidx, &h->meta, &h->rhs, &h->x, &h->cone_dev,
-                    &h->vp, &h->dpi, &h->M, &h->cwork, &h->cinfo};
+  DevBuf* bufs[] = {&h->dinv, &h->plist, &h->lsqr_ws, &h->binv, &h->K, &h->ipiv, &h->s, &h->kidx, &h->meta, &h->rhs,
+                    &h->x, &h->cone_dev, &h->vp, &h->dpi, &h->cwork, &h->cinfo, &h->csplit};
   for (auto* b : bufs) b->release();
   for (auto& b : h->own_in) b.release();
   for (auto& b : h->csc_in) b.release();
@@ -161,14 +145,8 @@ int dopt_destroy(dopt_handle* h) {
     (void)hipEventDestroy(pe.second.second);
   }
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
-  for (int k = 0; k < DOPT_MAX_LU_STREAMS; ++k) {
-    if (h->sub_stream[k]) {
-      (void)hipStreamSynchronize(h->sub_stream[k]);
-      (void)hipStreamDestroy(h->sub_stream[k]);
-    }
-    if (h->join_ev[k]) (void)hipEventDestroy(h->join_ev[k]);
-  }
-  if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
+  if (h->meta_host) (void)hipHostFree(h->meta_host);
+  if (h->meta_ev) (void)hipEventDestroy(h->meta_ev);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -190,15 +168,6 @@ int dopt_set_memory(dopt_handle* h, int32_t mem) {
   return guarded(h, [&]() {
     if (mem != DOPT_MEM_HOST && mem != DOPT_MEM_DEVICE) throw Error(-1, "bad memory mode");
     h->mem = mem;
-    return 0;
-  });
-}
-
-int dopt_set_qp_fast_max(dopt_handle* h, int32_t fast_max) {
-  return guarded(h, [&]() {
-    if (fast_max < 0 || fast_max > dopt::FAST_MAX_N) throw Error(-1, "fast_max must be in [0, 512]");
-    h->fast_max = fast_max;
-    h->factored = false;
     return 0;
   });
 }
@@ -370,7 +339,7 @@ int dopt_qp_forward_reverse(dopt_handle* h, const double* dl_dz, const double* d
     const double* f = stage_in(*h, h->tin[6], db, B * p);
     double* o1 = out_ptr(*h, h->tout[0], out_rev, B * L);
     double* o2 = out_ptr(*h, h->tout[1], out_fwd, B * L);
-    h->factored = false;  // the fused path always re-factorises (one solve = factor + fwd + rev)
+    h->factored = false;  // one solve = factor + fwd + rev (the factors are kept for later calls)
     dopt::qp_forward_reverse(*h, r, a, b, c, d, e, f, o1, o2);
     copy_out(*h, out_rev, o1, B * L);
     copy_out(*h, out_fwd, o2, B * L);
@@ -394,6 +363,41 @@ int dopt_get_info(dopt_handle* h, int32_t* info) {
       DOPT_CHECK_HIP(hipMemcpyAsync(info, h->cinfo.p, h->batch * sizeof(int32_t),
                                     hipMemcpyDeviceToHost, h->stream));
       DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    }
+    return 0;
+  });
+}
+
+int dopt_qp_get_kept(dopt_handle* h, int8_t* kept) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "QP only");
+    if (!kept) throw Error(-1, "kept is required");
+    if (!h->factored) throw Error(-1, "no factorisation has run");
+    const size_t B = h->batch, m = h->m;
+    std::vector<int32_t> rpos(B * m);
+    if (B * m)
+      DOPT_CHECK_HIP(hipMemcpyAsync(rpos.data(), h->kidx.as<int32_t>() + B * m, B * m * sizeof(int32_t),
+                                    hipMemcpyDeviceToHost, h->stream));
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    for (size_t i = 0; i < B * m; ++i) kept[i] = rpos[i] >= 0;
+    return 0;
+  });
+}
+
+int dopt_qp_get_lu_kind(dopt_handle* h, int8_t* kinds) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "QP only");
+    if (!kinds) throw Error(-1, "kinds is required");
+    std::vector<dopt::QPMeta> meta(h->batch);
+    DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h->meta.p, h->batch * sizeof(dopt::QPMeta),
+                                  hipMemcpyDeviceToHost, h->stream));
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    for (int64_t i = 0; i < h->batch; ++i) {
+      const auto& mm = meta[i];
+      const int r = dopt::qp_route(mm.iterative, mm.nsys);
+      kinds[i] = r == dopt::ROUTE_LSQR ? DOPT_LU_KIND_LSQR
+                 : r == dopt::ROUTE_GENERIC ? DOPT_LU_KIND_PIVOT
+                 : mm.lu == dopt::LU_NOPIV ? DOPT_LU_KIND_NOPIV : DOPT_LU_KIND_PIVOT;
     }
     return 0;
   });
@@ -433,18 +437,6 @@ int dopt_get_system_size(dopt_handle* h, int32_t* sizes) {
 
 double dopt_last_time(const dopt_handle* h) { return h ? h->last_time : -1.0; }
 
-int dopt_debug_stamps(dopt_handle* h, int64_t* out, int32_t n) {
-  return guarded(h, [&]() {
-    if (!h->stamps.p) return 0;
-    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
-    unsigned long long buf[8] = {0};
-    DOPT_CHECK_HIP(hipMemcpy(buf, h->stamps.p, sizeof(buf), hipMemcpyDeviceToHost));
-    for (int i = 0; i < n && i < 8; ++i) out[i] = (int64_t)buf[i];
-    DOPT_CHECK_HIP(hipMemset(h->stamps.p, 0, sizeof(buf)));
-    return 8;
-  });
-}
-
 int dopt_set_profiling(dopt_handle* h, int32_t on) {
   return guarded(h, [&]() {
     h->collect_phases();
@@ -471,8 +463,8 @@ int dopt_get_phase_times(dopt_handle* h, double* ms, int32_t* counts, int32_t np
 
 const char* dopt_phase_name(int32_t phase) {
   static const char* names[DOPT_NUM_PHASES] = {
-      "qp_prepare", "qp_assemble", "qp_lu", "qp_rhs", "qp_solve", "qp_lsqr", "qp_output",
-      "conic_cone", "conic_rhs", "conic_lsqr", "conic_output", "qp_fused"};
+      "qp_assemble", "qp_lu", "qp_lu_pivot", "qp_rhs", "qp_solve", "qp_lsqr", "qp_output",
+      "conic_cone", "conic_rhs", "conic_lsqr", "conic_output"};
   return (phase >= 0 && phase < DOPT_NUM_PHASES) ? names[phase] : "unknown";
 }
 

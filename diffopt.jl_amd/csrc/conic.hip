@@ -56,7 +56,7 @@ __device__ __forceinline__ int tri_idx(int i, int j) { return j * (j + 1) / 2 + 
 __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
     const ConeDesc* __restrict__ cones, int ncones, const double* __restrict__ y,
     const double* __restrict__ s, int m, int plen, double* __restrict__ v_out,
-    double* __restrict__ vp_out, double* __restrict__ params) {
+    double* __restrict__ vp_out, double* __restrict__ params, int* __restrict__ bad) {
   __shared__ double X[PSD_MAX][PSD_MAX + 1];
   __shared__ double V[PSD_MAX][PSD_MAX + 1];
   __shared__ double red[8];
@@ -71,7 +71,15 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
   double* vpb = vp_out + (size_t)b * m + cd.row;
   double* P = params + (size_t)b * plen + cd.poff;
   const int dim = cd.dim;
-  for (int i = t; i < dim; i += CTPB) vb[i] = yb[i] - sb[i];
+  // missing starts (NaN, the reference's marker) → the caller reports
+  // ConicProgram.jl:186-196's error: bit 0 for y (dual), bit 1 for s (primal)
+  int nan_bits = 0;
+  for (int i = t; i < dim; i += CTPB) {
+    const double yi = yb[i], si = sb[i];
+    nan_bits |= (yi != yi ? 1 : 0) | (si != si ? 2 : 0);
+    vb[i] = yi - si;
+  }
+  if (nan_bits) atomicOr(bad, nan_bits);
   __syncthreads();
   if (cd.code == DOPT_CONE_ZEROS) {
     for (int i = t; i < dim; i += CTPB) vpb[i] = vb[i];
@@ -1157,15 +1165,26 @@ void conic_factor(Handle& h) {
     DOPT_CHECK_HIP(hipMemcpyAsync(h.cone_dev.p, cd.data(), nc * sizeof(ConeDesc), hipMemcpyHostToDevice, h.stream));
   h.vp.ensure((size_t)2 * B * std::max(m, 1) * sizeof(double));  // v then vp
   h.dpi.ensure((size_t)B * h.dpi_len * sizeof(double));
+  h.csc_err.ensure(sizeof(int));
+  int* bad = h.csc_err.as<int>();
+  DOPT_CHECK_HIP(hipMemsetAsync(bad, 0, sizeof(int), h.stream));
   {
     PhaseTimer pt(h, DOPT_PHASE_CONIC_CONE);
     if (nc && B) {
       hipLaunchKernelGGL(conic_cone_kernel, dim3(nc, B), dim3(CTPB), 0, h.stream,
                          h.cone_dev.as<ConeDesc>(), nc, h.cy, h.cs, m, h.dpi_len,
-                         h.vp.as<double>(), h.vp.as<double>() + (size_t)B * m, h.dpi.as<double>());
+                         h.vp.as<double>(), h.vp.as<double>() + (size_t)B * m, h.dpi.as<double>(), bad);
       ccheck();
     }
   }
+  int hbad = 0;
+  DOPT_CHECK_HIP(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, h.stream));
+  DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+  // ConicProgram.jl:186-196 checks the dual start first
+  if (hbad & 1)
+    throw Error(-1, "Some constraints are missing a value for the `ConstraintDualStart` attribute.");
+  if (hbad & 2)
+    throw Error(-1, "Some constraints are missing a value for the `ConstraintPrimalStart` attribute.");
   h.cfactored = true;
 }
 

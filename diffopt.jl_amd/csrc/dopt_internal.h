@@ -47,29 +47,39 @@ struct DevBuf {
 };
 
 // Per-problem QP metadata (device, batch entries).
+// Factorisation kinds (QPMeta::lu).
+enum QPLu { LU_NONE = 0, LU_NOPIV = 1, LU_PIVOT = 2, LU_REJECT = 3 };
+// selection masks of the solve launches (bit k: solve problems with lu == k)
+constexpr int LU_SEL_NOPIV = 1 << LU_NOPIV;
+constexpr int LU_SEL_PIVOT = 1 << LU_PIVOT;
+constexpr int LU_SEL_ALL = LU_SEL_NOPIV | LU_SEL_PIVOT;
 struct QPMeta {
   int32_t nk;        // kept inequality rows
   int32_t nsys;      // size of the factorised system = n + nk + p
   int32_t iterative; // 1: LSQR branch (norm(Q) == 0)
-  int32_t info;      // 0 ok, k>0 zero pivot at column k
+  int32_t info;      // 0 ok, k>0 zero pivot at column k of the reduced system
+  int32_t lu;        // QPLu: which factors K holds
+  int32_t pad[3];
 };
 
-// Workgroup size of the fast QP kernels (qp_fast.hip); the launch sites in
-// qp.hip must use exactly this (the kernels' thread mappings assume it).
-constexpr int FAST_THREADS = 512;
-constexpr int FAST_MAX_N = 512;      // largest reduced system of the fused one-WG path
-constexpr int BLOCKED_MAX = 1536;    // largest reduced system of the blocked step path
-#define DOPT_MAX_LU_STREAMS 4
+constexpr int ASM_THREADS = 512;     // prepare + assembly workgroup size (qp_assemble.hip)
+constexpr int BLOCKED_MAX = 1536;    // largest reduced system of the blocked path
 
 // Which factorisation path a problem takes (decided per problem on the
-// device from its reduced size; fast_max ≤ FAST_MAX_N is a handle setting).
-enum QPRoute { ROUTE_LSQR = 0, ROUTE_FAST = 1, ROUTE_BLOCKED = 2, ROUTE_GENERIC = 3 };
-__host__ __device__ inline int qp_route(int iterative, int nsys, int fast_max) {
+// device from its reduced size).
+enum QPRoute { ROUTE_LSQR = 0, ROUTE_BLOCKED = 2, ROUTE_GENERIC = 3 };
+__host__ __device__ inline int qp_route(int iterative, int nsys) {
   if (iterative) return ROUTE_LSQR;
-  if (nsys <= fast_max) return ROUTE_FAST;
   if (nsys <= BLOCKED_MAX) return ROUTE_BLOCKED;
   return ROUTE_GENERIC;
 }
+
+// The no-pivot LU accepts a problem's factors only while every multiplier
+// satisfies |l_ij| ≤ NOPIV_LMAX, i.e. the diagonal passes the threshold test
+// |a_jj| ≥ τ·max_i |a_ij| with τ = 1/NOPIV_LMAX = 0.1 — UMFPACK's default
+// pivot tolerance (the reference's `LHS \ RHS`, QuadraticProgram.jl:490);
+// otherwise the problem is re-assembled and factorised with partial pivoting.
+constexpr double NOPIV_LMAX = 10.0;
 
 // QP problem inputs / forward tangents as seen by the kernels (device pointers)
 struct QPIn {
@@ -97,37 +107,21 @@ struct Handle {
   DevBuf csc_in[9], csc_in_val[3], csc_err;   // host-mode copies of CSC colptr / rowval / nzval
   int32_t nmax = 0, ld = 0;  // max system size, K row stride (doubles)
   DevBuf K, ipiv, s, kidx, meta, rhs, x;
-  DevBuf ws;                 // per-workgroup KKT workspace of the fused kernel
-  DevBuf dinv;               // per-problem diagonal-block inverses (split path)
+  DevBuf dinv;               // per-problem diagonal-block inverses (L11⁻¹ | U11⁻¹ per 32-block)
+  DevBuf plist;              // problem indices of the partial-pivoting re-factorisation
+  DevBuf lsqr_ws;            // LSQR vectors of the `iterative` branch (5 per problem)
+  DevBuf binv;               // no-pivot LU: packed 64×64 inverse of the current diagonal block
   DevBuf stamps;             // diagnostic in-kernel cycle stamps (env DOPT_STAMPS=1)
-  int32_t wg_per_cu = 2;     // persistent-grid occupancy of the fast kernels
-  // reduced sizes above this take the blocked path (env DOPT_FAST_MAX).  Default 0:
-  // the blocked step path is faster at every measured size and batch
-  // (tools/route_sweep.py, profiles/r01f_route_sweep.jsonl: 1.5–1.8× at batch
-  // 1024, ≥ parity at batch 128); the fused kernel stays as an opt-in route.
-  int32_t fast_max = 0;
-  // blocked LU: batch chunks stepped on concurrent streams (env DOPT_LU_STREAMS)
-  // panels per trailing update of the blocked LU (env DOPT_LU_GROUP): 0 = the
-  // pair scheme with the in-panel correction (default); 2–4 = left-looking
-  // panel groups with a separate U12 kernel and one rank-32g update, measured
-  // 5–11 % slower on configs 2/3 (r01f: the rank-128 tile update is latency-
-  // bound at 2 WGs/CU and the U12 strips re-read the group's U rows)
-  int32_t lu_group = 0;
-  // column tiles per rank-64 update workgroup (env DOPT_UPD_CT: 1, 2, 4); the
-  // prefetching strip kernel measured within ±2 % of one tile per WG (r01f)
-  int32_t upd_ct = 1;
-  int32_t lu_streams = 1;   // 2–4 measured no faster on configs 2 and 3 (r01f)
-  // solve2 workgroup order (env DOPT_SOLVE_ILV): 0 = all row sweeps then all
-  // column sweeps; 1 = the two directions of each group of 8 problems
-  // adjacent in dispatch order, on the same XCD, so the launch does not end
-  // with only column sweeps in flight (r01j: config-2 solve phase
-  // 0.458 → 0.413 ms, config 3 unchanged; HBM reads only 2 % lower)
-  int32_t solve_ilv = 1;
-  hipStream_t sub_stream[DOPT_MAX_LU_STREAMS] = {};
-  hipEvent_t join_ev[DOPT_MAX_LU_STREAMS] = {};
-  hipEvent_t fork_ev = nullptr;
+  QPMeta* meta_host = nullptr;     // pinned copy of `meta` (asynchronous read-back)
+  hipEvent_t meta_ev = nullptr;    // recorded after the read-back copy
+  // factorisation: 1 = no-pivot blocked LU with the threshold test and a
+  // partial-pivoting re-factorisation of rejected problems (default);
+  // 0 = partial pivoting for every problem (env DOPT_LU=0)
+  int32_t lu_mode = 1;
   int32_t blocked_npmax = 0;       // largest padded blocked system of the current factorisation
-  bool has_generic = true;         // some problem exceeds BLOCKED_MAX (set by the read-back)
+  bool has_generic = true;         // some problem exceeds BLOCKED_MAX
+  bool has_lsqr = true;            // some problem takes the LSQR branch
+  int32_t n_pivot = 0;             // problems factorised with partial pivoting (last factorisation)
   bool set = false, factored = false;
 
   // ---- CONIC ----
@@ -136,7 +130,7 @@ struct Handle {
   DevBuf own_cin[6];
   std::vector<int32_t> cones;   // (code, dim) pairs
   DevBuf cone_dev;              // device copy of cone table (+ offsets)
-  DevBuf vp, dpi, M, cwork, cinfo;
+  DevBuf vp, dpi, cwork, cinfo;
   DevBuf csplit;                // split-path LSQR vectors, partial products, state
   int32_t conic_split = -1;     // -1 auto, 0 persistent kernel, 1 split (env DOPT_CONIC_SPLIT)
   int32_t dpi_len = 0;          // doubles per problem of packed Dπ blocks
@@ -208,12 +202,18 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
                         const double* dq, const double* dG, const double* dh,
                         const double* dA, const double* db, double* out_rev,
                         double* out_fwd);
-// blocked step path (qp_blocked.hip) for ROUTE_BLOCKED problems, on the
-// per-problem K / perm (ipiv) / dinv buffers the assembly filled
-void qp_blocked_factor(Handle& h, double* dinv);
-void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rhs, double* x);
+// blocked path for ROUTE_BLOCKED problems, on the per-problem K / perm
+// (ipiv) / dinv buffers the assembly filled:
+//   qp_nopiv.hip    no-pivot blocked LU (64-column blocks, MFMA) + threshold test
+//   qp_blocked.hip  partial-pivoting blocked LU (the re-factorisation of the
+//                   rejected problems, `plist`; every problem when lu_mode = 0)
+//                   and the triangular solves shared by both
+void qp_nopiv_factor(Handle& h, double* dinv);
+void qp_blocked_factor(Handle& h, double* dinv, const int32_t* plist, int count);
+void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rhs, double* x, int sel);
 void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, const double* rhs_fwd,
-                       double* x_rev, double* x_fwd);
+                       double* x_rev, double* x_fwd, int sel);
+size_t dinv_stride(int nmax);
 void conic_factor(Handle& h);
 void conic_forward(Handle& h, const double* dA, const double* db, const double* dc,
                    double* out, double* out_dx);

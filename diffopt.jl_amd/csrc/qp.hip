@@ -1,21 +1,20 @@
-// QP sensitivity path: KKT assembly, batched blocked LU (FP64 MFMA trailing
-// update), forward/transposed triangular solves, dense batched LSQR for the
-// `norm(Q) == 0` branch, and output recovery.  gfx950 (CDNA4) only.
+// QP sensitivity path: host orchestration, the generic LU for reduced systems
+// above BLOCKED_MAX, the dense batched LSQR for the `norm(Q) == 0` branch,
+// right-hand sides and output recovery.  gfx950 (CDNA4) only.
 //
 // Reference: src/QuadraticProgram/QuadraticProgram.jl
 //   create_LHS_matrix :256-282   reverse_differentiate! :316-351
 //   forward_differentiate! :357-446   solve_system :486-496
 //
-// This file: the fallback kernels (generic LU for reduced systems > 512,
-// lazy-swap solves, dense LSQR for the iterative branch, their RHS/outputs)
-// and the host-side orchestration.  The fast path lives in qp_fast.hip.
+// Other files: qp_assemble.hip (prepare + assembly), qp_nopiv.hip (default
+// blocked LU), qp_blocked.hip (partial-pivoting blocked LU, solves).
 //
 // Layout in HBM (per problem b, fixed stride so every problem is independent):
 //   K     : nmax × ld doubles, ROW-major (row swaps are contiguous), ld = nmax = round_up(n+m+p, 32)
-//   ipiv  : nmax int32 (absolute row index chosen for each column)
+//   ipiv  : nmax int32 (blocked path: logical → physical row; generic: LAPACK ipiv)
 //   s     : m doubles  (G z − h, Julia sparse-matvec summation order)
 //   kidx  : m int32 (kept inequality rows, ascending)  rpos: m int32 (row → kk | -1)
-//   meta  : QPMeta {nk, nsys, iterative, info}
+//   meta  : QPMeta {nk, nsys, iterative, info, lu}
 #include "dopt_internal.h"
 
 namespace dopt {
@@ -43,10 +42,10 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 }
 
 // ---------------------------------------------------------------------------
-// 3. generic fallback LU (reduced systems larger than the fast path's 512):
+// 3. generic LU (reduced systems larger than BLOCKED_MAX):
 // unblocked right-looking on global memory, panel width 1, trailing-only
 // ("lazy") row swaps: K = P₁⁻¹M₁P₂⁻¹M₂…U, undone by qp_solve_kernel.
-// Problem data was assembled into the per-problem K buffer by qp_fast.hip.
+// Problem data was assembled into the per-problem K buffer by qp_assemble.hip.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(TPB) void qp_lu_generic_kernel(
     double* __restrict__ K, int32_t* __restrict__ ipiv, QPMeta* __restrict__ meta,
@@ -57,7 +56,7 @@ __global__ __launch_bounds__(TPB) void qp_lu_generic_kernel(
   const int lane = t & 63, wv = t >> 6;
   if (meta[b].iterative) return;
   const int N = meta[b].nsys;
-  if (N <= BLOCKED_MAX) return;   // fused / blocked paths own these
+  if (N <= BLOCKED_MAX) return;   // the blocked path owns these
   double* Kb = K + (size_t)b * nmax * ld;
   int32_t* piv = ipiv + (size_t)b * nmax;
   int info = 0;
@@ -125,7 +124,7 @@ __global__ __launch_bounds__(TPB) void qp_solve_kernel(
   const int lane = t & 63, wv = t >> 6;
   if (meta[b].iterative) return;
   const int N = meta[b].nsys;
-  if (N <= BLOCKED_MAX) return;   // fused / blocked paths own these
+  if (N <= BLOCKED_MAX) return;   // the blocked path owns these
   const int nb = 1;                // generic LU: panel width 1, lazy swaps
   const double* Kb = K + (size_t)b * nmax * ld;
   const int32_t* piv = ipiv + (size_t)b * nmax;
@@ -245,7 +244,9 @@ __global__ __launch_bounds__(TPB) void qp_solve_kernel(
 // ---------------------------------------------------------------------------
 // 5. dense batched LSQR for the `iterative` branch (QuadraticProgram.jl:488):
 // IterativeSolvers.lsqr(LHS or LHSᵀ, RHS) on the FULL (unreduced) KKT matrix,
-// restating oracle/lsqr.py operation for operation.  One workgroup/problem.
+// restating oracle/lsqr.py operation for operation.  One workgroup/problem;
+// the five N-vectors live in a per-problem global workspace (L2-resident), so
+// the launch has no size limit.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void dense_matvec(const double* __restrict__ Kb, int ld, int N, int trans,
                              const double* __restrict__ v, double* __restrict__ out) {
@@ -271,14 +272,13 @@ __device__ __forceinline__ void dense_matvec(const double* __restrict__ Kb, int 
 __global__ __launch_bounds__(TPB) void qp_lsqr_kernel(
     const double* __restrict__ K, const QPMeta* __restrict__ meta, int nmax,
     int ld, int trans, const double* __restrict__ rhs, double* __restrict__ xout,
-    int32_t* __restrict__ iters) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* __restrict__ work) {
   __shared__ double red[4];
   const int b = blockIdx.x, t = threadIdx.x;
   if (!meta[b].iterative) return;
   const int N = meta[b].nsys;
   const double* Kb = K + (size_t)b * nmax * ld;
-  double* x = smem;
+  double* x = work + (size_t)b * 5 * nmax;
   double* u = x + N;
   double* v = u + N;
   double* w = v + N;
@@ -374,7 +374,6 @@ __global__ __launch_bounds__(TPB) void qp_lsqr_kernel(
   }
   __syncthreads();
   for (int i = t; i < N; i += TPB) xout[(size_t)b * nmax + i] = x[i];
-  if (t == 0 && iters) iters[b] = it;
 }
 
 // ---------------------------------------------------------------------------
@@ -383,36 +382,38 @@ __global__ __launch_bounds__(TPB) void qp_lsqr_kernel(
 // reverse RHS: [dl_dz; 0] reduced (QuadraticProgram.jl:329)
 __global__ __launch_bounds__(TPB) void qp_rev_rhs_kernel(
     const double* __restrict__ dl_dz, const QPMeta* __restrict__ meta, int n,
-    int nmax, int fast_max, double* __restrict__ rhs) {
+    int nmax, double* __restrict__ rhs) {
   const int b = blockIdx.x, t = threadIdx.x;
   const int N = meta[b].nsys;
-  if (qp_route(meta[b].iterative, N, fast_max) == ROUTE_FAST) return;
   for (int i = t; i < N; i += TPB) rhs[(size_t)b * nmax + i] = (i < n) ? dl_dz[(size_t)b * n + i] : 0.0;
 }
 
 // forward RHS (QuadraticProgram.jl:429-433):
 //   [dQ z + dq + dGᵀλ + dAᵀν; λ.*(dG z) − λ.*dh; dA z − db]
-// full-length copy in `full` (n+m+p per problem, stride nmax) and reduced copy in rhs.
+// full-length copy in `full` (n+m+p per problem, stride nmax; the eliminated
+// rows' entries are read back by the output kernel) and reduced copy in rhs.
+// z is staged in LDS when it fits (`zcap` doubles), read from HBM otherwise.
 __global__ __launch_bounds__(TPB) void qp_fwd_rhs_kernel(
     const double* __restrict__ dQ, const double* __restrict__ dq,
     const double* __restrict__ dG, const double* __restrict__ dh,
     const double* __restrict__ dA, const double* __restrict__ db,
     const double* __restrict__ z, const double* __restrict__ lam,
     const double* __restrict__ nu, const int32_t* __restrict__ rpos,
-    const QPMeta* __restrict__ meta, int n, int m, int p, int nmax, int fast_max,
+    const QPMeta* __restrict__ meta, int n, int m, int p, int nmax, int zcap,
     double* __restrict__ full, double* __restrict__ rhs) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  if (qp_route(meta[b].iterative, meta[b].nsys, fast_max) == ROUTE_FAST) return;
-  double* zs = smem;            // n
-  double* ls = zs + n;          // m
-  double* ns = ls + m;          // p
-  double* r = ns + p;           // n + m + p
-  for (int i = t; i < n; i += TPB) zs[i] = z[(size_t)b * n + i];
-  for (int i = t; i < m; i += TPB) ls[i] = lam[(size_t)b * m + i];
-  for (int i = t; i < p; i += TPB) ns[i] = nu[(size_t)b * p + i];
+  const double* zg = z + (size_t)b * n;
+  const double* lb = lam + (size_t)b * m;
+  const double* nb = nu + (size_t)b * p;
+  const bool staged = n <= zcap;
+  if (staged)
+    for (int i = t; i < n; i += TPB) smem[i] = zg[i];
   __syncthreads();
-  // r1 = dQ z + dq
+  const double* zs = staged ? smem : zg;
+  double* r = full + (size_t)b * nmax;
+  // r1 = dQ z + dq + dGᵀλ + dAᵀν  (wave per entry for the transposed products,
+  // same summation order as before: the dQ·z sum, + dq, then + dGᵀλ, + dAᵀν)
   for (int i = t; i < n; i += TPB) {
     double acc = 0.0;
     if (dQ) {
@@ -423,12 +424,11 @@ __global__ __launch_bounds__(TPB) void qp_fwd_rhs_kernel(
     r[i] = acc;
   }
   __syncthreads();
-  // r1 += dGᵀλ ; r1 += dAᵀν  (wave per column, lanes over rows)
   if (dG && m > 0) {
     const double* Gb = dG + (size_t)b * m * n;
     for (int i = wv; i < n; i += 4) {
       double acc = 0.0;
-      for (int l = lane; l < m; l += 64) acc = fma(Gb[l + (size_t)i * m], ls[l], acc);
+      for (int l = lane; l < m; l += 64) acc = fma(Gb[l + (size_t)i * m], lb[l], acc);
       acc = wave_sum(acc);
       if (lane == 0) r[i] += acc;
     }
@@ -438,7 +438,7 @@ __global__ __launch_bounds__(TPB) void qp_fwd_rhs_kernel(
     const double* Ab = dA + (size_t)b * p * n;
     for (int i = wv; i < n; i += 4) {
       double acc = 0.0;
-      for (int l = lane; l < p; l += 64) acc = fma(Ab[l + (size_t)i * p], ns[l], acc);
+      for (int l = lane; l < p; l += 64) acc = fma(Ab[l + (size_t)i * p], nb[l], acc);
       acc = wave_sum(acc);
       if (lane == 0) r[i] += acc;
     }
@@ -451,7 +451,7 @@ __global__ __launch_bounds__(TPB) void qp_fwd_rhs_kernel(
       for (int j = 0; j < n; ++j) gz = fma(Gb[l + (size_t)j * m], zs[j], gz);
     }
     const double hh = dh ? dh[(size_t)b * m + l] : 0.0;
-    r[n + l] = ls[l] * gz - ls[l] * hh;
+    r[n + l] = lb[l] * gz - lb[l] * hh;
   }
   // r3 = dA z − db
   for (int e = t; e < p; e += TPB) {
@@ -462,11 +462,9 @@ __global__ __launch_bounds__(TPB) void qp_fwd_rhs_kernel(
     }
     r[n + m + e] = az - (db ? db[(size_t)b * p + e] : 0.0);
   }
-  __syncthreads();
+  __syncthreads();   // r (global) complete within the workgroup
   const int nk = meta[b].nk;
-  double* fb = full + (size_t)b * nmax;
   double* rb = rhs + (size_t)b * nmax;
-  for (int i = t; i < n + m + p; i += TPB) fb[i] = r[i];
   for (int i = t; i < n; i += TPB) rb[i] = r[i];
   for (int l = t; l < m; l += TPB) {
     const int kk = rpos[(size_t)b * m + l];
@@ -483,15 +481,18 @@ __global__ __launch_bounds__(TPB) void qp_output_kernel(
     const double* __restrict__ x, const double* __restrict__ G,
     const double* __restrict__ s, const int32_t* __restrict__ rpos,
     const QPMeta* __restrict__ meta, const double* __restrict__ full, int n,
-    int m, int p, int nmax, int fast_max, int trans, double* __restrict__ out) {
+    int m, int p, int nmax, int zcap, int trans, double* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x, t = threadIdx.x;
-  if (qp_route(meta[b].iterative, meta[b].nsys, fast_max) == ROUTE_FAST) return;
   const int nk = meta[b].nk;
   const double* xb = x + (size_t)b * nmax;
   double* ob = out + (size_t)b * (n + m + p);
-  double* xz = smem;
-  for (int i = t; i < n; i += TPB) { xz[i] = xb[i]; ob[i] = -xb[i]; }
+  const bool staged = n <= zcap;
+  const double* xz = staged ? smem : xb;
+  for (int i = t; i < n; i += TPB) {
+    if (staged) smem[i] = xb[i];
+    ob[i] = -xb[i];
+  }
   for (int e = t; e < p; e += TPB) ob[n + m + e] = -xb[n + nk + e];
   __syncthreads();
   const double* Gb = G + (size_t)b * m * n;
@@ -626,24 +627,16 @@ void csc_to_dense(Handle& h, const int64_t* colptr, const int64_t* rowval, const
 // ---------------------------------------------------------------------------
 static void check_launch() { DOPT_CHECK_HIP(hipGetLastError()); }
 
-// fast path (qp_fast.hip)
-__global__ void qp_fused_kernel(QPIn, FwdTangents, const double*, int, double*, size_t, double*, int,
-                                int, double*, int32_t*, int32_t*, QPMeta*, double*, double*,
-                                double*, int, int, unsigned long long*, int);
-__global__ void qp_factor_fast_kernel(QPIn, int, double*, int, int, double*, int32_t*, int32_t*,
-                                      int32_t*, double*, QPMeta*, int);
-__global__ void qp_solve_fast_kernel(QPIn, FwdTangents, const double*, int, const double*, int, int,
-                                     const double*, const int32_t*, const int32_t*, const double*,
-                                     const QPMeta*, double*, int, double*, int);
-__global__ void qp_prep_asm_kernel(QPIn, double*, int, int, double*, int32_t*, int32_t*, QPMeta*, int);
+// qp_assemble.hip
+__global__ void qp_prep_asm_kernel(QPIn, double*, int, int, double*, int32_t*, int32_t*, QPMeta*, int,
+                                   const int32_t*);
 int prep_asm_cap(int n, int m);
 size_t prep_asm_lds(int n, int cap);
-size_t fast_dyn_lds(int n);
-size_t fast_ws_stride();
-size_t fast_dinv_stride(int nmax);
+
+constexpr int ZCAP = 4096;   // z staged in LDS by the RHS / output kernels up to this n
 
 static double* dinv_of(Handle& h) {
-  h.dinv.ensure((size_t)h.batch * fast_dinv_stride(h.nmax) * sizeof(double));
+  h.dinv.ensure((size_t)h.batch * dinv_stride(h.nmax) * sizeof(double));
   return h.dinv.as<double>();
 }
 
@@ -663,51 +656,128 @@ static QPIn qp_inputs(Handle& h) {
   return P;
 }
 
-static int fast_grid(Handle& h) {
-  int cus = 256;
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h.device);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(h.batch, (int64_t)cus * h.wg_per_cu));
+static int32_t* rpos_of(Handle& h) { return h.kidx.as<int32_t>() + (size_t)h.batch * h.m; }
+
+// prepare + assembly of `count` problems (plist: their indices; null = all)
+static void prep_assemble(Handle& h, const int32_t* plist, int count) {
+  if (count == 0) return;
+  const int cap = prep_asm_cap(h.n, h.m);
+  hipLaunchKernelGGL(qp_prep_asm_kernel, dim3(count), dim3(ASM_THREADS), prep_asm_lds(h.n, cap), h.stream,
+                     qp_inputs(h), h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(), h.kidx.as<int32_t>(),
+                     rpos_of(h), h.meta.as<QPMeta>(), cap, plist);
+  check_launch();
 }
 
-static int32_t* rpos_of(Handle& h) { return h.kidx.as<int32_t>() + (size_t)h.batch * h.m; }
-static int32_t* perm_of(Handle& h) { return h.ipiv.as<int32_t>(); }
+// Asynchronous read-back of the per-problem metadata into pinned memory; the
+// caller may queue independent kernels before waiting (meta_wait), so the
+// host turnaround overlaps them.
+static void meta_copy(Handle& h) {
+  if (!h.meta_host) {
+    DOPT_CHECK_HIP(hipHostMalloc((void**)&h.meta_host, std::max<size_t>(h.batch, 1) * sizeof(QPMeta)));
+    DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.meta_ev, hipEventDisableTiming));
+  }
+  DOPT_CHECK_HIP(hipMemcpyAsync(h.meta_host, h.meta.p, h.batch * sizeof(QPMeta), hipMemcpyDeviceToHost,
+                                h.stream));
+  DOPT_CHECK_HIP(hipEventRecord(h.meta_ev, h.stream));
+}
 
-// fast_max == 0: no problem takes the fused route, so prepare + assembly run in
-// the standalone high-occupancy kernel (one workgroup per problem)
-static void prep_assemble(Handle& h) {
-  const int cap = prep_asm_cap(h.n, h.m);
-  hipLaunchKernelGGL(qp_prep_asm_kernel, dim3(h.batch), dim3(FAST_THREADS), prep_asm_lds(h.n, cap),
-                     h.stream, qp_inputs(h), h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(),
-                     h.kidx.as<int32_t>(), rpos_of(h), h.meta.as<QPMeta>(), cap);
+// After the assembly: largest padded blocked system (sizes the blocked
+// launches), whether any problem needs the generic or the LSQR kernels.
+static void meta_sizes(Handle& h) {
+  DOPT_CHECK_HIP(hipEventSynchronize(h.meta_ev));
+  int npmax = 0;
+  h.has_generic = h.has_lsqr = false;
+  for (int64_t b = 0; b < h.batch; ++b) {
+    const QPMeta& mm = h.meta_host[b];
+    const int r = qp_route(mm.iterative, mm.nsys);
+    if (r == ROUTE_BLOCKED) npmax = std::max(npmax, (mm.nsys + 31) & ~31);
+    h.has_generic |= r == ROUTE_GENERIC;
+    h.has_lsqr |= r == ROUTE_LSQR;
+  }
+  h.blocked_npmax = npmax;
+}
+
+// After the no-pivot LU: the problems it rejected, re-assembled and
+// factorised with partial pivoting.  Returns their count.
+static int pivot_fallback(Handle& h) {
+  DOPT_CHECK_HIP(hipEventSynchronize(h.meta_ev));
+  std::vector<int32_t> list;
+  for (int64_t b = 0; b < h.batch; ++b)
+    if (h.meta_host[b].lu == LU_REJECT) list.push_back((int32_t)b);
+  const int count = (int)list.size();
+  if (count) {
+    h.plist.ensure(list.size() * sizeof(int32_t));
+    DOPT_CHECK_HIP(hipMemcpyAsync(h.plist.p, list.data(), list.size() * sizeof(int32_t),
+                                  hipMemcpyHostToDevice, h.stream));
+    const int32_t* pl = h.plist.as<int32_t>();
+    prep_assemble(h, pl, count);
+    qp_blocked_factor(h, dinv_of(h), pl, count);
+    // the host copy of `list` must outlive the asynchronous upload
+    DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+  }
+  return count;
+}
+
+static void generic_lu(Handle& h) {
+  if (!(h.nmax > BLOCKED_MAX && h.has_generic)) return;
+  hipLaunchKernelGGL(qp_lu_generic_kernel, dim3(h.batch), dim3(TPB), 0, h.stream, h.K.as<double>(),
+                     h.ipiv.as<int32_t>(), h.meta.as<QPMeta>(), h.nmax, h.ld);
   check_launch();
+}
+
+// Factorisation of the assembled batch (prepare + assembly already queued and
+// the metadata read back).  Blocked problems: the no-pivot LU, then partial
+// pivoting for the problems it rejects (lu_mode 1), or partial pivoting for
+// all (lu_mode 0).  `spec` (optional) is queued right after the no-pivot LU,
+// before the host waits for the rejected list: work that skips rejected
+// problems (the solves of the fused call).
+template <class F>
+static void factor_blocked(Handle& h, F&& spec) {
+  if (h.lu_mode == 1) {
+    {
+      PhaseTimer pt(h, DOPT_PHASE_QP_LU);
+      qp_nopiv_factor(h, dinv_of(h));
+    }
+    if (h.blocked_npmax) meta_copy(h);
+    spec();
+    h.n_pivot = 0;
+    if (h.blocked_npmax) {
+      DOPT_CHECK_HIP(hipEventSynchronize(h.meta_ev));
+      bool any = false;
+      for (int64_t b = 0; b < h.batch && !any; ++b) any = h.meta_host[b].lu == LU_REJECT;
+      if (any) {
+        PhaseTimer pt(h, DOPT_PHASE_QP_LU_PIVOT);
+        h.n_pivot = pivot_fallback(h);
+      }
+    }
+  } else {
+    {
+      PhaseTimer pt(h, DOPT_PHASE_QP_LU_PIVOT);
+      qp_blocked_factor(h, dinv_of(h), nullptr, (int)h.batch);
+    }
+    spec();
+    h.n_pivot = -1;
+  }
+  if (h.nmax > BLOCKED_MAX && h.has_generic) {
+    PhaseTimer pt(h, DOPT_PHASE_QP_LU);
+    generic_lu(h);
+  }
 }
 
 void qp_factor(Handle& h) {
   if (!h.set) throw Error(-1, "dopt_qp_factor: dopt_qp_set has not been called");
-  const int B = (int)h.batch;
-  QPMeta* meta = h.meta.as<QPMeta>();
   {
-    PhaseTimer pt(h, DOPT_PHASE_QP_LU);
-    if (h.fast_max == 0) {
-      prep_assemble(h);
-    } else {
-      hipLaunchKernelGGL(qp_factor_fast_kernel, dim3(fast_grid(h)), dim3(FAST_THREADS), fast_dyn_lds(h.n),
-                         h.stream, qp_inputs(h), B, h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(),
-                         h.kidx.as<int32_t>(), rpos_of(h), perm_of(h), dinv_of(h), meta, h.fast_max);
-      check_launch();
-    }
-    if (h.nmax > h.fast_max) qp_blocked_factor(h, dinv_of(h));
-    if (h.nmax > BLOCKED_MAX && h.has_generic) {
-      hipLaunchKernelGGL(qp_lu_generic_kernel, dim3(B), dim3(TPB), 0, h.stream, h.K.as<double>(),
-                         h.ipiv.as<int32_t>(), meta, h.nmax, h.ld);
-      check_launch();
-    }
+    PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
+    prep_assemble(h, nullptr, (int)h.batch);
+    meta_copy(h);
   }
+  meta_sizes(h);
+  factor_blocked(h, [] {});
   h.factored = true;
 }
 
-// Per-direction work buffers of the non-fused problems (trans 0 = reverse,
-// 1 = forward): reduced RHS, solution, and the full-length forward RHS.
+// Per-direction work buffers (trans 0 = reverse, 1 = forward): reduced RHS,
+// solution, and the full-length forward RHS.
 static double* rhs_of(Handle& h, int trans) {
   return h.rhs.as<double>() + (size_t)(trans ? 2 : 0) * h.batch * h.nmax;
 }
@@ -716,9 +786,9 @@ static double* x_of(Handle& h, int trans) {
   return h.x.as<double>() + (size_t)(trans ? 1 : 0) * h.batch * h.nmax;
 }
 
-// generic solves, LSQR and output recovery of the non-fused problems for one
-// direction (the blocked solves are launched by the callers)
-static void fallback_finish(Handle& h, int trans, double* out) {
+// generic solves, LSQR and output recovery for one direction (the blocked
+// solves are launched by the callers)
+static void finish(Handle& h, int trans, double* out) {
   const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
   const int nmax = h.nmax, ld = h.ld;
   QPMeta* meta = h.meta.as<QPMeta>();
@@ -726,46 +796,42 @@ static void fallback_finish(Handle& h, int trans, double* out) {
   double* x = x_of(h, trans);
   if (nmax > BLOCKED_MAX && h.has_generic) {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
+    if ((size_t)nmax * sizeof(double) > 64 * 1024) throw Error(-1, "generic solve: system too large");
     hipLaunchKernelGGL(qp_solve_kernel, dim3(B), dim3(TPB), (size_t)nmax * sizeof(double), h.stream,
                        h.K.as<double>(), h.ipiv.as<int32_t>(), meta, nmax, ld, trans, rhs, x);
     check_launch();
   }
-  {
+  if (h.has_lsqr) {
     PhaseTimer pt(h, DOPT_PHASE_QP_LSQR);
-    hipLaunchKernelGGL(qp_lsqr_kernel, dim3(B), dim3(TPB), (size_t)5 * nmax * sizeof(double), h.stream,
-                       h.K.as<double>(), meta, nmax, ld, trans, rhs, x, (int32_t*)nullptr);
+    h.lsqr_ws.ensure((size_t)B * 5 * nmax * sizeof(double));
+    hipLaunchKernelGGL(qp_lsqr_kernel, dim3(B), dim3(TPB), 0, h.stream, h.K.as<double>(), meta, nmax, ld,
+                       trans, rhs, x, h.lsqr_ws.as<double>());
     check_launch();
   }
   static const double dummy = 0.0;
   PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
-  hipLaunchKernelGGL(qp_output_kernel, dim3(B), dim3(TPB), (size_t)n * sizeof(double), h.stream,
-                     x, m ? h.G : &dummy, h.s.as<double>(), rpos_of(h), meta, full_of(h), n, m, p,
-                     nmax, h.fast_max, trans, out);
+  hipLaunchKernelGGL(qp_output_kernel, dim3(B), dim3(TPB), (size_t)std::min(n, ZCAP) * sizeof(double),
+                     h.stream, x, m ? h.G : &dummy, h.s.as<double>(), rpos_of(h), meta, full_of(h), n, m, p,
+                     nmax, ZCAP, trans, out);
   check_launch();
 }
 
-static void fallback_rev_rhs(Handle& h, const double* dl_dz) {
+static void rev_rhs(Handle& h, const double* dl_dz) {
   PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
-  hipLaunchKernelGGL(qp_rev_rhs_kernel, dim3(h.batch), dim3(TPB), 0, h.stream, dl_dz,
-                     h.meta.as<QPMeta>(), h.n, h.nmax, h.fast_max, rhs_of(h, 0));
+  hipLaunchKernelGGL(qp_rev_rhs_kernel, dim3(h.batch), dim3(TPB), 0, h.stream, dl_dz, h.meta.as<QPMeta>(),
+                     h.n, h.nmax, rhs_of(h, 0));
   check_launch();
 }
 
-static void fallback_fwd_rhs(Handle& h, const FwdTangents& T) {
+static void fwd_rhs(Handle& h, const FwdTangents& T) {
   const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
   static const double dummy = 0.0;
   PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
-  hipLaunchKernelGGL(qp_fwd_rhs_kernel, dim3(B), dim3(TPB), (size_t)(2 * n + 2 * m + 2 * p) * sizeof(double),
+  hipLaunchKernelGGL(qp_fwd_rhs_kernel, dim3(B), dim3(TPB), (size_t)std::min(n, ZCAP) * sizeof(double),
                      h.stream, T.dQ, T.dq, T.dG, T.dh, T.dA, T.db, h.z, m ? h.lam : &dummy,
-                     p ? h.nu : &dummy, rpos_of(h), h.meta.as<QPMeta>(), n, m, p, h.nmax, h.fast_max,
-                     full_of(h), rhs_of(h, 1));
+                     p ? h.nu : &dummy, rpos_of(h), h.meta.as<QPMeta>(), n, m, p, h.nmax, ZCAP, full_of(h),
+                     rhs_of(h, 1));
   check_launch();
-}
-
-static void blocked_solve(Handle& h, int trans) {
-  if (h.nmax <= h.fast_max) return;
-  PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
-  qp_blocked_solve(h, dinv_of(h), trans, rhs_of(h, trans), x_of(h, trans));
 }
 
 static FwdTangents tangents(Handle& h, const double* dQ, const double* dq, const double* dG,
@@ -782,38 +848,23 @@ static FwdTangents tangents(Handle& h, const double* dQ, const double* dq, const
 
 void qp_reverse(Handle& h, const double* dl_dz, double* out) {
   if (!h.factored) qp_factor(h);
-  const int B = (int)h.batch;
-  double* full = full_of(h);
+  rev_rhs(h, dl_dz);
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
-    hipLaunchKernelGGL(qp_solve_fast_kernel, dim3(fast_grid(h)), dim3(FAST_THREADS), 0, h.stream, qp_inputs(h),
-                       tangents(h, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr), dl_dz, B,
-                       h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(), rpos_of(h), perm_of(h),
-                       dinv_of(h), h.meta.as<QPMeta>(), full, 0, out, h.fast_max);
-    check_launch();
+    qp_blocked_solve(h, dinv_of(h), 0, rhs_of(h, 0), x_of(h, 0), LU_SEL_ALL);
   }
-  fallback_rev_rhs(h, dl_dz);
-  blocked_solve(h, 0);
-  fallback_finish(h, 0, out);
+  finish(h, 0, out);
 }
 
 void qp_forward(Handle& h, const double* dQ, const double* dq, const double* dG,
                 const double* dh, const double* dA, const double* db, double* out) {
   if (!h.factored) qp_factor(h);
-  const int B = (int)h.batch;
-  double* full = full_of(h);
-  const FwdTangents T = tangents(h, dQ, dq, dG, dh, dA, db);
+  fwd_rhs(h, tangents(h, dQ, dq, dG, dh, dA, db));
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
-    hipLaunchKernelGGL(qp_solve_fast_kernel, dim3(fast_grid(h)), dim3(FAST_THREADS), 0, h.stream, qp_inputs(h),
-                       T, (const double*)nullptr, B, h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(),
-                       rpos_of(h), perm_of(h), dinv_of(h), h.meta.as<QPMeta>(), full, 1, out,
-                       h.fast_max);
-    check_launch();
+    qp_blocked_solve(h, dinv_of(h), 1, rhs_of(h, 1), x_of(h, 1), LU_SEL_ALL);
   }
-  fallback_fwd_rhs(h, T);
-  blocked_solve(h, 1);
-  fallback_finish(h, 1, out);
+  finish(h, 1, out);
 }
 
 void qp_reverse_grads(Handle& h, const double* rev, double* dQ, double* dq, double* dG, double* gc,
@@ -829,47 +880,34 @@ void qp_reverse_grads(Handle& h, const double* rev, double* dQ, double* dq, doub
   check_launch();
 }
 
+// One full sensitivity solve per problem (the batched throughput path):
+// prepare + assembly, both right-hand sides (queued while the host reads the
+// metadata back), the factorisation, both solves in one launch (queued while
+// the host checks for rejected problems), the partial-pivoting re-solve of
+// those, LSQR / generic problems, outputs.
 void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
                         const double* dq, const double* dG, const double* dh,
                         const double* dA, const double* db, double* out_rev,
                         double* out_fwd) {
-  const int B = (int)h.batch;
-  const int grid = fast_grid(h);
-  const size_t ws_stride = fast_ws_stride();
-  double* full = full_of(h);
+  if (!h.set) throw Error(-1, "dopt_qp_forward_reverse: dopt_qp_set has not been called");
   const FwdTangents T = tangents(h, dQ, dq, dG, dh, dA, db);
-  if (h.fast_max == 0) {
+  {
     PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
-    prep_assemble(h);
-  } else {
-    h.ws.ensure((size_t)grid * ws_stride * sizeof(double));
-    PhaseTimer pt(h, DOPT_PHASE_QP_FUSED);
-    hipLaunchKernelGGL(qp_fused_kernel, dim3(grid), dim3(FAST_THREADS), fast_dyn_lds(h.n), h.stream,
-                       qp_inputs(h), T, dl_dz, B, h.ws.as<double>(), ws_stride, h.K.as<double>(), h.ld,
-                       h.nmax, h.s.as<double>(), h.kidx.as<int32_t>(), rpos_of(h), h.meta.as<QPMeta>(),
-                       full, out_rev, out_fwd, 1, 1, h.stamps.as<unsigned long long>(), h.fast_max);
-    check_launch();
+    prep_assemble(h, nullptr, (int)h.batch);
+    meta_copy(h);
   }
-  // fallback problems were prepared + assembled by the fused kernel
-  if (h.nmax > h.fast_max) {
-    PhaseTimer pt(h, DOPT_PHASE_QP_LU);
-    qp_blocked_factor(h, dinv_of(h));
-  }
-  if (h.nmax > BLOCKED_MAX && h.has_generic) {
-    PhaseTimer pt(h, DOPT_PHASE_QP_LU);
-    hipLaunchKernelGGL(qp_lu_generic_kernel, dim3(B), dim3(TPB), 0, h.stream, h.K.as<double>(),
-                       h.ipiv.as<int32_t>(), h.meta.as<QPMeta>(), h.nmax, h.ld);
-    check_launch();
-  }
-  fallback_rev_rhs(h, dl_dz);
-  fallback_fwd_rhs(h, T);
-  if (h.nmax > h.fast_max) {   // both directions of the blocked problems in one pass
+  rev_rhs(h, dl_dz);
+  fwd_rhs(h, T);
+  meta_sizes(h);
+  auto solve2 = [&](int sel) {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
-    qp_blocked_solve2(h, dinv_of(h), rhs_of(h, 0), rhs_of(h, 1), x_of(h, 0), x_of(h, 1));
-  }
-  fallback_finish(h, 0, out_rev);
-  fallback_finish(h, 1, out_fwd);
-  h.factored = false;   // the fused path leaves no reusable factorisation
+    qp_blocked_solve2(h, dinv_of(h), rhs_of(h, 0), rhs_of(h, 1), x_of(h, 0), x_of(h, 1), sel);
+  };
+  factor_blocked(h, [&] { solve2(h.lu_mode == 1 ? LU_SEL_NOPIV : LU_SEL_ALL); });
+  if (h.n_pivot > 0) solve2(LU_SEL_PIVOT);
+  finish(h, 0, out_rev);
+  finish(h, 1, out_fwd);
+  h.factored = true;   // the factors stay valid for later reverse / forward calls
 }
 
 }  // namespace dopt

@@ -1,8 +1,9 @@
-// Blocked step path — the default route for reduced KKT systems N ≤ BLOCKED_MAX
-// (config 2: N' = 290, config 3: N' ≈ 1450): the batched LU is a sequence of
-// launches per 32-column panel, each covering EVERY problem of the batch, so
-// the O(N³) trailing update is spread over all 256 CUs instead of one
-// workgroup per problem.
+// Blocked path, part 2: the partial-pivoting blocked LU and the triangular
+// solves.  The default factorisation is the no-pivot blocked LU of
+// qp_nopiv.hip; the kernels here re-factorise the problems it rejects (the
+// threshold test), or every problem when lu_mode = 0 (env DOPT_LU=0).  Each
+// launch covers a list of problems (`plist`), one 32-column panel step at a
+// time, so the O(N³) trailing update is spread over all 256 CUs:
 //
 //   panel   (1 WG / problem)        partial-pivot LU of the R × 32 panel held in
 //                                   registers (RPT rows per thread), pivoting by
@@ -11,13 +12,14 @@
 //   update  (WG per 64×64 tile)     A22 −= L21 · U12 (MFMA; U12 tile staged in
 //                                   LDS), XCD-aware tile order so one problem's
 //                                   tiles share an L2
-//   solve   (1 WG / problem)        the block-inverse GEMV sweeps of qp_fast.hip
-//                                   for K x = b and Kᵀ x = b, several entries per
-//                                   thread
+//   solve   (1 WG / problem)        block-inverse GEMV sweeps for K x = b and
+//                                   Kᵀ x = b with the stored diagonal-block
+//                                   inverses; both factor kinds (the no-pivot
+//                                   factors carry perm = identity)
 //
-// Same factor format as the fused path (row-major K whose physical rows never
-// move, logical→physical `perm`, diagonal-block inverses), so the LAPACK getf2
-// pivot rule (first max |a| in the current logical order) is shared.
+// Factor format: row-major K whose physical rows never move, logical→physical
+// `perm`, diagonal-block inverses; pivot rule of LAPACK getf2 (first max |a| in
+// the current logical order).
 //
 // Reference: QuadraticProgram.jl create_LHS_matrix :256-282 and the `LHS \ RHS`
 // of solve_system :486-496 (reverse :316-351, forward :357-446).
@@ -40,23 +42,6 @@ constexpr int PT = DOPT_SOLVE_PT;        // solve workgroup size (tuning builds:
 __device__ __forceinline__ d4b bmfma(double a, double b, d4b c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
-
-// diagnostic phase stamps (thread 0, s_memtime), accumulated per slot when
-// `stamps` is non-null (env DOPT_STAMPS=1, read with dopt_debug_stamps)
-struct BStamp {
-  unsigned long long* acc;
-  unsigned long long last;
-  __device__ __forceinline__ void start() {
-    if (acc && threadIdx.x == 0) last = __builtin_amdgcn_s_memtime();
-  }
-  __device__ __forceinline__ void mark(int k) {
-    if (acc && threadIdx.x == 0) {
-      const unsigned long long now = __builtin_amdgcn_s_memtime();
-      atomicAdd(&acc[k], now - last);
-      last = now;
-    }
-  }
-};
 
 // wave max of a double (DPP butterfly within rows, row_bcast across rows,
 // result broadcast from lane 63)
@@ -85,41 +70,36 @@ __device__ __forceinline__ int wave_min_i32(int v) {
   return v;
 }
 
-__device__ __forceinline__ int blocked_np(const QPMeta& mm, int fast_max) {
-  if (qp_route(mm.iterative, mm.nsys, fast_max) != ROUTE_BLOCKED) return 0;
+__device__ __forceinline__ int blocked_np(const QPMeta& mm) {
+  if (qp_route(mm.iterative, mm.nsys) != ROUTE_BLOCKED) return 0;
   return (mm.nsys + BNB - 1) & ~(BNB - 1);
 }
 
 // ---------------------------------------------------------------------------
 // Panel: logical rows c0 .. Np−1, columns c0 .. c0+31.  Thread t owns local
 // rows t + TPB·q (q < RPT) in a rotating register window (r[q][c] holds panel
-// column (j + c) mod 32 at column step j), exactly the scheme of qp_fast.hip's
-// lu_fast, generalised to several rows per thread.  Two barriers per column.
+// column (j + c) mod 32 at column step j).  One barrier per column.
 // ---------------------------------------------------------------------------
 template <int TPB, int RPT>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void blu_panel_kernel(double* __restrict__ K, int ld, int nmax,
                                                        int32_t* __restrict__ perm,
                                                        double* __restrict__ dinv, size_t dstride,
                                                        QPMeta* __restrict__ meta, int c0,
-                                                       int fast_max, int corr,
-                                                       unsigned long long* __restrict__ stamps, int b0) {
+                                                       int corr, const int32_t* __restrict__ plist) {
   constexpr int TW = TPB / 64;   // waves
   __shared__ double slot_val[2][TW];
   __shared__ int slot_pos[2][TW];
   __shared__ __attribute__((aligned(16))) double slot_row[2][TW][BNB];
   __shared__ double Lt[BNB * BLP], Linv[BNB * BLP], Uinv[BNB * BLP];
   __shared__ int ptop[BNB];
-  const int b = b0 + (int)blockIdx.x;
+  const int b = plist ? plist[blockIdx.x] : (int)blockIdx.x;
   const QPMeta mm = meta[b];
-  const int Np = blocked_np(mm, fast_max);
+  const int Np = blocked_np(mm);
   if (c0 >= Np) return;   // not a blocked problem, or already factored
   const int R = Np - c0;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   double* Kb = K + (size_t)b * nmax * ld;
   int32_t* pb = perm + (size_t)b * nmax;
-  BStamp st;
-  st.acc = stamps;
-  st.start();
 
   int phys[RPT], pos[RPT];
   double r[RPT][BNB];
@@ -140,10 +120,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void b
     }
   }
   int info = 0;
-  if (stamps) {
-    __syncthreads();   // diagnostic: attribute the panel load to slot 0
-    st.mark(0);
-  }
   // One barrier per column: every wave publishes its best candidate (|a| as a
   // double, logical position, and the candidate's rotated row) to a
   // double-buffered slot; after the barrier every thread folds the TW slots
@@ -240,7 +216,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void b
     for (int q = 0; q < RPT; ++q) r[q][BNB - 1] = r0[q];
   }
   __syncthreads();   // every thread has read its perm entries
-  st.mark(1);
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
     if (pos[q] >= 0) {
@@ -256,7 +231,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void b
     }
   }
   __syncthreads();
-  st.mark(2);
   // U12 = L11⁻¹·A12 over 16-column tiles of the trailing columns, wave-strided;
   // the first tile's A12 strip is loaded before the inverses so its latency
   // overlaps them.  Each wave overwrites only the strip it read.
@@ -266,7 +240,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void b
 #pragma unroll
   for (int s = 0; s < BNB / 4; ++s) ro[s] = (size_t)ptop[4 * s + g] * ld;
   double bv[BNB / 4];
-  if (corr >= 0 && wv < ntile) {
+  if (wv < ntile) {
 #pragma unroll
     for (int s = 0; s < BNB / 4; ++s) bv[s] = Kb[ro[s] + c0 + BNB + 16 * wv + l16];
   }
@@ -299,15 +273,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void b
     for (int jj = 0; jj < BNB; ++jj) Uinv[jj * BLP + c] = x[jj];
   }
   __syncthreads();
-  st.mark(3);
   double* Db = dinv + (size_t)b * dstride + (size_t)(c0 / BNB) * BDINV;
   for (int i = t; i < BDINV; i += TPB) {
     const int e = i & (BNB * BNB - 1);
     Db[i] = ((i < BNB * BNB) ? Linv : Uinv)[(e >> 5) * BLP + (e & 31)];
   }
-  if (t == 0 && info != 0 && mm.info == 0) meta[b].info = info;
-  st.mark(4);
-  if (corr < 0 || wv >= ntile) return;   // corr < 0: U12 left to blu_u12_kernel
+  if (t == 0) {
+    if (info != 0 && mm.info == 0) meta[b].info = info;
+    if (c0 == 0) meta[b].lu = LU_PIVOT;
+  }
+  if (wv >= ntile) return;
   double a0[BNB / 4], a1[BNB / 4];
 #pragma unroll
   for (int s = 0; s < BNB / 4; ++s) {
@@ -373,10 +348,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void b
       Kb[(size_t)rw2[rr] * ld + colL] = u1[rr];
     }
   }
-  if (stamps) {
-    __builtin_amdgcn_s_waitcnt(0);
-    st.mark(5);
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -385,9 +356,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void b
 // columns from c0+KW, columns limited to `cols_max` (the narrow update of the
 // pair's second panel uses 32).  64×64 tiles: wave w owns tile rows
 // 16w..16w+15 × 64 columns (4 MFMA tiles); the KW×64 U tile is staged once in
-// LDS.  1-D grid of nrt·nct·B tiles with an XCD-aware remap: logical tiles of
-// one problem are consecutive, so they run on one XCD and share its L2 for
-// the L and U operands.
+// LDS.  1-D grid of nrt·nct·count tiles (count problems of `plist`) with an
+// XCD-aware remap: logical tiles of one problem are consecutive, so they run
+// on one XCD and share its L2 for the L and U operands.
 // ---------------------------------------------------------------------------
 constexpr int ULD = 64 + 16;   // LDS row stride (doubles) of the staged U tile
 
@@ -395,8 +366,8 @@ template <int KW>
 __global__ __launch_bounds__(256) void blu_update_kernel(double* __restrict__ K, int ld, int nmax,
                                                          const int32_t* __restrict__ perm,
                                                          const QPMeta* __restrict__ meta, int c0,
-                                                         int fast_max, int cols_max, int nrt,
-                                                         int nct, int total, int b0) {
+                                                         int cols_max, int nrt, int nct, int total,
+                                                         const int32_t* __restrict__ plist) {
   __shared__ double U[KW * ULD];
   // bijective XCD remap (blocks L and L+8 share an XCD)
   const int L = blockIdx.x;
@@ -405,9 +376,9 @@ __global__ __launch_bounds__(256) void blu_update_kernel(double* __restrict__ K,
   const int tiles = nrt * nct;
   const int bl = logical / tiles;
   const int tile = logical - bl * tiles;
-  const int b = b0 + bl;
+  const int b = plist ? plist[bl] : bl;
   const int rt = tile / nct, ct = tile - rt * nct;
-  const int Np = blocked_np(meta[b], fast_max);
+  const int Np = blocked_np(meta[b]);
   const int R2 = Np - c0 - KW;          // trailing rows (multiple of 32, may be ≤ 0)
   const int C2 = min(R2, cols_max);     // trailing columns updated by this launch
   if (rt * 64 >= R2 || ct * 64 >= C2) return;   // workgroup-uniform
@@ -466,194 +437,8 @@ __global__ __launch_bounds__(256) void blu_update_kernel(double* __restrict__ K,
   }
 }
 
-// Strip variant of the trailing update: one workgroup owns 64 rows × CT
-// column tiles.  The L operand (64 × KW) is loaded once per strip instead of
-// once per tile, and the next tile's C block and U rows are loaded into
-// registers while the current tile's MFMAs run (U re-staged through LDS
-// between two barriers).  Same arithmetic order per element as
-// blu_update_kernel, hence bit-identical factors.
-template <int KW, int CT>
-__global__ __launch_bounds__(256) void blu_update_strip_kernel(double* __restrict__ K, int ld, int nmax,
-                                                               const int32_t* __restrict__ perm,
-                                                               const QPMeta* __restrict__ meta, int c0,
-                                                               int fast_max, int cols_max, int nrt,
-                                                               int ncs, int total, int b0) {
-  __shared__ double U[KW * ULD];
-  const int L = blockIdx.x;
-  const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
-  const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
-  const int tiles = nrt * ncs;
-  const int bl = logical / tiles;
-  const int tile = logical - bl * tiles;
-  const int b = b0 + bl;
-  const int rt = tile / ncs, cs = tile - rt * ncs;
-  const int Np = blocked_np(meta[b], fast_max);
-  const int R2 = Np - c0 - KW;
-  const int C2 = min(R2, cols_max);
-  if (rt * 64 >= R2 || cs * CT * 64 >= C2) return;   // workgroup-uniform
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
-  double* Kb = K + (size_t)b * nmax * ld;
-  const int32_t* pb = perm + (size_t)b * nmax;
-  const int cend = c0 + KW + C2;
-  const int c8 = (t & 7) * 8;
-  size_t urow[KW / 32];
-#pragma unroll
-  for (int h = 0; h < KW / 32; ++h) urow[h] = (size_t)pb[c0 + 32 * h + (t >> 3)] * ld;
-  double uv[KW / 32][8];
-  auto load_u = [&](int cb) {
-    const bool ok = cb + c8 < cend;   // 32-aligned halves: all-or-nothing
-#pragma unroll
-    for (int h = 0; h < KW / 32; ++h) {
-      const double* src = Kb + urow[h] + (ok ? cb + c8 : 0);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) uv[h][u] = ok ? src[u] : 0.0;
-    }
-  };
-  auto store_u = [&]() {
-#pragma unroll
-    for (int h = 0; h < KW / 32; ++h) {
-      const int k = 32 * h + (t >> 3);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) U[k * ULD + c8 + u] = uv[h][u];
-    }
-  };
-  const int rbase = c0 + KW + rt * 64 + 16 * wv;
-  const bool wact = rt * 64 + 16 * wv < R2;   // wave-uniform
-  double a[KW / 4];
-  size_t ro[4];
-  d4b acc[4], accn[4];
-  int ct = cs * CT;
-  int cbase = c0 + KW + ct * 64;
-  load_u(cbase);
-  if (wact) {
-    const double* arow = Kb + (size_t)pb[rbase + l16] * ld + c0;
-#pragma unroll
-    for (int s = 0; s < KW / 4; ++s) a[s] = -arow[4 * s + g];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) ro[rr] = (size_t)pb[rbase + g + 4 * rr] * ld;
-    const int nq = min(4, (C2 - ct * 64) >> 4);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int cq = cbase + 16 * min(q, nq - 1) + l16;
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) acc[q][rr] = Kb[ro[rr] + cq];
-    }
-  }
-  store_u();
-  __syncthreads();
-#pragma unroll 1
-  for (int j = 0; j < CT; ++j) {
-    const int nq = min(4, (C2 - ct * 64) >> 4);
-    const bool more = j + 1 < CT && (ct + 1) * 64 < C2;   // workgroup-uniform
-    if (more) {
-      load_u(cbase + 64);
-      if (wact) {
-        const int nqn = min(4, (C2 - (ct + 1) * 64) >> 4);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int cq = cbase + 64 + 16 * min(q, nqn - 1) + l16;
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) accn[q][rr] = Kb[ro[rr] + cq];
-        }
-      }
-    }
-    if (wact) {
-#pragma unroll
-      for (int s = 0; s < KW / 4; ++s) {
-        double bq[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) bq[q] = U[(4 * s + g) * ULD + 16 * q + l16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = bmfma(a[s], bq[q], acc[q]);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (q < nq) {
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) Kb[ro[rr] + cbase + 16 * q + l16] = acc[q][rr];
-        }
-      }
-    }
-    if (!more) break;
-    __syncthreads();   // every wave has read U of this tile
-    store_u();
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = accn[q];
-    ++ct;
-    cbase += 64;
-  }
-}
-
 // ---------------------------------------------------------------------------
-// U12 of panel i of a panel group (group scheme, see qp_blocked_factor):
-//   A12 −= L[pivot rows, kc pending columns c0g .. c0g+kc) · U[those rows, trailing]
-//   U12  = L11⁻¹ · A12
-// for the 32 pivot rows of the panel at column ci over its trailing columns
-// ≥ ci+32.  One 256-thread workgroup per (problem, 64-column tile), one
-// 16-column MFMA strip per wave; the same operand layouts as the panel
-// kernel's in-kernel U12 (A operand −L / L11⁻¹ rows, B operand row-k strips).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void blu_u12_kernel(double* __restrict__ K, int ld, int nmax,
-                                                      const int32_t* __restrict__ perm,
-                                                      const double* __restrict__ dinv,
-                                                      size_t dstride, const QPMeta* __restrict__ meta,
-                                                      int c0g, int ci, int kc, int fast_max, int nct,
-                                                      int total, int b0) {
-  const int L = blockIdx.x;
-  const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
-  const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
-  const int bl = logical / nct;
-  const int ct = logical - bl * nct;
-  const int b = b0 + bl;
-  const int Np = blocked_np(meta[b], fast_max);
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
-  const int ntile = (Np - ci - BNB) >> 4;   // 16-column strips right of the panel
-  const int q = ct * 4 + wv;
-  if (ci + BNB >= Np || q >= ntile) return;   // wave-uniform
-  double* Kb = K + (size_t)b * nmax * ld;
-  const int32_t* pb = perm + (size_t)b * nmax;
-  const double* Db = dinv + (size_t)b * dstride + (size_t)(ci / BNB) * BDINV;   // L11⁻¹, row-major
-  const int colL = ci + BNB + 16 * q + l16;
-  int ptop0 = pb[ci + l16], ptop1 = pb[ci + 16 + l16];
-  double bv[BNB / 4];
-#pragma unroll
-  for (int s = 0; s < BNB / 4; ++s) bv[s] = Kb[(size_t)pb[ci + 4 * s + g] * ld + colL];
-  d4b c0v = {bv[0], bv[1], bv[2], bv[3]}, c1v = {bv[4], bv[5], bv[6], bv[7]};
-  for (int kb = c0g; kb < c0g + kc; kb += BNB) {
-    double lp0[BNB / 4], lp1[BNB / 4], up[BNB / 4];
-#pragma unroll
-    for (int s = 0; s < BNB / 4; ++s) {
-      lp0[s] = -Kb[(size_t)ptop0 * ld + kb + 4 * s + g];
-      lp1[s] = -Kb[(size_t)ptop1 * ld + kb + 4 * s + g];
-      up[s] = Kb[(size_t)pb[kb + 4 * s + g] * ld + colL];
-    }
-#pragma unroll
-    for (int s = 0; s < BNB / 4; ++s) {
-      c0v = bmfma(lp0[s], up[s], c0v);
-      c1v = bmfma(lp1[s], up[s], c1v);
-    }
-  }
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    bv[rr] = c0v[rr];
-    bv[4 + rr] = c1v[rr];
-  }
-  d4b u0 = {0, 0, 0, 0}, u1 = {0, 0, 0, 0};
-#pragma unroll
-  for (int s = 0; s < BNB / 4; ++s) {
-    u0 = bmfma(Db[l16 * BNB + 4 * s + g], bv[s], u0);
-    u1 = bmfma(Db[(16 + l16) * BNB + 4 * s + g], bv[s], u1);
-  }
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    Kb[(size_t)pb[ci + g + 4 * rr] * ld + colL] = u0[rr];
-    Kb[(size_t)pb[ci + 16 + g + 4 * rr] * ld + colL] = u1[rr];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Solves with the relabelled factors (see lu_solve_fast in qp_fast.hip):
+// Solves with the relabelled factors:
 //   trans = 0:  K x = b   →  L U x = P b          (x in unknown order)
 //   trans = 1:  Kᵀ x = b  →  Uᵀ w = b, Lᵀ v = w, x = Pᵀ v
 // Four right-looking block sweeps; per 32-block: the diagonal GEMV with the
@@ -666,13 +451,13 @@ template <int ENT>
 __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict__ K, int ld, int nmax,
                                                 const int32_t* __restrict__ perm,
                                                 const double* __restrict__ dinv, size_t dstride,
-                                                const QPMeta* __restrict__ meta, int fast_max, int trans,
+                                                const QPMeta* __restrict__ meta, int trans, int sel,
                                                 const double* __restrict__ rhs,
                                                 double* __restrict__ xout, double* v, double* y, int* ps,
                                                 double* part) {
   const QPMeta mm = meta[b];
-  const int Np = blocked_np(mm, fast_max);
-  if (Np == 0) return;
+  const int Np = blocked_np(mm);
+  if (Np == 0 || !((sel >> mm.lu) & 1)) return;
   const int N = mm.nsys;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const double* Kb = K + (size_t)b * nmax * ld;
@@ -749,14 +534,14 @@ __global__ __launch_bounds__(PT) void blu_solve_kernel(const double* __restrict_
                                                        const int32_t* __restrict__ perm,
                                                        const double* __restrict__ dinv,
                                                        size_t dstride, const QPMeta* __restrict__ meta,
-                                                       int fast_max, int trans,
+                                                       int trans, int sel,
                                                        const double* __restrict__ rhs,
                                                        double* __restrict__ xout) {
   __shared__ double v[BLOCKED_MAX];
   __shared__ double y[BLOCKED_MAX];
   __shared__ int ps[BLOCKED_MAX];
   __shared__ double part[BNB];
-  solve_cols_body<ENT>(blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, fast_max, trans, rhs, xout,
+  solve_cols_body<ENT>(blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, trans, sel, rhs, xout,
                        v, y, ps, part);
 }
 
@@ -774,13 +559,13 @@ constexpr int RCH = 8;          // passes per load chunk
 __device__ __forceinline__ void solve_rows_body(int b, const double* __restrict__ K, int ld, int nmax,
                                                 const int32_t* __restrict__ perm,
                                                 const double* __restrict__ dinv, size_t dstride,
-                                                const QPMeta* __restrict__ meta, int fast_max,
+                                                const QPMeta* __restrict__ meta, int sel,
                                                 const double* __restrict__ rhs,
                                                 double* __restrict__ xout, double* v, int* ps,
                                                 double* part) {
   const QPMeta mm = meta[b];
-  const int Np = blocked_np(mm, fast_max);
-  if (Np == 0) return;
+  const int Np = blocked_np(mm);
+  if (Np == 0 || !((sel >> mm.lu) & 1)) return;
   const int N = mm.nsys;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int g8 = t & 7, rid = t >> 3;
@@ -855,14 +640,13 @@ __global__ __launch_bounds__(PT) void blu_solve_rows_kernel(const double* __rest
                                                             const int32_t* __restrict__ perm,
                                                             const double* __restrict__ dinv,
                                                             size_t dstride,
-                                                            const QPMeta* __restrict__ meta,
-                                                            int fast_max,
+                                                            const QPMeta* __restrict__ meta, int sel,
                                                             const double* __restrict__ rhs,
                                                             double* __restrict__ xout) {
   __shared__ double v[BLOCKED_MAX];
   __shared__ int ps[BLOCKED_MAX];
   __shared__ double part[BNB];
-  solve_rows_body(blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, fast_max, rhs, xout, v, ps, part);
+  solve_rows_body(blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, sel, rhs, xout, v, ps, part);
 }
 
 // Both directions of one forward+reverse step in ONE launch (2B workgroups):
@@ -876,82 +660,42 @@ __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict
                                                         const int32_t* __restrict__ perm,
                                                         const double* __restrict__ dinv,
                                                         size_t dstride, const QPMeta* __restrict__ meta,
-                                                        int fast_max, int B,
+                                                        int B, int sel,
                                                         const double* __restrict__ rhs_rev,
                                                         const double* __restrict__ rhs_fwd,
                                                         double* __restrict__ x_rev,
-                                                        double* __restrict__ x_fwd, int ilv) {
+                                                        double* __restrict__ x_fwd) {
   __shared__ double v[BLOCKED_MAX];
   __shared__ double y[BLOCKED_MAX];
   __shared__ int ps[BLOCKED_MAX];
   __shared__ double part[BNB];
   int L = blockIdx.x;
-  if (ilv) {   // B % 8 == 0: workgroups 16g+j (rows) and 16g+8+j (columns) solve problem 8g+j
+  if (B % 8 == 0) {   // workgroups 16g+j (rows) and 16g+8+j (columns) solve problem 8g+j
     const int g = L >> 4, j = L & 7;
     L = (L & 8) ? B + 8 * g + j : 8 * g + j;
   }
   if (L < B)
-    solve_rows_body(L, K, ld, nmax, perm, dinv, dstride, meta, fast_max, rhs_rev, x_rev, v, ps, part);
+    solve_rows_body(L, K, ld, nmax, perm, dinv, dstride, meta, sel, rhs_rev, x_rev, v, ps, part);
   else
-    solve_cols_body<ENT>(L - B, K, ld, nmax, perm, dinv, dstride, meta, fast_max, 1, rhs_fwd, x_fwd, v,
+    solve_cols_body<ENT>(L - B, K, ld, nmax, perm, dinv, dstride, meta, 1, sel, rhs_fwd, x_fwd, v,
                          y, ps, part);
 }
 
 }  // namespace
 
-size_t fast_dinv_stride(int nmax);
-
-// Largest padded blocked size in the batch (host read-back of the per-problem
-// metadata the assembly wrote; one small D2H copy per factorisation).  Also
-// records whether any problem needs the generic (> BLOCKED_MAX) kernels.
-static int blocked_npmax(Handle& h) {
-  std::vector<QPMeta> meta(h.batch);
-  DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h.meta.p, h.batch * sizeof(QPMeta),
-                                hipMemcpyDeviceToHost, h.stream));
-  DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
-  int npmax = 0;
-  h.has_generic = false;
-  for (auto& mm : meta) {
-    const int r = qp_route(mm.iterative, mm.nsys, h.fast_max);
-    if (r == ROUTE_BLOCKED) npmax = std::max(npmax, (mm.nsys + BNB - 1) & ~(BNB - 1));
-    h.has_generic |= r == ROUTE_GENERIC;
-  }
-  return npmax;
-}
-
-void qp_blocked_factor(Handle& h, double* dinv) {
-  const int npmax = blocked_npmax(h);
-  h.blocked_npmax = npmax;
-  if (npmax == 0) return;
-  const int B = (int)h.batch;
-  const size_t dstride = fast_dinv_stride(h.nmax);
+// Partial-pivoting blocked LU of `count` problems (plist: their indices; null
+// = problems 0 .. count−1).  Panels go in pairs (c0, c0+32): panel A; narrow
+// rank-32 update of panel B's columns; panel B (with the pending rank-32
+// correction of its pivot rows' trailing columns); one rank-64 update of
+// everything right of and below the pair — half the trailing-matrix traffic of
+// rank-32 steps.  Sized by h.blocked_npmax (the read-back of the metadata).
+void qp_blocked_factor(Handle& h, double* dinv, const int32_t* plist, int count) {
+  const int npmax = h.blocked_npmax;
+  if (npmax == 0 || count == 0) return;
+  const size_t dstride = dinv_stride(h.nmax);
   double* K = h.K.as<double>();
   int32_t* perm = h.ipiv.as<int32_t>();
   QPMeta* meta = h.meta.as<QPMeta>();
-  // Panels go in pairs (c0, c0+32): panel A; narrow rank-32 update of panel
-  // B's columns; panel B (with the pending rank-32 correction of its pivot
-  // rows' trailing columns); one rank-64 update of everything right of and
-  // below the pair — half the trailing-matrix traffic of rank-32 steps.
-  unsigned long long* st = h.stamps.as<unsigned long long>();
-  // The batch is cut into `ns` contiguous chunks, each stepping through its
-  // panels on its own HIP stream: one chunk's latency-bound panel kernels
-  // overlap another chunk's MFMA trailing updates (env DOPT_LU_STREAMS).
-  const int ns = std::max(1, std::min<int>(h.lu_streams, std::min(B / 64, DOPT_MAX_LU_STREAMS)));
-  hipStream_t sts[DOPT_MAX_LU_STREAMS];
-  sts[0] = h.stream;
-  if (ns > 1) {
-    if (!h.fork_ev) DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.fork_ev, hipEventDisableTiming));
-    DOPT_CHECK_HIP(hipEventRecord(h.fork_ev, h.stream));
-    for (int k = 1; k < ns; ++k) {
-      if (!h.sub_stream[k]) {
-        DOPT_CHECK_HIP(hipStreamCreateWithFlags(&h.sub_stream[k], hipStreamNonBlocking));
-        DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.join_ev[k], hipEventDisableTiming));
-      }
-      sts[k] = h.sub_stream[k];
-      DOPT_CHECK_HIP(hipStreamWaitEvent(sts[k], h.fork_ev, 0));
-    }
-  }
-  int b0 = 0, bc = B;
   hipStream_t stm = h.stream;
   auto panel = [&](int c0, int corr) {
     // workgroup shape by panel height: the per-column pivot overhead (argmax,
@@ -959,18 +703,10 @@ void qp_blocked_factor(Handle& h, double* dinv) {
     // few waves with several rows per thread (two waves up to 384 rows, four
     // workgroups per CU), tall panels 8 waves with 2–3 rows per thread
     const int R = npmax - c0;
-#define DOPT_PANEL(T, Q)                                                                     \
-  hipLaunchKernelGGL((blu_panel_kernel<T, Q>), dim3(bc), dim3(T), 0, stm, K, h.ld, h.nmax, \
-                     perm, dinv, dstride, meta, c0, h.fast_max, corr, st, b0)
-#ifndef DOPT_PANEL_VARIANT
-#define DOPT_PANEL_VARIANT 0
-#endif
-    if (DOPT_PANEL_VARIANT == 1 && R > 128 && R <= 512) {   // tuning build: 4 waves, 1–2 rows/thread
-      if (R <= 256) DOPT_PANEL(256, 1);
-      else DOPT_PANEL(256, 2);
-    } else if (DOPT_PANEL_VARIANT == 2 && R <= 128) {   // tuning build: one wave, no cross-wave fold
-      DOPT_PANEL(64, 2);
-    } else if (R <= 128) DOPT_PANEL(128, 1);
+#define DOPT_PANEL(T, Q)                                                                        \
+  hipLaunchKernelGGL((blu_panel_kernel<T, Q>), dim3(count), dim3(T), 0, stm, K, h.ld, h.nmax, \
+                     perm, dinv, dstride, meta, c0, corr, plist)
+    if (R <= 128) DOPT_PANEL(128, 1);
     else if (R <= 256) DOPT_PANEL(128, 2);
     else if (R <= 384) DOPT_PANEL(128, 3);
     else if (R <= 512) DOPT_PANEL(256, 2);
@@ -983,128 +719,67 @@ void qp_blocked_factor(Handle& h, double* dinv) {
     const int R2 = npmax - c0 - kw;
     if (R2 <= 0) return;
     const int nrt = (R2 + 63) / 64, nct = (std::min(R2, cols_max) + 63) / 64;
-    const int CT = h.upd_ct;
-    if (CT > 1 && nct > 1) {   // strip kernel: CT column tiles per workgroup
-      const int ncs = (nct + CT - 1) / CT;
-      const long long tot = (long long)nrt * ncs * bc;
-      if (tot > 0x7fffffffLL) throw Error(-1, "blocked LU: trailing-update grid too large");
-#define DOPT_STRIP(KW, C)                                                                           \
-  hipLaunchKernelGGL((blu_update_strip_kernel<KW, C>), dim3((unsigned)tot), dim3(256), 0, stm, K, h.ld, \
-                     h.nmax, perm, meta, c0, h.fast_max, cols_max, nrt, ncs, (int)tot, b0)
-      if (kw == 64) {
-        if (CT == 2) DOPT_STRIP(64, 2);
-        else DOPT_STRIP(64, 4);
-        DOPT_CHECK_HIP(hipGetLastError());
-        return;
-      }
-#undef DOPT_STRIP
-    }
-    const long long total = (long long)nrt * nct * bc;
+    const long long total = (long long)nrt * nct * count;
     if (total > 0x7fffffffLL) throw Error(-1, "blocked LU: trailing-update grid too large");
-#define DOPT_UPDATE(KW)                                                                           \
-  hipLaunchKernelGGL(blu_update_kernel<KW>, dim3((unsigned)total), dim3(256), 0, stm, K, h.ld, h.nmax, \
-                     perm, meta, c0, h.fast_max, cols_max, nrt, nct, (int)total, b0)
-    if (kw == 128) DOPT_UPDATE(128);
-    else if (kw == 96) DOPT_UPDATE(96);
-    else if (kw == 64) DOPT_UPDATE(64);
-    else DOPT_UPDATE(32);
-#undef DOPT_UPDATE
+    if (kw == 64)
+      hipLaunchKernelGGL(blu_update_kernel<64>, dim3((unsigned)total), dim3(256), 0, stm, K, h.ld, h.nmax,
+                         perm, meta, c0, cols_max, nrt, nct, (int)total, plist);
+    else
+      hipLaunchKernelGGL(blu_update_kernel<32>, dim3((unsigned)total), dim3(256), 0, stm, K, h.ld, h.nmax,
+                         perm, meta, c0, cols_max, nrt, nct, (int)total, plist);
     DOPT_CHECK_HIP(hipGetLastError());
   };
-  // chunks issued step-interleaved so every stream has work queued early
-  int cb0[DOPT_MAX_LU_STREAMS], cbc[DOPT_MAX_LU_STREAMS];
-  for (int k = 0; k < ns; ++k) {
-    cb0[k] = (int)((long long)B * k / ns);
-    cbc[k] = (int)((long long)B * (k + 1) / ns) - cb0[k];
-  }
-  auto u12 = [&](int c0g, int ci, int kc) {
-    const int R = npmax - ci - BNB;
-    if (R <= 0) return;
-    const int nct = (R + 63) / 64;
-    const long long total = (long long)nct * bc;
-    if (total > 0x7fffffffLL) throw Error(-1, "blocked LU: U12 grid too large");
-    hipLaunchKernelGGL(blu_u12_kernel, dim3((unsigned)total), dim3(256), 0, stm, K, h.ld, h.nmax, perm,
-                       dinv, dstride, meta, c0g, ci, kc, h.fast_max, nct, (int)total, b0);
-    DOPT_CHECK_HIP(hipGetLastError());
-  };
-  const int G = h.lu_group;
-  for (int c0 = 0; c0 < npmax; c0 += (G ? G : 2) * BNB) {
-    for (int k = 0; k < ns; ++k) {
-      b0 = cb0[k];
-      bc = cbc[k];
-      stm = sts[k];
-      if (G == 0) {   // panel pairs with the in-panel pending-rank-32 correction
-        panel(c0, 0);
-        if (npmax - c0 <= BNB) continue;
-        update(c0, BNB, BNB);          // panel B's 32 columns, all rows below panel A
-        panel(c0 + BNB, 1);
-        update(c0, 2 * BNB, 1 << 30);  // rank 64, rows and columns from c0+64
-        continue;
-      }
-      // Panel group of g ≤ G panels, left-looking inside the group: panel i's
-      // 32 columns get the group's pending rank-32i update (rows ≥ ci), then
-      // the panel factors, then its U12 strip applies the same pending update
-      // to its pivot rows and multiplies by L11⁻¹; one rank-32g update of
-      // everything right of and below the group ends it — C traffic ∝ 1/g.
-      const int g = std::min(G, (npmax - c0) / BNB);
-      for (int i = 0; i < g; ++i) {
-        const int ci = c0 + i * BNB;
-        if (i > 0) update(c0, i * BNB, BNB);
-        panel(ci, -1);
-        u12(c0, ci, i * BNB);
-      }
-      update(c0, g * BNB, 1 << 30);
-    }
-  }
-  for (int k = 1; k < ns; ++k) {
-    DOPT_CHECK_HIP(hipEventRecord(h.join_ev[k], sts[k]));
-    DOPT_CHECK_HIP(hipStreamWaitEvent(h.stream, h.join_ev[k], 0));
+  for (int c0 = 0; c0 < npmax; c0 += 2 * BNB) {
+    panel(c0, 0);
+    if (npmax - c0 <= BNB) continue;
+    update(c0, BNB, BNB);          // panel B's 32 columns, all rows below panel A
+    panel(c0 + BNB, 1);
+    update(c0, 2 * BNB, 1 << 30);  // rank 64, rows and columns from c0+64
   }
 }
 
-void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rhs, double* x) {
+void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rhs, double* x, int sel) {
   const int npmax = h.blocked_npmax;
   if (npmax == 0) return;
   const int B = (int)h.batch;
-  const size_t dstride = fast_dinv_stride(h.nmax);
+  const size_t dstride = dinv_stride(h.nmax);
   const double* K = h.K.as<double>();
   const int32_t* perm = h.ipiv.as<int32_t>();
   const QPMeta* meta = h.meta.as<QPMeta>();
   if (!trans) {
     hipLaunchKernelGGL(blu_solve_rows_kernel, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
-                       dinv, dstride, meta, h.fast_max, rhs, x);
+                       dinv, dstride, meta, sel, rhs, x);
   } else {
     // Kᵀ x = b: the slices are column segments, contiguous across entries, so
     // one entry per thread is already coalesced
     const int ent = (npmax + PT - 1) / PT;
     if (ent <= 1)
       hipLaunchKernelGGL(blu_solve_kernel<1>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
-                         dinv, dstride, meta, h.fast_max, trans, rhs, x);
+                         dinv, dstride, meta, trans, sel, rhs, x);
     else if (ent == 2)
       hipLaunchKernelGGL(blu_solve_kernel<2>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
-                         dinv, dstride, meta, h.fast_max, trans, rhs, x);
+                         dinv, dstride, meta, trans, sel, rhs, x);
     else
       hipLaunchKernelGGL(blu_solve_kernel<3>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
-                         dinv, dstride, meta, h.fast_max, trans, rhs, x);
+                         dinv, dstride, meta, trans, sel, rhs, x);
   }
   DOPT_CHECK_HIP(hipGetLastError());
 }
 
 void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, const double* rhs_fwd,
-                       double* x_rev, double* x_fwd) {
+                       double* x_rev, double* x_fwd, int sel) {
   const int npmax = h.blocked_npmax;
   if (npmax == 0) return;
   const int B = (int)h.batch;
   if (2LL * B > 0x7fffffffLL) throw Error(-1, "blocked solve: grid too large");
-  const size_t dstride = fast_dinv_stride(h.nmax);
+  const size_t dstride = dinv_stride(h.nmax);
   const double* K = h.K.as<double>();
   const int32_t* perm = h.ipiv.as<int32_t>();
   const QPMeta* meta = h.meta.as<QPMeta>();
   const int ent = (npmax + PT - 1) / PT;
 #define DOPT_SOLVE2(E)                                                                            \
   hipLaunchKernelGGL(blu_solve2_kernel<E>, dim3(2 * B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm, \
-                     dinv, dstride, meta, h.fast_max, B, rhs_rev, rhs_fwd, x_rev, x_fwd, ilv)
-  const int ilv = h.solve_ilv && B % 8 == 0;
+                     dinv, dstride, meta, B, sel, rhs_rev, rhs_fwd, x_rev, x_fwd)
   if (ent <= 1) DOPT_SOLVE2(1);
   else if (ent == 2) DOPT_SOLVE2(2);
   else DOPT_SOLVE2(3);

@@ -1,0 +1,678 @@
+// Blocked path, part 1: the no-pivot blocked LU of the reduced KKT systems
+// (the default factorisation of every ROUTE_BLOCKED problem).
+//
+// Why no pivoting.  The reference factorises `LHS \ RHS` with UMFPACK
+// (QuadraticProgram.jl:490), whose pivoting is *threshold* pivoting with a
+// diagonal preference (pivot tolerance 0.1), not LAPACK's partial pivoting.
+// This engine factorises K = L·U in its natural order and accepts the factors
+// of a problem only if every multiplier satisfies |l_ij| ≤ NOPIV_LMAX = 10,
+// i.e. every diagonal pivot passes |a_jj| ≥ 0.1·max_{i>j}|a_ij| on the
+// Schur complement it is taken from — the same acceptance test with the
+// diagonal as the candidate.  A problem that fails (a zero or non-finite
+// pivot, or a multiplier above 10) is marked LU_REJECT; the host re-assembles
+// it and factorises it with partial pivoting (qp_blocked.hip).  For strictly
+// convex QPs the reduced KKT [Q, G_kᵀΛ_k; G_k, D(s_k)] is a column-scaled
+// quasi-definite matrix, whose no-pivot LU exists and is stable (DESIGN.md
+// §2.1 measures max|l| ≈ 1–2 on configs 1–3).
+//
+// Without pivoting the panel has no column-by-column argmax over the whole
+// panel height: per 64-column block step
+//
+//   nlu_diag_kernel   (one 256-thread WG per problem)
+//     factor the 64×64 diagonal block in registers (4×4 tile per thread, one
+//     barrier per column), its inverses L11⁻¹ / U11⁻¹ (LDS, MFMA for the
+//     off-diagonal blocks), the 32×32 diagonal-block inverses (dinv) the
+//     solves use
+//   nlu_trsm_kernel   (one 256-thread WG per 64-row / 64-column strip)
+//     L21 = A21·U11⁻¹ and U12 = L11⁻¹·A12 on v_mfma_f64_16x16x4f64 (the
+//     triangular structure of the inverses skips 3/8 of the k-steps) and the
+//     threshold test on L21
+//   nlu_update_kernel (one 256-thread WG per 64×64 trailing tile)
+//     A22 −= L21·U12, rank 64 on MFMA, the U12 tile staged in LDS, XCD-aware
+//     tile order (one problem's tiles share an L2)
+//
+// Factor format: K row-major, L strictly below / U on and above the diagonal,
+// perm = identity, dinv as the partial-pivoting path writes it — the solves of
+// qp_blocked.hip serve both.
+//
+// Reference: QuadraticProgram.jl create_LHS_matrix :256-282 and solve_system
+// :486-496 (reverse :316-351, forward :357-446).
+#include "dopt_internal.h"
+
+// tools/probe/nlu_probe.hip builds this file with -DNLU_STOP=k to time the
+// diagonal kernel up to phase k; the product build never stops early
+#ifndef NLU_STOP
+#define NLU_STOP 99
+#endif
+// probe builds with -DNLU_STAMPS: per-phase s_memtime cycles of the diagonal
+// kernel summed over workgroups into nlu_stamps[] (thread 0)
+#ifdef NLU_STAMPS
+__device__ unsigned long long nlu_stamps[16];
+#define NLU_MARK(k)                                                              \
+  do {                                                                          \
+    if (threadIdx.x == 0) {                                                     \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();             \
+      atomicAdd(&nlu_stamps[k], now_ - st_last_);                               \
+      st_last_ = now_;                                                          \
+    }                                                                           \
+  } while (0)
+#define NLU_MARK_INIT unsigned long long st_last_ = __builtin_amdgcn_s_memtime()
+#else
+#define NLU_MARK(k) do {} while (0)
+#define NLU_MARK_INIT do {} while (0)
+#endif
+
+namespace dopt {
+
+namespace {
+
+typedef double d4n __attribute__((ext_vector_type(4)));
+
+constexpr int NB64 = 64;           // diagonal block width
+constexpr int SLD = NB64 + 1;      // LDS row stride of the 64×64 block
+constexpr int PNT = 256;           // panel threads
+constexpr int DBLK = 2 * 32 * 32;  // doubles per 32-block in dinv (L⁻¹ | U⁻¹)
+
+__device__ __forceinline__ d4n nmfma(double a, double b, d4n c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int nlu_np(const QPMeta& mm) {
+  if (qp_route(mm.iterative, mm.nsys) != ROUTE_BLOCKED) return 0;
+  return (mm.nsys + 31) & ~31;
+}
+
+// ---------------------------------------------------------------------------
+// Single-wave LU (no pivoting) of the 32×32 block at rows / columns o..o+31
+// of the LDS image S: lane = 4×4 tile (ti = lane >> 3, tj = lane & 7); the
+// owners of row / column j publish them through `rowb` / `colb` and the wave
+// reads them back — no workgroup barrier.  Column j's multipliers go straight
+// into S, the U part is written from the registers at the end.  Returns the
+// wave's threshold verdict (1: a zero / non-finite pivot or |l| > NOPIV_LMAX).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double* colb) {
+  const int lane = threadIdx.x & 63, ti = lane >> 3, tj = lane & 7;
+  double a[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a[r][c] = S[(o + 4 * ti + r) * SLD + o + 4 * tj + c];
+  int bad = 0;
+#pragma unroll 1
+  for (int j4 = 0; j4 < 8; ++j4) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = 4 * j4 + jj;
+      if (ti == j4) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) rowb[4 * tj + c] = a[jj][c];
+      }
+      if (tj == j4) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) colb[4 * ti + r] = a[r][jj];
+      }
+      wave_sync();
+      const double piv = rowb[j];
+      const double rcp = 1.0 / piv;
+      double l[4], lm[4], um[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        l[r] = colb[4 * ti + r] * rcp;
+        lm[r] = (4 * ti + r > j) ? l[r] : 0.0;
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const double u = rowb[4 * tj + c];
+        um[c] = (4 * tj + c > j) ? u : 0.0;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a[r][c] = fma(-lm[r], um[c], a[r][c]);
+      int over = !(fabs(piv) > 0.0) || !(fabs(piv) <= 1.7976931348623157e308);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) over |= (4 * ti + r > j) & !(fabs(l[r]) <= NOPIV_LMAX);
+      if (tj == j4) {
+        bad |= over;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * ti + r > j) S[(o + 4 * ti + r) * SLD + o + j] = l[r];
+      }
+      wave_sync();   // this step's reads of rowb / colb precede the next publish
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (4 * ti + r <= 4 * tj + c) S[(o + 4 * ti + r) * SLD + o + 4 * tj + c] = a[r][c];
+  return __any(bad) ? 1 : 0;
+}
+
+// x = column `c` of the inverse of the unit-lower 32×32 block at (o, o) of S
+// (right-looking forward substitution, one column per lane)
+__device__ __forceinline__ void lower_inv_col(const double* S, int o, int c, double* x) {
+#pragma unroll
+  for (int jj = 0; jj < 32; ++jj) x[jj] = (jj == c) ? 1.0 : 0.0;
+#pragma unroll
+  for (int i = 0; i < 31; ++i) {
+#pragma unroll
+    for (int jj = i + 1; jj < 32; ++jj) x[jj] = fma(-S[(o + jj) * SLD + o + i], x[i], x[jj]);
+  }
+}
+
+// x = column `c` of the inverse of the upper 32×32 block at (o, o) of S
+__device__ __forceinline__ void upper_inv_col(const double* S, int o, int c, double* x) {
+#pragma unroll
+  for (int jj = 0; jj < 32; ++jj) x[jj] = (jj == c) ? 1.0 : 0.0;
+#pragma unroll
+  for (int jj = 31; jj >= 0; --jj) {
+    x[jj] = x[jj] / S[(o + jj) * SLD + o + jj];
+#pragma unroll
+    for (int i = 0; i < jj; ++i) x[i] = fma(-S[(o + i) * SLD + o + jj], x[jj], x[i]);
+  }
+}
+
+// one 16×16 tile of a 32×32×32 product on MFMA: acc = A[tr.., :] · B[:, tc..]
+// with A(i, k) / B(k, j) given by functors (lane: A row tr+l16, B column tc+l16)
+template <class FA, class FB>
+__device__ __forceinline__ d4n tile32(int tr, int tc, FA A, FB Bm) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+  double av[8], bv[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {   // every operand load issued before the first MFMA
+    av[s] = A(tr + l16, 4 * s + g);
+    bv[s] = Bm(4 * s + g, tc + l16);
+  }
+  d4n acc = {0, 0, 0, 0};
+#pragma unroll
+  for (int s = 0; s < 8; ++s) acc = nmfma(av[s], bv[s], acc);
+  return acc;
+}
+
+// ---------------------------------------------------------------------------
+// Diagonal block of step c0 (multiple of 64) of problem blockIdx.x: rows and
+// columns c0 .. c0+63 (the last block may be 32 wide), factorised
+// recursively as two 32×32 blocks a, b:
+//   A  wave 0: LU of a (wave_lu32)
+//   B  waves 0–3: L_aa⁻¹, U_aa⁻¹ (the solves' dinv), U_ab = L_aa⁻¹A_ab,
+//      L_ba = A_ba U_aa⁻¹ (+ threshold test), one column / row per lane
+//   C  A_bb −= L_ba U_ab (MFMA)
+//   D  wave 0: LU of b
+//   E  waves 0–1: L_bb⁻¹, U_bb⁻¹; waves 2–3: T_L = L_ba L_aa⁻¹, T_U = U_aa⁻¹U_ab
+//   F  L⁻¹_ba = −L_bb⁻¹T_L, U⁻¹_ab = −T_U U_bb⁻¹ (MFMA)
+// Writes L11 / U11 to K, perm = identity, the 32×32 diagonal-block inverses to
+// dinv and the packed 64×64 inverse (L11⁻¹ strictly below the diagonal,
+// U11⁻¹ on and above it) to `binv` for the TRSM launch.  ~35 KB of LDS and
+// one 256-thread workgroup per problem: 4 per CU, a 1024-problem batch runs
+// in one round.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_diag_kernel(
+    double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
+    size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv) {
+  __shared__ double S[NB64 * SLD];
+  __shared__ double rowb[32], colb[32];
+  __shared__ int sbad;
+  const int b = blockIdx.x;
+  const QPMeta mm = meta[b];
+  const int Np = nlu_np(mm);
+  if (c0 >= Np || mm.lu == LU_REJECT) return;   // workgroup-uniform
+  const int Wv = min(NB64, Np - c0);             // 32 or 64
+  const bool trsm = Np - c0 > NB64;              // a TRSM launch follows
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int g = lane >> 4, l16 = lane & 15;
+  double* Kb = K + (size_t)b * nmax * ld;
+  double* Db = dinv + (size_t)b * dstride + (size_t)(c0 / 32) * DBLK;
+  double* Bg = binv + (size_t)b * NB64 * NB64;
+  auto to_K = [&](int r0, int cc0) {   // 32×32 block (r0, cc0) of S → K
+    for (int e = t; e < 32 * 32; e += PNT) {
+      const int i = r0 + (e >> 5), j = cc0 + (e & 31);
+      Kb[(size_t)(c0 + i) * ld + c0 + j] = S[i * SLD + j];
+    }
+  };
+
+  NLU_MARK_INIT;
+  // ---- 0. the block → LDS (identity beyond Wv); all 16 loads in flight
+  {
+    double v[NB64 * NB64 / PNT];
+#pragma unroll
+    for (int q = 0; q < NB64 * NB64 / PNT; ++q) {
+      const int e = t + PNT * q, i = e >> 6, j = e & 63;
+      const bool in = i < Wv && j < Wv;
+      v[q] = Kb[(size_t)(c0 + (in ? i : 0)) * ld + c0 + (in ? j : 0)];
+    }
+#pragma unroll
+    for (int q = 0; q < NB64 * NB64 / PNT; ++q) {
+      const int e = t + PNT * q, i = e >> 6, j = e & 63;
+      const bool in = i < Wv && j < Wv;
+      S[i * SLD + j] = in ? v[q] : (i == j ? 1.0 : 0.0);
+    }
+  }
+  if (t == 0) {
+    sbad = 0;
+    if (c0 == 0) meta[b].lu = LU_NOPIV;   // LU_REJECT below if a test fails
+  }
+  if (t < Wv) perm[(size_t)b * nmax + c0 + t] = c0 + t;
+  __syncthreads();
+  NLU_MARK(0);
+  if (NLU_STOP <= 1) return;
+
+  // ---- A. LU of block a
+  if (wv == 0) {
+    const int bad = wave_lu32(S, 0, rowb, colb);
+    if (lane == 0 && bad) sbad = 1;
+  }
+  __syncthreads();
+  if (sbad) {
+    if (t == 0) meta[b].lu = LU_REJECT;
+    return;
+  }
+  NLU_MARK(1);
+  to_K(0, 0);
+  if (NLU_STOP <= 2) return;
+
+  // ---- B. inverses of block a, U_ab, L_ba (lanes 0–31 of each wave)
+  {
+    const int c = lane;
+    double x[32];
+    int bad = 0;
+    if (lane < 32) {
+      if (wv == 0) {
+        lower_inv_col(S, 0, c, x);
+      } else if (wv == 1) {
+        upper_inv_col(S, 0, c, x);
+      } else if (wv == 2 && Wv == NB64) {   // U_ab column c = L_aa⁻¹ A_ab[:, c]
+#pragma unroll
+        for (int i = 0; i < 32; ++i) x[i] = S[i * SLD + 32 + c];
+#pragma unroll
+        for (int i = 0; i < 31; ++i) {
+#pragma unroll
+          for (int jj = i + 1; jj < 32; ++jj) x[jj] = fma(-S[jj * SLD + i], x[i], x[jj]);
+        }
+      } else if (wv == 3 && Wv == NB64) {   // L_ba row c: x U_aa = A_ba[c, :]
+#pragma unroll
+        for (int j = 0; j < 32; ++j) x[j] = S[(32 + c) * SLD + j];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          x[j] = x[j] / S[j * SLD + j];
+          bad |= !(fabs(x[j]) <= NOPIV_LMAX);
+#pragma unroll
+          for (int jj = j + 1; jj < 32; ++jj) x[jj] = fma(-x[j], S[j * SLD + jj], x[jj]);
+        }
+      }
+    }
+    if (bad) sbad = 1;
+    __syncthreads();   // every lane has read the factors of block a
+    if (lane < 32) {
+      if (wv < 2) {
+        double* D = Db + (wv == 0 ? 0 : 32 * 32);
+#pragma unroll
+        for (int jj = 0; jj < 32; ++jj) {
+          D[jj * 32 + c] = x[jj];
+          if (wv == 0 ? jj > c : jj <= c) S[jj * SLD + c] = x[jj];
+        }
+      } else if (wv == 2 && Wv == NB64) {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) S[i * SLD + 32 + c] = x[i];
+      } else if (wv == 3 && Wv == NB64) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) S[(32 + c) * SLD + j] = x[j];
+      }
+    }
+  }
+  __syncthreads();
+  if (sbad) {
+    if (t == 0) meta[b].lu = LU_REJECT;
+    return;
+  }
+  NLU_MARK(2);
+  if (Wv < NB64) return;   // a 32-wide last block: done (no TRSM follows)
+  if (NLU_STOP <= 3) return;
+
+  // ---- C. A_bb −= L_ba U_ab (one 16×16 tile per wave); U_ab, L_ba → K
+  {
+    const int tr = (wv >> 1) * 16, tc = (wv & 1) * 16;
+    d4n acc = tile32(tr, tc, [&](int i, int k) { return S[(32 + i) * SLD + k]; },
+                     [&](int k, int j) { return S[k * SLD + 32 + j]; });
+    to_K(0, 32);
+    to_K(32, 0);
+    __syncthreads();   // every wave has read L_ba / U_ab; A_bb not read before the update
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      double* p = &S[(32 + tr + g + 4 * rr) * SLD + 32 + tc + l16];
+      *p -= acc[rr];
+    }
+  }
+  __syncthreads();
+  NLU_MARK(3);
+
+  // ---- D. LU of block b
+  if (wv == 0) {
+    const int bad = wave_lu32(S, 32, rowb, colb);
+    if (lane == 0 && bad) sbad = 1;
+  }
+  __syncthreads();
+  if (sbad) {
+    if (t == 0) meta[b].lu = LU_REJECT;
+    return;
+  }
+  NLU_MARK(4);
+  to_K(32, 32);
+  if (!trsm) {   // last block: only the solves' dinv of block b
+    if (wv < 2 && lane < 32) {
+      double x[32];
+      if (wv == 0) lower_inv_col(S, 32, lane, x);
+      else upper_inv_col(S, 32, lane, x);
+      double* D = Db + DBLK + (wv == 0 ? 0 : 32 * 32);
+#pragma unroll
+      for (int jj = 0; jj < 32; ++jj) D[jj * 32 + lane] = x[jj];
+    }
+    return;
+  }
+  if (NLU_STOP <= 4) return;
+
+  // ---- E. inverses of block b (waves 0–1); T_L, T_U (waves 2–3) → binv
+  {
+    double x[32];
+    if (wv < 2 && lane < 32) {
+      if (wv == 0) lower_inv_col(S, 32, lane, x);
+      else upper_inv_col(S, 32, lane, x);
+    } else if (wv == 2) {   // T_L = L_ba · L_aa⁻¹ → binv rows 32.., cols 0..31
+      d4n acc[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        acc[q] = tile32((q >> 1) * 16, (q & 1) * 16, [&](int i, int k) { return S[(32 + i) * SLD + k]; },
+                        [&](int k, int j) { return k == j ? 1.0 : (k > j ? S[k * SLD + j] : 0.0); });
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          Bg[(32 + (q >> 1) * 16 + g + 4 * rr) * NB64 + (q & 1) * 16 + l16] = acc[q][rr];
+    } else if (wv == 3) {   // T_U = U_aa⁻¹ · U_ab → binv rows 0..31, cols 32..
+      d4n acc[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        acc[q] = tile32((q >> 1) * 16, (q & 1) * 16, [&](int i, int k) { return k >= i ? S[i * SLD + k] : 0.0; },
+                        [&](int k, int j) { return S[k * SLD + 32 + j]; });
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          Bg[((q >> 1) * 16 + g + 4 * rr) * NB64 + 32 + (q & 1) * 16 + l16] = acc[q][rr];
+    }
+    __syncthreads();   // the factors of block b have been read; T is in binv
+    if (wv < 2 && lane < 32) {
+      double* D = Db + DBLK + (wv == 0 ? 0 : 32 * 32);
+#pragma unroll
+      for (int jj = 0; jj < 32; ++jj) {
+        D[jj * 32 + lane] = x[jj];
+        if (wv == 0 ? jj > lane : jj <= lane) S[(32 + jj) * SLD + 32 + lane] = x[jj];
+      }
+    }
+  }
+  __syncthreads();
+  NLU_MARK(5);
+
+  // ---- F. off-diagonal inverse blocks (two 16×16 tiles per wave)
+  {
+    d4n acc[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int tile = (wv & 1) * 2 + q;
+      const int tr = (tile >> 1) * 16, tc = (tile & 1) * 16;
+      if (wv < 2)   // L⁻¹_ba = −L_bb⁻¹ · T_L
+        acc[q] = tile32(tr, tc,
+                        [&](int i, int k) { return k == i ? 1.0 : (k < i ? S[(32 + i) * SLD + 32 + k] : 0.0); },
+                        [&](int k, int j) { return Bg[(32 + k) * NB64 + j]; });
+      else          // U⁻¹_ab = −T_U · U_bb⁻¹
+        acc[q] = tile32(tr, tc, [&](int i, int k) { return Bg[i * NB64 + 32 + k]; },
+                        [&](int k, int j) { return k <= j ? S[(32 + k) * SLD + 32 + j] : 0.0; });
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int tile = (wv & 1) * 2 + q;
+      const int tr = (tile >> 1) * 16, tc = (tile & 1) * 16;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        if (wv < 2) S[(32 + tr + g + 4 * rr) * SLD + tc + l16] = -acc[q][rr];
+        else S[(tr + g + 4 * rr) * SLD + 32 + tc + l16] = -acc[q][rr];
+      }
+    }
+  }
+  __syncthreads();
+  NLU_MARK(6);
+  // ---- G. the packed 64×64 inverse → binv (row-major, coalesced)
+  for (int e = t; e < NB64 * NB64; e += PNT) Bg[e] = S[(e >> 6) * SLD + (e & 63)];
+  NLU_MARK(7);
+}
+
+// ---------------------------------------------------------------------------
+// TRSM of step c0 by the inverses: L21 = A21·U11⁻¹ (side 0, a 64-row strip
+// of rows ≥ c0+64) and U12 = L11⁻¹·A12 (side 1, a 64-column strip of columns
+// ≥ c0+64), with the threshold test |l| ≤ NOPIV_LMAX on L21.  One 256-thread
+// workgroup per (problem, side, strip); wave w owns 16 output rows × 64
+// columns; the operand shared by the four waves (U11⁻¹, or the A12 strip) is
+// staged in LDS.  The k-steps that meet only the zero triangle of an inverse
+// are skipped at compile time (40 of 64 per wave on average).  XCD-aware
+// order: one problem's strips are consecutive.
+// ---------------------------------------------------------------------------
+constexpr int TLD = 64 + 16;   // LDS row stride (doubles) of a staged 64×64 operand
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_trsm_kernel(double* __restrict__ K, int ld, int nmax,
+                                                       QPMeta* __restrict__ meta, int c0,
+                                                       const double* __restrict__ binv, int nst,
+                                                       int total) {
+  __shared__ double X[NB64 * TLD];
+  const int L = blockIdx.x;
+  const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
+  const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
+  const int b = logical / (2 * nst);
+  const int rem = logical - b * 2 * nst;
+  const int side = rem / nst, st = rem - side * nst;
+  const QPMeta mm = meta[b];
+  const int Np = nlu_np(mm);
+  const int R2 = Np - c0 - NB64;
+  if (mm.lu == LU_REJECT || st * 64 >= R2) return;   // workgroup-uniform
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
+  double* Kb = K + (size_t)b * nmax * ld;
+  const double* Bg = binv + (size_t)b * NB64 * NB64;
+  const int s0 = c0 + NB64 + 64 * st;          // first row (side 0) / column (side 1) of the strip
+  const int sw = min(64, R2 - 64 * st);        // 32 or 64
+  if (side == 0) {
+    // stage U11⁻¹ (upper triangle of the packed inverse, zero below)
+    for (int e = t; e < NB64 * NB64; e += 256) {
+      const int k = e >> 6, c = e & 63;
+      const double v = Bg[e];
+      X[k * TLD + c] = k <= c ? v : 0.0;
+    }
+    const int row = s0 + 16 * wv;
+    const bool wact = 16 * wv < sw;              // wave-uniform
+    double av[16];
+    if (wact) {
+      const double* Ar = Kb + (size_t)(row + l16) * ld + c0;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) av[s] = Ar[4 * s + g];
+    }
+    __syncthreads();
+    if (!wact) return;
+    d4n acc[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      acc[ct] = (d4n){0, 0, 0, 0};
+#pragma unroll
+      for (int s = 0; s < 4 * (ct + 1); ++s)
+        acc[ct] = nmfma(av[s], X[(4 * s + g) * TLD + 16 * ct + l16], acc[ct]);
+    }
+    int over = 0;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        Kb[(size_t)(row + g + 4 * rr) * ld + c0 + 16 * ct + l16] = acc[ct][rr];
+        over |= !(fabs(acc[ct][rr]) <= NOPIV_LMAX);
+      }
+    }
+    if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;   // every writer stores the same value
+  } else {
+    // stage the A12 strip: rows c0 .. c0+63, columns s0 .. s0+63 (zero past Np)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = 32 * h + (t >> 3), c8 = (t & 7) * 8;
+      const bool ok = c8 < sw;
+      const double* src = Kb + (size_t)(c0 + k) * ld + (ok ? s0 + c8 : 0);
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) X[k * TLD + c8 + u] = ok ? v[u] : 0.0;
+    }
+    // A operand: L11⁻¹ rows 16wv + l16 (unit diagonal, zero above); row tile
+    // wv needs k < 16(wv+1)
+    const int ii = 16 * wv + l16;
+    double av[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = 4 * s + g;
+      const double v = Bg[ii * NB64 + k];
+      av[s] = k == ii ? 1.0 : (k < ii ? v : 0.0);
+    }
+    __syncthreads();
+    d4n acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = (d4n){0, 0, 0, 0};
+    const int ns = 4 * (wv + 1);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s < ns) {   // wave-uniform
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = nmfma(av[s], X[(4 * s + g) * TLD + 16 * q + l16], acc[q]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (16 * q < sw) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) Kb[(size_t)(c0 + 16 * wv + g + 4 * rr) * ld + s0 + 16 * q + l16] = acc[q][rr];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Trailing update A22 −= L21·U12 (rank 64) for the rows and columns from
+// c0+64.  64×64 tiles: wave w owns tile rows 16w..16w+15 × 64 columns (4 MFMA
+// tiles); the 64×64 U12 tile is staged once in LDS.  1-D grid of nrt·nct·B
+// tiles with an XCD-aware remap: the logical tiles of one problem are
+// consecutive, so they run on one XCD and share its L2 for L21 and U12.
+// ---------------------------------------------------------------------------
+constexpr int ULD = 64 + 16;   // LDS row stride (doubles) of the staged U tile
+
+__global__ __launch_bounds__(256) void nlu_update_kernel(double* __restrict__ K, int ld, int nmax,
+                                                         const QPMeta* __restrict__ meta, int c0,
+                                                         int nrt, int nct, int total) {
+  __shared__ double U[NB64 * ULD];
+  const int L = blockIdx.x;
+  const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
+  const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
+  const int tiles = nrt * nct;
+  const int b = logical / tiles;
+  const int tile = logical - b * tiles;
+  const int rt = tile / nct, ct = tile - rt * nct;
+  const QPMeta mm = meta[b];
+  const int Np = nlu_np(mm);
+  const int R2 = Np - c0 - NB64;               // trailing rows = columns (multiple of 32)
+  if (mm.lu == LU_REJECT || rt * 64 >= R2 || ct * 64 >= R2) return;   // workgroup-uniform
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
+  double* Kb = K + (size_t)b * nmax * ld;
+  const int cbase = c0 + NB64 + ct * 64;
+  const int cend = c0 + NB64 + R2;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    // stage U12[k][cbase .. cbase+63]: thread → (row k, 8 contiguous columns)
+    const int k = 32 * h + (t >> 3), c8 = (t & 7) * 8;
+    const bool ok = cbase + c8 < cend;   // 32-aligned halves: all-or-nothing
+    const double* src = Kb + (size_t)(c0 + k) * ld + (ok ? cbase + c8 : 0);
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = src[u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) U[k * ULD + c8 + u] = ok ? v[u] : 0.0;
+  }
+  const int rbase = c0 + NB64 + rt * 64 + 16 * wv;
+  const bool wact = rt * 64 + 16 * wv < R2;   // wave-uniform
+  const int nq = min(4, (R2 - ct * 64) >> 4);
+  double a[NB64 / 4];
+  d4n acc[4];
+  if (wact) {
+    const double* arow = Kb + (size_t)(rbase + l16) * ld + c0;
+#pragma unroll
+    for (int s = 0; s < NB64 / 4; ++s) a[s] = -arow[4 * s + g];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int cq = cbase + 16 * min(q, nq - 1) + l16;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) acc[q][rr] = Kb[(size_t)(rbase + g + 4 * rr) * ld + cq];
+    }
+  }
+  __syncthreads();
+  if (!wact) return;
+#pragma unroll
+  for (int s = 0; s < NB64 / 4; ++s) {
+    double bq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bq[q] = U[(4 * s + g) * ULD + 16 * q + l16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = nmfma(a[s], bq[q], acc[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q < nq) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) Kb[(size_t)(rbase + g + 4 * rr) * ld + cbase + 16 * q + l16] = acc[q][rr];
+    }
+  }
+}
+
+}  // namespace
+
+// No-pivot blocked LU of every ROUTE_BLOCKED problem: per 64-column block a
+// diagonal launch (B workgroups), a TRSM launch and a rank-64 trailing-update
+// launch.  Sized by h.blocked_npmax (the read-back of the metadata after the
+// assembly).
+void qp_nopiv_factor(Handle& h, double* dinv) {
+  const int npmax = h.blocked_npmax;
+  if (npmax == 0) return;
+  const int B = (int)h.batch;
+  const size_t dstride = dinv_stride(h.nmax);
+  double* K = h.K.as<double>();
+  int32_t* perm = h.ipiv.as<int32_t>();
+  QPMeta* meta = h.meta.as<QPMeta>();
+  h.binv.ensure((size_t)B * NB64 * NB64 * sizeof(double));
+  double* binv = h.binv.as<double>();
+  for (int c0 = 0; c0 < npmax; c0 += NB64) {
+    hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv,
+                       dstride, meta, c0, binv);
+    DOPT_CHECK_HIP(hipGetLastError());
+    const int R2 = npmax - c0 - NB64;
+    if (R2 <= 0) break;
+    const int nt = (R2 + 63) / 64;
+    const long long tot_s = 2LL * nt * B;
+    if (tot_s > 0x7fffffffLL) throw Error(-1, "no-pivot LU: TRSM grid too large");
+    hipLaunchKernelGGL(nlu_trsm_kernel, dim3((unsigned)tot_s), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta,
+                       c0, binv, nt, (int)tot_s);
+    DOPT_CHECK_HIP(hipGetLastError());
+    const long long total = (long long)nt * nt * B;
+    if (total > 0x7fffffffLL) throw Error(-1, "no-pivot LU: trailing-update grid too large");
+    hipLaunchKernelGGL(nlu_update_kernel, dim3((unsigned)total), dim3(256), 0, h.stream, K, h.ld, h.nmax,
+                       meta, c0, nt, nt, (int)total);
+    DOPT_CHECK_HIP(hipGetLastError());
+  }
+}
+
+}  // namespace dopt

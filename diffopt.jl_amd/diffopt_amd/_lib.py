@@ -10,9 +10,6 @@ import os
 
 LIB_NAME = "libdiffopt_mi355x.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
-if os.environ.get("DOPT_LIB_VARIANT"):
-    # tuning builds (libdiffopt_mi355x.<variant>.so next to the product library)
-    LIB_PATH = LIB_PATH[:-3] + "." + os.environ["DOPT_LIB_VARIANT"] + ".so"
 
 DOPT_KIND_QP = 0
 DOPT_KIND_CONIC = 1
@@ -36,7 +33,6 @@ SIGNATURES = {
     "dopt_last_error": (ctypes.c_char_p, [_h]),
     "dopt_set_stream": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_set_memory": (ctypes.c_int, [_h, ctypes.c_int32]),
-    "dopt_set_qp_fast_max": (ctypes.c_int, [_h, ctypes.c_int32]),
     "dopt_qp_set": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 7),
     "dopt_qp_factor": (ctypes.c_int, [_h]),
     "dopt_qp_reverse": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_void_p]),
@@ -53,14 +49,17 @@ SIGNATURES = {
     "dopt_conic_reverse": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 5),
     "dopt_get_info": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_get_iterative": (ctypes.c_int, [_h, ctypes.c_void_p]),
+    "dopt_qp_get_kept": (ctypes.c_int, [_h, ctypes.c_void_p]),
+    "dopt_qp_get_lu_kind": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_get_system_size": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_last_time": (ctypes.c_double, [_h]),
     "dopt_set_profiling": (ctypes.c_int, [_h, ctypes.c_int32]),
     "dopt_get_phase_times": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]),
     "dopt_phase_name": (ctypes.c_char_p, [ctypes.c_int32]),
-    "dopt_debug_stamps": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_int32]),
 }
-NUM_PHASES = 12
+NUM_PHASES = 11
+ABI_VERSION = 2
+LU_KIND_LSQR, LU_KIND_NOPIV, LU_KIND_PIVOT = 0, 1, 2
 
 
 class EngineUnavailable(RuntimeError):
@@ -102,6 +101,9 @@ def load():
     except ImportError:
         pass
     lib = ctypes.CDLL(LIB_PATH)
+    if lib.dopt_abi_version() != ABI_VERSION:
+        raise EngineUnavailable(f"{LIB_PATH}: ABI version {lib.dopt_abi_version()}, "
+                                f"expected {ABI_VERSION} (rebuild the engine)")
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res

@@ -26,6 +26,21 @@ from ._arrays import _is_torch as _is_t
 LE, EQ = "LessThan", "EqualTo"
 
 
+def _check_out(o, shape, device):
+    """A caller-supplied output buffer must be exactly what the kernels write:
+    float64, C-contiguous, `shape`, and in the memory kind of the call."""
+    if _is_t(o):
+        import torch
+        ok = (o.dtype == torch.float64 and o.is_contiguous() and tuple(o.shape) == tuple(shape)
+              and o.is_cuda == bool(device))
+    else:
+        ok = (not device and isinstance(o, np.ndarray) and o.dtype == np.float64
+              and o.flags.c_contiguous and o.shape == tuple(shape))
+    if not ok:
+        raise TypeError(f"output buffer must be a C-contiguous float64 {'CUDA tensor' if device else 'numpy array'} "
+                        f"of shape {tuple(shape)}")
+
+
 class QPBatch:
     """Batched QP sensitivity engine (C-ABI handle wrapper)."""
 
@@ -160,6 +175,8 @@ class QPBatch:
                 vector(db, (B, p)) if (db is not None and p) else None]
         o1 = out_rev if out_rev is not None else self._out(dev)
         o2 = out_fwd if out_fwd is not None else self._out(dev)
+        for o in (o1, o2):
+            _check_out(o, (B, self.L), dev)
         rc = self.lib.dopt_qp_forward_reverse(self.h, *[st.ptr(a) for a in args],
                                               st.ptr(o1), st.ptr(o2))
         _lib.check(rc, self.h, singular_ok)
@@ -210,10 +227,19 @@ class QPBatch:
     def last_time(self):
         return self.lib.dopt_last_time(self.h)
 
-    def set_fast_max(self, fast_max):
-        """Reduced KKT sizes ≤ fast_max (0..512) use the fused per-problem
-        kernel, larger ones the blocked step path (dopt_set_qp_fast_max)."""
-        _lib.check(self.lib.dopt_set_qp_fast_max(self.h, int(fast_max)), self.h)
+    def kept(self):
+        """(B, m) bool mask of the inequality rows kept in the factorised
+        system (False: eliminated exactly, λ_i == 0 and (Gz − h)_i != 0)."""
+        buf = np.zeros((self.batch, self.m), dtype=np.int8)
+        _lib.check(self.lib.dopt_qp_get_kept(self.h, buf.ctypes.data), self.h)
+        return buf.astype(bool)
+
+    def lu_kind(self):
+        """Per-problem factorisation kind of the last factorisation:
+        _lib.LU_KIND_LSQR / LU_KIND_NOPIV / LU_KIND_PIVOT."""
+        buf = np.zeros(self.batch, dtype=np.int8)
+        _lib.check(self.lib.dopt_qp_get_lu_kind(self.h, buf.ctypes.data), self.h)
+        return buf
 
     def set_profiling(self, on=True):
         _lib.check(self.lib.dopt_set_profiling(self.h, int(bool(on))), self.h)

@@ -5,6 +5,8 @@ a seeded permutation makes ⌊φ·m⌋ rows active (s_i = 0, λ_i ~ U(0.5,1.5)),
 others inactive (λ_i = 0, s_i ~ −U(0.5,1.5)); ν ~ N(0,1); h = Gz − s; b = Az;
 q = −(Qz + Gᵀλ + Aᵀν).  Reverse seed dl/dz ~ N(0,1); forward tangents
 dq, dh, db ~ N(0,1) (dQ = dG = dA = 0 unless `dense_tangents`).
+`lam_eps` > 0 gives the inactive rows λ_i = lam_eps instead of 0 (interior-
+point-like duals: no row is eliminated exactly, N' = n + m + p).
 Seeds: 20250307 + config index.  No solver is needed: (z, λ, ν) is the exact
 primal–dual optimum of the generated problem.
 """
@@ -27,7 +29,7 @@ CONIC_CONFIGS = {
 }
 
 
-def qp_numpy(batch, n, m, p, phi, seed, dense_tangents=False):
+def qp_numpy(batch, n, m, p, phi, seed, dense_tangents=False, lam_eps=0.0):
     rng = np.random.default_rng(seed)
     out = {k: [] for k in ["Q", "q", "G", "h", "A", "b", "z", "lam", "nu", "dl_dz",
                            "dq", "dh", "db", "dQ", "dG", "dA"]}
@@ -39,7 +41,7 @@ def qp_numpy(batch, n, m, p, phi, seed, dense_tangents=False):
         A = rng.standard_normal((p, n)) / math.sqrt(n)
         z = rng.standard_normal(n)
         perm = rng.permutation(m)
-        lam = np.zeros(m)
+        lam = np.full(m, float(lam_eps))
         s = np.zeros(m)
         act, ina = perm[:k_act], perm[k_act:]
         lam[act] = rng.uniform(0.5, 1.5, size=k_act)
@@ -69,7 +71,7 @@ def qp_config_numpy(cfg, batch=None, **kw):
     return qp_numpy(batch or c["batch"], c["n"], c["m"], c["p"], c["phi"], SEED0 + cfg, **kw)
 
 
-def qp_torch(batch, n, m, p, phi, seed, device="cuda", rank_offset=0):
+def qp_torch(batch, n, m, p, phi, seed, device="cuda", rank_offset=0, lam_eps=0.0):
     """Same construction on the GPU with torch (for bench-sized batches).
     `rank_offset` shifts the seed so every rank gets distinct problems."""
     import torch
@@ -87,7 +89,8 @@ def qp_torch(batch, n, m, p, phi, seed, device="cuda", rank_offset=0):
     perm = torch.argsort(keys, dim=1)
     act = torch.zeros(batch, m, dtype=torch.bool, device=device)
     act.scatter_(1, perm[:, :k_act], True)
-    lam = torch.where(act, 0.5 + torch.rand(batch, m, generator=g, **f64), torch.zeros((), **f64))
+    lam = torch.where(act, 0.5 + torch.rand(batch, m, generator=g, **f64),
+                      torch.full((), float(lam_eps), **f64))
     s = torch.where(act, torch.zeros((), **f64), -(0.5 + torch.rand(batch, m, generator=g, **f64)))
     nu = torch.randn(batch, p, generator=g, **f64)
     h = torch.einsum("bmn,bn->bm", G, z) - s

@@ -53,7 +53,7 @@ extern "C" {
 #define DOPT_CONE_SOC 3          /* MOI.SecondOrderCone                       */
 #define DOPT_CONE_PSD_TRI 4      /* MOI.PositiveSemidefiniteConeTriangle      */
 
-#define DOPT_ABI_VERSION 1
+#define DOPT_ABI_VERSION 2
 
 typedef struct dopt_handle dopt_handle;
 
@@ -74,13 +74,6 @@ int dopt_abi_version(void);
  * stream) so the engine's kernels are ordered after that work. */
 int dopt_set_stream(dopt_handle* h, void* stream);
 int dopt_set_memory(dopt_handle* h, int32_t mem);
-/* QP factorisation path threshold: problems whose reduced KKT size is
- * ≤ fast_max (0..512, default 0, env DOPT_FAST_MAX) use the fused
- * one-workgroup-per-problem kernel; larger ones (≤ 1536) the blocked step
- * path that spreads each LU over the whole GPU; beyond that a generic kernel.
- * Results agree to rounding; this is a performance setting (no reference
- * counterpart — the reference always calls UMFPACK, QuadraticProgram.jl:490). */
-int dopt_set_qp_fast_max(dopt_handle* h, int32_t fast_max);
 
 /* ---- QuadraticProgram ------------------------------------------------------
  * Problem data + primal-dual point.  Replaces `_gradient_cache`'s inputs
@@ -110,7 +103,12 @@ int dopt_qp_set_csc(dopt_handle* h,
  * select the solve branch per problem (`iterative = norm(Q) ≈ 0`, :333/:436)
  * and LU-factorise it ONCE (the reference re-factorises per call, :490).
  * Rows with λ_i == 0 and (Gz−h)_i != 0 are eliminated exactly (their
- * unknowns decouple).  Optional: dopt_qp_reverse/forward factor on demand. */
+ * unknowns decouple).  Pivoting: the factors of a problem are accepted
+ * without row interchanges when every multiplier satisfies |l_ij| ≤ 10 (the
+ * diagonal passes UMFPACK's threshold test with tolerance 0.1); otherwise the
+ * problem is factorised with partial pivoting (env DOPT_LU=0: partial
+ * pivoting for every problem).  Optional: dopt_qp_reverse/forward factor on
+ * demand. */
 int dopt_qp_factor(dopt_handle* h);
 /* reverse_differentiate! (QuadraticProgram.jl:316-351):
  * out[b] = [dz (n) | dλ (m) | dν (p)] = −LHS \ [dl_dz; 0; 0]. */
@@ -164,7 +162,11 @@ int dopt_conic_set_csc(dopt_handle* h, const int64_t* A_colptr, const int64_t* A
                        const double* A_nzval, int64_t A_nnz, const double* b, const double* c,
                        const double* x, const double* s, const double* y,
                        const int32_t* cone_desc, int32_t ncones);
-/* _gradient_cache (ConicProgram.jl:172-255): v = y − s, Dπ(v), π(v), M. */
+/* _gradient_cache (ConicProgram.jl:172-255): v = y − s, Dπ(v), π(v), M.
+ * Returns −1 with the reference's message ("Some constraints are missing a
+ * value for the `ConstraintDualStart` attribute." / `ConstraintPrimalStart`,
+ * ConicProgram.jl:186-196) when some y or s entry is NaN (the reference's
+ * marker of a missing start). */
 int dopt_conic_factor(dopt_handle* h);
 /* forward_differentiate! (ConicProgram.jl:257-334): out[b] = [du | dv | dw]
  * (n+m+1) = lsqr(M, [dAᵀvp + dc; −dA x + db; −dc·x − db·vp]) (0 if the RHS is
@@ -186,14 +188,24 @@ int dopt_conic_reverse(dopt_handle* h, const double* dx, double* out_g,
 int dopt_get_info(dopt_handle* h, int32_t* info);
 /* per-problem `iterative` branch flags (QP; 1 = LSQR branch). */
 int dopt_get_iterative(dopt_handle* h, int8_t* flags);
+/* QP kept-row mask of the last factorisation: kept[b·m + i] = 1 if
+ * inequality row i of problem b stays in the factorised system, 0 if it was
+ * eliminated exactly (λ_i == 0 and (Gz − h)_i != 0, with Gz − h summed in
+ * Julia's sparse mul! order) — the bit-exact discrete selection. */
+int dopt_qp_get_kept(dopt_handle* h, int8_t* kept);
+/* QP factorisation kind per problem of the last factorisation. */
+#define DOPT_LU_KIND_LSQR 0      /* `iterative` branch (no factorisation)        */
+#define DOPT_LU_KIND_NOPIV 1     /* no-pivot LU passed the threshold test        */
+#define DOPT_LU_KIND_PIVOT 2     /* partial pivoting                             */
+int dopt_qp_get_lu_kind(dopt_handle* h, int8_t* kinds);
 /* per-problem size of the factorised (reduced) KKT system (QP) or LSQR
  * iteration count of the last solve (CONIC). */
 int dopt_get_system_size(dopt_handle* h, int32_t* sizes);
 /* Per-phase GPU time, measured with HIP events on the handle's stream around
  * each phase's kernels while profiling is on (off by default). */
-#define DOPT_PHASE_QP_PREPARE 0   /* branch flag, s = Gz − h, row elimination   */
-#define DOPT_PHASE_QP_ASSEMBLE 1  /* KKT matrix assembly                         */
-#define DOPT_PHASE_QP_LU 2        /* blocked LU (MFMA trailing update)           */
+#define DOPT_PHASE_QP_ASSEMBLE 0  /* branch flag, s = Gz − h, elimination, KKT   */
+#define DOPT_PHASE_QP_LU 1        /* no-pivot blocked LU (+ generic LU)          */
+#define DOPT_PHASE_QP_LU_PIVOT 2  /* partial-pivoting LU (rejected problems)     */
 #define DOPT_PHASE_QP_RHS 3       /* forward/reverse right-hand sides            */
 #define DOPT_PHASE_QP_SOLVE 4     /* triangular solves                           */
 #define DOPT_PHASE_QP_LSQR 5      /* LSQR (norm(Q) == 0 branch)                  */
@@ -202,19 +214,13 @@ int dopt_get_system_size(dopt_handle* h, int32_t* sizes);
 #define DOPT_PHASE_CONIC_RHS 8    /* conic right-hand sides                      */
 #define DOPT_PHASE_CONIC_LSQR 9   /* conic LSQR on M                             */
 #define DOPT_PHASE_CONIC_OUTPUT 10
-#define DOPT_PHASE_QP_FUSED 11    /* fused prepare+assemble+LU+both solves      */
-#define DOPT_NUM_PHASES 12
+#define DOPT_NUM_PHASES 11
 int dopt_set_profiling(dopt_handle* h, int32_t on);
 /* Accumulated milliseconds and launch counts per phase since the last call
  * (arrays of length nphases ≤ DOPT_NUM_PHASES); resets the accumulators. */
 int dopt_get_phase_times(dopt_handle* h, double* ms, int32_t* counts,
                          int32_t nphases);
 const char* dopt_phase_name(int32_t phase);
-/* Diagnostic: in-kernel cycle stamps of the fused QP kernel, summed over
- * workgroups, when the process runs with DOPT_STAMPS=1 (slots: prepare,
- * assemble, LU panel, LU L11⁻¹, LU trailing update, reverse, forward).
- * Returns the number of slots written (0 if stamps are off); resets them. */
-int dopt_debug_stamps(dopt_handle* h, int64_t* out, int32_t n);
 /* wall time (s) of the last forward/reverse call, incl. any factorisation it
  * triggered — the DifferentiateTimeSec analogue (diff_opt.jl:256-266). */
 double dopt_last_time(const dopt_handle* h);

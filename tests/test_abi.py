@@ -49,7 +49,7 @@ def test_abi_version_and_errors_without_device():
     if not os.path.exists(_lib.LIB_PATH):
         pytest.skip("library not built")
     lib = _lib.load()
-    assert lib.dopt_abi_version() == 1
+    assert lib.dopt_abi_version() == _lib.ABI_VERSION
     # null handle paths never touch the device
     assert lib.dopt_last_error(None) == b"null handle"
     assert lib.dopt_destroy(None) == 0

@@ -1,8 +1,15 @@
 """ConicProgram sensitivity path on the GPU (via the C-ABI) against the CPU
 oracle and the reference's own fixtures (test/conic_program.jl, see
-tests/golden/make_golden.py).  Tolerance: north_star's 1e-6 relative
-Frobenius against the oracle; the fixture tolerances for the reference's
-expected values."""
+tests/golden/make_golden.py).
+
+Parity bar: north_star's 1e-6 relative Frobenius against the oracle, per
+problem and per output.  One exception, counted and capped per test: when M
+is numerically singular and LSQR stops at maxiter (istop 7 — the config-4
+bench shape, the PSD+POS fixture), the oracle itself moves by ≫ 1e-6 under a
+1-ulp perturbation of its inputs, so no implementation can meet 1e-6; such
+an output is held to 10× the oracle's own 1-ulp spread instead ("relaxed").
+Every test reports how many outputs were judged under the relaxed bar and
+asserts its cap (0 for the well-posed shapes)."""
 
 import json
 import os
@@ -15,6 +22,7 @@ from oracle import conic as ocn
 pytestmark = pytest.mark.gpu
 RTOL = 1e-6
 HERE = os.path.dirname(os.path.abspath(__file__))
+SEED0 = 20250307
 
 
 def relfro(a, b):
@@ -34,27 +42,46 @@ def relcomb(a, b, scale):
     return np.linalg.norm(a - b) / den if den > 0 else np.linalg.norm(a)
 
 
-def noise_envelope(solve, args, ref, trials=4):
-    """Rounding-noise envelope of the oracle at one input: the largest relative
-    change of its output when the right-hand side data is perturbed by one ulp
-    (relative 2⁻⁵², seeded).  For a singular M whose LSQR stops at maxiter
-    (istop 7 — e.g. the PSD+POS fixture, cond(M) ≈ 8e16) this is ≫ 1e-6: the
-    reference itself then returns a different vector under another BLAS or
-    summation order, so no implementation can meet 1e-6 there.  The bar for
-    such inputs is "within 10× the oracle's own 1-ulp spread" (plus the
-    reference fixture's tolerance, asserted separately)."""
+class Tally:
+    """Counts the outputs judged under the relaxed (1-ulp envelope) bar."""
+
+    def __init__(self, name):
+        self.name, self.total, self.relaxed, self.worst = name, 0, 0, 0.0
+
+    def check(self, err, envelope_fn, what):
+        """err ≤ RTOL, or (only if the oracle's own envelope exceeds RTOL/10)
+        err ≤ 10 × envelope.  `envelope_fn` is evaluated lazily."""
+        self.total += 1
+        self.worst = max(self.worst, err)
+        if err <= RTOL:
+            return
+        env = envelope_fn()
+        assert env > RTOL / 10, (what, err, env)
+        assert err <= 10.0 * env, (what, err, env)
+        self.relaxed += 1
+
+    def report(self, cap):
+        print(f"[parity] {self.name}: {self.total} outputs, {self.relaxed} under the relaxed "
+              f"envelope bar (cap {cap}), worst error {self.worst:.2e}")
+        log = os.environ.get("DOPT_PARITY_LOG")
+        if log:
+            with open(log, "a") as f:
+                f.write(json.dumps(dict(test=self.name, outputs=self.total, relaxed=self.relaxed,
+                                        cap=cap, worst=self.worst)) + "\n")
+        if not os.environ.get("DOPT_PARITY_CALIBRATE"):
+            assert self.relaxed <= cap, (self.name, self.relaxed, cap)
+
+
+def envelope(solve, args, ref, metric, trials=3):
+    """Largest change of the oracle's output when its right-hand-side data is
+    perturbed by one ulp (relative 2⁻⁵², seeded)."""
     rng = np.random.default_rng(7)
     worst = 0.0
     for _ in range(trials):
         pert = [np.asarray(a, float) * (1.0 + 2.0 ** -52 * rng.standard_normal(np.shape(a)))
                 for a in args]
-        worst = max(worst, relfro(solve(*pert), ref))
+        worst = max(worst, metric(solve(*pert), ref))
     return worst
-
-
-def parity_bar(solve, args, ref):
-    env = noise_envelope(solve, args, ref)
-    return RTOL if env <= RTOL / 10 else 10.0 * env
 
 
 @pytest.fixture(scope="module")
@@ -64,6 +91,7 @@ def ConicBatch():
 
 
 FX = json.load(open(os.path.join(HERE, "golden", "conic_fixtures.json")))
+FX_CAP = {"conic_psd_pos": 2}   # LSQR stops at maxiter on cond(M) ≈ 8e16
 
 
 @pytest.mark.parametrize("fx", FX, ids=[f["name"] for f in FX])
@@ -76,6 +104,8 @@ def test_fixture_forward_reverse(ConicBatch, fx):
     e = ConicBatch(1, n, cones)
     e.set(A[None], np.array(fx["b"])[None], c[None], np.array(fx["x"])[None],
           np.array(fx["s"])[None], np.array(fx["y"])[None])
+    tally = Tally(fx["name"])
+    x = np.array(fx["x"], dtype=float)
     for t in fx["forward"]:
         dA = np.array(t["dA"], dtype=float)
         out, dx = e.forward(dA[None], np.array(t["db"])[None], np.array(t["dc"])[None])
@@ -86,25 +116,26 @@ def test_fixture_forward_reverse(ConicBatch, fx):
         def fsolve(dA_, db_, dc_):
             _, a, b_, c_ = ocn.forward_differentiate(cache, dA_, db_, dc_)
             return np.concatenate([a, b_, [c_]])
-        bar = parity_bar(fsolve, [dA, t["db"], t["dc"]], ref)
-        assert relfro(out[0], ref) <= bar
-        x = np.array(fx["x"], dtype=float)
+        env = lambda: envelope(fsolve, [dA, t["db"], t["dc"]], ref, relfro)
+        tally.check(relfro(out[0], ref), env, "forward")
         sol = np.linalg.norm(ref)
-        assert relcomb(dx[0], odx, sol * (1 + np.linalg.norm(x))) <= bar
+        tally.check(relcomb(dx[0], odx, sol * (1 + np.linalg.norm(x))), env, "dx")
     for t in fx["reverse"]:
         g, dA, db, dc = e.reverse(np.array(t["dx"], dtype=float)[None])
         np.testing.assert_allclose(db[0][t["rows"]], t["db"], atol=t["atol"], rtol=t["rtol"])
         og, _ = ocn.reverse_differentiate(cache, t["dx"])
-        bar = parity_bar(lambda dx_: ocn.reverse_differentiate(cache, dx_)[0], [t["dx"]], og)
-        assert relfro(g[0], og) <= bar
+        tally.check(relfro(g[0], og), lambda: envelope(
+            lambda dx_: ocn.reverse_differentiate(cache, dx_)[0], [t["dx"]], og, relfro), "reverse")
     e.close()
+    tally.report(FX_CAP.get(fx["name"], 0))
 
 
 def _oracle_outputs(cache, dA, db, dc, dx):
-    odx, du, dv, dw = ocn.forward_differentiate(cache, dA, db, dc)
-    og, _ = ocn.reverse_differentiate(cache, dx)
+    (odx, du, dv, dw), fi = ocn.forward_differentiate(cache, dA, db, dc, return_info=True)
+    (og, _), ri = ocn.reverse_differentiate(cache, dx, return_info=True)
     odA, odb, odc = ocn.reverse_outputs(cache, og)
-    return dict(fwd=np.concatenate([du, dv, [dw]]), dx=odx, g=og, dA=odA, db=odb, dc=odc)
+    return dict(fwd=np.concatenate([du, dv, [dw]]), dx=odx, g=og, dA=odA, db=odb, dc=odc,
+                info=(fi, ri))
 
 
 def _errors(got, ref, cache):
@@ -120,62 +151,88 @@ def _errors(got, ref, cache):
                 dc=relcomb(got["dc"], ref["dc"], ng * (1 + nx)))
 
 
-def _synthetic_check(ConicBatch, B, n, cones, seed):
-    """GPU vs oracle per problem and output.  Bar: RTOL, or 10× the oracle's
-    own 1-ulp rounding envelope where that exceeds RTOL/10 (LSQR on the
-    singular M — see noise_envelope)."""
+def _synthetic_check(ConicBatch, B, n, cones, seed, name, cap=0, trials=3, want_dA=True):
+    """GPU vs oracle per problem and output (tallied: RTOL, or the relaxed
+    envelope bar where the oracle's own 1-ulp spread exceeds RTOL/10).
+    Returns (tally, engine LSQR iteration counts fwd, rev, oracle infos)."""
     from diffopt_amd.synthetic import conic_numpy
     d = conic_numpy(B, n, cones, seed)
     e = ConicBatch(B, n, cones)
     e.set(d["A"], d["b"], d["c"], d["x"], d["s"], d["y"])
     out, dx = e.forward(d["dA"], d["db"], d["dc"])
-    g, dA, db, dc = e.reverse(d["dx"])
+    it_f = e.iterations()
+    g, dA, db, dc = e.reverse(d["dx"], want_dA=want_dA)
+    it_r = e.iterations()
     e.close()
-    rng = np.random.default_rng(7)
-    worst = {}
+    tally = Tally(name)
+    infos = []
     for b in range(B):
         cache = ocn.Cache(d["A"][b], d["b"][b], d["c"][b], d["x"][b], d["s"][b], d["y"][b], cones)
         args = [d["dA"][b], d["db"][b], d["dc"][b], d["dx"][b]]
         ref = _oracle_outputs(cache, *args)
-        got = dict(fwd=out[b], dx=dx[b], g=g[b], dA=dA[b], db=db[b], dc=dc[b])
+        infos.append(ref["info"])
+        got = dict(fwd=out[b], dx=dx[b], g=g[b], dA=dA[b] if want_dA else ref["dA"], db=db[b], dc=dc[b])
         err = _errors(got, ref, cache)
-        env = dict.fromkeys(err, 0.0)
-        for _ in range(3):
-            pert = [a * (1.0 + 2.0 ** -52 * rng.standard_normal(a.shape)) for a in args]
-            pe = _errors(_oracle_outputs(cache, *pert), ref, cache)
-            env = {k: max(env[k], pe[k]) for k in env}
+        env_cache = {}
+
+        def env_of(k):
+            if not env_cache:   # one set of perturbed oracle solves serves every output
+                rng = np.random.default_rng(7)
+                env_cache.update(dict.fromkeys(err, 0.0))
+                for _ in range(trials):
+                    pert = [a * (1.0 + 2.0 ** -52 * rng.standard_normal(a.shape)) for a in args]
+                    pe = _errors(_oracle_outputs(cache, *pert), ref, cache)
+                    env_cache.update({kk: max(env_cache[kk], pe[kk]) for kk in env_cache})
+            return env_cache[k]
         for k in err:
-            bar = RTOL if env[k] <= RTOL / 10 else 10.0 * env[k]
-            assert err[k] <= bar, (b, k, err[k], env[k])
-            worst[k] = max(worst.get(k, 0.0), err[k])
-    return worst
+            tally.check(err[k], lambda k=k: env_of(k), (b, k))
+    tally.report(cap)
+    return tally, it_f, it_r, infos
 
 
 def test_well_posed_batch(ConicBatch):
-    # m > n (unique primal) and LSQR converging (istop 1): the oracle's own
-    # envelope is ~1e-6 here (LSQR stops at a √eps-relative residual), so the
-    # GPU must agree to within ~1e-5
-    w = _synthetic_check(ConicBatch, 2, 100, [(3, 10)] * 20, 21)
-    assert max(w.values()) <= 1e-5, w
+    # m > n (unique primal) and LSQR converging (istop 1)
+    _synthetic_check(ConicBatch, 2, 100, [(3, 10)] * 20, 21, "well-posed SOC")
 
 
 def test_mixed_cones_batch(ConicBatch):
-    _synthetic_check(ConicBatch, 6, 30, [(0, 3), (1, 10), (3, 6), (2, 4), (4, 6)], 11)
+    _synthetic_check(ConicBatch, 6, 30, [(0, 3), (1, 10), (3, 6), (2, 4), (4, 6)], 11, "mixed cones",
+                     cap=36)
 
 
 def test_soc_only_batch(ConicBatch):
-    _synthetic_check(ConicBatch, 4, 40, [(3, 5)] * 8, 12)
+    _synthetic_check(ConicBatch, 4, 40, [(3, 5)] * 8, 12, "SOC only", cap=24)
 
 
 def test_psd_blocks_batch(ConicBatch):
-    _synthetic_check(ConicBatch, 3, 25, [(4, 10), (4, 15), (1, 5)], 13)
+    _synthetic_check(ConicBatch, 3, 25, [(4, 10), (4, 15), (1, 5)], 13, "PSD blocks", cap=18)
 
 
-def test_config4_shape_small_batch(ConicBatch):
-    # BASELINE config 4 shape (n=500, 20 SOCs; cone dim 50 so m = 1000 > n and
-    # the instance is non-degenerate) at batch 2
-    w = _synthetic_check(ConicBatch, 2, 500, [(3, 50)] * 20, 14)
-    assert max(w.values()) <= 1e-5, w
+def test_config4_nondegenerate_shape(ConicBatch):
+    # config-4 structure (n=500, 20 SOCs) with cone dim 50, so m = 1000 > n and
+    # M is non-singular: LSQR converges and the strict bar holds everywhere
+    _synthetic_check(ConicBatch, 2, 500, [(3, 50)] * 20, 14, "config-4 structure, m=1000")
+
+
+def test_config4_bench_shape(ConicBatch):
+    """The exact config-4 bench shape and generator (20 × SOC(25), n = 500,
+    seed SEED0 + 4: the first two problems of bench.py's batch).  M is
+    singular there: both LSQR directions stop at maxiter = N = 1001 (istop 7)
+    in the engine and in the oracle alike; outputs are judged under the
+    tallied bar."""
+    tally, it_f, it_r, infos = _synthetic_check(ConicBatch, 2, 500, [(3, 25)] * 20, SEED0 + 4,
+                                                "config-4 bench shape", cap=12, trials=2)
+    assert (it_f == 1001).all() and (it_r == 1001).all()
+    assert all(fi == (1001, 7) and ri == (1001, 7) for fi, ri in infos)
+
+
+def test_config5_full_shape(ConicBatch):
+    """The full config-5 SDP shape (10 × PSD(50): m = 12 750, n = 500, seed
+    SEED0 + 5: bench.py's first problem), batch 1 — 13 251 unknowns, the split
+    (row-block) LSQR path.  dA is not materialised (51 MB per problem)."""
+    tally, it_f, it_r, infos = _synthetic_check(ConicBatch, 1, 500, [(4, 1275)] * 10, SEED0 + 5,
+                                                "config-5 full shape", cap=6, trials=1, want_dA=False)
+    print(f"[parity] config-5 LSQR iterations: engine fwd {it_f[0]} rev {it_r[0]}, oracle {infos[0]}")
 
 
 def test_zero_rhs_gives_zero(ConicBatch):
@@ -191,10 +248,30 @@ def test_zero_rhs_gives_zero(ConicBatch):
     e.close()
 
 
-def test_csc_staging_matches_dense(ConicBatch):
+def test_missing_starts_raise(ConicBatch):
+    """NaN in y or s (the reference's marker of a missing start) fails the
+    factorisation with ConicProgram.jl:186-196's messages, dual first."""
+    from diffopt_amd import EngineError
+    from diffopt_amd.synthetic import conic_numpy
+    cones = [(1, 6), (3, 4)]
+    d = conic_numpy(2, 8, cones, 15)
+    for key, word in (("y", "ConstraintDualStart"), ("s", "ConstraintPrimalStart")):
+        bad = dict(d)
+        bad[key] = d[key].copy()
+        bad[key][1, 7] = np.nan
+        e = ConicBatch(2, 8, cones)
+        e.set(bad["A"], bad["b"], bad["c"], bad["x"], bad["s"], bad["y"])
+        with pytest.raises(EngineError, match=word):
+            e.factor()
+        with pytest.raises(EngineError, match=word):
+            e.reverse(d["dx"])
+        e.close()
+
+
+def test_csc_staging_matches_dense_and_oracle(ConicBatch):
     """dopt_conic_set_csc (A_moi as Julia CSC arrays, 1-based, densified on the
-    device) is bit-identical to dopt_conic_set with the same dense A; a
-    malformed colptr raises."""
+    device): against the oracle on the same sparse problems, and bit-identical
+    to dopt_conic_set with the dense A; a malformed colptr raises."""
     import scipy.sparse as sp
     from diffopt_amd import EngineError
     from diffopt_amd.synthetic import conic_numpy
@@ -215,6 +292,20 @@ def test_csc_staging_matches_dense(ConicBatch):
         e.close()
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
+    tally = Tally("CSC staging")
+    for b in range(3):
+        cache = ocn.Cache(A[b], d["b"][b], d["c"][b], d["x"][b], d["s"][b], d["y"][b], cones)
+        _, du, dv, dw = ocn.forward_differentiate(cache, None, d["db"][b], d["dc"][b])
+        og, _ = ocn.reverse_differentiate(cache, d["dx"][b])
+        ref = np.concatenate([du, dv, [dw]])
+        def fsolve(db_, dc_):
+            _, a, v, w = ocn.forward_differentiate(cache, None, db_, dc_)
+            return np.concatenate([a, v, [w]])
+        tally.check(relfro(outs[1][0][b], ref),
+                    lambda: envelope(fsolve, [d["db"][b], d["dc"][b]], ref, relfro), (b, "fwd"))
+        tally.check(relfro(outs[1][2][b], og), lambda: envelope(
+            lambda dx_: ocn.reverse_differentiate(cache, dx_)[0], [d["dx"][b]], og, relfro), (b, "rev"))
+    tally.report(6)
     e = ConicBatch(1, 20, cones)
     bad = sp.csc_matrix(A[0])
     bad.indptr[5] = bad.indptr[4] - 1     # non-monotone colptr
@@ -235,16 +326,16 @@ def SplitConicBatch(ConicBatch, monkeypatch):
 
 
 def test_split_mixed_cones_batch(SplitConicBatch):
-    _synthetic_check(SplitConicBatch, 6, 30, [(0, 3), (1, 10), (3, 6), (2, 4), (4, 6)], 11)
+    _synthetic_check(SplitConicBatch, 6, 30, [(0, 3), (1, 10), (3, 6), (2, 4), (4, 6)], 11,
+                     "split: mixed cones", cap=36)
 
 
 def test_split_well_posed_batch(SplitConicBatch):
-    w = _synthetic_check(SplitConicBatch, 2, 100, [(3, 10)] * 20, 21)
-    assert max(w.values()) <= 1e-5, w
+    _synthetic_check(SplitConicBatch, 2, 100, [(3, 10)] * 20, 21, "split: well-posed SOC")
 
 
 def test_split_psd_blocks_batch(SplitConicBatch):
-    _synthetic_check(SplitConicBatch, 3, 25, [(4, 10), (4, 15), (1, 5)], 13)
+    _synthetic_check(SplitConicBatch, 3, 25, [(4, 10), (4, 15), (1, 5)], 13, "split: PSD blocks", cap=18)
 
 
 def test_split_zero_rhs_gives_zero(SplitConicBatch):
@@ -270,7 +361,7 @@ def test_split_matches_persistent_kernel(ConicBatch, monkeypatch):
     assert relfro(res["1"][1], res["0"][1]) <= 1e-5
 
 
-def test_config5_shape_multi_rowblock(ConicBatch):
-    # BASELINE config 5 structure (PSD(50) cones, m ≫ n) scaled to oracle
-    # speed: 3 PSD(50) → m = 3825 = 8 row blocks, auto split path
-    _synthetic_check(ConicBatch, 2, 100, [(4, 1275)] * 3, 16)
+def test_config5_structure_multi_rowblock(ConicBatch):
+    # config-5 structure (PSD(50) cones, m ≫ n) at oracle speed: 3 PSD(50)
+    # → m = 3825 = 8 row blocks, auto split path
+    _synthetic_check(ConicBatch, 2, 100, [(4, 1275)] * 3, 16, "config-5 structure, 3 cones", cap=12)

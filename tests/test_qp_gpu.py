@@ -1,7 +1,12 @@
-"""QP path on the MI355X: HIP engine vs the CPU oracle and the reference's
-golden fixtures.  Parity bar (BASELINE.json north_star): 1e-6 relative
-Frobenius in Float64 on (dz, dλ, dν) forward and reverse; bit-exact discrete
-selections (iterative branch, eliminated-row set)."""
+"""QP path on the MI355X: HIP engine (through the C-ABI) vs the CPU oracle and
+the reference's golden fixtures.  Parity bar (BASELINE.json north_star): 1e-6
+relative Frobenius in Float64 on (dz, dλ, dν) forward and reverse; bit-exact
+discrete selections (the `iterative` branch and the kept / eliminated
+inequality rows, compared as masks).
+
+Both factorisations are covered: the default no-pivot blocked LU with its
+threshold test (problems that fail it are re-factorised with partial
+pivoting: `lu_kind`), and partial pivoting for every problem (DOPT_LU=0)."""
 
 import json
 import os
@@ -14,6 +19,7 @@ from oracle import qp as oqp
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 RTOL = 1e-6   # relative Frobenius, north_star
+NOPIV, PIVOT, LSQR = 1, 2, 0
 
 
 def relfro(a, b):
@@ -27,6 +33,17 @@ def relfro(a, b):
 def QPBatch():
     from diffopt_amd.qp import QPBatch
     return QPBatch
+
+
+@pytest.fixture(params=["nopiv", "pivot"])
+def lu_mode(request, monkeypatch):
+    """The factorisation (read by dopt_create): default, or partial pivoting
+    for every problem."""
+    if request.param == "pivot":
+        monkeypatch.setenv("DOPT_LU", "0")
+    else:
+        monkeypatch.delenv("DOPT_LU", raising=False)
+    return request.param
 
 
 def _fixtures():
@@ -66,7 +83,7 @@ def _engine_solve(QPBatch, a, fw):
 
 
 @pytest.mark.parametrize("fx", FX, ids=[f["name"] for f in FX])
-def test_engine_matches_reference_fixture_and_oracle(QPBatch, fx):
+def test_engine_matches_reference_fixture_and_oracle(QPBatch, lu_mode, fx):
     from test_oracle_golden import qp_outputs
     a, fw = _arr(fx)
     (dz, dl, dn), (fz, fl, fn), it = _engine_solve(QPBatch, a, fw)
@@ -84,24 +101,32 @@ def test_engine_matches_reference_fixture_and_oracle(QPBatch, fx):
         assert relfro(np.concatenate(g), np.concatenate(r)) <= RTOL
 
 
-def _synthetic(batch, n, m, p, phi, seed, dense=False):
+def _synthetic(batch, n, m, p, phi, seed, dense=False, lam_eps=0.0):
     from diffopt_amd.synthetic import qp_numpy
-    return qp_numpy(batch, n, m, p, phi, seed, dense_tangents=dense)
+    return qp_numpy(batch, n, m, p, phi, seed, dense_tangents=dense, lam_eps=lam_eps)
 
 
-def _check_batch(QPBatch, d, dense=False, fast_max=None):
+def _oracle_kept(d, b):
+    """The reference's elimination set: λ == 0 and (Gz − h) != 0 with Gz − h in
+    Julia's sparse mul! order — the rows kept are the complement."""
+    s = oqp.gz_minus_h(d["G"][b], d["z"][b], d["h"][b])
+    return ~((d["lam"][b] == 0) & (s != 0))
+
+
+def _check_batch(QPBatch, d, dense=False, kinds=None):
+    """GPU vs oracle on every problem; kept-row masks bit-equal; optionally the
+    expected factorisation kind per problem.  Returns the engine."""
     B, n = d["z"].shape
     m = d["lam"].shape[1]
     p = d["nu"].shape[1]
     e = QPBatch(B, n, m, p)
-    if fast_max is not None:
-        e.set_fast_max(fast_max)
     e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
     fkw = dict(dq=d["dq"], dh=d["dh"], db=d["db"])
     if dense:
         fkw.update(dQ=d["dQ"], dG=d["dG"], dA=d["dA"])
     rev, fwd = e.forward_reverse(d["dl_dz"], **fkw)
     sizes = e.system_size()
+    kept = e.kept()
     worst = 0.0
     for b in range(B):
         args = [d[k][b] for k in ["Q", "G", "h", "A", "z", "lam", "nu"]]
@@ -110,109 +135,87 @@ def _check_batch(QPBatch, d, dense=False, fast_max=None):
         oz, ol, on = oqp.forward_differentiate(*args, **fk)
         worst = max(worst, relfro(rev[b], np.concatenate([rz, rl, rn])),
                     relfro(fwd[b], np.concatenate([oz, ol, on])))
-        # bit-exact elimination set: λ == 0 and (Gz − h) != 0 (Julia summation order)
-        s = oqp.gz_minus_h(d["G"][b], d["z"][b], d["h"][b])
-        kept = np.count_nonzero(~((d["lam"][b] == 0) & (s != 0)))
-        assert sizes[b] == n + kept + p
+        ok = _oracle_kept(d, b)
+        np.testing.assert_array_equal(kept[b], ok)   # bit-exact index selection
+        assert sizes[b] == n + ok.sum() + p
     assert worst <= RTOL, worst
+    if kinds is not None:
+        np.testing.assert_array_equal(e.lu_kind(), kinds)
     return e
 
 
-def test_cfg1_shape_batch(QPBatch):
-    _check_batch(QPBatch, _synthetic(4, 50, 80, 30, 0.2, 20250308))
+def test_cfg1_shape_batch(QPBatch, lu_mode):
+    _check_batch(QPBatch, _synthetic(4, 50, 80, 30, 0.2, 20250308),
+                 kinds=[NOPIV if lu_mode == "nopiv" else PIVOT] * 4)
 
 
-def test_cfg2_shape_small_batch(QPBatch):
-    _check_batch(QPBatch, _synthetic(6, 200, 300, 0, 0.3, 20250309))
+def test_cfg2_shape_small_batch(QPBatch, lu_mode):
+    _check_batch(QPBatch, _synthetic(6, 200, 300, 0, 0.3, 20250309),
+                 kinds=[NOPIV if lu_mode == "nopiv" else PIVOT] * 6)
 
 
-def test_dense_tangents(QPBatch):
+def test_dense_tangents(QPBatch, lu_mode):
     _check_batch(QPBatch, _synthetic(3, 40, 60, 10, 0.5, 7, dense=True), dense=True)
 
 
-def test_blocked_path_mid_size(QPBatch):
-    """Reduced system 512 < N' ≤ 1536 (here 560) takes the blocked step path
-    (panel / U12 / MFMA trailing-update launches over the whole batch)."""
+def test_blocked_mid_size(QPBatch, lu_mode):
+    """Reduced system 560: several 64-column blocks with a 32-wide tail."""
     _check_batch(QPBatch, _synthetic(2, 300, 400, 20, 0.6, 11))
 
 
-def test_blocked_path_cfg3_shape(QPBatch):
-    """BASELINE config 3 shape (n=1000, m=1500, 30 % active ⇒ N' = 1450, three
-    panel rows per thread) at batch 2."""
+def test_blocked_cfg3_shape(QPBatch, lu_mode):
+    """BASELINE config 3 shape (n=1000, m=1500, 30 % active ⇒ N' = 1450) at batch 2."""
     _check_batch(QPBatch, _synthetic(2, 1000, 1500, 0, 0.3, 20250310))
 
 
-def test_fused_path_small_and_ragged(QPBatch):
-    """fast_max = 512 routes every LU problem with N' ≤ 512 to the fused
-    one-workgroup-per-problem kernel (the default route is the blocked path)."""
-    _check_batch(QPBatch, _synthetic(3, 200, 300, 0, 0.3, 20250309), fast_max=512)
-    _check_batch(QPBatch, _synthetic(3, 50, 80, 30, 0.2, 20250308), fast_max=512)
-    _check_batch(QPBatch, _synthetic(3, 40, 60, 10, 0.5, 7, dense=True), dense=True, fast_max=512)
-    for (n, m, p) in [(1, 1, 0), (3, 0, 0), (5, 0, 2), (7, 3, 0), (33, 31, 1), (64, 1, 63)]:
-        _check_batch(QPBatch, _synthetic(2, n, m, p, 0.5, 100 + n), fast_max=512)
-
-
-def test_blocked_path_forced_small_and_ragged(QPBatch):
-    """fast_max = 0 forces every LU problem onto the blocked path: config-1/2
-    shapes and ragged sizes (p = 0, m = 0, N' not a multiple of 32)."""
-    _check_batch(QPBatch, _synthetic(3, 200, 300, 0, 0.3, 20250309), fast_max=0)
-    _check_batch(QPBatch, _synthetic(3, 50, 80, 30, 0.2, 20250308), fast_max=0)
-    for (n, m, p) in [(1, 1, 0), (3, 0, 0), (7, 3, 0), (33, 31, 1), (64, 1, 63)]:
-        _check_batch(QPBatch, _synthetic(2, n, m, p, 0.5, 100 + n), fast_max=0)
-
-
-@pytest.mark.parametrize("group", ["2", "3", "4"])
-def test_blocked_panel_groups(QPBatch, monkeypatch, group):
-    """Left-looking panel groups (DOPT_LU_GROUP, read at handle creation):
-    separate U12 kernel with the group's pending update, rank-32g trailing
-    update; shapes whose panel count is not a multiple of the group."""
-    monkeypatch.setenv("DOPT_LU_GROUP", group)
-    _check_batch(QPBatch, _synthetic(3, 200, 300, 0, 0.3, 20250309))
-    _check_batch(QPBatch, _synthetic(2, 300, 400, 20, 0.6, 11))
-    for (n, m, p) in [(7, 3, 0), (33, 31, 1), (64, 1, 63)]:
+def test_ragged_shapes(QPBatch, lu_mode):
+    for (n, m, p) in [(1, 1, 0), (3, 0, 0), (5, 0, 2), (7, 3, 0), (33, 31, 1), (64, 1, 63),
+                      (40, 50, 7), (90, 10, 5)]:
         _check_batch(QPBatch, _synthetic(2, n, m, p, 0.5, 100 + n))
 
 
-@pytest.mark.parametrize("ct", ["2", "4"])
-def test_blocked_update_strips(QPBatch, monkeypatch, ct):
-    """Strip trailing-update kernel (DOPT_UPD_CT column tiles per workgroup,
-    prefetched): bit-identical to the one-tile kernel, and oracle parity on
-    shapes with ragged column-tile counts."""
-    d = _synthetic(2, 300, 400, 20, 0.6, 11)
-    B, n = d["z"].shape
-    outs = []
-    for env in (None, ct):
-        if env is None:
-            monkeypatch.delenv("DOPT_UPD_CT", raising=False)
-        else:
-            monkeypatch.setenv("DOPT_UPD_CT", env)
-        e = QPBatch(B, n, 400, 20)
-        e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
-        outs.append(e.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"]))
-    np.testing.assert_array_equal(outs[0][0], outs[1][0])
-    np.testing.assert_array_equal(outs[0][1], outs[1][1])
-    _check_batch(QPBatch, _synthetic(2, 200, 300, 0, 0.3, 20250309))
-    _check_batch(QPBatch, _synthetic(2, 1000, 1500, 0, 0.3, 20250310))
+def test_no_elimination_worst_case(QPBatch, lu_mode):
+    """Interior-point-like duals: inactive rows get λ = 1e-9 (not exactly 0),
+    so nothing is eliminated and N' = n + m (bench.py --lam-eps)."""
+    d = _synthetic(3, 200, 300, 0, 0.3, 20250312, lam_eps=1e-9)
+    e = _check_batch(QPBatch, d)
+    assert (e.system_size() == 500).all()
 
 
-@pytest.mark.parametrize("B", [16, 12])
-def test_solve2_interleaved_order(QPBatch, monkeypatch, B):
-    """Both-direction solve with the directions of each group of 8 problems
-    adjacent in dispatch order (DOPT_SOLVE_ILV=1, the default; B % 8 != 0
-    falls back to the split order): bit-identical to the split order, and
-    oracle parity."""
-    d = _synthetic(B, 120, 150, 10, 0.4, 20250311)
-    n = d["z"].shape[1]
-    outs = []
-    for env in ("0", "1"):
-        monkeypatch.setenv("DOPT_SOLVE_ILV", env)
-        e = QPBatch(B, n, 150, 10)
-        e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
-        outs.append(e.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"]))
-    np.testing.assert_array_equal(outs[0][0], outs[1][0])
-    np.testing.assert_array_equal(outs[0][1], outs[1][1])
-    monkeypatch.delenv("DOPT_SOLVE_ILV")
-    _check_batch(QPBatch, d)
+def _indefinite(d, idx, seed=5):
+    """Replace Q of the problems `idx` by a symmetric indefinite matrix with a
+    tiny diagonal: the no-pivot LU's first multipliers are ~1e4, so those
+    problems fail the threshold test and take partial pivoting.  (z, λ, ν)
+    stays a KKT point: the engine never reads q."""
+    rng = np.random.default_rng(seed)
+    n = d["Q"].shape[1]
+    for b in idx:
+        S = rng.standard_normal((n, n))
+        Q = (S + S.T) / 2
+        Q[np.diag_indices(n)] = 1e-4
+        d["Q"][b] = Q
+    return d
+
+
+def test_pivot_fallback_mixed_batch(QPBatch, lu_mode):
+    """Problems that fail the no-pivot threshold test, interleaved with ones
+    that pass: the rejected ones are re-assembled and factorised with partial
+    pivoting (their solves run after the speculative no-pivot solves)."""
+    d = _indefinite(_synthetic(6, 60, 80, 5, 0.4, 41), [1, 4])
+    want = [NOPIV, PIVOT, NOPIV, NOPIV, PIVOT, NOPIV] if lu_mode == "nopiv" else [PIVOT] * 6
+    e = _check_batch(QPBatch, d, kinds=want)
+    # the split API reuses the same factors: bit-equal to the fused call
+    rev, fwd = e.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
+    e.factor()
+    np.testing.assert_array_equal(e.reverse(d["dl_dz"]), rev)
+    np.testing.assert_array_equal(e.forward(dq=d["dq"], dh=d["dh"], db=d["db"]), fwd)
+    np.testing.assert_array_equal(e.lu_kind(), want)
+
+
+def test_pivot_fallback_every_problem(QPBatch):
+    """Every problem rejected (tall blocked systems with several blocks)."""
+    d = _indefinite(_synthetic(3, 150, 160, 0, 0.5, 43), [0, 1, 2])
+    _check_batch(QPBatch, d, kinds=[PIVOT] * 3)
 
 
 def test_reverse_grads_materialised(QPBatch):
@@ -244,10 +247,11 @@ def test_reverse_grads_materialised(QPBatch):
         np.testing.assert_array_equal(g2[k].cpu().numpy(), g[k])
 
 
-def test_csc_staging_matches_dense(QPBatch):
+def test_csc_staging_matches_dense_and_oracle(QPBatch):
     """dopt_qp_set_csc (MOI matrix form: Julia CSC, Int64, 1-based) densified
-    on the device gives bit-identical sensitivities to dopt_qp_set with the
-    same dense matrices; sparse G/A with empty columns; malformed CSC raises."""
+    on the device: against the oracle on the same sparse problems, and
+    bit-identical to dopt_qp_set with the dense matrices; sparse G/A with an
+    empty column; malformed CSC raises."""
     import scipy.sparse as sp
     from diffopt_amd import EngineError
     d = _synthetic(3, 40, 60, 10, 0.5, 77)
@@ -258,13 +262,19 @@ def test_csc_staging_matches_dense(QPBatch):
     G[:, :, 3] = 0.0                      # an empty column
     A = d["A"] * (rng.random(d["A"].shape) < 0.5)
     h = np.einsum("bmn,bn->bm", G, d["z"]) - np.einsum("bmn,bn->bm", d["G"], d["z"]) + d["h"]
-    e1 = QPBatch(B, n, m, p)
-    e1.set(d["Q"], G, h, A, d["z"], d["lam"], d["nu"])
-    r1, f1 = e1.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
     e2 = QPBatch(B, n, m, p)
     e2.set_csc([sp.csc_matrix(q) for q in d["Q"]], [sp.csc_matrix(g) for g in G], h,
                [sp.csc_matrix(a) for a in A], d["z"], d["lam"], d["nu"])
     r2, f2 = e2.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
+    for b in range(B):
+        args = [d["Q"][b], G[b], h[b], A[b], d["z"][b], d["lam"][b], d["nu"][b]]
+        ref_r = np.concatenate(oqp.reverse_differentiate(*args, d["dl_dz"][b]))
+        ref_f = np.concatenate(oqp.forward_differentiate(*args, dq=d["dq"][b], dh=d["dh"][b],
+                                                         db=d["db"][b]))
+        assert relfro(r2[b], ref_r) <= RTOL and relfro(f2[b], ref_f) <= RTOL
+    e1 = QPBatch(B, n, m, p)
+    e1.set(d["Q"], G, h, A, d["z"], d["lam"], d["nu"])
+    r1, f1 = e1.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
     np.testing.assert_array_equal(r1, r2)
     np.testing.assert_array_equal(f1, f2)
     bad = sp.csc_matrix(G[0])
@@ -273,67 +283,39 @@ def test_csc_staging_matches_dense(QPBatch):
         e2.set_csc(sp.csc_matrix(d["Q"][0]), bad, h, sp.csc_matrix(A[0]), d["z"], d["lam"], d["nu"])
 
 
-def test_blocked_matches_fused_and_split(QPBatch):
-    """Same batch through the fused kernel and the blocked path: agreement to
-    rounding (different accumulation order only); blocked split calls
-    (factor → reverse → forward) bit-equal to the blocked fused call."""
-    d = _synthetic(4, 120, 200, 10, 0.4, 21)
-    B, n = d["z"].shape
-    e1 = QPBatch(B, n, 200, 10)
-    e1.set_fast_max(512)
-    e1.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
-    r1, f1 = e1.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
-    e2 = QPBatch(B, n, 200, 10)
-    e2.set_fast_max(0)
-    e2.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
-    r2, f2 = e2.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
-    for a, b in ((r1, r2), (f1, f2)):
-        assert max(relfro(a[i], b[i]) for i in range(B)) <= 1e-11
-    e2.factor()
-    r3 = e2.reverse(d["dl_dz"])
-    f3 = e2.forward(dq=d["dq"], dh=d["dh"], db=d["db"])
-    np.testing.assert_array_equal(r2, r3)
-    np.testing.assert_array_equal(f2, f3)
-
-
-def test_mixed_routes_in_one_batch(QPBatch):
-    """One batch whose problems take different paths — fused (N' ≤ fast_max)
-    and blocked (N' > fast_max), interleaved — with forward tangents that
-    reach eliminated rows (the `full` RHS buffer both paths share).  The LSQR
-    branch in a mixed batch: test_lp_iterative_batch_mixed_with_qp."""
-    lo = _synthetic(3, 60, 80, 4, 0.2, 31)    # N' = 60 + 16 + 4 = 80
-    hi = _synthetic(3, 60, 80, 4, 0.6, 32)    # N' = 60 + 48 + 4 = 112 (48 + 4 < n: LICQ)
-    d = {k: np.concatenate([np.stack([lo[k][i], hi[k][i]]) for i in range(3)]) for k in lo}
-    _check_batch(QPBatch, d, fast_max=100)
-
-
-def test_generic_large_system_path(QPBatch):
-    """Reduced system > 1536 unknowns takes the generic LU kernel."""
-    _check_batch(QPBatch, _synthetic(2, 1200, 700, 0, 0.6, 12))
-
-
-def test_ragged_shapes(QPBatch):
-    for (n, m, p) in [(1, 1, 0), (3, 0, 0), (5, 0, 2), (7, 3, 0), (33, 31, 1), (64, 1, 63)]:
-        _check_batch(QPBatch, _synthetic(2, n, m, p, 0.5, 100 + n))
-
-
-def test_reverse_forward_separately_equal_fused(QPBatch):
+def test_factor_then_reverse_forward(QPBatch, lu_mode):
+    """dopt_qp_factor once, then reverse and forward on the kept factors (the
+    reference re-factorises per call): against the oracle, and bit-equal to
+    the fused forward_reverse call; a second reverse with another seed reuses
+    the factorisation."""
     d = _synthetic(5, 30, 40, 5, 0.4, 3)
     B, n = d["z"].shape
     e = QPBatch(B, n, 40, 5)
     e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
-    r1, f1 = e.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
     e.factor()
     r2 = e.reverse(d["dl_dz"])
     f2 = e.forward(dq=d["dq"], dh=d["dh"], db=d["db"])
+    seed2 = d["dl_dz"][::-1].copy()
+    r3 = e.reverse(seed2)
+    for b in range(B):
+        args = [d[k][b] for k in ["Q", "G", "h", "A", "z", "lam", "nu"]]
+        assert relfro(r2[b], np.concatenate(oqp.reverse_differentiate(*args, d["dl_dz"][b]))) <= RTOL
+        assert relfro(r3[b], np.concatenate(oqp.reverse_differentiate(*args, seed2[b]))) <= RTOL
+        assert relfro(f2[b], np.concatenate(oqp.forward_differentiate(
+            *args, dq=d["dq"][b], dh=d["dh"][b], db=d["db"][b]))) <= RTOL
+    r1, f1 = e.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
     np.testing.assert_array_equal(r1, r2)
     np.testing.assert_array_equal(f1, f2)
 
 
-@pytest.mark.parametrize("fast_max", [512, 0])
-def test_singular_kkt_raises(QPBatch, fast_max):
+def test_generic_large_system_path(QPBatch, lu_mode):
+    """Reduced system > 1536 unknowns takes the generic LU kernel."""
+    _check_batch(QPBatch, _synthetic(2, 1200, 700, 0, 0.6, 12), kinds=[PIVOT, PIVOT])
+
+
+def test_singular_kkt_raises(QPBatch, lu_mode):
     """λ_i == 0 and s_i == 0 → zero row/column in LHS → SingularException
-    (fused path and blocked path)."""
+    (the no-pivot LU rejects the zero pivot; partial pivoting reports it)."""
     from diffopt_amd import SingularException
     Q = np.eye(2)[None]
     G = np.array([[[1.0, 0.0]]])
@@ -341,14 +323,13 @@ def test_singular_kkt_raises(QPBatch, fast_max):
     h = np.array([1.0])[None]           # s = Gz − h = 0
     lam = np.zeros((1, 1))
     e = QPBatch(1, 2, 1, 0)
-    e.set_fast_max(fast_max)
     e.set(Q, G, h, np.zeros((1, 0, 2)), z, lam, np.zeros((1, 0)))
     with pytest.raises(SingularException):
         e.reverse(np.ones((1, 2)))
     assert e.info()[0] > 0
 
 
-def test_lp_iterative_batch_mixed_with_qp(QPBatch):
+def test_lp_iterative_batch_mixed_with_qp(QPBatch, lu_mode):
     """A batch mixing Q == 0 (LSQR branch) and Q != 0 (LU branch)."""
     with open(os.path.join(HERE, "golden", "lp_fixtures.json")) as fh:
         lp = json.load(fh)
@@ -361,10 +342,34 @@ def test_lp_iterative_batch_mixed_with_qp(QPBatch):
           np.stack([a["z"]] * 2), np.stack([a["lam"]] * 2), np.zeros((2, 0)))
     rev = e.reverse(np.stack([a["dzb"]] * 2))
     assert list(e.iterative()) == [True, False]
+    assert e.lu_kind()[0] == LSQR
     for b in range(2):
         rz, rl, rn = oqp.reverse_differentiate(Qs[b], a["G"], a["h"], np.zeros((0, n)),
                                                a["z"], a["lam"], np.zeros(0), a["dzb"])
         assert relfro(rev[b], np.concatenate([rz, rl, rn])) <= RTOL
+
+
+def test_lsqr_branch_beyond_lds_size(QPBatch):
+    """The LSQR branch on a system of n + m + p = 4200 > 4096 unknowns (its
+    vectors live in a global workspace; a batch with LU problems too):
+    LSQR's own stopping guarantee on the KKT residual, and the LU problem
+    against the oracle."""
+    rng = np.random.default_rng(9)
+    n, m = 200, 4000
+    d = _synthetic(2, n, m, 0, 0.02, 31)
+    d["Q"][0] = 0.0                              # problem 0: LP → LSQR on the full LHS
+    e = QPBatch(2, n, m, 0)
+    e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    seed = rng.standard_normal((2, n))
+    rev = np.asarray(e.reverse(seed))
+    assert list(e.iterative()) == [True, False]
+    LHS = oqp.create_LHS_matrix(d["z"][0], d["lam"][0], d["Q"][0], d["G"][0], d["h"][0], d["A"][0])
+    rhs = np.concatenate([seed[0], np.zeros(m)])
+    x = -rev[0]
+    r = np.linalg.norm(LHS.T @ (LHS @ x - rhs))   # least-squares optimality (LSQR's test2)
+    assert r <= 1e-6 * np.linalg.norm(LHS) ** 2 * np.linalg.norm(x) + 1e-6 * np.linalg.norm(rhs)
+    args = [d[k][1] for k in ["Q", "G", "h", "A", "z", "lam", "nu"]]
+    assert relfro(rev[1], np.concatenate(oqp.reverse_differentiate(*args, seed[1]))) <= RTOL
 
 
 def test_device_mode_matches_host_mode(QPBatch):
@@ -382,14 +387,28 @@ def test_device_mode_matches_host_mode(QPBatch):
     np.testing.assert_array_equal(f1, f2.cpu().numpy())
 
 
+def test_output_buffers_are_validated(QPBatch):
+    """Caller-supplied outputs of the wrong dtype, shape, layout or memory kind
+    raise before any kernel writes."""
+    import torch
+    d = _synthetic(2, 10, 12, 2, 0.3, 6)
+    e = QPBatch(2, 10, 12, 2)
+    e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    L = 24
+    for bad in (np.empty((2, L), np.float32), np.empty((2, L - 1)), np.empty((L, 2)).T,
+                torch.empty(2, L, dtype=torch.float64, device="cuda")):
+        with pytest.raises(TypeError):
+            e.forward_reverse(d["dl_dz"], dq=d["dq"], out_rev=bad, out_fwd=np.empty((2, L)))
+
+
 @pytest.mark.parametrize("cfg", [(200, 300, 20250309), (1000, 1500, 20250310)],
                          ids=["config2", "config3"])
 def test_full_batch_kkt_residual_property(QPBatch, cfg):
     """BASELINE configs 2 and 3 at full batch (1024 × n=200, m=300 and
     1024 × n=1000, m=1500): size-independent check — every solution satisfies
     its KKT system (reverse: LHS x = rhs, forward: LHSᵀ x = rhs) to 1e-9
-    relative, computed in fp64 on the GPU — plus bit-exact kept-set sizes
-    against a GPU recount of λ == 0 ∧ s ≠ 0."""
+    relative, computed in fp64 on the GPU; every problem passes the no-pivot
+    threshold test; the kept masks equal a GPU recount of λ == 0 ∧ s ≠ 0."""
     import torch
     from diffopt_amd.synthetic import qp_torch
     n, m, seed = cfg
@@ -415,10 +434,12 @@ def test_full_batch_kkt_residual_property(QPBatch, cfg):
     res = torch.sqrt((f1 ** 2).sum(1) + (f2 ** 2).sum(1)) / nrm
     assert float(res.max()) < 1e-9
     assert (e.info() == 0).all()
+    assert (e.lu_kind() == NOPIV).all()
     # by construction inactive rows have s = −U(0.5, 1.5), far from 0, so the
     # kept set is exactly the active set whatever the summation order
-    kept = (~((lam == 0) & (s != 0))).sum(1).cpu().numpy()
-    np.testing.assert_array_equal(e.system_size(), n + kept)
+    kept = ~((lam == 0) & (s != 0)).cpu().numpy()
+    np.testing.assert_array_equal(e.kept(), kept)
+    np.testing.assert_array_equal(e.system_size(), n + kept.sum(1))
     del d, rev, fwd, Q, G, z, lam, s
     e.close()
     torch.cuda.empty_cache()

@@ -1,10 +1,19 @@
-"""Compact view of a rocprofv3 kernel_stats.csv: short name, calls, total ms,
-avg µs, share; `per` = number of bench steps (incl. warmup) to divide by."""
-import csv, re, sys
+"""Compact view of a rocprofv3 kernel_stats.csv (a file, or the directory
+rocprofv3 -d wrote): short name, calls, total ms, avg µs, share; `per` =
+number of bench steps (incl. warmup) to divide the totals by."""
+import csv
+import glob
+import os
+import re
+import sys
+
 path = sys.argv[1]
+if os.path.isdir(path):
+    path = sorted(glob.glob(os.path.join(path, "**", "*kernel_stats.csv"), recursive=True))[0]
 per = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
 rows = list(csv.DictReader(open(path)))
-for r in rows[:14]:
+print(path)
+for r in rows[:20]:
     name = r["Name"]
     m = re.search(r"(\w+(?:<[^>]*>)?)\(", name)
     short = m.group(1) if m else name[:60]
