@@ -16,20 +16,31 @@
 // §2.1 measures max|l| ≈ 1–2 on configs 1–3).
 //
 // Without pivoting the panel has no column-by-column argmax over the whole
-// panel height: per 64-column block step
+// panel height, so a 64-column block step is
 //
-//   nlu_diag_kernel   (one 256-thread WG per problem)
-//     factor the 64×64 diagonal block in registers (4×4 tile per thread, one
-//     barrier per column), its inverses L11⁻¹ / U11⁻¹ (LDS, MFMA for the
-//     off-diagonal blocks), the 32×32 diagonal-block inverses (dinv) the
-//     solves use
-//   nlu_trsm_kernel   (one 256-thread WG per 64-row / 64-column strip)
-//     L21 = A21·U11⁻¹ and U12 = L11⁻¹·A12 on v_mfma_f64_16x16x4f64 (the
-//     triangular structure of the inverses skips 3/8 of the k-steps) and the
-//     threshold test on L21
-//   nlu_update_kernel (one 256-thread WG per 64×64 trailing tile)
-//     A22 −= L21·U12, rank 64 on MFMA, the U12 tile staged in LDS, XCD-aware
-//     tile order (one problem's tiles share an L2)
+//   diag_core        the 64×64 diagonal block: LU (recursive 32×32 halves,
+//                    single-wave), its inverses L11⁻¹ / U11⁻¹ (MFMA for the
+//                    off-diagonal blocks), the 32×32 diagonal-block inverses
+//                    (dinv) the solves use
+//                    (nlu_diag_kernel, one 256-thread WG per problem)
+//   nlu_trsm_kernel  one 256-thread WG per 64-row / 64-column strip:
+//                    L21 = A21·U11⁻¹ and U12 = L11⁻¹·A12 on
+//                    v_mfma_f64_16x16x4f64 (the triangles of the inverses skip
+//                    3/8 of the k-steps) and the threshold test on L21
+//   nlu_update_kernel one 256-thread WG per 64×64 trailing tile:
+//                    A22 −= L21·U12, rank 64 on MFMA, the U12 tile staged in
+//                    LDS, XCD-aware tile order (one problem's tiles share an L2)
+//
+// Two designs measured slower on config 2 (B = 1024, Np = 320) and dropped:
+//  * TRSM folded into the update tiles (each tile recomputing its L21 / U12
+//    pieces from the inverse): 533 µs at c0 = 0 against 171 + 309 µs — f64
+//    MFMA is the scarcer resource (measured ≈44 ns per 16x16x4 per SIMD, i.e.
+//    ≈47 TF/s, tools/probe/mfma_rate.hip), and the fold doubles the MFMAs;
+//  * the next diagonal block folded into tile (0, 0) of the update: with 4
+//    workgroups per CU (LDS) a ~100 µs latency-bound diagonal workgroup parks
+//    a quarter of a CU while the short tiles queue behind it (1.4 ms).
+// The diagonal latency is hidden instead by running the two halves of the
+// batch on two streams (qp_nopiv_factor).
 //
 // Factor format: K row-major, L strictly below / U on and above the diagonal,
 // perm = identity, dinv as the partial-pivoting path writes it — the solves of
@@ -197,9 +208,9 @@ __device__ __forceinline__ d4n tile32(int tr, int tc, FA A, FB Bm) {
 }
 
 // ---------------------------------------------------------------------------
-// Diagonal block of step c0 (multiple of 64) of problem blockIdx.x: rows and
-// columns c0 .. c0+63 (the last block may be 32 wide), factorised
-// recursively as two 32×32 blocks a, b:
+// Diagonal block of step c0 (multiple of 64) of one problem: rows and columns
+// c0 .. c0+63 (the last block may be 32 wide), already in the LDS image S
+// (identity beyond Wv), factorised recursively as two 32×32 blocks a, b:
 //   A  wave 0: LU of a (wave_lu32)
 //   B  waves 0–3: L_aa⁻¹, U_aa⁻¹ (the solves' dinv), U_ab = L_aa⁻¹A_ab,
 //      L_ba = A_ba U_aa⁻¹ (+ threshold test), one column / row per lane
@@ -208,69 +219,50 @@ __device__ __forceinline__ d4n tile32(int tr, int tc, FA A, FB Bm) {
 //   E  waves 0–1: L_bb⁻¹, U_bb⁻¹; waves 2–3: T_L = L_ba L_aa⁻¹, T_U = U_aa⁻¹U_ab
 //   F  L⁻¹_ba = −L_bb⁻¹T_L, U⁻¹_ab = −T_U U_bb⁻¹ (MFMA)
 // Writes L11 / U11 to K, perm = identity, the 32×32 diagonal-block inverses to
-// dinv and the packed 64×64 inverse (L11⁻¹ strictly below the diagonal,
-// U11⁻¹ on and above it) to `binv` for the TRSM launch.  ~35 KB of LDS and
-// one 256-thread workgroup per problem: 4 per CU, a 1024-problem batch runs
-// in one round.
+// dinv and, when a trailing step follows, the packed 64×64 inverse (L11⁻¹
+// strictly below the diagonal, U11⁻¹ on and above it) to `Bg`.  A failed
+// threshold test marks the problem LU_REJECT and stops.  Called by the whole
+// 256-thread workgroup (workgroup-uniform arguments).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_diag_kernel(
-    double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
-    size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv) {
-  __shared__ double S[NB64 * SLD];
-  __shared__ double rowb[32], colb[32];
-  __shared__ int sbad;
-  const int b = blockIdx.x;
-  const QPMeta mm = meta[b];
-  const int Np = nlu_np(mm);
-  if (c0 >= Np || mm.lu == LU_REJECT) return;   // workgroup-uniform
-  const int Wv = min(NB64, Np - c0);             // 32 or 64
-  const bool trsm = Np - c0 > NB64;              // a TRSM launch follows
+struct DiagLds {
+  double* S;      // 64 × SLD
+  double* rowb;   // 32
+  double* colb;   // 32
+  int* sbad;
+  // all four inside one 64 × ULD buffer (ULD below), past the 64 × SLD image
+  __device__ explicit DiagLds(double* buf)
+      : S(buf), rowb(buf + NB64 * SLD), colb(buf + NB64 * SLD + 32),
+        sbad(reinterpret_cast<int*>(buf + NB64 * SLD + 64)) {}
+};
+
+__device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__ Kb, int ld,
+                                          int32_t* __restrict__ permb, double* __restrict__ Db,
+                                          QPMeta* __restrict__ mb, int c0, int Np, double* __restrict__ Bg) {
+  double* S = L.S;
+  const int Wv = min(NB64, Np - c0);   // 32 or 64
+  const bool trsm = Np - c0 > NB64;    // a trailing step follows
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int g = lane >> 4, l16 = lane & 15;
-  double* Kb = K + (size_t)b * nmax * ld;
-  double* Db = dinv + (size_t)b * dstride + (size_t)(c0 / 32) * DBLK;
-  double* Bg = binv + (size_t)b * NB64 * NB64;
   auto to_K = [&](int r0, int cc0) {   // 32×32 block (r0, cc0) of S → K
     for (int e = t; e < 32 * 32; e += PNT) {
       const int i = r0 + (e >> 5), j = cc0 + (e & 31);
       Kb[(size_t)(c0 + i) * ld + c0 + j] = S[i * SLD + j];
     }
   };
-
   NLU_MARK_INIT;
-  // ---- 0. the block → LDS (identity beyond Wv); all 16 loads in flight
-  {
-    double v[NB64 * NB64 / PNT];
-#pragma unroll
-    for (int q = 0; q < NB64 * NB64 / PNT; ++q) {
-      const int e = t + PNT * q, i = e >> 6, j = e & 63;
-      const bool in = i < Wv && j < Wv;
-      v[q] = Kb[(size_t)(c0 + (in ? i : 0)) * ld + c0 + (in ? j : 0)];
-    }
-#pragma unroll
-    for (int q = 0; q < NB64 * NB64 / PNT; ++q) {
-      const int e = t + PNT * q, i = e >> 6, j = e & 63;
-      const bool in = i < Wv && j < Wv;
-      S[i * SLD + j] = in ? v[q] : (i == j ? 1.0 : 0.0);
-    }
-  }
-  if (t == 0) {
-    sbad = 0;
-    if (c0 == 0) meta[b].lu = LU_NOPIV;   // LU_REJECT below if a test fails
-  }
-  if (t < Wv) perm[(size_t)b * nmax + c0 + t] = c0 + t;
+  if (t == 0) *L.sbad = 0;
+  if (t < Wv) permb[c0 + t] = c0 + t;
   __syncthreads();
-  NLU_MARK(0);
   if (NLU_STOP <= 1) return;
 
   // ---- A. LU of block a
   if (wv == 0) {
-    const int bad = wave_lu32(S, 0, rowb, colb);
-    if (lane == 0 && bad) sbad = 1;
+    const int bad = wave_lu32(S, 0, L.rowb, L.colb);
+    if (lane == 0 && bad) *L.sbad = 1;
   }
   __syncthreads();
-  if (sbad) {
-    if (t == 0) meta[b].lu = LU_REJECT;
+  if (*L.sbad) {
+    if (t == 0) mb->lu = LU_REJECT;
     return;
   }
   NLU_MARK(1);
@@ -307,7 +299,7 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
         }
       }
     }
-    if (bad) sbad = 1;
+    if (bad) *L.sbad = 1;
     __syncthreads();   // every lane has read the factors of block a
     if (lane < 32) {
       if (wv < 2) {
@@ -327,12 +319,12 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
     }
   }
   __syncthreads();
-  if (sbad) {
-    if (t == 0) meta[b].lu = LU_REJECT;
+  if (*L.sbad) {
+    if (t == 0) mb->lu = LU_REJECT;
     return;
   }
   NLU_MARK(2);
-  if (Wv < NB64) return;   // a 32-wide last block: done (no TRSM follows)
+  if (Wv < NB64) return;   // a 32-wide last block: done (no trailing step follows)
   if (NLU_STOP <= 3) return;
 
   // ---- C. A_bb −= L_ba U_ab (one 16×16 tile per wave); U_ab, L_ba → K
@@ -354,12 +346,12 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
 
   // ---- D. LU of block b
   if (wv == 0) {
-    const int bad = wave_lu32(S, 32, rowb, colb);
-    if (lane == 0 && bad) sbad = 1;
+    const int bad = wave_lu32(S, 32, L.rowb, L.colb);
+    if (lane == 0 && bad) *L.sbad = 1;
   }
   __syncthreads();
-  if (sbad) {
-    if (t == 0) meta[b].lu = LU_REJECT;
+  if (*L.sbad) {
+    if (t == 0) mb->lu = LU_REJECT;
     return;
   }
   NLU_MARK(4);
@@ -377,36 +369,26 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
   }
   if (NLU_STOP <= 4) return;
 
-  // ---- E. inverses of block b (waves 0–1); T_L, T_U (waves 2–3) → binv
+  // ---- E. inverses of block b (waves 0–1); T_L, T_U (waves 2–3), which
+  // replace L_ba / U_ab in S (both already in K)
   {
     double x[32];
+    d4n acc[4];
     if (wv < 2 && lane < 32) {
       if (wv == 0) lower_inv_col(S, 32, lane, x);
       else upper_inv_col(S, 32, lane, x);
-    } else if (wv == 2) {   // T_L = L_ba · L_aa⁻¹ → binv rows 32.., cols 0..31
-      d4n acc[4];
+    } else if (wv == 2) {   // T_L = L_ba · L_aa⁻¹
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         acc[q] = tile32((q >> 1) * 16, (q & 1) * 16, [&](int i, int k) { return S[(32 + i) * SLD + k]; },
                         [&](int k, int j) { return k == j ? 1.0 : (k > j ? S[k * SLD + j] : 0.0); });
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-          Bg[(32 + (q >> 1) * 16 + g + 4 * rr) * NB64 + (q & 1) * 16 + l16] = acc[q][rr];
-    } else if (wv == 3) {   // T_U = U_aa⁻¹ · U_ab → binv rows 0..31, cols 32..
-      d4n acc[4];
+    } else if (wv == 3) {   // T_U = U_aa⁻¹ · U_ab
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         acc[q] = tile32((q >> 1) * 16, (q & 1) * 16, [&](int i, int k) { return k >= i ? S[i * SLD + k] : 0.0; },
                         [&](int k, int j) { return S[k * SLD + 32 + j]; });
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-          Bg[((q >> 1) * 16 + g + 4 * rr) * NB64 + 32 + (q & 1) * 16 + l16] = acc[q][rr];
     }
-    __syncthreads();   // the factors of block b have been read; T is in binv
+    __syncthreads();   // the factors of block b, L_ba and U_ab have been read
     if (wv < 2 && lane < 32) {
       double* D = Db + DBLK + (wv == 0 ? 0 : 32 * 32);
 #pragma unroll
@@ -414,12 +396,22 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
         D[jj * 32 + lane] = x[jj];
         if (wv == 0 ? jj > lane : jj <= lane) S[(32 + jj) * SLD + 32 + lane] = x[jj];
       }
+    } else if (wv >= 2) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int i = (q >> 1) * 16 + g + 4 * rr, j = (q & 1) * 16 + l16;
+          if (wv == 2) S[(32 + i) * SLD + j] = acc[q][rr];
+          else S[i * SLD + 32 + j] = acc[q][rr];
+        }
     }
   }
   __syncthreads();
   NLU_MARK(5);
 
-  // ---- F. off-diagonal inverse blocks (two 16×16 tiles per wave)
+  // ---- F. off-diagonal inverse blocks (two 16×16 tiles per wave), in place
+  // of T_L / T_U
   {
     d4n acc[2];
 #pragma unroll
@@ -429,11 +421,12 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
       if (wv < 2)   // L⁻¹_ba = −L_bb⁻¹ · T_L
         acc[q] = tile32(tr, tc,
                         [&](int i, int k) { return k == i ? 1.0 : (k < i ? S[(32 + i) * SLD + 32 + k] : 0.0); },
-                        [&](int k, int j) { return Bg[(32 + k) * NB64 + j]; });
+                        [&](int k, int j) { return S[(32 + k) * SLD + j]; });
       else          // U⁻¹_ab = −T_U · U_bb⁻¹
-        acc[q] = tile32(tr, tc, [&](int i, int k) { return Bg[i * NB64 + 32 + k]; },
+        acc[q] = tile32(tr, tc, [&](int i, int k) { return S[i * SLD + 32 + k]; },
                         [&](int k, int j) { return k <= j ? S[(32 + k) * SLD + 32 + j] : 0.0; });
     }
+    __syncthreads();   // every wave has read T_L / T_U
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int tile = (wv & 1) * 2 + q;
@@ -447,9 +440,52 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
   }
   __syncthreads();
   NLU_MARK(6);
-  // ---- G. the packed 64×64 inverse → binv (row-major, coalesced)
+  // ---- G. the packed 64×64 inverse → Bg (row-major, coalesced)
   for (int e = t; e < NB64 * NB64; e += PNT) Bg[e] = S[(e >> 6) * SLD + (e & 63)];
   NLU_MARK(7);
+}
+
+// the LDS one block step needs: the 64×64 diagonal image (SLD stride) of the
+// diagonal kernel and the staged 64×64 U12 tile (ULD stride) of the step
+// kernel share one buffer
+constexpr int ULD = 64 + 16;   // LDS row stride (doubles) of the staged U12 tile (update)
+constexpr int STEP_LDS = NB64 * ULD;   // 40 KB: 4 workgroups per CU
+static_assert(NB64 * SLD + 64 + 1 <= STEP_LDS, "diagonal image + rowb/colb/sbad must fit 40 KB");
+
+// Diagonal block of step c0 of every problem: one 256-thread workgroup per
+// problem, 40 KB of LDS: 4 per CU, a 1024-problem batch runs in one round.
+__global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_diag_kernel(
+    double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
+    size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv) {
+  __shared__ double S[STEP_LDS];
+  const int b = blockIdx.x;
+  const QPMeta mm = meta[b];
+  const int Np = nlu_np(mm);
+  if (c0 >= Np || mm.lu == LU_REJECT) return;   // workgroup-uniform
+  const int Wv = min(NB64, Np - c0);
+  const int t = threadIdx.x;
+  double* Kb = K + (size_t)b * nmax * ld;
+  NLU_MARK_INIT;
+  // the block → LDS (identity beyond Wv); all 16 loads in flight
+  {
+    double v[NB64 * NB64 / PNT];
+#pragma unroll
+    for (int q = 0; q < NB64 * NB64 / PNT; ++q) {
+      const int e = t + PNT * q, i = e >> 6, j = e & 63;
+      const bool in = i < Wv && j < Wv;
+      v[q] = Kb[(size_t)(c0 + (in ? i : 0)) * ld + c0 + (in ? j : 0)];
+    }
+#pragma unroll
+    for (int q = 0; q < NB64 * NB64 / PNT; ++q) {
+      const int e = t + PNT * q, i = e >> 6, j = e & 63;
+      const bool in = i < Wv && j < Wv;
+      S[i * SLD + j] = in ? v[q] : (i == j ? 1.0 : 0.0);
+    }
+  }
+  if (t == 0 && c0 == 0) meta[b].lu = LU_NOPIV;   // LU_REJECT below if a test fails
+  NLU_MARK(0);
+  diag_core(DiagLds(S), Kb, ld, perm + (size_t)b * nmax, dinv + (size_t)b * dstride + (size_t)(c0 / 32) * DBLK,
+            meta + b, c0, Np, binv + (size_t)b * NB64 * NB64);
 }
 
 // ---------------------------------------------------------------------------
@@ -571,7 +607,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 // tiles with an XCD-aware remap: the logical tiles of one problem are
 // consecutive, so they run on one XCD and share its L2 for L21 and U12.
 // ---------------------------------------------------------------------------
-constexpr int ULD = 64 + 16;   // LDS row stride (doubles) of the staged U tile
 
 __global__ __launch_bounds__(256) void nlu_update_kernel(double* __restrict__ K, int ld, int nmax,
                                                          const QPMeta* __restrict__ meta, int c0,
@@ -641,38 +676,59 @@ __global__ __launch_bounds__(256) void nlu_update_kernel(double* __restrict__ K,
 
 }  // namespace
 
-// No-pivot blocked LU of every ROUTE_BLOCKED problem: per 64-column block a
-// diagonal launch (B workgroups), a TRSM launch and a rank-64 trailing-update
-// launch.  Sized by h.blocked_npmax (the read-back of the metadata after the
-// assembly).
-void qp_nopiv_factor(Handle& h, double* dinv) {
+// No-pivot blocked LU of problems [b0, b0+nb): per 64-column block a diagonal
+// launch (nb workgroups), a TRSM launch and a rank-64 trailing-update launch
+// on `st`.
+static void nopiv_chain(Handle& h, double* dinv, int b0, int nb, hipStream_t st) {
   const int npmax = h.blocked_npmax;
-  if (npmax == 0) return;
-  const int B = (int)h.batch;
   const size_t dstride = dinv_stride(h.nmax);
-  double* K = h.K.as<double>();
-  int32_t* perm = h.ipiv.as<int32_t>();
-  QPMeta* meta = h.meta.as<QPMeta>();
-  h.binv.ensure((size_t)B * NB64 * NB64 * sizeof(double));
-  double* binv = h.binv.as<double>();
+  double* K = h.K.as<double>() + (size_t)b0 * h.nmax * h.ld;
+  int32_t* perm = h.ipiv.as<int32_t>() + (size_t)b0 * h.nmax;
+  QPMeta* meta = h.meta.as<QPMeta>() + b0;
+  double* binv = h.binv.as<double>() + (size_t)b0 * NB64 * NB64;
+  dinv += (size_t)b0 * dstride;
   for (int c0 = 0; c0 < npmax; c0 += NB64) {
-    hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv,
-                       dstride, meta, c0, binv);
+    hipLaunchKernelGGL(nlu_diag_kernel, dim3(nb), dim3(PNT), 0, st, K, h.ld, h.nmax, perm, dinv, dstride, meta, c0,
+                       binv);
     DOPT_CHECK_HIP(hipGetLastError());
     const int R2 = npmax - c0 - NB64;
     if (R2 <= 0) break;
     const int nt = (R2 + 63) / 64;
-    const long long tot_s = 2LL * nt * B;
+    const long long tot_s = 2LL * nt * nb;
     if (tot_s > 0x7fffffffLL) throw Error(-1, "no-pivot LU: TRSM grid too large");
-    hipLaunchKernelGGL(nlu_trsm_kernel, dim3((unsigned)tot_s), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta,
-                       c0, binv, nt, (int)tot_s);
+    hipLaunchKernelGGL(nlu_trsm_kernel, dim3((unsigned)tot_s), dim3(256), 0, st, K, h.ld, h.nmax, meta, c0, binv, nt,
+                       (int)tot_s);
     DOPT_CHECK_HIP(hipGetLastError());
-    const long long total = (long long)nt * nt * B;
+    const long long total = (long long)nt * nt * nb;
     if (total > 0x7fffffffLL) throw Error(-1, "no-pivot LU: trailing-update grid too large");
-    hipLaunchKernelGGL(nlu_update_kernel, dim3((unsigned)total), dim3(256), 0, h.stream, K, h.ld, h.nmax,
-                       meta, c0, nt, nt, (int)total);
+    hipLaunchKernelGGL(nlu_update_kernel, dim3((unsigned)total), dim3(256), 0, st, K, h.ld, h.nmax, meta, c0, nt, nt,
+                       (int)total);
     DOPT_CHECK_HIP(hipGetLastError());
   }
+}
+
+// No-pivot blocked LU of every ROUTE_BLOCKED problem, sized by
+// h.blocked_npmax (the read-back of the metadata after the assembly).  The
+// batch is split in two halves on two streams: the diagonal launches are
+// latency-bound (one problem per SIMD, ~85 µs for a 64-block) and use a
+// fraction of the chip, so one half's diagonal block runs under the other
+// half's TRSM / update instead of in series with it.
+void qp_nopiv_factor(Handle& h, double* dinv) {
+  if (h.blocked_npmax == 0) return;
+  const int B = (int)h.batch;
+  h.binv.ensure((size_t)B * NB64 * NB64 * sizeof(double));
+  const int half = B >= 64 ? B / 2 : 0;
+  if (half == 0) {
+    nopiv_chain(h, dinv, 0, B, h.stream);
+    return;
+  }
+  h.ensure_aux_stream();
+  DOPT_CHECK_HIP(hipEventRecord(h.ev_fork, h.stream));
+  DOPT_CHECK_HIP(hipStreamWaitEvent(h.aux_stream, h.ev_fork, 0));
+  nopiv_chain(h, dinv, 0, half, h.stream);
+  nopiv_chain(h, dinv, half, B - half, h.aux_stream);
+  DOPT_CHECK_HIP(hipEventRecord(h.ev_join, h.aux_stream));
+  DOPT_CHECK_HIP(hipStreamWaitEvent(h.stream, h.ev_join, 0));
 }
 
 }  // namespace dopt

@@ -1,7 +1,8 @@
 // Probe: launch time of the no-pivot LU kernels (qp_nopiv.hip, compiled in)
 // on a synthetic batch of diagonally dominant K slabs.
 //   hipcc --offload-arch=gfx950 -O3 -DNLU_STOP=k tools/probe/nlu_probe.hip -o nlu_k
-//   ./nlu_k B NP          → µs per launch of diag / trsm / update at c0 = 0
+//   ./nlu_k B NP          → µs per launch of the first diagonal block and of
+//                           the step kernel at each c0 (same binv: timing only)
 #include "../../diffopt.jl_amd/csrc/qp_nopiv.hip"
 #include <cstdio>
 #include <cstdlib>
@@ -57,24 +58,25 @@ int main(int argc, char** argv) {
       hipEventElapsedTime(&ms, e0, e1);
       if (r) tot += ms;   // rep 0 = warm-up
     }
-    printf("NLU_STOP=%d B=%d Np=%d %-8s %9.2f us/launch\n", NLU_STOP, B, Np, nm, 1e3 * tot / reps);
+    printf("NLU_STOP=%d B=%d Np=%d %-12s %9.2f us/launch\n", NLU_STOP, B, Np, nm, 1e3 * tot / reps);
   };
   timeit("diag", [&] {
     hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
                        dinv_stride(nmax), meta, 0, binv);
   });
   if (NLU_STOP == 99) {
-    // diag once more so binv holds this data's inverse for the TRSM
+    // diag once more so binv holds this data's inverse for the step
     hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, 0, K0, ld, nmax, perm, dinv,
                        dinv_stride(nmax), meta, 0, binv);
-    timeit("trsm", [&] {
-      hipLaunchKernelGGL(nlu_trsm_kernel, dim3(2 * nt * B), dim3(256), 0, 0, K, ld, nmax, meta, 0, binv, nt,
-                         2 * nt * B);
-    });
-    timeit("update", [&] {
-      hipLaunchKernelGGL(nlu_update_kernel, dim3(nt * nt * B), dim3(256), 0, 0, K, ld, nmax, meta, 0, nt, nt,
-                         nt * nt * B);
-    });
+    for (int c0 = 0; c0 + 64 < Np; c0 += 64) {
+      const int R2 = Np - c0 - 64, nrt = (R2 + 127) / 128, nct = (R2 + 63) / 64;
+      char nm[32];
+      snprintf(nm, sizeof nm, "step c0=%d", c0);
+      timeit(nm, [&] {
+        hipLaunchKernelGGL(nlu_step_kernel, dim3(nrt * nct * B), dim3(STP), 0, 0, K, ld, nmax, meta, c0, binv, nrt,
+                           nct, nrt * nct * B);
+      });
+    }
   }
 #ifdef NLU_STAMPS
   {
