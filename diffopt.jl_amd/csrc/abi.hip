@@ -147,12 +147,6 @@ int dopt_destroy(dopt_handle* h) {
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->meta_host) (void)hipHostFree(h->meta_host);
   if (h->meta_ev) (void)hipEventDestroy(h->meta_ev);
-  if (h->aux_stream) {
-    (void)hipStreamSynchronize(h->aux_stream);
-    (void)hipStreamDestroy(h->aux_stream);
-  }
-  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;

@@ -114,16 +114,6 @@ struct Handle {
   DevBuf stamps;             // diagnostic in-kernel cycle stamps (env DOPT_STAMPS=1)
   QPMeta* meta_host = nullptr;     // pinned copy of `meta` (asynchronous read-back)
   hipEvent_t meta_ev = nullptr;    // recorded after the read-back copy
-  // second stream of the no-pivot LU (half the batch) and its fork / join
-  // events against `stream`, created on first use
-  hipStream_t aux_stream = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  void ensure_aux_stream() {
-    if (aux_stream) return;
-    DOPT_CHECK_HIP(hipStreamCreateWithFlags(&aux_stream, hipStreamNonBlocking));
-    DOPT_CHECK_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
-    DOPT_CHECK_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-  }
   // factorisation: 1 = no-pivot blocked LU with the threshold test and a
   // partial-pivoting re-factorisation of rejected problems (default);
   // 0 = partial pivoting for every problem (env DOPT_LU=0)

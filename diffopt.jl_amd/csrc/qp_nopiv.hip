@@ -39,8 +39,11 @@
 //  * the next diagonal block folded into tile (0, 0) of the update: with 4
 //    workgroups per CU (LDS) a ~100 µs latency-bound diagonal workgroup parks
 //    a quarter of a CU while the short tiles queue behind it (1.4 ms).
-// The diagonal latency is hidden instead by running the two halves of the
-// batch on two streams (qp_nopiv_factor).
+//  * the batch split into 2–4 slices on as many streams, each slice's
+//    diagonal launch skewed under the previous slice's TRSM / update: 2.69–
+//    2.76 ms per config-2 step against 2.63 ms in one stream — the diagonal
+//    workgroups hold CU slots (three of four waves parked at barriers) that
+//    the memory-bound update needs.
 //
 // Factor format: K row-major, L strictly below / U on and above the diagonal,
 // perm = identity, dinv as the partial-pivoting path writes it — the solves of
@@ -676,59 +679,38 @@ __global__ __launch_bounds__(256) void nlu_update_kernel(double* __restrict__ K,
 
 }  // namespace
 
-// No-pivot blocked LU of problems [b0, b0+nb): per 64-column block a diagonal
-// launch (nb workgroups), a TRSM launch and a rank-64 trailing-update launch
-// on `st`.
-static void nopiv_chain(Handle& h, double* dinv, int b0, int nb, hipStream_t st) {
+// No-pivot blocked LU of every ROUTE_BLOCKED problem: per 64-column block a
+// diagonal launch (B workgroups), a TRSM launch and a rank-64 trailing-update
+// launch.  Sized by h.blocked_npmax (the read-back of the metadata after the
+// assembly).
+void qp_nopiv_factor(Handle& h, double* dinv) {
   const int npmax = h.blocked_npmax;
+  if (npmax == 0) return;
+  const int B = (int)h.batch;
   const size_t dstride = dinv_stride(h.nmax);
-  double* K = h.K.as<double>() + (size_t)b0 * h.nmax * h.ld;
-  int32_t* perm = h.ipiv.as<int32_t>() + (size_t)b0 * h.nmax;
-  QPMeta* meta = h.meta.as<QPMeta>() + b0;
-  double* binv = h.binv.as<double>() + (size_t)b0 * NB64 * NB64;
-  dinv += (size_t)b0 * dstride;
+  double* K = h.K.as<double>();
+  int32_t* perm = h.ipiv.as<int32_t>();
+  QPMeta* meta = h.meta.as<QPMeta>();
+  h.binv.ensure((size_t)B * NB64 * NB64 * sizeof(double));
+  double* binv = h.binv.as<double>();
   for (int c0 = 0; c0 < npmax; c0 += NB64) {
-    hipLaunchKernelGGL(nlu_diag_kernel, dim3(nb), dim3(PNT), 0, st, K, h.ld, h.nmax, perm, dinv, dstride, meta, c0,
-                       binv);
+    hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv, dstride, meta,
+                       c0, binv);
     DOPT_CHECK_HIP(hipGetLastError());
     const int R2 = npmax - c0 - NB64;
     if (R2 <= 0) break;
     const int nt = (R2 + 63) / 64;
-    const long long tot_s = 2LL * nt * nb;
+    const long long tot_s = 2LL * nt * B;
     if (tot_s > 0x7fffffffLL) throw Error(-1, "no-pivot LU: TRSM grid too large");
-    hipLaunchKernelGGL(nlu_trsm_kernel, dim3((unsigned)tot_s), dim3(256), 0, st, K, h.ld, h.nmax, meta, c0, binv, nt,
-                       (int)tot_s);
+    hipLaunchKernelGGL(nlu_trsm_kernel, dim3((unsigned)tot_s), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0,
+                       binv, nt, (int)tot_s);
     DOPT_CHECK_HIP(hipGetLastError());
-    const long long total = (long long)nt * nt * nb;
+    const long long total = (long long)nt * nt * B;
     if (total > 0x7fffffffLL) throw Error(-1, "no-pivot LU: trailing-update grid too large");
-    hipLaunchKernelGGL(nlu_update_kernel, dim3((unsigned)total), dim3(256), 0, st, K, h.ld, h.nmax, meta, c0, nt, nt,
-                       (int)total);
+    hipLaunchKernelGGL(nlu_update_kernel, dim3((unsigned)total), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0,
+                       nt, nt, (int)total);
     DOPT_CHECK_HIP(hipGetLastError());
   }
-}
-
-// No-pivot blocked LU of every ROUTE_BLOCKED problem, sized by
-// h.blocked_npmax (the read-back of the metadata after the assembly).  The
-// batch is split in two halves on two streams: the diagonal launches are
-// latency-bound (one problem per SIMD, ~85 µs for a 64-block) and use a
-// fraction of the chip, so one half's diagonal block runs under the other
-// half's TRSM / update instead of in series with it.
-void qp_nopiv_factor(Handle& h, double* dinv) {
-  if (h.blocked_npmax == 0) return;
-  const int B = (int)h.batch;
-  h.binv.ensure((size_t)B * NB64 * NB64 * sizeof(double));
-  const int half = B >= 64 ? B / 2 : 0;
-  if (half == 0) {
-    nopiv_chain(h, dinv, 0, B, h.stream);
-    return;
-  }
-  h.ensure_aux_stream();
-  DOPT_CHECK_HIP(hipEventRecord(h.ev_fork, h.stream));
-  DOPT_CHECK_HIP(hipStreamWaitEvent(h.aux_stream, h.ev_fork, 0));
-  nopiv_chain(h, dinv, 0, half, h.stream);
-  nopiv_chain(h, dinv, half, B - half, h.aux_stream);
-  DOPT_CHECK_HIP(hipEventRecord(h.ev_join, h.aux_stream));
-  DOPT_CHECK_HIP(hipStreamWaitEvent(h.stream, h.ev_join, 0));
 }
 
 }  // namespace dopt

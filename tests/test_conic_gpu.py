@@ -192,12 +192,15 @@ def _synthetic_check(ConicBatch, B, n, cones, seed, name, cap=0, trials=3, want_
 
 def test_well_posed_batch(ConicBatch):
     # m > n (unique primal) and LSQR converging (istop 1)
-    _synthetic_check(ConicBatch, 2, 100, [(3, 10)] * 20, 21, "well-posed SOC")
+    # cap 4: LSQR converges (istop 1) but stops at the reference's √eps
+    # tolerance, so two correct runs differ by ≈ cond(M)·1.5e-8 — 4 of the 12
+    # outputs land in (1e-6, 2.8e-6], inside the oracle's 1-ulp envelope (r02)
+    _synthetic_check(ConicBatch, 2, 100, [(3, 10)] * 20, 21, "well-posed SOC", cap=4)
 
 
 def test_mixed_cones_batch(ConicBatch):
     _synthetic_check(ConicBatch, 6, 30, [(0, 3), (1, 10), (3, 6), (2, 4), (4, 6)], 11, "mixed cones",
-                     cap=36)
+                     cap=32)
 
 
 def test_soc_only_batch(ConicBatch):
@@ -211,7 +214,8 @@ def test_psd_blocks_batch(ConicBatch):
 def test_config4_nondegenerate_shape(ConicBatch):
     # config-4 structure (n=500, 20 SOCs) with cone dim 50, so m = 1000 > n and
     # M is non-singular: LSQR converges and the strict bar holds everywhere
-    _synthetic_check(ConicBatch, 2, 500, [(3, 50)] * 20, 14, "config-4 structure, m=1000")
+    # cap 2: converged at √eps as above, 2 of 12 outputs in (1e-6, 4.9e-6] (r02)
+    _synthetic_check(ConicBatch, 2, 500, [(3, 50)] * 20, 14, "config-4 structure, m=1000", cap=2)
 
 
 def test_config4_bench_shape(ConicBatch):
@@ -231,7 +235,7 @@ def test_config5_full_shape(ConicBatch):
     SEED0 + 5: bench.py's first problem), batch 1 — 13 251 unknowns, the split
     (row-block) LSQR path.  dA is not materialised (51 MB per problem)."""
     tally, it_f, it_r, infos = _synthetic_check(ConicBatch, 1, 500, [(4, 1275)] * 10, SEED0 + 5,
-                                                "config-5 full shape", cap=6, trials=1, want_dA=False)
+                                                "config-5 full shape", cap=0, trials=1, want_dA=False)
     print(f"[parity] config-5 LSQR iterations: engine fwd {it_f[0]} rev {it_r[0]}, oracle {infos[0]}")
 
 
@@ -292,6 +296,10 @@ def test_csc_staging_matches_dense_and_oracle(ConicBatch):
         e.close()
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
+    # every problem here stops at maxiter (istop 7) and the oracle's 1-ulp
+    # spread is heavy-tailed: problem 1 (reverse) measured 1.4e-5 as the max
+    # of 3 seeded perturbations but 1.6e-3 as the max of 20 — the envelope
+    # takes 20
     tally = Tally("CSC staging")
     for b in range(3):
         cache = ocn.Cache(A[b], d["b"][b], d["c"][b], d["x"][b], d["s"][b], d["y"][b], cones)
@@ -302,9 +310,10 @@ def test_csc_staging_matches_dense_and_oracle(ConicBatch):
             _, a, v, w = ocn.forward_differentiate(cache, None, db_, dc_)
             return np.concatenate([a, v, [w]])
         tally.check(relfro(outs[1][0][b], ref),
-                    lambda: envelope(fsolve, [d["db"][b], d["dc"][b]], ref, relfro), (b, "fwd"))
+                    lambda: envelope(fsolve, [d["db"][b], d["dc"][b]], ref, relfro, trials=20), (b, "fwd"))
         tally.check(relfro(outs[1][2][b], og), lambda: envelope(
-            lambda dx_: ocn.reverse_differentiate(cache, dx_)[0], [d["dx"][b]], og, relfro), (b, "rev"))
+            lambda dx_: ocn.reverse_differentiate(cache, dx_)[0], [d["dx"][b]], og, relfro, trials=20),
+            (b, "rev"))
     tally.report(6)
     e = ConicBatch(1, 20, cones)
     bad = sp.csc_matrix(A[0])
@@ -327,11 +336,11 @@ def SplitConicBatch(ConicBatch, monkeypatch):
 
 def test_split_mixed_cones_batch(SplitConicBatch):
     _synthetic_check(SplitConicBatch, 6, 30, [(0, 3), (1, 10), (3, 6), (2, 4), (4, 6)], 11,
-                     "split: mixed cones", cap=36)
+                     "split: mixed cones", cap=32)
 
 
 def test_split_well_posed_batch(SplitConicBatch):
-    _synthetic_check(SplitConicBatch, 2, 100, [(3, 10)] * 20, 21, "split: well-posed SOC")
+    _synthetic_check(SplitConicBatch, 2, 100, [(3, 10)] * 20, 21, "split: well-posed SOC", cap=0)
 
 
 def test_split_psd_blocks_batch(SplitConicBatch):
@@ -364,4 +373,4 @@ def test_split_matches_persistent_kernel(ConicBatch, monkeypatch):
 def test_config5_structure_multi_rowblock(ConicBatch):
     # config-5 structure (PSD(50) cones, m ≫ n) at oracle speed: 3 PSD(50)
     # → m = 3825 = 8 row blocks, auto split path
-    _synthetic_check(ConicBatch, 2, 100, [(4, 1275)] * 3, 16, "config-5 structure, 3 cones", cap=12)
+    _synthetic_check(ConicBatch, 2, 100, [(4, 1275)] * 3, 16, "config-5 structure, 3 cones", cap=1)
