@@ -130,7 +130,7 @@ int dopt_destroy(dopt_handle* h) {
   if (!h) return 0;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  DevBuf* bufs[] = {&h->dinv, &h->plist, &h->lsqr_ws, &h->binv, &h->K, &h->ipiv, &h->s, &h->kidx, &h->meta, &h->rhs,
+  DevBuf* bufs[] = {&h->dinv, &h->plist, &h->lsqr_ws, &h->binv, &h->fwdw, &h->K, &h->ipiv, &h->s, &h->kidx, &h->meta, &h->rhs,
                     &h->x, &h->cone_dev, &h->vp, &h->dpi, &h->cwork, &h->cinfo, &h->csplit};
   for (auto* b : bufs) b->release();
   for (auto& b : h->own_in) b.release();

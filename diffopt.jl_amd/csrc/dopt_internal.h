@@ -111,6 +111,7 @@ struct Handle {
   DevBuf plist;              // problem indices of the partial-pivoting re-factorisation
   DevBuf lsqr_ws;            // LSQR vectors of the `iterative` branch (5 per problem)
   DevBuf binv;               // no-pivot LU: packed 64×64 inverse of the current diagonal block
+  DevBuf fwdw;               // fused call: both right-hand sides, forward-swept inside the no-pivot LU
   DevBuf stamps;             // diagnostic in-kernel cycle stamps (env DOPT_STAMPS=1)
   QPMeta* meta_host = nullptr;     // pinned copy of `meta` (asynchronous read-back)
   hipEvent_t meta_ev = nullptr;    // recorded after the read-back copy
@@ -208,11 +209,12 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
 //   qp_blocked.hip  partial-pivoting blocked LU (the re-factorisation of the
 //                   rejected problems, `plist`; every problem when lu_mode = 0)
 //                   and the triangular solves shared by both
-void qp_nopiv_factor(Handle& h, double* dinv);
+void qp_nopiv_factor(Handle& h, double* dinv, double* w0 = nullptr, double* w1 = nullptr);
 void qp_blocked_factor(Handle& h, double* dinv, const int32_t* plist, int count);
 void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rhs, double* x, int sel);
 void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, const double* rhs_fwd,
-                       double* x_rev, double* x_fwd, int sel);
+                       double* x_rev, double* x_fwd, int sel, const double* w_rev = nullptr,
+                       const double* w_fwd = nullptr);
 size_t dinv_stride(int nmax);
 void conic_factor(Handle& h);
 void conic_forward(Handle& h, const double* dA, const double* db, const double* dc,

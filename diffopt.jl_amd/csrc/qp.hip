@@ -732,11 +732,11 @@ static void generic_lu(Handle& h) {
 // before the host waits for the rejected list: work that skips rejected
 // problems (the solves of the fused call).
 template <class F>
-static void factor_blocked(Handle& h, F&& spec) {
+static void factor_blocked(Handle& h, F&& spec, double* w0 = nullptr, double* w1 = nullptr) {
   if (h.lu_mode == 1) {
     {
       PhaseTimer pt(h, DOPT_PHASE_QP_LU);
-      qp_nopiv_factor(h, dinv_of(h));
+      qp_nopiv_factor(h, dinv_of(h), w0, w1);
     }
     if (h.blocked_npmax) meta_copy(h);
     spec();
@@ -899,12 +899,24 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
   rev_rhs(h, dl_dz);
   fwd_rhs(h, T);
   meta_sizes(h);
-  auto solve2 = [&](int sel) {
+  // no-pivot LU: both right-hand sides ride along as a bordering column / row
+  // and come out forward-swept (w0, w1), leaving the solves the backward
+  // sweeps; rhs itself stays intact for the partial-pivoting re-solve
+  double *w0 = nullptr, *w1 = nullptr;
+  if (h.lu_mode == 1 && h.blocked_npmax) {
+    const size_t len = (size_t)h.batch * h.nmax;
+    h.fwdw.ensure(2 * len * sizeof(double));
+    w0 = h.fwdw.as<double>();
+    w1 = w0 + len;
+    DOPT_CHECK_HIP(hipMemcpyAsync(w0, rhs_of(h, 0), len * sizeof(double), hipMemcpyDeviceToDevice, h.stream));
+    DOPT_CHECK_HIP(hipMemcpyAsync(w1, rhs_of(h, 1), len * sizeof(double), hipMemcpyDeviceToDevice, h.stream));
+  }
+  auto solve2 = [&](int sel, const double* sw0, const double* sw1) {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
-    qp_blocked_solve2(h, dinv_of(h), rhs_of(h, 0), rhs_of(h, 1), x_of(h, 0), x_of(h, 1), sel);
+    qp_blocked_solve2(h, dinv_of(h), rhs_of(h, 0), rhs_of(h, 1), x_of(h, 0), x_of(h, 1), sel, sw0, sw1);
   };
-  factor_blocked(h, [&] { solve2(h.lu_mode == 1 ? LU_SEL_NOPIV : LU_SEL_ALL); });
-  if (h.n_pivot > 0) solve2(LU_SEL_PIVOT);
+  factor_blocked(h, [&] { solve2(h.lu_mode == 1 ? LU_SEL_NOPIV : LU_SEL_ALL, w0, w1); }, w0, w1);
+  if (h.n_pivot > 0) solve2(LU_SEL_PIVOT, nullptr, nullptr);
   finish(h, 0, out_rev);
   finish(h, 1, out_fwd);
   h.factored = true;   // the factors stay valid for later reverse / forward calls

@@ -454,7 +454,7 @@ __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict_
                                                 const QPMeta* __restrict__ meta, int trans, int sel,
                                                 const double* __restrict__ rhs,
                                                 double* __restrict__ xout, double* v, double* y, int* ps,
-                                                double* part) {
+                                                double* part, int sweep0 = 0) {
   const QPMeta mm = meta[b];
   const int Np = blocked_np(mm);
   if (Np == 0 || !((sel >> mm.lu) & 1)) return;
@@ -472,7 +472,7 @@ __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict_
   for (int i = t; i < Np; i += PT) v[i] = trans ? y[i] : y[ps[i]];
   __syncthreads();
   const int nblk = Np / BNB;
-  for (int sweep = 0; sweep < 2; ++sweep) {
+  for (int sweep = sweep0; sweep < 2; ++sweep) {
     const bool fwd = sweep == 0;
     const bool useU = (sweep == 1) != (trans != 0);
     for (int s = 0; s < nblk; ++s) {
@@ -562,7 +562,7 @@ __device__ __forceinline__ void solve_rows_body(int b, const double* __restrict_
                                                 const QPMeta* __restrict__ meta, int sel,
                                                 const double* __restrict__ rhs,
                                                 double* __restrict__ xout, double* v, int* ps,
-                                                double* part) {
+                                                double* part, int sweep0 = 0) {
   const QPMeta mm = meta[b];
   const int Np = blocked_np(mm);
   if (Np == 0 || !((sel >> mm.lu) & 1)) return;
@@ -580,7 +580,7 @@ __device__ __forceinline__ void solve_rows_body(int b, const double* __restrict_
   }
   __syncthreads();
   const int nblk = Np / BNB;
-  for (int sweep = 0; sweep < 2; ++sweep) {
+  for (int sweep = sweep0; sweep < 2; ++sweep) {
     const bool fwd = sweep == 0;
     for (int s = 0; s < nblk; ++s) {
       const int bk = fwd ? s : nblk - 1 - s;
@@ -654,7 +654,10 @@ __global__ __launch_bounds__(PT) void blu_solve_rows_kernel(const double* __rest
 // slices), so the two sweeps over each problem's factors run concurrently and
 // the second direction's reads hit L2 / MALL (blocks L and L+B share an XCD
 // when B is a multiple of 8).  Same per-problem code as the one-direction
-// kernels, hence bit-identical results.
+// kernels.  w_rev / w_fwd (fused call, else null): the right-hand sides
+// forward-swept inside the no-pivot LU (qp_nopiv.hip fwd_block) — its
+// problems run only the backward sweeps from them; partial-pivoting problems
+// solve from rhs_rev / rhs_fwd in full.
 template <int ENT>
 __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict__ K, int ld, int nmax,
                                                         const int32_t* __restrict__ perm,
@@ -664,7 +667,9 @@ __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict
                                                         const double* __restrict__ rhs_rev,
                                                         const double* __restrict__ rhs_fwd,
                                                         double* __restrict__ x_rev,
-                                                        double* __restrict__ x_fwd) {
+                                                        double* __restrict__ x_fwd,
+                                                        const double* __restrict__ w_rev,
+                                                        const double* __restrict__ w_fwd) {
   __shared__ double v[BLOCKED_MAX];
   __shared__ double y[BLOCKED_MAX];
   __shared__ int ps[BLOCKED_MAX];
@@ -674,11 +679,14 @@ __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict
     const int g = L >> 4, j = L & 7;
     L = (L & 8) ? B + 8 * g + j : 8 * g + j;
   }
+  const int pb = L < B ? L : L - B;
+  const bool swept = w_rev && meta[pb].lu == LU_NOPIV;
   if (L < B)
-    solve_rows_body(L, K, ld, nmax, perm, dinv, dstride, meta, sel, rhs_rev, x_rev, v, ps, part);
+    solve_rows_body(L, K, ld, nmax, perm, dinv, dstride, meta, sel, swept ? w_rev : rhs_rev, x_rev, v, ps, part,
+                    swept ? 1 : 0);
   else
-    solve_cols_body<ENT>(L - B, K, ld, nmax, perm, dinv, dstride, meta, 1, sel, rhs_fwd, x_fwd, v,
-                         y, ps, part);
+    solve_cols_body<ENT>(L - B, K, ld, nmax, perm, dinv, dstride, meta, 1, sel, swept ? w_fwd : rhs_fwd, x_fwd, v,
+                         y, ps, part, swept ? 1 : 0);
 }
 
 }  // namespace
@@ -767,7 +775,7 @@ void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rh
 }
 
 void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, const double* rhs_fwd,
-                       double* x_rev, double* x_fwd, int sel) {
+                       double* x_rev, double* x_fwd, int sel, const double* w_rev, const double* w_fwd) {
   const int npmax = h.blocked_npmax;
   if (npmax == 0) return;
   const int B = (int)h.batch;
@@ -779,7 +787,7 @@ void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, con
   const int ent = (npmax + PT - 1) / PT;
 #define DOPT_SOLVE2(E)                                                                            \
   hipLaunchKernelGGL(blu_solve2_kernel<E>, dim3(2 * B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm, \
-                     dinv, dstride, meta, B, sel, rhs_rev, rhs_fwd, x_rev, x_fwd)
+                     dinv, dstride, meta, B, sel, rhs_rev, rhs_fwd, x_rev, x_fwd, w_rev, w_fwd)
   if (ent <= 1) DOPT_SOLVE2(1);
   else if (ent == 2) DOPT_SOLVE2(2);
   else DOPT_SOLVE2(3);

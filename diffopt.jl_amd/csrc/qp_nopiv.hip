@@ -232,15 +232,51 @@ struct DiagLds {
   double* rowb;   // 32
   double* colb;   // 32
   int* sbad;
-  // all four inside one 64 × ULD buffer (ULD below), past the 64 × SLD image
+  double* vec;    // 128: the right-hand-side blocks of the fused forward sweeps
+  // all inside one 64 × ULD buffer (ULD below), past the 64 × SLD image
   __device__ explicit DiagLds(double* buf)
       : S(buf), rowb(buf + NB64 * SLD), colb(buf + NB64 * SLD + 32),
-        sbad(reinterpret_cast<int*>(buf + NB64 * SLD + 64)) {}
+        sbad(reinterpret_cast<int*>(buf + NB64 * SLD + 64)), vec(buf + NB64 * SLD + 72) {}
 };
+
+// Fused forward sweeps (the batched forward+reverse call): with the packed
+// inverse of the diagonal block in S, replace block c0 of the reverse RHS w0
+// (K x = b: L y = b) by L11⁻¹ b_k and block c0 of the forward RHS w1
+// (Kᵀ x = c: Uᵀ y = c) by c_k U11⁻¹.  Entries past N (identity padding) are
+// read as 0.  The trailing update subtracts L21·b′ / c′·U12 from the later
+// blocks (nlu_update_kernel), so after the factorisation w0 / w1 hold the
+// forward-swept vectors and the solves run only the backward sweeps.
+__device__ __forceinline__ void fwd_block(const DiagLds& L, double* __restrict__ w0b, double* __restrict__ w1b,
+                                          int c0, int N, int Wv) {
+  const double* S = L.S;
+  double* v = L.vec;
+  const int t = threadIdx.x;
+  if (t < 128) {
+    const int i = t & 63;
+    const bool in = i < Wv && c0 + i < N;
+    v[t] = in ? (t < 64 ? w0b : w1b)[c0 + i] : 0.0;
+  }
+  __syncthreads();
+  if (t < 64) {   // b′_i = b_i + Σ_{j<i} (L11⁻¹)_ij b_j  (one row per lane)
+    double acc = v[t];
+#pragma unroll 8
+    for (int j = 0; j < NB64; ++j)
+      if (j < t) acc = fma(S[t * SLD + j], v[j], acc);
+    if (t < Wv) w0b[c0 + t] = acc;
+  } else if (t < 128) {   // c′_j = Σ_{i≤j} c_i (U11⁻¹)_ij  (one column per lane)
+    const int j = t - 64;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int i = 0; i < NB64; ++i)
+      if (i <= j) acc = fma(v[64 + i], S[i * SLD + j], acc);
+    if (j < Wv) w1b[c0 + j] = acc;
+  }
+}
 
 __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__ Kb, int ld,
                                           int32_t* __restrict__ permb, double* __restrict__ Db,
-                                          QPMeta* __restrict__ mb, int c0, int Np, double* __restrict__ Bg) {
+                                          QPMeta* __restrict__ mb, int c0, int Np, int N, double* __restrict__ Bg,
+                                          double* __restrict__ w0b, double* __restrict__ w1b) {
   double* S = L.S;
   const int Wv = min(NB64, Np - c0);   // 32 or 64
   const bool trsm = Np - c0 > NB64;    // a trailing step follows
@@ -327,7 +363,10 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
     return;
   }
   NLU_MARK(2);
-  if (Wv < NB64) return;   // a 32-wide last block: done (no trailing step follows)
+  if (Wv < NB64) {   // a 32-wide last block: done (no trailing step follows)
+    if (w0b) fwd_block(L, w0b, w1b, c0, N, Wv);   // S: L_aa⁻¹ \ U_aa⁻¹, identity frame
+    return;
+  }
   if (NLU_STOP <= 3) return;
 
   // ---- C. A_bb −= L_ba U_ab (one 16×16 tile per wave); U_ab, L_ba → K
@@ -359,7 +398,7 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
   }
   NLU_MARK(4);
   to_K(32, 32);
-  if (!trsm) {   // last block: only the solves' dinv of block b
+  if (!trsm && !w0b) {   // last block, nothing to sweep: only the solves' dinv of block b
     if (wv < 2 && lane < 32) {
       double x[32];
       if (wv == 0) lower_inv_col(S, 32, lane, x);
@@ -443,8 +482,10 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
   }
   __syncthreads();
   NLU_MARK(6);
-  // ---- G. the packed 64×64 inverse → Bg (row-major, coalesced)
-  for (int e = t; e < NB64 * NB64; e += PNT) Bg[e] = S[(e >> 6) * SLD + (e & 63)];
+  // ---- G. the packed 64×64 inverse → Bg (row-major, coalesced), for the TRSM
+  if (trsm)
+    for (int e = t; e < NB64 * NB64; e += PNT) Bg[e] = S[(e >> 6) * SLD + (e & 63)];
+  if (w0b) fwd_block(L, w0b, w1b, c0, N, Wv);
   NLU_MARK(7);
 }
 
@@ -459,7 +500,8 @@ static_assert(NB64 * SLD + 64 + 1 <= STEP_LDS, "diagonal image + rowb/colb/sbad 
 // problem, 40 KB of LDS: 4 per CU, a 1024-problem batch runs in one round.
 __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_diag_kernel(
     double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
-    size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv) {
+    size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv, double* __restrict__ w0,
+    double* __restrict__ w1) {
   __shared__ double S[STEP_LDS];
   const int b = blockIdx.x;
   const QPMeta mm = meta[b];
@@ -488,7 +530,8 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
   if (t == 0 && c0 == 0) meta[b].lu = LU_NOPIV;   // LU_REJECT below if a test fails
   NLU_MARK(0);
   diag_core(DiagLds(S), Kb, ld, perm + (size_t)b * nmax, dinv + (size_t)b * dstride + (size_t)(c0 / 32) * DBLK,
-            meta + b, c0, Np, binv + (size_t)b * NB64 * NB64);
+            meta + b, c0, Np, mm.nsys, binv + (size_t)b * NB64 * NB64, w0 ? w0 + (size_t)b * nmax : nullptr,
+            w0 ? w1 + (size_t)b * nmax : nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -613,7 +656,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 
 __global__ __launch_bounds__(256) void nlu_update_kernel(double* __restrict__ K, int ld, int nmax,
                                                          const QPMeta* __restrict__ meta, int c0,
-                                                         int nrt, int nct, int total) {
+                                                         int nrt, int nct, int total, double* __restrict__ w0,
+                                                         double* __restrict__ w1) {
   __shared__ double U[NB64 * ULD];
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
@@ -659,7 +703,23 @@ __global__ __launch_bounds__(256) void nlu_update_kernel(double* __restrict__ K,
     }
   }
   __syncthreads();
+  if (w1 && rt == 0 && wv == 0) {   // fused forward sweep of Kᵀ: c_J −= c′ U12_J (a column per lane)
+    const double* cp = w1 + (size_t)b * nmax + c0;   // c′ of this step (diagonal kernel)
+    double cs = 0.0;
+#pragma unroll 8
+    for (int k = 0; k < NB64; ++k) cs = fma(cp[k], U[k * ULD + lane], cs);
+    if (lane < 16 * nq) w1[(size_t)b * nmax + cbase + lane] -= cs;
+  }
   if (!wact) return;
+  if (w0 && ct == 0) {   // fused forward sweep of K: b_I −= L21_I b′ (a = −L21)
+    const double* bp = w0 + (size_t)b * nmax + c0;
+    double ps = 0.0;
+#pragma unroll
+    for (int s = 0; s < NB64 / 4; ++s) ps = fma(a[s], bp[4 * s + g], ps);
+    ps += __shfl_xor(ps, 16);
+    ps += __shfl_xor(ps, 32);
+    if (g == 0) w0[(size_t)b * nmax + rbase + l16] += ps;
+  }
 #pragma unroll
   for (int s = 0; s < NB64 / 4; ++s) {
     double bq[4];
@@ -682,8 +742,9 @@ __global__ __launch_bounds__(256) void nlu_update_kernel(double* __restrict__ K,
 // No-pivot blocked LU of every ROUTE_BLOCKED problem: per 64-column block a
 // diagonal launch (B workgroups), a TRSM launch and a rank-64 trailing-update
 // launch.  Sized by h.blocked_npmax (the read-back of the metadata after the
-// assembly).
-void qp_nopiv_factor(Handle& h, double* dinv) {
+// assembly).  w0 / w1 (both or neither): the reverse / forward right-hand
+// sides, forward-swept in place along the way (fwd_block).
+void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   const int npmax = h.blocked_npmax;
   if (npmax == 0) return;
   const int B = (int)h.batch;
@@ -695,7 +756,7 @@ void qp_nopiv_factor(Handle& h, double* dinv) {
   double* binv = h.binv.as<double>();
   for (int c0 = 0; c0 < npmax; c0 += NB64) {
     hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv, dstride, meta,
-                       c0, binv);
+                       c0, binv, w0, w1);
     DOPT_CHECK_HIP(hipGetLastError());
     const int R2 = npmax - c0 - NB64;
     if (R2 <= 0) break;
@@ -708,7 +769,7 @@ void qp_nopiv_factor(Handle& h, double* dinv) {
     const long long total = (long long)nt * nt * B;
     if (total > 0x7fffffffLL) throw Error(-1, "no-pivot LU: trailing-update grid too large");
     hipLaunchKernelGGL(nlu_update_kernel, dim3((unsigned)total), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0,
-                       nt, nt, (int)total);
+                       nt, nt, (int)total, w0, w1);
     DOPT_CHECK_HIP(hipGetLastError());
   }
 }

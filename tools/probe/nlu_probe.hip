@@ -2,7 +2,7 @@
 // on a synthetic batch of diagonally dominant K slabs.
 //   hipcc --offload-arch=gfx950 -O3 -DNLU_STOP=k tools/probe/nlu_probe.hip -o nlu_k
 //   ./nlu_k B NP          → µs per launch of the first diagonal block and of
-//                           the step kernel at each c0 (same binv: timing only)
+//                           the TRSM / update at each c0 (same binv: timing only)
 #include "../../diffopt.jl_amd/csrc/qp_nopiv.hip"
 #include <cstdio>
 #include <cstdlib>
@@ -62,19 +62,24 @@ int main(int argc, char** argv) {
   };
   timeit("diag", [&] {
     hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
-                       dinv_stride(nmax), meta, 0, binv);
+                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr);
   });
   if (NLU_STOP == 99) {
     // diag once more so binv holds this data's inverse for the step
     hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, 0, K0, ld, nmax, perm, dinv,
-                       dinv_stride(nmax), meta, 0, binv);
+                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr);
     for (int c0 = 0; c0 + 64 < Np; c0 += 64) {
-      const int R2 = Np - c0 - 64, nrt = (R2 + 127) / 128, nct = (R2 + 63) / 64;
+      const int nt = (Np - c0 - 64 + 63) / 64;
       char nm[32];
-      snprintf(nm, sizeof nm, "step c0=%d", c0);
+      snprintf(nm, sizeof nm, "trsm c0=%d", c0);
       timeit(nm, [&] {
-        hipLaunchKernelGGL(nlu_step_kernel, dim3(nrt * nct * B), dim3(STP), 0, 0, K, ld, nmax, meta, c0, binv, nrt,
-                           nct, nrt * nct * B);
+        hipLaunchKernelGGL(nlu_trsm_kernel, dim3(2 * nt * B), dim3(256), 0, 0, K, ld, nmax, meta, c0, binv, nt,
+                           2 * nt * B);
+      });
+      snprintf(nm, sizeof nm, "update c0=%d", c0);
+      timeit(nm, [&] {
+        hipLaunchKernelGGL(nlu_update_kernel, dim3(nt * nt * B), dim3(256), 0, 0, K, ld, nmax, meta, c0, nt, nt,
+                           nt * nt * B, nullptr, nullptr);
       });
     }
   }
@@ -85,7 +90,7 @@ int main(int argc, char** argv) {
     hipMemcpy(K, K0, hK.size() * 8, hipMemcpyDeviceToDevice);
     hipMemcpy(meta, hm.data(), B * sizeof(QPMeta), hipMemcpyHostToDevice);
     hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
-                       dinv_stride(nmax), meta, 0, binv);
+                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr);
     hipDeviceSynchronize();
     hipMemcpyFromSymbol(st, HIP_SYMBOL(nlu_stamps), sizeof(st));
     const char* nm[8] = {"load", "A lu_a", "B inv/trsm", "C schur", "D lu_b", "E inv_b/T", "F offdiag", "G binv"};
