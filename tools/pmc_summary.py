@@ -5,6 +5,10 @@ HBM bytes per launch per engine kernel.
 
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports ½ of the
 bytes of wide coalesced reads → doubled here; WRITE_SIZE is taken as is.
+Calibrated per access width on this machine (tools/probe/pmc_cal.hip,
+tools/pmc_calibrate.py → profiles/pmc_calibration.json): 4-, 8- and 16-byte
+per-lane streaming loads and the LU's 4-row × 128-B pattern all read as 0.500
+of the streamed bytes, 4-, 8- and 16-byte stores as 1.000 — one factor each.
 FETCH_SIZE/WRITE_SIZE are in KB (rocprofv3 derived counters) → ×1024.
 
   python tools/pmc_summary.py <fetch_dir> <write_dir> <out.json>   (merges into out.json)
@@ -30,7 +34,8 @@ KERNEL_PHASE = {
 # update sequence of one factorisation, the two solve kernels of one step);
 # summed over the dispatches and divided by the number of steps, counted by
 # the per-step qp_prep_asm_kernel dispatch
-QP_GROUPS = {"qp_lu": ("blu_panel_kernel", "blu_update_kernel"),
+QP_GROUPS = {"qp_lu": ("nlu_diag_kernel", "nlu_trsm_kernel", "nlu_update_kernel", "blu_panel_kernel",
+                       "blu_update_kernel"),
              "qp_solve": ("blu_solve_kernel", "blu_solve_rows_kernel", "blu_solve2_kernel")}
 QP_STEP = "qp_prep_asm_kernel"
 # split-path LSQR: every conic_split_* dispatch belongs to the LSQR call opened
