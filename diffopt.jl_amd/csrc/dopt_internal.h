@@ -112,7 +112,6 @@ struct Handle {
   DevBuf lsqr_ws;            // LSQR vectors of the `iterative` branch (5 per problem)
   DevBuf binv;               // no-pivot LU: packed 64×64 inverse of the current diagonal block
   DevBuf fwdw;               // fused call: both right-hand sides, forward-swept inside the no-pivot LU
-  DevBuf stamps;             // diagnostic in-kernel cycle stamps (env DOPT_STAMPS=1)
   QPMeta* meta_host = nullptr;     // pinned copy of `meta` (asynchronous read-back)
   hipEvent_t meta_ev = nullptr;    // recorded after the read-back copy
   // factorisation: 1 = no-pivot blocked LU with the threshold test and a
