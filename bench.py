@@ -392,7 +392,9 @@ def main():
                         unit="TFLOP/s", frac=round(achieved / PEAK_FP64_TFLOPS, 4))
         else:
             if name == "qp_solve":
-                work = float((16.0 * Ns ** 2).sum())              # both directions read the factors
+                # both directions' backward sweeps (the forward sweeps run
+                # inside the no-pivot LU): each reads half of K, 8·N'² together
+                work = float((8.0 * Ns ** 2).sum())
             elif name == "qp_assemble":
                 work = float(B * 8.0 * (n * n + 2 * m * n) + (8.0 * Ns ** 2).sum())
             else:
@@ -401,7 +403,10 @@ def main():
             roof = dict(bound="hbm", achieved=round(achieved, 1), peak=PEAK_HBM_GBS,
                         unit="GB/s", frac=round(achieved / PEAK_HBM_GBS, 4))
         roof["kernel"] = name
-        roof["traffic"] = _load_pmc(name if args.config == 2 else f"{name}@cfg{args.config}")
+        # PMC bytes per launch measured for this workload (profiles/pmc_latest.json:
+        # config 2 unsuffixed, others @cfgN, the --lam-eps worst case @lam), or null
+        pkey = name if args.config == 2 else f"{name}@cfg{args.config}"
+        roof["traffic"] = _load_pmc(pkey + "@lam" if args.lam_eps > 0 else pkey)
         roof["avg_launch_ms"] = round(avg_s * 1e3, 4)
         roof["phases_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in sorted(phases.items())}
         value = world * B * args.steps / elapsed
