@@ -657,15 +657,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 __global__ __launch_bounds__(256) void nlu_update_kernel(double* __restrict__ K, int ld, int nmax,
                                                          const QPMeta* __restrict__ meta, int c0,
                                                          int nrt, int nct, int total, double* __restrict__ w0,
-                                                         double* __restrict__ w1) {
+                                                         double* __restrict__ w1, int cross) {
   __shared__ double U[NB64 * ULD];
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
   const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
-  const int tiles = nrt * nct;
+  // cross = 1: only the tiles of block row 0 and block column 0 (2·nct − 1 per
+  // problem, nrt = nct) — the first half of a paired step (nlu_update2_kernel)
+  const int tiles = cross ? 2 * nct - 1 : nrt * nct;
   const int b = logical / tiles;
   const int tile = logical - b * tiles;
-  const int rt = tile / nct, ct = tile - rt * nct;
+  const int rt = cross ? (tile < nct ? 0 : tile - nct + 1) : tile / nct;
+  const int ct = cross ? (tile < nct ? tile : 0) : tile - rt * nct;
   const QPMeta mm = meta[b];
   const int Np = nlu_np(mm);
   const int R2 = Np - c0 - NB64;               // trailing rows = columns (multiple of 32)
@@ -737,11 +740,124 @@ __global__ __launch_bounds__(256) void nlu_update_kernel(double* __restrict__ K,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Second half of a paired block step (steps c0 and c0+64): the trailing
+// tiles from c0+128 take both rank-64 updates in one pass,
+//   A22 −= L21⁽ᵏ⁾·U12⁽ᵏ⁾ + L21⁽ᵏ⁺¹⁾·U12⁽ᵏ⁺¹⁾,
+// after the cross update of step c0 (nlu_update_kernel, cross = 1) and the
+// diagonal block and TRSM of step c0+64 — so the trailing matrix is read and
+// written once per two steps.  U12⁽ᵏ⁾ / U12⁽ᵏ⁺¹⁾ are staged in turn through
+// one 40 KB LDS tile.  Tiles (I, 0) / (0, J) of this grid also carry the
+// fused forward sweeps of step c0+64.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_update2_kernel(double* __restrict__ K, int ld, int nmax,
+                                                          const QPMeta* __restrict__ meta, int c0, int nrt,
+                                                          int nct, int total, double* __restrict__ w0,
+                                                          double* __restrict__ w1) {
+  __shared__ double U[NB64 * ULD];
+  const int L = blockIdx.x;
+  const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
+  const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
+  const int tiles = nrt * nct;
+  const int b = logical / tiles;
+  const int tile = logical - b * tiles;
+  const int rt = tile / nct, ct = tile - rt * nct;
+  const QPMeta mm = meta[b];
+  const int Np = nlu_np(mm);
+  const int R2 = Np - c0 - 2 * NB64;   // rows = columns after both steps (multiple of 32)
+  if (mm.lu == LU_REJECT || rt * 64 >= R2 || ct * 64 >= R2) return;   // workgroup-uniform
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
+  double* Kb = K + (size_t)b * nmax * ld;
+  const int cbase = c0 + 2 * NB64 + ct * 64;
+  const int cend = c0 + 2 * NB64 + R2;
+  const int rbase = c0 + 2 * NB64 + rt * 64 + 16 * wv;
+  const bool wact = rt * 64 + 16 * wv < R2;   // wave-uniform
+  const int nq = min(4, (R2 - ct * 64) >> 4);
+  auto stage = [&](int k0) {   // U12 rows k0 .. k0+63, columns cbase .. cbase+63
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = 32 * h + (t >> 3), c8 = (t & 7) * 8;
+      const bool ok = cbase + c8 < cend;   // 32-aligned halves: all-or-nothing
+      const double* src = Kb + (size_t)(k0 + k) * ld + (ok ? cbase + c8 : 0);
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) U[k * ULD + c8 + u] = ok ? v[u] : 0.0;
+    }
+  };
+  double a[NB64 / 4];
+  d4n acc[4];
+  stage(c0);
+  if (wact) {
+    const double* arow = Kb + (size_t)(rbase + l16) * ld + c0;
+#pragma unroll
+    for (int s = 0; s < NB64 / 4; ++s) a[s] = -arow[4 * s + g];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int cq = cbase + 16 * min(q, nq - 1) + l16;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) acc[q][rr] = Kb[(size_t)(rbase + g + 4 * rr) * ld + cq];
+    }
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int half = 0; half < 2; ++half) {
+    if (wact) {
+#pragma unroll
+      for (int s = 0; s < NB64 / 4; ++s) {
+        double bq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bq[q] = U[(4 * s + g) * ULD + 16 * q + l16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = nmfma(a[s], bq[q], acc[q]);
+      }
+    }
+    if (half == 1) break;
+    __syncthreads();   // every wave is done with U12⁽ᵏ⁾
+    stage(c0 + NB64);
+    if (wact) {
+      const double* arow = Kb + (size_t)(rbase + l16) * ld + c0 + NB64;
+#pragma unroll
+      for (int s = 0; s < NB64 / 4; ++s) a[s] = -arow[4 * s + g];
+    }
+    __syncthreads();
+  }
+  // fused forward sweeps of step c0+64 (its c′ / b′ written by its diagonal launch)
+  if (w1 && rt == 0 && wv == 0) {
+    const double* cp = w1 + (size_t)b * nmax + c0 + NB64;
+    double cs = 0.0;
+#pragma unroll 8
+    for (int k = 0; k < NB64; ++k) cs = fma(cp[k], U[k * ULD + lane], cs);
+    if (lane < 16 * nq) w1[(size_t)b * nmax + cbase + lane] -= cs;
+  }
+  if (!wact) return;
+  if (w0 && ct == 0) {
+    const double* bp = w0 + (size_t)b * nmax + c0 + NB64;
+    double ps = 0.0;
+#pragma unroll
+    for (int s = 0; s < NB64 / 4; ++s) ps = fma(a[s], bp[4 * s + g], ps);
+    ps += __shfl_xor(ps, 16);
+    ps += __shfl_xor(ps, 32);
+    if (g == 0) w0[(size_t)b * nmax + rbase + l16] += ps;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q < nq) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) Kb[(size_t)(rbase + g + 4 * rr) * ld + cbase + 16 * q + l16] = acc[q][rr];
+    }
+  }
+}
+
 }  // namespace
 
 // No-pivot blocked LU of every ROUTE_BLOCKED problem: per 64-column block a
-// diagonal launch (B workgroups), a TRSM launch and a rank-64 trailing-update
-// launch.  Sized by h.blocked_npmax (the read-back of the metadata after the
+// diagonal launch (B workgroups) and a TRSM launch; the trailing updates go
+// in pairs of steps (h.lu_pair, default): step c0 updates only its cross
+// band, step c0+64's diagonal block and TRSM follow, one rank-128 pass
+// updates the rest — a third less trailing-matrix traffic than one rank-64
+// pass per step.  Sized by h.blocked_npmax (the read-back of the metadata after the
 // assembly).  w0 / w1 (both or neither): the reverse / forward right-hand
 // sides, forward-swept in place along the way (fwd_block).
 void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
@@ -754,23 +870,49 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   QPMeta* meta = h.meta.as<QPMeta>();
   h.binv.ensure((size_t)B * NB64 * NB64 * sizeof(double));
   double* binv = h.binv.as<double>();
-  for (int c0 = 0; c0 < npmax; c0 += NB64) {
-    hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv, dstride, meta,
-                       c0, binv, w0, w1);
+  auto grid = [](long long g) {
+    if (g > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
+    return dim3((unsigned)g);
+  };
+  auto diag = [&](int c0) {
+    hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv, dstride,
+                       meta, c0, binv, w0, w1);
     DOPT_CHECK_HIP(hipGetLastError());
+  };
+  auto trsm = [&](int c0, int nt) {
+    const long long tot = 2LL * nt * B;
+    hipLaunchKernelGGL(nlu_trsm_kernel, grid(tot), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0, binv, nt,
+                       (int)tot);
+    DOPT_CHECK_HIP(hipGetLastError());
+  };
+  auto update = [&](int c0, int nt, int cross) {
+    const long long tot = (cross ? 2LL * nt - 1 : (long long)nt * nt) * B;
+    hipLaunchKernelGGL(nlu_update_kernel, grid(tot), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0, nt, nt,
+                       (int)tot, w0, w1, cross);
+    DOPT_CHECK_HIP(hipGetLastError());
+  };
+  for (int c0 = 0; c0 < npmax;) {
+    diag(c0);
     const int R2 = npmax - c0 - NB64;
     if (R2 <= 0) break;
     const int nt = (R2 + 63) / 64;
-    const long long tot_s = 2LL * nt * B;
-    if (tot_s > 0x7fffffffLL) throw Error(-1, "no-pivot LU: TRSM grid too large");
-    hipLaunchKernelGGL(nlu_trsm_kernel, dim3((unsigned)tot_s), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0,
-                       binv, nt, (int)tot_s);
+    trsm(c0, nt);
+    if (!h.lu_pair || R2 <= NB64) {   // one rank-64 step
+      update(c0, nt, 0);
+      c0 += NB64;
+      continue;
+    }
+    // a paired step: cross band of step c0, step c0+64's diagonal block and
+    // TRSM, then both rank-64 updates of the rest in one pass
+    update(c0, nt, 1);
+    diag(c0 + NB64);
+    const int nt2 = (R2 - NB64 + 63) / 64;
+    trsm(c0 + NB64, nt2);
+    const long long tot = (long long)nt2 * nt2 * B;
+    hipLaunchKernelGGL(nlu_update2_kernel, grid(tot), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0, nt2, nt2,
+                       (int)tot, w0, w1);
     DOPT_CHECK_HIP(hipGetLastError());
-    const long long total = (long long)nt * nt * B;
-    if (total > 0x7fffffffLL) throw Error(-1, "no-pivot LU: trailing-update grid too large");
-    hipLaunchKernelGGL(nlu_update_kernel, dim3((unsigned)total), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0,
-                       nt, nt, (int)total, w0, w1);
-    DOPT_CHECK_HIP(hipGetLastError());
+    c0 += 2 * NB64;
   }
 }
 

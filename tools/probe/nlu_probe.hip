@@ -79,7 +79,7 @@ int main(int argc, char** argv) {
       snprintf(nm, sizeof nm, "update c0=%d", c0);
       timeit(nm, [&] {
         hipLaunchKernelGGL(nlu_update_kernel, dim3(nt * nt * B), dim3(256), 0, 0, K, ld, nmax, meta, c0, nt, nt,
-                           nt * nt * B, nullptr, nullptr);
+                           nt * nt * B, nullptr, nullptr, 0);
       });
     }
   }
