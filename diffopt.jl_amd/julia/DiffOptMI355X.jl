@@ -1,16 +1,18 @@
 # DiffOptMI355X.jl — Julia side of the drop-in boundary (INTEGRATION.md).
 #
-# A `DiffOpt.AbstractModel` back-end (the plug point of reference
+# Two `DiffOpt.AbstractModel` back-ends (the plug point of reference
 # src/diff_opt.jl:274, selected with `MOI.set(model, DiffOpt.ModelConstructor(),
-# DiffOptMI355X.QPModel)`, src/moi_wrapper.jl:504-514) whose
-# forward_differentiate! / reverse_differentiate! run the KKT sensitivity
-# solves on an MI355X through libdiffopt_mi355x.so (include/diffopt_mi355x.h).
+# DiffOptMI355X.QPModel)` or `DiffOptMI355X.ConicModel`,
+# src/moi_wrapper.jl:504-514) whose forward_differentiate! /
+# reverse_differentiate! run the sensitivity solves on an MI355X through
+# libdiffopt_mi355x.so (include/diffopt_mi355x.h).
 #
-# Storage, starts, input caches and every getter are those of
-# DiffOpt.QuadraticProgram.Model (`inner`): this back-end only replaces the
-# LHS assembly + `solve_system` (QuadraticProgram.jl:256-282, 316-446, 486-496)
-# by one C-ABI call, so results, sign conventions and getters are the
-# reference's.  Not exercised in CI: the build image has no Julia (SURVEY.md
+# Storage, starts, input caches and every getter are those of the reference
+# model they wrap (`inner`): QPModel replaces only the LHS assembly +
+# `solve_system` of DiffOpt.QuadraticProgram.Model (QuadraticProgram.jl:256-282,
+# 316-446, 486-496), ConicModel only `_gradient_cache`'s M and the two `lsqr`
+# calls of DiffOpt.ConicProgram.Model (ConicProgram.jl:172-255, 257-394) — so
+# results, sign conventions and getters are the reference's.  Not exercised in CI: the build image has no Julia (SURVEY.md
 # §8(c)); the C-ABI it binds is exercised by the Python ctypes harness.
 module DiffOptMI355X
 
@@ -23,6 +25,7 @@ const QP = DiffOpt.QuadraticProgram
 const LIB = get(ENV, "DIFFOPT_MI355X_LIB",
                 joinpath(@__DIR__, "..", "diffopt_amd", "libdiffopt_mi355x.so"))
 const KIND_QP = Int32(0)
+const KIND_CONIC = Int32(1)
 
 # ---------------------------------------------------------------- handle ----
 mutable struct Handle
@@ -39,11 +42,11 @@ function _check(rc::Cint, ptr::Ptr{Cvoid})
     return error("diffopt_mi355x: ", msg)
 end
 
-function Handle(n::Int, m::Int, p::Int; device::Integer = 0)
+function Handle(n::Int, m::Int, p::Int; device::Integer = 0, kind::Int32 = KIND_QP)
     r = Ref{Ptr{Cvoid}}(C_NULL)
     rc = ccall((:dopt_create, LIB), Cint,
                (Ptr{Ptr{Cvoid}}, Cint, Int64, Int32, Int32, Int32, Int32),
-               r, device, 1, n, m, p, KIND_QP)
+               r, device, 1, n, m, p, kind)
     _check(rc, r[])
     h = Handle(r[], n, m, p)
     finalizer(h) do hh
@@ -209,6 +212,163 @@ function DiffOpt.forward_differentiate!(m::QPModel)
                          out), h.ptr)
         end
         inner.forw_grad_cache = _split(out, n, mi)
+    end
+    return
+end
+
+# ------------------------------------------------------------ conic model ----
+const CP = DiffOpt.ConicProgram
+
+# MOI set → cone code of include/diffopt_mi355x.h (DOPT_CONE_*)
+_cone_code(::Type{<:MOI.Zeros}) = Int32(0)
+_cone_code(::Type{<:MOI.Nonnegatives}) = Int32(1)
+_cone_code(::Type{<:MOI.Nonpositives}) = Int32(2)
+_cone_code(::Type{<:MOI.SecondOrderCone}) = Int32(3)
+_cone_code(::Type{<:MOI.PositiveSemidefiniteConeTriangle}) = Int32(4)
+_cone_code(S::Type) = error("diffopt_mi355x: cone $S is not supported by the MI355X back-end")
+
+mutable struct ConicModel <: DiffOpt.AbstractModel
+    inner::CP.Model                      # reference storage + getters
+    model::CP.Form{Float64}              # === inner.model (DiffOpt forwards here)
+    input_cache::DiffOpt.InputCache      # === inner.input_cache
+    x::Vector{Float64}                   # === inner.x
+    s::Vector{Float64}                   # === inner.s
+    y::Vector{Float64}                   # === inner.y
+    handle::Union{Nothing,Handle}
+    factored::Bool
+    device::Int
+end
+
+function ConicModel(; device::Integer = 0)
+    inner = CP.Model()
+    return ConicModel(inner, inner.model, inner.input_cache, inner.x, inner.s, inner.y, nothing, false, device)
+end
+
+MOI.is_empty(m::ConicModel) = MOI.is_empty(m.inner)
+function MOI.empty!(m::ConicModel)
+    MOI.empty!(m.inner)
+    m.handle = nothing
+    m.factored = false
+    return
+end
+MOI.supports_constraint(m::ConicModel, F::Type{MOI.VectorAffineFunction{Float64}},
+                        S::Type{<:MOI.AbstractVectorSet}) = MOI.supports_constraint(m.inner, F, S)
+MOI.get(m::ConicModel, a::DiffOpt.DifferentiateTimeSec) = MOI.get(m.inner, a)
+function MOI.set(m::ConicModel, a::MOI.ConstraintPrimalStart, ci::MOI.ConstraintIndex, v)
+    m.factored = false
+    return MOI.set(m.inner, a, ci, v)
+end
+function MOI.set(m::ConicModel, a::MOI.ConstraintDualStart, ci::MOI.ConstraintIndex, v)
+    m.factored = false
+    return MOI.set(m.inner, a, ci, v)
+end
+MOI.get(m::ConicModel, a::DiffOpt.ForwardVariablePrimal, vi::MOI.VariableIndex) = MOI.get(m.inner, a, vi)
+MOI.get(m::ConicModel, a::DiffOpt.ReverseObjectiveFunction) = MOI.get(m.inner, a)
+MOI.get(m::ConicModel, a::MOI.ConstraintFunction, ci::MOI.ConstraintIndex) = MOI.get(m.inner, a, ci)
+DiffOpt._get_dA(m::ConicModel, ci::MOI.ConstraintIndex) = DiffOpt._get_dA(m.inner, ci)
+DiffOpt._get_db(m::ConicModel, ci::MOI.ConstraintIndex) = DiffOpt._get_db(m.inner, ci)
+
+# (code, dimension) pairs in row order: the ProductOfSets layout
+# (product_of_sets.jl:15-74) read back through MOI.Utilities.rows
+function _cone_desc(m::ConicModel)
+    cons = m.model.constraints
+    desc = Tuple{Int,Int32,Int32}[]
+    for (F, S) in MOI.get(m.model, MOI.ListOfConstraintTypesPresent())
+        for ci in MOI.get(m.model, MOI.ListOfConstraintIndices{F,S}())
+            r = MOI.Utilities.rows(cons, ci)
+            push!(desc, (first(r), _cone_code(S), Int32(length(r))))
+        end
+    end
+    sort!(desc; by = first)
+    return Int32[v for (_, c, d) in desc for v in (c, d)]
+end
+
+# the engine's counterpart of `_gradient_cache` (ConicProgram.jl:172-255): A_moi
+# as the MOI matrix (the diffcp sign flip is applied on the device), c negated
+# for MAX_SENSE (:206-208), the NaN-start guard (:186-196) raised by the engine
+function _ensure!(m::ConicModel)
+    m.factored && return m.handle
+    inner = m.inner
+    Amoi = convert(SparseArrays.SparseMatrixCSC{Float64,Int64}, m.model.constraints.coefficients)
+    b = Vector{Float64}(m.model.constraints.constants)
+    mr, n = size(Amoi)
+    if length(inner.y) < mr
+        error("Some constraints are missing a value for the `ConstraintDualStart` attribute.")
+    elseif length(inner.s) < mr
+        error("Some constraints are missing a value for the `ConstraintPrimalStart` attribute.")
+    end
+    sense = MOI.get(m.model, MOI.ObjectiveSense())
+    c = if sense == MOI.FEASIBILITY_SENSE
+        zeros(n)
+    else
+        obj = MOI.get(m.model, MOI.ObjectiveFunction{MOI.ScalarAffineFunction{Float64}}())
+        cc = Vector{Float64}(DiffOpt.sparse_array_representation(obj, n).terms)
+        sense == MOI.MAX_SENSE ? -cc : cc
+    end
+    desc = _cone_desc(m)
+    h = m.handle
+    if h === nothing || (h.n, h.m) != (n, mr)
+        h = m.handle = Handle(n, mr, 0; device = m.device, kind = KIND_CONIC)
+    end
+    colptr, rowval, nzval, nnz = _csc(Amoi)
+    GC.@preserve Amoi b c inner desc begin
+        _check(ccall((:dopt_conic_set_csc, LIB), Cint,
+                     (Ptr{Cvoid}, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}, Int64,
+                      Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                      Ptr{Int32}, Int32),
+                     h.ptr, colptr, rowval, nzval, nnz, _ptr(b), _ptr(c), _ptr(inner.x),
+                     _ptr(inner.s), _ptr(inner.y), desc, Int32(length(desc) ÷ 2)), h.ptr)
+        _check(ccall((:dopt_conic_factor, LIB), Cint, (Ptr{Cvoid},), h.ptr), h.ptr)
+    end
+    m.factored = true
+    return h
+end
+
+# forward_differentiate! (ConicProgram.jl:257-334): the tangents gathered with
+# the reference's own `_fill` (dA, db in MOI layout), [du | dv | dw] from the
+# device, the reference's ForwCache so ForwardVariablePrimal is its getter
+function DiffOpt.forward_differentiate!(m::ConicModel)
+    inner = m.inner
+    inner.diff_time = @elapsed begin
+        h = _ensure!(m)
+        n, mr = h.n, h.m
+        f = DiffOpt._convert(MOI.ScalarAffineFunction{Float64}, m.input_cache.objective)
+        dc = Vector{Float64}(DiffOpt.sparse_array_representation(f, n).terms)
+        db = zeros(mr)
+        DiffOpt._fill(S -> false, nothing, m.input_cache, m.model.constraints.sets, db)
+        I, J, V = Int[], Int[], Float64[]
+        DiffOpt._fill(S -> false, nothing, m.input_cache, m.model.constraints.sets, I, J, V)
+        dA = Matrix{Float64}(SparseArrays.sparse(I, J, V, mr, n))
+        out = Vector{Float64}(undef, n + mr + 1)
+        GC.@preserve dA db dc begin
+            _check(ccall((:dopt_conic_forward, LIB), Cint,
+                         (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                         h.ptr, _ptr(dA), _ptr(db), _ptr(dc), out, Ptr{Float64}(C_NULL)), h.ptr)
+        end
+        inner.forw_grad_cache = CP.ForwCache(out[1:n], out[n+1:n+mr], [out[end]])
+    end
+    return
+end
+
+# reverse_differentiate! (ConicProgram.jl:336-394): g from the device, πz =
+# [x; π(v); 1] with the reference's own projection (:375-379), so the lazy
+# getters (:396-443) are the reference's
+function DiffOpt.reverse_differentiate!(m::ConicModel)
+    inner = m.inner
+    inner.diff_time = @elapsed begin
+        h = _ensure!(m)
+        n, mr = h.n, h.m
+        dx = zeros(n)
+        for (vi, value) in m.input_cache.dx
+            dx[vi.value] = value
+        end
+        g = Vector{Float64}(undef, n + mr + 1)
+        n0 = Ptr{Float64}(C_NULL)
+        _check(ccall((:dopt_conic_reverse, LIB), Cint,
+                     (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                     h.ptr, dx, g, n0, n0, n0), h.ptr)
+        vp = DiffOpt.π(inner.y - inner.s, m.model, m.model.constraints.sets)
+        inner.back_grad_cache = CP.ReverseCache(g, vcat(inner.x, vp, 1.0))
     end
     return
 end
