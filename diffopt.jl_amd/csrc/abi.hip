@@ -322,6 +322,46 @@ int dopt_qp_forward(dopt_handle* h, const double* dQ, const double* dq, const do
   });
 }
 
+int dopt_qp_reverse_k(dopt_handle* h, int32_t k, const double* dl_dz, double* out) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_reverse_k on a non-QP handle");
+    if (!dl_dz || !out) throw Error(-1, "dl_dz and out are required");
+    if (k <= 0) throw Error(-1, "k must be positive");
+    Timer tm;
+    const size_t B = h->batch, n = h->n, L = h->n + h->m + h->p, K = (size_t)k;
+    const double* d = stage_in(*h, h->tin[0], dl_dz, K * B * n);
+    double* o = out_ptr(*h, h->tout[0], out, K * B * L);
+    dopt::qp_reverse_k(*h, k, d, o);
+    copy_out(*h, out, o, K * B * L);
+    const int rc = first_info(*h);
+    h->last_time = tm.s();
+    return rc;
+  });
+}
+
+int dopt_qp_forward_k(dopt_handle* h, int32_t k, const double* dQ, const double* dq, const double* dG,
+                      const double* dh, const double* dA, const double* db, double* out) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_forward_k on a non-QP handle");
+    if (!out) throw Error(-1, "out is required");
+    if (k <= 0) throw Error(-1, "k must be positive");
+    Timer tm;
+    const size_t B = h->batch, n = h->n, m = h->m, p = h->p, L = n + m + p, K = (size_t)k;
+    const double* a = stage_in(*h, h->tin[1], dQ, K * B * n * n);
+    const double* b = stage_in(*h, h->tin[2], dq, K * B * n);
+    const double* c = stage_in(*h, h->tin[3], dG, K * B * m * n);
+    const double* d = stage_in(*h, h->tin[4], dh, K * B * m);
+    const double* e = stage_in(*h, h->tin[5], dA, K * B * p * n);
+    const double* f = stage_in(*h, h->tin[6], db, K * B * p);
+    double* o = out_ptr(*h, h->tout[1], out, K * B * L);
+    dopt::qp_forward_k(*h, k, a, b, c, d, e, f, o);
+    copy_out(*h, out, o, K * B * L);
+    const int rc = first_info(*h);
+    h->last_time = tm.s();
+    return rc;
+  });
+}
+
 int dopt_qp_forward_reverse(dopt_handle* h, const double* dl_dz, const double* dQ,
                             const double* dq, const double* dG, const double* dh,
                             const double* dA, const double* db, double* out_rev,

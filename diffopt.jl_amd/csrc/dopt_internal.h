@@ -112,6 +112,7 @@ struct Handle {
   DevBuf lsqr_ws;            // LSQR vectors of the `iterative` branch (5 per problem)
   DevBuf binv;               // no-pivot LU: packed 64×64 inverse of the current diagonal block
   DevBuf fwdw;               // fused call: both right-hand sides, forward-swept inside the no-pivot LU
+  DevBuf krhs, kx, kfull;    // multi-RHS calls: k seeds' reduced RHS, solutions, full forward RHS
   QPMeta* meta_host = nullptr;     // pinned copy of `meta` (asynchronous read-back)
   hipEvent_t meta_ev = nullptr;    // recorded after the read-back copy
   // factorisation: 1 = no-pivot blocked LU with the threshold test and a
@@ -212,6 +213,11 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
 void qp_nopiv_factor(Handle& h, double* dinv, double* w0 = nullptr, double* w1 = nullptr);
 void qp_blocked_factor(Handle& h, double* dinv, const int32_t* plist, int count);
 void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rhs, double* x, int sel);
+void qp_blocked_solve_multi(Handle& h, const double* dinv, int trans, int k, const double* rhs, double* x,
+                            int sel);
+void qp_reverse_k(Handle& h, int k, const double* dl_dz, double* out);
+void qp_forward_k(Handle& h, int k, const double* dQ, const double* dq, const double* dG, const double* dh,
+                  const double* dA, const double* db, double* out);
 void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, const double* rhs_fwd,
                        double* x_rev, double* x_fwd, int sel, const double* w_rev = nullptr,
                        const double* w_fwd = nullptr);

@@ -520,6 +520,63 @@ __global__ __launch_bounds__(TPB) void qp_output_kernel(
   }
 }
 
+// k-seed outputs (multi-RHS calls): the qp_output_kernel recovery for up to
+// OKC seeds per workgroup (grid B × ⌈k/OKC⌉), so the reverse direction's
+// eliminated rows read their G row once per OKC seeds instead of once per
+// seed; each seed's arithmetic (and summation order) is qp_output_kernel's.
+// Seed j of problem b: x / full at + (j·B + b)·nmax, out at + (j·B + b)·(n+m+p).
+constexpr int OKC = 16;
+__global__ __launch_bounds__(TPB) void qp_output_k_kernel(
+    const double* __restrict__ x, const double* __restrict__ G, const double* __restrict__ s,
+    const int32_t* __restrict__ rpos, const QPMeta* __restrict__ meta, const double* __restrict__ full,
+    int B, int k, int n, int m, int p, int nmax, int trans, double* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];   // x_z of the chunk: n × OKC (when staged)
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int j0 = blockIdx.y * OKC, kc = min(OKC, k - j0);
+  const int nk = meta[b].nk;
+  const size_t L = (size_t)n + m + p;
+  const bool staged = !trans && n * OKC * 8 <= 48 * 1024;
+  for (int c = 0; c < kc; ++c) {
+    const double* xb = x + ((size_t)(j0 + c) * B + b) * nmax;
+    double* ob = out + ((size_t)(j0 + c) * B + b) * L;
+    for (int i = t; i < n; i += TPB) {
+      if (staged) smem[i * OKC + c] = xb[i];
+      ob[i] = -xb[i];
+    }
+    for (int e = t; e < p; e += TPB) ob[n + m + e] = -xb[n + nk + e];
+  }
+  __syncthreads();
+  const double* Gb = G + (size_t)b * m * n;
+  for (int l = t; l < m; l += TPB) {
+    const int kk = rpos[(size_t)b * m + l];
+    const double sl = s[(size_t)b * m + l];
+    if (kk >= 0 || trans) {
+      for (int c = 0; c < kc; ++c) {
+        const size_t pj = (size_t)(j0 + c) * B + b;
+        const double xl = kk >= 0 ? x[pj * nmax + n + kk] : full[pj * nmax + n + l] / sl;
+        out[pj * L + n + l] = -xl;
+      }
+      continue;
+    }
+    double acc[OKC];
+#pragma unroll
+    for (int c = 0; c < OKC; ++c) acc[c] = 0.0;
+    for (int j = 0; j < n; ++j) {   // one G load serves every seed of the chunk
+      const double gv = Gb[l + (size_t)j * m];
+#pragma unroll
+      for (int c = 0; c < OKC; ++c) {
+        if (c < kc) {
+          const double xz = staged ? smem[j * OKC + c] : x[((size_t)(j0 + c) * B + b) * nmax + j];
+          acc[c] = fma(gv, xz, acc[c]);
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < OKC; ++c)
+      if (c < kc) out[((size_t)(j0 + c) * B + b) * L + n + l] = -((0.0 - acc[c]) / sl);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Batched reverse-gradient materialisation (the reference's lazy getters,
 // materialised for every problem at once): from rev = [dz | dλ | dν]
@@ -787,13 +844,12 @@ static double* x_of(Handle& h, int trans) {
 }
 
 // generic solves, LSQR and output recovery for one direction (the blocked
-// solves are launched by the callers)
-static void finish(Handle& h, int trans, double* out) {
+// solves are launched by the callers); rhs / x / full: this direction's work
+// vectors (stride nmax per problem)
+static void finish_into(Handle& h, int trans, double* rhs, double* x, const double* full, double* out) {
   const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
   const int nmax = h.nmax, ld = h.ld;
   QPMeta* meta = h.meta.as<QPMeta>();
-  double* rhs = rhs_of(h, trans);
-  double* x = x_of(h, trans);
   if (nmax > BLOCKED_MAX && h.has_generic) {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     if ((size_t)nmax * sizeof(double) > 64 * 1024) throw Error(-1, "generic solve: system too large");
@@ -811,9 +867,12 @@ static void finish(Handle& h, int trans, double* out) {
   static const double dummy = 0.0;
   PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
   hipLaunchKernelGGL(qp_output_kernel, dim3(B), dim3(TPB), (size_t)std::min(n, ZCAP) * sizeof(double),
-                     h.stream, x, m ? h.G : &dummy, h.s.as<double>(), rpos_of(h), meta, full_of(h), n, m, p,
+                     h.stream, x, m ? h.G : &dummy, h.s.as<double>(), rpos_of(h), meta, full, n, m, p,
                      nmax, ZCAP, trans, out);
   check_launch();
+}
+static void finish(Handle& h, int trans, double* out) {
+  finish_into(h, trans, rhs_of(h, trans), x_of(h, trans), full_of(h), out);
 }
 
 static void rev_rhs(Handle& h, const double* dl_dz) {
@@ -823,15 +882,17 @@ static void rev_rhs(Handle& h, const double* dl_dz) {
   check_launch();
 }
 
-static void fwd_rhs(Handle& h, const FwdTangents& T) {
+static void fwd_rhs_into(Handle& h, const FwdTangents& T, double* full, double* rhs) {
   const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
   static const double dummy = 0.0;
-  PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
   hipLaunchKernelGGL(qp_fwd_rhs_kernel, dim3(B), dim3(TPB), (size_t)std::min(n, ZCAP) * sizeof(double),
                      h.stream, T.dQ, T.dq, T.dG, T.dh, T.dA, T.db, h.z, m ? h.lam : &dummy,
-                     p ? h.nu : &dummy, rpos_of(h), h.meta.as<QPMeta>(), n, m, p, h.nmax, ZCAP, full_of(h),
-                     rhs_of(h, 1));
+                     p ? h.nu : &dummy, rpos_of(h), h.meta.as<QPMeta>(), n, m, p, h.nmax, ZCAP, full, rhs);
   check_launch();
+}
+static void fwd_rhs(Handle& h, const FwdTangents& T) {
+  PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
+  fwd_rhs_into(h, T, full_of(h), rhs_of(h, 1));
 }
 
 static FwdTangents tangents(Handle& h, const double* dQ, const double* dq, const double* dG,
@@ -865,6 +926,96 @@ void qp_forward(Handle& h, const double* dQ, const double* dq, const double* dG,
     qp_blocked_solve(h, dinv_of(h), 1, rhs_of(h, 1), x_of(h, 1), LU_SEL_ALL);
   }
   finish(h, 1, out);
+}
+
+// k seeds / tangents per problem on the kept factorisation (the §8(f)
+// multi-RHS row): seed j's inputs and outputs are standard batch blocks at
+// offset j·B·len; the blocked problems' k solves run in one launch
+// (qp_multi.hip), the other routes and the outputs per seed.
+static void solve_k(Handle& h, int trans, int k, double* rk, double* xk, double* fk, double* out) {
+  const size_t blk = (size_t)h.batch * h.nmax;
+  const int B = (int)h.batch, n = h.n, m = h.m, p = h.p, nmax = h.nmax;
+  {
+    PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
+    const size_t lds = (size_t)h.blocked_npmax * (16 * sizeof(double) + sizeof(int));
+    if (lds <= 160 * 1024) {
+      qp_blocked_solve_multi(h, dinv_of(h), trans, k, rk, xk, LU_SEL_ALL);
+    } else {   // the chunk does not fit LDS: one single-RHS solve per seed
+      for (int j = 0; j < k; ++j) qp_blocked_solve(h, dinv_of(h), trans, rk + j * blk, xk + j * blk, LU_SEL_ALL);
+    }
+  }
+  // generic / LSQR routes per seed, then every seed's outputs in one launch
+  QPMeta* meta = h.meta.as<QPMeta>();
+  for (int j = 0; j < k; ++j) {
+    double* rhs = rk + j * blk;
+    double* x = xk + j * blk;
+    if (nmax > BLOCKED_MAX && h.has_generic) {
+      PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
+      if ((size_t)nmax * sizeof(double) > 64 * 1024) throw Error(-1, "generic solve: system too large");
+      hipLaunchKernelGGL(qp_solve_kernel, dim3(B), dim3(TPB), (size_t)nmax * sizeof(double), h.stream,
+                         h.K.as<double>(), h.ipiv.as<int32_t>(), meta, nmax, h.ld, trans, rhs, x);
+      check_launch();
+    }
+    if (h.has_lsqr) {
+      PhaseTimer pt(h, DOPT_PHASE_QP_LSQR);
+      h.lsqr_ws.ensure((size_t)B * 5 * nmax * sizeof(double));
+      hipLaunchKernelGGL(qp_lsqr_kernel, dim3(B), dim3(TPB), 0, h.stream, h.K.as<double>(), meta, nmax, h.ld,
+                         trans, rhs, x, h.lsqr_ws.as<double>());
+      check_launch();
+    }
+  }
+  static const double dummy = 0.0;
+  PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
+  const int nck = (k + OKC - 1) / OKC;
+  const size_t lds = (!trans && (size_t)n * OKC * 8 <= 48 * 1024) ? (size_t)n * OKC * 8 : 0;
+  hipLaunchKernelGGL(qp_output_k_kernel, dim3(B, nck), dim3(TPB), lds, h.stream, xk, m ? h.G : &dummy,
+                     h.s.as<double>(), rpos_of(h), meta, fk ? fk : xk, B, k, n, m, p, nmax, trans, out);
+  check_launch();
+}
+
+void qp_reverse_k(Handle& h, int k, const double* dl_dz, double* out) {
+  if (k <= 0) throw Error(-1, "dopt_qp_reverse_k: k must be positive");
+  if (k == 1) return qp_reverse(h, dl_dz, out);   // the single-seed path is faster for one seed
+  if (!h.factored) qp_factor(h);
+  const size_t blk = (size_t)h.batch * h.nmax;
+  h.krhs.ensure((size_t)k * blk * sizeof(double));
+  h.kx.ensure((size_t)k * blk * sizeof(double));
+  double* rk = h.krhs.as<double>();
+  double* xk = h.kx.as<double>();
+  {
+    PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
+    for (int j = 0; j < k; ++j) {
+      hipLaunchKernelGGL(qp_rev_rhs_kernel, dim3(h.batch), dim3(TPB), 0, h.stream, dl_dz + (size_t)j * h.batch * h.n,
+                         h.meta.as<QPMeta>(), h.n, h.nmax, rk + j * blk);
+      check_launch();
+    }
+  }
+  solve_k(h, 0, k, rk, xk, nullptr, out);
+}
+
+void qp_forward_k(Handle& h, int k, const double* dQ, const double* dq, const double* dG, const double* dh,
+                  const double* dA, const double* db, double* out) {
+  if (k <= 0) throw Error(-1, "dopt_qp_forward_k: k must be positive");
+  if (k == 1) return qp_forward(h, dQ, dq, dG, dh, dA, db, out);
+  if (!h.factored) qp_factor(h);
+  const size_t B = h.batch, n = h.n, m = h.m, p = h.p;
+  const size_t blk = B * h.nmax;
+  h.krhs.ensure((size_t)k * blk * sizeof(double));
+  h.kx.ensure((size_t)k * blk * sizeof(double));
+  h.kfull.ensure((size_t)k * blk * sizeof(double));
+  double* rk = h.krhs.as<double>();
+  double* xk = h.kx.as<double>();
+  double* fk = h.kfull.as<double>();
+  {
+    PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
+    for (int j = 0; j < k; ++j) {
+      auto at = [&](const double* a, size_t len) { return a ? a + (size_t)j * B * len : nullptr; };
+      const FwdTangents T = tangents(h, at(dQ, n * n), at(dq, n), at(dG, m * n), at(dh, m), at(dA, p * n),
+                                     at(db, p));
+      fwd_rhs_into(h, T, fk + j * blk, rk + j * blk);
+    }
+  }
+  solve_k(h, 1, k, rk, xk, fk, out);
 }
 
 void qp_reverse_grads(Handle& h, const double* rev, double* dQ, double* dq, double* dG, double* gc,

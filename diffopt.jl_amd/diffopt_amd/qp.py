@@ -160,6 +160,40 @@ class QPBatch:
         _lib.check(rc, self.h, singular_ok)
         return out
 
+    def reverse_k(self, dl_dz, singular_ok=False):
+        """k seeds per problem on one factorisation (dopt_qp_reverse_k):
+        dl_dz (k, B, n) → (k, B, n+m+p); equal to k ``reverse`` calls to
+        rounding, the blocked problems' k solves in one MFMA launch."""
+        k = int(dl_dz.shape[0])
+        B, n = self.batch, self.n
+        st = self._stage([dl_dz])
+        d = vector(dl_dz, (k, B, n))
+        out = Staged.empty((k, B, self.L), st.mem == _lib.DOPT_MEM_DEVICE)
+        rc = self.lib.dopt_qp_reverse_k(self.h, k, st.ptr(d), st.ptr(out))
+        _lib.check(rc, self.h, singular_ok)
+        return out
+
+    def forward_k(self, dQ=None, dq=None, dG=None, dh=None, dA=None, db=None, singular_ok=False):
+        """k tangents per problem (dopt_qp_forward_k): each given tangent has a
+        leading seed axis (k, B, …) → (k, B, n+m+p)."""
+        given = [a for a in (dQ, dq, dG, dh, dA, db) if a is not None]
+        if not given:
+            raise ValueError("forward_k needs at least one tangent")
+        k = int(given[0].shape[0])
+        B, n, m, p = self.batch, self.n, self.m, self.p
+        st = self._stage([dQ, dq, dG, dh, dA, db])
+        kb = k * B
+        args = [colmajor(dQ, (kb, n, n)) if dQ is not None else None,
+                vector(dq, (kb, n)) if dq is not None else None,
+                colmajor(dG, (kb, m, n)) if (dG is not None and m) else None,
+                vector(dh, (kb, m)) if (dh is not None and m) else None,
+                colmajor(dA, (kb, p, n)) if (dA is not None and p) else None,
+                vector(db, (kb, p)) if (db is not None and p) else None]
+        out = Staged.empty((k, B, self.L), st.mem == _lib.DOPT_MEM_DEVICE)
+        rc = self.lib.dopt_qp_forward_k(self.h, k, *[st.ptr(a) for a in args], st.ptr(out))
+        _lib.check(rc, self.h, singular_ok)
+        return out
+
     def forward_reverse(self, dl_dz, dQ=None, dq=None, dG=None, dh=None, dA=None,
                         db=None, out_rev=None, out_fwd=None, singular_ok=False):
         """One full sensitivity solve per problem: factor + reverse + forward."""

@@ -134,6 +134,19 @@ int dopt_qp_forward(dopt_handle* h, const double* dQ, const double* dq,
  * Column-major per problem, batch-major.  Any output may be NULL. */
 int dopt_qp_reverse_grads(dopt_handle* h, const double* rev, double* dQ, double* dq,
                           double* dG, double* g_const, double* dA, double* a_const);
+/* k seeds / tangents per problem on one factorisation (the reference calls
+ * reverse_differentiate! / forward_differentiate! once per seed on the same
+ * model, re-solving each time: QuadraticProgram.jl:316-351, 357-446,
+ * 486-496; callers such as docs/src/examples/sensitivity-analysis-ridge.jl:
+ * 120-131 loop many seeds).  Seed-major layout: seed j's inputs are a
+ * standard batch block at offset j·B·len (dl_dz: n×B×k, dq: n×B×k, dQ:
+ * n×n×B×k, …), out: (n+m+p)×B×k.  Results equal k dopt_qp_reverse /
+ * dopt_qp_forward calls to rounding; the blocked problems' k solves run as
+ * one MFMA multi-RHS launch.  Factorises first if needed. */
+int dopt_qp_reverse_k(dopt_handle* h, int32_t k, const double* dl_dz, double* out);
+int dopt_qp_forward_k(dopt_handle* h, int32_t k, const double* dQ, const double* dq,
+                      const double* dG, const double* dh, const double* dA,
+                      const double* db, double* out);
 /* Fused forward + reverse for one factorisation (the batched throughput path;
  * results identical to dopt_qp_reverse + dopt_qp_forward). */
 int dopt_qp_forward_reverse(dopt_handle* h, const double* dl_dz,
