@@ -284,6 +284,43 @@ int dopt_qp_reverse_grads(dopt_handle* h, const double* rev, double* dQ, double*
   });
 }
 
+int dopt_qp_params_reverse(dopt_handle* h, const double* rev, int32_t nparam, int64_t nterms,
+                           const int32_t* t_param, const int32_t* t_kind, const int32_t* t_index,
+                           const double* t_coef, double* out_dp) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_params_reverse on a non-QP handle");
+    if (!rev || (nparam > 0 && !out_dp)) throw Error(-1, "rev and out_dp are required");
+    const size_t B = h->batch, L = (size_t)h->n + h->m + h->p, P = nparam > 0 ? (size_t)nparam : 0;
+    const double* r = stage_in(*h, h->tin[0], rev, B * L);
+    double* o = P ? out_ptr(*h, h->tout[0], out_dp, B * P) : nullptr;
+    dopt::qp_params_reverse(*h, r, nparam, nterms, t_param, t_kind, t_index, t_coef, o);
+    if (P) copy_out(*h, out_dp, o, B * P);
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  });
+}
+
+int dopt_qp_params_forward(dopt_handle* h, const double* dp, int32_t nparam, int64_t nterms,
+                           const int32_t* t_param, const int32_t* t_kind, const int32_t* t_index,
+                           const double* t_coef, double* dq, double* dh, double* db) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_params_forward on a non-QP handle");
+    if ((nparam > 0 && !dp) || !dq || (h->m && !dh) || (h->p && !db))
+      throw Error(-1, "dp, dq, dh (m > 0) and db (p > 0) are required");
+    const size_t B = h->batch, n = h->n, m = h->m, p = h->p, P = nparam > 0 ? (size_t)nparam : 0;
+    const double* d = P ? stage_in(*h, h->tin[0], dp, B * P) : nullptr;
+    double* oq = out_ptr(*h, h->tout[0], dq, B * n);
+    double* oh = m ? out_ptr(*h, h->tout[1], dh, B * m) : nullptr;
+    double* ob = p ? out_ptr(*h, h->tout[2], db, B * p) : nullptr;
+    dopt::qp_params_forward(*h, d, nparam, nterms, t_param, t_kind, t_index, t_coef, oq, oh, ob);
+    copy_out(*h, dq, oq, B * n);
+    if (m) copy_out(*h, dh, oh, B * m);
+    if (p) copy_out(*h, db, ob, B * p);
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  });
+}
+
 int dopt_qp_reverse(dopt_handle* h, const double* dl_dz, double* out) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_reverse on a non-QP handle");

@@ -216,6 +216,11 @@ void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rh
 void qp_blocked_solve_multi(Handle& h, const double* dinv, int trans, int k, const double* rhs, double* x,
                             int sel);
 void qp_reverse_k(Handle& h, int k, const double* dl_dz, double* out);
+void qp_params_reverse(Handle& h, const double* rev, int nparam, int64_t nterms, const int32_t* t_param,
+                       const int32_t* t_kind, const int32_t* t_index, const double* t_coef, double* out);
+void qp_params_forward(Handle& h, const double* dp, int nparam, int64_t nterms, const int32_t* t_param,
+                       const int32_t* t_kind, const int32_t* t_index, const double* t_coef, double* dq,
+                       double* dh, double* db);
 void qp_forward_k(Handle& h, int k, const double* dQ, const double* dq, const double* dG, const double* dh,
                   const double* dA, const double* db, double* out);
 void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, const double* rhs_fwd,

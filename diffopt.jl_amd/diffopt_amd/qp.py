@@ -216,6 +216,49 @@ class QPBatch:
         _lib.check(rc, self.h, singular_ok)
         return o1, o2
 
+    # ---- parameters (ParametricOptInterface glue, reference src/parameters.jl)
+    @staticmethod
+    def _terms(terms):
+        """terms: iterable of (param, kind, index, coef) — kinds 0 LessThan row,
+        1 EqualTo row, 2 objective, 3 objective parameter×variable (index = v)."""
+        t = list(terms)
+        par = np.ascontiguousarray([int(x[0]) for x in t], dtype=np.int32)
+        kind = np.ascontiguousarray([int(x[1]) for x in t], dtype=np.int32)
+        idx = np.ascontiguousarray([int(x[2]) for x in t], dtype=np.int32)
+        coef = np.ascontiguousarray([float(x[3]) for x in t], dtype=np.float64)
+        return len(t), par, kind, idx, coef
+
+    def params_reverse(self, rev, terms, nparam):
+        """ReverseConstraintSet of every parameter of every problem, (B, nparam),
+        from a reverse output ``rev`` (B, n+m+p) — dopt_qp_params_reverse."""
+        B = self.batch
+        nt, par, kind, idx, coef = self._terms(terms)
+        st = self._stage([rev])
+        r = vector(rev, (B, self.L))
+        out = Staged.empty((B, nparam), st.mem == _lib.DOPT_MEM_DEVICE)
+        p = Staged.ptr
+        rc = self.lib.dopt_qp_params_reverse(self.h, st.ptr(r), nparam, nt, p(par), p(kind), p(idx), p(coef),
+                                             st.ptr(out))
+        _lib.check(rc, self.h)
+        return out
+
+    def params_forward(self, dp, terms):
+        """Parameter tangents dp (B, nparam) → the forward tangents (dq, dh, db)
+        the reference's POI glue sets (dopt_qp_params_forward), ready for
+        ``forward(dq=…, dh=…, db=…)``."""
+        B, n, m, p_ = self.batch, self.n, self.m, self.p
+        nparam = int(dp.shape[1])
+        nt, par, kind, idx, coef = self._terms(terms)
+        st = self._stage([dp])
+        d = vector(dp, (B, nparam))
+        dev = st.mem == _lib.DOPT_MEM_DEVICE
+        dq, dh, db = Staged.empty((B, n), dev), Staged.empty((B, m), dev), Staged.empty((B, p_), dev)
+        pp = Staged.ptr
+        rc = self.lib.dopt_qp_params_forward(self.h, st.ptr(d), nparam, nt, pp(par), pp(kind), pp(idx), pp(coef),
+                                             st.ptr(dq), st.ptr(dh) if m else None, st.ptr(db) if p_ else None)
+        _lib.check(rc, self.h)
+        return dq, dh, db
+
     def reverse_grads(self, rev, dQ=True, dG=True, dA=True):
         """Materialised reverse gradients of every problem from a reverse
         output ``rev`` (B, n+m+p) — ``ReverseObjectiveFunction`` /

@@ -155,6 +155,31 @@ int dopt_qp_forward_reverse(dopt_handle* h, const double* dl_dz,
                             const double* dA, const double* db,
                             double* out_rev, double* out_fwd);
 
+/* ---- parameters (ParametricOptInterface glue, reference src/parameters.jl) ----
+ * A parametric term t: t_param[t] ∈ [0, nparam), t_kind[t]:
+ *   0  parameter term of LessThan row t_index[t]   (ParametricAffineFunction)
+ *   1  parameter term of EqualTo row t_index[t]
+ *   2  parameter term of the objective (t_index ignored)
+ *   3  parameter×variable term of the objective, variable t_index[t]
+ * and coefficient t_coef[t]; identical for every problem of the batch.  Term
+ * arrays are host memory in both memory modes; sums run in term order.
+ * Reverse (parameters.jl:341-534, reverse_differentiate! of POI.Optimizer):
+ * out_dp (nparam×B) = Σ_t c_t·s_t from a reverse output rev ((n+m+p)×B):
+ * s = λ_i·dλ_i (kind 0, the constant of ReverseConstraintFunction), dν_i
+ * (kind 1), 0 (kind 2, ReverseObjectiveFunction's constant), dz_v (kind 3, its
+ * coefficient of v) — ReverseConstraintSet of each parameter.
+ * Forward (parameters.jl:91-300, forward_differentiate! of POI.Optimizer):
+ * from parameter tangents dp (nparam×B), the constraint / objective tangents
+ * in dopt_qp_forward's inputs: dh_i = −Σ c·dp (LessThan constants, the
+ * `_fill` negation), db_i = −Σ c·dp (EqualTo), dq_v = Σ c·dp (kind 3);
+ * kind 2 does not enter the KKT system. */
+int dopt_qp_params_reverse(dopt_handle* h, const double* rev, int32_t nparam, int64_t nterms,
+                           const int32_t* t_param, const int32_t* t_kind, const int32_t* t_index,
+                           const double* t_coef, double* out_dp);
+int dopt_qp_params_forward(dopt_handle* h, const double* dp, int32_t nparam, int64_t nterms,
+                           const int32_t* t_param, const int32_t* t_kind, const int32_t* t_index,
+                           const double* t_coef, double* dq, double* dh, double* db);
+
 /* ---- ConicProgram ----------------------------------------------------------
  * A: m×n MOI coefficients (A_moi x + b ∈ K; the diffcp sign flip of
  * ConicProgram.jl:179-183 is applied inside), b: m MOI constants, c: n
