@@ -651,6 +651,49 @@ int dopt_conic_forward(dopt_handle* h, const double* dA, const double* db, const
   });
 }
 
+int dopt_conic_forward_reverse(dopt_handle* h, const double* dA, const double* db, const double* dc,
+                               const double* dx, double* out, double* out_dx, double* out_g, double* out_dA,
+                               double* out_db, double* out_dc) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_CONIC) throw Error(-1, "dopt_conic_forward_reverse on a non-conic handle");
+    if (!out || !dx || !out_g) throw Error(-1, "out, dx and out_g are required");
+    Timer tm;
+    const size_t B = h->batch, n = h->n, m = h->m, N = n + m + 1;
+    const double* a = stage_in(*h, h->tin[1], dA, B * m * n);
+    const double* b = stage_in(*h, h->tin[2], db, B * m);
+    const double* c = stage_in(*h, h->tin[3], dc, B * n);
+    const double* d = stage_in(*h, h->tin[0], dx, B * n);
+    double* o = out_ptr(*h, h->tout[0], out, B * N);
+    double* ox = out_ptr(*h, h->tout[1], out_dx, B * n);
+    double* og = out_ptr(*h, h->tout[2], out_g, B * N);
+    double* oA = out_ptr(*h, h->tout[3], out_dA, B * m * n);
+    double* ob = out_ptr(*h, h->tout[4], out_db, B * m);
+    double* oc = out_ptr(*h, h->tout[5], out_dc, B * n);
+    dopt::conic_forward_reverse(*h, a, b, c, d, o, ox, og, oA, ob, oc);
+    copy_out(*h, out, o, B * N);
+    copy_out(*h, out_dx, ox, B * n);
+    copy_out(*h, out_g, og, B * N);
+    copy_out(*h, out_dA, oA, B * m * n);
+    copy_out(*h, out_db, ob, B * m);
+    copy_out(*h, out_dc, oc, B * n);
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    h->last_time = tm.s();
+    return 0;
+  });
+}
+
+int dopt_conic_lsqr_stats(dopt_handle* h, int32_t* stats) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_CONIC) throw Error(-1, "dopt_conic_lsqr_stats on a non-conic handle");
+    if (!stats) throw Error(-1, "stats is required");
+    if (!h->cinfo.p) throw Error(-1, "no conic solve has run");
+    DOPT_CHECK_HIP(hipMemcpyAsync(stats, h->cinfo.p, 4 * h->batch * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                  h->stream));
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  });
+}
+
 int dopt_conic_reverse(dopt_handle* h, const double* dx, double* out_g, double* out_dA,
                        double* out_db, double* out_dc) {
   return guarded(h, [&]() {

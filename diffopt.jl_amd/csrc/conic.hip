@@ -379,57 +379,72 @@ constexpr int PAIR_K = 8;
 constexpr int PAIR_NC = DOPT_PAIR_NC;   // columns in flight per wave
 constexpr int PAIR_ROWS = 64 * PAIR_K;
 
-template <int PK = PAIR_K>
-__device__ __forceinline__ void gemv_pair(const double* __restrict__ A, int ld, int m, int n,
-                                          const double* __restrict__ x, const double* __restrict__ w,
-                                          double* __restrict__ y, double* __restrict__ g,
-                                          double* __restrict__ ys) {
+// NV independent pairs in one sweep over A (co-iterated forward + reverse
+// LSQR, NV = 2): y_v = A_moi·x_v, g_v = A_moiᵀ·w_v.  Each product keeps the
+// NV = 1 summation order exactly (the column chunk NC only groups loads), so
+// the co-iterated sequences are bit-identical to separate ones.  NC = 2 for
+// NV = 2 keeps two waves per SIMD.  ys: NV·4·PAIR_ROWS doubles.
+template <int NV, int PK = PAIR_K, int NC = (NV == 1 ? PAIR_NC : 2)>
+__device__ __forceinline__ void gemv_multi(const double* __restrict__ A, int ld, int m, int n,
+                                           const double* const* x, const double* const* w, double* const* y,
+                                           double* const* g, double* __restrict__ ys) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (m <= 0) {
-    for (int j = threadIdx.x; j < n; j += CTPB) g[j] = 0.0;
+    for (int q = 0; q < NV; ++q)
+      for (int j = threadIdx.x; j < n; j += CTPB) g[q][j] = 0.0;
     __syncthreads();
     return;
   }
   for (int r0 = 0; r0 < m; r0 += (64 * PK)) {
-    double wr[PK], ya[PK];
+    double wr[NV][PK], ya[NV][PK];
     bool ok[PK];
 #pragma unroll
     for (int k = 0; k < PK; ++k) {
       const int i = r0 + lane + 64 * k;
       ok[k] = i < m;
-      wr[k] = ok[k] ? w[i] : 0.0;
-      ya[k] = 0.0;
+#pragma unroll
+      for (int q = 0; q < NV; ++q) {
+        wr[q][k] = ok[k] ? w[q][i] : 0.0;
+        ya[q][k] = 0.0;
+      }
     }
     const double* Ar = A + r0 + lane;
     int j = wv;
-    for (; j + 4 * (PAIR_NC - 1) < n; j += 4 * PAIR_NC) {
-      double a[PAIR_NC][PK];
+    for (; j + 4 * (NC - 1) < n; j += 4 * NC) {
+      double a[NC][PK];
 #pragma unroll
-      for (int c = 0; c < PAIR_NC; ++c) {
+      for (int c = 0; c < NC; ++c) {
         const double* cc = Ar + (size_t)(j + 4 * c) * ld;
 #pragma unroll
         for (int k = 0; k < PK; ++k) a[c][k] = ok[k] ? cc[64 * k] : 0.0;
       }
-      double sc[PAIR_NC];
+      double sc[NV][NC];
 #pragma unroll
-      for (int c = 0; c < PAIR_NC; ++c) {
-        const double xc = x[j + 4 * c];
-        double acc = 0.0;
+      for (int q = 0; q < NV; ++q) {
 #pragma unroll
-        for (int k = 0; k < PK; ++k) {
-          acc = fma(a[c][k], wr[k], acc);
-          ya[k] = fma(a[c][k], xc, ya[k]);
+        for (int c = 0; c < NC; ++c) {
+          const double xc = x[q][j + 4 * c];
+          double acc = 0.0;
+#pragma unroll
+          for (int k = 0; k < PK; ++k) {
+            acc = fma(a[c][k], wr[q][k], acc);
+            ya[q][k] = fma(a[c][k], xc, ya[q][k]);
+          }
+          sc[q][c] = acc;
         }
-        sc[c] = acc;
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) {
 #pragma unroll
-        for (int c = 0; c < PAIR_NC; ++c) sc[c] += __shfl_xor(sc[c], o);
+        for (int q = 0; q < NV; ++q)
+#pragma unroll
+          for (int c = 0; c < NC; ++c) sc[q][c] += __shfl_xor(sc[q][c], o);
       }
       if (lane == 0) {
 #pragma unroll
-        for (int c = 0; c < PAIR_NC; ++c) g[j + 4 * c] = r0 ? g[j + 4 * c] + sc[c] : sc[c];
+        for (int q = 0; q < NV; ++q)
+#pragma unroll
+          for (int c = 0; c < NC; ++c) g[q][j + 4 * c] = r0 ? g[q][j + 4 * c] + sc[q][c] : sc[q][c];
       }
     }
     for (; j < n; j += 4) {
@@ -437,23 +452,43 @@ __device__ __forceinline__ void gemv_pair(const double* __restrict__ A, int ld, 
       double a0[PK];
 #pragma unroll
       for (int k = 0; k < PK; ++k) a0[k] = ok[k] ? c0[64 * k] : 0.0;
-      const double x0 = x[j];
-      double s0 = 0.0;
 #pragma unroll
-      for (int k = 0; k < PK; ++k) {
-        s0 = fma(a0[k], wr[k], s0);
-        ya[k] = fma(a0[k], x0, ya[k]);
+      for (int q = 0; q < NV; ++q) {
+        const double x0 = x[q][j];
+        double s0 = 0.0;
+#pragma unroll
+        for (int k = 0; k < PK; ++k) {
+          s0 = fma(a0[k], wr[q][k], s0);
+          ya[q][k] = fma(a0[k], x0, ya[q][k]);
+        }
+        s0 = cwave_sum(s0);
+        if (lane == 0) g[q][j] = r0 ? g[q][j] + s0 : s0;
       }
-      s0 = cwave_sum(s0);
-      if (lane == 0) g[j] = r0 ? g[j] + s0 : s0;
     }
 #pragma unroll
-    for (int k = 0; k < PK; ++k) ys[wv * (64 * PK) + lane + 64 * k] = ya[k];
+    for (int q = 0; q < NV; ++q)
+#pragma unroll
+      for (int k = 0; k < PK; ++k) ys[(q * 4 + wv) * (64 * PK) + lane + 64 * k] = ya[q][k];
     __syncthreads();
-    for (int r = threadIdx.x; r < (64 * PK) && r0 + r < m; r += CTPB)
-      y[r0 + r] = (ys[r] + ys[(64 * PK) + r]) + (ys[2 * (64 * PK) + r] + ys[3 * (64 * PK) + r]);
+    for (int q = 0; q < NV; ++q) {
+      const double* yq = ys + q * 4 * (64 * PK);
+      for (int r = threadIdx.x; r < (64 * PK) && r0 + r < m; r += CTPB)
+        y[q][r0 + r] = (yq[r] + yq[(64 * PK) + r]) + (yq[2 * (64 * PK) + r] + yq[3 * (64 * PK) + r]);
+    }
     __syncthreads();
   }
+}
+
+template <int PK = PAIR_K>
+__device__ __forceinline__ void gemv_pair(const double* __restrict__ A, int ld, int m, int n,
+                                          const double* __restrict__ x, const double* __restrict__ w,
+                                          double* __restrict__ y, double* __restrict__ g,
+                                          double* __restrict__ ys) {
+  const double* xs[1] = {x};
+  const double* ws[1] = {w};
+  double* yv[1] = {y};
+  double* gv[1] = {g};
+  gemv_multi<1, PK>(A, ld, m, n, xs, ws, yv, gv, ys);
 }
 
 struct ConicProblem {
@@ -507,6 +542,79 @@ __device__ __forceinline__ void MT_apply(const ConicProblem& pr, const ConeDesc*
   const double s = cblock_sum(cp + bq, red);
   if (t == 0) out[n + m] = s;
   __syncthreads();
+}
+
+// M and Mᵀ applies of two sequences sharing one sweep over A (each sequence's
+// arithmetic as M_apply / MT_apply; scratch per sequence)
+__device__ __forceinline__ void M_apply2(const ConicProblem& pr, const ConeDesc* cones, int ncones,
+                                         const double* z0, double* out0, double* Dv0, double* Au0, double* g0,
+                                         const double* z1, double* out1, double* Dv1, double* Au1, double* g1,
+                                         double* lds, double* red, double* ys) {
+  const int n = pr.n, m = pr.m, t = threadIdx.x;
+  dpi_apply(cones, ncones, pr.v, pr.P, z0 + n, Dv0, 0, lds, red);
+  dpi_apply(cones, ncones, pr.v, pr.P, z1 + n, Dv1, 0, lds, red);
+  const double* xs[2] = {z0, z1};
+  const double* ws[2] = {Dv0, Dv1};
+  double* yv[2] = {Au0, Au1};
+  double* gv[2] = {g0, g1};
+  gemv_multi<2>(pr.A, m, m, n, xs, ws, yv, gv, ys);
+  const double* zz[2] = {z0, z1};
+  double* oo[2] = {out0, out1};
+  const double* dd[2] = {Dv0, Dv1};
+  const double* aa[2] = {Au0, Au1};
+  const double* gg[2] = {g0, g1};
+  for (int q = 0; q < 2; ++q) {
+    const double* z = zz[q];
+    double* out = oo[q];
+    const double w = z[n + m];
+    double cu = 0.0, bd = 0.0;
+    for (int j = t; j < n; j += CTPB) {
+      out[j] = -gg[q][j] + pr.c[j] * w;
+      cu = fma(pr.c[j], z[j], cu);
+    }
+    for (int i = t; i < m; i += CTPB) {
+      out[n + i] = aa[q][i] + z[n + i] - dd[q][i] + pr.b[i] * w;
+      bd = fma(pr.b[i], dd[q][i], bd);
+    }
+    const double s = cblock_sum(-cu - bd, red);
+    if (t == 0) out[n + m] = s;
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void MT_apply2(const ConicProblem& pr, const ConeDesc* cones, int ncones,
+                                          const double* r0v, double* out0, double* tmpm0, double* Ap0, double* g0,
+                                          const double* r1v, double* out1, double* tmpm1, double* Ap1, double* g1,
+                                          double* lds, double* red, double* ys) {
+  const int n = pr.n, m = pr.m, t = threadIdx.x;
+  const double* xs[2] = {r0v, r1v};
+  const double* ws[2] = {r0v + n, r1v + n};
+  double* yv[2] = {Ap0, Ap1};
+  double* gv[2] = {g0, g1};
+  gemv_multi<2>(pr.A, m, m, n, xs, ws, yv, gv, ys);
+  const double* rr[2] = {r0v, r1v};
+  double* oo[2] = {out0, out1};
+  double* tm[2] = {tmpm0, tmpm1};
+  for (int q = 0; q < 2; ++q) {
+    const double* r = rr[q];
+    double* out = oo[q];
+    const double tw = r[n + m];
+    for (int i = t; i < m; i += CTPB) tm[q][i] = -yv[q][i] - r[n + i] - pr.b[i] * tw;
+    __syncthreads();
+    dpi_apply(cones, ncones, pr.v, pr.P, tm[q], out + n, 1, lds, red);
+    double cp = 0.0, bq = 0.0;
+    for (int j = t; j < n; j += CTPB) {
+      out[j] = gv[q][j] - pr.c[j] * tw;
+      cp = fma(pr.c[j], r[j], cp);
+    }
+    for (int i = t; i < m; i += CTPB) {
+      out[n + i] += r[n + i];
+      bq = fma(pr.b[i], r[n + i], bq);
+    }
+    const double s = cblock_sum(cp + bq, red);
+    if (t == 0) out[n + m] = s;
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -644,6 +752,213 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
   if (t == 0 && info) {
     info[bidx] = istop;
     info[gridDim.x + bidx] = it;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Co-iterated LSQR: the forward and the reverse sequence of one problem in
+// one workgroup, in lockstep, so every M / Mᵀ apply of the two shares one
+// sweep over A (gemv_multi<2>) — half the A traffic of two separate runs.
+// Each sequence keeps its own scalars, stopping tests and iteration count
+// (per-direction rules of conic_lsqr_kernel, oracle/lsqr.py); once one has
+// stopped, the other continues on the single applies, so both results are
+// bit-identical to two conic_lsqr_kernel runs.
+// ---------------------------------------------------------------------------
+struct LsqrSeq {
+  double *x, *u, *vv, *w, *tmp, *s1, *s2, *s4;
+  const double* rb;
+  double alpha, beta, anorm, ddnorm, res2, xxnorm, zz, sn2, cs2, rhobar, phibar, bnorm;
+  int it, istop;
+  bool live;
+};
+
+__global__ __launch_bounds__(CTPB) __attribute__((amdgpu_waves_per_eu(2))) void conic_lsqr2_kernel(
+    const ConeDesc* __restrict__ cones_g, int ncones, const double* __restrict__ A,
+    const double* __restrict__ b, const double* __restrict__ c,
+    const double* __restrict__ v, const double* __restrict__ P, int plen, int m, int n,
+    const double* __restrict__ rhs_f, double tol_f, const double* __restrict__ rhs_r, double tol_r,
+    double* __restrict__ work, double* __restrict__ xout_f, double* __restrict__ xout_r,
+    int32_t* __restrict__ info_f, int32_t* __restrict__ info_r) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ double red[4];
+  __shared__ ConeDesc cones[128];
+  __shared__ double ys[2 * 4 * PAIR_ROWS];
+  const int bidx = blockIdx.x, t = threadIdx.x;
+  const int N = n + m + 1;
+  const ConeDesc* cn = cones_g;
+  if (ncones <= 128) {
+    for (int k = t; k < ncones; k += CTPB) cones[k] = cones_g[k];
+    cn = cones;
+  }
+  ConicProblem pr;
+  pr.A = A + (size_t)bidx * m * n;
+  pr.b = b + (size_t)bidx * m;
+  pr.c = c + (size_t)bidx * n;
+  pr.v = v + (size_t)bidx * m;
+  pr.P = P + (size_t)bidx * plen;
+  pr.m = m;
+  pr.n = n;
+  const size_t wl = (size_t)5 * N + 3 * (size_t)m + n;
+  LsqrSeq S[2];
+  for (int q = 0; q < 2; ++q) {
+    LsqrSeq& Q = S[q];
+    Q.x = work + ((size_t)2 * bidx + q) * wl;
+    Q.u = Q.x + N;
+    Q.vv = Q.u + N;
+    Q.w = Q.vv + N;
+    Q.tmp = Q.w + N;
+    Q.s1 = Q.tmp + N;
+    Q.s2 = Q.s1 + m;
+    Q.s4 = Q.s2 + 2 * (size_t)m;
+    Q.rb = (q == 0 ? rhs_f : rhs_r) + (size_t)bidx * N;
+    Q.it = 0;
+    Q.istop = 0;
+    Q.live = false;
+    double bb = 0.0;
+    for (int i = t; i < N; i += CTPB) {
+      const double r = Q.rb[i];
+      Q.u[i] = r;
+      Q.x[i] = 0.0;
+      bb = fma(r, r, bb);
+    }
+    Q.beta = sqrt(cblock_sum(bb, red));
+  }
+  const bool go0 = S[0].beta > tol_f, go1 = S[1].beta > tol_r;
+  for (int q = 0; q < 2; ++q)
+    if (q == 0 ? go0 : go1)
+      for (int i = t; i < N; i += CTPB) S[q].u[i] /= S[q].beta;
+  __syncthreads();
+  if (go0 && go1)
+    MT_apply2(pr, cn, ncones, S[0].u, S[0].vv, S[0].s1, S[0].s2, S[0].s4, S[1].u, S[1].vv, S[1].s1, S[1].s2,
+              S[1].s4, lds, red, ys);
+  else if (go0 || go1) {
+    LsqrSeq& Q = S[go0 ? 0 : 1];
+    MT_apply(pr, cn, ncones, Q.u, Q.vv, Q.s1, Q.s2, Q.s4, lds, red, ys);
+  }
+  for (int q = 0; q < 2; ++q) {
+    if (!(q == 0 ? go0 : go1)) continue;
+    LsqrSeq& Q = S[q];
+    double aa = 0.0;
+    for (int i = t; i < N; i += CTPB) aa = fma(Q.vv[i], Q.vv[i], aa);
+    Q.alpha = sqrt(cblock_sum(aa, red));
+    if (Q.alpha > 0.0) {
+      for (int i = t; i < N; i += CTPB) { Q.vv[i] /= Q.alpha; Q.w[i] = Q.vv[i]; }
+      __syncthreads();
+      Q.anorm = Q.ddnorm = Q.res2 = Q.xxnorm = Q.zz = 0.0;
+      Q.sn2 = 0.0;
+      Q.cs2 = -1.0;
+      Q.rhobar = Q.alpha;
+      Q.phibar = Q.beta;
+      Q.bnorm = Q.beta;
+      Q.live = true;
+    }
+  }
+  const double eps = 2.220446049250313e-16;
+  const double atol = sqrt(eps), btol = sqrt(eps), ctol = sqrt(eps);
+  const int maxiter = N;
+  while (S[0].live || S[1].live) {
+    // M·v of the live sequences
+    if (S[0].live && S[1].live)
+      M_apply2(pr, cn, ncones, S[0].vv, S[0].tmp, S[0].s1, S[0].s2, S[0].s4, S[1].vv, S[1].tmp, S[1].s1, S[1].s2,
+               S[1].s4, lds, red, ys);
+    else {
+      LsqrSeq& Q = S[S[0].live ? 0 : 1];
+      M_apply(pr, cn, ncones, Q.vv, Q.tmp, Q.s1, Q.s2, Q.s4, lds, red, ys);
+    }
+    bool mt[2] = {false, false};
+    for (int q = 0; q < 2; ++q) {
+      LsqrSeq& Q = S[q];
+      if (!Q.live) continue;
+      ++Q.it;
+      double su = 0.0;
+      for (int i = t; i < N; i += CTPB) { const double ui = Q.tmp[i] - Q.alpha * Q.u[i]; Q.u[i] = ui; su = fma(ui, ui, su); }
+      Q.beta = sqrt(cblock_sum(su, red));
+      if (Q.beta > 0.0) {
+        for (int i = t; i < N; i += CTPB) Q.u[i] /= Q.beta;
+        __syncthreads();
+        Q.anorm = sqrt(Q.anorm * Q.anorm + Q.alpha * Q.alpha + Q.beta * Q.beta);
+        mt[q] = true;
+      }
+    }
+    // Mᵀ·u of those with β > 0
+    if (mt[0] && mt[1])
+      MT_apply2(pr, cn, ncones, S[0].u, S[0].tmp, S[0].s1, S[0].s2, S[0].s4, S[1].u, S[1].tmp, S[1].s1, S[1].s2,
+                S[1].s4, lds, red, ys);
+    else if (mt[0] || mt[1]) {
+      LsqrSeq& Q = S[mt[0] ? 0 : 1];
+      MT_apply(pr, cn, ncones, Q.u, Q.tmp, Q.s1, Q.s2, Q.s4, lds, red, ys);
+    }
+    for (int q = 0; q < 2; ++q) {
+      LsqrSeq& Q = S[q];
+      if (!Q.live) continue;
+      if (mt[q]) {
+        double sv = 0.0;
+        for (int i = t; i < N; i += CTPB) { const double vi = Q.tmp[i] - Q.beta * Q.vv[i]; Q.vv[i] = vi; sv = fma(vi, vi, sv); }
+        Q.alpha = sqrt(cblock_sum(sv, red));
+        if (Q.alpha > 0.0) for (int i = t; i < N; i += CTPB) Q.vv[i] /= Q.alpha;
+        __syncthreads();
+      }
+      const double rhobar1 = Q.rhobar;
+      const double rho = hypot(rhobar1, Q.beta);
+      const double cs = rhobar1 / rho, sn = Q.beta / rho;
+      const double theta = sn * Q.alpha;
+      Q.rhobar = -cs * Q.alpha;
+      const double phi = cs * Q.phibar;
+      Q.phibar = sn * Q.phibar;
+      const double tau = sn * phi;
+      const double t1 = phi / rho, t2 = -theta / rho;
+      double sw = 0.0;
+      for (int i = t; i < N; i += CTPB) {
+        const double wi = Q.w[i];
+        sw = fma(wi, wi, sw);
+        Q.x[i] = Q.x[i] + t1 * wi;
+        Q.w[i] = Q.vv[i] + t2 * wi;
+      }
+      Q.ddnorm += cblock_sum(sw, red) / (rho * rho);
+      const double delta = Q.sn2 * rho, gambar = -Q.cs2 * rho;
+      const double rhs_ = phi - delta * Q.zz;
+      const double zbar = rhs_ / gambar;
+      const double xnorm = sqrt(Q.xxnorm + zbar * zbar);
+      const double gamma = hypot(gambar, theta);
+      Q.cs2 = gambar / gamma;
+      Q.sn2 = theta / gamma;
+      Q.zz = rhs_ / gamma;
+      Q.xxnorm += Q.zz * Q.zz;
+      const double acond = Q.anorm * sqrt(Q.ddnorm);
+      const double rnorm = sqrt(Q.phibar * Q.phibar + Q.res2);
+      const double arnorm = Q.alpha * fabs(tau);
+      const double test1 = rnorm / Q.bnorm;
+      const double test2 = (Q.anorm * rnorm != 0.0) ? arnorm / (Q.anorm * rnorm) : 0.0;
+      const double test3 = (acond != 0.0) ? 1.0 / acond : 0.0;
+      const double t1r = test1 / (1.0 + Q.anorm * xnorm / Q.bnorm);
+      const double rtol = btol + atol * Q.anorm * xnorm / Q.bnorm;
+      int istop = 0;
+      if (Q.it >= maxiter) istop = 7;
+      if (1.0 + test3 <= 1.0) istop = 6;
+      if (1.0 + test2 <= 1.0) istop = 5;
+      if (1.0 + t1r <= 1.0) istop = 4;
+      if (test3 <= ctol) istop = 3;
+      if (test2 <= atol) istop = 2;
+      if (test1 <= rtol) istop = 1;
+      Q.istop = istop;
+      __syncthreads();
+      if (istop) Q.live = false;
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < N; i += CTPB) {
+    xout_f[(size_t)bidx * N + i] = S[0].x[i];
+    xout_r[(size_t)bidx * N + i] = S[1].x[i];
+  }
+  if (t == 0) {
+    if (info_f) {
+      info_f[bidx] = S[0].istop;
+      info_f[gridDim.x + bidx] = S[0].it;
+    }
+    if (info_r) {
+      info_r[bidx] = S[1].istop;
+      info_r[gridDim.x + bidx] = S[1].it;
+    }
   }
 }
 
@@ -1267,7 +1582,7 @@ static void conic_lsqr(Handle& h, double tol, double* out) {
   const size_t N = (size_t)n + m + 1;
   const size_t wl = 5 * N + 3 * (size_t)m + n;
   h.cwork.ensure((size_t)B * (wl + N) * sizeof(double));
-  h.cinfo.ensure((size_t)2 * std::max(B, 1) * sizeof(int32_t));
+  h.cinfo.ensure((size_t)4 * std::max(B, 1) * sizeof(int32_t));
   double* rhs = h.cwork.as<double>() + (size_t)B * wl;
   if (use_split(h)) {
     conic_lsqr_split(h, tol, rhs, out);
@@ -1323,6 +1638,57 @@ void conic_reverse(Handle& h, const double* dx, double* out_g, double* out_dA, d
                        h.vp.as<double>() + (size_t)B * m, m, n, out_dA, out_db, out_dc);
     ccheck();
   }
+}
+
+// Forward and reverse of every problem in one call: both right-hand sides,
+// then the co-iterated LSQR (conic_lsqr2_kernel: one sweep over A per M / Mᵀ
+// apply for both directions), then both output kernels.  Results are
+// bit-identical to conic_forward + conic_reverse.  Info: the reverse run's
+// [istop | iterations] where a single call leaves them (dopt_get_info), the
+// forward run's behind it (dopt_conic_lsqr_stats).  The split path (m >
+// 2·PAIR_ROWS) runs the two directions one after the other.
+void conic_forward_reverse(Handle& h, const double* dA, const double* db, const double* dc, const double* dx,
+                           double* out_f, double* out_dx, double* out_g, double* out_dA, double* out_db,
+                           double* out_dc) {
+  if (!h.cfactored) conic_factor(h);
+  const int B = (int)h.batch, m = h.m, n = h.n;
+  h.cinfo.ensure((size_t)4 * std::max(B, 1) * sizeof(int32_t));
+  if (use_split(h)) {
+    conic_forward(h, dA, db, dc, out_f, out_dx);
+    DOPT_CHECK_HIP(hipMemcpyAsync(h.cinfo.as<int32_t>() + 2 * B, h.cinfo.p, 2 * B * sizeof(int32_t),
+                                  hipMemcpyDeviceToDevice, h.stream));
+    conic_reverse(h, dx, out_g, out_dA, out_db, out_dc);
+    return;
+  }
+  const int nc = (int)h.cones.size() / 2;
+  const size_t N = (size_t)n + m + 1;
+  const size_t wl = 5 * N + 3 * (size_t)m + n;
+  h.cwork.ensure((size_t)B * (2 * wl + 2 * N) * sizeof(double));
+  double* rhs_f = h.cwork.as<double>() + (size_t)B * 2 * wl;
+  double* rhs_r = rhs_f + (size_t)B * N;
+  {
+    PhaseTimer pt(h, DOPT_PHASE_CONIC_RHS);
+    hipLaunchKernelGGL(conic_fwd_rhs_kernel, dim3(B), dim3(CTPB), 0, h.stream, dA, db, dc, h.cx,
+                       h.vp.as<double>() + (size_t)B * m, m, n, rhs_f);
+    hipLaunchKernelGGL(conic_rev_rhs_kernel, dim3(B), dim3(CTPB), 0, h.stream, dx, h.cx, m, n, rhs_r);
+    ccheck();
+  }
+  {
+    PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
+    int32_t* info = h.cinfo.as<int32_t>();
+    hipLaunchKernelGGL(conic_lsqr2_kernel, dim3(B), dim3(CTPB), dpi_lds_bytes(h.cones), h.stream,
+                       h.cone_dev.as<ConeDesc>(), nc, h.cA, h.cb, h.cc, h.vp.as<double>(), h.dpi.as<double>(),
+                       h.dpi_len, m, n, rhs_f, 0.0, rhs_r, 1e-4, h.cwork.as<double>(), out_f, out_g,
+                       info + 2 * B, info);
+    ccheck();
+  }
+  PhaseTimer pt(h, DOPT_PHASE_CONIC_OUTPUT);
+  if (out_dx)
+    hipLaunchKernelGGL(conic_fwd_out_kernel, dim3(B), dim3(CTPB), 0, h.stream, out_f, h.cx, m, n, out_dx);
+  if (out_dA || out_db || out_dc)
+    hipLaunchKernelGGL(conic_rev_out_kernel, dim3(B), dim3(CTPB), 0, h.stream, out_g, h.cx,
+                       h.vp.as<double>() + (size_t)B * m, m, n, out_dA, out_db, out_dc);
+  ccheck();
 }
 
 }  // namespace dopt

@@ -232,6 +232,9 @@ void conic_forward(Handle& h, const double* dA, const double* db, const double* 
                    double* out, double* out_dx);
 void conic_reverse(Handle& h, const double* dx, double* out_g, double* out_dA,
                    double* out_db, double* out_dc);
+void conic_forward_reverse(Handle& h, const double* dA, const double* db, const double* dc, const double* dx,
+                           double* out_f, double* out_dx, double* out_g, double* out_dA, double* out_db,
+                           double* out_dc);
 
 inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 

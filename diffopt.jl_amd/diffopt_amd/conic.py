@@ -138,6 +138,39 @@ class ConicBatch:
             dA = dA.transpose(0, 2, 1) if not dev else dA.transpose(1, 2)
         return g, dA, db, dc
 
+    def forward_reverse(self, dx, dA=None, db=None, dc=None, want_dA=True):
+        """Both directions in one call, the two LSQR runs co-iterated
+        (dopt_conic_forward_reverse): ((out, dx_fwd), (g, dA, db, dc)) as
+        ``forward`` / ``reverse`` return them, bit-identical to those calls."""
+        B, n, m = self.batch, self.n, self.m
+        st = self._stage([dA, db, dc, dx])
+        dev = st.mem == _lib.DOPT_MEM_DEVICE
+        args = [colmajor(dA, (B, m, n)) if dA is not None else None,
+                vector(db, (B, m)) if db is not None else None,
+                vector(dc, (B, n)) if dc is not None else None,
+                vector(dx, (B, n))]
+        out = Staged.empty((B, self.N), dev)
+        fdx = Staged.empty((B, n), dev)
+        g = Staged.empty((B, self.N), dev)
+        rA = Staged.empty((B, n, m), dev) if want_dA else None
+        rb = Staged.empty((B, m), dev)
+        rc_ = Staged.empty((B, n), dev)
+        rc = self.lib.dopt_conic_forward_reverse(self.h, *[st.ptr(a) for a in args], st.ptr(out), st.ptr(fdx),
+                                                 st.ptr(g), st.ptr(rA), st.ptr(rb), st.ptr(rc_))
+        _lib.check(rc, self.h)
+        if rA is not None:
+            rA = rA.transpose(0, 2, 1) if not dev else rA.transpose(1, 2)
+        return (out, fdx), (g, rA, rb, rc_)
+
+    def lsqr_stats(self):
+        """(istop, iterations) of the last run and, after ``forward_reverse``,
+        of its forward run: dict of (B,) arrays."""
+        buf = np.zeros(4 * self.batch, dtype=np.int32)
+        _lib.check(self.lib.dopt_conic_lsqr_stats(self.h, buf.ctypes.data), self.h)
+        B = self.batch
+        return {"istop": buf[:B], "iterations": buf[B:2 * B], "fwd_istop": buf[2 * B:3 * B],
+                "fwd_iterations": buf[3 * B:]}
+
     def info(self):
         buf = np.zeros(self.batch, dtype=np.int32)
         _lib.check(self.lib.dopt_get_info(self.h, buf.ctypes.data), self.h)

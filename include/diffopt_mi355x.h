@@ -219,6 +219,20 @@ int dopt_conic_forward(dopt_handle* h, const double* dA, const double* db,
  * (getters :396-443). */
 int dopt_conic_reverse(dopt_handle* h, const double* dx, double* out_g,
                        double* out_dA, double* out_db, double* out_dc);
+/* forward_differentiate! and reverse_differentiate! of every problem in one
+ * call (the bench step): both LSQR runs co-iterated in one kernel, sharing
+ * each sweep over A (ConicProgram.jl:323, :372; per-direction stopping rules
+ * kept), outputs as dopt_conic_forward (out, out_dx) and dopt_conic_reverse
+ * (out_g, out_dA, out_db, out_dc; any of out_dx / out_dA / out_db / out_dc
+ * may be NULL).  Bit-identical to the two separate calls. */
+int dopt_conic_forward_reverse(dopt_handle* h, const double* dA, const double* db,
+                               const double* dc, const double* dx, double* out,
+                               double* out_dx, double* out_g, double* out_dA,
+                               double* out_db, double* out_dc);
+/* LSQR statistics of the last conic call, 4·B int32: [istop | iterations] of
+ * the last (or, after dopt_conic_forward_reverse, the reverse) run, then
+ * [istop | iterations] of the forward run of dopt_conic_forward_reverse. */
+int dopt_conic_lsqr_stats(dopt_handle* h, int32_t* stats);
 
 /* ---- introspection ---------------------------------------------------------*/
 /* per-problem status of the last factor/solve: QP: 0 ok, k>0 zero pivot at

@@ -374,3 +374,32 @@ def test_config5_structure_multi_rowblock(ConicBatch):
     # config-5 structure (PSD(50) cones, m ≫ n) at oracle speed: 3 PSD(50)
     # → m = 3825 = 8 row blocks, auto split path
     _synthetic_check(ConicBatch, 2, 100, [(4, 1275)] * 3, 16, "config-5 structure, 3 cones", cap=1)
+
+
+# ---------------------------------------------------------------------------
+# co-iterated forward + reverse (dopt_conic_forward_reverse, conic_lsqr2_kernel):
+# one sweep over A per M / Mᵀ apply for both directions, per-direction stopping
+# rules — bit-identical to the two separate calls, iteration counts included
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("shape", [
+    ("mixed cones", 3, 30, [(0, 3), (1, 10), (3, 6), (2, 4), (4, 6)], 11),
+    ("well-posed SOC", 2, 100, [(3, 10)] * 20, 21),
+    ("config-4 bench shape", 2, 500, [(3, 25)] * 20, 14),
+], ids=lambda s: s[0])
+def test_forward_reverse_coiterated_bitwise(ConicBatch, shape):
+    from diffopt_amd.synthetic import conic_numpy
+    _, B, n, cones, seed = shape
+    d = conic_numpy(B, n, cones, seed)
+    e = ConicBatch(B, n, cones)
+    e.set(d["A"], d["b"], d["c"], d["x"], d["s"], d["y"])
+    out, fdx = e.forward(d["dA"], d["db"], d["dc"])
+    it_f = e.iterations().copy()
+    g, dA, db, dc = e.reverse(d["dx"])
+    it_r = e.iterations().copy()
+    (out2, fdx2), (g2, dA2, db2, dc2) = e.forward_reverse(d["dx"], d["dA"], d["db"], d["dc"])
+    for a, b in [(out, out2), (fdx, fdx2), (g, g2), (dA, dA2), (db, db2), (dc, dc2)]:
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+    st = e.lsqr_stats()
+    np.testing.assert_array_equal(st["fwd_iterations"], it_f)
+    np.testing.assert_array_equal(st["iterations"], it_r)
+    e.close()
