@@ -1058,6 +1058,11 @@ __global__ __launch_bounds__(CTPB) void conic_rev_out_kernel(
 // Scalars live in a per-problem LsqrState; a finished problem sets `done`
 // and every later launch returns at once for it.  The host checks the count
 // of unfinished problems every SPLIT_CHUNK iterations.
+// Co-iteration (dopt_conic_forward_reverse): nq = 2 sequences per problem as
+// 2B virtual problems q·B + b sharing problem b's data; the per-sequence
+// kernels run on all 2B, the pass kernel sweeps each row block of A once for
+// both live sequences of its problem (gemv_multi<2>, each product in the
+// single-sequence order: bit-identical to two separate runs).
 // ---------------------------------------------------------------------------
 constexpr int SPLIT_CHUNK = 8;
 #ifndef DOPT_SPLIT_K
@@ -1072,9 +1077,11 @@ struct LsqrState {
 };
 
 struct SplitWS {
-  // per-problem vectors (stride N or m), partial Aᵀ products (RB·n)
+  // per-sequence vectors (stride N or m), partial Aᵀ products (RB·n)
   double *x, *u, *v, *w, *out, *Dv, *tmpm, *yb, *gpart;
   int N, m, n, RB;
+  int B;   // problems; sequence bv belongs to problem bv % B
+  __device__ int phys(int bv) const { return bv % B; }
   __device__ double* vec(double* base, int b) const { return base + (size_t)b * N; }
   __device__ double* mvec(double* base, int b) const { return base + (size_t)b * m; }
 };
@@ -1085,10 +1092,11 @@ __device__ __forceinline__ void split_finish(int b, int32_t* active, LsqrState& 
 }
 
 __global__ __launch_bounds__(CTPB) void conic_split_init_kernel(
-    const double* __restrict__ rhs, double tol, SplitWS ws, LsqrState* __restrict__ stv,
+    const double* __restrict__ rhs, double tol0, double tol1, SplitWS ws, LsqrState* __restrict__ stv,
     int32_t* __restrict__ active) {
   __shared__ double red[4];
   const int b = blockIdx.x, t = threadIdx.x, N = ws.N;
+  const double tol = b < ws.B ? tol0 : tol1;
   const double* rb = rhs + (size_t)b * N;
   double* u = ws.vec(ws.u, b);
   double* x = ws.vec(ws.x, b);
@@ -1112,32 +1120,50 @@ __global__ __launch_bounds__(CTPB) void conic_split_init_kernel(
 
 // rows [r0, r0+rows) of the pair of products; `dir` 0: M·v (x = v_n, w = Dv),
 // 1: Mᵀ·u (x = u_n, w = u_m)
+// grid (row blocks, problems): every live sequence of problem b (nq of them)
+// from one sweep over the row block
 __global__ __launch_bounds__(CTPB) void conic_split_pass_kernel(
     int dir, const double* __restrict__ A, const double* __restrict__ bvec, SplitWS ws,
-    const LsqrState* __restrict__ stv) {
-  __shared__ double ys[4 * SPLIT_ROWS];
+    const LsqrState* __restrict__ stv, int nq) {
+  __shared__ double ys[2 * 4 * SPLIT_ROWS];
   const int rb = blockIdx.x, b = blockIdx.y;
-  const LsqrState& st = stv[b];
-  if (st.done || (dir == 1 && st.skipT)) return;
+  int sq[2], cnt = 0;
+  for (int q = 0; q < nq; ++q) {
+    const LsqrState& st = stv[q * ws.B + b];
+    if (!(st.done || (dir == 1 && st.skipT))) sq[cnt++] = q * ws.B + b;
+  }
+  if (cnt == 0) return;   // workgroup-uniform
   const int m = ws.m, n = ws.n, N = ws.N;
   const int r0 = rb * SPLIT_ROWS;
   const int rows = min(SPLIT_ROWS, m - r0);
   const double* Ab = A + (size_t)b * m * n + r0;
-  const double* src = dir == 0 ? ws.vec(ws.v, b) : ws.vec(ws.u, b);
-  const double* wv = dir == 0 ? ws.mvec(ws.Dv, b) + r0 : src + n + r0;
-  double* yb = ws.mvec(ws.yb, b) + r0;
-  gemv_pair<SPLIT_K>(Ab, m, rows, n, src, wv, yb, ws.gpart + ((size_t)b * ws.RB + rb) * n, ys);
-  const double last = src[N - 1];
+  const double* src[2];
+  const double* wv[2];
+  double* yb[2];
+  double* gp[2];
+  for (int c = 0; c < cnt; ++c) {
+    const int bv = sq[c];
+    src[c] = dir == 0 ? ws.vec(ws.v, bv) : ws.vec(ws.u, bv);
+    wv[c] = dir == 0 ? ws.mvec(ws.Dv, bv) + r0 : src[c] + n + r0;
+    yb[c] = ws.mvec(ws.yb, bv) + r0;
+    gp[c] = ws.gpart + ((size_t)bv * ws.RB + rb) * n;
+  }
+  if (cnt == 2) gemv_multi<2, SPLIT_K>(Ab, m, rows, n, src, wv, yb, gp, ys);
+  else gemv_multi<1, SPLIT_K>(Ab, m, rows, n, src, wv, yb, gp, ys);
   const double* bb = bvec + (size_t)b * m + r0;
-  if (dir == 0) {
-    double* o = ws.vec(ws.out, b) + n + r0;
-    const double* vm = src + n + r0;
-    const double* Dv = ws.mvec(ws.Dv, b) + r0;
-    for (int i = threadIdx.x; i < rows; i += CTPB) o[i] = yb[i] + vm[i] - Dv[i] + bb[i] * last;
-  } else {
-    double* tm = ws.mvec(ws.tmpm, b) + r0;
-    const double* um = src + n + r0;
-    for (int i = threadIdx.x; i < rows; i += CTPB) tm[i] = -yb[i] - um[i] - bb[i] * last;
+  for (int c = 0; c < cnt; ++c) {
+    const int bv = sq[c];
+    const double last = src[c][N - 1];
+    if (dir == 0) {
+      double* o = ws.vec(ws.out, bv) + n + r0;
+      const double* vm = src[c] + n + r0;
+      const double* Dv = ws.mvec(ws.Dv, bv) + r0;
+      for (int i = threadIdx.x; i < rows; i += CTPB) o[i] = yb[c][i] + vm[i] - Dv[i] + bb[i] * last;
+    } else {
+      double* tm = ws.mvec(ws.tmpm, bv) + r0;
+      const double* um = src[c] + n + r0;
+      for (int i = threadIdx.x; i < rows; i += CTPB) tm[i] = -yb[c][i] - um[i] - bb[i] * last;
+    }
   }
 }
 
@@ -1151,8 +1177,8 @@ __global__ __launch_bounds__(CTPB) void conic_split_dpi_kernel(
   const LsqrState& st = stv[b];
   if (st.done || (dir == 1 && st.skipT)) return;
   const ConeDesc cd = cones_g[k];
-  const double* pv = vcone + (size_t)b * ws.m;
-  const double* pp = P + (size_t)b * plen;
+  const double* pv = vcone + (size_t)ws.phys(b) * ws.m;
+  const double* pp = P + (size_t)ws.phys(b) * plen;
   if (dir == 0)
     dpi_apply(&cd, 1, pv, pp, ws.vec(ws.v, b) + ws.n, ws.mvec(ws.Dv, b), 0, lds, red);
   else
@@ -1239,8 +1265,8 @@ __global__ __launch_bounds__(VT) void conic_split_upd_u_kernel(
   const double* v = ws.vec(ws.v, b);
   double* out = ws.vec(ws.out, b);
   double* u = ws.vec(ws.u, b);
-  const double* c = cvec + (size_t)b * n;
-  const double* bb = bvec + (size_t)b * m;
+  const double* c = cvec + (size_t)ws.phys(b) * n;
+  const double* bb = bvec + (size_t)ws.phys(b) * m;
   const double* Dv = ws.mvec(ws.Dv, b);
   const double* gp = ws.gpart + (size_t)b * ws.RB * n;
   const double w = v[N - 1];
@@ -1281,8 +1307,8 @@ __device__ __forceinline__ void split_finish_T(const SplitWS& ws, int b, const d
   const int t = threadIdx.x, n = ws.n, m = ws.m, N = ws.N;
   const double* u = ws.vec(ws.u, b);
   double* out = ws.vec(ws.out, b);
-  const double* c = cvec + (size_t)b * n;
-  const double* bb = bvec + (size_t)b * m;
+  const double* c = cvec + (size_t)ws.phys(b) * n;
+  const double* bb = bvec + (size_t)ws.phys(b) * m;
   const double* gp = ws.gpart + (size_t)b * ws.RB * n;
   const double tw = u[N - 1];
   double cp = 0.0, bq = 0.0;
@@ -1433,15 +1459,19 @@ __global__ __launch_bounds__(VT) void conic_split_upd_v_kernel(
   stv[b] = st;
 }
 
+// grid nq·B: sequence bv → (xout0, info0) for bv < B, (xout1, info1) after
 __global__ __launch_bounds__(CTPB) void conic_split_out_kernel(
-    SplitWS ws, const LsqrState* __restrict__ stv, double* __restrict__ xout,
-    int32_t* __restrict__ info) {
-  const int b = blockIdx.x, t = threadIdx.x, N = ws.N;
-  const double* x = ws.vec(ws.x, b);
+    SplitWS ws, const LsqrState* __restrict__ stv, double* __restrict__ xout0, int32_t* __restrict__ info0,
+    double* __restrict__ xout1, int32_t* __restrict__ info1) {
+  const int bv = blockIdx.x, t = threadIdx.x, N = ws.N;
+  const int b = ws.phys(bv);
+  double* xout = bv < ws.B ? xout0 : xout1;
+  int32_t* info = bv < ws.B ? info0 : info1;
+  const double* x = ws.vec(ws.x, bv);
   for (int i = t; i < N; i += CTPB) xout[(size_t)b * N + i] = x[i];
   if (t == 0 && info) {
-    info[b] = stv[b].istop;
-    info[gridDim.x + b] = stv[b].it;
+    info[b] = stv[bv].istop;
+    info[ws.B + b] = stv[bv].it;
   }
 }
 
@@ -1503,71 +1533,70 @@ void conic_factor(Handle& h) {
   h.cfactored = true;
 }
 
-// Split-path LSQR (see conic_split_* above); rhs already in place.
-static void conic_lsqr_split(Handle& h, double tol, const double* rhs, double* out) {
+// Split-path LSQR (see conic_split_* above) of nq sequences per problem
+// (rhs: nq·B right-hand sides, sequence q·B + b), co-iterated for nq = 2.
+static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const double* rhs, double* out0,
+                             int32_t* info0, double* out1, int32_t* info1) {
   const int B = (int)h.batch, m = h.m, n = h.n;
+  const int V = nq * B;   // sequences
   const int nc = (int)h.cones.size() / 2;
   const int N = n + m + 1;
   const int RB = std::max(1, (m + SPLIT_ROWS - 1) / SPLIT_ROWS);
   const size_t per = (size_t)5 * N + 4 * (size_t)std::max(m, 1) + (size_t)RB * n;
-  h.csplit.ensure((size_t)B * per * sizeof(double) + (size_t)B * sizeof(LsqrState) + 64);
+  h.csplit.ensure((size_t)V * per * sizeof(double) + (size_t)V * sizeof(LsqrState) + 64);
   SplitWS ws;
   double* base = h.csplit.as<double>();
   ws.x = base;
-  ws.u = ws.x + (size_t)B * N;
-  ws.v = ws.u + (size_t)B * N;
-  ws.w = ws.v + (size_t)B * N;
-  ws.out = ws.w + (size_t)B * N;
-  ws.Dv = ws.out + (size_t)B * N;
-  ws.tmpm = ws.Dv + (size_t)B * std::max(m, 1);
-  ws.yb = ws.tmpm + (size_t)B * std::max(m, 1);
-  ws.gpart = ws.yb + (size_t)B * std::max(m, 1);
+  ws.u = ws.x + (size_t)V * N;
+  ws.v = ws.u + (size_t)V * N;
+  ws.w = ws.v + (size_t)V * N;
+  ws.out = ws.w + (size_t)V * N;
+  ws.Dv = ws.out + (size_t)V * N;
+  ws.tmpm = ws.Dv + (size_t)V * std::max(m, 1);
+  ws.yb = ws.tmpm + (size_t)V * std::max(m, 1);
+  ws.gpart = ws.yb + (size_t)V * std::max(m, 1);
   ws.N = N;
   ws.m = m;
   ws.n = n;
   ws.RB = RB;
-  LsqrState* st = reinterpret_cast<LsqrState*>(base + (size_t)B * per);
-  int32_t* active = reinterpret_cast<int32_t*>(st + B);
+  ws.B = B;
+  LsqrState* st = reinterpret_cast<LsqrState*>(base + (size_t)V * per);
+  int32_t* active = reinterpret_cast<int32_t*>(st + V);
   const size_t dl = dpi_lds_bytes(h.cones);
   const double* vcone = h.vp.as<double>();
   const double* P = h.dpi.as<double>();
   const ConeDesc* cd = h.cone_dev.as<ConeDesc>();
-  const int32_t nact = B;
+  const int32_t nact = V;
   DOPT_CHECK_HIP(hipMemcpyAsync(active, &nact, sizeof(int32_t), hipMemcpyHostToDevice, h.stream));
-  int32_t left = B;
+  int32_t left = V;
   PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
   auto passT = [&]() {
-    hipLaunchKernelGGL(conic_split_pass_kernel, dim3(RB, B), dim3(CTPB), 0, h.stream, 1, h.cA,
-                       h.cb, ws, st);
+    hipLaunchKernelGGL(conic_split_pass_kernel, dim3(RB, B), dim3(CTPB), 0, h.stream, 1, h.cA, h.cb, ws, st, nq);
     if (nc)
-      hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, B), dim3(CTPB), dl, h.stream, 1, cd,
-                         vcone, P, h.dpi_len, ws, st);
+      hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, V), dim3(CTPB), dl, h.stream, 1, cd, vcone, P,
+                         h.dpi_len, ws, st);
   };
-  hipLaunchKernelGGL(conic_split_init_kernel, dim3(B), dim3(CTPB), 0, h.stream, rhs, tol, ws, st,
-                     active);
+  hipLaunchKernelGGL(conic_split_init_kernel, dim3(V), dim3(CTPB), 0, h.stream, rhs, tol0, tol1, ws, st, active);
   passT();
-  hipLaunchKernelGGL(conic_split_init2_kernel, dim3(B), dim3(VT), 0, h.stream, h.cb, h.cc, ws,
-                     st, active);
+  hipLaunchKernelGGL(conic_split_init2_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st, active);
   ccheck();
   for (int it = 0; it < N && left > 0;) {
     for (int k = 0; k < SPLIT_CHUNK && it < N; ++k, ++it) {
       if (nc)
-        hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, B), dim3(CTPB), dl, h.stream, 0, cd,
-                           vcone, P, h.dpi_len, ws, st);
-      hipLaunchKernelGGL(conic_split_pass_kernel, dim3(RB, B), dim3(CTPB), 0, h.stream, 0, h.cA,
-                         h.cb, ws, st);
-      hipLaunchKernelGGL(conic_split_upd_u_kernel, dim3(B), dim3(VT), 0, h.stream, h.cb, h.cc,
-                         ws, st);
+        hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, V), dim3(CTPB), dl, h.stream, 0, cd, vcone, P,
+                           h.dpi_len, ws, st);
+      hipLaunchKernelGGL(conic_split_pass_kernel, dim3(RB, B), dim3(CTPB), 0, h.stream, 0, h.cA, h.cb, ws, st,
+                         nq);
+      hipLaunchKernelGGL(conic_split_upd_u_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st);
       passT();
-      hipLaunchKernelGGL(conic_split_upd_v_kernel, dim3(B), dim3(VT), 0, h.stream, h.cb, h.cc,
-                         ws, st, N, active);
+      hipLaunchKernelGGL(conic_split_upd_v_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st, N,
+                         active);
     }
     ccheck();
     DOPT_CHECK_HIP(hipMemcpyAsync(&left, active, sizeof(int32_t), hipMemcpyDeviceToHost, h.stream));
     DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
   }
-  hipLaunchKernelGGL(conic_split_out_kernel, dim3(B), dim3(CTPB), 0, h.stream, ws, st, out,
-                     h.cinfo.as<int32_t>());
+  hipLaunchKernelGGL(conic_split_out_kernel, dim3(V), dim3(CTPB), 0, h.stream, ws, st, out0, info0, out1, info1);
   ccheck();
 }
 
@@ -1585,7 +1614,7 @@ static void conic_lsqr(Handle& h, double tol, double* out) {
   h.cinfo.ensure((size_t)4 * std::max(B, 1) * sizeof(int32_t));
   double* rhs = h.cwork.as<double>() + (size_t)B * wl;
   if (use_split(h)) {
-    conic_lsqr_split(h, tol, rhs, out);
+    conic_lsqr_split(h, 1, tol, tol, rhs, out, h.cinfo.as<int32_t>(), nullptr, nullptr);
     return;
   }
   PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
@@ -1641,25 +1670,18 @@ void conic_reverse(Handle& h, const double* dx, double* out_g, double* out_dA, d
 }
 
 // Forward and reverse of every problem in one call: both right-hand sides,
-// then the co-iterated LSQR (conic_lsqr2_kernel: one sweep over A per M / Mᵀ
+// then the co-iterated LSQR (conic_lsqr2_kernel, or the split path with two
+// sequences per problem for m > 2·PAIR_ROWS: one sweep over A per M / Mᵀ
 // apply for both directions), then both output kernels.  Results are
 // bit-identical to conic_forward + conic_reverse.  Info: the reverse run's
 // [istop | iterations] where a single call leaves them (dopt_get_info), the
-// forward run's behind it (dopt_conic_lsqr_stats).  The split path (m >
-// 2·PAIR_ROWS) runs the two directions one after the other.
+// forward run's behind it (dopt_conic_lsqr_stats).
 void conic_forward_reverse(Handle& h, const double* dA, const double* db, const double* dc, const double* dx,
                            double* out_f, double* out_dx, double* out_g, double* out_dA, double* out_db,
                            double* out_dc) {
   if (!h.cfactored) conic_factor(h);
   const int B = (int)h.batch, m = h.m, n = h.n;
   h.cinfo.ensure((size_t)4 * std::max(B, 1) * sizeof(int32_t));
-  if (use_split(h)) {
-    conic_forward(h, dA, db, dc, out_f, out_dx);
-    DOPT_CHECK_HIP(hipMemcpyAsync(h.cinfo.as<int32_t>() + 2 * B, h.cinfo.p, 2 * B * sizeof(int32_t),
-                                  hipMemcpyDeviceToDevice, h.stream));
-    conic_reverse(h, dx, out_g, out_dA, out_db, out_dc);
-    return;
-  }
   const int nc = (int)h.cones.size() / 2;
   const size_t N = (size_t)n + m + 1;
   const size_t wl = 5 * N + 3 * (size_t)m + n;
@@ -1673,7 +1695,10 @@ void conic_forward_reverse(Handle& h, const double* dA, const double* db, const 
     hipLaunchKernelGGL(conic_rev_rhs_kernel, dim3(B), dim3(CTPB), 0, h.stream, dx, h.cx, m, n, rhs_r);
     ccheck();
   }
-  {
+  if (use_split(h)) {
+    int32_t* info = h.cinfo.as<int32_t>();
+    conic_lsqr_split(h, 2, 0.0, 1e-4, rhs_f, out_f, info + 2 * B, out_g, info);
+  } else {
     PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
     int32_t* info = h.cinfo.as<int32_t>();
     hipLaunchKernelGGL(conic_lsqr2_kernel, dim3(B), dim3(CTPB), dpi_lds_bytes(h.cones), h.stream,

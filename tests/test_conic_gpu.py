@@ -403,3 +403,13 @@ def test_forward_reverse_coiterated_bitwise(ConicBatch, shape):
     np.testing.assert_array_equal(st["fwd_iterations"], it_f)
     np.testing.assert_array_equal(st["iterations"], it_r)
     e.close()
+
+
+@pytest.mark.parametrize("shape", [
+    ("split: mixed cones", 3, 30, [(0, 3), (1, 10), (3, 6), (2, 4), (4, 6)], 11),
+    ("split: PSD blocks", 2, 25, [(4, 10), (4, 15), (1, 5)], 13),
+], ids=lambda s: s[0])
+def test_forward_reverse_coiterated_split_bitwise(SplitConicBatch, shape):
+    """The split path (row-block × problem grids) co-iterated: 2B sequences,
+    one pass over each row block of A for both live sequences."""
+    test_forward_reverse_coiterated_bitwise(SplitConicBatch, shape)
