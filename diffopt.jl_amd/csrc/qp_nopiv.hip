@@ -31,11 +31,14 @@
 //                    A22 −= L21·U12, rank 64 on MFMA, the U12 tile staged in
 //                    LDS, XCD-aware tile order (one problem's tiles share an L2)
 //
-// Two designs measured slower on config 2 (B = 1024, Np = 320) and dropped:
+// Designs measured slower on config 2 (B = 1024, Np = 320) and dropped:
 //  * TRSM folded into the update tiles (each tile recomputing its L21 / U12
 //    pieces from the inverse): 533 µs at c0 = 0 against 171 + 309 µs — f64
 //    MFMA is the scarcer resource (measured ≈44 ns per 16x16x4 per SIMD, i.e.
 //    ≈47 TF/s, tools/probe/mfma_rate.hip), and the fold doubles the MFMAs;
+//  * the TRSM folded into the diagonal workgroup (inverse kept in LDS): LU
+//    1.38 → 2.00 ms — one workgroup per problem serialises the strips and
+//    the diagonal kernel spills (189); single-strip steps only: 1.57 ms;
 //  * the next diagonal block folded into tile (0, 0) of the update: with 4
 //    workgroups per CU (LDS) a ~100 µs latency-bound diagonal workgroup parks
 //    a quarter of a CU while the short tiles queue behind it (1.4 ms).
@@ -567,11 +570,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
   const int s0 = c0 + NB64 + 64 * st;          // first row (side 0) / column (side 1) of the strip
   const int sw = min(64, R2 - 64 * st);        // 32 or 64
   if (side == 0) {
-    // stage U11⁻¹ (upper triangle of the packed inverse, zero below)
-    for (int e = t; e < NB64 * NB64; e += 256) {
-      const int k = e >> 6, c = e & 63;
-      const double v = Bg[e];
-      X[k * TLD + c] = k <= c ? v : 0.0;
+    // stage U11⁻¹ (upper triangle of the packed inverse, zero below); all 16
+    // loads of a thread in flight before the first LDS store
+    {
+      double v[NB64 * NB64 / 256];
+#pragma unroll
+      for (int q = 0; q < NB64 * NB64 / 256; ++q) v[q] = Bg[t + 256 * q];
+#pragma unroll
+      for (int q = 0; q < NB64 * NB64 / 256; ++q) {
+        const int e = t + 256 * q, k = e >> 6, c = e & 63;
+        X[k * TLD + c] = k <= c ? v[q] : 0.0;
+      }
     }
     const int row = s0 + 16 * wv;
     const bool wact = 16 * wv < sw;              // wave-uniform
