@@ -98,7 +98,6 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
       if (e[0] == '0' || e[0] == '1') h->conic_split = e[0] - '0';
     }
     if (const char* e = getenv("DOPT_LU")) h->lu_mode = atoi(e) != 0;
-    if (const char* e = getenv("DOPT_LU_PAIR")) h->lu_pair = atoi(e) != 0;
     if (kind == DOPT_KIND_QP) {
       // largest supported system: the generic solve stages an nmax vector in
       // LDS (64 KB), the blocked path is limited to BLOCKED_MAX unknowns

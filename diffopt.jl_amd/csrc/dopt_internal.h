@@ -119,7 +119,6 @@ struct Handle {
   // partial-pivoting re-factorisation of rejected problems (default);
   // 0 = partial pivoting for every problem (env DOPT_LU=0)
   int32_t lu_mode = 1;
-  int32_t lu_pair = 1;             // no-pivot LU: paired rank-128 trailing updates (env DOPT_LU_PAIR=0: rank 64)
   int32_t blocked_npmax = 0;       // largest padded blocked system of the current factorisation
   bool has_generic = true;         // some problem exceeds BLOCKED_MAX
   bool has_lsqr = true;            // some problem takes the LSQR branch

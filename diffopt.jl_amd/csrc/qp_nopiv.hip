@@ -120,7 +120,6 @@ __device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double*
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int c = 0; c < 4; ++c) a[r][c] = S[(o + 4 * ti + r) * SLD + o + 4 * tj + c];
-  int bad = 0;
 #pragma unroll 1
   for (int j4 = 0; j4 < 8; ++j4) {
 #pragma unroll
@@ -135,28 +134,31 @@ __device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double*
         for (int r = 0; r < 4; ++r) colb[4 * ti + r] = a[r][jj];
       }
       wave_sync();
+      // every read of the step issued before the first use
+      double cv[4], uv[4];
       const double piv = rowb[j];
-      const double rcp = 1.0 / piv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cv[r] = colb[4 * ti + r];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) uv[c] = rowb[4 * tj + c];
+      // 1/piv: v_rcp_f64 + two Newton steps (a zero / non-finite pivot turns
+      // every later multiplier into inf / NaN, which the final check rejects)
+      double rcp = __builtin_amdgcn_rcp(piv);
+      rcp = fma(fma(-piv, rcp, 1.0), rcp, rcp);
+      rcp = fma(fma(-piv, rcp, 1.0), rcp, rcp);
       double l[4], lm[4], um[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        l[r] = colb[4 * ti + r] * rcp;
+        l[r] = cv[r] * rcp;
         lm[r] = (4 * ti + r > j) ? l[r] : 0.0;
       }
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const double u = rowb[4 * tj + c];
-        um[c] = (4 * tj + c > j) ? u : 0.0;
-      }
+      for (int c = 0; c < 4; ++c) um[c] = (4 * tj + c > j) ? uv[c] : 0.0;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int c = 0; c < 4; ++c) a[r][c] = fma(-lm[r], um[c], a[r][c]);
-      int over = !(fabs(piv) > 0.0) || !(fabs(piv) <= 1.7976931348623157e308);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) over |= (4 * ti + r > j) & !(fabs(l[r]) <= NOPIV_LMAX);
       if (tj == j4) {
-        bad |= over;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (4 * ti + r > j) S[(o + 4 * ti + r) * SLD + o + j] = l[r];
@@ -164,11 +166,20 @@ __device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double*
       wave_sync();   // this step's reads of rowb / colb precede the next publish
     }
   }
+  // U from the registers; the threshold test once, on the final values (a
+  // pivot and a multiplier never change after their step): every pivot
+  // non-zero and finite, every |l| ≤ NOPIV_LMAX (NaN fails)
+  int bad = 0;
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-      if (4 * ti + r <= 4 * tj + c) S[(o + 4 * ti + r) * SLD + o + 4 * tj + c] = a[r][c];
+    for (int c = 0; c < 4; ++c) {
+      const int gi = 4 * ti + r, gj = 4 * tj + c;
+      double* p = &S[(o + gi) * SLD + o + gj];
+      if (gi <= gj) *p = a[r][c];
+      if (gi == gj) bad |= !(fabs(a[r][c]) > 0.0) || !(fabs(a[r][c]) <= 1.7976931348623157e308);
+      if (gi > gj) bad |= !(fabs(*p) <= NOPIV_LMAX);
+    }
   return __any(bad) ? 1 : 0;
 }
 
@@ -863,7 +874,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 
 // No-pivot blocked LU of every ROUTE_BLOCKED problem: per 64-column block a
 // diagonal launch (B workgroups) and a TRSM launch; the trailing updates go
-// in pairs of steps (h.lu_pair, default): step c0 updates only its cross
+// in pairs of steps (rank 64 per step measured slower): step c0 updates only its cross
 // band, step c0+64's diagonal block and TRSM follow, one rank-128 pass
 // updates the rest — a third less trailing-matrix traffic than one rank-64
 // pass per step.  Sized by h.blocked_npmax (the read-back of the metadata after the
@@ -906,7 +917,7 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
     if (R2 <= 0) break;
     const int nt = (R2 + 63) / 64;
     trsm(c0, nt);
-    if (!h.lu_pair || R2 <= NB64) {   // one rank-64 step
+    if (R2 <= NB64) {   // the last trailing block: one rank-64 step
       update(c0, nt, 0);
       c0 += NB64;
       continue;
