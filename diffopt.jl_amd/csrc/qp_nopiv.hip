@@ -113,26 +113,29 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double* colb) {
+__device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double* colb, double* trash,
+                                          double* __restrict__ Kd, int ld) {
   const int lane = threadIdx.x & 63, ti = lane >> 3, tj = lane & 7;
   double a[4][4];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int c = 0; c < 4; ++c) a[r][c] = S[(o + 4 * ti + r) * SLD + o + 4 * tj + c];
+  double* mine = trash + 4 * lane;   // 32-byte aligned per lane
 #pragma unroll 1
   for (int j4 = 0; j4 < 8; ++j4) {
+    // branch-free publishing: the owners of row / column j write the shared
+    // buffers, every other lane its own trash slot
+    double* rdst = ti == j4 ? rowb + 4 * tj : mine;
+    double* cdst = tj == j4 ? colb + 4 * ti : mine;
+    const bool ocol = tj == j4;
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int j = 4 * j4 + jj;
-      if (ti == j4) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) rowb[4 * tj + c] = a[jj][c];
-      }
-      if (tj == j4) {
+      for (int c = 0; c < 4; ++c) rdst[c] = a[jj][c];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) colb[4 * ti + r] = a[r][jj];
-      }
+      for (int r = 0; r < 4; ++r) cdst[r] = a[r][jj];
       wave_sync();
       // every read of the step issued before the first use
       double cv[4], uv[4];
@@ -146,11 +149,14 @@ __device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double*
       double rcp = __builtin_amdgcn_rcp(piv);
       rcp = fma(fma(-piv, rcp, 1.0), rcp, rcp);
       rcp = fma(fma(-piv, rcp, 1.0), rcp, rcp);
-      double l[4], lm[4], um[4];
+      double lm[4], um[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        l[r] = cv[r] * rcp;
-        lm[r] = (4 * ti + r > j) ? l[r] : 0.0;
+        const double l = cv[r] * rcp;
+        lm[r] = (4 * ti + r > j) ? l : 0.0;
+        // the column's owner keeps its multipliers in place (column j is
+        // never updated again: um = 0 there from now on)
+        if (ocol && 4 * ti + r > j) a[r][jj] = l;
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c) um[c] = (4 * tj + c > j) ? uv[c] : 0.0;
@@ -158,16 +164,11 @@ __device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double*
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int c = 0; c < 4; ++c) a[r][c] = fma(-lm[r], um[c], a[r][c]);
-      if (tj == j4) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (4 * ti + r > j) S[(o + 4 * ti + r) * SLD + o + j] = l[r];
-      }
       wave_sync();   // this step's reads of rowb / colb precede the next publish
     }
   }
-  // U from the registers; the threshold test once, on the final values (a
-  // pivot and a multiplier never change after their step): every pivot
+  // L and U from the registers (to S and to K at Kd); the threshold test once, on the final values
+  // (a pivot and a multiplier never change after their step): every pivot
   // non-zero and finite, every |l| ≤ NOPIV_LMAX (NaN fails)
   int bad = 0;
 #pragma unroll
@@ -175,52 +176,151 @@ __device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double*
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int gi = 4 * ti + r, gj = 4 * tj + c;
-      double* p = &S[(o + gi) * SLD + o + gj];
-      if (gi <= gj) *p = a[r][c];
+      S[(o + gi) * SLD + o + gj] = a[r][c];
+      Kd[(size_t)gi * ld + gj] = a[r][c];
       if (gi == gj) bad |= !(fabs(a[r][c]) > 0.0) || !(fabs(a[r][c]) <= 1.7976931348623157e308);
-      if (gi > gj) bad |= !(fabs(*p) <= NOPIV_LMAX);
+      if (gi > gj) bad |= !(fabs(a[r][c]) <= NOPIV_LMAX);
     }
   return __any(bad) ? 1 : 0;
 }
 
-// x = column `c` of the inverse of the unit-lower 32×32 block at (o, o) of S
-// (right-looking forward substitution, one column per lane)
-__device__ __forceinline__ void lower_inv_col(const double* S, int o, int c, double* x) {
+// In-place inverses of the unit-lower L and the upper U of the 32×32 LU block
+// at (o, o) of S — packed as the factors are: L⁻¹ strictly below the diagonal,
+// U⁻¹ on and above it — by 16-blocks:
+//   the four 16×16 diagonal inverses by substitution, a column per lane (lane
+//   group g = lane >> 4: g & 1 selects the 16-block, groups 2–3 repeat 0–1);
+//   the off-diagonal blocks on MFMA, the first product's output registers
+//   being the second's B operand (rows g + 4s of a 16x16x4 result are the
+//   k-rows 4s + g of step s):
+//     (L⁻¹)21 = −L22⁻¹ (L21 L11⁻¹),   (U⁻¹)12 = −U11⁻¹ (U12 U22⁻¹).
+// Wave `wl` inverts L, wave `wu` U (disjoint parts of S, each wave reads its
+// part before writing it); other waves return at once.  The caller
+// synchronises before anyone else reads the block.
+__device__ __forceinline__ void tri_inv32(double* S, int o, int wv, int wl, int wu) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+  const int bo = o + 16 * (g & 1), c = l16;
+  if (wv == wl) {
+    // column i of L (rows > i) loaded one iteration ahead; the scheduling
+    // barrier keeps the compiler from hoisting all 120 loads (register spills)
+    double x[16], cur[16], nxt[16];
 #pragma unroll
-  for (int jj = 0; jj < 32; ++jj) x[jj] = (jj == c) ? 1.0 : 0.0;
+    for (int jj = 0; jj < 16; ++jj) x[jj] = (jj == c) ? 1.0 : 0.0;
 #pragma unroll
-  for (int i = 0; i < 31; ++i) {
+    for (int jj = 1; jj < 16; ++jj) cur[jj] = S[(bo + jj) * SLD + bo];
 #pragma unroll
-    for (int jj = i + 1; jj < 32; ++jj) x[jj] = fma(-S[(o + jj) * SLD + o + i], x[i], x[jj]);
+    for (int i = 0; i < 15; ++i) {
+#pragma unroll
+      for (int jj = i + 2; jj < 16; ++jj) nxt[jj] = S[(bo + jj) * SLD + bo + i + 1];
+#pragma unroll
+      for (int jj = i + 1; jj < 16; ++jj) {
+        x[jj] = fma(-cur[jj], x[i], x[jj]);
+        asm volatile("" : "+v"(x[jj]));   // computed here, not after every load
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int jj = i + 2; jj < 16; ++jj) cur[jj] = nxt[jj];
+    }
+    // groups 2–3 store the same values to the same addresses as 0–1 (an
+    // unconditional store keeps the compiler from sinking the substitution)
+#pragma unroll
+    for (int jj = 1; jj < 16; ++jj)
+      if (jj > c) S[(bo + jj) * SLD + bo + c] = x[jj];
+    d4n tm = {0, 0, 0, 0}, xm = {0, 0, 0, 0};
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {   // T = L21 · L11⁻¹
+      const int k = 4 * st + g;
+      const double av = S[(o + 16 + l16) * SLD + o + k];
+      const double bv = k == l16 ? 1.0 : (k > l16 ? S[(o + k) * SLD + o + l16] : 0.0);
+      tm = nmfma(av, bv, tm);
+    }
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {   // X21 = L22⁻¹ · T
+      const int k = 4 * st + g;
+      const double av = l16 == k ? 1.0 : (l16 > k ? S[(o + 16 + l16) * SLD + o + 16 + k] : 0.0);
+      xm = nmfma(av, tm[st], xm);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) S[(o + 16 + g + 4 * rr) * SLD + o + l16] = -xm[rr];
+  } else if (wv == wu) {
+    // row r = c of U⁻¹ (y U = e_r, ascending: y_i /= U_ii, then
+    // y_j −= y_i U_ij for j > i), row i of U loaded one iteration ahead
+    double y[16], cur[16], nxt[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) y[jj] = (jj == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) cur[j] = S[bo * SLD + bo + j];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (i < 15) {
+#pragma unroll
+        for (int j = i + 1; j < 16; ++j) nxt[j] = S[(bo + i + 1) * SLD + bo + j];
+      }
+      const double d = cur[i];
+      double r = __builtin_amdgcn_rcp(d);
+      r = fma(fma(-d, r, 1.0), r, r);
+      y[i] *= fma(fma(-d, r, 1.0), r, r);
+#pragma unroll
+      for (int j = i + 1; j < 16; ++j) {
+        y[j] = fma(-y[i], cur[j], y[j]);
+        asm volatile("" : "+v"(y[j]));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (i < 15) {
+#pragma unroll
+        for (int j = i + 1; j < 16; ++j) cur[j] = nxt[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j >= c) S[(bo + c) * SLD + bo + j] = y[j];
+    d4n tm = {0, 0, 0, 0}, ym = {0, 0, 0, 0};
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {   // T = U12 · U22⁻¹
+      const int k = 4 * st + g;
+      const double av = S[(o + l16) * SLD + o + 16 + k];
+      const double bv = k <= l16 ? S[(o + 16 + k) * SLD + o + 16 + l16] : 0.0;
+      tm = nmfma(av, bv, tm);
+    }
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {   // Y12 = U11⁻¹ · T
+      const int k = 4 * st + g;
+      const double av = l16 <= k ? S[(o + l16) * SLD + o + k] : 0.0;
+      ym = nmfma(av, tm[st], ym);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) S[(o + g + 4 * rr) * SLD + o + 16 + l16] = -ym[rr];
   }
 }
 
-// x = column `c` of the inverse of the upper 32×32 block at (o, o) of S
-__device__ __forceinline__ void upper_inv_col(const double* S, int o, int c, double* x) {
-#pragma unroll
-  for (int jj = 0; jj < 32; ++jj) x[jj] = (jj == c) ? 1.0 : 0.0;
-#pragma unroll
-  for (int jj = 31; jj >= 0; --jj) {
-    x[jj] = x[jj] / S[(o + jj) * SLD + o + jj];
-#pragma unroll
-    for (int i = 0; i < jj; ++i) x[i] = fma(-S[(o + i) * SLD + o + jj], x[jj], x[i]);
+// the solves' dinv block (L⁻¹ | U⁻¹, each 32×32 row-major with its unit
+// diagonal / zeros) from the packed inverse at (o, o) of S; whole workgroup
+__device__ __forceinline__ void dinv32(const double* S, int o, double* __restrict__ D) {
+  for (int e = threadIdx.x; e < 32 * 32; e += PNT) {
+    const int i = e >> 5, j = e & 31;
+    const double v = S[(o + i) * SLD + o + j];
+    D[e] = i > j ? v : (i == j ? 1.0 : 0.0);
+    D[32 * 32 + e] = i <= j ? v : 0.0;
   }
 }
 
 // one 16×16 tile of a 32×32×32 product on MFMA: acc = A[tr.., :] · B[:, tc..]
 // with A(i, k) / B(k, j) given by functors (lane: A row tr+l16, B column tc+l16)
+// (k-steps past `ns` skipped: ns wave-uniform, 4 or 8)
 template <class FA, class FB>
-__device__ __forceinline__ d4n tile32(int tr, int tc, FA A, FB Bm) {
+__device__ __forceinline__ d4n tile32(int tr, int tc, FA A, FB Bm, int ns = 8) {
   const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
   double av[8], bv[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {   // every operand load issued before the first MFMA
-    av[s] = A(tr + l16, 4 * s + g);
-    bv[s] = Bm(4 * s + g, tc + l16);
+    if (s < ns) {
+      av[s] = A(tr + l16, 4 * s + g);
+      bv[s] = Bm(4 * s + g, tc + l16);
+    }
   }
   d4n acc = {0, 0, 0, 0};
 #pragma unroll
-  for (int s = 0; s < 8; ++s) acc = nmfma(av[s], bv[s], acc);
+  for (int s = 0; s < 8; ++s)
+    if (s < ns) acc = nmfma(av[s], bv[s], acc);
   return acc;
 }
 
@@ -228,12 +328,13 @@ __device__ __forceinline__ d4n tile32(int tr, int tc, FA A, FB Bm) {
 // Diagonal block of step c0 (multiple of 64) of one problem: rows and columns
 // c0 .. c0+63 (the last block may be 32 wide), already in the LDS image S
 // (identity beyond Wv), factorised recursively as two 32×32 blocks a, b:
-//   A  wave 0: LU of a (wave_lu32)
-//   B  waves 0–3: L_aa⁻¹, U_aa⁻¹ (the solves' dinv), U_ab = L_aa⁻¹A_ab,
-//      L_ba = A_ba U_aa⁻¹ (+ threshold test), one column / row per lane
+//   A  wave 0: LU of a (wave_lu32, L_aa \ U_aa → S and K)
+//   B  waves 0–1: L_aa⁻¹, U_aa⁻¹ by 16-blocks (tri_inv32; the solves' dinv);
+//      all waves: U_ab = L_aa⁻¹A_ab, L_ba = A_ba U_aa⁻¹ (MFMA, + threshold test)
 //   C  A_bb −= L_ba U_ab (MFMA)
 //   D  wave 0: LU of b
-//   E  waves 0–1: L_bb⁻¹, U_bb⁻¹; waves 2–3: T_L = L_ba L_aa⁻¹, T_U = U_aa⁻¹U_ab
+//   E  waves 0–1: L_bb⁻¹, U_bb⁻¹ (tri_inv32); waves 2–3: T_L = L_ba L_aa⁻¹,
+//      T_U = U_aa⁻¹U_ab (MFMA)
 //   F  L⁻¹_ba = −L_bb⁻¹T_L, U⁻¹_ab = −T_U U_bb⁻¹ (MFMA)
 // Writes L11 / U11 to K, perm = identity, the 32×32 diagonal-block inverses to
 // dinv and, when a trailing step follows, the packed 64×64 inverse (L11⁻¹
@@ -247,10 +348,12 @@ struct DiagLds {
   double* colb;   // 32
   int* sbad;
   double* vec;    // 128: the right-hand-side blocks of the fused forward sweeps
+  double* trash;  // 256: the non-owners' publishing slots of wave_lu32
   // all inside one 64 × ULD buffer (ULD below), past the 64 × SLD image
   __device__ explicit DiagLds(double* buf)
       : S(buf), rowb(buf + NB64 * SLD), colb(buf + NB64 * SLD + 32),
-        sbad(reinterpret_cast<int*>(buf + NB64 * SLD + 64)), vec(buf + NB64 * SLD + 72) {}
+        sbad(reinterpret_cast<int*>(buf + NB64 * SLD + 64)), vec(buf + NB64 * SLD + 72),
+        trash(buf + NB64 * SLD + 200) {}
 };
 
 // Fused forward sweeps (the batched forward+reverse call): with the packed
@@ -296,12 +399,6 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
   const bool trsm = Np - c0 > NB64;    // a trailing step follows
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int g = lane >> 4, l16 = lane & 15;
-  auto to_K = [&](int r0, int cc0) {   // 32×32 block (r0, cc0) of S → K
-    for (int e = t; e < 32 * 32; e += PNT) {
-      const int i = r0 + (e >> 5), j = cc0 + (e & 31);
-      Kb[(size_t)(c0 + i) * ld + c0 + j] = S[i * SLD + j];
-    }
-  };
   NLU_MARK_INIT;
   if (t == 0) *L.sbad = 0;
   if (t < Wv) permb[c0 + t] = c0 + t;
@@ -310,7 +407,7 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
 
   // ---- A. LU of block a
   if (wv == 0) {
-    const int bad = wave_lu32(S, 0, L.rowb, L.colb);
+    const int bad = wave_lu32(S, 0, L.rowb, L.colb, L.trash, Kb + (size_t)c0 * ld + c0, ld);
     if (lane == 0 && bad) *L.sbad = 1;
   }
   __syncthreads();
@@ -319,57 +416,40 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
     return;
   }
   NLU_MARK(1);
-  to_K(0, 0);
   if (NLU_STOP <= 2) return;
 
-  // ---- B. inverses of block a, U_ab, L_ba (lanes 0–31 of each wave)
+  // ---- B. inverses of block a by 16-blocks (waves 0–1, tri_inv32), the
+  // solves' dinv of a; then U_ab = L_aa⁻¹A_ab and L_ba = A_ba U_aa⁻¹ on MFMA
+  // (one tile of each per wave; the triangles skip k-steps) + the threshold
+  // test on L_ba; U_ab, L_ba → S and K
+  tri_inv32(S, 0, wv, 0, 1);
+  __syncthreads();
+  dinv32(S, 0, Db);
+  if (Wv < NB64) {   // a 32-wide last block: done (no trailing step follows)
+    NLU_MARK(2);
+    if (w0b) fwd_block(L, w0b, w1b, c0, N, Wv);   // S: L_aa⁻¹ \ U_aa⁻¹, identity frame
+    return;
+  }
   {
-    const int c = lane;
-    double x[32];
+    const int tr = (wv >> 1) * 16, tc = (wv & 1) * 16;
+    const int i = tr + l16, j = tc + l16;
+    // U_ab tile: k ≤ tr + 15 (L_aa⁻¹ is lower); L_ba tile: k ≤ tc + 15
+    const d4n au = tile32(tr, tc, [&](int, int k) { return k == i ? 1.0 : (k < i ? S[i * SLD + k] : 0.0); },
+                          [&](int k, int) { return S[k * SLD + 32 + j]; }, tr ? 8 : 4);
+    const d4n al = tile32(tr, tc, [&](int, int k) { return S[(32 + i) * SLD + k]; },
+                          [&](int k, int) { return k <= j ? S[k * SLD + j] : 0.0; }, tc ? 8 : 4);
+    __syncthreads();   // every wave has read A_ab / A_ba
     int bad = 0;
-    if (lane < 32) {
-      if (wv == 0) {
-        lower_inv_col(S, 0, c, x);
-      } else if (wv == 1) {
-        upper_inv_col(S, 0, c, x);
-      } else if (wv == 2 && Wv == NB64) {   // U_ab column c = L_aa⁻¹ A_ab[:, c]
 #pragma unroll
-        for (int i = 0; i < 32; ++i) x[i] = S[i * SLD + 32 + c];
-#pragma unroll
-        for (int i = 0; i < 31; ++i) {
-#pragma unroll
-          for (int jj = i + 1; jj < 32; ++jj) x[jj] = fma(-S[jj * SLD + i], x[i], x[jj]);
-        }
-      } else if (wv == 3 && Wv == NB64) {   // L_ba row c: x U_aa = A_ba[c, :]
-#pragma unroll
-        for (int j = 0; j < 32; ++j) x[j] = S[(32 + c) * SLD + j];
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-          x[j] = x[j] / S[j * SLD + j];
-          bad |= !(fabs(x[j]) <= NOPIV_LMAX);
-#pragma unroll
-          for (int jj = j + 1; jj < 32; ++jj) x[jj] = fma(-x[j], S[j * SLD + jj], x[jj]);
-        }
-      }
+    for (int rr = 0; rr < 4; ++rr) {
+      const int i = tr + g + 4 * rr, j = tc + l16;
+      S[i * SLD + 32 + j] = au[rr];
+      Kb[(size_t)(c0 + i) * ld + c0 + 32 + j] = au[rr];
+      S[(32 + i) * SLD + j] = al[rr];
+      Kb[(size_t)(c0 + 32 + i) * ld + c0 + j] = al[rr];
+      bad |= !(fabs(al[rr]) <= NOPIV_LMAX);
     }
-    if (bad) *L.sbad = 1;
-    __syncthreads();   // every lane has read the factors of block a
-    if (lane < 32) {
-      if (wv < 2) {
-        double* D = Db + (wv == 0 ? 0 : 32 * 32);
-#pragma unroll
-        for (int jj = 0; jj < 32; ++jj) {
-          D[jj * 32 + c] = x[jj];
-          if (wv == 0 ? jj > c : jj <= c) S[jj * SLD + c] = x[jj];
-        }
-      } else if (wv == 2 && Wv == NB64) {
-#pragma unroll
-        for (int i = 0; i < 32; ++i) S[i * SLD + 32 + c] = x[i];
-      } else if (wv == 3 && Wv == NB64) {
-#pragma unroll
-        for (int j = 0; j < 32; ++j) S[(32 + c) * SLD + j] = x[j];
-      }
-    }
+    if (__any(bad) && lane == 0) *L.sbad = 1;   // every writer stores the same value
   }
   __syncthreads();
   if (*L.sbad) {
@@ -377,20 +457,14 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
     return;
   }
   NLU_MARK(2);
-  if (Wv < NB64) {   // a 32-wide last block: done (no trailing step follows)
-    if (w0b) fwd_block(L, w0b, w1b, c0, N, Wv);   // S: L_aa⁻¹ \ U_aa⁻¹, identity frame
-    return;
-  }
   if (NLU_STOP <= 3) return;
 
-  // ---- C. A_bb −= L_ba U_ab (one 16×16 tile per wave); U_ab, L_ba → K
+  // ---- C. A_bb −= L_ba U_ab (one 16×16 tile per wave; each wave updates
+  // only its own tile, the others read L_ba / U_ab)
   {
     const int tr = (wv >> 1) * 16, tc = (wv & 1) * 16;
     d4n acc = tile32(tr, tc, [&](int i, int k) { return S[(32 + i) * SLD + k]; },
                      [&](int k, int j) { return S[k * SLD + 32 + j]; });
-    to_K(0, 32);
-    to_K(32, 0);
-    __syncthreads();   // every wave has read L_ba / U_ab; A_bb not read before the update
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       double* p = &S[(32 + tr + g + 4 * rr) * SLD + 32 + tc + l16];
@@ -402,7 +476,7 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
 
   // ---- D. LU of block b
   if (wv == 0) {
-    const int bad = wave_lu32(S, 32, L.rowb, L.colb);
+    const int bad = wave_lu32(S, 32, L.rowb, L.colb, L.trash, Kb + (size_t)(c0 + 32) * ld + c0 + 32, ld);
     if (lane == 0 && bad) *L.sbad = 1;
   }
   __syncthreads();
@@ -411,59 +485,43 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
     return;
   }
   NLU_MARK(4);
-  to_K(32, 32);
   if (!trsm && !w0b) {   // last block, nothing to sweep: only the solves' dinv of block b
-    if (wv < 2 && lane < 32) {
-      double x[32];
-      if (wv == 0) lower_inv_col(S, 32, lane, x);
-      else upper_inv_col(S, 32, lane, x);
-      double* D = Db + DBLK + (wv == 0 ? 0 : 32 * 32);
-#pragma unroll
-      for (int jj = 0; jj < 32; ++jj) D[jj * 32 + lane] = x[jj];
-    }
+    tri_inv32(S, 32, wv, 0, 1);
+    __syncthreads();
+    dinv32(S, 32, Db + DBLK);
     return;
   }
   if (NLU_STOP <= 4) return;
 
-  // ---- E. inverses of block b (waves 0–1); T_L, T_U (waves 2–3), which
-  // replace L_ba / U_ab in S (both already in K)
-  {
-    double x[32];
+  // ---- E. inverses of block b (waves 0–1, tri_inv32); T_L = L_ba L_aa⁻¹
+  // (wave 2), T_U = U_aa⁻¹U_ab (wave 3), each in place of its operand L_ba /
+  // U_ab (both already in K; every tile read before the first write)
+  if (wv < 2) {
+    tri_inv32(S, 32, wv, 0, 1);
+  } else {
     d4n acc[4];
-    if (wv < 2 && lane < 32) {
-      if (wv == 0) lower_inv_col(S, 32, lane, x);
-      else upper_inv_col(S, 32, lane, x);
-    } else if (wv == 2) {   // T_L = L_ba · L_aa⁻¹
+    if (wv == 2) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         acc[q] = tile32((q >> 1) * 16, (q & 1) * 16, [&](int i, int k) { return S[(32 + i) * SLD + k]; },
                         [&](int k, int j) { return k == j ? 1.0 : (k > j ? S[k * SLD + j] : 0.0); });
-    } else if (wv == 3) {   // T_U = U_aa⁻¹ · U_ab
+    } else {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         acc[q] = tile32((q >> 1) * 16, (q & 1) * 16, [&](int i, int k) { return k >= i ? S[i * SLD + k] : 0.0; },
                         [&](int k, int j) { return S[k * SLD + 32 + j]; });
     }
-    __syncthreads();   // the factors of block b, L_ba and U_ab have been read
-    if (wv < 2 && lane < 32) {
-      double* D = Db + DBLK + (wv == 0 ? 0 : 32 * 32);
 #pragma unroll
-      for (int jj = 0; jj < 32; ++jj) {
-        D[jj * 32 + lane] = x[jj];
-        if (wv == 0 ? jj > lane : jj <= lane) S[(32 + jj) * SLD + 32 + lane] = x[jj];
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int i = (q >> 1) * 16 + g + 4 * rr, j = (q & 1) * 16 + l16;
+        if (wv == 2) S[(32 + i) * SLD + j] = acc[q][rr];
+        else S[i * SLD + 32 + j] = acc[q][rr];
       }
-    } else if (wv >= 2) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int i = (q >> 1) * 16 + g + 4 * rr, j = (q & 1) * 16 + l16;
-          if (wv == 2) S[(32 + i) * SLD + j] = acc[q][rr];
-          else S[i * SLD + 32 + j] = acc[q][rr];
-        }
-    }
   }
   __syncthreads();
+  dinv32(S, 32, Db + DBLK);   // F does not write block b
   NLU_MARK(5);
 
   // ---- F. off-diagonal inverse blocks (two 16×16 tiles per wave), in place
@@ -508,7 +566,8 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
 // kernel share one buffer
 constexpr int ULD = 64 + 16;   // LDS row stride (doubles) of the staged U12 tile (update)
 constexpr int STEP_LDS = NB64 * ULD;   // 40 KB: 4 workgroups per CU
-static_assert(NB64 * SLD + 64 + 1 <= STEP_LDS, "diagonal image + rowb/colb/sbad must fit 40 KB");
+static_assert(NB64 * SLD + 200 + 256 <= STEP_LDS, "diagonal image + rowb/colb/sbad/vec/trash must fit 40 KB");
+static_assert((NB64 * SLD + 200) % 2 == 0, "trash slots 16-byte aligned");
 
 // Diagonal block of step c0 of every problem: one 256-thread workgroup per
 // problem, 40 KB of LDS: 4 per CU, a 1024-problem batch runs in one round.
