@@ -79,7 +79,8 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
                 int32_t p, int32_t kind) {
   if (!out) return -1;
   *out = nullptr;
-  if (batch < 0 || n < 0 || m < 0 || p < 0 || (kind != DOPT_KIND_QP && kind != DOPT_KIND_CONIC))
+  if (batch < 0 || n < 0 || m < 0 || p < 0 ||
+      (kind != DOPT_KIND_QP && kind != DOPT_KIND_CONIC && kind != DOPT_KIND_NLP))
     return -1;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -4;
@@ -131,8 +132,10 @@ int dopt_destroy(dopt_handle* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   DevBuf* bufs[] = {&h->dinv, &h->plist, &h->lsqr_ws, &h->binv, &h->fwdw, &h->K, &h->ipiv, &h->s, &h->kidx, &h->meta, &h->rhs,
-                    &h->x, &h->cone_dev, &h->vp, &h->dpi, &h->cwork, &h->cinfo, &h->csplit};
+                    &h->x, &h->cone_dev, &h->vp, &h->dpi, &h->cwork, &h->cinfo, &h->csplit, &h->krhs, &h->kx,
+                    &h->kfull, &h->nlp_map, &h->nlp_shift, &h->nlp_scale};
   for (auto* b : bufs) b->release();
+  for (auto& b : h->own_nin) b.release();
   for (auto& b : h->own_in) b.release();
   for (auto& b : h->csc_in) b.release();
   for (auto& b : h->csc_in_val) b.release();
@@ -423,6 +426,206 @@ int dopt_qp_forward_reverse(dopt_handle* h, const double* dl_dz, const double* d
     const int rc = first_info(*h);
     h->last_time = tm.s();
     return rc;
+  });
+}
+
+// ---- NonLinearProgram back-end ---------------------------------------------
+
+int dopt_nlp_set_structure(dopt_handle* h, const int32_t* con_kind, const int8_t* has_low,
+                           const int8_t* has_up, int32_t sense) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_set_structure on a non-NLP handle");
+    if (sense != 1 && sense != -1) throw Error(-1, "sense must be +1 (MIN_SENSE) or -1 (MAX_SENSE)");
+    const int n = h->n, c = h->m;
+    if (c && !con_kind) throw Error(-1, "con_kind is required when the model has constraints");
+    // index maps of _compute_solution_and_bounds (nlp_utilities.jl:181-279):
+    // slacks of the ≥ rows first, then of the ≤ rows, each in row order
+    std::vector<int32_t> slack_of_row(c, -1), geq, leq;
+    for (int k = 0; k < c; ++k) {
+      if (con_kind[k] == 1) geq.push_back(k);
+      else if (con_kind[k] == 2) leq.push_back(k);
+      else if (con_kind[k] != 0) throw Error(-1, "con_kind entries must be 0, 1 or 2");
+    }
+    const int ng = (int)geq.size(), nl = (int)leq.size(), w = n + ng + nl;
+    std::vector<int32_t> row_of_slack(ng + nl);
+    for (int i = 0; i < ng; ++i) slack_of_row[geq[i]] = n + i, row_of_slack[i] = geq[i];
+    for (int i = 0; i < nl; ++i) slack_of_row[leq[i]] = n + ng + i, row_of_slack[ng + i] = leq[i];
+    std::vector<int32_t> low_idx, up_idx, lowpos(w, -1), uppos(w, -1);
+    for (int j = 0; j < n; ++j)
+      if (has_low && has_low[j]) low_idx.push_back(j);
+    const int nlowp = (int)low_idx.size();
+    for (int i = 0; i < ng; ++i) low_idx.push_back(n + i);
+    for (int j = 0; j < n; ++j)
+      if (has_up && has_up[j]) up_idx.push_back(j);
+    const int nupp = (int)up_idx.size();
+    for (int i = 0; i < nl; ++i) up_idx.push_back(n + ng + i);
+    for (size_t i = 0; i < low_idx.size(); ++i) lowpos[low_idx[i]] = (int32_t)i;
+    for (size_t i = 0; i < up_idx.size(); ++i) uppos[up_idx[i]] = (int32_t)i;
+    std::vector<int32_t> map;
+    for (auto* v : {&slack_of_row, &row_of_slack, &lowpos, &uppos, &low_idx, &up_idx})
+      map.insert(map.end(), v->begin(), v->end());
+    map.push_back(0);
+    h->nlp_kkt = false;
+    h->nlp_sense = sense;
+    h->nlp_num_w = w;
+    h->nlp_ng = ng;
+    h->nlp_nl = nl;
+    h->nlp_nlo = (int32_t)low_idx.size();
+    h->nlp_nup = (int32_t)up_idx.size();
+    h->nlp_nlowp = nlowp;
+    h->nlp_nupp = nupp;
+    h->nlp_ncons = c;
+    h->nlp_rows = w + c + h->nlp_nlo + h->nlp_nup;
+    dopt::nlp_configure(*h);
+    h->nlp_map.ensure(map.size() * sizeof(int32_t));
+    DOPT_CHECK_HIP(hipMemcpyAsync(h->nlp_map.p, map.data(), map.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                                  h->stream));
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    h->nstruct = true;
+    h->nset = false;
+    return 0;
+  });
+}
+
+int dopt_nlp_set(dopt_handle* h, const double* Hxx, const double* Hxp, const double* Jx,
+                 const double* Jp, const double* x, const double* cval, const double* crhs,
+                 const double* y, const double* xl, const double* xu, const double* yl,
+                 const double* yu) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_set on a non-NLP handle");
+    if (!h->nstruct || h->nlp_kkt) throw Error(-1, "dopt_nlp_set: call dopt_nlp_set_structure first");
+    const size_t B = h->batch, n = h->n, c = h->m, P = h->p;
+    if (!Hxx || !x) throw Error(-1, "Hxx and x are required");
+    if (P && !Hxp) throw Error(-1, "Hxp is required when the model has parameters");
+    if (c && (!Jx || !cval || !crhs || !y)) throw Error(-1, "Jx, cval, crhs and y are required when c > 0");
+    if (c && P && !Jp) throw Error(-1, "Jp is required when the model has constraints and parameters");
+    if (h->nlp_nlowp && (!xl || !yl)) throw Error(-1, "xl and yl are required when a variable has a lower bound");
+    if (h->nlp_nupp && (!xu || !yu)) throw Error(-1, "xu and yu are required when a variable has an upper bound");
+    const double* src[12] = {Hxx, Hxp, Jx, Jp, x, cval, crhs, y, xl, xu, yl, yu};
+    const size_t cnt[12] = {B * n * n, B * n * P, B * c * n, B * c * P, B * n, B * c, B * c, B * c,
+                            B * n, B * n, B * n, B * n};
+    for (int k = 0; k < 12; ++k) h->nin[k] = cnt[k] ? stage_in(*h, h->own_nin[k], src[k], cnt[k]) : nullptr;
+    h->nset = true;
+    h->nfactored = false;
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  });
+}
+
+int dopt_nlp_set_kkt(dopt_handle* h, int32_t rows, int32_t num_w, int32_t num_cons, const double* M) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_set_kkt on a non-NLP handle");
+    if (rows <= 0 || num_w < 0 || num_cons < 0 || num_w + num_cons > rows)
+      throw Error(-1, "dopt_nlp_set_kkt: bad sizes");
+    if (!M) throw Error(-1, "M is required");
+    h->nlp_kkt = true;
+    h->nlp_rows = rows;
+    h->nlp_num_w = num_w;
+    h->nlp_ncons = num_cons;
+    h->nlp_ng = h->nlp_nl = h->nlp_nlo = h->nlp_nup = h->nlp_nlowp = h->nlp_nupp = 0;
+    dopt::nlp_configure(*h);
+    h->nlp_map.ensure(4 * sizeof(int32_t));
+    for (auto& p : h->nin) p = nullptr;
+    h->nin[0] = stage_in(*h, h->own_nin[0], M, (size_t)h->batch * rows * rows);
+    h->nstruct = true;
+    h->nset = true;
+    h->nfactored = false;
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  });
+}
+
+int dopt_nlp_factor(dopt_handle* h) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_factor on a non-NLP handle");
+    Timer tm;
+    dopt::nlp_factor(*h);
+    h->last_time = tm.s();
+    return 0;
+  });
+}
+
+int dopt_nlp_forward(dopt_handle* h, const double* dp, double* dx, double* ddual) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_forward on a non-NLP handle");
+    if (!dx || !ddual) throw Error(-1, "dx and ddual are required");
+    if (h->p && !dp) throw Error(-1, "dp is required");
+    Timer tm;
+    const size_t B = h->batch, nd = (size_t)h->m + h->nlp_nlowp + h->nlp_nupp;
+    static const double zero = 0.0;
+    const double* d = h->p ? stage_in(*h, h->tin[0], dp, B * h->p) : &zero;
+    double* ox = out_ptr(*h, h->tout[0], dx, B * h->n);
+    double* od = out_ptr(*h, h->tout[1], ddual, B * nd);
+    dopt::nlp_forward(*h, d, ox, od);
+    copy_out(*h, dx, ox, B * h->n);
+    copy_out(*h, ddual, od, B * nd);
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    h->last_time = tm.s();
+    return 0;
+  });
+}
+
+int dopt_nlp_reverse(dopt_handle* h, const double* dx, const double* ddual, double* dp) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_reverse on a non-NLP handle");
+    if (h->p && !dp) throw Error(-1, "dp is required");
+    Timer tm;
+    const size_t B = h->batch, nd = (size_t)h->m + h->nlp_nlowp + h->nlp_nupp;
+    const double* ix = stage_in(*h, h->tin[0], dx, B * h->n);
+    const double* id = stage_in(*h, h->tin[1], ddual, B * nd);
+    double* op = out_ptr(*h, h->tout[0], dp, B * h->p);
+    dopt::nlp_reverse(*h, ix, id, op);
+    copy_out(*h, dp, op, B * h->p);
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    h->last_time = tm.s();
+    return 0;
+  });
+}
+
+int dopt_nlp_jacobian(dopt_handle* h, double* ds) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_jacobian on a non-NLP handle");
+    if (!ds) throw Error(-1, "ds is required");
+    const size_t cnt = (size_t)h->batch * h->nlp_rows * h->p;
+    double* o = out_ptr(*h, h->tout[0], ds, cnt);
+    dopt::nlp_jacobian(*h, o);
+    copy_out(*h, ds, o, cnt);
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  });
+}
+
+int dopt_nlp_kkt_solve(dopt_handle* h, int32_t k, const double* rhs, double* x) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_NLP || !h->nlp_kkt) throw Error(-1, "dopt_nlp_kkt_solve needs dopt_nlp_set_kkt");
+    if (k <= 0) throw Error(-1, "k must be positive");
+    if (!rhs || !x) throw Error(-1, "rhs and x are required");
+    const size_t cnt = (size_t)k * h->batch * h->nlp_rows;
+    const double* r = stage_in(*h, h->tin[0], rhs, cnt);
+    double* o = out_ptr(*h, h->tout[0], x, cnt);
+    dopt::nlp_kkt_solve(*h, k, r, o);
+    copy_out(*h, x, o, cnt);
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  });
+}
+
+int dopt_nlp_get_corrections(dopt_handle* h, int32_t* corr) {
+  return guarded(h, [&]() {
+    if (!corr) throw Error(-1, "corr is required");
+    if (!h->nfactored) throw Error(-1, "dopt_nlp_get_corrections: not factorised");
+    std::copy(h->nlp_corr.begin(), h->nlp_corr.end(), corr);
+    return 0;
+  });
+}
+
+int dopt_nlp_get_layout(dopt_handle* h, int32_t* layout) {
+  return guarded(h, [&]() {
+    if (!layout) throw Error(-1, "layout is required");
+    const int32_t v[7] = {h->nlp_rows, h->nlp_num_w, h->nlp_ncons, h->nlp_nlo, h->nlp_nup, h->nlp_nlowp,
+                          h->nlp_nupp};
+    std::copy(v, v + 7, layout);
+    return 0;
   });
 }
 

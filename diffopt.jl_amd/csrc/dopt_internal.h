@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -137,6 +138,22 @@ struct Handle {
   int32_t dpi_len = 0;          // doubles per problem of packed Dπ blocks
   bool cset = false, cfactored = false;
 
+  // ---- NLP (nlp.hip) ----
+  // structured mode: M / N built from the derivatives at the solution
+  // (nlp_utilities.jl:286-396); KKT mode (nlp_kkt): M given per problem
+  int32_t nlp_sense = 1;
+  int32_t nlp_rows = 0;            // size of M
+  int32_t nlp_num_w = 0, nlp_ng = 0, nlp_nl = 0, nlp_nlo = 0, nlp_nup = 0, nlp_nlowp = 0, nlp_nupp = 0;
+  int32_t nlp_ncons = 0;           // constraint rows of M (KKT mode: as given)
+  bool nlp_kkt = false;
+  DevBuf nlp_map;                  // int32 index maps (nlp.hip NLPMap)
+  const double* nin[12] = {};      // Hxx, Hxp, Jx, Jp, x, cval, crhs, y, xl, xu, yl, yu (KKT mode: nin[0] = M)
+  DevBuf own_nin[12];
+  DevBuf nlp_shift;                // per problem: inertia corrections applied (int32); −1: failed
+  DevBuf nlp_scale;                // per problem × assembly row block: max |M| (the pivot test's scale)
+  std::vector<int32_t> nlp_corr;   // host copy of nlp_shift after the factorisation
+  bool nstruct = false, nset = false, nfactored = false;
+
   // scratch for host-mode tangents / outputs
   DevBuf tin[8], tout[6];
 
@@ -226,6 +243,16 @@ void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, con
                        double* x_rev, double* x_fwd, int sel, const double* w_rev = nullptr,
                        const double* w_fwd = nullptr);
 size_t dinv_stride(int nmax);
+// re-assembly of a list of problems (plist: device indices, count)
+using ReasmFn = std::function<void(const int32_t*, int)>;
+void factor_dense(Handle& h, const ReasmFn& reasm);
+double* dense_dinv(Handle& h);
+void nlp_configure(Handle& h);
+void nlp_factor(Handle& h);
+void nlp_forward(Handle& h, const double* dp, double* dx, double* ddual);
+void nlp_reverse(Handle& h, const double* dx, const double* ddual, double* dp);
+void nlp_jacobian(Handle& h, double* ds);
+void nlp_kkt_solve(Handle& h, int k, const double* rhs, double* x);
 void conic_factor(Handle& h);
 void conic_forward(Handle& h, const double* dA, const double* db, const double* dc,
                    double* out, double* out_dx);

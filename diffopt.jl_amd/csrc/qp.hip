@@ -754,9 +754,9 @@ static void meta_sizes(Handle& h) {
   h.blocked_npmax = npmax;
 }
 
-// After the no-pivot LU: the problems it rejected, re-assembled and
+// After the no-pivot LU: the problems it rejected, re-assembled (`reasm`) and
 // factorised with partial pivoting.  Returns their count.
-static int pivot_fallback(Handle& h) {
+static int pivot_fallback(Handle& h, const ReasmFn& reasm) {
   DOPT_CHECK_HIP(hipEventSynchronize(h.meta_ev));
   std::vector<int32_t> list;
   for (int64_t b = 0; b < h.batch; ++b)
@@ -767,7 +767,7 @@ static int pivot_fallback(Handle& h) {
     DOPT_CHECK_HIP(hipMemcpyAsync(h.plist.p, list.data(), list.size() * sizeof(int32_t),
                                   hipMemcpyHostToDevice, h.stream));
     const int32_t* pl = h.plist.as<int32_t>();
-    prep_assemble(h, pl, count);
+    reasm(pl, count);
     qp_blocked_factor(h, dinv_of(h), pl, count);
     // the host copy of `list` must outlive the asynchronous upload
     DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
@@ -789,7 +789,7 @@ static void generic_lu(Handle& h) {
 // before the host waits for the rejected list: work that skips rejected
 // problems (the solves of the fused call).
 template <class F>
-static void factor_blocked(Handle& h, F&& spec, double* w0 = nullptr, double* w1 = nullptr) {
+static void factor_blocked(Handle& h, F&& spec, double* w0, double* w1, const ReasmFn& reasm) {
   if (h.lu_mode == 1) {
     {
       PhaseTimer pt(h, DOPT_PHASE_QP_LU);
@@ -804,7 +804,7 @@ static void factor_blocked(Handle& h, F&& spec, double* w0 = nullptr, double* w1
       for (int64_t b = 0; b < h.batch && !any; ++b) any = h.meta_host[b].lu == LU_REJECT;
       if (any) {
         PhaseTimer pt(h, DOPT_PHASE_QP_LU_PIVOT);
-        h.n_pivot = pivot_fallback(h);
+        h.n_pivot = pivot_fallback(h, reasm);
       }
     }
   } else {
@@ -821,6 +821,10 @@ static void factor_blocked(Handle& h, F&& spec, double* w0 = nullptr, double* w1
   }
 }
 
+static ReasmFn qp_reasm(Handle& h) {
+  return [&h](const int32_t* pl, int count) { prep_assemble(h, pl, count); };
+}
+
 void qp_factor(Handle& h) {
   if (!h.set) throw Error(-1, "dopt_qp_factor: dopt_qp_set has not been called");
   {
@@ -829,9 +833,20 @@ void qp_factor(Handle& h) {
     meta_copy(h);
   }
   meta_sizes(h);
-  factor_blocked(h, [] {});
+  factor_blocked(h, [] {}, nullptr, nullptr, qp_reasm(h));
   h.factored = true;
 }
+
+// The blocked factorisation of a batch already assembled into K / meta by a
+// caller (the NLP back-end), with `reasm` re-assembling the problems the
+// no-pivot LU rejects.  Sizes from h.blocked_npmax; blocked route only.
+void factor_dense(Handle& h, const ReasmFn& reasm) {
+  h.has_generic = false;
+  h.has_lsqr = false;
+  factor_blocked(h, [] {}, nullptr, nullptr, reasm);
+}
+
+double* dense_dinv(Handle& h) { return dinv_of(h); }
 
 // Per-direction work buffers (trans 0 = reverse, 1 = forward): reduced RHS,
 // solution, and the full-length forward RHS.
@@ -1066,7 +1081,7 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     qp_blocked_solve2(h, dinv_of(h), rhs_of(h, 0), rhs_of(h, 1), x_of(h, 0), x_of(h, 1), sel, sw0, sw1);
   };
-  factor_blocked(h, [&] { solve2(h.lu_mode == 1 ? LU_SEL_NOPIV : LU_SEL_ALL, w0, w1); }, w0, w1);
+  factor_blocked(h, [&] { solve2(h.lu_mode == 1 ? LU_SEL_NOPIV : LU_SEL_ALL, w0, w1); }, w0, w1, qp_reasm(h));
   if (h.n_pivot > 0) solve2(LU_SEL_PIVOT, nullptr, nullptr);
   finish(h, 0, out_rev);
   finish(h, 1, out_fwd);

@@ -523,6 +523,7 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
   __syncthreads();
   dinv32(S, 32, Db + DBLK);   // F does not write block b
   NLU_MARK(5);
+  if (NLU_STOP <= 5) return;
 
   // ---- F. off-diagonal inverse blocks (two 16×16 tiles per wave), in place
   // of T_L / T_U
@@ -554,6 +555,7 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
   }
   __syncthreads();
   NLU_MARK(6);
+  if (NLU_STOP <= 6) return;
   // ---- G. the packed 64×64 inverse → Bg (row-major, coalesced), for the TRSM
   if (trsm)
     for (int e = t; e < NB64 * NB64; e += PNT) Bg[e] = S[(e >> 6) * SLD + (e & 63)];
@@ -640,25 +642,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
   const int s0 = c0 + NB64 + 64 * st;          // first row (side 0) / column (side 1) of the strip
   const int sw = min(64, R2 - 64 * st);        // 32 or 64
   if (side == 0) {
-    // stage U11⁻¹ (upper triangle of the packed inverse, zero below); all 16
-    // loads of a thread in flight before the first LDS store
-    {
-      double v[NB64 * NB64 / 256];
-#pragma unroll
-      for (int q = 0; q < NB64 * NB64 / 256; ++q) v[q] = Bg[t + 256 * q];
-#pragma unroll
-      for (int q = 0; q < NB64 * NB64 / 256; ++q) {
-        const int e = t + 256 * q, k = e >> 6, c = e & 63;
-        X[k * TLD + c] = k <= c ? v[q] : 0.0;
-      }
-    }
+    // every global load of the workgroup in flight before the first LDS
+    // store: U11⁻¹ (the packed inverse, L2-resident) and the A21 rows (HBM)
     const int row = s0 + 16 * wv;
     const bool wact = 16 * wv < sw;              // wave-uniform
-    double av[16];
+    double v[NB64 * NB64 / 256], av[16];
+#pragma unroll
+    for (int q = 0; q < NB64 * NB64 / 256; ++q) v[q] = Bg[t + 256 * q];
     if (wact) {
       const double* Ar = Kb + (size_t)(row + l16) * ld + c0;
 #pragma unroll
       for (int s = 0; s < 16; ++s) av[s] = Ar[4 * s + g];
+    }
+    // stage U11⁻¹ (upper triangle, zero below)
+#pragma unroll
+    for (int q = 0; q < NB64 * NB64 / 256; ++q) {
+      const int e = t + 256 * q, k = e >> 6, c = e & 63;
+      X[k * TLD + c] = k <= c ? v[q] : 0.0;
     }
     __syncthreads();
     if (!wact) return;
@@ -681,27 +681,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
     }
     if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;   // every writer stores the same value
   } else {
-    // stage the A12 strip: rows c0 .. c0+63, columns s0 .. s0+63 (zero past Np)
+    // the A12 strip (rows c0 .. c0+63, columns s0 .. s0+63, zero past Np)
+    // and the A operand, L11⁻¹ rows 16wv + l16 (unit diagonal, zero above;
+    // row tile wv needs k < 16(wv+1)): every global load in flight before
+    // the first LDS store
+    const int c8 = (t & 7) * 8;
+    const bool ok = c8 < sw;
+    double v[16], av[16];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int k = 32 * h + (t >> 3), c8 = (t & 7) * 8;
-      const bool ok = c8 < sw;
-      const double* src = Kb + (size_t)(c0 + k) * ld + (ok ? s0 + c8 : 0);
-      double v[8];
+      const double* src = Kb + (size_t)(c0 + 32 * h + (t >> 3)) * ld + (ok ? s0 + c8 : 0);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = src[u];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) X[k * TLD + c8 + u] = ok ? v[u] : 0.0;
+      for (int u = 0; u < 8; ++u) v[8 * h + u] = src[u];
     }
-    // A operand: L11⁻¹ rows 16wv + l16 (unit diagonal, zero above); row tile
-    // wv needs k < 16(wv+1)
     const int ii = 16 * wv + l16;
-    double av[16];
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const int k = 4 * s + g;
-      const double v = Bg[ii * NB64 + k];
-      av[s] = k == ii ? 1.0 : (k < ii ? v : 0.0);
+      const double bv = Bg[ii * NB64 + k];
+      av[s] = k == ii ? 1.0 : (k < ii ? bv : 0.0);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = 32 * h + (t >> 3);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) X[k * TLD + c8 + u] = ok ? v[8 * h + u] : 0.0;
     }
     __syncthreads();
     d4n acc[4];

@@ -13,6 +13,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 DOPT_KIND_QP = 0
 DOPT_KIND_CONIC = 1
+DOPT_KIND_NLP = 2
 DOPT_MEM_HOST = 0
 DOPT_MEM_DEVICE = 1
 
@@ -55,6 +56,17 @@ SIGNATURES = {
     "dopt_conic_factor": (ctypes.c_int, [_h]),
     "dopt_conic_forward": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 5),
     "dopt_conic_reverse": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 5),
+    "dopt_nlp_set_structure": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_int32]),
+    "dopt_nlp_set": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 12),
+    "dopt_nlp_factor": (ctypes.c_int, [_h]),
+    "dopt_nlp_forward": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 3),
+    "dopt_nlp_reverse": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 3),
+    "dopt_nlp_jacobian": (ctypes.c_int, [_h, ctypes.c_void_p]),
+    "dopt_nlp_get_corrections": (ctypes.c_int, [_h, ctypes.c_void_p]),
+    "dopt_nlp_get_layout": (ctypes.c_int, [_h, ctypes.c_void_p]),
+    "dopt_nlp_set_kkt": (ctypes.c_int, [_h, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
+    "dopt_nlp_kkt_solve": (ctypes.c_int, [_h, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
     "dopt_get_info": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_get_iterative": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_qp_get_kept": (ctypes.c_int, [_h, ctypes.c_void_p]),

@@ -164,3 +164,67 @@ def conic_numpy(batch, n, cones, seed, guard=1e-3):
         out["db"].append(rng.standard_normal(m))
         out["dc"].append(rng.standard_normal(n))
     return {k: np.stack(v) for k, v in out.items()}
+
+
+def nlp_numpy(batch, n, c, P, seed, frac_geq=0.4, frac_leq=0.3, frac_low=0.5, frac_up=0.3, active=0.3,
+              sense=1):
+    """NLP KKT data at a strictly complementary point (nlp_utilities.jl
+    conventions, MOI duals): shared structure (row kinds: EqualTo, then
+    GreaterThan, then LessThan, shuffled; variable bounds), per problem a
+    symmetric Hxx = LLᵀ/n + 0.1I (times `sense`), dense Hxp, Jx ~ N(0,1)/√n,
+    Jp ~ N(0,1); a fraction `active` of the inequality rows / bounds is
+    active (slack 0, dual ±U(0.5,1.5) by the set's sign), the rest inactive
+    (slack ±U(0.5,1.5), dual 0).  Returns (structure dict, point dict, dp,
+    dx seed, ddual seed)."""
+    rng = np.random.default_rng(seed)
+    ng, nl = int(frac_geq * c), int(frac_leq * c)
+    kinds = np.array([1] * ng + [2] * nl + [0] * (c - ng - nl), dtype=np.int32)
+    rng.shuffle(kinds)
+    has_low = (rng.random(n) < frac_low).astype(np.int8)
+    has_up = (rng.random(n) < frac_up).astype(np.int8)
+    st = dict(con_kind=kinds, has_low=has_low, has_up=has_up, sense=sense)
+    keys = ["Hxx", "Hxp", "Jx", "Jp", "x", "cval", "crhs", "y", "xl", "xu", "yl", "yu"]
+    pt = {k: [] for k in keys}
+    u = lambda size=None: rng.uniform(0.5, 1.5, size)
+    for _ in range(batch):
+        L = rng.standard_normal((n, n))
+        pt["Hxx"].append(sense * (L @ L.T / n + 0.1 * np.eye(n)))
+        pt["Hxp"].append(rng.standard_normal((n, P)))
+        pt["Jx"].append(rng.standard_normal((c, n)) / math.sqrt(n))
+        pt["Jp"].append(rng.standard_normal((c, P)))
+        x = rng.standard_normal(n)
+        cval = rng.standard_normal(c)
+        crhs = cval.copy()
+        y = np.zeros(c)
+        for k in range(c):
+            act = rng.random() < active
+            if kinds[k] == 0:
+                y[k] = rng.standard_normal()
+            elif kinds[k] == 1:   # GreaterThan: slack = cval − crhs ≥ 0, dual ≥ 0
+                if act:
+                    y[k] = u()
+                else:
+                    crhs[k] = cval[k] - u()
+            else:                 # LessThan: slack ≤ 0, dual ≤ 0
+                if act:
+                    y[k] = -u()
+                else:
+                    crhs[k] = cval[k] + u()
+        xl, xu, yl, yu = (np.zeros(n) for _ in range(4))
+        for j in range(n):
+            if has_low[j]:
+                if rng.random() < active:
+                    xl[j], yl[j] = x[j], u()
+                else:
+                    xl[j] = x[j] - u()
+            if has_up[j]:
+                if rng.random() < active and not (has_low[j] and xl[j] == x[j]):
+                    xu[j], yu[j] = x[j], -u()
+                else:
+                    xu[j] = x[j] + u()
+        for k, v in zip(keys[4:], (x, cval, crhs, y, xl, xu, yl, yu)):
+            pt[k].append(v)
+    pt = {k: np.stack(v) for k, v in pt.items()}
+    nd = c + int(has_low.sum()) + int(has_up.sum())
+    return st, pt, rng.standard_normal((batch, P)), rng.standard_normal((batch, n)), \
+        rng.standard_normal((batch, nd))

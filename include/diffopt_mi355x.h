@@ -42,6 +42,7 @@ extern "C" {
 
 #define DOPT_KIND_QP 0
 #define DOPT_KIND_CONIC 1
+#define DOPT_KIND_NLP 2
 
 #define DOPT_MEM_HOST 0
 #define DOPT_MEM_DEVICE 1
@@ -237,6 +238,59 @@ int dopt_conic_lsqr_stats(dopt_handle* h, int32_t* stats);
 /* ---- introspection ---------------------------------------------------------*/
 /* per-problem status of the last factor/solve: QP: 0 ok, k>0 zero pivot at
  * column k of the (reduced) KKT; CONIC: LSQR istop of the last solve. */
+/* ---- NonLinearProgram back-end (kind DOPT_KIND_NLP) ------------------------
+ * dopt_create's n = primal variables, m = NLP constraints c, p = parameters P.
+ * Replaces the KKT part of src/NonLinearProgram (the derivatives at the
+ * solution are evaluated by the caller, as the reference's MOI Nonlinear
+ * evaluator does, nlp_utilities.jl:35-92):
+ *   _compute_solution_and_bounds + _build_sensitivity_matrices
+ *     (nlp_utilities.jl:181-396)                  -> dopt_nlp_set_structure / _set
+ *   _lu_with_inertia_correction (NonLinearProgram.jl:394-422) -> dopt_nlp_factor
+ *   forward_differentiate! (NonLinearProgram.jl:502-528)       -> dopt_nlp_forward
+ *   reverse_differentiate! (NonLinearProgram.jl:530-582)       -> dopt_nlp_reverse
+ *   _compute_sensitivity's ∂s (nlp_utilities.jl:457-500)      -> dopt_nlp_jacobian
+ * Every array is batch-major; matrices are column-major per problem (Julia
+ * layout, as the QP entry points). */
+/* con_kind[c]: 0 EqualTo, 1 GreaterThan, 2 LessThan, in NLP constraint order;
+ * has_low / has_up[n]: VariableIndex-in-GreaterThan / LessThan bounds;
+ * sense: +1 MIN_SENSE, -1 MAX_SENSE.  Shared by the batch. */
+int dopt_nlp_set_structure(dopt_handle* h, const int32_t* con_kind, const int8_t* has_low,
+                           const int8_t* has_up, int32_t sense);
+/* Hxx[n×n], Hxp[n×P]: Hessian of f − sense·yᵀc (eval_hessian_lagrangian with
+ * σ = 1, μ = −sense·y) over primal × primal / primal × parameter;
+ * Jx[c×n], Jp[c×P]: constraint Jacobian; x[n]; cval[c] = c(x) and crhs[c] the
+ * set constant (slack = cval − crhs); y[c], yl[n], yu[n]: MOI ConstraintDual
+ * values of the rows and of the bounds; xl[n], xu[n]: bound values (entries of
+ * unbounded variables are ignored; yl/yu/xl/xu may be NULL when no variable
+ * has that bound). */
+int dopt_nlp_set(dopt_handle* h, const double* Hxx, const double* Hxp, const double* Jx,
+                 const double* Jp, const double* x, const double* cval, const double* crhs,
+                 const double* y, const double* xl, const double* xu, const double* yl,
+                 const double* yu);
+/* LU of every problem's M with the reference's inertia correction
+ * (M + k·1e-6·D, k ≤ 50); a problem whose correction fails gets ∂s = 0, as
+ * in the reference (nlp_utilities.jl:436-439). */
+int dopt_nlp_factor(dopt_handle* h);
+/* dp[P] → dx[n], ddual[c + nlow + nup] (constraint duals, then the duals of
+ * the primal lower and upper bounds in variable order): ∂s·Δp. */
+int dopt_nlp_forward(dopt_handle* h, const double* dp, double* dx, double* ddual);
+/* dx[n], ddual[c + nlow + nup] (either may be NULL = 0) → dp[P] = ∂sᵀΔw. */
+int dopt_nlp_reverse(dopt_handle* h, const double* dx, const double* ddual, double* dp);
+/* ∂s itself: ds[rows × P] per problem (column-major), rows = the size of M
+ * (dopt_nlp_get_layout). */
+int dopt_nlp_jacobian(dopt_handle* h, double* ds);
+/* corrections applied per problem (0 none, k > 0, -1 failed) */
+int dopt_nlp_get_corrections(dopt_handle* h, int32_t* corr);
+/* layout[7] = {rows, num_w, c, nlo, nup, nlow_primal, nup_primal} */
+int dopt_nlp_get_layout(dopt_handle* h, int32_t* layout);
+/* KKT mode — the reference's NonLinearKKTJacobianFactorization plug point
+ * (`(M, model) -> K`, then ldiv!(∂s, K, N), nlp_utilities.jl:436-442): M[rows ×
+ * rows] per problem, num_w / num_cons set the inertia correction's D.  Then
+ * dopt_nlp_factor and dopt_nlp_kkt_solve: x = K \ rhs for k right-hand sides
+ * per problem, rhs / x seed-major (k × batch × rows). */
+int dopt_nlp_set_kkt(dopt_handle* h, int32_t rows, int32_t num_w, int32_t num_cons, const double* M);
+int dopt_nlp_kkt_solve(dopt_handle* h, int32_t k, const double* rhs, double* x);
+
 int dopt_get_info(dopt_handle* h, int32_t* info);
 /* per-problem `iterative` branch flags (QP; 1 = LSQR branch). */
 int dopt_get_iterative(dopt_handle* h, int8_t* flags);

@@ -1,0 +1,219 @@
+"""NLP back-end on the GPU (csrc/nlp.hip through the C-ABI) against the
+oracle (oracle/nlp.py, pinned by tests/test_nlp_oracle.py) and the
+reference's own expected values: the golden fixtures, seeded synthetic
+batches (mixed row kinds, bounds, MIN and MAX, both LU routes), the inertia
+correction (KKT mode with the reference's singular matrix, and a structured
+problem with a dependent constraint), device-mode inputs and the adjoint
+identity.  Bar: north_star's 1e-6 relative Frobenius against the oracle (the
+fixtures additionally at their reference tolerance)."""
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import nlp as onlp
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-6
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "nlp_fixtures.json")))
+KEYS = ["Hxx", "Hxp", "Jx", "Jp", "x", "cval", "crhs", "y", "xl", "xu", "yl", "yu"]
+
+
+def relfro(a, b):
+    a, b = np.asarray(a, dtype=float), np.asarray(b, dtype=float)
+    nb = np.linalg.norm(b)
+    return np.linalg.norm(a - b) / (nb if nb > 0 else 1.0)
+
+
+@pytest.fixture(params=["nopiv", "pivot"])
+def lu_mode(request, monkeypatch):
+    if request.param == "pivot":
+        monkeypatch.setenv("DOPT_LU", "0")
+    else:
+        monkeypatch.delenv("DOPT_LU", raising=False)
+    return request.param
+
+
+def engine(st, pt, B):
+    from diffopt_amd.nlp import NLPBatch
+    n = pt["x"].shape[1]
+    c = pt["Jx"].shape[1]
+    P = pt["Hxp"].shape[2]
+    e = NLPBatch(B, n, c, P)
+    e.set_structure(st["con_kind"], st["has_low"], st["has_up"], st["sense"])
+    e.set(*[pt[k] for k in KEYS])
+    e.factor()
+    return e
+
+
+def oracle_problem(st, pt, b):
+    return onlp.compute_sensitivity(st["con_kind"], st["has_low"], st["has_up"], st["sense"],
+                                    *[pt[k][b] for k in KEYS], return_info=True)
+
+
+def check_against_oracle(e, st, pt, dp, dx, dd, problems):
+    fx, fd = e.forward(dp)
+    rp = e.reverse(dx, dd)
+    J = e.jacobian()
+    worst = 0.0
+    for b in problems:
+        ds, L, M, N, corr = oracle_problem(st, pt, b)
+        ox, od = onlp.forward(ds, L, dp[b])
+        op = onlp.reverse(ds, L, dx[b], dd[b])
+        # the forward output as one vector (∂s·Δp restricted to primal and duals):
+        # a block can be ~0 in exact arithmetic (NLP_1_3: x does not depend on p3)
+        worst = max(worst, relfro(np.concatenate([fx[b], fd[b]]), np.concatenate([ox, od])), relfro(rp[b], op),
+                    relfro(J[b], ds))
+    assert worst <= RTOL, worst
+    return fx, fd, rp, J
+
+
+# ---- golden fixtures -------------------------------------------------------
+def _fixture_batch(f, B=2):
+    st = dict(con_kind=np.asarray(f["con_kind"], np.int32), has_low=np.asarray(f["has_low"], np.int8),
+              has_up=np.asarray(f["has_up"], np.int8), sense=f["sense"])
+    pt = {k: np.stack([np.asarray(f["point"][k], dtype=float)] * B) for k in KEYS}
+    return st, pt
+
+
+@pytest.mark.parametrize("f", GOLD["fixtures"], ids=lambda f: f["name"])
+def test_fixture(f, lu_mode):
+    st, pt = _fixture_batch(f)
+    e = engine(st, pt, 2)
+    assert (e.corrections() == 0).all()
+    B, P = 2, pt["Hxp"].shape[2]
+    nd = e.ndual
+    rng = np.random.default_rng(11)
+    dp = np.stack([np.asarray(f["fwd"]["dp"], float)] * B) if "fwd" in f else rng.standard_normal((B, P))
+    if "rev" in f:
+        dx = np.stack([np.asarray(f["rev"]["dx"], float)] * B)
+        dd = np.stack([np.asarray(f["rev"]["ddual"], float)] * B)
+    else:
+        dx, dd = rng.standard_normal((B, pt["x"].shape[1])), rng.standard_normal((B, nd))
+    fx, fd, rp, _ = check_against_oracle(e, st, pt, dp, dx, dd, range(B))
+    tol = dict(atol=f["atol"], rtol=f.get("rtol", 0.0))
+    c, nlowp = len(f["con_kind"]), e.layout()["nlow_primal"]
+    for key, want in f.get("expect_fwd", {}).items():
+        got = {"dx": fx[0], "dy": fd[0, :c], "dvl": fd[0, c:c + nlowp], "dvu": fd[0, c + nlowp:]}[key]
+        np.testing.assert_allclose(got, want, err_msg=key, **tol)
+    if "expect_rev" in f:
+        np.testing.assert_allclose(rp[0], f["expect_rev"]["dp"], **tol)
+
+
+# ---- synthetic batches -----------------------------------------------------
+@pytest.mark.parametrize("sense", [1, -1])
+def test_synthetic_batch(lu_mode, sense):
+    from diffopt_amd.synthetic import nlp_numpy
+    st, pt, dp, dx, dd = nlp_numpy(8, 60, 40, 7, 1234 + sense, sense=sense)
+    e = engine(st, pt, 8)
+    lay = e.layout()
+    assert lay["rows"] == onlp.Layout(st["con_kind"], st["has_low"], st["has_up"]).rows
+    check_against_oracle(e, st, pt, dp, dx, dd, range(8))
+
+
+def test_synthetic_multiblock():
+    """M larger than one 64-column LU block step pair (rows ≈ 420): the
+    blocked LU's paired trailing updates and the multi-RHS Jacobian."""
+    from diffopt_amd.synthetic import nlp_numpy
+    st, pt, dp, dx, dd = nlp_numpy(4, 150, 110, 20, 99)
+    e = engine(st, pt, 4)
+    assert e.layout()["rows"] > 256
+    check_against_oracle(e, st, pt, dp, dx, dd, [0, 3])
+
+
+def test_adjoint_identity():
+    """⟨Δw, ∂s·Δp⟩ = ⟨∂sᵀΔw, Δp⟩ through the engine's two solves."""
+    from diffopt_amd.synthetic import nlp_numpy
+    st, pt, dp, dx, dd = nlp_numpy(6, 50, 30, 9, 5)
+    e = engine(st, pt, 6)
+    fx, fd = e.forward(dp)
+    rp = e.reverse(dx, dd)
+    lhs = np.einsum("bi,bi->b", dx, fx) + np.einsum("bi,bi->b", dd, fd)
+    rhs = np.einsum("bi,bi->b", rp, dp)
+    np.testing.assert_allclose(lhs, rhs, rtol=1e-10, atol=1e-12)
+
+
+# ---- inertia correction ------------------------------------------------------
+def test_kkt_mode_inertia_correction():
+    """test_inertia_correction (test/nlp_program.jl:767-795) in KKT mode — the
+    NonLinearKKTJacobianFactorization plug point: the singular M is corrected
+    (k = 1, as the oracle) and K \\ rhs matches the oracle's corrected factor;
+    a regular M in the same batch is not touched."""
+    from diffopt_amd.nlp import NLPBatch
+    k = GOLD["kkt"][0]
+    M = np.asarray(k["M"], dtype=float)
+    rng = np.random.default_rng(8)
+    R = rng.standard_normal((5, 5)) + 5 * np.eye(5)
+    Ms = np.stack([M, R, M])
+    e = NLPBatch(3, 5, 0, 0)
+    e.set_kkt(Ms, k["num_w"], k["num_cons"])
+    e.factor()
+    Ko, corr = onlp.inertia_correction(M, k["num_cons"], k["num_w"])
+    np.testing.assert_array_equal(e.corrections(), [corr, 0, corr])
+    rhs = rng.standard_normal((4, 3, 5))
+    x = e.kkt_solve(rhs)
+    for j in range(4):
+        for b, want in ((0, Ko.solve(rhs[j, 0])), (1, np.linalg.solve(R, rhs[j, 1])), (2, Ko.solve(rhs[j, 2]))):
+            assert relfro(x[j, b], want) <= 1e-8, (j, b)
+
+
+def test_structured_dependent_constraint():
+    """Two identical equality rows (LICQ fails): M is exactly singular, the
+    inertia correction regularises it; the engine's correction count and ∂s
+    match the oracle's."""
+    from diffopt_amd.synthetic import nlp_numpy
+    st, pt, dp, dx, dd = nlp_numpy(3, 20, 12, 4, 77)
+    kinds = st["con_kind"]
+    eq = np.flatnonzero(kinds == 0)
+    assert len(eq) >= 2
+    i, j = eq[:2]
+    b = 1   # only problem 1 becomes singular
+    pt["Jx"][b, j] = pt["Jx"][b, i]
+    pt["Jp"][b, j] = pt["Jp"][b, i]
+    e = engine(st, pt, 3)
+    _, _, _, _, corr = oracle_problem(st, pt, b)
+    assert corr >= 1
+    got = e.corrections()
+    assert got[0] == 0 and got[2] == 0 and got[1] == corr, (got, corr)
+    fx, fd = e.forward(dp)
+    ds, L, *_ = oracle_problem(st, pt, b)
+    ox, od = onlp.forward(ds, L, dp[b])
+    # the corrected system is ill-conditioned (shift 1e-6·k): a looser bar
+    assert relfro(np.concatenate([fx[b], fd[b]]), np.concatenate([ox, od])) <= 1e-4
+
+
+# ---- memory modes and errors -------------------------------------------------
+def test_device_mode_matches_host():
+    import torch
+    from diffopt_amd.nlp import NLPBatch
+    from diffopt_amd.synthetic import nlp_numpy
+    st, pt, dp, dx, dd = nlp_numpy(4, 30, 20, 5, 21)
+    eh = engine(st, pt, 4)
+    hx, hd = eh.forward(dp)
+    hp = eh.reverse(dx, dd)
+    t = lambda a: torch.as_tensor(a, device="cuda")
+    ed = NLPBatch(4, 30, 20, 5)
+    ed.set_structure(st["con_kind"], st["has_low"], st["has_up"], st["sense"])
+    ed.set(*[t(pt[k]) for k in KEYS])
+    ed.factor()
+    gx, gd = ed.forward(t(dp))
+    gp = ed.reverse(t(dx), t(dd))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(gx.cpu().numpy(), hx, rtol=1e-13, atol=1e-14)
+    np.testing.assert_allclose(gd.cpu().numpy(), hd, rtol=1e-13, atol=1e-14)
+    np.testing.assert_allclose(gp.cpu().numpy(), hp, rtol=1e-13, atol=1e-14)
+
+
+def test_argument_errors():
+    from diffopt_amd import EngineError
+    from diffopt_amd.nlp import NLPBatch
+    e = NLPBatch(2, 3, 2, 1)
+    with pytest.raises(EngineError, match="set_structure"):
+        e.set(np.zeros((2, 3, 3)), np.zeros((2, 3, 1)), np.zeros((2, 2, 3)), np.zeros((2, 2, 1)), np.zeros((2, 3)),
+              np.zeros((2, 2)), np.zeros((2, 2)), np.zeros((2, 2)))
+    with pytest.raises(EngineError, match="con_kind"):
+        e.set_structure([0, 5])
+    with pytest.raises(EngineError, match="sense"):
+        e.set_structure([0, 1], sense=0)
