@@ -41,6 +41,12 @@ QP_CFG = {2: dict(id=2, n=200, m=300, p=0, phi=0.3, batch=1024),
 # conic configs (BASELINE.json configs[3], [4]); batch = problems per GPU
 # (config 5: 64 SDPs over 4 GPUs = 16 per GPU)
 CONIC_CFG = {4: dict(batch=512), 5: dict(batch=16)}
+# NLP back-end (§8(f)4; not a BASELINE config — no published number): 1024
+# problems, 200 primal variables, 100 constraints (40 ≥, 30 ≤, 30 =), 20
+# parameters, 50 % / 30 % of the variables bounded below / above → M of
+# about 600 rows
+NLP_CFG = {6: dict(batch=1024, n=200, c=100, P=20)}
+NLP_KEYS = ["Hxx", "Hxp", "Jx", "Jp", "x", "cval", "crhs", "y", "xl", "xu", "yl", "yu"]
 
 
 # --------------------------------------------------------------------------
@@ -79,6 +85,139 @@ def cpu_baseline(cfg, seconds, workers):
                 sample=(f"{solves} config-{cfg.get('id', 2)} QP solves (n={cfg['n']}, m={cfg['m']}, fwd+rev, "
                         f"SuperLU re-factorised per direction) on {workers} processes "
                         f"× {seconds:.0f} s (wall {wall:.1f} s)"))
+
+
+def _nlp_cpu_worker(args):
+    cfg, seed, seconds = args
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"
+    from diffopt_amd.synthetic import nlp_numpy
+    from oracle import nlp as onlp
+    st, pt, dp, dx, dd = nlp_numpy(2, cfg["n"], cfg["c"], cfg["P"], seed)
+    n_done = 0
+    t0 = time.perf_counter()
+    while True:
+        b = n_done % 2
+        a = [pt[k][b] for k in NLP_KEYS]
+        sk = (st["con_kind"], st["has_low"], st["has_up"], st["sense"])
+        # forward_differentiate! and reverse_differentiate! each recompute ∂s
+        # (NonLinearProgram.jl:516, 536): two factorisations per fwd+rev
+        ds, L, *_ = onlp.compute_sensitivity(*sk, *a, return_info=True)
+        onlp.forward(ds, L, dp[b])
+        ds, L, *_ = onlp.compute_sensitivity(*sk, *a, return_info=True)
+        onlp.reverse(ds, L, dx[b], dd[b])
+        n_done += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    return n_done, time.perf_counter() - t0
+
+
+def run_nlp(args, world, rank, local_rank):
+    """NLP KKT sensitivities (config 6): one step = for every problem the sIpopt
+    KKT assembly, LU with the inertia-correction check, forward (Δp → Δx,
+    Δdual) and reverse (Δx, Δdual → Δp) solves."""
+    cfg = dict(NLP_CFG[args.config])
+    B = args.batch or cfg["batch"]
+    n, c, P = cfg["n"], cfg["c"], cfg["P"]
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import multiprocessing as mp
+        workers = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
+        t0 = time.perf_counter()
+        with mp.get_context("fork").Pool(workers) as pool:
+            res = pool.map(_nlp_cpu_worker, [(cfg, 3000 + i, args.cpu_seconds) for i in range(workers)])
+        wall = time.perf_counter() - t0
+        cpu = dict(value=round(sum(r[0] / r[1] for r in res), 2), unit="solves/s", cores=workers, kind="port",
+                   sample=(f"{sum(r[0] for r in res)} config-6 NLP solves (n={n}, c={c}, P={P}; ∂s recomputed "
+                           f"per direction with SuperLU, as the reference) on {workers} processes × "
+                           f"{args.cpu_seconds:.0f} s (wall {wall:.1f} s)"))
+    import numpy as np
+    import torch
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+    from diffopt_amd.nlp import NLPBatch
+    from diffopt_amd.synthetic import SEED0, nlp_numpy
+    st, pt, dp, dx, dd = nlp_numpy(B, n, c, P, SEED0 + args.config + 7919 * rank)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")
+    eng = NLPBatch(B, n, c, P, device=local_rank)
+    eng.set_structure(st["con_kind"], st["has_low"], st["has_up"], st["sense"])
+    eng.set(*[t(pt[k]) for k in NLP_KEYS])
+    dp_t, dx_t, dd_t = t(dp), t(dx), t(dd)
+    rows = eng.layout()["rows"]
+
+    def step():
+        eng.factor()
+        eng.forward(dp_t)
+        eng.reverse(dx_t, dd_t)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.phase_times()
+    eng.set_profiling(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.set_profiling(False)
+    phases = eng.phase_times()
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    corr = eng.corrections()
+    kinds = eng.lu_kind()
+    if rank == 0:
+        name, (ms_tot, cnt) = max(phases.items(), key=lambda kv: kv[1][0])
+        avg_s = ms_tot / cnt / 1e3
+        if name in ("qp_lu", "qp_lu_pivot"):
+            work = B * 2.0 / 3.0 * rows ** 3
+            achieved = work / avg_s / 1e12
+            roof = dict(bound="mfma", achieved=round(achieved, 3), peak=PEAK_FP64_TFLOPS, unit="TFLOP/s",
+                        frac=round(achieved / PEAK_FP64_TFLOPS, 4))
+        else:
+            work = B * 8.0 * rows * rows   # one read of the factors
+            achieved = work / avg_s / 1e9
+            roof = dict(bound="hbm", achieved=round(achieved, 1), peak=PEAK_HBM_GBS, unit="GB/s",
+                        frac=round(achieved / PEAK_HBM_GBS, 4))
+        roof["kernel"] = name.replace("qp_", "nlp_")
+        roof["traffic"] = _load_pmc(name + "@cfg6")
+        roof["avg_launch_ms"] = round(avg_s * 1e3, 4)
+        roof["phases_ms_per_step"] = {k.replace("qp_", "nlp_"): round(v[0] / args.steps, 4)
+                                      for k, v in sorted(phases.items())}
+        line = {
+            "metric": "NLP KKT sensitivity solves/sec (fwd+rev)",
+            "value": round(world * B * args.steps / elapsed, 1),
+            "unit": "solves/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded strictly complementary NLP KKT point, diffopt_amd.synthetic.nlp_numpy)",
+            "config": {"workload": "config 6: NLP KKT batch (sIpopt system + inertia correction), fwd+rev",
+                       "problems_per_gpu": B, "n": n, "constraints": c, "params": P, "kkt_rows": rows,
+                       "inertia_corrections": int((corr != 0).sum()),
+                       "factorisation": {"no_pivot": int((kinds == 1).sum()),
+                                         "partial_pivoting": int((kinds == 2).sum())},
+                       "parallelism": f"batch-sharded x{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
 
 
 def _conic_cpu_worker(args):
@@ -284,7 +423,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=None, choices=sorted(QP_CFG) + sorted(CONIC_CFG),
+    ap.add_argument("--config", type=int, default=None, choices=sorted(QP_CFG) + sorted(CONIC_CFG) + sorted(NLP_CFG),
                     help="default: 2 at N = 1, 3 (the north_star headline) under torchrun")
     ap.add_argument("--lam-eps", type=float, default=0.0,
                     help="QP: inactive rows get λ = LAM_EPS instead of 0 (no exact elimination)")
@@ -304,6 +443,8 @@ def main():
         args.config = 3 if world > 1 else 2
     if args.config in CONIC_CFG:
         return run_conic(args, world, rank, local_rank)
+    if args.config in NLP_CFG:
+        return run_nlp(args, world, rank, local_rank)
     cfg = dict(QP_CFG[args.config])
     cfg["lam_eps"] = args.lam_eps
     if args.batch:

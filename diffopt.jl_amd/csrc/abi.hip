@@ -666,7 +666,7 @@ int dopt_qp_get_kept(dopt_handle* h, int8_t* kept) {
 
 int dopt_qp_get_lu_kind(dopt_handle* h, int8_t* kinds) {
   return guarded(h, [&]() {
-    if (h->kind != DOPT_KIND_QP) throw Error(-1, "QP only");
+    if (h->kind != DOPT_KIND_QP && h->kind != DOPT_KIND_NLP) throw Error(-1, "QP and NLP handles only");
     if (!kinds) throw Error(-1, "kinds is required");
     std::vector<dopt::QPMeta> meta(h->batch);
     DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h->meta.p, h->batch * sizeof(dopt::QPMeta),

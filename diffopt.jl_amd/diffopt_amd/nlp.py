@@ -128,6 +128,21 @@ class NLPBatch:
         lay = self.layout()
         return self.c + lay["nlow_primal"] + lay["nup_primal"]
 
+    def lu_kind(self):
+        """Per-problem factorisation kind (the shared blocked LU):
+        _lib.LU_KIND_NOPIV / LU_KIND_PIVOT."""
+        buf = np.zeros(self.batch, dtype=np.int8)
+        _lib.check(self.lib.dopt_qp_get_lu_kind(self.h, buf.ctypes.data), self.h)
+        return buf
+
+    def set_profiling(self, on=True):
+        _lib.check(self.lib.dopt_set_profiling(self.h, int(bool(on))), self.h)
+
+    def phase_times(self):
+        """{phase name: (total ms, launches)} since the last call; the NLP path
+        reports under the shared QP phase names (assembly, LU, solve, …)."""
+        return _lib.phase_times(self.lib, self.h)
+
     # ---- sensitivities -----------------------------------------------------
     def forward(self, dp):
         """Δp (B, P) → (Δx (B, n), Δdual (B, c + nlow + nup))."""
