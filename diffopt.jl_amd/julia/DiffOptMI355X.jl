@@ -26,6 +26,7 @@ const LIB = get(ENV, "DIFFOPT_MI355X_LIB",
                 joinpath(@__DIR__, "..", "diffopt_amd", "libdiffopt_mi355x.so"))
 const KIND_QP = Int32(0)
 const KIND_CONIC = Int32(1)
+const KIND_NLP = Int32(2)
 
 # ---------------------------------------------------------------- handle ----
 mutable struct Handle
@@ -371,6 +372,57 @@ function DiffOpt.reverse_differentiate!(m::ConicModel)
         inner.back_grad_cache = CP.ReverseCache(g, vcat(inner.x, vp, 1.0))
     end
     return
+end
+
+# -------------------------------------------------------- NLP factorization ----
+# The NonLinearProgram back-end's own plug point: the
+# `NonLinearKKTJacobianFactorization` model attribute (reference
+# src/diff_opt.jl:97-112, default `_lu_with_inertia_correction` set by
+# src/DiffOpt.jl:45-49) is a function `(M, model) -> K` whose result is used as
+# `ldiv!(∂s, K, N)` (nlp_utilities.jl:436-442).  `mi355x_factorization`
+# returns a K that lives on the MI355X: the KKT Jacobian is factorised there
+# with the reference's inertia correction (M + k·1e-6·D, k ≤ 50; D = −1 on the
+# constraint rows), and `ldiv!` solves all columns of N in one launch.
+#
+#   MOI.set(model, DiffOpt.NonLinearKKTJacobianFactorization(),
+#           DiffOptMI355X.mi355x_factorization)
+const NLP = DiffOpt.NonLinearProgram
+
+struct KKTFactor
+    h::Handle
+    rows::Int
+end
+
+function mi355x_factorization(M::SparseArrays.SparseMatrixCSC, model::NLP.Model)
+    num_w = NLP._get_num_primal_vars(model) + length(model.cache.leq_locations) +
+            length(model.cache.geq_locations)                       # NonLinearProgram.jl:400-404
+    num_cons = NLP._get_num_constraints(model)
+    rows = size(M, 1)
+    h = Handle(rows, 0, 0; kind = KIND_NLP)
+    Md = Matrix{Float64}(M)                                        # column-major rows × rows
+    GC.@preserve Md _check(ccall((:dopt_nlp_set_kkt, LIB), Cint,
+                                 (Ptr{Cvoid}, Int32, Int32, Int32, Ptr{Float64}),
+                                 h.ptr, rows, num_w, num_cons, Md), h.ptr)
+    _check(ccall((:dopt_nlp_factor, LIB), Cint, (Ptr{Cvoid},), h.ptr), h.ptr)
+    corr = Ref{Int32}(0)
+    _check(ccall((:dopt_nlp_get_corrections, LIB), Cint, (Ptr{Cvoid}, Ptr{Int32}), h.ptr, corr), h.ptr)
+    if corr[] < 0                                                  # as _inertia_correction's failure
+        @warn "Inertia correction failed."
+        return nothing
+    end
+    return KKTFactor(h, rows)
+end
+
+function LinearAlgebra.ldiv!(Y::AbstractMatrix{Float64}, K::KKTFactor, N::AbstractMatrix)
+    k = size(N, 2)
+    k == 0 && return Y
+    Nd = Matrix{Float64}(N)                                        # rows × k = seed-major (k × 1 × rows)
+    Yd = Matrix{Float64}(undef, K.rows, k)
+    GC.@preserve Nd Yd _check(ccall((:dopt_nlp_kkt_solve, LIB), Cint,
+                                    (Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}),
+                                    K.h.ptr, k, Nd, Yd), K.h.ptr)
+    copyto!(Y, Yd)
+    return Y
 end
 
 end # module
