@@ -26,6 +26,7 @@ KERNEL_PHASE = {
     "qp_factor_fast_kernel": "qp_lu",
     "qp_solve_fast_kernel": "qp_solve",
     "conic_lsqr_kernel": "conic_lsqr",
+    "conic_lsqr2_kernel": "conic_lsqr",     # co-iterated forward + reverse (one launch per call)
     "conic_cone_kernel": "conic_cone",
     "conic_split_pass_kernel": "conic_split_pass",
     "qp_prep_asm_kernel": "qp_assemble",
@@ -38,6 +39,12 @@ QP_GROUPS = {"qp_lu": ("nlu_diag_kernel", "nlu_trsm_kernel", "nlu_update_kernel"
                        "blu_panel_kernel", "blu_update_kernel"),
              "qp_solve": ("blu_solve_kernel", "blu_solve_rows_kernel", "blu_solve2_kernel")}
 QP_STEP = "qp_prep_asm_kernel"
+# NLP back-end (bench config 6): the step is counted by the assembly; its LU
+# is the partial-pivoting blocked LU, its solves the blocked solve kernels
+NLP_GROUPS = {"qp_assemble": ("nlp_assemble_kernel",),
+              "qp_lu_pivot": ("blu_panel_kernel", "blu_update_kernel"),
+              "qp_solve": ("blu_solve_kernel", "blu_solve_rows_kernel")}
+NLP_STEP = "nlp_assemble_kernel"
 # split-path LSQR: every conic_split_* dispatch belongs to the LSQR call opened
 # by the preceding conic_split_init_kernel; reported per LSQR call under the
 # bench's phase name "conic_lsqr" (key "conic_lsqr_split")
@@ -72,21 +79,22 @@ def per_launch(d, counter):
                         calls.add(row.get("Dispatch_Id"))
     if calls:
         res["conic_lsqr_split"] = tot / len(calls)
-    gtot, steps = defaultdict(float), set()
-    for f in files:
-        with open(f) as fh:
-            for row in csv.DictReader(fh):
-                if row.get("Counter_Name") != counter:
-                    continue
-                kn = row.get("Kernel_Name", "")
-                if QP_STEP in kn:
-                    steps.add(row.get("Dispatch_Id"))
-                for ph, frags in QP_GROUPS.items():
-                    if any(fr in kn for fr in frags):
-                        gtot[ph] += float(row["Counter_Value"])
-    if steps:
-        for ph, v in gtot.items():
-            res[ph] = v / len(steps)
+    for groups, step in ((QP_GROUPS, QP_STEP), (NLP_GROUPS, NLP_STEP)):
+        gtot, steps = defaultdict(float), set()
+        for f in files:
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if row.get("Counter_Name") != counter:
+                        continue
+                    kn = row.get("Kernel_Name", "")
+                    if step in kn:
+                        steps.add(row.get("Dispatch_Id"))
+                    for ph, frags in groups.items():
+                        if any(fr in kn for fr in frags):
+                            gtot[ph] += float(row["Counter_Value"])
+        if steps:
+            for ph, v in gtot.items():
+                res[ph] = v / len(steps)
     return res
 
 
