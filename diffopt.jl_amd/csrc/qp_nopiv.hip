@@ -61,6 +61,9 @@
 #ifndef NLU_STOP
 #define NLU_STOP 99
 #endif
+#ifndef NLU_ROT
+#define NLU_ROT (blockIdx.x & 3)
+#endif
 // probe builds with -DNLU_STAMPS: per-phase s_memtime cycles of the diagonal
 // kernel summed over workgroups into nlu_stamps[] (thread 0)
 #ifdef NLU_STAMPS
@@ -397,7 +400,9 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
   double* S = L.S;
   const int Wv = min(NB64, Np - c0);   // 32 or 64
   const bool trsm = Np - c0 > NB64;    // a trailing step follows
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // wave roles rotate with the problem index, so that the single-wave phases
+  // (A, D) of the four workgroups sharing a CU land on different SIMDs
+  const int t = threadIdx.x, lane = t & 63, wv = ((t >> 6) + NLU_ROT) & 3;
   const int g = lane >> 4, l16 = lane & 15;
   NLU_MARK_INIT;
   if (t == 0) *L.sbad = 0;
@@ -571,8 +576,64 @@ constexpr int STEP_LDS = NB64 * ULD;   // 40 KB: 4 workgroups per CU
 static_assert(NB64 * SLD + 200 + 256 <= STEP_LDS, "diagonal image + rowb/colb/sbad/vec/trash must fit 40 KB");
 static_assert((NB64 * SLD + 200) % 2 == 0, "trash slots 16-byte aligned");
 
+// TRSM of strip 0 of step c0 in the diagonal workgroup, from the packed
+// inverse in S: L21(0) = A21(0)·U11⁻¹ (wave w: rows 16w..16w+15 of the strip)
+// and U12(0) = L11⁻¹·A12(0) (wave w: columns 16w..16w+15), both to K, with the
+// threshold test on L21(0).  The k-steps that meet only the zero triangle of
+// an inverse are skipped.  nlu_cross_kernel, which computes the other strips
+// of the step, reads these two as its shared operands.  sw: strip width (32
+// or 64); no barrier follows, so inactive waves return at once.
+__device__ __forceinline__ void diag_strip0(const double* S, double* __restrict__ Kb, int ld, int c0, int sw,
+                                            QPMeta* __restrict__ mb) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
+  if (16 * wv >= sw) return;   // wave-uniform
+  const int r0 = c0 + NB64;
+  double av[16], bv[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) av[s] = Kb[(size_t)(r0 + 16 * wv + l16) * ld + c0 + 4 * s + g];
+  d4n acc[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {   // U11⁻¹ is upper: k ≤ 16ct + 15
+    acc[ct] = (d4n){0, 0, 0, 0};
+    const int c = 16 * ct + l16;
+#pragma unroll
+    for (int s = 0; s < 4 * (ct + 1); ++s) {
+      const int k = 4 * s + g;
+      acc[ct] = nmfma(av[s], k <= c ? S[k * SLD + c] : 0.0, acc[ct]);
+    }
+  }
+  int over = 0;
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      Kb[(size_t)(r0 + 16 * wv + g + 4 * rr) * ld + c0 + 16 * ct + l16] = acc[ct][rr];
+      over |= !(fabs(acc[ct][rr]) <= NOPIV_LMAX);
+    }
+  if (__any(over) && lane == 0) mb->lu = LU_REJECT;   // every writer stores the same value
+  const double* bsrc = Kb + (size_t)(c0 + g) * ld + r0 + 16 * wv + l16;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) bv[s] = bsrc[(size_t)4 * s * ld];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {   // L11⁻¹ is unit lower: k ≤ 16it + 15
+    acc[it] = (d4n){0, 0, 0, 0};
+    const int i = 16 * it + l16;
+#pragma unroll
+    for (int s = 0; s < 4 * (it + 1); ++s) {
+      const int k = 4 * s + g;
+      acc[it] = nmfma(k == i ? 1.0 : (k < i ? S[i * SLD + k] : 0.0), bv[s], acc[it]);
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < 4; ++it)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) Kb[(size_t)(c0 + 16 * it + g + 4 * rr) * ld + r0 + 16 * wv + l16] = acc[it][rr];
+}
+
 // Diagonal block of step c0 of every problem: one 256-thread workgroup per
 // problem, 40 KB of LDS: 4 per CU, a 1024-problem batch runs in one round.
+// STRIP0: also strip 0 of the step's TRSM (diag_strip0), for the cross kernel.
+template <bool STRIP0>
 __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_diag_kernel(
     double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
     size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv, double* __restrict__ w0,
@@ -607,6 +668,13 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
   diag_core(DiagLds(S), Kb, ld, perm + (size_t)b * nmax, dinv + (size_t)b * dstride + (size_t)(c0 / 32) * DBLK,
             meta + b, c0, Np, mm.nsys, binv + (size_t)b * NB64 * NB64, w0 ? w0 + (size_t)b * nmax : nullptr,
             w0 ? w1 + (size_t)b * nmax : nullptr);
+  if constexpr (STRIP0) {
+    const int sw = min(NB64, Np - c0 - NB64);
+    if (sw <= 0) return;   // no trailing step for this problem
+    __syncthreads();       // S final (and the threshold verdicts of diag_core)
+    if (*DiagLds(S).sbad) return;
+    diag_strip0(S, Kb, ld, c0, sw, meta + b);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -730,87 +798,184 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 }
 
 // ---------------------------------------------------------------------------
-// Trailing update A22 −= L21·U12 (rank 64) for the rows and columns from
-// c0+64.  64×64 tiles: wave w owns tile rows 16w..16w+15 × 64 columns (4 MFMA
-// tiles); the 64×64 U12 tile is staged once in LDS.  1-D grid of nrt·nct·B
-// tiles with an XCD-aware remap: the logical tiles of one problem are
-// consecutive, so they run on one XCD and share its L2 for L21 and U12.
+// Cross band of step c0 with the TRSM of strips ≥ 1 fused in: the tiles of
+// block row 0 and block column 0 of the trailing matrix (2·nt − 1 per
+// problem; with nt = 1 the whole last trailing block),
+//   tile (I, 0), I ≥ 1:  L21(I) = A21(I)·U11⁻¹ (→ K, threshold test), then
+//                        C(I, 0) −= L21(I)·U12(0);
+//   tile (0, J), J ≥ 1:  U12(J) = L11⁻¹·A12(J) (→ K), then
+//                        C(0, J) −= L21(0)·U12(J);
+//   tile (0, 0):         C(0, 0) −= L21(0)·U12(0),
+// where L21(0) / U12(0) come from the diagonal launch (diag_strip0).  Every
+// strip is computed once, by the tile that consumes it, so the panel is not
+// written and read back between a TRSM and an update launch.  L21(I) is
+// computed transposed, D = (U11⁻¹)ᵀ·A21(I)ᵀ, so that the MFMA result lands in
+// the A-operand layout of the update (lane (g, l16) holds L21[16w + l16]
+// [16ct + g + 4rr] = k-step 4ct + rr); U12(J) goes through LDS as the
+// update's B operand.  Wave w owns the tile's rows 16w..16w+15.  XCD-aware
+// order: one problem's tiles are consecutive.  The fused forward sweeps of
+// step c0 ride on tiles (0, J) (c −= c′U12) and (I, 0) (b −= L21 b′).
 // ---------------------------------------------------------------------------
-
-__global__ __launch_bounds__(256) void nlu_update_kernel(double* __restrict__ K, int ld, int nmax,
-                                                         const QPMeta* __restrict__ meta, int c0,
-                                                         int nrt, int nct, int total, double* __restrict__ w0,
-                                                         double* __restrict__ w1, int cross) {
-  __shared__ double U[NB64 * ULD];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_cross_kernel(
+    double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
+    int nt, int total, double* __restrict__ w0, double* __restrict__ w1) {
+  __shared__ double X[NB64 * TLD];
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
   const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
-  // cross = 1: only the tiles of block row 0 and block column 0 (2·nct − 1 per
-  // problem, nrt = nct) — the first half of a paired step (nlu_update2_kernel)
-  const int tiles = cross ? 2 * nct - 1 : nrt * nct;
+  const int tiles = 2 * nt - 1;
   const int b = logical / tiles;
   const int tile = logical - b * tiles;
-  const int rt = cross ? (tile < nct ? 0 : tile - nct + 1) : tile / nct;
-  const int ct = cross ? (tile < nct ? tile : 0) : tile - rt * nct;
+  const int I = tile < nt ? 0 : tile - nt + 1;   // row strip (L21, C rows)
+  const int J = tile < nt ? tile : 0;            // column strip (U12, C columns)
   const QPMeta mm = meta[b];
   const int Np = nlu_np(mm);
-  const int R2 = Np - c0 - NB64;               // trailing rows = columns (multiple of 32)
-  if (mm.lu == LU_REJECT || rt * 64 >= R2 || ct * 64 >= R2) return;   // workgroup-uniform
+  const int R2 = Np - c0 - NB64;                 // trailing rows = columns (multiple of 32)
+  if (mm.lu == LU_REJECT || I * 64 >= R2 || J * 64 >= R2) return;   // workgroup-uniform
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
   double* Kb = K + (size_t)b * nmax * ld;
-  const int cbase = c0 + NB64 + ct * 64;
-  const int cend = c0 + NB64 + R2;
+  const double* Bg = binv + (size_t)b * NB64 * NB64;
+  const int swI = min(64, R2 - 64 * I), swJ = min(64, R2 - 64 * J);   // 32 or 64
+  const int r0 = c0 + NB64 + 64 * I;   // first row of strip I
+  const int s0 = c0 + NB64 + 64 * J;   // first column of strip J
+  const int row = r0 + 16 * wv;        // this wave's first tile row
+  const bool wact = 16 * wv < swI;     // wave-uniform
+  const int nq = swJ >> 4;             // 16-column groups of the tile (2 or 4)
+  const int c8 = (t & 7) * 8;
+  const bool okJ = c8 < swJ;           // 32-aligned halves: all-or-nothing
+  // stage rows c0..c0+63, columns s0.. of K (A12(J), or U12(0)) as a B operand
+  auto stage = [&](const double* v) {
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    // stage U12[k][cbase .. cbase+63]: thread → (row k, 8 contiguous columns)
-    const int k = 32 * h + (t >> 3), c8 = (t & 7) * 8;
-    const bool ok = cbase + c8 < cend;   // 32-aligned halves: all-or-nothing
-    const double* src = Kb + (size_t)(c0 + k) * ld + (ok ? cbase + c8 : 0);
-    double v[8];
+    for (int h = 0; h < 2; ++h) {
+      const int k = 32 * h + (t >> 3);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = src[u];
+      for (int u = 0; u < 8; ++u) X[k * TLD + c8 + u] = okJ ? v[8 * h + u] : 0.0;
+    }
+  };
+  auto load_strip = [&](double* v) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) U[k * ULD + c8 + u] = ok ? v[u] : 0.0;
-  }
-  const int rbase = c0 + NB64 + rt * 64 + 16 * wv;
-  const bool wact = rt * 64 + 16 * wv < R2;   // wave-uniform
-  const int nq = min(4, (R2 - ct * 64) >> 4);
-  double a[NB64 / 4];
-  d4n acc[4];
-  if (wact) {
-    const double* arow = Kb + (size_t)(rbase + l16) * ld + c0;
+    for (int h = 0; h < 2; ++h) {
+      const double* src = Kb + (size_t)(c0 + 32 * h + (t >> 3)) * ld + (okJ ? s0 + c8 : 0);
 #pragma unroll
-    for (int s = 0; s < NB64 / 4; ++s) a[s] = -arow[4 * s + g];
+      for (int u = 0; u < 8; ++u) v[8 * h + u] = src[u];
+    }
+  };
+  double a[16];   // −L21 rows row + l16, k-step s: column 4s + g (the update's A operand)
+  if (I > 0) {
+    // L21(I), transposed through the MFMA: U11⁻¹ (upper, zero below) staged
+    double v[16], av[16], u[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = Bg[t + 256 * q];
+    if (wact) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) av[s] = Kb[(size_t)(row + l16) * ld + c0 + 4 * s + g];
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = t + 256 * q, k = e >> 6, c = e & 63;
+      X[k * TLD + c] = k <= c ? v[q] : 0.0;
+    }
+    __syncthreads();
+    load_strip(u);   // U12(0), for after the TRSM (in flight during it)
+    if (wact) {
+      int over = 0;
+      // column tiles in descending order: av[s] is dead after tile s / 4, so
+      // the A operand a[] grows as av[] shrinks
+#pragma unroll
+      for (int ct = 3; ct >= 0; --ct) {
+        d4n lt = {0, 0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < 4 * (ct + 1); ++s) lt = nmfma(X[(4 * s + g) * TLD + 16 * ct + l16], av[s], lt);
+        __builtin_amdgcn_sched_barrier(0);   // one column tile's LDS reads in flight at a time
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          Kb[(size_t)(row + l16) * ld + c0 + 16 * ct + g + 4 * rr] = lt[rr];
+          over |= !(fabs(lt[rr]) <= NOPIV_LMAX);
+          a[4 * ct + rr] = -lt[rr];
+        }
+      }
+      if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;   // every writer stores the same value
+    }
+    __syncthreads();   // every wave is done with U11⁻¹
+    stage(u);
+  } else if (J > 0) {
+    // U12(J) = L11⁻¹·A12(J): A12(J) staged, L11⁻¹ rows 16w + l16 as the A operand
+    double v[16], al[16];
+    load_strip(v);
+    const int ii = 16 * wv + l16;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = 4 * s + g;
+      const double bv = Bg[ii * NB64 + k];
+      al[s] = k == ii ? 1.0 : (k < ii ? bv : 0.0);
+    }
+    stage(v);
+    __syncthreads();
+    d4n um[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) um[q] = (d4n){0, 0, 0, 0};
+    const int ns = 4 * (wv + 1);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s < ns) {   // wave-uniform
+#pragma unroll
+        for (int q = 0; q < 4; ++q) um[q] = nmfma(al[s], X[(4 * s + g) * TLD + 16 * q + l16], um[q]);
+      }
+    }
+    if (wact) {   // L21(0) rows (diagonal launch)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) a[s] = -Kb[(size_t)(row + l16) * ld + c0 + 4 * s + g];
+    }
+    __syncthreads();   // every wave is done with A12(J)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int cq = cbase + 16 * min(q, nq - 1) + l16;
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) acc[q][rr] = Kb[(size_t)(rbase + g + 4 * rr) * ld + cq];
+      for (int rr = 0; rr < 4; ++rr) {
+        X[(16 * wv + g + 4 * rr) * TLD + 16 * q + l16] = um[q][rr];
+        if (16 * q < swJ) Kb[(size_t)(c0 + 16 * wv + g + 4 * rr) * ld + s0 + 16 * q + l16] = um[q][rr];
+      }
+    }
+  } else {
+    double u[16];
+    load_strip(u);   // U12(0)
+    if (wact) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) a[s] = -Kb[(size_t)(row + l16) * ld + c0 + 4 * s + g];
+    }
+    stage(u);
+  }
+  d4n acc[4];
+  if (wact) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int cq = s0 + 16 * min(q, nq - 1) + l16;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) acc[q][rr] = Kb[(size_t)(row + g + 4 * rr) * ld + cq];
     }
   }
-  __syncthreads();
-  if (w1 && rt == 0 && wv == 0) {   // fused forward sweep of Kᵀ: c_J −= c′ U12_J (a column per lane)
+  __syncthreads();   // the U12 tile is in X
+  if (w1 && I == 0 && wv == 0) {   // fused forward sweep of Kᵀ: c_J −= c′ U12(J) (a column per lane)
     const double* cp = w1 + (size_t)b * nmax + c0;   // c′ of this step (diagonal kernel)
     double cs = 0.0;
 #pragma unroll 8
-    for (int k = 0; k < NB64; ++k) cs = fma(cp[k], U[k * ULD + lane], cs);
-    if (lane < 16 * nq) w1[(size_t)b * nmax + cbase + lane] -= cs;
+    for (int k = 0; k < NB64; ++k) cs = fma(cp[k], X[k * TLD + lane], cs);
+    if (lane < 16 * nq) w1[(size_t)b * nmax + s0 + lane] -= cs;
   }
   if (!wact) return;
-  if (w0 && ct == 0) {   // fused forward sweep of K: b_I −= L21_I b′ (a = −L21)
+  if (w0 && J == 0) {   // fused forward sweep of K: b_I −= L21(I) b′ (a = −L21)
     const double* bp = w0 + (size_t)b * nmax + c0;
     double ps = 0.0;
 #pragma unroll
-    for (int s = 0; s < NB64 / 4; ++s) ps = fma(a[s], bp[4 * s + g], ps);
+    for (int s = 0; s < 16; ++s) ps = fma(a[s], bp[4 * s + g], ps);
     ps += __shfl_xor(ps, 16);
     ps += __shfl_xor(ps, 32);
-    if (g == 0) w0[(size_t)b * nmax + rbase + l16] += ps;
+    if (g == 0) w0[(size_t)b * nmax + row + l16] += ps;
   }
 #pragma unroll
-  for (int s = 0; s < NB64 / 4; ++s) {
+  for (int s = 0; s < 16; ++s) {
     double bq[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) bq[q] = U[(4 * s + g) * ULD + 16 * q + l16];
+    for (int q = 0; q < 4; ++q) bq[q] = X[(4 * s + g) * TLD + 16 * q + l16];
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = nmfma(a[s], bq[q], acc[q]);
   }
@@ -818,7 +983,7 @@ __global__ __launch_bounds__(256) void nlu_update_kernel(double* __restrict__ K,
   for (int q = 0; q < 4; ++q) {
     if (q < nq) {
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) Kb[(size_t)(rbase + g + 4 * rr) * ld + cbase + 16 * q + l16] = acc[q][rr];
+      for (int rr = 0; rr < 4; ++rr) Kb[(size_t)(row + g + 4 * rr) * ld + s0 + 16 * q + l16] = acc[q][rr];
     }
   }
 }
@@ -935,14 +1100,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 
 }  // namespace
 
-// No-pivot blocked LU of every ROUTE_BLOCKED problem: per 64-column block a
-// diagonal launch (B workgroups) and a TRSM launch; the trailing updates go
-// in pairs of steps (rank 64 per step measured slower): step c0 updates only its cross
-// band, step c0+64's diagonal block and TRSM follow, one rank-128 pass
-// updates the rest — a third less trailing-matrix traffic than one rank-64
-// pass per step.  Sized by h.blocked_npmax (the read-back of the metadata after the
-// assembly).  w0 / w1 (both or neither): the reverse / forward right-hand
-// sides, forward-swept in place along the way (fwd_block).
+// No-pivot blocked LU of every ROUTE_BLOCKED problem, by pairs of 64-column
+// block steps (rank 64 per step measured slower):
+//   step c0:     diagonal block + TRSM strip 0 (one launch), then the cross
+//                band with the other strips' TRSM fused in (nlu_cross_kernel);
+//   step c0+64:  diagonal block, TRSM (nlu_trsm_kernel), and one rank-128
+//                pass over the rest of the trailing matrix (nlu_update2_kernel)
+//                — a third less trailing-matrix traffic than one rank-64 pass
+//                per step.
+// A single remaining trailing block (R2 ≤ 64) is the cross launch with nt = 1.
+// Sized by h.blocked_npmax (the read-back of the metadata after the assembly).
+// w0 / w1 (both or neither): the reverse / forward right-hand sides,
+// forward-swept in place along the way (fwd_block).
 void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   const int npmax = h.blocked_npmax;
   if (npmax == 0) return;
@@ -957,40 +1126,41 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
     if (g > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
     return dim3((unsigned)g);
   };
-  auto diag = [&](int c0) {
-    hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv, dstride,
-                       meta, c0, binv, w0, w1);
+  auto diag = [&](int c0, bool strip0) {
+    if (strip0)
+      hipLaunchKernelGGL(nlu_diag_kernel<true>, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv, dstride,
+                         meta, c0, binv, w0, w1);
+    else
+      hipLaunchKernelGGL(nlu_diag_kernel<false>, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv,
+                         dstride, meta, c0, binv, w0, w1);
     DOPT_CHECK_HIP(hipGetLastError());
   };
-  auto trsm = [&](int c0, int nt) {
-    const long long tot = 2LL * nt * B;
-    hipLaunchKernelGGL(nlu_trsm_kernel, grid(tot), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0, binv, nt,
-                       (int)tot);
-    DOPT_CHECK_HIP(hipGetLastError());
-  };
-  auto update = [&](int c0, int nt, int cross) {
-    const long long tot = (cross ? 2LL * nt - 1 : (long long)nt * nt) * B;
-    hipLaunchKernelGGL(nlu_update_kernel, grid(tot), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0, nt, nt,
-                       (int)tot, w0, w1, cross);
+  auto cross = [&](int c0, int nt) {
+    const long long tot = (2LL * nt - 1) * B;
+    hipLaunchKernelGGL(nlu_cross_kernel, grid(tot), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0, binv, nt,
+                       (int)tot, w0, w1);
     DOPT_CHECK_HIP(hipGetLastError());
   };
   for (int c0 = 0; c0 < npmax;) {
-    diag(c0);
     const int R2 = npmax - c0 - NB64;
-    if (R2 <= 0) break;
+    if (R2 <= 0) {   // the last diagonal block
+      diag(c0, false);
+      break;
+    }
     const int nt = (R2 + 63) / 64;
-    trsm(c0, nt);
-    if (R2 <= NB64) {   // the last trailing block: one rank-64 step
-      update(c0, nt, 0);
+    diag(c0, true);
+    cross(c0, nt);
+    if (R2 <= NB64) {   // one trailing block: the cross launch was its whole update
       c0 += NB64;
       continue;
     }
-    // a paired step: cross band of step c0, step c0+64's diagonal block and
-    // TRSM, then both rank-64 updates of the rest in one pass
-    update(c0, nt, 1);
-    diag(c0 + NB64);
+    // step c0+64: diagonal block, TRSM, both rank-64 updates of the rest in one pass
+    diag(c0 + NB64, false);
     const int nt2 = (R2 - NB64 + 63) / 64;
-    trsm(c0 + NB64, nt2);
+    const long long tt = 2LL * nt2 * B;
+    hipLaunchKernelGGL(nlu_trsm_kernel, grid(tt), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0 + NB64, binv,
+                       nt2, (int)tt);
+    DOPT_CHECK_HIP(hipGetLastError());
     const long long tot = (long long)nt2 * nt2 * B;
     hipLaunchKernelGGL(nlu_update2_kernel, grid(tot), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0, nt2, nt2,
                        (int)tot, w0, w1);

@@ -35,7 +35,7 @@ KERNEL_PHASE = {
 # update sequence of one factorisation, the two solve kernels of one step);
 # summed over the dispatches and divided by the number of steps, counted by
 # the per-step qp_prep_asm_kernel dispatch
-QP_GROUPS = {"qp_lu": ("nlu_diag_kernel", "nlu_trsm_kernel", "nlu_update_kernel", "nlu_update2_kernel",
+QP_GROUPS = {"qp_lu": ("nlu_diag_kernel", "nlu_trsm_kernel", "nlu_cross_kernel", "nlu_update2_kernel",
                        "blu_panel_kernel", "blu_update_kernel"),
              "qp_solve": ("blu_solve_kernel", "blu_solve_rows_kernel", "blu_solve2_kernel")}
 QP_STEP = "qp_prep_asm_kernel"

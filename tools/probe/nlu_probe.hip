@@ -2,7 +2,7 @@
 // on a synthetic batch of diagonally dominant K slabs.
 //   hipcc --offload-arch=gfx950 -O3 -DNLU_STOP=k tools/probe/nlu_probe.hip -o nlu_k
 //   ./nlu_k B NP          → µs per launch of the first diagonal block and of
-//                           the TRSM / update at each c0 (same binv: timing only)
+//                           the diagonal+strip-0, TRSM and cross launches at each c0 (same binv: timing only)
 #include "../../diffopt.jl_amd/csrc/qp_nopiv.hip"
 #include <cstdio>
 #include <cstdlib>
@@ -61,25 +61,30 @@ int main(int argc, char** argv) {
     printf("NLU_STOP=%d B=%d Np=%d %-12s %9.2f us/launch\n", NLU_STOP, B, Np, nm, 1e3 * tot / reps);
   };
   timeit("diag", [&] {
-    hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
+    hipLaunchKernelGGL(nlu_diag_kernel<false>, dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
                        dinv_stride(nmax), meta, 0, binv, nullptr, nullptr);
   });
   if (NLU_STOP == 99) {
     // diag once more so binv holds this data's inverse for the step
-    hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, 0, K0, ld, nmax, perm, dinv,
+    hipLaunchKernelGGL(nlu_diag_kernel<false>, dim3(B), dim3(PNT), 0, 0, K0, ld, nmax, perm, dinv,
                        dinv_stride(nmax), meta, 0, binv, nullptr, nullptr);
     for (int c0 = 0; c0 + 64 < Np; c0 += 64) {
       const int nt = (Np - c0 - 64 + 63) / 64;
       char nm[32];
+      snprintf(nm, sizeof nm, "diag+s0 c0=%d", c0);
+      timeit(nm, [&] {
+        hipLaunchKernelGGL(nlu_diag_kernel<true>, dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
+                           dinv_stride(nmax), meta, c0, binv, nullptr, nullptr);
+      });
       snprintf(nm, sizeof nm, "trsm c0=%d", c0);
       timeit(nm, [&] {
         hipLaunchKernelGGL(nlu_trsm_kernel, dim3(2 * nt * B), dim3(256), 0, 0, K, ld, nmax, meta, c0, binv, nt,
                            2 * nt * B);
       });
-      snprintf(nm, sizeof nm, "update c0=%d", c0);
+      snprintf(nm, sizeof nm, "cross c0=%d", c0);
       timeit(nm, [&] {
-        hipLaunchKernelGGL(nlu_update_kernel, dim3(nt * nt * B), dim3(256), 0, 0, K, ld, nmax, meta, c0, nt, nt,
-                           nt * nt * B, nullptr, nullptr, 0);
+        hipLaunchKernelGGL(nlu_cross_kernel, dim3((2 * nt - 1) * B), dim3(256), 0, 0, K, ld, nmax, meta, c0, binv,
+                           nt, (2 * nt - 1) * B, nullptr, nullptr);
       });
     }
   }
@@ -89,7 +94,7 @@ int main(int argc, char** argv) {
     hipMemcpyToSymbol(HIP_SYMBOL(nlu_stamps), z, sizeof(z));
     hipMemcpy(K, K0, hK.size() * 8, hipMemcpyDeviceToDevice);
     hipMemcpy(meta, hm.data(), B * sizeof(QPMeta), hipMemcpyHostToDevice);
-    hipLaunchKernelGGL(nlu_diag_kernel, dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
+    hipLaunchKernelGGL(nlu_diag_kernel<false>, dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
                        dinv_stride(nmax), meta, 0, binv, nullptr, nullptr);
     hipDeviceSynchronize();
     hipMemcpyFromSymbol(st, HIP_SYMBOL(nlu_stamps), sizeof(st));
