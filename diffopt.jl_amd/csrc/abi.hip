@@ -112,6 +112,8 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
       h->ipiv.ensure((size_t)batch * std::max(h->nmax, 1) * sizeof(int32_t));
       h->s.ensure((size_t)batch * std::max(m, 1) * sizeof(double));
       h->kidx.ensure((size_t)2 * batch * std::max(m, 1) * sizeof(int32_t));
+      h->kls.ensure((size_t)2 * batch * std::max(m, 1) * sizeof(double));
+      h->gk.ensure((size_t)batch * std::max(n, 1) * std::max(m, 1) * sizeof(double));
       h->meta.ensure((size_t)std::max<int64_t>(batch, 1) * sizeof(dopt::QPMeta));
       // rhs: [reverse RHS | full forward RHS | reduced forward RHS]; x: [reverse | forward]
       h->rhs.ensure((size_t)3 * batch * std::max(h->nmax, 1) * sizeof(double));

@@ -60,10 +60,11 @@ struct QPMeta {
   int32_t iterative; // 1: LSQR branch (norm(Q) == 0)
   int32_t info;      // 0 ok, k>0 zero pivot at column k of the reduced system
   int32_t lu;        // QPLu: which factors K holds
-  int32_t pad[3];
+  int32_t gk_ok;     // assembly: the speculative G_k copy (kept = λ ≠ 0 rows) is the kept set
+  int32_t pad[2];
 };
 
-constexpr int ASM_THREADS = 512;     // prepare + assembly workgroup size (qp_assemble.hip)
+constexpr int ASM_WPP = 16;          // assembly tile workgroups per problem (qp_assemble.hip)
 constexpr int BLOCKED_MAX = 1536;    // largest reduced system of the blocked path
 
 // Which factorisation path a problem takes (decided per problem on the
@@ -108,6 +109,8 @@ struct Handle {
   DevBuf csc_in[9], csc_in_val[3], csc_err;   // host-mode copies of CSC colptr / rowval / nzval
   int32_t nmax = 0, ld = 0;  // max system size, K row stride (doubles)
   DevBuf K, ipiv, s, kidx, meta, rhs, x;
+  DevBuf kls;                // kept rows' λ_k and s_k, compacted (assembly tiles)
+  DevBuf gk;                 // kept rows of G, compacted column-major (n × m per problem; assembly tiles)
   DevBuf dinv;               // per-problem diagonal-block inverses (L11⁻¹ | U11⁻¹ per 32-block)
   DevBuf plist;              // problem indices of the partial-pivoting re-factorisation
   DevBuf lsqr_ws;            // LSQR vectors of the `iterative` branch (5 per problem)

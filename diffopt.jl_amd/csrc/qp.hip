@@ -685,10 +685,14 @@ void csc_to_dense(Handle& h, const int64_t* colptr, const int64_t* rowval, const
 static void check_launch() { DOPT_CHECK_HIP(hipGetLastError()); }
 
 // qp_assemble.hip
-__global__ void qp_prep_asm_kernel(QPIn, double*, int, int, double*, int32_t*, int32_t*, QPMeta*, int,
-                                   const int32_t*);
-int prep_asm_cap(int n, int m);
-size_t prep_asm_lds(int n, int cap);
+template <int RPT>
+__global__ void qp_prep_kernel(QPIn, double*, int32_t*, int32_t*, double*, double*, int64_t, QPMeta*,
+                               const int32_t*);
+__global__ void qp_asm_tile_kernel(QPIn, const int32_t*, const double*, const double*, int64_t, const QPMeta*, double*,
+                                   int, int, const int32_t*);
+int prep_rows_per_thread(int m);
+int prep_threads(int m);
+size_t prep_lds(int n);
 
 constexpr int ZCAP = 4096;   // z staged in LDS by the RHS / output kernels up to this n
 
@@ -715,15 +719,32 @@ static QPIn qp_inputs(Handle& h) {
 
 static int32_t* rpos_of(Handle& h) { return h.kidx.as<int32_t>() + (size_t)h.batch * h.m; }
 
-// prepare + assembly of `count` problems (plist: their indices; null = all)
-static void prep_assemble(Handle& h, const int32_t* plist, int count) {
+// prepare (s, kept rows, metadata) + assembly of `count` problems (plist:
+// their indices; null = all).  `after_prep` runs between the two launches
+// (the metadata read-back: it only needs the prepare kernel, so the host's
+// wait overlaps the tile kernel).
+template <class F>
+static void prep_assemble(Handle& h, const int32_t* plist, int count, F&& after_prep) {
   if (count == 0) return;
-  const int cap = prep_asm_cap(h.n, h.m);
-  hipLaunchKernelGGL(qp_prep_asm_kernel, dim3(count), dim3(ASM_THREADS), prep_asm_lds(h.n, cap), h.stream,
-                     qp_inputs(h), h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(), h.kidx.as<int32_t>(),
-                     rpos_of(h), h.meta.as<QPMeta>(), cap, plist);
+  const QPIn P = qp_inputs(h);
+  const dim3 pg(count), pb(prep_threads(h.m));
+  if (prep_rows_per_thread(h.m) == 2)
+    hipLaunchKernelGGL(qp_prep_kernel<2>, pg, pb, prep_lds(h.n), h.stream, P, h.s.as<double>(),
+                       h.kidx.as<int32_t>(), rpos_of(h), h.kls.as<double>(), h.gk.as<double>(), h.batch, h.meta.as<QPMeta>(),
+                       plist);
+  else
+    hipLaunchKernelGGL(qp_prep_kernel<1>, pg, pb, prep_lds(h.n), h.stream, P, h.s.as<double>(),
+                       h.kidx.as<int32_t>(), rpos_of(h), h.kls.as<double>(), h.gk.as<double>(), h.batch, h.meta.as<QPMeta>(),
+                       plist);
+  check_launch();
+  after_prep();
+  hipLaunchKernelGGL(qp_asm_tile_kernel, dim3((unsigned)count * ASM_WPP), dim3(512), 0, h.stream, P,
+                     h.kidx.as<int32_t>(), h.kls.as<double>(), h.gk.as<double>(), h.batch, h.meta.as<QPMeta>(),
+                     h.K.as<double>(), h.ld,
+                     h.nmax, plist);
   check_launch();
 }
+static void prep_assemble(Handle& h, const int32_t* plist, int count) { prep_assemble(h, plist, count, [] {}); }
 
 // Asynchronous read-back of the per-problem metadata into pinned memory; the
 // caller may queue independent kernels before waiting (meta_wait), so the
@@ -829,8 +850,7 @@ void qp_factor(Handle& h) {
   if (!h.set) throw Error(-1, "dopt_qp_factor: dopt_qp_set has not been called");
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
-    prep_assemble(h, nullptr, (int)h.batch);
-    meta_copy(h);
+    prep_assemble(h, nullptr, (int)h.batch, [&] { meta_copy(h); });
   }
   meta_sizes(h);
   factor_blocked(h, [] {}, nullptr, nullptr, qp_reasm(h));
@@ -1059,8 +1079,7 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
   const FwdTangents T = tangents(h, dQ, dq, dG, dh, dA, db);
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
-    prep_assemble(h, nullptr, (int)h.batch);
-    meta_copy(h);
+    prep_assemble(h, nullptr, (int)h.batch, [&] { meta_copy(h); });
   }
   rev_rhs(h, dl_dz);
   fwd_rhs(h, T);

@@ -1,69 +1,86 @@
-// QP prepare + KKT assembly (one 512-thread workgroup per problem).
+// QP prepare + KKT assembly, two launches.
 //
-//   prepare   branch flag `iterative = norm(Q) ≈ 0` (exact zero test), s = Gz − h in
-//             Julia's sparse mul! order (bit-exact with the oracle), the kept
-//             inequality rows (λ_i ≠ 0 or s_i == 0: exact elimination of the
-//             decoupled rows), per-problem metadata
-//   assemble  the reduced KKT  K = [Q, G_kᵀD(λ_k), Aᵀ; G_k, D(s_k), 0; A, 0, 0]
-//             row-major into the per-problem K slab, identity-padded to a
-//             multiple of 32; the G blocks of the rows with λ_i ≠ 0 are
-//             written during prepare from the registers that form s (one HBM
-//             read of G), a separate G pass only when a row with λ_i = 0 and
-//             s_i == 0 joins the kept set
+//   qp_prep_kernel       one workgroup per problem, two inequality rows per
+//                        thread (one 16-byte load per column): branch flag `iterative = norm(Q) ≈ 0` (exact
+//                        zero test), s = Gz − h in Julia's sparse mul! order
+//                        (bit-exact with the oracle), the kept rows (λ_i ≠ 0 or
+//                        s_i == 0: exact elimination of the decoupled rows, in
+//                        ascending order, with their λ_k / s_k compacted),
+//                        per-problem metadata.  Reads G once, PREP_U loads in
+//                        flight per thread, no K writes.
+//   qp_asm_tile_kernel   ASM_WPP workgroups per problem, each taking 64×64
+//                        tiles of the reduced KKT
+//                          K = [Q, G_kᵀD(λ_k), Aᵀ; G_k, D(s_k), 0; A, 0, 0]
+//                        (row-major, identity-padded to Np = round_up(N, 32))
+//                        in mirrored pairs (R, C) / (C, R): the pair reads the
+//                        same lines of G (the G_k row band and the G_kᵀΛ column
+//                        band), the second time from L2.  Columns c < n come
+//                        from column-major sources (Q, G_k, A rows): loaded with
+//                        the lanes along r and transposed through LDS; columns
+//                        c ≥ n (G_kᵀΛ, Aᵀ, the diagonal, the padding) are loaded
+//                        in place.  Both tiles of a pair are loaded before
+//                        either is stored (a wave's vmcnt counts stores and
+//                        loads in one order), stores are 16 bytes per lane.
+//
+// The single-workgroup-per-problem predecessor (prepare and tile loop in one
+// workgroup, G blocks written from the s-loop registers) measured 527 µs on
+// config 2, about half of it in each phase: each workgroup walked ~50 serial
+// rounds of loads with its stores interleaved.
 //
 // Reference: QuadraticProgram.jl create_LHS_matrix :256-282, `iterative`
 // :333/:436; the elimination is exact algebra.
 #include "dopt_internal.h"
 
-// tools/probe/asm_probe.hip builds this file with -DASM_STAMPS: per-phase
-// s_memtime cycles summed over workgroups into asm_stamps[] (thread 0)
-#ifdef ASM_STAMPS
-__device__ unsigned long long asm_stamps[8];
-#define ASM_MARK(k)                                                              \
-  do {                                                                          \
-    if (threadIdx.x == 0) {                                                     \
-      const unsigned long long now_ = __builtin_amdgcn_s_memtime();             \
-      atomicAdd(&asm_stamps[k], now_ - st_last_);                               \
-      st_last_ = now_;                                                          \
-    }                                                                           \
-  } while (0)
-#define ASM_MARK_INIT unsigned long long st_last_ = __builtin_amdgcn_s_memtime()
-#else
-#define ASM_MARK(k) do {} while (0)
-#define ASM_MARK_INIT do {} while (0)
-#endif
-
 namespace dopt {
 
-constexpr int FT = ASM_THREADS;    // threads per workgroup (8 waves)
-constexpr int NW = FT / 64;        // waves per workgroup
+constexpr int PREP_U = 16;    // G loads in flight per thread (s = Gz − h), one row per thread
+constexpr int PREP_U2 = 8;    // 16-byte G loads per buffer (two rows per thread, double-buffered)
+constexpr int PREP_MAXT = 256;    // rows beyond 2·256 (or 256) are taken in chunks
+constexpr int ZLDS_MAX = 8192;   // z staged in LDS up to this n
+constexpr int BUF_FLAGS = 0x00020000;   // raw buffer resource, word 3 (gfx9 family)
+
+typedef double dv2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32v2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32v4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ dv2 bload2(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, unsigned off, double x) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32v2, x), r, off, 0, 0);
+}
 
 // ---------------------------------------------------------------------------
-// s = Gz − h (Julia sparse-matvec order), branch flag, row classification.
-// While s is accumulated, the rows that are kept whatever s turns out to be
-// (λ_i ≠ 0, or every row in the `iterative` branch) are written into K from
-// the same registers: K row n+ci (G_k) and column n+ci (G_kᵀΛ), ci = the
-// row's rank among them — so G is read from HBM once.  Returns whether that
-// speculative set is the final kept set (no row with λ_i = 0 and s_i == 0);
-// if not, the caller rewrites the G blocks with the final positions.
-__device__ __forceinline__ int prepare_wg(const QPIn& P, int b, double* s_out, int32_t* kidx,
-                                          int32_t* rpos, QPMeta* meta, double* zs, int* cnt,
-                                          double* __restrict__ K, int ld, int* spec_ok) {
+// s = Gz − h (Julia sparse-matvec order), branch flag, kept rows, metadata.
+// RPT rows per thread: 2 (rows 2t, 2t+1 read as one 16-byte load; m even, so
+// every load is aligned) or 1.  blockDim.x = prep_threads(m) (a multiple of
+// 64, ≤ 1024); dynamic LDS: z (n doubles) when n ≤ ZLDS_MAX.  Besides kidx /
+// rpos the kept rows' λ_k and s_k are written compacted (kls: λ_k at
+// [b·m + ci], s_k at [(B + b)·m + ci]) for the tile kernel.
+template <int RPT>
+__global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* __restrict__ s_out,
+                                                            int32_t* __restrict__ kidx, int32_t* __restrict__ rpos,
+                                                            double* __restrict__ kls, double* __restrict__ gk,
+                                                            int64_t B, QPMeta* __restrict__ meta,
+                                                            const int32_t* __restrict__ plist) {
+  extern __shared__ __attribute__((aligned(16))) double zdyn[];
+  __shared__ int cnt[PREP_MAXT / 64 + 1], scnt[PREP_MAXT / 64 + 1];
+  __shared__ int extra;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int T = (int)blockDim.x, NW = T >> 6;
+  const int b = plist ? plist[blockIdx.x] : (int)blockIdx.x;
   const int n = P.n, m = P.m, p = P.p;
   const double* Qb = P.Q + (size_t)b * n * n;
   // branch flag: norm(Q) ≈ 0 ⇔ Q == 0 (exact zero test); batched loads with
   // a workgroup early exit once a nonzero is seen (dense QPs: first batch)
-  ASM_MARK_INIT;
   int iterative = 1;
   {
     const size_t nn = (size_t)n * n;
-    for (size_t i0 = 0; i0 < nn; i0 += (size_t)8 * FT) {
+    for (size_t i0 = 0; i0 < nn; i0 += (size_t)8 * T) {
       int nz = 0;
       double q[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const size_t i = i0 + (size_t)u * FT + t;
+        const size_t i = i0 + (size_t)u * T + t;
         q[u] = Qb[i < nn ? i : 0];
       }
 #pragma unroll
@@ -71,305 +88,321 @@ __device__ __forceinline__ int prepare_wg(const QPIn& P, int b, double* s_out, i
       if (__syncthreads_or(nz)) { iterative = 0; break; }
     }
   }
-  ASM_MARK(0);
-  for (int j = t; j < n; j += FT) zs[j] = P.z[(size_t)b * n + j];
+  const bool zl = n <= ZLDS_MAX;
+  if (zl)
+    for (int j = t; j < n; j += T) zdyn[j] = P.z[(size_t)b * n + j];
+  const double* zs = zl ? zdyn : P.z + (size_t)b * n;
   if (t == 0) {
     cnt[NW] = 0;
-    cnt[NW + 1] = 0;   // rows kept beyond the speculative set
+    scnt[NW] = 0;
+    extra = 0;
   }
   __syncthreads();
   const double* Gb = P.G + (size_t)b * m * n;
-  int spec_base = 0;   // speculative kept rows of the earlier chunks (uniform)
-  for (int i0 = 0; i0 < m; i0 += FT) {
-    const int i = i0 + t;
-    const double li = i < m ? P.lam[(size_t)b * m + i] : 0.0;
-    // speculative rank: a ballot prefix over this chunk + the rows before it
-    const int spec = i < m && (iterative || li != 0.0);
-    const unsigned long long sb = __ballot(spec);
-    if (lane == 0) cnt[wv] = __popcll(sb);
-    __syncthreads();
-    int ci = spec_base + __popcll(sb & ((1ull << lane) - 1ull)), chunk = 0;
-    for (int w = 0; w < NW; ++w) {
-      ci += w < wv ? cnt[w] : 0;
-      chunk += cnt[w];
+  double* gkb = gk + (size_t)b * n * m;
+  const double* lb = P.lam + (size_t)b * m;
+  const double* hb = P.h + (size_t)b * m;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int i0 = 0; i0 < m; i0 += RPT * T) {
+    const int i = i0 + RPT * t;
+    bool valid[RPT];
+    double acc[RPT], li[RPT];
+    int spec[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      valid[q] = i + q < m;
+      acc[q] = 0.0;
+      li[q] = valid[q] ? lb[i + q] : 0.0;
+      spec[q] = valid[q] && (iterative || li[q] != 0.0);
     }
-    spec_base += chunk;
-    __syncthreads();   // cnt[] is reused by the kept-row ballot below
-    int keep = 0;
-    if (i < m) {
-      double* krow = K + (size_t)(n + ci) * ld;   // K row n+ci: G_k
-      double* kcol = K + n + ci;                  // K column n+ci: G_kᵀΛ
-      double acc = 0.0;
+    // speculative rank among the rows kept whatever s turns out (λ ≠ 0, or
+    // every row in the iterative branch): their G rows are copied to gk
+    // (column-major, compacted) from the registers that form s
+    int sci[RPT];
+    {
+      int sbelow = 0, scount = 0;
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) {
+        const unsigned long long ball = __ballot(spec[q]);
+        sbelow += __popcll(ball & lt);
+        scount += __popcll(ball);
+      }
+      if (lane == 0) scnt[wv] = scount;
+      __syncthreads();
+      int soff = scnt[NW];
+      for (int w = 0; w < wv; ++w) soff += scnt[w];
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) sci[q] = soff + sbelow + (q ? spec[0] : 0);
+    }
+    {
+      const double* gp = Gb + (valid[RPT - 1] ? i : 0);
+      double* gw0 = gkb + sci[0];
       int j = 0;
-      constexpr int SCH = 8;   // columns per load batch (64 VGPRs: 8 waves per SIMD)
-      for (; j + SCH <= n; j += SCH) {
-        double gv[SCH];
+      if constexpr (RPT == 2) {
+        // buffer accesses with 32-bit offsets (few address registers); a
+        // non-speculative row's gk stores go to an out-of-range offset, which
+        // the buffer unit drops.  Double-buffered: the next PREP_U2 columns'
+        // loads are issued before this chunk's gk stores (vmcnt counts both
+        // in issue order).
+        const unsigned bytes = (unsigned)((size_t)n * m * sizeof(double));
+        const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(Gb), 0, bytes, BUF_FLAGS);
+        const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(gkb, 0, bytes, BUF_FLAGS);
+        const unsigned mb = (unsigned)m * 8u, lo = (unsigned)(valid[1] ? i : 0) * 8u;
+        const unsigned so0 = spec[0] ? (unsigned)sci[0] * 8u : 0x80000000u;
+        const unsigned so1 = spec[1] ? (unsigned)sci[1] * 8u : 0x80000000u;
+        dv2 cur[PREP_U2], nxt[PREP_U2];
+        if (PREP_U2 <= n) {
 #pragma unroll
-        for (int u = 0; u < SCH; ++u) gv[u] = Gb[i + (size_t)(j + u) * m];
+          for (int u = 0; u < PREP_U2; ++u) cur[u] = bload2(gr, lo + (unsigned)u * mb);
+        }
+        for (; j + PREP_U2 <= n; j += PREP_U2) {
+          const bool more = j + 2 * PREP_U2 <= n;
+          if (more) {
 #pragma unroll
-        for (int u = 0; u < SCH; ++u) acc = __dadd_rn(acc, __dmul_rn(gv[u], zs[j + u]));
-        if (spec) {
+            for (int u = 0; u < PREP_U2; ++u) nxt[u] = bload2(gr, lo + (unsigned)(j + PREP_U2 + u) * mb);
+          }
 #pragma unroll
-          for (int u = 0; u < SCH; u += 2) *reinterpret_cast<double2*>(krow + j + u) = make_double2(gv[u], gv[u + 1]);
+          for (int u = 0; u < PREP_U2; ++u) {
+            acc[0] = __dadd_rn(acc[0], __dmul_rn(cur[u].x, zs[j + u]));
+            acc[1] = __dadd_rn(acc[1], __dmul_rn(cur[u].y, zs[j + u]));
+            bstore1(wr, so0 + (unsigned)(j + u) * mb, cur[u].x);
+            bstore1(wr, so1 + (unsigned)(j + u) * mb, cur[u].y);
+          }
+          if (more) {
 #pragma unroll
-          for (int u = 0; u < SCH; ++u) kcol[(size_t)(j + u) * ld] = gv[u] * li;
+            for (int u = 0; u < PREP_U2; ++u) cur[u] = nxt[u];
+          }
+        }
+        for (; j < n; ++j) {
+          const dv2 g2 = bload2(gr, lo + (unsigned)j * mb);
+          acc[0] = __dadd_rn(acc[0], __dmul_rn(g2.x, zs[j]));
+          acc[1] = __dadd_rn(acc[1], __dmul_rn(g2.y, zs[j]));
+          bstore1(wr, so0 + (unsigned)j * mb, g2.x);
+          bstore1(wr, so1 + (unsigned)j * mb, g2.y);
+        }
+      } else {
+        for (; j + PREP_U <= n; j += PREP_U) {
+          double gv[PREP_U];
+#pragma unroll
+          for (int u = 0; u < PREP_U; ++u) gv[u] = gp[(size_t)(j + u) * m];
+#pragma unroll
+          for (int u = 0; u < PREP_U; ++u) {
+            acc[0] = __dadd_rn(acc[0], __dmul_rn(gv[u], zs[j + u]));
+            if (spec[0]) gw0[(size_t)(j + u) * m] = gv[u];
+          }
+        }
+        for (; j < n; ++j) {
+          const double g = gp[(size_t)j * m];
+          acc[0] = __dadd_rn(acc[0], __dmul_rn(g, zs[j]));
+          if (spec[0]) gw0[(size_t)j * m] = g;
         }
       }
-      for (; j < n; ++j) {
-        const double g = Gb[i + (size_t)j * m];
-        acc = __dadd_rn(acc, __dmul_rn(g, zs[j]));
-        if (spec) {
-          krow[j] = g;
-          kcol[(size_t)j * ld] = g * li;
-        }
-      }
-      const double si = __dsub_rn(acc, P.h[(size_t)b * m + i]);
-      s_out[(size_t)b * m + i] = si;
-      keep = iterative ? 1 : !(li == 0.0 && si != 0.0);
-      if (keep && !spec) atomicAdd(&cnt[NW + 1], 1);
     }
-    const unsigned long long ball = __ballot(keep);
-    const int prefix = __popcll(ball & ((1ull << lane) - 1ull));
-    if (lane == 0) cnt[wv] = __popcll(ball);
+    int keep[RPT];
+    double si[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      keep[q] = 0;
+      si[q] = 0.0;
+      if (valid[q]) {
+        si[q] = __dsub_rn(acc[q], hb[i + q]);
+        s_out[(size_t)b * m + i + q] = si[q];
+        keep[q] = iterative ? 1 : !(li[q] == 0.0 && si[q] != 0.0);
+        if (keep[q] && !spec[q]) atomicAdd(&extra, 1);
+      }
+    }
+    // ascending compaction of the kept rows: ballot prefixes within the wave
+    // (row i before row i+1 of the same lane), the per-wave counts across the
+    // workgroup, the running total across chunks
+    int prefix[RPT], wcount = 0, below = 0;
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const unsigned long long ball = __ballot(keep[q]);
+      below += __popcll(ball & lt);
+      wcount += __popcll(ball);
+    }
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) prefix[q] = below + (q ? keep[0] : 0);
+    if (lane == 0) cnt[wv] = wcount;
     __syncthreads();
     int off = cnt[NW];
     for (int w = 0; w < wv; ++w) off += cnt[w];
-    if (i < m) {
-      if (keep) kidx[(size_t)b * m + off + prefix] = i;
-      rpos[(size_t)b * m + i] = keep ? off + prefix : -1;
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      if (valid[q]) {
+        const int ci = off + prefix[q];
+        if (keep[q]) {
+          kidx[(size_t)b * m + ci] = i + q;
+          kls[(size_t)b * m + ci] = li[q];
+          kls[((size_t)B + b) * m + ci] = si[q];
+        }
+        rpos[(size_t)b * m + i + q] = keep[q] ? ci : -1;
+      }
     }
     __syncthreads();
     if (t == 0) {
-      int sum = 0;
-      for (int w = 0; w < NW; ++w) sum += cnt[w];
+      int sum = 0, ssum = 0;
+      for (int w = 0; w < NW; ++w) {
+        sum += cnt[w];
+        ssum += scnt[w];
+      }
       cnt[NW] += sum;
+      scnt[NW] += ssum;
     }
     __syncthreads();
   }
-  const int nk = cnt[NW];
-  *spec_ok = cnt[NW + 1] == 0;
-  ASM_MARK(1);
   if (t == 0) {
+    const int nk = cnt[NW];
     meta[b].nk = nk;
     meta[b].nsys = n + nk + p;
     meta[b].iterative = iterative;
     meta[b].info = 0;
     meta[b].lu = LU_NONE;
+    meta[b].gk_ok = extra == 0;
   }
-  __syncthreads();
-  return iterative;
 }
+template __global__ void qp_prep_kernel<1>(QPIn, double*, int32_t*, int32_t*, double*, double*, int64_t, QPMeta*,
+                                           const int32_t*);
+template __global__ void qp_prep_kernel<2>(QPIn, double*, int32_t*, int32_t*, double*, double*, int64_t, QPMeta*,
+                                           const int32_t*);
 
-// K (row-major, stride ld) = [Q, G_kᵀD(λ_k), Aᵀ; G_k, D(s_k), 0; A, 0, 0],
-// identity-padded to Np = round_up(N, 32).  16×16 tiles owned by waves (no
-// workgroup barriers inside the tile loop); column-major sources (c < n) are
-// transposed through a wave-private LDS tile.  Every global load is
-// unconditional (a select picks the source address, out-of-block elements
-// read a dummy and are discarded), so a tile's loads are in flight together.
-// kidx, λ_k and s_k are staged in the dynamic LDS (`kid`, `lamk`, `sk`, `cap`
-// entries); kept sets larger than `cap` are gathered from global memory
-// instead (`tiles` = one 16×17 transpose tile per wave).  The G_k blocks are
-// written by a separate G pass (64 kept rows × 64 columns of G per step).
-constexpr int GP_R = 64, GP_C = 64, GP_LD = GP_C + 1;
+int prep_rows_per_thread(int m) { return (m % 2 == 0) ? 2 : 1; }
+int prep_threads(int m) {
+  const int rows = (m + prep_rows_per_thread(m) - 1) / prep_rows_per_thread(m);
+  return std::min(PREP_MAXT, std::max(64, (rows + 63) & ~63));
+}
+size_t prep_lds(int n) { return n <= ZLDS_MAX ? (size_t)std::max(n, 1) * sizeof(double) : 0; }
 
-__device__ __forceinline__ void assemble_rows(const QPIn& P, int b, const double* s,
-                                              const int32_t* kidx, int nk, double* K, int ld,
-                                              int* kid_l, double* lamk_l, double* sk_l, int cap,
-                                              double (*tiles)[16 * 17], double* gtile, bool g_done) {
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+// ---------------------------------------------------------------------------
+// Reduced-KKT tiles.  Grid: ASM_WPP workgroups per problem (blockIdx.x =
+// slot·ASM_WPP + g), ATH threads; workgroup g takes the tile pairs q = g,
+// g + ASM_WPP, … of the upper triangle of the problem's TT×TT tile grid.
+// Per pair: the kept rows' (index, λ, s) of both tile ranges staged in LDS;
+// every load of both tiles issued (column-major sources transposed into the
+// LDS tiles, the rest written in place); one barrier; 16-byte row stores.
+constexpr int AT = 64, ATLD = AT + 2, ATH = 512;
+constexpr int AK1 = AT * AT / ATH;   // elements per thread per tile (8)
+
+__global__ __launch_bounds__(ATH) void qp_asm_tile_kernel(QPIn P, const int32_t* __restrict__ kidx,
+                                                          const double* __restrict__ kls,
+                                                          const double* __restrict__ gk, int64_t B,
+                                                          const QPMeta* __restrict__ meta, double* __restrict__ Kper,
+                                                          int ld, int nmax, const int32_t* __restrict__ plist) {
+  __shared__ __attribute__((aligned(16))) double Ts[2][AT * ATLD];
+  __shared__ int kid_s[2][AT];
+  __shared__ double lam_s[2][AT], s_s[2][AT];
+  const int t = threadIdx.x;
+  const int slot = (int)blockIdx.x / ASM_WPP, g = (int)blockIdx.x % ASM_WPP;
+  const int b = plist ? plist[slot] : slot;
   const int n = P.n, m = P.m, p = P.p;
-  const int N = n + nk + p;
+  const int nk = meta[b].nk;
+  const bool gk_ok = meta[b].gk_ok != 0;
+  const int N = n + nk + p, Np = (N + 31) & ~31, TT = (Np + AT - 1) / AT;
+  const int npairs = TT * (TT + 1) / 2;
+  if (g >= npairs) return;
+  double* K = Kper + (size_t)b * nmax * ld;
   const double* Qb = P.Q + (size_t)b * n * n;
   const double* Gb = P.G + (size_t)b * m * n;
   const double* Ab = P.A + (size_t)b * p * n;
-  const double* lb = P.lam + (size_t)b * m;
-  const double* sb = s + (size_t)b * m;
   const int32_t* kb = kidx + (size_t)b * m;
-  ASM_MARK_INIT;
-  const bool staged = nk <= cap;
-  if (staged) {
-    for (int i = t; i < nk; i += (int)blockDim.x) {
-      const int k = kb[i];
-      kid_l[i] = k;
-      lamk_l[i] = lb[k];
-      sk_l[i] = sb[k];
-    }
-  }
-  __syncthreads();
-  const int* kid = staged ? kid_l : kb;
-  double* tl = tiles[wv];
-  const int NWB = (int)blockDim.x >> 6;
-  const int Np = (N + 31) & ~31;
-  const int T = Np >> 4;
-  const int lr = lane & 15, lg = lane >> 4;
-  // ASM_U tiles per wave per iteration: every tile's global loads are issued
-  // before the first transpose, so a wave keeps 8·ASM_U loads in flight
-  constexpr int ASM_U = 2;
-  auto tile_loads = [&](int tile, double* vt, double* vd) {
-    const int r0 = (tile / T) * 16, c0 = (tile % T) * 16;
-    if (c0 < n) {   // transpose source: lane reads source row r0+lr, columns c0+lg+4q
-      const int r = r0 + lr;
-      const double* base;
-      size_t cstride;
-      if (r < n) { base = Qb + r; cstride = n; }
-      else if (r < n + nk) { base = Qb; cstride = 0; }   // G_k rows: written by the G pass below
-      else if (r < N) { base = Ab + (r - n - nk); cstride = p; }
-      else { base = Qb; cstride = 0; }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c = c0 + lg + 4 * q;
-        const bool ok = r < N && c < n;
-        vt[q] = base[(size_t)(ok ? c : 0) * cstride];
-        vt[q] = ok ? vt[q] : 0.0;
-      }
-    }
-    // direct source: lane writes K rows r0+lg+4q, column c0+lr
-    const int c = c0 + lr;
-    const bool cA = c >= n + nk && c < N;
-    const double* cbase = cA ? Ab + (c - n - nk) : Qb;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = r0 + lg + 4 * q;
-      const bool ld_ok = r < n && cA;
-      vd[q] = cbase[(size_t)(ld_ok ? r : 0) * (cA ? (size_t)p : 0)];
-    }
-  };
-  auto tile_store = [&](int tile, const double* vt, const double* vd) {
-    const int r0 = (tile / T) * 16, c0 = (tile % T) * 16;
+  const double* lkb = kls + (size_t)b * m;
+  const double* skb = kls + ((size_t)B + b) * m;
+  // G_k row ci: the compacted copy (contiguous over ci, stride m per column)
+  // when the speculative set is the kept set, else row kid[ci] of G
+  const double* gkb = gk + (size_t)b * n * m;
+  auto grow = [&](int rng, int e, int ci) { return gk_ok ? gkb + ci : Gb + kid_s[rng][e]; };
+  // transposed-load mapping (columns c < n): lane ↔ row, 8 columns per thread
+  const int tr = t & 63, tc = t >> 6;
+  // direct mapping (columns c ≥ n): lane ↔ column, 8 rows per thread
+  const int scol = t & 63, srow = t >> 6;
+
+  // tile at (r0, c0) into Ts[slot]; rng_r / rng_c: the staged index ranges
+  // holding rows r0.. / columns c0..
+  auto tile_load = [&](int r0, int c0, int rng_r, int rng_c, double* Tl) {
     if (c0 < n) {
+      const int r = r0 + tr;
+      const double* base = Qb;
+      size_t cs = 0;
+      bool live = true;
+      if (r < n) { base = Qb + r; cs = n; }
+      else if (r < n + nk) { base = grow(rng_r, tr, r - n); cs = m; }
+      else if (r < N) { base = Ab + (r - n - nk); cs = p; }
+      else live = false;
+      double w[AK1];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) tl[(lg + 4 * q) * 17 + lr] = vt[q];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    const int c = c0 + lr;
-    const bool cG = c >= n && c < n + nk, cA = c >= n + nk && c < N;
-    const int ci = cG ? c - n : 0;
-    double v[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = r0 + lg + 4 * q;
-      const bool ld_ok = r < n && cA;
-      double val;
-      if (c < n) val = tl[lr * 17 + lg + 4 * q];
-      else if (ld_ok) val = vd[q];
-      else if (r == c) {
-        const int ki = max(r - n, 0);
-        val = (r >= N) ? 1.0 : ((r >= n && r < n + nk) ? (staged ? sk_l[ki] : sb[kid[ki]]) : 0.0);
+      for (int k = 0; k < AK1; ++k) {
+        const int c = c0 + tc + 8 * k;
+        w[k] = base[(size_t)((live && c < n) ? c : 0) * cs];
       }
-      else val = 0.0;
-      v[q] = val;
-    }
-    (void)ci;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = r0 + lg + 4 * q;
-      if (!((r < n && cG) || (r >= n && r < n + nk && c < n)))
-        K[(size_t)r * ld + c] = v[q];
-    }
-    __builtin_amdgcn_wave_barrier();   // the transpose tile is reused by the next tile
-  };
-  ASM_MARK(2);
-  // tiles wholly inside the G_k row band or the G_kᵀΛ column band hold
-  // nothing the tile loop writes: they are skipped (wave-uniform)
-  auto live = [&](int tile) {
-    if (tile >= T * T) return false;
-    const int r0 = (tile / T) * 16, c0 = (tile % T) * 16;
-    const bool rG = r0 >= n && r0 + 16 <= n + nk, cQ = c0 + 16 <= n;
-    const bool rQ = r0 + 16 <= n, cG = c0 >= n && c0 + 16 <= n + nk;
-    return !((rG && cQ) || (rQ && cG));
-  };
-  for (int tile0 = wv; tile0 < T * T; tile0 += NWB * ASM_U) {
-    double vt[ASM_U][4], vd[ASM_U][4];
-#pragma unroll
-    for (int u = 0; u < ASM_U; ++u)
-      if (live(tile0 + u * NWB)) tile_loads(tile0 + u * NWB, vt[u], vd[u]);
-#pragma unroll
-    for (int u = 0; u < ASM_U; ++u)
-      if (live(tile0 + u * NWB)) tile_store(tile0 + u * NWB, vt[u], vd[u]);
-  }
-  {
-    __syncthreads();   // the G-pass tile aliases the transpose tiles
-    ASM_MARK(3);
-    // G pass: 64 kept rows × 64 columns per step.  Wave w loads columns
-    // j0 + w + 8u (u < 8) of the 64 kept rows (lane ↔ kept row: sorted row
-    // indices, so a wave's loads cover the same lines a dense sweep would),
-    // writes G_kᵀΛ straight out (K row j, 64 consecutive columns n + ci) and
-    // stages the values in LDS; then the block writes the G_k rows out as
-    // 64-column (512 B) contiguous segments.
-    const int NT = (int)blockDim.x;
-    for (int ci0 = 0; ci0 < (g_done ? 0 : nk); ci0 += GP_R) {
-      const int ci = ci0 + lane;
-      const bool rok = ci < nk;
-      const int gi = rok ? kid[ci] : 0;
-      const double li = rok ? (staged ? lamk_l[ci] : lb[gi]) : 0.0;
-      for (int j0 = 0; j0 < n; j0 += GP_C) {
-        double gv[GP_C / 8];
-#pragma unroll
-        for (int u = 0; u < GP_C / 8; ++u) {
-          const int j = j0 + wv + 8 * u;
-          gv[u] = Gb[gi + (size_t)min(j, n - 1) * m];
-        }
-#pragma unroll
-        for (int u = 0; u < GP_C / 8; ++u) {
-          const int j = j0 + wv + 8 * u;
-          if (rok && j < n) K[(size_t)j * ld + n + ci] = gv[u] * li;
-          gtile[lane * GP_LD + wv + 8 * u] = gv[u];
-        }
-        __syncthreads();
-        for (int e = t; e < GP_R * GP_C; e += NT) {
-          const int rr = e / GP_C, cc = e - rr * GP_C;
-          if (ci0 + rr < nk && j0 + cc < n)
-            K[(size_t)(n + ci0 + rr) * ld + j0 + cc] = gtile[rr * GP_LD + cc];
-        }
-        __syncthreads();
+      for (int k = 0; k < AK1; ++k) {
+        const int c = c0 + tc + 8 * k;
+        if (c < n) Tl[tr * ATLD + tc + 8 * k] = live ? w[k] : 0.0;
       }
     }
+    const int c = c0 + scol;
+    if (c >= n) {
+      // rows r < n: G_kᵀΛ (scaled), Aᵀ or nothing; rows r ≥ n: the diagonal
+      // s_k, 0 (A rows) or 1 (padding)
+      const double* base = Qb;
+      size_t rs = 0;
+      double li = 1.0, dval = 1.0;
+      bool cok = true, gcol = false;
+      if (c < n + nk) {
+        base = grow(rng_c, scol, c - n); rs = m; li = lam_s[rng_c][scol]; gcol = true;
+        dval = s_s[rng_c][scol];
+      } else if (c < N) {
+        base = Ab + (c - n - nk); rs = p; dval = 0.0;
+      } else {
+        cok = false;
+      }
+      double v[AK1];
+#pragma unroll
+      for (int k = 0; k < AK1; ++k) {
+        const int r = r0 + srow + 8 * k;
+        v[k] = base[(size_t)((cok && r < n) ? r : 0) * rs];
+      }
+#pragma unroll
+      for (int k = 0; k < AK1; ++k) {
+        const int r = r0 + srow + 8 * k;
+        Tl[(srow + 8 * k) * ATLD + scol] = r < n ? (cok ? (gcol ? v[k] * li : v[k]) : 0.0) : (r == c ? dval : 0.0);
+      }
+    }
+  };
+  auto tile_store = [&](int r0, int c0, const double* Tl) {
+    const int cp = 2 * (t & 31), rw = t >> 5;
+    if (c0 + cp >= Np) return;
+#pragma unroll
+    for (int k = 0; k < AT / 16; ++k) {
+      const int rr = rw + 16 * k, r = r0 + rr;
+      if (r < Np)
+        *reinterpret_cast<double2*>(K + (size_t)r * ld + c0 + cp) =
+            *reinterpret_cast<const double2*>(Tl + rr * ATLD + cp);
+    }
+  };
+
+  for (int q = g; q < npairs; q += ASM_WPP) {
+    int R = 0, rem = q;
+    while (rem >= TT - R) { rem -= TT - R; ++R; }
+    const int C = R + rem;
+    // stage the kept rows' index / λ / s for positions R·64.. and C·64..
+    if (t < 2 * AT) {
+      const int which = t >> 6, e = t & 63;
+      const int ci = (which ? C : R) * AT + e - n;
+      const bool ok = ci >= 0 && ci < nk;
+      kid_s[which][e] = ok ? kb[ci] : 0;
+      lam_s[which][e] = ok ? lkb[ci] : 0.0;
+      s_s[which][e] = ok ? skb[ci] : 0.0;
+    }
+    __syncthreads();
+    tile_load(R * AT, C * AT, 0, 1, Ts[0]);
+    if (R != C) tile_load(C * AT, R * AT, 1, 0, Ts[1]);
+    __syncthreads();
+    tile_store(R * AT, C * AT, Ts[0]);
+    if (R != C) tile_store(C * AT, R * AT, Ts[1]);
+    __syncthreads();   // Ts and the staged ranges are reused by the next pair
   }
-  __syncthreads();
-  ASM_MARK(4);
 }
-
-// Prepare + assembly, one 512-thread workgroup per problem with a slim LDS
-// footprint (z, the kept-row staging, the transpose tiles), so several
-// problems share a CU.  `plist` (optional) maps blockIdx.x to the problem
-// index (re-assembly of the problems whose no-pivot LU was rejected).
-__global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(8))) void qp_prep_asm_kernel(
-    QPIn P, double* __restrict__ Kper, int ld_per, int nmax, double* __restrict__ s,
-    int32_t* __restrict__ kidx, int32_t* __restrict__ rpos, QPMeta* __restrict__ meta, int cap,
-    const int32_t* __restrict__ plist) {
-  // the transpose tiles (tile loop) and the G-pass tile are never live together
-  __shared__ double tbuf[GP_R * GP_LD > NW * 16 * 17 ? GP_R * GP_LD : NW * 16 * 17];
-  double (*tiles)[16 * 17] = reinterpret_cast<double (*)[16 * 17]>(tbuf);
-  double* gtile = tbuf;
-  __shared__ int cnt[NW + 2];
-  __shared__ int spec_ok;
-  extern __shared__ __attribute__((aligned(16))) double dyn[];
-  double* zsm = dyn;                           // n
-  double* lamk = zsm + P.n;                    // cap
-  double* sk = lamk + cap;                     // cap
-  int* kid = (int*)(sk + cap);                 // cap
-  const int b = plist ? plist[blockIdx.x] : (int)blockIdx.x;
-  double* Kb = Kper + (size_t)b * nmax * ld_per;
-  prepare_wg(P, b, s, kidx, rpos, meta, zsm, cnt, Kb, ld_per, &spec_ok);
-  const int nk = meta[b].nk;
-  assemble_rows(P, b, s, kidx, nk, Kb, ld_per, kid, lamk, sk, cap, tiles, gtile, spec_ok != 0);
-}
-
-// kept-row staging capacity of qp_prep_asm_kernel: all of m while static +
-// dynamic LDS stay within 40 KB (4 workgroups per CU, so a 1024-problem batch
-// is one dispatch round), else what fits there (a larger kept set is gathered
-// from global memory); at least 64 rows, then up to 64 KB of dynamic LDS.
-constexpr int ASM_STATIC_LDS = ((int)(sizeof(double) * (GP_R * GP_LD > NW * 16 * 17 ? GP_R * GP_LD : NW * 16 * 17) +
-                                      sizeof(int) * (NW + 3)) + 511) & ~511;
-int prep_asm_cap(int n, int m) {
-  const int dyn4 = (40 * 1024 - ASM_STATIC_LDS - std::max(n, 1) * 8) / 20;
-  if (dyn4 >= std::min(m, 64)) return std::max(0, std::min(m, dyn4));
-  const int avail = (64 * 1024 - std::max(n, 1) * 8) / 20;
-  return std::max(0, std::min(m, avail));
-}
-size_t prep_asm_lds(int n, int cap) { return (size_t)std::max(n, 1) * 8 + (size_t)cap * 20; }
 
 size_t dinv_stride(int nmax) { return (size_t)((nmax + 31) / 32) * 2 * 32 * 32; }
 

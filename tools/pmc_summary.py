@@ -29,16 +29,16 @@ KERNEL_PHASE = {
     "conic_lsqr2_kernel": "conic_lsqr",     # co-iterated forward + reverse (one launch per call)
     "conic_cone_kernel": "conic_cone",
     "conic_split_pass_kernel": "conic_split_pass",
-    "qp_prep_asm_kernel": "qp_assemble",
 }
 # blocked QP route: one bench phase = several launches (the panel / trailing-
 # update sequence of one factorisation, the two solve kernels of one step);
 # summed over the dispatches and divided by the number of steps, counted by
-# the per-step qp_prep_asm_kernel dispatch
-QP_GROUPS = {"qp_lu": ("nlu_diag_kernel", "nlu_trsm_kernel", "nlu_cross_kernel", "nlu_update2_kernel",
+# the per-step qp_prep_kernel dispatch
+QP_GROUPS = {"qp_assemble": ("qp_prep_kernel", "qp_asm_tile_kernel"),
+             "qp_lu": ("nlu_diag_kernel", "nlu_trsm_kernel", "nlu_cross_kernel", "nlu_update2_kernel",
                        "blu_panel_kernel", "blu_update_kernel"),
              "qp_solve": ("blu_solve_kernel", "blu_solve_rows_kernel", "blu_solve2_kernel")}
-QP_STEP = "qp_prep_asm_kernel"
+QP_STEP = "qp_prep_kernel"
 # NLP back-end (bench config 6): the step is counted by the assembly; its LU
 # is the partial-pivoting blocked LU, its solves the blocked solve kernels
 NLP_GROUPS = {"qp_assemble": ("nlp_assemble_kernel",),

@@ -1,6 +1,6 @@
-// Probe: per-phase cycles of qp_prep_asm_kernel (qp_assemble.hip compiled in
-// with -DASM_STAMPS) on a synthetic config-2-shaped batch.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DASM_STAMPS tools/probe/asm_probe.hip -o asm_st
+// Probe: times qp_prep_kernel and qp_asm_tile_kernel (qp_assemble.hip compiled
+// in) on a synthetic config-2-shaped batch.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probe/asm_probe.hip -o asm_st
 //   ./asm_st B n m phi
 #include "../../diffopt.jl_amd/csrc/qp_assemble.hip"
 #include <cstdio>
@@ -27,35 +27,40 @@ int main(int argc, char** argv) {
   P.Q = up(Q); P.G = up(G); P.h = up(h); P.z = up(z); P.lam = up(lam);
   double dummy = 0; double* dd; hipMalloc(&dd, 64); hipMemcpy(dd, &dummy, 8, hipMemcpyHostToDevice);
   P.A = dd; P.nu = dd; P.n = n; P.m = m; P.p = p;
-  const int nmax = (n + m + p + 31) / 32 * 32, ld = nmax;
+  const int ldpad = argc > 5 ? atoi(argv[5]) : 0;
+  const int nmax = (n + m + p + 31) / 32 * 32, ld = nmax + ldpad;
   double *K, *s; int32_t *kidx, *rpos; QPMeta* meta;
   hipMalloc(&K, (size_t)B * nmax * ld * 8);
   hipMalloc(&s, (size_t)B * m * 8);
   hipMalloc(&kidx, (size_t)B * m * 4);
   hipMalloc(&rpos, (size_t)B * m * 4);
   hipMalloc(&meta, (size_t)B * sizeof(QPMeta));
-  const int cap = prep_asm_cap(n, m);
-  const size_t lds = prep_asm_lds(n, cap);
-  hipEvent_t e0, e1;
-  hipEventCreate(&e0); hipEventCreate(&e1);
-  float tot = 0;
+  double *kls, *gkb;
+  hipMalloc(&gkb, (size_t)B * n * m * 8);
+  hipMalloc(&kls, (size_t)2 * B * m * 8);
+  hipEvent_t e0, e1, e2;
+  hipEventCreate(&e0); hipEventCreate(&e1); hipEventCreate(&e2);
+  float t1 = 0, t2 = 0;
   for (int r = 0; r <= 5; ++r) {
-    unsigned long long zz[8] = {0};
-    hipMemcpyToSymbol(HIP_SYMBOL(asm_stamps), zz, sizeof(zz));
     hipEventRecord(e0);
-    hipLaunchKernelGGL(qp_prep_asm_kernel, dim3(B), dim3(ASM_THREADS), lds, 0, P, K, ld, nmax, s, kidx, rpos, meta,
-                       cap, nullptr);
+    if (prep_rows_per_thread(m) == 2)
+      hipLaunchKernelGGL(qp_prep_kernel<2>, dim3(B), dim3(prep_threads(m)), prep_lds(n), 0, P, s, kidx, rpos, kls, gkb, (int64_t)B, meta, nullptr);
+    else
+      hipLaunchKernelGGL(qp_prep_kernel<1>, dim3(B), dim3(prep_threads(m)), prep_lds(n), 0, P, s, kidx, rpos, kls, gkb, (int64_t)B, meta, nullptr);
     hipEventRecord(e1);
-    hipEventSynchronize(e1);
-    float ms; hipEventElapsedTime(&ms, e0, e1);
-    if (r) tot += ms;
+    hipLaunchKernelGGL(qp_asm_tile_kernel, dim3(B * ASM_WPP), dim3(512), 0, 0, P, kidx, kls, gkb, (int64_t)B, meta, K, ld, nmax, nullptr);
+    hipEventRecord(e2);
+    hipEventSynchronize(e2);
+    float a1, a2;
+    hipEventElapsedTime(&a1, e0, e1);
+    hipEventElapsedTime(&a2, e1, e2);
+    if (r) { t1 += a1; t2 += a2; }
   }
-  unsigned long long stp[8];
-  hipMemcpyFromSymbol(stp, HIP_SYMBOL(asm_stamps), sizeof(stp));
   std::vector<QPMeta> hm(B);
   hipMemcpy(hm.data(), meta, B * sizeof(QPMeta), hipMemcpyDeviceToHost);
-  printf("B=%d n=%d m=%d nk[0]=%d cap=%d lds=%zu  %.1f us/launch\n", B, n, m, hm[0].nk, cap, lds, 1e3 * tot / 5);
-  const char* nm[5] = {"Q zero test", "s = Gz-h, rows", "staging", "tile loop", "G pass"};
-  for (int k = 0; k < 5; ++k) printf("  %-16s %9.0f cycles/WG\n", nm[k], (double)stp[k] / B);
+  double bytes = 0;
+  for (int b = 0; b < B; ++b) { const double Np = (hm[b].nsys + 31) / 32 * 32; bytes += 8.0 * (Np * Np + n * n + (double)m * n); }
+  printf("ld+%d B=%d n=%d m=%d nk[0]=%d  prep %.1f us  tiles %.1f us  (%.0f GB/s on Q+G+K)\n", ldpad, B, n, m, hm[0].nk, 1e3 * t1 / 5,
+         1e3 * t2 / 5, bytes / (1e-3 * (t1 + t2) / 5) / 1e9);
   return 0;
 }
