@@ -52,13 +52,30 @@ void copy_out(Handle& h, double* dst, const double* dev, size_t count) {
   DOPT_CHECK_HIP(hipMemcpyAsync(dst, dev, count * sizeof(double), hipMemcpyDeviceToHost, h.stream));
 }
 
+// A singular problem's info in the coordinates of the reference's LHS
+// (QuadraticProgram.jl:256-282, unknowns [z; λ; ν]): the factorised system
+// is the reduced one (kept inequality rows only), so a reduced column k maps
+// back to z_k, λ_{kidx[k−n]} or ν_{k−n−nk} (1-based).
+int full_column(Handle& h, int64_t b, const dopt::QPMeta& mm) {
+  const int k = mm.info, n = h.n;
+  if (k <= n) return k;
+  if (k <= n + mm.nk) {
+    int32_t row = 0;
+    DOPT_CHECK_HIP(hipMemcpyAsync(&row, h.kidx.as<int32_t>() + (size_t)b * h.m + (k - n - 1), sizeof(int32_t),
+                                  hipMemcpyDeviceToHost, h.stream));
+    DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+    return n + row + 1;
+  }
+  return n + h.m + (k - n - mm.nk);
+}
+
 int first_info(Handle& h) {
   std::vector<dopt::QPMeta> meta(h.batch);
   DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h.meta.p, h.batch * sizeof(dopt::QPMeta),
                                 hipMemcpyDeviceToHost, h.stream));
   DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
-  for (auto& mm : meta)
-    if (!mm.iterative && mm.info > 0) return mm.info;
+  for (int64_t b = 0; b < h.batch; ++b)
+    if (!meta[b].iterative && meta[b].info > 0) return full_column(h, b, meta[b]);
   return 0;
 }
 
@@ -639,7 +656,8 @@ int dopt_get_info(dopt_handle* h, int32_t* info) {
       DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h->meta.p, h->batch * sizeof(dopt::QPMeta),
                                     hipMemcpyDeviceToHost, h->stream));
       DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
-      for (int64_t i = 0; i < h->batch; ++i) info[i] = meta[i].iterative ? 0 : meta[i].info;
+      for (int64_t i = 0; i < h->batch; ++i)
+        info[i] = (meta[i].iterative || meta[i].info <= 0) ? 0 : full_column(*h, i, meta[i]);
     } else {
       if (!h->cinfo.p) throw Error(-1, "no conic solve has run");
       DOPT_CHECK_HIP(hipMemcpyAsync(info, h->cinfo.p, h->batch * sizeof(int32_t),

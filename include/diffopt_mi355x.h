@@ -237,7 +237,9 @@ int dopt_conic_lsqr_stats(dopt_handle* h, int32_t* stats);
 
 /* ---- introspection ---------------------------------------------------------*/
 /* per-problem status of the last factor/solve: QP: 0 ok, k>0 zero pivot at
- * column k of the (reduced) KKT; CONIC: LSQR istop of the last solve. */
+ * column k of the reference's KKT matrix LHS (unknowns [z; λ; ν], 1-based;
+ * the engine factorises the reduced system and maps its column back);
+ * CONIC: LSQR istop of the last solve. */
 /* ---- NonLinearProgram back-end (kind DOPT_KIND_NLP) ------------------------
  * dopt_create's n = primal variables, m = NLP constraints c, p = parameters P.
  * Replaces the KKT part of src/NonLinearProgram (the derivatives at the

@@ -337,6 +337,25 @@ def test_singular_kkt_raises(QPBatch, lu_mode):
     assert e.info()[0] > 0
 
 
+def test_singular_info_in_full_kkt_columns(QPBatch, lu_mode):
+    """The zero pivot is reported in the reference LHS's coordinates
+    ([z; λ; ν], 1-based), not the reduced system's: row 0 is eliminated
+    (λ = 0, s ≠ 0), row 1 (λ = 0, s = 0) is the zero column, reduced column
+    3 → LHS column n + 1 + 1 = 4."""
+    from diffopt_amd import SingularException
+    Q = np.eye(2)[None]
+    G = np.array([[[1.0, 0.0], [0.0, 1.0], [1.0, 1.0]]])
+    z = np.array([[1.0, 2.0]])
+    h = np.array([[3.0, 2.0, 3.0]])     # s = Gz − h = (−2, 0, 0)
+    lam = np.array([[0.0, 0.0, 1.0]])
+    e = QPBatch(1, 2, 3, 0)
+    e.set(Q, G, h, np.zeros((1, 0, 2)), z, lam, np.zeros((1, 0)))
+    with pytest.raises(SingularException) as ex:
+        e.reverse(np.ones((1, 2)))
+    assert e.info()[0] == 4
+    assert ex.value.info == 4
+
+
 def test_lp_iterative_batch_mixed_with_qp(QPBatch, lu_mode):
     """A batch mixing Q == 0 (LSQR branch) and Q != 0 (LU branch)."""
     with open(os.path.join(HERE, "golden", "lp_fixtures.json")) as fh:
