@@ -786,7 +786,7 @@ static void conic_set_common(Handle* h, const double* A, const double* b, const 
       int d = 0;
       while (d * (d + 1) / 2 < dim) ++d;
       if (d * (d + 1) / 2 != dim) throw Error(-1, "PSD triangle dimension is not triangular");
-      if (d > 64) throw Error(-1, "PSD cones larger than 64×64 are not supported");
+      if (d > 256) throw Error(-1, "PSD cones larger than 256×256 are not supported");
     }
     rows += dim;
   }

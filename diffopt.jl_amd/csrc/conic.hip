@@ -19,10 +19,12 @@
 namespace dopt {
 
 constexpr int CTPB = 256;
-constexpr int PSD_MAX = 64;
+constexpr int PSD_MAX = 64;       // PSD sides up to this: eigensolver and Dπ apply in LDS
+constexpr int PSD_BIG_MAX = 256;  // larger sides (≤ this): the same code on global scratch
 
 struct ConeDesc {
   int32_t code, dim, row, poff;  // poff: offset into the per-problem param block
+  int32_t woff, pad;             // PSD side > PSD_MAX: offset into the global scratch
 };
 
 __device__ __forceinline__ double cwave_sum(double v) {
@@ -56,13 +58,14 @@ __device__ __forceinline__ int tri_idx(int i, int j) { return j * (j + 1) / 2 + 
 __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
     const ConeDesc* __restrict__ cones, int ncones, const double* __restrict__ y,
     const double* __restrict__ s, int m, int plen, double* __restrict__ v_out,
-    double* __restrict__ vp_out, double* __restrict__ params, int* __restrict__ bad) {
-  __shared__ double X[PSD_MAX][PSD_MAX + 1];
-  __shared__ double V[PSD_MAX][PSD_MAX + 1];
+    double* __restrict__ vp_out, double* __restrict__ params, int* __restrict__ bad,
+    double* __restrict__ psd_ws, int wlen) {
+  __shared__ double Xl[PSD_MAX * (PSD_MAX + 1)];
+  __shared__ double Vl[PSD_MAX * (PSD_MAX + 1)];
   __shared__ double red[8];
-  __shared__ double rot_c[PSD_MAX / 2], rot_s[PSD_MAX / 2];
-  __shared__ int pp[PSD_MAX / 2], qq[PSD_MAX / 2];
-  __shared__ int perm[PSD_MAX];
+  __shared__ double rot_c[PSD_BIG_MAX / 2], rot_s[PSD_BIG_MAX / 2];
+  __shared__ int pp[PSD_BIG_MAX / 2], qq[PSD_BIG_MAX / 2];
+  __shared__ int perm[PSD_BIG_MAX];
   const int k = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   const ConeDesc cd = cones[k];
   const double* yb = y + (size_t)b * m + cd.row;
@@ -110,23 +113,30 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
     if (t == 0) { P[0] = cs; P[1] = tt; P[2] = nx; P[3] = 0.0; }
   } else if (cd.code == DOPT_CONE_PSD_TRI) {
     const int d = psd_side(dim);
+    // X, V: LDS up to PSD_MAX, else this problem's global scratch (same code)
+    const bool big = d > PSD_MAX;
+    const int lx = big ? d : PSD_MAX + 1;
+    double* Xp = big ? psd_ws + (size_t)b * wlen + cd.woff : Xl;
+    double* Vp = big ? Xp + (size_t)d * d : Vl;
+#define X(i, j) Xp[(i) * lx + (j)]
+#define V(i, j) Vp[(i) * lx + (j)]
     // X = smat(v) (unscaled), V = I
     for (int e = t; e < d * d; e += CTPB) {
       const int i = e / d, j = e % d;
-      X[i][j] = (i <= j) ? vb[tri_idx(i, j)] : vb[tri_idx(j, i)];
-      V[i][j] = (i == j) ? 1.0 : 0.0;
+      X(i, j) = (i <= j) ? vb[tri_idx(i, j)] : vb[tri_idx(j, i)];
+      V(i, j) = (i == j) ? 1.0 : 0.0;
     }
     __syncthreads();
     // parallel cyclic Jacobi (round-robin pairing), d padded to even
     const int de = d + (d & 1);
     double fro = 0.0;
-    for (int e = t; e < d * d; e += CTPB) fro = fma(X[e / d][e % d], X[e / d][e % d], fro);
+    for (int e = t; e < d * d; e += CTPB) fro = fma(X(e / d, e % d), X(e / d, e % d), fro);
     const double nrm2 = cblock_sum(fro, red);
     for (int sweep = 0; sweep < 40; ++sweep) {
       double off = 0.0;
       for (int e = t; e < d * d; e += CTPB) {
         const int i = e / d, j = e % d;
-        if (i != j) off = fma(X[i][j], X[i][j], off);
+        if (i != j) off = fma(X(i, j), X(i, j), off);
       }
       off = cblock_sum(off, red);
       if (off <= 1e-32 * nrm2 || off == 0.0) break;
@@ -140,9 +150,9 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
           qq[t] = c;
           double cth = 1.0, sth = 0.0;
           if (c < d) {
-            const double apq = X[a][c];
+            const double apq = X(a, c);
             if (apq != 0.0) {
-              const double app = X[a][a], aqq = X[c][c];
+              const double app = X(a, a), aqq = X(c, c);
               const double tau = (aqq - app) / (2.0 * apq);
               const double tn = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
               cth = 1.0 / sqrt(1.0 + tn * tn);
@@ -159,9 +169,9 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
           const int a = pp[r], c = qq[r];
           if (c < d) {
             const double cth = rot_c[r], sth = rot_s[r];
-            const double xa = X[a][col], xc = X[c][col];
-            X[a][col] = cth * xa - sth * xc;
-            X[c][col] = sth * xa + cth * xc;
+            const double xa = X(a, col), xc = X(c, col);
+            X(a, col) = cth * xa - sth * xc;
+            X(c, col) = sth * xa + cth * xc;
           }
         }
         __syncthreads();
@@ -171,12 +181,12 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
           const int a = pp[r], c = qq[r];
           if (c < d) {
             const double cth = rot_c[r], sth = rot_s[r];
-            const double xa = X[row][a], xc = X[row][c];
-            X[row][a] = cth * xa - sth * xc;
-            X[row][c] = sth * xa + cth * xc;
-            const double va = V[row][a], vc = V[row][c];
-            V[row][a] = cth * va - sth * vc;
-            V[row][c] = sth * va + cth * vc;
+            const double xa = X(row, a), xc = X(row, c);
+            X(row, a) = cth * xa - sth * xc;
+            X(row, c) = sth * xa + cth * xc;
+            const double va = V(row, a), vc = V(row, c);
+            V(row, a) = cth * va - sth * vc;
+            V(row, c) = sth * va + cth * vc;
           }
         }
         __syncthreads();
@@ -188,7 +198,7 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
       for (int i = 0; i < d; ++i) {
         int mi = i;
         for (int j = i + 1; j < d; ++j)
-          if (X[perm[j]][perm[j]] < X[perm[mi]][perm[mi]]) mi = j;
+          if (X(perm[j], perm[j]) < X(perm[mi], perm[mi])) mi = j;
         const int tmp = perm[i]; perm[i] = perm[mi]; perm[mi] = tmp;
       }
     }
@@ -198,13 +208,13 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
     double* Bm = P + d * d;
     for (int e = t; e < d * d; e += CTPB) {
       const int i = e / d, j = e % d;
-      U[i * d + j] = V[i][perm[j]];
+      U[i * d + j] = V(i, perm[j]);
     }
     int allpos = 1;
-    for (int i = 0; i < d; ++i) allpos &= (X[perm[i]][perm[i]] >= 0.0);
+    for (int i = 0; i < d; ++i) allpos &= (X(perm[i], perm[i]) >= 0.0);
     for (int e = t; e < d * d; e += CTPB) {
       const int i = e / d, j = e % d;
-      const double li = X[perm[i]][perm[i]], lj = X[perm[j]][perm[j]];
+      const double li = X(perm[i], perm[i]), lj = X(perm[j], perm[j]);
       double w;
       if (li == lj) w = (li > 0.0) ? 1.0 : 0.0;
       else w = (fmax(li, 0.0) - fmax(lj, 0.0)) / (li - lj);
@@ -218,9 +228,11 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
       while ((j + 1) * (j + 2) / 2 <= e) ++j;
       const int i = e - j * (j + 1) / 2;
       double acc = 0.0;
-      for (int q = 0; q < d; ++q) acc = fma(V[i][perm[q]] * fmax(X[perm[q]][perm[q]], 0.0), V[j][perm[q]], acc);
+      for (int q = 0; q < d; ++q) acc = fma(V(i, perm[q]) * fmax(X(perm[q], perm[q]), 0.0), V(j, perm[q]), acc);
       vpb[e] = acc;
     }
+#undef X
+#undef V
   }
 }
 
@@ -261,9 +273,66 @@ __device__ __forceinline__ void psd_gemm4(int d, int dp, bool upper, FA a, FB b,
   }
 }
 
+// One PSD cone of dpi_apply: Xs / Ys / Us are the three dp × (dp+1) images
+// (LDS, or global scratch for sides > PSD_MAX — separate inlined copies, so no
+// pointer selects across address spaces: one crashed the compiler).
+__device__ __forceinline__ void psd_apply_cone(const ConeDesc cd, const double* __restrict__ P, const double* in,
+                                            double* out, int trans, double* Xs, double* Ys, double* Us) {
+  const int t = threadIdx.x;
+  const int d = psd_side(cd.dim);
+  const int dp = (d + 3) & ~3;
+  const int ld = dp + 1;
+  const double* U = P + cd.poff;
+  const double* Bm = U + d * d;
+  const bool ident = U[2 * d * d] != 0.0;
+  const double* w = in + cd.row;
+  double* o = out + cd.row;
+  if (ident) {
+    for (int i = t; i < cd.dim; i += CTPB) o[i] = w[i];
+    return;
+  }
+  // X = smat(S^{-2} w) for Dπ (=Jᵀ = S²JS⁻²), smat(w) for Dπᵀ (= J)
+  for (int e = t; e < dp * dp; e += CTPB) {
+    const int i = e / dp, j = e % dp;
+    double val = 0.0, uv = 0.0;
+    if (i < d && j < d) {
+      const int a = i <= j ? i : j, c = i <= j ? j : i;
+      val = w[tri_idx(a, c)];
+      if (!trans && a != c) val *= 0.5;
+      uv = U[i * d + j];
+    }
+    Xs[i * ld + j] = val;
+    Us[i * ld + j] = uv;
+  }
+  __syncthreads();
+  // Y = Uᵀ X
+  psd_gemm4(d, dp, false, [&](int i, int q) { return Us[q * ld + i]; },
+            [&](int q, int j) { return Xs[q * ld + j]; },
+            [&](int i, int j, double v) { Ys[i * ld + j] = v; });
+  __syncthreads();
+  // X = (Y U) ∘ B
+  psd_gemm4(d, dp, false, [&](int i, int q) { return Ys[i * ld + q]; },
+            [&](int q, int j) { return Us[q * ld + j]; },
+            [&](int i, int j, double v) { Xs[i * ld + j] = (i < d && j < d) ? v * Bm[i * d + j] : 0.0; });
+  __syncthreads();
+  // Y = U X
+  psd_gemm4(d, dp, false, [&](int i, int q) { return Us[i * ld + q]; },
+            [&](int q, int j) { return Xs[q * ld + j]; },
+            [&](int i, int j, double v) { Ys[i * ld + j] = v; });
+  __syncthreads();
+  // out = tri(Y Uᵀ) (upper-triangle tiles only), times S² for Dπ
+  psd_gemm4(d, dp, true, [&](int i, int q) { return Ys[i * ld + q]; },
+            [&](int q, int j) { return Us[j * ld + q]; },
+            [&](int i, int j, double v) {
+              if (i <= j && j < d) o[tri_idx(i, j)] = (!trans && i != j) ? 2.0 * v : v;
+            });
+  __syncthreads();
+}
+
+template <bool BIG = false>
 __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, const double* __restrict__ v,
                           const double* __restrict__ P, const double* in, double* out,
-                          int trans, double* lds, double* red) {
+                          int trans, double* lds, double* red, double* gws) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   // diagonal / identity cones: elementwise; SOC: one wave per cone
   for (int k = 0; k < ncones; ++k) {
@@ -306,61 +375,19 @@ __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, con
   // PSD cones: whole workgroup per cone; the four d×d products run on 4×4
   // register tiles (8 LDS reads per 16 FMAs) over the side padded to dp =
   // round_up(d, 4); padded rows/columns are zero on load and the q-sums stop
-  // at d, so they never reach a kept entry.
-  double* Xs = lds;                                  // dp × (dp+1)
-  double* Ys = lds + PSD_MAX * (PSD_MAX + 1);
-  double* Us = lds + 2 * PSD_MAX * (PSD_MAX + 1);
+  // at d, so they never reach a kept entry.  Sides > PSD_MAX: the same on the
+  // sequence's global scratch `gws` at the cone's woff (split path only).
   for (int k = 0; k < ncones; ++k) {
     const ConeDesc cd = cones[k];
     if (cd.code != DOPT_CONE_PSD_TRI) continue;
     const int d = psd_side(cd.dim);
-    const int dp = (d + 3) & ~3;
-    const int ld = dp + 1;
-    const double* U = P + cd.poff;
-    const double* Bm = U + d * d;
-    const bool ident = U[2 * d * d] != 0.0;
-    const double* w = in + cd.row;
-    double* o = out + cd.row;
-    if (ident) {
-      for (int i = t; i < cd.dim; i += CTPB) o[i] = w[i];
-      continue;
+    if (BIG && d > PSD_MAX) {
+      const size_t img = (size_t)((d + 3) & ~3) * (((d + 3) & ~3) + 1);
+      double* g = gws + cd.woff;
+      psd_apply_cone(cd, P, in, out, trans, g, g + img, g + 2 * img);
+    } else {
+      psd_apply_cone(cd, P, in, out, trans, lds, lds + PSD_MAX * (PSD_MAX + 1), lds + 2 * PSD_MAX * (PSD_MAX + 1));
     }
-    // X = smat(S^{-2} w) for Dπ (=Jᵀ = S²JS⁻²), smat(w) for Dπᵀ (= J)
-    for (int e = t; e < dp * dp; e += CTPB) {
-      const int i = e / dp, j = e % dp;
-      double val = 0.0, uv = 0.0;
-      if (i < d && j < d) {
-        const int a = i <= j ? i : j, c = i <= j ? j : i;
-        val = w[tri_idx(a, c)];
-        if (!trans && a != c) val *= 0.5;
-        uv = U[i * d + j];
-      }
-      Xs[i * ld + j] = val;
-      Us[i * ld + j] = uv;
-    }
-    __syncthreads();
-    // Y = Uᵀ X
-    psd_gemm4(d, dp, false, [&](int i, int q) { return Us[q * ld + i]; },
-              [&](int q, int j) { return Xs[q * ld + j]; },
-              [&](int i, int j, double v) { Ys[i * ld + j] = v; });
-    __syncthreads();
-    // X = (Y U) ∘ B
-    psd_gemm4(d, dp, false, [&](int i, int q) { return Ys[i * ld + q]; },
-              [&](int q, int j) { return Us[q * ld + j]; },
-              [&](int i, int j, double v) { Xs[i * ld + j] = (i < d && j < d) ? v * Bm[i * d + j] : 0.0; });
-    __syncthreads();
-    // Y = U X
-    psd_gemm4(d, dp, false, [&](int i, int q) { return Us[i * ld + q]; },
-              [&](int q, int j) { return Xs[q * ld + j]; },
-              [&](int i, int j, double v) { Ys[i * ld + j] = v; });
-    __syncthreads();
-    // out = tri(Y Uᵀ) (upper-triangle tiles only), times S² for Dπ
-    psd_gemm4(d, dp, true, [&](int i, int q) { return Ys[i * ld + q]; },
-              [&](int q, int j) { return Us[j * ld + q]; },
-              [&](int i, int j, double v) {
-                if (i <= j && j < d) o[tri_idx(i, j)] = (!trans && i != j) ? 2.0 * v : v;
-              });
-    __syncthreads();
   }
   __syncthreads();
 }
@@ -501,7 +528,7 @@ __device__ __forceinline__ void M_apply(const ConicProblem& pr, const ConeDesc* 
                         const double* z, double* out, double* Dv, double* Au, double* g,
                         double* lds, double* red, double* ys) {
   const int n = pr.n, m = pr.m, t = threadIdx.x;
-  dpi_apply(cones, ncones, pr.v, pr.P, z + n, Dv, 0, lds, red);
+  dpi_apply(cones, ncones, pr.v, pr.P, z + n, Dv, 0, lds, red, nullptr);
   // A_moi u (= −A u) and A_moiᵀ Dv (= −AᵀDv) in one sweep
   gemv_pair(pr.A, m, m, n, z, Dv, Au, g, ys);
   const double w = z[n + m];
@@ -529,7 +556,7 @@ __device__ __forceinline__ void MT_apply(const ConicProblem& pr, const ConeDesc*
   const double tw = r[n + m];
   for (int i = t; i < m; i += CTPB) tmpm[i] = -Ap[i] - r[n + i] - pr.b[i] * tw;
   __syncthreads();
-  dpi_apply(cones, ncones, pr.v, pr.P, tmpm, out + n, 1, lds, red);
+  dpi_apply(cones, ncones, pr.v, pr.P, tmpm, out + n, 1, lds, red, nullptr);
   double cp = 0.0, bq = 0.0;
   for (int j = t; j < n; j += CTPB) {
     out[j] = g[j] - pr.c[j] * tw;
@@ -551,8 +578,8 @@ __device__ __forceinline__ void M_apply2(const ConicProblem& pr, const ConeDesc*
                                          const double* z1, double* out1, double* Dv1, double* Au1, double* g1,
                                          double* lds, double* red, double* ys) {
   const int n = pr.n, m = pr.m, t = threadIdx.x;
-  dpi_apply(cones, ncones, pr.v, pr.P, z0 + n, Dv0, 0, lds, red);
-  dpi_apply(cones, ncones, pr.v, pr.P, z1 + n, Dv1, 0, lds, red);
+  dpi_apply(cones, ncones, pr.v, pr.P, z0 + n, Dv0, 0, lds, red, nullptr);
+  dpi_apply(cones, ncones, pr.v, pr.P, z1 + n, Dv1, 0, lds, red, nullptr);
   const double* xs[2] = {z0, z1};
   const double* ws[2] = {Dv0, Dv1};
   double* yv[2] = {Au0, Au1};
@@ -601,7 +628,7 @@ __device__ __forceinline__ void MT_apply2(const ConicProblem& pr, const ConeDesc
     const double tw = r[n + m];
     for (int i = t; i < m; i += CTPB) tm[q][i] = -yv[q][i] - r[n + i] - pr.b[i] * tw;
     __syncthreads();
-    dpi_apply(cones, ncones, pr.v, pr.P, tm[q], out + n, 1, lds, red);
+    dpi_apply(cones, ncones, pr.v, pr.P, tm[q], out + n, 1, lds, red, nullptr);
     double cp = 0.0, bq = 0.0;
     for (int j = t; j < n; j += CTPB) {
       out[j] = gv[q][j] - pr.c[j] * tw;
@@ -1170,7 +1197,8 @@ __global__ __launch_bounds__(CTPB) void conic_split_pass_kernel(
 // Dπ (dir 0: Dv = Dπ v_m) or Dπᵀ (dir 1: out_m = Dπᵀ tmpm), one cone per WG
 __global__ __launch_bounds__(CTPB) void conic_split_dpi_kernel(
     int dir, const ConeDesc* __restrict__ cones_g, const double* __restrict__ vcone,
-    const double* __restrict__ P, int plen, SplitWS ws, const LsqrState* __restrict__ stv) {
+    const double* __restrict__ P, int plen, SplitWS ws, const LsqrState* __restrict__ stv,
+    double* __restrict__ gws, int wlen) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ double red[4];
   const int k = blockIdx.x, b = blockIdx.y;
@@ -1179,10 +1207,11 @@ __global__ __launch_bounds__(CTPB) void conic_split_dpi_kernel(
   const ConeDesc cd = cones_g[k];
   const double* pv = vcone + (size_t)ws.phys(b) * ws.m;
   const double* pp = P + (size_t)ws.phys(b) * plen;
+  double* g = gws + (size_t)b * wlen;
   if (dir == 0)
-    dpi_apply(&cd, 1, pv, pp, ws.vec(ws.v, b) + ws.n, ws.mvec(ws.Dv, b), 0, lds, red);
+    dpi_apply<true>(&cd, 1, pv, pp, ws.vec(ws.v, b) + ws.n, ws.mvec(ws.Dv, b), 0, lds, red, g);
   else
-    dpi_apply(&cd, 1, pv, pp, ws.mvec(ws.tmpm, b), ws.vec(ws.out, b) + ws.n, 1, lds, red);
+    dpi_apply<true>(&cd, 1, pv, pp, ws.mvec(ws.tmpm, b), ws.vec(ws.out, b) + ws.n, 1, lds, red, g);
 }
 
 // The per-problem vector kernels below run 1024-thread workgroups and issue
@@ -1491,10 +1520,10 @@ void conic_factor(Handle& h) {
   const int B = (int)h.batch, m = h.m;
   const int nc = (int)h.cones.size() / 2;
   std::vector<ConeDesc> cd(nc);
-  int row = 0, poff = 0;
+  int row = 0, poff = 0, woff = 0;
   for (int k = 0; k < nc; ++k) {
     const int code = h.cones[2 * k], dim = h.cones[2 * k + 1];
-    cd[k] = {code, dim, row, poff};
+    cd[k] = {code, dim, row, poff, 0, 0};
     row += dim;
     if (code == DOPT_CONE_NONNEG || code == DOPT_CONE_NONPOS) poff += dim;
     else if (code == DOPT_CONE_SOC) poff += 4;
@@ -1502,9 +1531,16 @@ void conic_factor(Handle& h) {
       int d = 0;
       while ((d + 1) * (d + 2) / 2 <= dim) ++d;
       poff += 2 * d * d + 2;
+      if (d > PSD_MAX) {   // global scratch: 3 apply images (≥ the eigensolver's X and V)
+        const int dp = (d + 3) & ~3;
+        cd[k].woff = woff;
+        woff += 3 * dp * (dp + 1);
+      }
     }
   }
   h.dpi_len = std::max(poff, 1);
+  h.psd_big_len = woff;
+  h.psd_eig.ensure(std::max<size_t>((size_t)B * woff, 1) * sizeof(double));
   h.cone_dev.ensure(std::max<size_t>(nc, 1) * sizeof(ConeDesc));
   if (nc)
     DOPT_CHECK_HIP(hipMemcpyAsync(h.cone_dev.p, cd.data(), nc * sizeof(ConeDesc), hipMemcpyHostToDevice, h.stream));
@@ -1518,7 +1554,8 @@ void conic_factor(Handle& h) {
     if (nc && B) {
       hipLaunchKernelGGL(conic_cone_kernel, dim3(nc, B), dim3(CTPB), 0, h.stream,
                          h.cone_dev.as<ConeDesc>(), nc, h.cy, h.cs, m, h.dpi_len,
-                         h.vp.as<double>(), h.vp.as<double>() + (size_t)B * m, h.dpi.as<double>(), bad);
+                         h.vp.as<double>(), h.vp.as<double>() + (size_t)B * m, h.dpi.as<double>(), bad,
+                         h.psd_eig.as<double>(), h.psd_big_len);
       ccheck();
     }
   }
@@ -1566,6 +1603,8 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
   const double* vcone = h.vp.as<double>();
   const double* P = h.dpi.as<double>();
   const ConeDesc* cd = h.cone_dev.as<ConeDesc>();
+  h.psd_app.ensure(std::max<size_t>((size_t)V * h.psd_big_len, 1) * sizeof(double));
+  double* gws = h.psd_app.as<double>();
   const int32_t nact = V;
   DOPT_CHECK_HIP(hipMemcpyAsync(active, &nact, sizeof(int32_t), hipMemcpyHostToDevice, h.stream));
   int32_t left = V;
@@ -1574,7 +1613,7 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
     hipLaunchKernelGGL(conic_split_pass_kernel, dim3(RB, B), dim3(CTPB), 0, h.stream, 1, h.cA, h.cb, ws, st, nq);
     if (nc)
       hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, V), dim3(CTPB), dl, h.stream, 1, cd, vcone, P,
-                         h.dpi_len, ws, st);
+                         h.dpi_len, ws, st, gws, h.psd_big_len);
   };
   hipLaunchKernelGGL(conic_split_init_kernel, dim3(V), dim3(CTPB), 0, h.stream, rhs, tol0, tol1, ws, st, active);
   passT();
@@ -1584,7 +1623,7 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
     for (int k = 0; k < SPLIT_CHUNK && it < N; ++k, ++it) {
       if (nc)
         hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, V), dim3(CTPB), dl, h.stream, 0, cd, vcone, P,
-                           h.dpi_len, ws, st);
+                           h.dpi_len, ws, st, gws, h.psd_big_len);
       hipLaunchKernelGGL(conic_split_pass_kernel, dim3(RB, B), dim3(CTPB), 0, h.stream, 0, h.cA, h.cb, ws, st,
                          nq);
       hipLaunchKernelGGL(conic_split_upd_u_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st);
@@ -1601,6 +1640,7 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
 }
 
 static bool use_split(const Handle& h) {
+  if (h.psd_big_len > 0) return true;   // PSD sides > PSD_MAX: Dπ apply on global scratch, split path only
   if (h.conic_split >= 0) return h.conic_split != 0;
   return h.m > 2 * PAIR_ROWS;   // several row blocks per problem: spread them over CUs
 }

@@ -139,6 +139,8 @@ struct Handle {
   DevBuf csplit;                // split-path LSQR vectors, partial products, state
   int32_t conic_split = -1;     // -1 auto, 0 persistent kernel, 1 split (env DOPT_CONIC_SPLIT)
   int32_t dpi_len = 0;          // doubles per problem of packed Dπ blocks
+  int32_t psd_big_len = 0;      // doubles of global scratch per problem / sequence for PSD sides > 64
+  DevBuf psd_eig, psd_app;      // that scratch: the eigensolver's (per problem), the Dπ apply's (per sequence)
   bool cset = false, cfactored = false;
 
   // ---- NLP (nlp.hip) ----

@@ -52,7 +52,7 @@ extern "C" {
 #define DOPT_CONE_NONNEG 1       /* MOI.Nonnegatives                          */
 #define DOPT_CONE_NONPOS 2       /* MOI.Nonpositives                          */
 #define DOPT_CONE_SOC 3          /* MOI.SecondOrderCone                       */
-#define DOPT_CONE_PSD_TRI 4      /* MOI.PositiveSemidefiniteConeTriangle      */
+#define DOPT_CONE_PSD_TRI 4      /* MOI.PositiveSemidefiniteConeTriangle (side ≤ 256; > 64 on global scratch) */
 
 #define DOPT_ABI_VERSION 2
 

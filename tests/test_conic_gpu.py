@@ -239,6 +239,18 @@ def test_config5_full_shape(ConicBatch):
     print(f"[parity] config-5 LSQR iterations: engine fwd {it_f[0]} rev {it_r[0]}, oracle {infos[0]}")
 
 
+@pytest.mark.parametrize("shape", [
+    ("large PSD (d = 66) + small cones", 2, 60, [(4, 2211), (4, 15), (1, 5)], 17, 2),   # converged at √eps: 2 of 12 in (1e-6, 3.2e-6] (r02)
+    ("large PSD (d = 100)", 1, 60, [(4, 5050)], 18, 0),
+], ids=["d66_mixed", "d100"])
+def test_large_psd_sides(ConicBatch, shape):
+    """PSD sides above 64 (the LDS eigensolver / Dπ apply limit): the same code
+    on global scratch, split LSQR path; reference: any MOI PSD triangle
+    (ConicProgram.jl:132-142, diff_opt.jl:491-519)."""
+    name, B, n, cones, seed, cap = shape
+    _synthetic_check(ConicBatch, B, n, cones, seed, name, cap=cap)
+
+
 def test_zero_rhs_gives_zero(ConicBatch):
     from diffopt_amd.synthetic import conic_numpy
     cones = [(1, 6), (3, 4)]
