@@ -118,7 +118,7 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
     if (const char* e = getenv("DOPT_LU")) h->lu_mode = atoi(e) != 0;
     if (kind == DOPT_KIND_QP) {
       // largest supported system: the generic solve stages an nmax vector in
-      // LDS (64 KB), the blocked path is limited to BLOCKED_MAX unknowns
+      // LDS (64 KB); the blocked route takes reduced systems up to BLOCKED_MAX
       if ((int64_t)n + m + p > 8192)
         throw Error(-1, "QP systems with n + m + p > 8192 are not supported");
       // Systems are identity-padded to whole 32-column blocks (qp_assemble.hip),

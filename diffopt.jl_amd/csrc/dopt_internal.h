@@ -49,7 +49,7 @@ struct DevBuf {
 
 // Per-problem QP metadata (device, batch entries).
 // Factorisation kinds (QPMeta::lu).
-enum QPLu { LU_NONE = 0, LU_NOPIV = 1, LU_PIVOT = 2, LU_REJECT = 3 };
+enum QPLu { LU_NONE = 0, LU_NOPIV = 1, LU_PIVOT = 2, LU_REJECT = 3, LU_GENERIC = 4 };
 // selection masks of the solve launches (bit k: solve problems with lu == k)
 constexpr int LU_SEL_NOPIV = 1 << LU_NOPIV;
 constexpr int LU_SEL_PIVOT = 1 << LU_PIVOT;
@@ -65,7 +65,9 @@ struct QPMeta {
 };
 
 constexpr int ASM_WPP = 16;          // assembly tile workgroups per problem (qp_assemble.hip)
-constexpr int BLOCKED_MAX = 1536;    // largest reduced system of the blocked path
+constexpr int BLOCKED_MAX = 4096;    // largest reduced system of the blocked route (no-pivot LU, blocked solves)
+constexpr int PIVOT_MAX = 1536;      // largest system of the partial-pivoting blocked LU (panel: 512 threads × 3 rows);
+                                     // larger blocked problems the no-pivot LU rejects take the generic LU
 
 // Which factorisation path a problem takes (decided per problem on the
 // device from its reduced size).
@@ -113,6 +115,7 @@ struct Handle {
   DevBuf gk;                 // kept rows of G, compacted column-major (n × m per problem; assembly tiles)
   DevBuf dinv;               // per-problem diagonal-block inverses (L11⁻¹ | U11⁻¹ per 32-block)
   DevBuf plist;              // problem indices of the partial-pivoting re-factorisation
+  DevBuf glist;              // problem indices of the generic LU
   DevBuf lsqr_ws;            // LSQR vectors of the `iterative` branch (5 per problem)
   DevBuf binv;               // no-pivot LU: packed 64×64 inverse of the current diagonal block
   DevBuf fwdw;               // fused call: both right-hand sides, forward-swept inside the no-pivot LU
@@ -125,6 +128,7 @@ struct Handle {
   int32_t lu_mode = 1;
   int32_t blocked_npmax = 0;       // largest padded blocked system of the current factorisation
   bool has_generic = true;         // some problem exceeds BLOCKED_MAX
+  int32_t n_generic = 0;           // problems factorised by the generic LU (last factorisation)
   bool has_lsqr = true;            // some problem takes the LSQR branch
   int32_t n_pivot = 0;             // problems factorised with partial pivoting (last factorisation)
   bool set = false, factored = false;

@@ -380,8 +380,8 @@ std::vector<int32_t> singular_list(Handle& h, const std::vector<int32_t>& among)
 // Buffers and sizes once the structure is known (dopt_nlp_set_structure /
 // dopt_nlp_set_kkt have filled the nlp_* counts and nlp_map).
 void nlp_configure(Handle& h) {
-  if (h.nlp_rows > BLOCKED_MAX)
-    throw Error(-1, "NLP KKT systems larger than " + std::to_string(BLOCKED_MAX) + " rows are not supported");
+  if (h.nlp_rows > PIVOT_MAX)
+    throw Error(-1, "NLP KKT systems larger than " + std::to_string(PIVOT_MAX) + " rows are not supported");
   const int64_t B = h.batch;
   h.nmax = (int32_t)round_up(std::max(h.nlp_rows, 1), 32);
   h.ld = h.nmax;

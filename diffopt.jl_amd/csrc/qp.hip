@@ -42,21 +42,20 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 }
 
 // ---------------------------------------------------------------------------
-// 3. generic LU (reduced systems larger than BLOCKED_MAX):
+// 3. generic LU (reduced systems larger than BLOCKED_MAX, and blocked ones
+// above PIVOT_MAX that the no-pivot LU rejects or DOPT_LU=0 leaves to it):
 // unblocked right-looking on global memory, panel width 1, trailing-only
 // ("lazy") row swaps: K = P₁⁻¹M₁P₂⁻¹M₂…U, undone by qp_solve_kernel.
 // Problem data was assembled into the per-problem K buffer by qp_assemble.hip.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(TPB) void qp_lu_generic_kernel(
     double* __restrict__ K, int32_t* __restrict__ ipiv, QPMeta* __restrict__ meta,
-    int nmax, int ld) {
+    int nmax, int ld, const int32_t* __restrict__ plist) {
   __shared__ double redv[4];
   __shared__ int redi[4];
-  const int b = blockIdx.x, t = threadIdx.x;
+  const int b = plist[blockIdx.x], t = threadIdx.x;
   const int lane = t & 63, wv = t >> 6;
-  if (meta[b].iterative) return;
   const int N = meta[b].nsys;
-  if (N <= BLOCKED_MAX) return;   // the blocked path owns these
   double* Kb = K + (size_t)b * nmax * ld;
   int32_t* piv = ipiv + (size_t)b * nmax;
   int info = 0;
@@ -105,7 +104,10 @@ __global__ __launch_bounds__(TPB) void qp_lu_generic_kernel(
     }
     __syncthreads();
   }
-  if (t == 0) meta[b].info = info;
+  if (t == 0) {
+    meta[b].info = info;
+    meta[b].lu = LU_GENERIC;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -122,9 +124,8 @@ __global__ __launch_bounds__(TPB) void qp_solve_kernel(
   __shared__ double part[8][33];
   const int b = blockIdx.x, t = threadIdx.x;
   const int lane = t & 63, wv = t >> 6;
-  if (meta[b].iterative) return;
+  if (meta[b].iterative || meta[b].lu != LU_GENERIC) return;   // factorised by the generic LU only
   const int N = meta[b].nsys;
-  if (N <= BLOCKED_MAX) return;   // the blocked path owns these
   const int nb = 1;                // generic LU: panel width 1, lazy swaps
   const double* Kb = K + (size_t)b * nmax * ld;
   const int32_t* piv = ipiv + (size_t)b * nmax;
@@ -781,7 +782,8 @@ static int pivot_fallback(Handle& h, const ReasmFn& reasm) {
   DOPT_CHECK_HIP(hipEventSynchronize(h.meta_ev));
   std::vector<int32_t> list;
   for (int64_t b = 0; b < h.batch; ++b)
-    if (h.meta_host[b].lu == LU_REJECT) list.push_back((int32_t)b);
+    if (h.meta_host[b].lu == LU_REJECT && ((h.meta_host[b].nsys + 31) & ~31) <= PIVOT_MAX)
+      list.push_back((int32_t)b);
   const int count = (int)list.size();
   if (count) {
     h.plist.ensure(list.size() * sizeof(int32_t));
@@ -796,21 +798,36 @@ static int pivot_fallback(Handle& h, const ReasmFn& reasm) {
   return count;
 }
 
-static void generic_lu(Handle& h) {
-  if (!(h.nmax > BLOCKED_MAX && h.has_generic)) return;
-  hipLaunchKernelGGL(qp_lu_generic_kernel, dim3(h.batch), dim3(TPB), 0, h.stream, h.K.as<double>(),
-                     h.ipiv.as<int32_t>(), h.meta.as<QPMeta>(), h.nmax, h.ld);
+// The generic (unblocked, partially pivoted) LU of the problems in `list`.
+static void generic_lu(Handle& h, const std::vector<int32_t>& list) {
+  h.n_generic = (int)list.size();
+  if (list.empty()) return;
+  h.glist.ensure(list.size() * sizeof(int32_t));
+  DOPT_CHECK_HIP(hipMemcpyAsync(h.glist.p, list.data(), list.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                                h.stream));
+  hipLaunchKernelGGL(qp_lu_generic_kernel, dim3((unsigned)list.size()), dim3(TPB), 0, h.stream, h.K.as<double>(),
+                     h.ipiv.as<int32_t>(), h.meta.as<QPMeta>(), h.nmax, h.ld, h.glist.as<int32_t>());
   check_launch();
+  DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));   // `list` outlives the upload
 }
 
 // Factorisation of the assembled batch (prepare + assembly already queued and
 // the metadata read back).  Blocked problems: the no-pivot LU, then partial
 // pivoting for the problems it rejects (lu_mode 1), or partial pivoting for
-// all (lu_mode 0).  `spec` (optional) is queued right after the no-pivot LU,
-// before the host waits for the rejected list: work that skips rejected
-// problems (the solves of the fused call).
+// all (lu_mode 0) — the partial-pivoting blocked LU up to PIVOT_MAX, the
+// generic LU above it (and for the ROUTE_GENERIC problems).  `spec`
+// (optional) is queued right after the no-pivot LU, before the host waits for
+// the rejected list: work that skips rejected problems (the solves of the
+// fused call).
 template <class F>
 static void factor_blocked(Handle& h, F&& spec, double* w0, double* w1, const ReasmFn& reasm) {
+  auto np_of = [](const QPMeta& mm) { return (mm.nsys + 31) & ~31; };
+  std::vector<int32_t> glist;   // problems for the generic LU
+  if (h.has_generic)
+    for (int64_t b = 0; b < h.batch; ++b) {
+      const QPMeta& mm = h.meta_host[b];
+      if (qp_route(mm.iterative, mm.nsys) == ROUTE_GENERIC) glist.push_back((int32_t)b);
+    }
   if (h.lu_mode == 1) {
     {
       PhaseTimer pt(h, DOPT_PHASE_QP_LU);
@@ -822,10 +839,24 @@ static void factor_blocked(Handle& h, F&& spec, double* w0, double* w1, const Re
     if (h.blocked_npmax) {
       DOPT_CHECK_HIP(hipEventSynchronize(h.meta_ev));
       bool any = false;
-      for (int64_t b = 0; b < h.batch && !any; ++b) any = h.meta_host[b].lu == LU_REJECT;
+      std::vector<int32_t> big;   // rejected problems too tall for the pivoting panel
+      for (int64_t b = 0; b < h.batch; ++b) {
+        const QPMeta& mm = h.meta_host[b];
+        if (mm.lu != LU_REJECT) continue;
+        if (np_of(mm) > PIVOT_MAX) big.push_back((int32_t)b);
+        else any = true;
+      }
       if (any) {
         PhaseTimer pt(h, DOPT_PHASE_QP_LU_PIVOT);
         h.n_pivot = pivot_fallback(h, reasm);
+      }
+      if (!big.empty()) {
+        h.plist.ensure(big.size() * sizeof(int32_t));
+        DOPT_CHECK_HIP(hipMemcpyAsync(h.plist.p, big.data(), big.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                                      h.stream));
+        reasm(h.plist.as<int32_t>(), (int)big.size());
+        DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+        glist.insert(glist.end(), big.begin(), big.end());
       }
     }
   } else {
@@ -835,10 +866,16 @@ static void factor_blocked(Handle& h, F&& spec, double* w0, double* w1, const Re
     }
     spec();
     h.n_pivot = -1;
+    if (h.blocked_npmax > PIVOT_MAX)
+      for (int64_t b = 0; b < h.batch; ++b) {
+        const QPMeta& mm = h.meta_host[b];
+        if (qp_route(mm.iterative, mm.nsys) == ROUTE_BLOCKED && np_of(mm) > PIVOT_MAX) glist.push_back((int32_t)b);
+      }
   }
-  if (h.nmax > BLOCKED_MAX && h.has_generic) {
-    PhaseTimer pt(h, DOPT_PHASE_QP_LU);
-    generic_lu(h);
+  h.n_generic = 0;
+  if (!glist.empty()) {   // timed as the fallback phase: qp_lu stays one launch sequence per factorisation
+    PhaseTimer pt(h, DOPT_PHASE_QP_LU_PIVOT);
+    generic_lu(h, glist);
   }
 }
 
@@ -885,7 +922,7 @@ static void finish_into(Handle& h, int trans, double* rhs, double* x, const doub
   const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
   const int nmax = h.nmax, ld = h.ld;
   QPMeta* meta = h.meta.as<QPMeta>();
-  if (nmax > BLOCKED_MAX && h.has_generic) {
+  if (h.n_generic > 0) {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     if ((size_t)nmax * sizeof(double) > 64 * 1024) throw Error(-1, "generic solve: system too large");
     hipLaunchKernelGGL(qp_solve_kernel, dim3(B), dim3(TPB), (size_t)nmax * sizeof(double), h.stream,
@@ -984,7 +1021,7 @@ static void solve_k(Handle& h, int trans, int k, double* rk, double* xk, double*
   for (int j = 0; j < k; ++j) {
     double* rhs = rk + j * blk;
     double* x = xk + j * blk;
-    if (nmax > BLOCKED_MAX && h.has_generic) {
+    if (h.n_generic > 0) {
       PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
       if ((size_t)nmax * sizeof(double) > 64 * 1024) throw Error(-1, "generic solve: system too large");
       hipLaunchKernelGGL(qp_solve_kernel, dim3(B), dim3(TPB), (size_t)nmax * sizeof(double), h.stream,

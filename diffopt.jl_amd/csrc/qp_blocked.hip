@@ -74,6 +74,11 @@ __device__ __forceinline__ int blocked_np(const QPMeta& mm) {
   if (qp_route(mm.iterative, mm.nsys) != ROUTE_BLOCKED) return 0;
   return (mm.nsys + BNB - 1) & ~(BNB - 1);
 }
+// the partial-pivoting LU's share of the blocked route (Np ≤ PIVOT_MAX)
+__device__ __forceinline__ int piv_np(const QPMeta& mm) {
+  const int Np = blocked_np(mm);
+  return Np <= PIVOT_MAX ? Np : 0;
+}
 
 // ---------------------------------------------------------------------------
 // Panel: logical rows c0 .. Np−1, columns c0 .. c0+31.  Thread t owns local
@@ -94,8 +99,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(2))) void b
   __shared__ int ptop[BNB];
   const int b = plist ? plist[blockIdx.x] : (int)blockIdx.x;
   const QPMeta mm = meta[b];
-  const int Np = blocked_np(mm);
-  if (c0 >= Np) return;   // not a blocked problem, or already factored
+  const int Np = piv_np(mm);
+  if (c0 >= Np) return;   // not a blocked problem (or too tall for the panel), or already factored
   const int R = Np - c0;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   double* Kb = K + (size_t)b * nmax * ld;
@@ -378,7 +383,7 @@ __global__ __launch_bounds__(256) void blu_update_kernel(double* __restrict__ K,
   const int tile = logical - bl * tiles;
   const int b = plist ? plist[bl] : bl;
   const int rt = tile / nct, ct = tile - rt * nct;
-  const int Np = blocked_np(meta[b]);
+  const int Np = piv_np(meta[b]);
   const int R2 = Np - c0 - KW;          // trailing rows (multiple of 32, may be ≤ 0)
   const int C2 = min(R2, cols_max);     // trailing columns updated by this launch
   if (rt * 64 >= R2 || ct * 64 >= C2) return;   // workgroup-uniform
@@ -447,6 +452,11 @@ __global__ __launch_bounds__(256) void blu_update_kernel(double* __restrict__ K,
 // per thread; all their slice loads are issued before the block's barrier.
 // rhs / x: per problem stride nmax, length nsys.
 // ---------------------------------------------------------------------------
+// dynamic LDS of the solve kernels: v, y (doubles) and ps (ints), each
+// min(nmax, BLOCKED_MAX) long (a blocked problem's Np never exceeds either)
+__host__ __device__ inline int solve_lds_np(int nmax) { return nmax < BLOCKED_MAX ? nmax : BLOCKED_MAX; }
+__host__ inline size_t solve_lds_bytes(int nmax) { return (size_t)solve_lds_np(nmax) * (2 * sizeof(double) + sizeof(int)); }
+
 template <int ENT>
 __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict__ K, int ld, int nmax,
                                                 const int32_t* __restrict__ perm,
@@ -478,42 +488,49 @@ __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict_
     for (int s = 0; s < nblk; ++s) {
       const int bk = fwd ? s : nblk - 1 - s;
       const int i0 = bk * BNB;
-      double f[ENT][BNB];
-      int ev[ENT];
-      bool has[ENT];
+      const int ebeg = fwd ? i0 + BNB : 0, eend = fwd ? Np : i0;
+      // entries in chunks of ENT·PT (systems taller than ENT·PT + 32): the
+      // first chunk's slice loads are issued before the block's barrier
+      for (int cb = ebeg; cb == ebeg || cb < eend; cb += ENT * PT) {
+        double f[ENT][BNB];
+        int ev[ENT];
+        bool has[ENT];
 #pragma unroll
-      for (int q = 0; q < ENT; ++q) {
-        const int e = (fwd ? i0 + BNB : 0) + t + PT * q;
-        has[q] = fwd ? e < Np : e < i0;
-        ev[q] = e;
-        const int ec = has[q] ? e : i0;
-        if (!__any(has[q])) continue;   // the whole wave is past the entries: no loads
-        if (!trans) {
-          const double* row = Kb + (size_t)ps[ec] * ld + i0;
+        for (int q = 0; q < ENT; ++q) {
+          const int e = cb + t + PT * q;
+          has[q] = e < eend;
+          ev[q] = e;
+          const int ec = has[q] ? e : i0;
+          if (!__any(has[q])) continue;   // the whole wave is past the entries: no loads
+          if (!trans) {
+            const double* row = Kb + (size_t)ps[ec] * ld + i0;
 #pragma unroll
-          for (int j = 0; j < BNB; ++j) f[q][j] = row[j];
-        } else {
+            for (int j = 0; j < BNB; ++j) f[q][j] = row[j];
+          } else {
 #pragma unroll
-          for (int j = 0; j < BNB; ++j) f[q][j] = Kb[(size_t)ps[i0 + j] * ld + ec];
+            for (int j = 0; j < BNB; ++j) f[q][j] = Kb[(size_t)ps[i0 + j] * ld + ec];
+          }
         }
-      }
-      if (wv == 0 && lane < BNB) {
-        const double* Dk = Dbase + (size_t)bk * BDINV + (useU ? BNB * BNB : 0);
-        const int rs = trans ? 1 : BNB, cs = trans ? BNB : 1;   // row `lane` or column `lane`
-        double acc = 0.0;
+        if (cb == ebeg) {
+          if (wv == 0 && lane < BNB) {
+            const double* Dk = Dbase + (size_t)bk * BDINV + (useU ? BNB * BNB : 0);
+            const int rs = trans ? 1 : BNB, cs = trans ? BNB : 1;   // row `lane` or column `lane`
+            double acc = 0.0;
 #pragma unroll 8
-        for (int j = 0; j < BNB; ++j) acc = fma(Dk[lane * rs + j * cs], v[i0 + j], acc);
-        part[lane] = acc;
-      }
-      __syncthreads();
-      if (wv == 0 && lane < BNB) v[i0 + lane] = part[lane];
+            for (int j = 0; j < BNB; ++j) acc = fma(Dk[lane * rs + j * cs], v[i0 + j], acc);
+            part[lane] = acc;
+          }
+          __syncthreads();
+          if (wv == 0 && lane < BNB) v[i0 + lane] = part[lane];
+        }
 #pragma unroll
-      for (int q = 0; q < ENT; ++q) {
-        if (has[q]) {   // e lies outside block k: no thread reads v[e] in this step
-          double acc = v[ev[q]];
+        for (int q = 0; q < ENT; ++q) {
+          if (has[q]) {   // e lies outside block k: no thread reads v[e] in this step
+            double acc = v[ev[q]];
 #pragma unroll
-          for (int j = 0; j < BNB; ++j) acc = fma(-f[q][j], part[j], acc);
-          v[ev[q]] = acc;
+            for (int j = 0; j < BNB; ++j) acc = fma(-f[q][j], part[j], acc);
+            v[ev[q]] = acc;
+          }
         }
       }
       __syncthreads();
@@ -537,10 +554,12 @@ __global__ __launch_bounds__(PT) void blu_solve_kernel(const double* __restrict_
                                                        int trans, int sel,
                                                        const double* __restrict__ rhs,
                                                        double* __restrict__ xout) {
-  __shared__ double v[BLOCKED_MAX];
-  __shared__ double y[BLOCKED_MAX];
-  __shared__ int ps[BLOCKED_MAX];
+  extern __shared__ __attribute__((aligned(16))) double sdyn[];   // v, y (Np each), ps (Np ints)
   __shared__ double part[BNB];
+  const int np = solve_lds_np(nmax);
+  double* v = sdyn;
+  double* y = sdyn + np;
+  int* ps = reinterpret_cast<int*>(sdyn + 2 * np);
   solve_cols_body<ENT>(blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, trans, sel, rhs, xout,
                        v, y, ps, part);
 }
@@ -643,9 +662,11 @@ __global__ __launch_bounds__(PT) void blu_solve_rows_kernel(const double* __rest
                                                             const QPMeta* __restrict__ meta, int sel,
                                                             const double* __restrict__ rhs,
                                                             double* __restrict__ xout) {
-  __shared__ double v[BLOCKED_MAX];
-  __shared__ int ps[BLOCKED_MAX];
+  extern __shared__ __attribute__((aligned(16))) double sdyn[];
   __shared__ double part[BNB];
+  const int np = solve_lds_np(nmax);
+  double* v = sdyn;
+  int* ps = reinterpret_cast<int*>(sdyn + 2 * np);
   solve_rows_body(blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, sel, rhs, xout, v, ps, part);
 }
 
@@ -670,10 +691,12 @@ __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict
                                                         double* __restrict__ x_fwd,
                                                         const double* __restrict__ w_rev,
                                                         const double* __restrict__ w_fwd) {
-  __shared__ double v[BLOCKED_MAX];
-  __shared__ double y[BLOCKED_MAX];
-  __shared__ int ps[BLOCKED_MAX];
+  extern __shared__ __attribute__((aligned(16))) double sdyn[];
   __shared__ double part[BNB];
+  const int np = solve_lds_np(nmax);
+  double* v = sdyn;
+  double* y = sdyn + np;
+  int* ps = reinterpret_cast<int*>(sdyn + 2 * np);
   int L = blockIdx.x;
   if (B % 8 == 0) {   // workgroups 16g+j (rows) and 16g+8+j (columns) solve problem 8g+j
     const int g = L >> 4, j = L & 7;
@@ -698,7 +721,9 @@ __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict
 // everything right of and below the pair — half the trailing-matrix traffic of
 // rank-32 steps.  Sized by h.blocked_npmax (the read-back of the metadata).
 void qp_blocked_factor(Handle& h, double* dinv, const int32_t* plist, int count) {
-  const int npmax = h.blocked_npmax;
+  // problems with Np > PIVOT_MAX are skipped by the kernels (piv_np) and take
+  // the generic LU (qp.hip)
+  const int npmax = std::min(h.blocked_npmax, PIVOT_MAX);
   if (npmax == 0 || count == 0) return;
   const size_t dstride = dinv_stride(h.nmax);
   double* K = h.K.as<double>();
@@ -746,6 +771,14 @@ void qp_blocked_factor(Handle& h, double* dinv, const int32_t* plist, int count)
   }
 }
 
+// dynamic LDS above 64 KB (Np > ~3270) needs the per-kernel opt-in
+template <class KF>
+static void solve_lds_optin(KF kf, size_t lds) {
+  if (lds > 64 * 1024)
+    DOPT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kf), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds));
+}
+
 void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rhs, double* x, int sel) {
   const int npmax = h.blocked_npmax;
   if (npmax == 0) return;
@@ -754,22 +787,23 @@ void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rh
   const double* K = h.K.as<double>();
   const int32_t* perm = h.ipiv.as<int32_t>();
   const QPMeta* meta = h.meta.as<QPMeta>();
+  const size_t lds = solve_lds_bytes(h.nmax);
   if (!trans) {
-    hipLaunchKernelGGL(blu_solve_rows_kernel, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
+    solve_lds_optin(blu_solve_rows_kernel, lds);
+    hipLaunchKernelGGL(blu_solve_rows_kernel, dim3(B), dim3(PT), lds, h.stream, K, h.ld, h.nmax, perm,
                        dinv, dstride, meta, sel, rhs, x);
   } else {
     // Kᵀ x = b: the slices are column segments, contiguous across entries, so
     // one entry per thread is already coalesced
     const int ent = (npmax + PT - 1) / PT;
-    if (ent <= 1)
-      hipLaunchKernelGGL(blu_solve_kernel<1>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
-                         dinv, dstride, meta, trans, sel, rhs, x);
-    else if (ent == 2)
-      hipLaunchKernelGGL(blu_solve_kernel<2>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
-                         dinv, dstride, meta, trans, sel, rhs, x);
-    else
-      hipLaunchKernelGGL(blu_solve_kernel<3>, dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm,
-                         dinv, dstride, meta, trans, sel, rhs, x);
+#define DOPT_SOLVE1(E)                                                                               \
+  solve_lds_optin(blu_solve_kernel<E>, lds);                                                         \
+  hipLaunchKernelGGL(blu_solve_kernel<E>, dim3(B), dim3(PT), lds, h.stream, K, h.ld, h.nmax, perm, dinv, \
+                     dstride, meta, trans, sel, rhs, x)
+    if (ent <= 1) { DOPT_SOLVE1(1); }
+    else if (ent == 2) { DOPT_SOLVE1(2); }
+    else { DOPT_SOLVE1(3); }   // taller: chunks of 3·PT entries
+#undef DOPT_SOLVE1
   }
   DOPT_CHECK_HIP(hipGetLastError());
 }
@@ -785,12 +819,14 @@ void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, con
   const int32_t* perm = h.ipiv.as<int32_t>();
   const QPMeta* meta = h.meta.as<QPMeta>();
   const int ent = (npmax + PT - 1) / PT;
+  const size_t lds = solve_lds_bytes(h.nmax);
 #define DOPT_SOLVE2(E)                                                                            \
-  hipLaunchKernelGGL(blu_solve2_kernel<E>, dim3(2 * B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, perm, \
+  solve_lds_optin(blu_solve2_kernel<E>, lds);                                                     \
+  hipLaunchKernelGGL(blu_solve2_kernel<E>, dim3(2 * B), dim3(PT), lds, h.stream, K, h.ld, h.nmax, perm, \
                      dinv, dstride, meta, B, sel, rhs_rev, rhs_fwd, x_rev, x_fwd, w_rev, w_fwd)
-  if (ent <= 1) DOPT_SOLVE2(1);
-  else if (ent == 2) DOPT_SOLVE2(2);
-  else DOPT_SOLVE2(3);
+  if (ent <= 1) { DOPT_SOLVE2(1); }
+  else if (ent == 2) { DOPT_SOLVE2(2); }
+  else { DOPT_SOLVE2(3); }
 #undef DOPT_SOLVE2
   DOPT_CHECK_HIP(hipGetLastError());
 }

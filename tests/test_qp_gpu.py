@@ -316,9 +316,27 @@ def test_factor_then_reverse_forward(QPBatch, lu_mode):
         np.testing.assert_array_equal(f1, f2)
 
 
-def test_generic_large_system_path(QPBatch, lu_mode):
-    """Reduced system > 1536 unknowns takes the generic LU kernel."""
-    _check_batch(QPBatch, _synthetic(2, 1200, 700, 0, 0.6, 12), kinds=[PIVOT, PIVOT])
+def test_large_reduced_system_blocked_route(QPBatch, lu_mode):
+    """Reduced systems above the partial-pivoting panel's 1536 rows (here
+    1620) take the no-pivot blocked LU (taller solves run in entry chunks);
+    with DOPT_LU=0 they take the generic LU."""
+    _check_batch(QPBatch, _synthetic(2, 1200, 700, 0, 0.6, 12),
+                 kinds=[NOPIV if lu_mode == "nopiv" else PIVOT] * 2)
+
+
+def test_large_rejected_problem_takes_generic_lu(QPBatch):
+    """A tall problem (reduced size > 1536) the no-pivot LU rejects is
+    re-assembled and factorised by the generic LU, next to accepted ones and a
+    small rejected one (partial-pivoting blocked LU) in the same batch."""
+    d = _indefinite(_synthetic(3, 1200, 700, 0, 0.6, 13), [1])
+    _check_batch(QPBatch, d, kinds=[NOPIV, PIVOT, NOPIV])
+
+
+def test_config3_no_elimination_shape(QPBatch):
+    """Config 3 with interior-point-like duals (λ = 1e-9 on inactive rows,
+    nothing eliminated: N' = 2500, the `--lam-eps` bench case) on the blocked
+    route, two problems against the oracle."""
+    _check_batch(QPBatch, _synthetic(2, 1000, 1500, 0, 0.3, 14, lam_eps=1e-9), kinds=[NOPIV] * 2)
 
 
 def test_singular_kkt_raises(QPBatch, lu_mode):
