@@ -120,6 +120,7 @@ struct Handle {
   DevBuf binv;               // no-pivot LU: packed 64×64 inverse of the current diagonal block
   DevBuf fwdw;               // fused call: both right-hand sides, forward-swept inside the no-pivot LU
   DevBuf krhs, kx, kfull;    // multi-RHS calls: k seeds' reduced RHS, solutions, full forward RHS
+  DevBuf mws;                // multi-RHS: per-workgroup vectors of tall systems (qp_multi.hip)
   QPMeta* meta_host = nullptr;     // pinned copy of `meta` (asynchronous read-back)
   hipEvent_t meta_ev = nullptr;    // recorded after the read-back copy
   // factorisation: 1 = no-pivot blocked LU with the threshold test and a

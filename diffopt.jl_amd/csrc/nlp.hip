@@ -499,16 +499,9 @@ void nlp_reverse(Handle& h, const double* dx, const double* ddual, double* dp) {
 }
 
 // k right-hand sides per problem (seed-major, stride B·nmax) through the
-// blocked factors: the multi-RHS kernel when its LDS chunk fits, else one
-// solve per seed
+// blocked factors, one multi-RHS launch
 static void solve_multi(Handle& h, int trans, int k, double* rk, double* xk) {
-  const size_t lds = (size_t)h.blocked_npmax * (16 * sizeof(double) + sizeof(int));
-  if (lds <= 160 * 1024) {
-    qp_blocked_solve_multi(h, dense_dinv(h), trans, k, rk, xk, LU_SEL_ALL);
-  } else {
-    const size_t blk = (size_t)h.batch * h.nmax;
-    for (int j = 0; j < k; ++j) qp_blocked_solve(h, dense_dinv(h), trans, rk + j * blk, xk + j * blk, LU_SEL_ALL);
-  }
+  qp_blocked_solve_multi(h, dense_dinv(h), trans, k, rk, xk, LU_SEL_ALL);
 }
 
 void nlp_jacobian(Handle& h, double* ds) {

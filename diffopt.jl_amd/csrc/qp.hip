@@ -1009,12 +1009,7 @@ static void solve_k(Handle& h, int trans, int k, double* rk, double* xk, double*
   const int B = (int)h.batch, n = h.n, m = h.m, p = h.p, nmax = h.nmax;
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
-    const size_t lds = (size_t)h.blocked_npmax * (16 * sizeof(double) + sizeof(int));
-    if (lds <= 160 * 1024) {
-      qp_blocked_solve_multi(h, dinv_of(h), trans, k, rk, xk, LU_SEL_ALL);
-    } else {   // the chunk does not fit LDS: one single-RHS solve per seed
-      for (int j = 0; j < k; ++j) qp_blocked_solve(h, dinv_of(h), trans, rk + j * blk, xk + j * blk, LU_SEL_ALL);
-    }
+    qp_blocked_solve_multi(h, dinv_of(h), trans, k, rk, xk, LU_SEL_ALL);
   }
   // generic / LSQR routes per seed, then every seed's outputs in one launch
   QPMeta* meta = h.meta.as<QPMeta>();

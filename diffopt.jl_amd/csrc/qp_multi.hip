@@ -14,6 +14,9 @@
 //                          tile e, M = L or U (Kᵀ: Uᵀ, Lᵀ), waves 0–3
 // so K is read once per 16 right-hand sides instead of once per seed.
 // Chunks of one problem share an XCD (blockIdx = chunk·B + b, B % 8 == 0).
+// Systems whose chunk does not fit LDS (Np > ~1190) keep V in a per-
+// workgroup global workspace instead (GV; L2-resident for the workgroup's
+// lifetime) — same code, K still read once per 16 right-hand sides.
 //
 //   trans 0:  K x = b   →  L U x = P b
 //   trans 1:  Kᵀ x = b  →  Uᵀ w = b, Lᵀ v = w, x = Pᵀ v
@@ -40,13 +43,14 @@ __device__ __forceinline__ int multi_np(const QPMeta& mm) {
   return (mm.nsys + MBN - 1) & ~(MBN - 1);
 }
 
-template <int TRANS>
+template <int TRANS, bool GV>
 __global__ __launch_bounds__(MT) void blu_solve_multi_kernel(const double* __restrict__ K, int ld, int nmax,
                                                              const int32_t* __restrict__ perm,
                                                              const double* __restrict__ dinv, size_t dstride,
                                                              const QPMeta* __restrict__ meta, int B, int k,
                                                              int sel, const double* __restrict__ rhs,
-                                                             double* __restrict__ xout) {
+                                                             double* __restrict__ xout, double* __restrict__ gws,
+                                                             int npmax) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x % B, chunk = blockIdx.x / B;
   const QPMeta mm = meta[b];
@@ -54,8 +58,9 @@ __global__ __launch_bounds__(MT) void blu_solve_multi_kernel(const double* __res
   if (Np == 0 || !((sel >> mm.lu) & 1)) return;   // workgroup-uniform
   const int N = mm.nsys;
   const int j0 = chunk * MKC, kc = min(MKC, k - j0);
-  double* V = smem;                                 // Np × MKC (row-major)
-  int* ps = reinterpret_cast<int*>(V + (size_t)Np * MKC);
+  // Np × MKC (row-major): LDS, or this workgroup's global workspace
+  double* V = GV ? gws + (size_t)blockIdx.x * npmax * MKC : smem;
+  int* ps = reinterpret_cast<int*>(GV ? smem : V + (size_t)Np * MKC);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
   const double* Kb = K + (size_t)b * nmax * ld;
   const double* Db = dinv + (size_t)b * dstride;
@@ -143,26 +148,34 @@ void qp_blocked_solve_multi(Handle& h, const double* dinv, int trans, int k, con
   const int nck = (k + MKC - 1) / MKC;
   const long long grid = (long long)nck * B;
   if (grid > 0x7fffffffLL) throw Error(-1, "multi-RHS solve: grid too large");
-  const size_t lds = (size_t)npmax * MKC * sizeof(double) + (size_t)npmax * sizeof(int);
-  if (lds > 160 * 1024) throw Error(-1, "multi-RHS solve: system too large for the LDS-resident chunk");
+  const size_t lds_v = (size_t)npmax * MKC * sizeof(double) + (size_t)npmax * sizeof(int);
+  const bool gv = lds_v > 150 * 1024;   // the chunk's V in global memory, ps alone in LDS
+  const size_t lds = gv ? (size_t)npmax * sizeof(int) : lds_v;
+  double* gws = nullptr;
+  if (gv) {
+    h.mws.ensure((size_t)grid * npmax * MKC * sizeof(double));
+    gws = h.mws.as<double>();
+  }
   const size_t dstride = dinv_stride(h.nmax);
   const double* K = h.K.as<double>();
   const int32_t* perm = h.ipiv.as<int32_t>();
   const QPMeta* meta = h.meta.as<QPMeta>();
-  // dynamic LDS above the 64 KB default (Np > ~480) needs the opt-in (per
-  // device: set on the handle's current device before each such launch)
-  if (lds > 64 * 1024) {
-    DOPT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&blu_solve_multi_kernel<0>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    DOPT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&blu_solve_multi_kernel<1>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+#define DOPT_MULTI(T, G)                                                                                 \
+  do {                                                                                                   \
+    /* dynamic LDS above the 64 KB default needs the opt-in (per device: set on the handle's current  */ \
+    /* device before each such launch)                                                                */ \
+    if (lds > 64 * 1024)                                                                                 \
+      DOPT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&blu_solve_multi_kernel<T, G>),  \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));         \
+    hipLaunchKernelGGL((blu_solve_multi_kernel<T, G>), dim3((unsigned)grid), dim3(MT), lds, h.stream, K, h.ld, \
+                       h.nmax, perm, dinv, dstride, meta, B, k, sel, rhs, x, gws, npmax);               \
+  } while (0)
+  if (trans) {
+    if (gv) DOPT_MULTI(1, true); else DOPT_MULTI(1, false);
+  } else {
+    if (gv) DOPT_MULTI(0, true); else DOPT_MULTI(0, false);
   }
-  if (trans)
-    hipLaunchKernelGGL(blu_solve_multi_kernel<1>, dim3((unsigned)grid), dim3(MT), lds, h.stream, K, h.ld, h.nmax,
-                       perm, dinv, dstride, meta, B, k, sel, rhs, x);
-  else
-    hipLaunchKernelGGL(blu_solve_multi_kernel<0>, dim3((unsigned)grid), dim3(MT), lds, h.stream, K, h.ld, h.nmax,
-                       perm, dinv, dstride, meta, B, k, sel, rhs, x);
+#undef DOPT_MULTI
   DOPT_CHECK_HIP(hipGetLastError());
 }
 

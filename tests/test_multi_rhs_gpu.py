@@ -101,6 +101,13 @@ def test_multi_rhs_large_system_lds_opt_in(QPBatch):
     assert (e.system_size() == 500).all()
 
 
+def test_multi_rhs_tall_system_global_chunk(QPBatch):
+    """Config-3 shape (N' ≈ 1600, Np > 1190): the 16-seed chunk (≥ 150 KB)
+    does not fit LDS and lives in a global workspace — one launch still."""
+    d = _data(2, 1000, 1500, 0, 606, 7)
+    _check(QPBatch, d, 7, oracle_problems=[0])
+
+
 def test_multi_rhs_mixed_factor_kinds(QPBatch):
     """No-pivot and partial-pivoting problems in one batch (relabelled rows)."""
     d = _data(6, 60, 80, 5, 404, 7)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Multi-RHS timing on config 2 (device-resident inputs, one factorisation):
+"""Multi-RHS timing on config 2 or 3 (device-resident inputs, one factorisation):
 k single-seed dopt_qp_reverse / _forward calls against one dopt_qp_reverse_k /
 _forward_k call (qp_multi.hip).  Prints one JSON line per k.
 
@@ -17,6 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "diffopt.jl_amd"))
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3])
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--k", type=int, nargs="+", default=[1, 7, 32])
     ap.add_argument("--reps", type=int, default=3)
@@ -24,9 +25,9 @@ def main():
     import torch
     from diffopt_amd.qp import QPBatch
     from diffopt_amd.synthetic import QP_CONFIGS, SEED0, qp_torch
-    c = QP_CONFIGS[2]
+    c = QP_CONFIGS[a.config]
     B, n, m, p = a.batch, c["n"], c["m"], c["p"]
-    d = qp_torch(B, n, m, p, c["phi"], SEED0 + 2)
+    d = qp_torch(B, n, m, p, c["phi"], SEED0 + a.config)
     e = QPBatch(B, n, m, p)
     e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
     e.factor()
@@ -51,7 +52,7 @@ def main():
         t_multi_r = timed(lambda: e.reverse_k(dl))
         t_loop_f = timed(lambda: [e.forward(dq=dq[j]) for j in range(k)])
         t_multi_f = timed(lambda: e.forward_k(dq=dq))
-        print(json.dumps({"config": "config 2 (n=200, m=300), factor kept", "batch": B, "k": k,
+        print(json.dumps({"config": f"config {a.config} (n={n}, m={m}), factor kept", "batch": B, "k": k,
                           "reverse_loop_ms": round(1e3 * t_loop_r, 3), "reverse_k_ms": round(1e3 * t_multi_r, 3),
                           "forward_loop_ms": round(1e3 * t_loop_f, 3), "forward_k_ms": round(1e3 * t_multi_f, 3),
                           "seed_solves_per_s_k": round(2 * k * B / (t_multi_r + t_multi_f), 1),
