@@ -386,7 +386,8 @@ __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, con
       double* g = gws + cd.woff;
       psd_apply_cone(cd, P, in, out, trans, g, g + img, g + 2 * img);
     } else {
-      psd_apply_cone(cd, P, in, out, trans, lds, lds + PSD_MAX * (PSD_MAX + 1), lds + 2 * PSD_MAX * (PSD_MAX + 1));
+      const size_t img = (size_t)((d + 3) & ~3) * (((d + 3) & ~3) + 1);   // this cone's image: dp × (dp+1)
+      psd_apply_cone(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
     }
   }
   __syncthreads();
@@ -1509,10 +1510,20 @@ __global__ __launch_bounds__(CTPB) void conic_split_out_kernel(
 // ---------------------------------------------------------------------------
 static void ccheck() { DOPT_CHECK_HIP(hipGetLastError()); }
 
+// dynamic LDS of the Dπ apply: three dp × (dp+1) images of the largest PSD
+// cone up to PSD_MAX (larger ones use global scratch) — sized to the cones
+// present, so small-PSD batches keep two or more workgroups per CU
 static size_t dpi_lds_bytes(const std::vector<int32_t>& cones) {
+  size_t best = 16;
   for (size_t k = 0; k < cones.size() / 2; ++k)
-    if (cones[2 * k] == DOPT_CONE_PSD_TRI) return (size_t)3 * PSD_MAX * (PSD_MAX + 1) * sizeof(double);
-  return 16;
+    if (cones[2 * k] == DOPT_CONE_PSD_TRI) {
+      int d = 0;
+      while ((d + 1) * (d + 2) / 2 <= cones[2 * k + 1]) ++d;
+      if (d > PSD_MAX) continue;
+      const size_t dp = (size_t)((d + 3) & ~3);
+      best = std::max(best, 3 * dp * (dp + 1) * sizeof(double));
+    }
+  return best;
 }
 
 void conic_factor(Handle& h) {

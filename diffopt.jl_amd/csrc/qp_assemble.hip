@@ -319,7 +319,33 @@ __global__ __launch_bounds__(ATH) void qp_asm_tile_kernel(QPIn P, const int32_t*
   // tile at (r0, c0) into Ts[slot]; rng_r / rng_c: the staged index ranges
   // holding rows r0.. / columns c0..
   auto tile_load = [&](int r0, int c0, int rng_r, int rng_c, double* Tl) {
-    if (c0 < n) {
+    // rows all inside Q, or all inside the compacted G_k copy, with even
+    // offsets and strides: row pairs as 16-byte loads (tile-uniform choice)
+    const double* vbase = nullptr;
+    size_t vstride = 0;
+    if (c0 < n && r0 + AT <= Np) {
+      if (r0 + AT <= n && (n & 1) == 0) { vbase = Qb + r0; vstride = n; }
+      else if (gk_ok && r0 >= n && r0 + AT <= n + nk && ((r0 - n) & 1) == 0 && (m & 1) == 0) {
+        vbase = gkb + (r0 - n); vstride = m;
+      }
+    }
+    if (vbase) {
+      const int rp = t & 31, cg = t >> 5;   // rows 2rp, 2rp+1; columns c0 + cg + 16k
+      dv2 w[AT / 16];
+#pragma unroll
+      for (int k = 0; k < AT / 16; ++k) {
+        const int c = c0 + cg + 16 * k;
+        w[k] = *reinterpret_cast<const dv2*>(vbase + (size_t)(c < n ? c : 0) * vstride + 2 * rp);
+      }
+#pragma unroll
+      for (int k = 0; k < AT / 16; ++k) {
+        const int c = c0 + cg + 16 * k;
+        if (c < n) {
+          Tl[(2 * rp) * ATLD + cg + 16 * k] = w[k].x;
+          Tl[(2 * rp + 1) * ATLD + cg + 16 * k] = w[k].y;
+        }
+      }
+    } else if (c0 < n) {
       const int r = r0 + tr;
       const double* base = Qb;
       size_t cs = 0;
