@@ -452,12 +452,29 @@ __global__ __launch_bounds__(256) void blu_update_kernel(double* __restrict__ K,
 // per thread; all their slice loads are issued before the block's barrier.
 // rhs / x: per problem stride nmax, length nsys.
 // ---------------------------------------------------------------------------
-// dynamic LDS of the solve kernels: v, y (doubles) and ps (ints), each
+// LDS of the solve kernels: v, y (doubles) and ps (ints).  Systems up to
+// SOLVE_STATIC rows (ENT ≤ 3 without entry chunks) use static arrays — the
+// compiler then keeps the diagonal GEMV's dinv loads in flight together
+// (with the arrays behind a dynamic-LDS pointer it issued them one by one:
+// 2.9× slower cols solves at Np = 608); taller ones (TALL) use dynamic LDS,
+// min(nmax, BLOCKED_MAX) long.
+constexpr int SOLVE_STATIC = 3 * PT + BNB;
+#define SOLVE_LDS(TALLV)                                                              \
+  __shared__ double part[BNB];                                                        \
+  __shared__ double v_st[TALLV ? 1 : SOLVE_STATIC], y_st[TALLV ? 1 : SOLVE_STATIC];    \
+  __shared__ int ps_st[TALLV ? 1 : SOLVE_STATIC];                                      \
+  extern __shared__ __attribute__((aligned(16))) double sdyn[];                       \
+  const int np_ = solve_lds_np(nmax);                                                 \
+  double* v = TALLV ? sdyn : v_st;                                                    \
+  double* y = TALLV ? sdyn + np_ : y_st;                                              \
+  int* ps = TALLV ? reinterpret_cast<int*>(sdyn + 2 * np_) : ps_st;                   \
+  (void)y
+// dynamic LDS of the TALL solve kernels: v, y (doubles) and ps (ints), each
 // min(nmax, BLOCKED_MAX) long (a blocked problem's Np never exceeds either)
 __host__ __device__ inline int solve_lds_np(int nmax) { return nmax < BLOCKED_MAX ? nmax : BLOCKED_MAX; }
 __host__ inline size_t solve_lds_bytes(int nmax) { return (size_t)solve_lds_np(nmax) * (2 * sizeof(double) + sizeof(int)); }
 
-template <int ENT>
+template <int ENT, bool TALL = false>
 __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict__ K, int ld, int nmax,
                                                 const int32_t* __restrict__ perm,
                                                 const double* __restrict__ dinv, size_t dstride,
@@ -488,9 +505,50 @@ __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict_
     for (int s = 0; s < nblk; ++s) {
       const int bk = fwd ? s : nblk - 1 - s;
       const int i0 = bk * BNB;
+      if constexpr (!TALL) {
       const int ebeg = fwd ? i0 + BNB : 0, eend = fwd ? Np : i0;
-      // entries in chunks of ENT·PT (systems taller than ENT·PT + 32): the
-      // first chunk's slice loads are issued before the block's barrier
+      double f[ENT][BNB];
+      int ev[ENT];
+      bool has[ENT];
+#pragma unroll
+      for (int q = 0; q < ENT; ++q) {
+        const int e = ebeg + t + PT * q;
+        has[q] = e < eend;
+        ev[q] = e;
+        const int ec = has[q] ? e : i0;
+        if (!__any(has[q])) continue;   // the whole wave is past the entries: no loads
+        if (!trans) {
+          const double* row = Kb + (size_t)ps[ec] * ld + i0;
+#pragma unroll
+          for (int j = 0; j < BNB; ++j) f[q][j] = row[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < BNB; ++j) f[q][j] = Kb[(size_t)ps[i0 + j] * ld + ec];
+        }
+      }
+      if (wv == 0 && lane < BNB) {
+        const double* Dk = Dbase + (size_t)bk * BDINV + (useU ? BNB * BNB : 0);
+        const int rs = trans ? 1 : BNB, cs = trans ? BNB : 1;   // row `lane` or column `lane`
+        double acc = 0.0;
+#pragma unroll 8
+        for (int j = 0; j < BNB; ++j) acc = fma(Dk[lane * rs + j * cs], v[i0 + j], acc);
+        part[lane] = acc;
+      }
+      __syncthreads();
+      if (wv == 0 && lane < BNB) v[i0 + lane] = part[lane];
+#pragma unroll
+      for (int q = 0; q < ENT; ++q) {
+        if (has[q]) {   // e lies outside block k: no thread reads v[e] in this step
+          double acc = v[ev[q]];
+#pragma unroll
+          for (int j = 0; j < BNB; ++j) acc = fma(-f[q][j], part[j], acc);
+          v[ev[q]] = acc;
+        }
+      }
+      } else {
+      const int ebeg = fwd ? i0 + BNB : 0, eend = fwd ? Np : i0;
+      // entries in chunks of ENT·PT; the first chunk's slice loads are issued
+      // before the block's barrier
       for (int cb = ebeg; cb == ebeg || cb < eend; cb += ENT * PT) {
         double f[ENT][BNB];
         int ev[ENT];
@@ -501,7 +559,7 @@ __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict_
           has[q] = e < eend;
           ev[q] = e;
           const int ec = has[q] ? e : i0;
-          if (!__any(has[q])) continue;   // the whole wave is past the entries: no loads
+          if (!__any(has[q])) continue;
           if (!trans) {
             const double* row = Kb + (size_t)ps[ec] * ld + i0;
 #pragma unroll
@@ -514,7 +572,7 @@ __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict_
         if (cb == ebeg) {
           if (wv == 0 && lane < BNB) {
             const double* Dk = Dbase + (size_t)bk * BDINV + (useU ? BNB * BNB : 0);
-            const int rs = trans ? 1 : BNB, cs = trans ? BNB : 1;   // row `lane` or column `lane`
+            const int rs = trans ? 1 : BNB, cs = trans ? BNB : 1;
             double acc = 0.0;
 #pragma unroll 8
             for (int j = 0; j < BNB; ++j) acc = fma(Dk[lane * rs + j * cs], v[i0 + j], acc);
@@ -525,13 +583,14 @@ __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict_
         }
 #pragma unroll
         for (int q = 0; q < ENT; ++q) {
-          if (has[q]) {   // e lies outside block k: no thread reads v[e] in this step
+          if (has[q]) {
             double acc = v[ev[q]];
 #pragma unroll
             for (int j = 0; j < BNB; ++j) acc = fma(-f[q][j], part[j], acc);
             v[ev[q]] = acc;
           }
         }
+      }
       }
       __syncthreads();
     }
@@ -546,7 +605,7 @@ __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict_
   }
 }
 
-template <int ENT>
+template <int ENT, bool TALL = false>
 __global__ __launch_bounds__(PT) void blu_solve_kernel(const double* __restrict__ K, int ld, int nmax,
                                                        const int32_t* __restrict__ perm,
                                                        const double* __restrict__ dinv,
@@ -554,13 +613,8 @@ __global__ __launch_bounds__(PT) void blu_solve_kernel(const double* __restrict_
                                                        int trans, int sel,
                                                        const double* __restrict__ rhs,
                                                        double* __restrict__ xout) {
-  extern __shared__ __attribute__((aligned(16))) double sdyn[];   // v, y (Np each), ps (Np ints)
-  __shared__ double part[BNB];
-  const int np = solve_lds_np(nmax);
-  double* v = sdyn;
-  double* y = sdyn + np;
-  int* ps = reinterpret_cast<int*>(sdyn + 2 * np);
-  solve_cols_body<ENT>(blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, trans, sel, rhs, xout,
+  SOLVE_LDS(TALL);
+  solve_cols_body<ENT, TALL>(blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, trans, sel, rhs, xout,
                        v, y, ps, part);
 }
 
@@ -679,7 +733,7 @@ __global__ __launch_bounds__(PT) void blu_solve_rows_kernel(const double* __rest
 // forward-swept inside the no-pivot LU (qp_nopiv.hip fwd_block) — its
 // problems run only the backward sweeps from them; partial-pivoting problems
 // solve from rhs_rev / rhs_fwd in full.
-template <int ENT>
+template <int ENT, bool TALL = false>
 __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict__ K, int ld, int nmax,
                                                         const int32_t* __restrict__ perm,
                                                         const double* __restrict__ dinv,
@@ -691,12 +745,7 @@ __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict
                                                         double* __restrict__ x_fwd,
                                                         const double* __restrict__ w_rev,
                                                         const double* __restrict__ w_fwd) {
-  extern __shared__ __attribute__((aligned(16))) double sdyn[];
-  __shared__ double part[BNB];
-  const int np = solve_lds_np(nmax);
-  double* v = sdyn;
-  double* y = sdyn + np;
-  int* ps = reinterpret_cast<int*>(sdyn + 2 * np);
+  SOLVE_LDS(TALL);
   int L = blockIdx.x;
   if (B % 8 == 0) {   // workgroups 16g+j (rows) and 16g+8+j (columns) solve problem 8g+j
     const int g = L >> 4, j = L & 7;
@@ -708,7 +757,7 @@ __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict
     solve_rows_body(L, K, ld, nmax, perm, dinv, dstride, meta, sel, swept ? w_rev : rhs_rev, x_rev, v, ps, part,
                     swept ? 1 : 0);
   else
-    solve_cols_body<ENT>(L - B, K, ld, nmax, perm, dinv, dstride, meta, 1, sel, swept ? w_fwd : rhs_fwd, x_fwd, v,
+    solve_cols_body<ENT, TALL>(L - B, K, ld, nmax, perm, dinv, dstride, meta, 1, sel, swept ? w_fwd : rhs_fwd, x_fwd, v,
                          y, ps, part, swept ? 1 : 0);
 }
 
@@ -796,13 +845,14 @@ void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rh
     // Kᵀ x = b: the slices are column segments, contiguous across entries, so
     // one entry per thread is already coalesced
     const int ent = (npmax + PT - 1) / PT;
-#define DOPT_SOLVE1(E)                                                                               \
-  solve_lds_optin(blu_solve_kernel<E>, lds);                                                         \
-  hipLaunchKernelGGL(blu_solve_kernel<E>, dim3(B), dim3(PT), lds, h.stream, K, h.ld, h.nmax, perm, dinv, \
+#define DOPT_SOLVE1(E, T)                                                                            \
+  solve_lds_optin(blu_solve_kernel<E, T>, T ? lds : 0);                                              \
+  hipLaunchKernelGGL((blu_solve_kernel<E, T>), dim3(B), dim3(PT), T ? lds : 0, h.stream, K, h.ld, h.nmax, perm, dinv, \
                      dstride, meta, trans, sel, rhs, x)
-    if (ent <= 1) { DOPT_SOLVE1(1); }
-    else if (ent == 2) { DOPT_SOLVE1(2); }
-    else { DOPT_SOLVE1(3); }   // taller: chunks of 3·PT entries
+    if (ent <= 1) { DOPT_SOLVE1(1, false); }
+    else if (ent == 2) { DOPT_SOLVE1(2, false); }
+    else if (npmax <= SOLVE_STATIC) { DOPT_SOLVE1(3, false); }
+    else { DOPT_SOLVE1(3, true); }   // taller: chunks of 3·PT entries
 #undef DOPT_SOLVE1
   }
   DOPT_CHECK_HIP(hipGetLastError());
@@ -820,13 +870,14 @@ void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, con
   const QPMeta* meta = h.meta.as<QPMeta>();
   const int ent = (npmax + PT - 1) / PT;
   const size_t lds = solve_lds_bytes(h.nmax);
-#define DOPT_SOLVE2(E)                                                                            \
-  solve_lds_optin(blu_solve2_kernel<E>, lds);                                                     \
-  hipLaunchKernelGGL(blu_solve2_kernel<E>, dim3(2 * B), dim3(PT), lds, h.stream, K, h.ld, h.nmax, perm, \
+#define DOPT_SOLVE2(E, T)                                                                         \
+  solve_lds_optin(blu_solve2_kernel<E, T>, T ? lds : 0);                                          \
+  hipLaunchKernelGGL((blu_solve2_kernel<E, T>), dim3(2 * B), dim3(PT), T ? lds : 0, h.stream, K, h.ld, h.nmax, perm, \
                      dinv, dstride, meta, B, sel, rhs_rev, rhs_fwd, x_rev, x_fwd, w_rev, w_fwd)
-  if (ent <= 1) { DOPT_SOLVE2(1); }
-  else if (ent == 2) { DOPT_SOLVE2(2); }
-  else { DOPT_SOLVE2(3); }
+  if (ent <= 1) { DOPT_SOLVE2(1, false); }
+  else if (ent == 2) { DOPT_SOLVE2(2, false); }
+  else if (npmax <= SOLVE_STATIC) { DOPT_SOLVE2(3, false); }
+  else { DOPT_SOLVE2(3, true); }   // taller: chunks of 3·PT entries
 #undef DOPT_SOLVE2
   DOPT_CHECK_HIP(hipGetLastError());
 }
