@@ -400,7 +400,10 @@ __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, con
 // j ≡ wv (mod 4), so g[j] needs only an in-wave reduction and y's four
 // per-wave partials are summed through LDS (`ys`, 4·PAIR_ROWS doubles).
 // PAIR_NC columns are in flight per wave (PAIR_NC·PAIR_K independent loads).
-constexpr int PAIR_K = 8;
+#ifndef DOPT_PAIR_K
+#define DOPT_PAIR_K 8   // tuning builds: -DDOPT_PAIR_K
+#endif
+constexpr int PAIR_K = DOPT_PAIR_K;
 #ifndef DOPT_PAIR_NC
 #define DOPT_PAIR_NC 3   // r01f sweep on config 4: 1 → 458, 2 → 570, 3 → 587, 4 → 530 solves/s
 #endif
