@@ -439,10 +439,14 @@ int dopt_qp_forward_reverse(dopt_handle* h, const double* dl_dz, const double* d
     double* o1 = out_ptr(*h, h->tout[0], out_rev, B * L);
     double* o2 = out_ptr(*h, h->tout[1], out_fwd, B * L);
     h->factored = false;  // one solve = factor + fwd + rev (the factors are kept for later calls)
+    h->info_clear = false;
     dopt::qp_forward_reverse(*h, r, a, b, c, d, e, f, o1, o2);
     copy_out(*h, out_rev, o1, B * L);
     copy_out(*h, out_fwd, o2, B * L);
-    const int rc = first_info(*h);
+    // device mode with every info known to be 0: stream-ordered return (the
+    // outputs land on the handle's stream, i.e. the caller's); else the
+    // synchronous check of the first singular problem
+    const int rc = (h->mem == DOPT_MEM_DEVICE && h->info_clear) ? 0 : first_info(*h);
     h->last_time = tm.s();
     return rc;
   });

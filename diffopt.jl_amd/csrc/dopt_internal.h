@@ -130,6 +130,7 @@ struct Handle {
   int32_t blocked_npmax = 0;       // largest padded blocked system of the current factorisation
   bool has_generic = true;         // some problem exceeds BLOCKED_MAX
   int32_t n_generic = 0;           // problems factorised by the generic LU (last factorisation)
+  bool info_clear = false;         // last factorisation: every problem's info is known to be 0 on the host
   bool has_lsqr = true;            // some problem takes the LSQR branch
   int32_t n_pivot = 0;             // problems factorised with partial pivoting (last factorisation)
   bool set = false, factored = false;

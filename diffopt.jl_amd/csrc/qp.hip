@@ -1137,6 +1137,10 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
   finish(h, 0, out_rev);
   finish(h, 1, out_fwd);
   h.factored = true;   // the factors stay valid for later reverse / forward calls
+  // the host already knows every info: the no-pivot LU accepted every blocked
+  // problem (an accepted factor has no zero pivot) and no fallback or generic
+  // LU ran — the ABI can then return before the outputs land (device mode)
+  h.info_clear = h.lu_mode == 1 && h.n_pivot == 0 && h.n_generic == 0;
 }
 
 }  // namespace dopt

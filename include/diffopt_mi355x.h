@@ -29,7 +29,8 @@
  *     Per-problem info: dopt_get_info().
  *   - Threading: a handle is used by one host thread at a time (the reference
  *     models are not thread-safe either).  Work runs on the handle's HIP stream;
- *     every call is synchronous at return.
+ *     every call is synchronous at return (except a device-mode
+ *     dopt_qp_forward_reverse with no singular problem: stream-ordered).
  */
 #ifndef DIFFOPT_MI355X_H
 #define DIFFOPT_MI355X_H
@@ -149,7 +150,12 @@ int dopt_qp_forward_k(dopt_handle* h, int32_t k, const double* dQ, const double*
                       const double* dG, const double* dh, const double* dA,
                       const double* db, double* out);
 /* Fused forward + reverse for one factorisation (the batched throughput path;
- * results identical to dopt_qp_reverse + dopt_qp_forward). */
+ * results identical to dopt_qp_reverse + dopt_qp_forward).  In device memory
+ * mode, when every problem's factorisation is known on the host to be
+ * non-singular (the no-pivot LU accepted all blocked problems), the call
+ * returns once the work is queued: the outputs are stream-ordered on the
+ * handle's stream (the caller's, dopt_set_stream) like any library call on
+ * that stream; otherwise it returns after the singularity check. */
 int dopt_qp_forward_reverse(dopt_handle* h, const double* dl_dz,
                             const double* dQ, const double* dq,
                             const double* dG, const double* dh,
