@@ -383,10 +383,14 @@ __global__ __launch_bounds__(TPB) void qp_lsqr_kernel(
 // reverse RHS: [dl_dz; 0] reduced (QuadraticProgram.jl:329)
 __global__ __launch_bounds__(TPB) void qp_rev_rhs_kernel(
     const double* __restrict__ dl_dz, const QPMeta* __restrict__ meta, int n,
-    int nmax, double* __restrict__ rhs) {
+    int nmax, double* __restrict__ rhs, double* __restrict__ rhs2) {
   const int b = blockIdx.x, t = threadIdx.x;
   const int N = meta[b].nsys;
-  for (int i = t; i < N; i += TPB) rhs[(size_t)b * nmax + i] = (i < n) ? dl_dz[(size_t)b * n + i] : 0.0;
+  for (int i = t; i < N; i += TPB) {
+    const double v = (i < n) ? dl_dz[(size_t)b * n + i] : 0.0;
+    rhs[(size_t)b * nmax + i] = v;
+    if (rhs2) rhs2[(size_t)b * nmax + i] = v;   // the fused call's forward-swept copy
+  }
 }
 
 // forward RHS (QuadraticProgram.jl:429-433):
@@ -401,7 +405,7 @@ __global__ __launch_bounds__(TPB) void qp_fwd_rhs_kernel(
     const double* __restrict__ z, const double* __restrict__ lam,
     const double* __restrict__ nu, const int32_t* __restrict__ rpos,
     const QPMeta* __restrict__ meta, int n, int m, int p, int nmax, int zcap,
-    double* __restrict__ full, double* __restrict__ rhs) {
+    double* __restrict__ full, double* __restrict__ rhs, double* __restrict__ rhs2) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const double* zg = z + (size_t)b * n;
@@ -466,12 +470,22 @@ __global__ __launch_bounds__(TPB) void qp_fwd_rhs_kernel(
   __syncthreads();   // r (global) complete within the workgroup
   const int nk = meta[b].nk;
   double* rb = rhs + (size_t)b * nmax;
-  for (int i = t; i < n; i += TPB) rb[i] = r[i];
+  double* rb2 = rhs2 ? rhs2 + (size_t)b * nmax : nullptr;   // the fused call's forward-swept copy
+  for (int i = t; i < n; i += TPB) {
+    rb[i] = r[i];
+    if (rb2) rb2[i] = r[i];
+  }
   for (int l = t; l < m; l += TPB) {
     const int kk = rpos[(size_t)b * m + l];
-    if (kk >= 0) rb[n + kk] = r[n + l];
+    if (kk >= 0) {
+      rb[n + kk] = r[n + l];
+      if (rb2) rb2[n + kk] = r[n + l];
+    }
   }
-  for (int e = t; e < p; e += TPB) rb[n + nk + e] = r[n + m + e];
+  for (int e = t; e < p; e += TPB) {
+    rb[n + nk + e] = r[n + m + e];
+    if (rb2) rb2[n + nk + e] = r[n + m + e];
+  }
 }
 
 // outputs: out = −[x_z | x_λ (scattered to all m rows) | x_ν]
@@ -947,24 +961,24 @@ static void finish(Handle& h, int trans, double* out) {
   finish_into(h, trans, rhs_of(h, trans), x_of(h, trans), full_of(h), out);
 }
 
-static void rev_rhs(Handle& h, const double* dl_dz) {
+static void rev_rhs(Handle& h, const double* dl_dz, double* copy = nullptr) {
   PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
   hipLaunchKernelGGL(qp_rev_rhs_kernel, dim3(h.batch), dim3(TPB), 0, h.stream, dl_dz, h.meta.as<QPMeta>(),
-                     h.n, h.nmax, rhs_of(h, 0));
+                     h.n, h.nmax, rhs_of(h, 0), copy);
   check_launch();
 }
 
-static void fwd_rhs_into(Handle& h, const FwdTangents& T, double* full, double* rhs) {
+static void fwd_rhs_into(Handle& h, const FwdTangents& T, double* full, double* rhs, double* copy = nullptr) {
   const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
   static const double dummy = 0.0;
   hipLaunchKernelGGL(qp_fwd_rhs_kernel, dim3(B), dim3(TPB), (size_t)std::min(n, ZCAP) * sizeof(double),
                      h.stream, T.dQ, T.dq, T.dG, T.dh, T.dA, T.db, h.z, m ? h.lam : &dummy,
-                     p ? h.nu : &dummy, rpos_of(h), h.meta.as<QPMeta>(), n, m, p, h.nmax, ZCAP, full, rhs);
+                     p ? h.nu : &dummy, rpos_of(h), h.meta.as<QPMeta>(), n, m, p, h.nmax, ZCAP, full, rhs, copy);
   check_launch();
 }
-static void fwd_rhs(Handle& h, const FwdTangents& T) {
+static void fwd_rhs(Handle& h, const FwdTangents& T, double* copy = nullptr) {
   PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
-  fwd_rhs_into(h, T, full_of(h), rhs_of(h, 1));
+  fwd_rhs_into(h, T, full_of(h), rhs_of(h, 1), copy);
 }
 
 static FwdTangents tangents(Handle& h, const double* dQ, const double* dq, const double* dG,
@@ -1053,7 +1067,7 @@ void qp_reverse_k(Handle& h, int k, const double* dl_dz, double* out) {
     PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
     for (int j = 0; j < k; ++j) {
       hipLaunchKernelGGL(qp_rev_rhs_kernel, dim3(h.batch), dim3(TPB), 0, h.stream, dl_dz + (size_t)j * h.batch * h.n,
-                         h.meta.as<QPMeta>(), h.n, h.nmax, rk + j * blk);
+                         h.meta.as<QPMeta>(), h.n, h.nmax, rk + j * blk, nullptr);
       check_launch();
     }
   }
@@ -1113,21 +1127,21 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
     PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
     prep_assemble(h, nullptr, (int)h.batch, [&] { meta_copy(h); });
   }
-  rev_rhs(h, dl_dz);
-  fwd_rhs(h, T);
-  meta_sizes(h);
   // no-pivot LU: both right-hand sides ride along as a bordering column / row
-  // and come out forward-swept (w0, w1), leaving the solves the backward
-  // sweeps; rhs itself stays intact for the partial-pivoting re-solve
+  // and come out forward-swept (w0, w1, written by the RHS kernels next to
+  // rhs), leaving the solves the backward sweeps; rhs itself stays intact for
+  // the partial-pivoting re-solve
   double *w0 = nullptr, *w1 = nullptr;
-  if (h.lu_mode == 1 && h.blocked_npmax) {
+  if (h.lu_mode == 1) {
     const size_t len = (size_t)h.batch * h.nmax;
     h.fwdw.ensure(2 * len * sizeof(double));
     w0 = h.fwdw.as<double>();
     w1 = w0 + len;
-    DOPT_CHECK_HIP(hipMemcpyAsync(w0, rhs_of(h, 0), len * sizeof(double), hipMemcpyDeviceToDevice, h.stream));
-    DOPT_CHECK_HIP(hipMemcpyAsync(w1, rhs_of(h, 1), len * sizeof(double), hipMemcpyDeviceToDevice, h.stream));
   }
+  rev_rhs(h, dl_dz, w0);
+  fwd_rhs(h, T, w1);
+  meta_sizes(h);
+  if (!h.blocked_npmax) w0 = w1 = nullptr;
   auto solve2 = [&](int sel, const double* sw0, const double* sw1) {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     qp_blocked_solve2(h, dinv_of(h), rhs_of(h, 0), rhs_of(h, 1), x_of(h, 0), x_of(h, 1), sel, sw0, sw1);
