@@ -744,7 +744,15 @@ double dopt_last_time(const dopt_handle* h) { return h ? h->last_time : -1.0; }
 int dopt_set_profiling(dopt_handle* h, int32_t on) {
   return guarded(h, [&]() {
     h->collect_phases();
-    h->prof = on != 0;
+    h->prof = on != 0 ? ~0u : 0u;
+    return 0;
+  });
+}
+
+int dopt_set_profiling_phases(dopt_handle* h, uint32_t mask) {
+  return guarded(h, [&]() {
+    h->collect_phases();
+    h->prof = mask;
     return 0;
   });
 }

@@ -169,7 +169,7 @@ struct Handle {
   DevBuf tin[8], tout[6];
 
   // per-phase GPU timing (HIP events on the handle's stream)
-  bool prof = false;
+  uint32_t prof = 0;   // phases timed (bit DOPT_PHASE_x)
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_pending;
   double phase_ms[DOPT_NUM_PHASES] = {0};
@@ -207,13 +207,13 @@ struct PhaseTimer {
   int phase;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   PhaseTimer(Handle& hh, int ph) : h(hh), phase(ph) {
-    if (!h.prof) return;
+    if (!(h.prof >> ph & 1u)) return;
     e0 = h.take_event();
     e1 = h.take_event();
     DOPT_CHECK_HIP(hipEventRecord(e0, h.stream));
   }
   ~PhaseTimer() {
-    if (!h.prof) return;
+    if (!e0) return;
     if (hipEventRecord(e1, h.stream) == hipSuccess) h.ev_pending.push_back({phase, {e0, e1}});
   }
 };

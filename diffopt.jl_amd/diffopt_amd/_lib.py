@@ -74,10 +74,24 @@ SIGNATURES = {
     "dopt_get_system_size": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_last_time": (ctypes.c_double, [_h]),
     "dopt_set_profiling": (ctypes.c_int, [_h, ctypes.c_int32]),
+    "dopt_set_profiling_phases": (ctypes.c_int, [_h, ctypes.c_uint32]),
     "dopt_get_phase_times": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]),
     "dopt_phase_name": (ctypes.c_char_p, [ctypes.c_int32]),
 }
 NUM_PHASES = 11
+
+
+def phase_mask(lib, names):
+    """Bit mask of the phases named (dopt_phase_name), for dopt_set_profiling_phases."""
+    known = {lib.dopt_phase_name(i).decode(): i for i in range(NUM_PHASES)}
+    mask = 0
+    for nm in names:
+        if nm not in known:
+            raise ValueError(f"unknown phase {nm!r}; phases: {sorted(known)}")
+        mask |= 1 << known[nm]
+    return mask
+
+
 ABI_VERSION = 2
 LU_KIND_LSQR, LU_KIND_NOPIV, LU_KIND_PIVOT = 0, 1, 2
 

@@ -181,8 +181,14 @@ class ConicBatch:
         _lib.check(self.lib.dopt_get_system_size(self.h, buf.ctypes.data), self.h)
         return buf
 
-    def set_profiling(self, on=True):
-        _lib.check(self.lib.dopt_set_profiling(self.h, int(bool(on))), self.h)
+    def set_profiling(self, on=True, phases=None):
+        """Per-phase HIP-event timing on (all phases, or only the phase names
+        in `phases`) or off."""
+        if phases is None:
+            _lib.check(self.lib.dopt_set_profiling(self.h, int(bool(on))), self.h)
+        else:
+            mask = _lib.phase_mask(self.lib, phases) if on else 0
+            _lib.check(self.lib.dopt_set_profiling_phases(self.h, mask), self.h)
 
     def phase_times(self):
         return _lib.phase_times(self.lib, self.h)

@@ -135,8 +135,14 @@ class NLPBatch:
         _lib.check(self.lib.dopt_qp_get_lu_kind(self.h, buf.ctypes.data), self.h)
         return buf
 
-    def set_profiling(self, on=True):
-        _lib.check(self.lib.dopt_set_profiling(self.h, int(bool(on))), self.h)
+    def set_profiling(self, on=True, phases=None):
+        """Per-phase HIP-event timing on (all phases, or only the phase names
+        in `phases`) or off."""
+        if phases is None:
+            _lib.check(self.lib.dopt_set_profiling(self.h, int(bool(on))), self.h)
+        else:
+            mask = _lib.phase_mask(self.lib, phases) if on else 0
+            _lib.check(self.lib.dopt_set_profiling_phases(self.h, mask), self.h)
 
     def phase_times(self):
         """{phase name: (total ms, launches)} since the last call; the NLP path

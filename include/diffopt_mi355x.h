@@ -330,6 +330,11 @@ int dopt_get_system_size(dopt_handle* h, int32_t* sizes);
 #define DOPT_PHASE_CONIC_OUTPUT 10
 #define DOPT_NUM_PHASES 11
 int dopt_set_profiling(dopt_handle* h, int32_t on);
+/* Profiling restricted to the phases in `mask` (bit DOPT_PHASE_x; 0 = off).
+ * The events of a timed phase cost a few microseconds of queue time each, so
+ * a benchmark times only the phase it reports live and takes the breakdown
+ * of the others from a separate pass. */
+int dopt_set_profiling_phases(dopt_handle* h, uint32_t mask);
 /* Accumulated milliseconds and launch counts per phase since the last call
  * (arrays of length nphases ≤ DOPT_NUM_PHASES); resets the accumulators. */
 int dopt_get_phase_times(dopt_handle* h, double* ms, int32_t* counts,

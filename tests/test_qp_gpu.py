@@ -488,3 +488,27 @@ def test_full_batch_kkt_residual_property(QPBatch, cfg):
     del d, rev, fwd, Q, G, z, lam, s
     e.close()
     torch.cuda.empty_cache()
+
+
+def test_profiling_restricted_to_named_phases(QPBatch):
+    """set_profiling(phases=[...]) times only the named phases (the bench's
+    timed region), set_profiling(True) every phase; results unchanged."""
+    d = _synthetic(4, 50, 80, 30, 0.2, 20250311)
+    B, n = d["z"].shape
+    e = QPBatch(B, n, d["lam"].shape[1], d["nu"].shape[1])
+    e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    kw = dict(dq=d["dq"], dh=d["dh"], db=d["db"])
+    e.set_profiling(True)
+    r_all, f_all = e.forward_reverse(d["dl_dz"], **kw)
+    e.set_profiling(False)
+    every = e.phase_times()
+    assert {"qp_assemble", "qp_lu", "qp_rhs", "qp_solve", "qp_output"} <= set(every)
+    e.set_profiling(True, phases=["qp_lu"])
+    r_one, f_one = e.forward_reverse(d["dl_dz"], **kw)
+    e.set_profiling(False)
+    one = e.phase_times()
+    assert set(one) == {"qp_lu"} and one["qp_lu"][1] == 1 and one["qp_lu"][0] > 0
+    np.testing.assert_array_equal(r_one, r_all)
+    np.testing.assert_array_equal(f_one, f_all)
+    with pytest.raises(ValueError):
+        e.set_profiling(True, phases=["no_such_phase"])
