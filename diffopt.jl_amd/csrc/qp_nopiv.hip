@@ -132,6 +132,9 @@ __device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double*
     double* rdst = ti == j4 ? rowb + 4 * tj : mine;
     double* cdst = tj == j4 ? colb + 4 * ti : mine;
     const bool ocol = tj == j4;
+    // 4ti + r > 4j4 + jj  ⟺  r > jj ? ti ≥ j4 : ti > j4 (r, jj compile-time):
+    // the row / column masks of the four steps from four compares
+    const bool rge = ti >= j4, rgt = ti > j4, cge = tj >= j4, cgt = tj > j4;
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int j = 4 * j4 + jj;
@@ -156,13 +159,14 @@ __device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double*
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const double l = cv[r] * rcp;
-        lm[r] = (4 * ti + r > j) ? l : 0.0;
+        const bool below = r > jj ? rge : rgt;   // row 4ti + r > j
+        lm[r] = below ? l : 0.0;
         // the column's owner keeps its multipliers in place (column j is
         // never updated again: um = 0 there from now on)
-        if (ocol && 4 * ti + r > j) a[r][jj] = l;
+        if (ocol && below) a[r][jj] = l;
       }
 #pragma unroll
-      for (int c = 0; c < 4; ++c) um[c] = (4 * tj + c > j) ? uv[c] : 0.0;
+      for (int c = 0; c < 4; ++c) um[c] = (c > jj ? cge : cgt) ? uv[c] : 0.0;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
