@@ -48,8 +48,10 @@
 //    workgroups hold CU slots (three of four waves parked at barriers) that
 //    the memory-bound update needs.
 //
-// Factor format: K row-major, L strictly below / U on and above the diagonal,
-// perm = identity, dinv as the partial-pivoting path writes it — the solves of
+// Factor format: K row-major, L strictly below / U on and above the diagonal
+// outside the 32×32 diagonal blocks (those keep the assembled values: the
+// solves never read them, they use the blocks' inverses in dinv), perm =
+// identity, dinv as the partial-pivoting path writes it — the solves of
 // qp_blocked.hip serve both.
 //
 // Reference: QuadraticProgram.jl create_LHS_matrix :256-282 and solve_system
@@ -116,8 +118,7 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double* colb, double* trash,
-                                          double* __restrict__ Kd, int ld) {
+__device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double* colb, double* trash) {
   const int lane = threadIdx.x & 63, ti = lane >> 3, tj = lane & 7;
   double a[4][4];
 #pragma unroll
@@ -174,7 +175,8 @@ __device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double*
       wave_sync();   // this step's reads of rowb / colb precede the next publish
     }
   }
-  // L and U from the registers (to S and to K at Kd); the threshold test once, on the final values
+  // L and U from the registers to S (K's 32×32 diagonal blocks are never
+  // read again: the solves use their inverses, dinv); the threshold test once, on the final values
   // (a pivot and a multiplier never change after their step): every pivot
   // non-zero and finite, every |l| ≤ NOPIV_LMAX (NaN fails)
   int bad = 0;
@@ -184,7 +186,6 @@ __device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double*
     for (int c = 0; c < 4; ++c) {
       const int gi = 4 * ti + r, gj = 4 * tj + c;
       S[(o + gi) * SLD + o + gj] = a[r][c];
-      Kd[(size_t)gi * ld + gj] = a[r][c];
       if (gi == gj) bad |= !(fabs(a[r][c]) > 0.0) || !(fabs(a[r][c]) <= 1.7976931348623157e308);
       if (gi > gj) bad |= !(fabs(a[r][c]) <= NOPIV_LMAX);
     }
@@ -343,7 +344,7 @@ __device__ __forceinline__ d4n tile32(int tr, int tc, FA A, FB Bm, int ns = 8) {
 //   E  waves 0–1: L_bb⁻¹, U_bb⁻¹ (tri_inv32); waves 2–3: T_L = L_ba L_aa⁻¹,
 //      T_U = U_aa⁻¹U_ab (MFMA)
 //   F  L⁻¹_ba = −L_bb⁻¹T_L, U⁻¹_ab = −T_U U_bb⁻¹ (MFMA)
-// Writes L11 / U11 to K, perm = identity, the 32×32 diagonal-block inverses to
+// Writes U_ab / L_ba to K, perm = identity, the 32×32 diagonal-block inverses to
 // dinv and, when a trailing step follows, the packed 64×64 inverse (L11⁻¹
 // strictly below the diagonal, U11⁻¹ on and above it) to `Bg`.  A failed
 // threshold test marks the problem LU_REJECT and stops.  Called by the whole
@@ -416,7 +417,7 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
 
   // ---- A. LU of block a
   if (wv == 0) {
-    const int bad = wave_lu32(S, 0, L.rowb, L.colb, L.trash, Kb + (size_t)c0 * ld + c0, ld);
+    const int bad = wave_lu32(S, 0, L.rowb, L.colb, L.trash);
     if (lane == 0 && bad) *L.sbad = 1;
   }
   __syncthreads();
@@ -433,7 +434,9 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
   // test on L_ba; U_ab, L_ba → S and K
   tri_inv32(S, 0, wv, 0, 1);
   __syncthreads();
+  NLU_MARK(8);
   dinv32(S, 0, Db);
+  NLU_MARK(9);
   if (Wv < NB64) {   // a 32-wide last block: done (no trailing step follows)
     NLU_MARK(2);
     if (w0b) fwd_block(L, w0b, w1b, c0, N, Wv);   // S: L_aa⁻¹ \ U_aa⁻¹, identity frame
@@ -448,6 +451,7 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
     const d4n al = tile32(tr, tc, [&](int, int k) { return S[(32 + i) * SLD + k]; },
                           [&](int k, int) { return k <= j ? S[k * SLD + j] : 0.0; }, tc ? 8 : 4);
     __syncthreads();   // every wave has read A_ab / A_ba
+    NLU_MARK(10);
     int bad = 0;
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
@@ -485,7 +489,7 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
 
   // ---- D. LU of block b
   if (wv == 0) {
-    const int bad = wave_lu32(S, 32, L.rowb, L.colb, L.trash, Kb + (size_t)(c0 + 32) * ld + c0 + 32, ld);
+    const int bad = wave_lu32(S, 32, L.rowb, L.colb, L.trash);
     if (lane == 0 && bad) *L.sbad = 1;
   }
   __syncthreads();

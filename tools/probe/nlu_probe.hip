@@ -98,8 +98,9 @@ int main(int argc, char** argv) {
                        dinv_stride(nmax), meta, 0, binv, nullptr, nullptr);
     hipDeviceSynchronize();
     hipMemcpyFromSymbol(st, HIP_SYMBOL(nlu_stamps), sizeof(st));
-    const char* nm[8] = {"load", "A lu_a", "B inv/trsm", "C schur", "D lu_b", "E inv_b/T", "F offdiag", "G binv"};
-    for (int k = 0; k < 8; ++k) printf("  stamp %-12s %9.0f cycles/WG\n", nm[k], (double)st[k] / B);
+    const char* nm[11] = {"load", "A lu_a", "B stores", "C schur", "D lu_b", "E inv_b/T", "F offdiag", "G binv",
+                          "B tri_inv_a", "B dinv_a", "B U_ab/L_ba"};
+    for (int k = 0; k < 11; ++k) printf("  stamp %-12s %9.0f cycles/WG\n", nm[k], (double)st[k] / B);
   }
 #endif
   hipMemcpy(hm.data(), meta, B * sizeof(QPMeta), hipMemcpyDeviceToHost);
