@@ -161,8 +161,13 @@ __global__ __launch_bounds__(NT) void nlp_assemble_kernel(NLPDims d, NLPMap mp, 
 // diagonal-block inverses) leaves rounding noise instead — so the test here
 // is rank-revealing: |u_ii| ≤ rows·ε·max|M| (or a non-finite u_ii) marks the
 // problem singular at column i (meta.info = i+1).  One workgroup per problem.
+// u_ii: the no-pivot LU does not store its 32×32 diagonal blocks back to K
+// (qp_nopiv.hip: the solves read only their inverses), so for LU_NOPIV
+// problems u_ii = 1 / (U⁻¹)_ii from the block's inverse in dinv (L⁻¹ | U⁻¹,
+// row-major 32×32 each); partial-pivoting problems keep U in K.
 __global__ __launch_bounds__(NT) void nlp_pivot_check_kernel(const double* __restrict__ K, int ld, int nmax,
                                                              const int32_t* __restrict__ perm,
+                                                             const double* __restrict__ dinv, size_t dstride,
                                                              QPMeta* __restrict__ meta,
                                                              const double* __restrict__ partial, int nparts,
                                                              int rows, const int32_t* __restrict__ plist) {
@@ -181,8 +186,11 @@ __global__ __launch_bounds__(NT) void nlp_pivot_check_kernel(const double* __res
   const double* Kb = K + (size_t)b * nmax * ld;
   const int32_t* pb = perm + (size_t)b * nmax;
   int first = 0x7fffffff;
+  const double* Db = dinv + (size_t)b * dstride;
+  const bool nopiv = mm.lu == LU_NOPIV;
   for (int i = threadIdx.x; i < rows; i += NT) {
-    const double u = Kb[(size_t)pb[i] * ld + i];
+    const double u = nopiv ? 1.0 / Db[(size_t)(i >> 5) * (2 * 32 * 32) + 32 * 32 + (i & 31) * 33]
+                           : Kb[(size_t)pb[i] * ld + i];
     if (!(fabs(u) > tol) && i < first) first = i;   // NaN fails too
   }
   for (int o = 32; o > 0; o >>= 1) first = min(first, __shfl_xor(first, o));
@@ -359,7 +367,8 @@ void assemble(Handle& h, const int32_t* plist, int count) {
 void pivot_check(Handle& h, const int32_t* plist, int count) {
   if (count == 0) return;
   hipLaunchKernelGGL(nlp_pivot_check_kernel, dim3(count), dim3(NT), 0, h.stream, h.K.as<double>(), h.ld, h.nmax,
-                     h.ipiv.as<int32_t>(), h.meta.as<QPMeta>(), h.nlp_scale.as<double>(), row_blocks(h),
+                     h.ipiv.as<int32_t>(), dense_dinv(h), dinv_stride(h.nmax), h.meta.as<QPMeta>(),
+                     h.nlp_scale.as<double>(), row_blocks(h),
                      h.nlp_rows, plist);
   DOPT_CHECK_HIP(hipGetLastError());
 }

@@ -184,6 +184,94 @@ def test_structured_dependent_constraint():
     assert relfro(np.concatenate([fx[b], fd[b]]), np.concatenate([ox, od])) <= 1e-4
 
 
+@pytest.mark.parametrize("shape", [(20, 12, 4), (100, 60, 8)], ids=["rows32", "rows160"])
+def test_saddle_only(lu_mode, shape):
+    """Equality constraints only, no bounds: M = [W Jxᵀ; Jx 0] is the one NLP
+    shape the no-pivot LU takes (nlp.hip: saddle_only).  Its factor keeps the
+    32×32 diagonal blocks only as inverses (dinv), so the singularity verdict
+    must read u_ii from there: no correction may be applied (the reference's
+    lu(M) is non-singular), and ∂s matches the oracle.  Rows 32 (one diagonal
+    block) and 160 (a trailing update and a 32-wide last block)."""
+    from diffopt_amd import _lib
+    from diffopt_amd.synthetic import nlp_numpy
+    n, c, P = shape
+    st, pt, dp, dx, dd = nlp_numpy(4, n, c, P, 314, frac_geq=0, frac_leq=0, frac_low=0, frac_up=0)
+    assert (st["con_kind"] == 0).all()
+    e = engine(st, pt, 4)
+    assert e.layout()["rows"] == n + c
+    want = _lib.LU_KIND_NOPIV if lu_mode == "nopiv" else _lib.LU_KIND_PIVOT
+    assert (e.lu_kind() == want).all(), e.lu_kind()
+    for b in range(4):
+        assert oracle_problem(st, pt, b)[4] == 0
+    np.testing.assert_array_equal(e.corrections(), 0)
+    check_against_oracle(e, st, pt, dp, dx, dd, range(4))
+
+
+@pytest.mark.parametrize("shape", [(20, 12, 4), (100, 60, 8)], ids=["rows32", "rows160"])
+def test_saddle_only_dependent_equality(lu_mode, shape):
+    """A saddle-only problem with two identical equality rows: M is singular in
+    exact arithmetic, but here no elimination order cancels the dependent
+    pivot to exactly zero — SuperLU leaves 4e-16 (rows 32) / 8e-33 (rows 160)
+    and does not flag it, and the reference's `lu(M; check=false).status`
+    (NonLinearProgram.jl:408-409) is then decided by UMFPACK's rounding, pinned
+    by no fixture.  The engine's rank-revealing verdict flags it and applies
+    the reference's correction loop: the count must equal the oracle's
+    `inertia_correction` on the same M (k = 1), and the regular neighbours are
+    untouched and at parity."""
+    from diffopt_amd.synthetic import nlp_numpy
+    n, c, P = shape
+    st, pt, dp, dx, dd = nlp_numpy(3, n, c, P, 2718, frac_geq=0, frac_leq=0, frac_low=0, frac_up=0)
+    b = 1
+    pt["Jx"][b, c - 1] = pt["Jx"][b, 0]
+    pt["Jp"][b, c - 1] = pt["Jp"][b, 0]
+    _, lay, M, _, _ = oracle_problem(st, pt, b)
+    Md = np.asarray(M.todense() if hasattr(M, "todense") else M)
+    corr = onlp.inertia_correction(Md, c, lay.num_w)[1]
+    assert corr >= 1
+    e = engine(st, pt, 3)
+    got = e.corrections()
+    assert got[0] == 0 and got[2] == 0 and got[1] == corr, (got, corr)
+    check_against_oracle(e, st, pt, dp, dx, dd, [0, 2])
+
+
+@pytest.mark.parametrize("delta", [1e-13, 1e-11])
+def test_near_singular_verdict(lu_mode, delta):
+    """The singularity verdict on a *near*-singular M:
+    the dependent-row problem of test_structured_dependent_constraint with
+    the duplicated row's Jacobian moved by delta·N(0,1).  The reference's
+    lu(M; check = false) flags only an exactly zero pivot, so UMFPACK (and the
+    oracle's SuperLU) factorise it without correction.  The engine's
+    rank-revealing test |u_ii| ≤ rows·ε·max|M| ≈ 2.4e-14 (nlp.hip) sits 7×
+    below the smallest pivot delta = 1e-13 leaves (1.7e-13), so it agrees:
+    0 corrections, as the oracle.  (Below roughly rows·ε·max|M| ≈ 1e-14 the
+    two rules can disagree: there UMFPACK's verdict depends on its rounding
+    and ordering, and no fixture of the reference pins it.)"""
+    from diffopt_amd.synthetic import nlp_numpy
+    st, pt, dp, dx, dd = nlp_numpy(3, 20, 12, 4, 77)
+    eq = np.flatnonzero(st["con_kind"] == 0)
+    i, j = eq[:2]
+    b = 1
+    rng = np.random.default_rng(5)
+    pt["Jx"][b, j] = pt["Jx"][b, i] + delta * rng.standard_normal(pt["Jx"].shape[2])
+    pt["Jp"][b, j] = pt["Jp"][b, i]
+    corr = oracle_problem(st, pt, b)[4]
+    assert corr == 0
+    e = engine(st, pt, 3)
+    np.testing.assert_array_equal(e.corrections(), [0, corr, 0])
+    check_against_oracle(e, st, pt, dp, dx, dd, [0, 2])
+
+
+def test_config6_shape():
+    """bench.py --config 6's shape (n = 200, c = 100, P = 20, 607 rows, partial
+    pivoting): two problems of the bench generator vs the oracle at 1e-6."""
+    from diffopt_amd.synthetic import SEED0, nlp_numpy
+    st, pt, dp, dx, dd = nlp_numpy(2, 200, 100, 20, SEED0 + 6)
+    e = engine(st, pt, 2)
+    assert e.layout()["rows"] > 560
+    np.testing.assert_array_equal(e.corrections(), 0)
+    check_against_oracle(e, st, pt, dp, dx, dd, range(2))
+
+
 # ---- memory modes and errors -------------------------------------------------
 def test_device_mode_matches_host():
     import torch
