@@ -49,6 +49,31 @@ NLP_CFG = {6: dict(batch=1024, n=200, c=100, P=20)}
 NLP_KEYS = ["Hxx", "Hxp", "Jx", "Jp", "x", "cval", "crhs", "y", "xl", "xu", "yl", "yu"]
 
 
+def host_cores():
+    """(usable, machine) host CPUs: `usable` is what this process may actually
+    run on — its affinity mask, capped by a cgroup-v2 CPU quota when one is
+    set (the GPU box gives each one-GPU job a share of a larger machine, and
+    os.cpu_count() reports the whole machine) — `machine` is os.cpu_count().
+    SURVEY.md §8(d): the CPU baseline runs on all usable host cores."""
+    machine = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = machine
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            usable = min(usable, max(1, math.ceil(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return usable, machine
+
+
+def cpu_workers(args):
+    return args.cpu_workers or host_cores()[0]
+
+
 # --------------------------------------------------------------------------
 # CPU baseline: the oracle restatement of the reference algorithm (sparse LU of
 # the full KKT via SuperLU, re-factorised for reverse and for forward exactly
@@ -81,7 +106,7 @@ def cpu_baseline(cfg, seconds, workers):
     wall = time.perf_counter() - t0
     solves = sum(r[0] for r in res)
     rate = sum(r[0] / r[1] for r in res)
-    return dict(value=round(rate, 2), unit="solves/s", cores=workers, kind="port",
+    return dict(value=round(rate, 2), unit="solves/s", cores=workers, machine_cpus=host_cores()[1], kind="port",
                 sample=(f"{solves} config-{cfg.get('id', 2)} QP solves (n={cfg['n']}, m={cfg['m']}, fwd+rev, "
                         f"SuperLU re-factorised per direction) on {workers} processes "
                         f"× {seconds:.0f} s (wall {wall:.1f} s)"))
@@ -121,12 +146,13 @@ def run_nlp(args, world, rank, local_rank):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import multiprocessing as mp
-        workers = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
+        workers = cpu_workers(args)
         t0 = time.perf_counter()
         with mp.get_context("fork").Pool(workers) as pool:
             res = pool.map(_nlp_cpu_worker, [(cfg, 3000 + i, args.cpu_seconds) for i in range(workers)])
         wall = time.perf_counter() - t0
-        cpu = dict(value=round(sum(r[0] / r[1] for r in res), 2), unit="solves/s", cores=workers, kind="port",
+        cpu = dict(value=round(sum(r[0] / r[1] for r in res), 2), unit="solves/s", cores=workers,
+                   machine_cpus=host_cores()[1], kind="port",
                    sample=(f"{sum(r[0] for r in res)} config-6 NLP solves (n={n}, c={c}, P={P}; ∂s recomputed "
                            f"per direction with SuperLU, as the reference) on {workers} processes × "
                            f"{args.cpu_seconds:.0f} s (wall {wall:.1f} s)"))
@@ -219,14 +245,19 @@ def run_nlp(args, world, rank, local_rank):
         dist.destroy_process_group()
 
 
+def _conic_gen(variant):
+    from diffopt_amd import synthetic
+    return synthetic.conic_numpy_wellcond if variant == "wellcond" else synthetic.conic_numpy
+
+
 def _conic_cpu_worker(args):
-    cfg, seed, seconds = args
+    cfg, seed, seconds, variant = args
     os.environ["OPENBLAS_NUM_THREADS"] = "1"
     import numpy as np
-    from diffopt_amd.synthetic import CONIC_CONFIGS, conic_numpy
+    from diffopt_amd.synthetic import CONIC_CONFIGS
     from oracle import conic as ocn
     c = CONIC_CONFIGS[cfg]
-    d = conic_numpy(1, c["n"], c["cones"], seed)
+    d = _conic_gen(variant)(1, c["n"], c["cones"], seed)
     t0 = time.perf_counter()
     cache = ocn.Cache(d["A"][0], d["b"][0], d["c"][0], d["x"][0], d["s"][0], d["y"][0], c["cones"])
     t_cache = time.perf_counter() - t0
@@ -255,21 +286,22 @@ def _conic_cpu_worker(args):
     return k, t_cache, t_it
 
 
-def conic_cpu_samples(cfg, seconds, workers):
+def conic_cpu_samples(cfg, seconds, workers, variant="bench"):
     import multiprocessing as mp
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
-        res = pool.map(_conic_cpu_worker, [(cfg, 1000 + i, seconds) for i in range(workers)])
+        res = pool.map(_conic_cpu_worker, [(cfg, 1000 + i, seconds, variant) for i in range(workers)])
     return res, time.perf_counter() - t0, workers
 
 
-def conic_cpu_baseline(cfg, seconds, samples, iters_per_solve):
+def conic_cpu_baseline(cfg, seconds, samples, iters_per_solve, variant="bench"):
     res, wall, workers = samples
     if cfg == 4:
         solves = sum(r[0] for r in res)
         rate = sum(r[0] / r[1] for r in res)
-        sample = (f"{solves} config-4 SOCP solves (n=500, 20 SOC(25), Dπ + fwd LSQR + rev LSQR, "
+        sample = (f"{solves} config-4{' converging-variant' if variant == 'wellcond' else ''} SOCP solves "
+                  f"(n=500, 20 SOC(25), Dπ + fwd LSQR + rev LSQR, "
                   f"IterativeSolvers defaults) on {workers} processes × {seconds:.0f} s "
                   f"(wall {wall:.1f} s)")
     else:
@@ -279,7 +311,37 @@ def conic_cpu_baseline(cfg, seconds, samples, iters_per_solve):
                   f"{sum(r[0] for r in res)} LSQR iterations (M·v + Mᵀ·u) timed for "
                   f"{seconds:.0f} s per process on {workers} processes, extrapolated to the "
                   f"engine's {iters_per_solve:.0f} fwd+rev iterations per solve (wall {wall:.1f} s)")
-    return dict(value=round(rate, 3), unit="solves/s", cores=workers, kind="port", sample=sample)
+    return dict(value=round(rate, 3), unit="solves/s", cores=workers, machine_cpus=host_cores()[1], kind="port",
+                sample=sample)
+
+
+def make_conic_step(eng, dev, gather, B):
+    """One bench step of the conic configs on `eng` (a ConicBatch holding this
+    rank's B problems; `dev` its device tensors dx / db / dc): Dπ, the
+    co-iterated forward + reverse LSQR, and with `gather` (world > 1) one RCCL
+    all-gather of the packed [forward | reverse] solutions of all problems of
+    the process group.
+    Returns (forward, reverse, gathered or None).  Module level so that
+    tests/test_parallel_gpu.py runs this exact step under a world-1 nccl
+    group."""
+    import torch
+    N = eng.N
+    packed = torch.empty(B, 2 * N, dtype=torch.float64, device="cuda") if gather else None
+
+    def step():
+        eng.factor()                                   # v, π(v), Dπ per cone
+        # both directions in one call: the two LSQR runs co-iterated, one sweep
+        # over A per M / Mᵀ apply for both (dopt_conic_forward_reverse)
+        (fo, fdx), (g, _, rdb, rdc) = eng.forward_reverse(dev["dx"], db=dev["db"], dc=dev["dc"],
+                                                          want_dA=False)
+        gathered = None
+        if packed is not None:
+            from diffopt_amd import parallel
+            packed[:, :N].copy_(fo)
+            packed[:, N:].copy_(g)
+            gathered = parallel.all_gather_rows(packed, _group_size() * B)
+        return fo, g, gathered
+    return step
 
 
 def run_conic(args, world, rank, local_rank):
@@ -289,8 +351,11 @@ def run_conic(args, world, rank, local_rank):
     import numpy as np
     import torch
     from diffopt_amd.conic import ConicBatch
-    from diffopt_amd.synthetic import CONIC_CONFIGS, SEED0, conic_numpy
+    from diffopt_amd.synthetic import CONIC_CONFIGS, SEED0
     c = CONIC_CONFIGS[args.config]
+    variant = args.conic_variant
+    if variant == "wellcond" and args.config != 4:
+        raise SystemExit("--conic-variant wellcond is defined for config 4 (SOC cones)")
     n, cones = c["n"], c["cones"]
     B = args.batch or CONIC_CFG[args.config]["batch"]
     m = sum(dim for _, dim in cones)
@@ -299,34 +364,20 @@ def run_conic(args, world, rank, local_rank):
     # counts, a host computation done after the GPU run)
     cpu_raw = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        workers = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
-        cpu_raw = conic_cpu_samples(args.config, args.cpu_seconds, workers)
+        workers = cpu_workers(args)
+        cpu_raw = conic_cpu_samples(args.config, args.cpu_seconds, workers, variant)
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", rank=rank, world_size=world,
                                 device_id=torch.device("cuda", local_rank))
-    d = conic_numpy(B, n, cones, SEED0 + args.config + 7919 * rank)
+    d = _conic_gen(variant)(B, n, cones, SEED0 + args.config + 7919 * rank)
     dev = {k: torch.from_numpy(d[k]).cuda() for k in ["A", "b", "c", "x", "s", "y", "dx", "db", "dc"]}
     del d
     eng = ConicBatch(B, n, cones, device=local_rank)
     eng.set(dev["A"], dev["b"], dev["c"], dev["x"], dev["s"], dev["y"])
-    N = n + m + 1
-    packed = torch.empty(B, 2 * N, dtype=torch.float64, device="cuda") if world > 1 else None
-
-    def step():
-        eng.factor()                                   # v, π(v), Dπ per cone
-        # both directions in one call: the two LSQR runs co-iterated, one sweep
-        # over A per M / Mᵀ apply for both (dopt_conic_forward_reverse)
-        (fo, fdx), (g, _, rdb, rdc) = eng.forward_reverse(dev["dx"], db=dev["db"], dc=dev["dc"],
-                                                          want_dA=False)
-        if packed is not None:
-            from diffopt_amd import parallel
-            packed[:, :N].copy_(fo)
-            packed[:, N:].copy_(g)
-            parallel.all_gather_rows(packed, world * B)
-        return fo, g
+    step = make_conic_step(eng, dev, world > 1, B)
 
     for _ in range(args.warmup):
         step()
@@ -359,7 +410,7 @@ def run_conic(args, world, rank, local_rank):
         cpu = None
         if cpu_raw is not None:
             cpu = conic_cpu_baseline(args.config, args.cpu_seconds, cpu_raw,
-                                     float(it_f.mean() + it_r.mean()))
+                                     float(it_f.mean() + it_r.mean()), variant)
         plen = 0
         for code, dim in cones:
             if code in (1, 2):
@@ -385,10 +436,13 @@ def run_conic(args, world, rank, local_rank):
         achieved = per_launch / avg_s / 1e9
         roof = dict(bound="hbm", achieved=round(achieved, 1), peak=PEAK_HBM_GBS, unit="GB/s",
                     frac=round(achieved / PEAK_HBM_GBS, 4),
-                    traffic=_load_pmc("conic_lsqr_split" if args.config == 5 else "conic_lsqr"),
+                    traffic=_load_pmc(("conic_lsqr_split" if args.config == 5 else "conic_lsqr")
+                                      + ("@wellcond" if variant == "wellcond" else "")),
                     kernel="conic_lsqr", avg_launch_ms=round(avg_s * 1e3, 4),
                     bytes_per_iteration=b_it,
                     lsqr_iterations_mean={"forward": float(it_f.mean()), "reverse": float(it_r.mean())},
+                    lsqr_istop={"forward": {str(k): int(v) for k, v in zip(*np.unique(stats["fwd_istop"], return_counts=True))},
+                                "reverse": {str(k): int(v) for k, v in zip(*np.unique(stats["istop"], return_counts=True))}},
                     phases_ms_per_step={k: round(v[0] / args.steps, 4) for k, v in sorted(phases.items())})
         value = world * B * args.steps / elapsed
         print(json.dumps({
@@ -396,9 +450,12 @@ def run_conic(args, world, rank, local_rank):
             "value": round(value, 3), "unit": "solves/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (seeded complementary cone pairs by construction, SURVEY.md §8(d))",
+            "data": ("synthetic (seeded complementary cone pairs by construction, SURVEY.md §8(d))" if variant == "bench"
+                     else "synthetic converging variant (diffopt_amd.synthetic.conic_numpy_wellcond: well-conditioned "
+                          "A, interior / dual-interior / boundary SOC pairs)"),
             "config": {"workload": f"config {args.config}: " + ("SOCP batch, 20 SOC(25)" if args.config == 4
-                                                                  else "SDP batch, 10 PSD(50)"),
+                                                                  else "SDP batch, 10 PSD(50)")
+                       + (" — converging variant (LSQR istop 1-2)" if variant == "wellcond" else ""),
                        "problems_per_gpu": B, "n": n, "m_rows": m,
                        "parallelism": f"batch-sharded x{world}" + (" + RCCL all-gather" if world > 1 else "")},
             "roofline": roof, "cpu_baseline": cpu}), flush=True)
@@ -437,6 +494,45 @@ def _load_pmc(kernel):
         return None
 
 
+def _group_size():
+    import torch.distributed as dist
+    return dist.get_world_size()
+
+
+def make_qp_step(eng, d, out_rev, out_fwd, gather, B, pipe=None):
+    """One bench step of the QP configs on `eng` (a QPBatch holding this
+    rank's B problems; `d` its device tensors): assembly, LU, both solves and
+    outputs into out_rev / out_fwd, then with `gather` (world > 1) one RCCL
+    all-gather of the packed [rev | fwd] rows of every rank's problems —
+    overlapped through `pipe`
+    (parallel.GatherPipeline; the result is pipe.result(k)) or blocking.
+    Returns the gathered tensor of a blocking gather, else None.  Module level
+    so that tests/test_parallel_gpu.py runs this exact step under a world-1
+    nccl group."""
+    import torch
+    from diffopt_amd import parallel
+    p = eng.p
+    L = out_rev.shape[1]
+    packed = torch.empty(B, 2 * L, dtype=torch.float64, device="cuda") if gather and pipe is None else None
+
+    def step():
+        eng.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"] if p else None,
+                            out_rev=out_rev, out_fwd=out_fwd)
+        if gather:
+            # weak scaling: every rank owns B problems of the world·B batch;
+            # one RCCL all-gather of the packed [rev | fwd] sensitivities per
+            # step, overlapped with the next step's kernels (GatherPipeline;
+            # every gather completes inside the timed region: drain() below)
+            if pipe is not None:
+                parallel.pack(out_rev, out_fwd, into=pipe.next_buffer())
+                pipe.submit()
+            else:
+                parallel.pack(out_rev, out_fwd, into=packed)
+                return parallel.all_gather_rows(packed, _group_size() * B)
+        return None
+    return step
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -448,7 +544,10 @@ def main():
                     help="QP: inactive rows get λ = LAM_EPS instead of 0 (no exact elimination)")
     ap.add_argument("--batch", type=int, default=None, help="problems per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-workers", type=int, default=None)
+    ap.add_argument("--cpu-workers", type=int, default=None,
+                    help="CPU-baseline processes (default: every usable host core, host_cores())")
+    ap.add_argument("--conic-variant", choices=["bench", "wellcond"], default="bench",
+                    help="config 4: the bench generator (LSQR stops at maxiter) or the converging variant")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--sync-allgather", action="store_true",
@@ -472,7 +571,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        workers = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
+        workers = cpu_workers(args)
         cpu = cpu_baseline(cfg, args.cpu_seconds, workers)
 
     import torch
@@ -496,24 +595,10 @@ def main():
     if world > 1 and not args.no_allgather:
         from diffopt_amd import parallel
         gathered = True
-        packed = torch.empty(B, 2 * L, dtype=torch.float64, device="cuda")
         if not args.sync_allgather:
             pipe = parallel.GatherPipeline(B, 2 * L, torch.float64, "cuda")
 
-    def step():
-        eng.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"] if p else None,
-                            out_rev=out_rev, out_fwd=out_fwd)
-        if gathered is not None:
-            # weak scaling: every rank owns B problems of the world·B batch;
-            # one RCCL all-gather of the packed [rev | fwd] sensitivities per
-            # step, overlapped with the next step's kernels (GatherPipeline;
-            # every gather completes inside the timed region: drain() below)
-            if pipe is not None:
-                parallel.pack(out_rev, out_fwd, into=pipe.next_buffer())
-                pipe.submit()
-            else:
-                parallel.pack(out_rev, out_fwd, into=packed)
-                parallel.all_gather_rows(packed, world * B)
+    step = make_qp_step(eng, d, out_rev, out_fwd, gathered is not None, B, pipe)
 
     for _ in range(args.warmup):
         step()

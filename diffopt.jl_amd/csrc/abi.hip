@@ -151,7 +151,7 @@ int dopt_destroy(dopt_handle* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   DevBuf* bufs[] = {&h->dinv, &h->plist, &h->lsqr_ws, &h->binv, &h->fwdw, &h->K, &h->ipiv, &h->s, &h->kidx, &h->meta, &h->rhs,
-                    &h->x, &h->cone_dev, &h->vp, &h->dpi, &h->cwork, &h->cinfo, &h->csplit, &h->krhs, &h->kx,
+                    &h->x, &h->cone_dev, &h->vp, &h->dpi, &h->cwork, &h->cinfo, &h->cnorm, &h->csplit, &h->krhs, &h->kx,
                     &h->kfull, &h->nlp_map, &h->nlp_shift, &h->nlp_scale};
   for (auto* b : bufs) b->release();
   for (auto& b : h->own_nin) b.release();
@@ -922,6 +922,18 @@ int dopt_conic_lsqr_stats(dopt_handle* h, int32_t* stats) {
     if (!stats) throw Error(-1, "stats is required");
     if (!h->cinfo.p) throw Error(-1, "no conic solve has run");
     DOPT_CHECK_HIP(hipMemcpyAsync(stats, h->cinfo.p, 4 * h->batch * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                  h->stream));
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  });
+}
+
+int dopt_conic_lsqr_norms(dopt_handle* h, double* norms) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_CONIC) throw Error(-1, "dopt_conic_lsqr_norms on a non-conic handle");
+    if (!norms) throw Error(-1, "norms is required");
+    if (!h->cnorm.p) throw Error(-1, "no conic solve has run");
+    DOPT_CHECK_HIP(hipMemcpyAsync(norms, h->cnorm.p, 8 * h->batch * sizeof(double), hipMemcpyDeviceToHost,
                                   h->stream));
     DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
     return 0;

@@ -658,7 +658,7 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
     const double* __restrict__ b, const double* __restrict__ c,
     const double* __restrict__ v, const double* __restrict__ P, int plen, int m, int n,
     const double* __restrict__ rhs, double rhs_zero_tol, double* __restrict__ work,
-    double* __restrict__ xout, int32_t* __restrict__ info) {
+    double* __restrict__ xout, int32_t* __restrict__ info, double* __restrict__ norms) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ double red[4];
   __shared__ ConeDesc cones[128];
@@ -698,6 +698,7 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
   }
   double beta = sqrt(cblock_sum(bb, red));
   int it = 0, istop = 0;
+  double fin[4] = {0.0, 0.0, 0.0, 0.0};   // terminal rnorm, arnorm, xnorm, anorm
   if (beta > rhs_zero_tol) {
     for (int i = t; i < N; i += CTPB) u[i] /= beta;
     __syncthreads();
@@ -765,6 +766,10 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
         const double test3 = (acond != 0.0) ? 1.0 / acond : 0.0;
         const double t1r = test1 / (1.0 + anorm * xnorm / bnorm);
         const double rtol = btol + atol * anorm * xnorm / bnorm;
+        fin[0] = rnorm;
+        fin[1] = arnorm;
+        fin[2] = xnorm;
+        fin[3] = anorm;
         istop = 0;
         if (it >= maxiter) istop = 7;
         if (1.0 + test3 <= 1.0) istop = 6;
@@ -784,6 +789,7 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
     info[bidx] = istop;
     info[gridDim.x + bidx] = it;
   }
+  if (t < 4 && norms) norms[(size_t)4 * bidx + t] = fin[t];
 }
 
 // ---------------------------------------------------------------------------
@@ -799,6 +805,7 @@ struct LsqrSeq {
   double *x, *u, *vv, *w, *tmp, *s1, *s2, *s4;
   const double* rb;
   double alpha, beta, anorm, ddnorm, res2, xxnorm, zz, sn2, cs2, rhobar, phibar, bnorm;
+  double fin[4];   // terminal rnorm, arnorm, xnorm, anorm
   int it, istop;
   bool live;
 };
@@ -809,7 +816,8 @@ __global__ __launch_bounds__(CTPB) __attribute__((amdgpu_waves_per_eu(2))) void 
     const double* __restrict__ v, const double* __restrict__ P, int plen, int m, int n,
     const double* __restrict__ rhs_f, double tol_f, const double* __restrict__ rhs_r, double tol_r,
     double* __restrict__ work, double* __restrict__ xout_f, double* __restrict__ xout_r,
-    int32_t* __restrict__ info_f, int32_t* __restrict__ info_r) {
+    int32_t* __restrict__ info_f, int32_t* __restrict__ info_r, double* __restrict__ norms_f,
+    double* __restrict__ norms_r) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ double red[4];
   __shared__ ConeDesc cones[128];
@@ -845,6 +853,7 @@ __global__ __launch_bounds__(CTPB) __attribute__((amdgpu_waves_per_eu(2))) void 
     Q.it = 0;
     Q.istop = 0;
     Q.live = false;
+    Q.fin[0] = Q.fin[1] = Q.fin[2] = Q.fin[3] = 0.0;
     double bb = 0.0;
     for (int i = t; i < N; i += CTPB) {
       const double r = Q.rb[i];
@@ -963,6 +972,10 @@ __global__ __launch_bounds__(CTPB) __attribute__((amdgpu_waves_per_eu(2))) void 
       const double test3 = (acond != 0.0) ? 1.0 / acond : 0.0;
       const double t1r = test1 / (1.0 + Q.anorm * xnorm / Q.bnorm);
       const double rtol = btol + atol * Q.anorm * xnorm / Q.bnorm;
+      Q.fin[0] = rnorm;
+      Q.fin[1] = arnorm;
+      Q.fin[2] = xnorm;
+      Q.fin[3] = Q.anorm;
       int istop = 0;
       if (Q.it >= maxiter) istop = 7;
       if (1.0 + test3 <= 1.0) istop = 6;
@@ -990,6 +1003,10 @@ __global__ __launch_bounds__(CTPB) __attribute__((amdgpu_waves_per_eu(2))) void 
       info_r[bidx] = S[1].istop;
       info_r[gridDim.x + bidx] = S[1].it;
     }
+  }
+  if (t < 4) {
+    if (norms_f) norms_f[(size_t)4 * bidx + t] = S[0].fin[t];
+    if (norms_r) norms_r[(size_t)4 * bidx + t] = S[1].fin[t];
   }
 }
 
@@ -1103,7 +1120,8 @@ constexpr int SPLIT_K = DOPT_SPLIT_K;            // rows per lane of a split row
 constexpr int SPLIT_ROWS = 64 * SPLIT_K;
 
 struct LsqrState {
-  double alpha, beta, rhobar, phibar, anorm, ddnorm, xxnorm, zz, sn2, cs2, bnorm, pad;
+  double alpha, beta, rhobar, phibar, anorm, ddnorm, xxnorm, zz, sn2, cs2, bnorm;
+  double rnorm, arnorm, xnorm;   // terminal estimates (with anorm)
   int32_t it, istop, done, skipT;
 };
 
@@ -1485,6 +1503,9 @@ __global__ __launch_bounds__(VT) void conic_split_upd_v_kernel(
   st.phibar = phibar;
   st.ddnorm = ddnorm;
   st.istop = istop;
+  st.rnorm = rnorm;
+  st.arnorm = arnorm;
+  st.xnorm = xnorm;
   if (istop) {
     st.done = 1;
     atomicSub(active, 1);
@@ -1495,7 +1516,8 @@ __global__ __launch_bounds__(VT) void conic_split_upd_v_kernel(
 // grid nq·B: sequence bv → (xout0, info0) for bv < B, (xout1, info1) after
 __global__ __launch_bounds__(CTPB) void conic_split_out_kernel(
     SplitWS ws, const LsqrState* __restrict__ stv, double* __restrict__ xout0, int32_t* __restrict__ info0,
-    double* __restrict__ xout1, int32_t* __restrict__ info1) {
+    double* __restrict__ xout1, int32_t* __restrict__ info1, double* __restrict__ norms0,
+    double* __restrict__ norms1) {
   const int bv = blockIdx.x, t = threadIdx.x, N = ws.N;
   const int b = ws.phys(bv);
   double* xout = bv < ws.B ? xout0 : xout1;
@@ -1505,6 +1527,11 @@ __global__ __launch_bounds__(CTPB) void conic_split_out_kernel(
   if (t == 0 && info) {
     info[b] = stv[bv].istop;
     info[ws.B + b] = stv[bv].it;
+  }
+  double* norms = bv < ws.B ? norms0 : norms1;
+  if (t < 4 && norms) {
+    const LsqrState& st = stv[bv];
+    norms[(size_t)4 * b + t] = t == 0 ? st.rnorm : t == 1 ? st.arnorm : t == 2 ? st.xnorm : st.anorm;
   }
 }
 
@@ -1587,7 +1614,7 @@ void conic_factor(Handle& h) {
 // Split-path LSQR (see conic_split_* above) of nq sequences per problem
 // (rhs: nq·B right-hand sides, sequence q·B + b), co-iterated for nq = 2.
 static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const double* rhs, double* out0,
-                             int32_t* info0, double* out1, int32_t* info1) {
+                             int32_t* info0, double* out1, int32_t* info1, double* norms0, double* norms1) {
   const int B = (int)h.batch, m = h.m, n = h.n;
   const int V = nq * B;   // sequences
   const int nc = (int)h.cones.size() / 2;
@@ -1649,7 +1676,8 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
     DOPT_CHECK_HIP(hipMemcpyAsync(&left, active, sizeof(int32_t), hipMemcpyDeviceToHost, h.stream));
     DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
   }
-  hipLaunchKernelGGL(conic_split_out_kernel, dim3(V), dim3(CTPB), 0, h.stream, ws, st, out0, info0, out1, info1);
+  hipLaunchKernelGGL(conic_split_out_kernel, dim3(V), dim3(CTPB), 0, h.stream, ws, st, out0, info0, out1, info1,
+                     norms0, norms1);
   ccheck();
 }
 
@@ -1666,16 +1694,18 @@ static void conic_lsqr(Handle& h, double tol, double* out) {
   const size_t wl = 5 * N + 3 * (size_t)m + n;
   h.cwork.ensure((size_t)B * (wl + N) * sizeof(double));
   h.cinfo.ensure((size_t)4 * std::max(B, 1) * sizeof(int32_t));
+  h.cnorm.ensure((size_t)8 * std::max(B, 1) * sizeof(double));
   double* rhs = h.cwork.as<double>() + (size_t)B * wl;
   if (use_split(h)) {
-    conic_lsqr_split(h, 1, tol, tol, rhs, out, h.cinfo.as<int32_t>(), nullptr, nullptr);
+    conic_lsqr_split(h, 1, tol, tol, rhs, out, h.cinfo.as<int32_t>(), nullptr, nullptr, h.cnorm.as<double>(),
+                     nullptr);
     return;
   }
   PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
   hipLaunchKernelGGL(conic_lsqr_kernel, dim3(B), dim3(CTPB), dpi_lds_bytes(h.cones), h.stream,
                      h.cone_dev.as<ConeDesc>(), nc, h.cA, h.cb, h.cc, h.vp.as<double>(),
                      h.dpi.as<double>(), h.dpi_len, m, n, rhs, tol, h.cwork.as<double>(), out,
-                     h.cinfo.as<int32_t>());
+                     h.cinfo.as<int32_t>(), h.cnorm.as<double>());
   ccheck();
 }
 
@@ -1736,6 +1766,8 @@ void conic_forward_reverse(Handle& h, const double* dA, const double* db, const 
   if (!h.cfactored) conic_factor(h);
   const int B = (int)h.batch, m = h.m, n = h.n;
   h.cinfo.ensure((size_t)4 * std::max(B, 1) * sizeof(int32_t));
+  h.cnorm.ensure((size_t)8 * std::max(B, 1) * sizeof(double));
+  double* nrm = h.cnorm.as<double>();
   const int nc = (int)h.cones.size() / 2;
   const size_t N = (size_t)n + m + 1;
   const size_t wl = 5 * N + 3 * (size_t)m + n;
@@ -1751,14 +1783,14 @@ void conic_forward_reverse(Handle& h, const double* dA, const double* db, const 
   }
   if (use_split(h)) {
     int32_t* info = h.cinfo.as<int32_t>();
-    conic_lsqr_split(h, 2, 0.0, 1e-4, rhs_f, out_f, info + 2 * B, out_g, info);
+    conic_lsqr_split(h, 2, 0.0, 1e-4, rhs_f, out_f, info + 2 * B, out_g, info, nrm + 4 * (size_t)B, nrm);
   } else {
     PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
     int32_t* info = h.cinfo.as<int32_t>();
     hipLaunchKernelGGL(conic_lsqr2_kernel, dim3(B), dim3(CTPB), dpi_lds_bytes(h.cones), h.stream,
                        h.cone_dev.as<ConeDesc>(), nc, h.cA, h.cb, h.cc, h.vp.as<double>(), h.dpi.as<double>(),
                        h.dpi_len, m, n, rhs_f, 0.0, rhs_r, 1e-4, h.cwork.as<double>(), out_f, out_g,
-                       info + 2 * B, info);
+                       info + 2 * B, info, nrm + 4 * (size_t)B, nrm);
     ccheck();
   }
   PhaseTimer pt(h, DOPT_PHASE_CONIC_OUTPUT);

@@ -141,7 +141,7 @@ struct Handle {
   DevBuf own_cin[6];
   std::vector<int32_t> cones;   // (code, dim) pairs
   DevBuf cone_dev;              // device copy of cone table (+ offsets)
-  DevBuf vp, dpi, cwork, cinfo;
+  DevBuf vp, dpi, cwork, cinfo, cnorm;   // cnorm: LSQR terminal estimates, 8·B doubles
   DevBuf csplit;                // split-path LSQR vectors, partial products, state
   int32_t conic_split = -1;     // -1 auto, 0 persistent kernel, 1 split (env DOPT_CONIC_SPLIT)
   int32_t dpi_len = 0;          // doubles per problem of packed Dπ blocks

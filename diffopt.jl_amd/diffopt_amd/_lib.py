@@ -48,6 +48,7 @@ SIGNATURES = {
     "dopt_qp_forward_k": (ctypes.c_int, [_h, ctypes.c_int32] + [ctypes.c_void_p] * 7),
     "dopt_conic_forward_reverse": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 10),
     "dopt_conic_lsqr_stats": (ctypes.c_int, [_h, ctypes.c_void_p]),
+    "dopt_conic_lsqr_norms": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_qp_params_reverse": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64]
                                + [ctypes.c_void_p] * 5),
     "dopt_qp_params_forward": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64]

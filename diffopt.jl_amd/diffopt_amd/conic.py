@@ -171,6 +171,15 @@ class ConicBatch:
         return {"istop": buf[:B], "iterations": buf[B:2 * B], "fwd_istop": buf[2 * B:3 * B],
                 "fwd_iterations": buf[3 * B:]}
 
+    def lsqr_norms(self):
+        """LSQR's terminal estimates (rnorm, arnorm, xnorm, anorm) of the last
+        run and, after ``forward_reverse``, of its forward run: dict of (B, 4)
+        arrays under "last" and "fwd"."""
+        buf = np.zeros(8 * self.batch, dtype=np.float64)
+        _lib.check(self.lib.dopt_conic_lsqr_norms(self.h, buf.ctypes.data), self.h)
+        B = self.batch
+        return {"last": buf[:4 * B].reshape(B, 4), "fwd": buf[4 * B:].reshape(B, 4)}
+
     def info(self):
         buf = np.zeros(self.batch, dtype=np.int32)
         _lib.check(self.lib.dopt_get_info(self.h, buf.ctypes.data), self.h)

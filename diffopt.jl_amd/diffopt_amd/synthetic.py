@@ -228,3 +228,82 @@ def nlp_numpy(batch, n, c, P, seed, frac_geq=0.4, frac_leq=0.3, frac_low=0.5, fr
     nd = c + int(has_low.sum()) + int(has_up.sum())
     return st, pt, rng.standard_normal((batch, P)), rng.standard_normal((batch, n)), \
         rng.standard_normal((batch, nd))
+
+
+def conic_numpy_wellcond(batch, n, cones, seed, f_interior=0.25, f_dual_interior=0.25, sigma=(1.0, 2.0),
+                         pair_norm=0.25):
+    """The converging variant of a conic shape: the same
+    cone list, but an instance family on which the reference's LSQR converges
+    (istop 1–2) well inside maxiter, so parity can be held to 1e-6 on every
+    output.  Differences from ``conic_numpy``:
+
+    * A = U·diag(σ)·Vᵀ with Haar-orthogonal U, V and σ ~ U(sigma) — a square
+      Gaussian A (config 4: m = n = 500) has σ_min ≈ 1/n and leaves M with
+      near-null singular values ~1e-3 beside its structural null space, so
+      LSQR crawls to maxiter (istop 7); with σ ∈ [1, 2] the non-zero spectrum
+      of M sits in about [0.3, 4];
+    * SOC cones draw one of three complementary cases: s strictly interior
+      with y = 0 (probability ``f_interior``; Dπ = 0), s = 0 with y strictly
+      interior (``f_dual_interior``; Dπ = I), or the boundary pair of
+      ``conic_numpy`` (the third, SOC-specific Dπ branch) — every Dπ branch of
+      ConicProgram's SOC projection is exercised;
+    * the SOC pair vectors have norm ``pair_norm`` and x ~ N(0,1)/√n, so b and
+      c (the last row / column of M) stay O(1).
+
+    M is singular at any exact primal–dual point — z = (x, y − s, 1) is always
+    in its null space (M·z = (c − A_moiᵀy, A_moi x + b − s, −(cᵀx + bᵀy)) = 0 by
+    feasibility and zero gap) — so LSQR returns the minimum-norm least-squares
+    solution, which is unique; "converging" means istop 1–2.  Nonnegatives /
+    Nonpositives / Zeros rows as in ``conic_numpy``; PSD cones are not
+    generated here."""
+    rng = np.random.default_rng(seed)
+    m = sum(d for _, d in cones)
+    out = {k: [] for k in ["A", "b", "c", "x", "s", "y", "dx", "dA", "db", "dc"]}
+    for _ in range(batch):
+        s = np.zeros(m)
+        y = np.zeros(m)
+        o = 0
+        for code, dim in cones:
+            if code == 0:
+                y[o:o + dim] = rng.standard_normal(dim)
+            elif code in (1, 2):
+                sg = 1.0 if code == 1 else -1.0
+                act = rng.random(dim) < 0.5
+                mag_s = rng.uniform(0.5, 1.5, dim)
+                mag_y = rng.uniform(0.5, 1.5, dim)
+                s[o:o + dim] = np.where(act, 0.0, sg * mag_s)
+                y[o:o + dim] = np.where(act, sg * mag_y, 0.0)
+            elif code == 3:
+                u = rng.standard_normal(dim - 1)
+                u *= pair_norm / np.linalg.norm(u)
+                al, be, lift = rng.uniform(0.5, 1.5), rng.uniform(0.5, 1.5), rng.uniform(1.5, 2.5)
+                r = rng.random()
+                if r < f_interior:            # s ∈ int K, y = 0
+                    s[o] = al * pair_norm * lift
+                    s[o + 1:o + dim] = al * u
+                elif r < f_interior + f_dual_interior:   # s = 0, y ∈ int K
+                    y[o] = be * pair_norm * lift
+                    y[o + 1:o + dim] = -be * u
+                else:                          # boundary pair
+                    s[o] = al * pair_norm
+                    s[o + 1:o + dim] = al * u
+                    y[o] = be * pair_norm
+                    y[o + 1:o + dim] = -be * u
+            else:
+                raise ValueError("conic_numpy_wellcond: cone code %d not generated" % code)
+            o += dim
+        k = min(m, n)
+        U, _ = np.linalg.qr(rng.standard_normal((m, m)))
+        V, _ = np.linalg.qr(rng.standard_normal((n, n)))
+        sv = rng.uniform(sigma[0], sigma[1], k)
+        A = (U[:, :k] * sv) @ V[:, :k].T
+        x = rng.standard_normal(n) / math.sqrt(n)
+        b = s - A @ x
+        c = A.T @ y
+        out["A"].append(A); out["b"].append(b); out["c"].append(c); out["x"].append(x)
+        out["s"].append(s); out["y"].append(y)
+        out["dx"].append(rng.standard_normal(n))
+        out["dA"].append(rng.standard_normal((m, n)))
+        out["db"].append(rng.standard_normal(m))
+        out["dc"].append(rng.standard_normal(n))
+    return {k: np.stack(v) for k, v in out.items()}

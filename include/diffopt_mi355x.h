@@ -240,6 +240,14 @@ int dopt_conic_forward_reverse(dopt_handle* h, const double* dA, const double* d
  * the last (or, after dopt_conic_forward_reverse, the reverse) run, then
  * [istop | iterations] of the forward run of dopt_conic_forward_reverse. */
 int dopt_conic_lsqr_stats(dopt_handle* h, int32_t* stats);
+/* LSQR's terminal scalar estimates of the same runs, 8·B doubles: per problem
+ * (rnorm, arnorm, xnorm, anorm) — ‖b − Mx‖, ‖Mᵀ(b − Mx)‖, ‖x‖ and the
+ * Frobenius estimate of ‖M‖ as IterativeSolvers' lsqr accumulates them at its
+ * last iteration (0 for a zero right-hand side) — of the last (or reverse)
+ * run, then of the forward run of dopt_conic_forward_reverse.  Test/bench
+ * introspection (no reference counterpart: lsqr's log is not kept,
+ * ConicProgram.jl:323, :372). */
+int dopt_conic_lsqr_norms(dopt_handle* h, double* norms);
 
 /* ---- introspection ---------------------------------------------------------*/
 /* per-problem status of the last factor/solve: QP: 0 ok, k>0 zero pivot at

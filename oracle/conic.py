@@ -101,7 +101,7 @@ def forward_rhs(cache, dA=None, db=None, dc=None):
                            [-(dc @ u) - (db @ vp)]])
 
 
-def forward_differentiate(cache, dA=None, db=None, dc=None, return_info=False):
+def forward_differentiate(cache, dA=None, db=None, dc=None, return_info=False, stats=None):
     """``forward_differentiate!`` (ConicProgram.jl:257-334).
 
     Returns ``(dx, du, dv, dw)`` where ``dx = −(du − x·dw)`` is
@@ -114,7 +114,7 @@ def forward_differentiate(cache, dA=None, db=None, dc=None, return_info=False):
         dz = np.zeros(N)
     else:
         dz, it, istop = lsqr(cache.matvec, cache.rmatvec, RHS, N,
-                             return_info=True)
+                             return_info=True, stats=stats)
         info = (it, istop)
     n, m = cache.n, cache.m
     du, dv, dw = dz[:n], dz[n:n + m], dz[-1]
@@ -123,7 +123,7 @@ def forward_differentiate(cache, dA=None, db=None, dc=None, return_info=False):
     return (out, info) if return_info else out
 
 
-def reverse_differentiate(cache, dx, return_info=False):
+def reverse_differentiate(cache, dx, return_info=False, stats=None):
     """``reverse_differentiate!`` (ConicProgram.jl:336-394) with dy = ds = 0.
 
     Returns ``(g, πz)``; ``lsqr`` is applied to ``M`` (not ``Mᵀ``, :372).
@@ -136,7 +136,7 @@ def reverse_differentiate(cache, dx, return_info=False):
         g = np.zeros(n + m + 1)
     else:
         g, it, istop = lsqr(cache.matvec, cache.rmatvec, dz, n + m + 1,
-                            return_info=True)
+                            return_info=True, stats=stats)
         info = (it, istop)
     piz = np.concatenate([cache.x, cache.vp, [1.0]])
     return ((g, piz), info) if return_info else (g, piz)

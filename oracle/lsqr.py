@@ -23,17 +23,21 @@ SQRT_EPS = math.sqrt(EPS)
 
 
 def lsqr(matvec, rmatvec, b, n, atol=SQRT_EPS, btol=SQRT_EPS,
-         conlim=1.0 / SQRT_EPS, maxiter=None, return_info=False):
+         conlim=1.0 / SQRT_EPS, maxiter=None, return_info=False, stats=None):
     """Minimum-norm least-squares solve of ``A x = b`` from ``x0 = 0``.
 
     ``matvec(v)`` computes ``A v`` (length m), ``rmatvec(u)`` computes ``Aᵀ u``
-    (length n).  ``maxiter`` defaults to ``max(m, n)``.
+    (length n).  ``maxiter`` defaults to ``max(m, n)``.  A dict passed as
+    ``stats`` receives the terminal estimates ``rnorm``, ``arnorm``, ``xnorm``,
+    ``anorm`` (0 when the loop does not run).
     """
     b = np.asarray(b, dtype=np.float64)
     m = b.shape[0]
     if maxiter is None:
         maxiter = max(m, n)
     x = np.zeros(n)
+    if stats is not None:
+        stats.update(rnorm=0.0, arnorm=0.0, xnorm=0.0, anorm=0.0)
     ctol = 1.0 / conlim if conlim > 0 else 0.0
     u = b.copy()
     beta = float(np.linalg.norm(u))
@@ -108,6 +112,8 @@ def lsqr(matvec, rmatvec, b, n, atol=SQRT_EPS, btol=SQRT_EPS,
         test3 = 1.0 / acond if acond != 0 else 0.0
         t1r = test1 / (1.0 + anorm * xnorm / bnorm)
         rtol = btol + atol * anorm * xnorm / bnorm
+        if stats is not None:
+            stats.update(rnorm=rnorm, arnorm=arnorm, xnorm=xnorm, anorm=anorm)
         if it >= maxiter:
             istop = 7
         if 1.0 + test3 <= 1.0:

@@ -151,12 +151,12 @@ def _errors(got, ref, cache):
                 dc=relcomb(got["dc"], ref["dc"], ng * (1 + nx)))
 
 
-def _synthetic_check(ConicBatch, B, n, cones, seed, name, cap=0, trials=3, want_dA=True):
+def _synthetic_check(ConicBatch, B, n, cones, seed, name, cap=0, trials=3, want_dA=True, gen=None):
     """GPU vs oracle per problem and output (tallied: RTOL, or the relaxed
     envelope bar where the oracle's own 1-ulp spread exceeds RTOL/10).
     Returns (tally, engine LSQR iteration counts fwd, rev, oracle infos)."""
     from diffopt_amd.synthetic import conic_numpy
-    d = conic_numpy(B, n, cones, seed)
+    d = (gen or conic_numpy)(B, n, cones, seed)
     e = ConicBatch(B, n, cones)
     e.set(d["A"], d["b"], d["c"], d["x"], d["s"], d["y"])
     out, dx = e.forward(d["dA"], d["db"], d["dc"])
@@ -218,16 +218,127 @@ def test_config4_nondegenerate_shape(ConicBatch):
     _synthetic_check(ConicBatch, 2, 500, [(3, 50)] * 20, 14, "config-4 structure, m=1000", cap=2)
 
 
+def test_config4_converging_variant(ConicBatch):
+    """Config 4's shape (n = 500, 20 × SOC(25), m = n) on the converging
+    instance family (synthetic.conic_numpy_wellcond: well-conditioned A, every
+    SOC Dπ branch — interior, dual-interior, boundary pair), seed SEED0 + 4 —
+    the first problems of `bench.py --config 4 --conic-variant wellcond`.
+    LSQR converges (istop 1–2) in ≈ 40–60 iterations in the engine and the
+    oracle; every output at 1e-6 relative Frobenius with NO relaxed output
+    (cap 0).  LSQR's own scalars: istop equal, the iteration count within one
+    (a 1-ulp perturbation of the oracle's inputs moves its own count by one on
+    2 of these 4 problems: the stopping test sits at √eps), rnorm and xnorm
+    to 1e-6 (converged quantities), anorm to 1e-3 where the counts agree (it
+    sums every α_k² + β_k² of the Golub–Kahan sequence, whose later terms
+    drift with the vectors' lost orthogonality: 4e-5 measured), arnorm not at
+    all (at istop 2 it is the √eps-level stopping residual, noise)."""
+    from diffopt_amd.synthetic import conic_numpy_wellcond
+    cones = [(3, 25)] * 20
+    B, n = 4, 500
+    d = conic_numpy_wellcond(B, n, cones, SEED0 + 4)
+    e = ConicBatch(B, n, cones)
+    e.set(d["A"], d["b"], d["c"], d["x"], d["s"], d["y"])
+    (out, fdx), (g, dA, db, dc) = e.forward_reverse(d["dx"], d["dA"], d["db"], d["dc"])
+    st = e.lsqr_stats()
+    nr = e.lsqr_norms()
+    e.close()
+    tally = Tally("config-4 converging variant")
+    keys = ("rnorm", "arnorm", "xnorm", "anorm")
+    for b in range(B):
+        cache = ocn.Cache(d["A"][b], d["b"][b], d["c"][b], d["x"][b], d["s"][b], d["y"][b], cones)
+        sf, sr = {}, {}
+        (odx, du, dv, dw), fi = ocn.forward_differentiate(cache, d["dA"][b], d["db"][b], d["dc"][b],
+                                                          return_info=True, stats=sf)
+        (og, _), ri = ocn.reverse_differentiate(cache, d["dx"][b], return_info=True, stats=sr)
+        odA, odb, odc = ocn.reverse_outputs(cache, og)
+        ref = dict(fwd=np.concatenate([du, dv, [dw]]), dx=odx, g=og, dA=odA, db=odb, dc=odc)
+        err = _errors(dict(fwd=out[b], dx=fdx[b], g=g[b], dA=dA[b], db=db[b], dc=dc[b]), ref, cache)
+        for k, v in err.items():
+            tally.check(v, lambda: 0.0, (b, k))   # envelope 0: no relaxed bar
+        for (istop, it), (est, ost), oi in (((st["fwd_istop"][b], st["fwd_iterations"][b]), (nr["fwd"][b], sf), fi),
+                                            ((st["istop"][b], st["iterations"][b]), (nr["last"][b], sr), ri)):
+            assert istop in (1, 2) and istop == oi[1], (b, istop, oi)
+            assert abs(int(it) - oi[0]) <= 1, (b, it, oi)
+            o = np.array([ost[k] for k in keys])
+            for j in (0, 2):
+                assert abs(est[j] - o[j]) <= 1e-6 * abs(o[j]), (b, keys[j], est[j], o[j])
+            if int(it) == oi[0]:
+                assert abs(est[3] - o[3]) <= 1e-3 * abs(o[3]), (b, "anorm", est[3], o[3])
+    tally.report(0)
+
+
+def _ls_quality(M, rhs, x):
+    """(‖Mx − rhs‖, ‖Mᵀ(Mx − rhs)‖ / (‖M‖₂‖Mx − rhs‖)) of an LSQR iterate."""
+    r = M @ x - rhs
+    nr = np.linalg.norm(r)
+    return nr, np.linalg.norm(M.T @ r) / (np.linalg.norm(M, 2) * nr)
+
+
 def test_config4_bench_shape(ConicBatch):
     """The exact config-4 bench shape and generator (20 × SOC(25), n = 500,
-    seed SEED0 + 4: the first two problems of bench.py's batch).  M is
-    singular there: both LSQR directions stop at maxiter = N = 1001 (istop 7)
-    in the engine and in the oracle alike; outputs are judged under the
-    tallied bar."""
+    seed SEED0 + 4: the first two problems of bench.py's batch).  M has, besides
+    its structural null space, singular values down to ~1e-17 (a square
+    Gaussian A): both LSQR directions stop at maxiter = N = 1001 (istop 7) in
+    the engine and in the oracle alike, and the final iterate is chaotic —
+    measured on the oracle itself, a 1-ulp relative perturbation of the
+    right-hand side moves its terminal rnorm by ~3e-3, xnorm and anorm by
+    ~1e-2, arnorm by up to 8×, and the true normal-equation residual ratio by
+    30× (profiles/r03/conic_cfg4_maxiter_spread.txt).  No implementation can
+    match such a run to 1e-6, so parity here is judged on what is stable:
+
+    * istop = 7 and 1001 iterations in both directions, as the oracle;
+    * LSQR's terminal estimates rnorm, xnorm, anorm inside the band the
+      oracle's own 1-ulp neighbours span (widened by twice that spread), arnorm
+      within 4× of that band in log scale;
+    * the engine iterate is as good a least-squares point as the oracle's:
+      the true ‖M x − b‖ inside the same band and ‖Mᵀ(Mx − b)‖/(‖M‖‖Mx − b‖)
+      at most 2× the worst of the oracle's runs.
+    The outputs themselves are still reported against the 1-ulp envelope
+    (tallied, cap 12) as a sanity bound; the 1e-6 claim for config 4 rests on
+    the converging variant above."""
     tally, it_f, it_r, infos = _synthetic_check(ConicBatch, 2, 500, [(3, 25)] * 20, SEED0 + 4,
                                                 "config-4 bench shape", cap=12, trials=2)
     assert (it_f == 1001).all() and (it_r == 1001).all()
     assert all(fi == (1001, 7) and ri == (1001, 7) for fi, ri in infos)
+    from diffopt_amd.synthetic import conic_numpy
+    cones = [(3, 25)] * 20
+    d = conic_numpy(2, 500, cones, SEED0 + 4)
+    e = ConicBatch(2, 500, cones)
+    e.set(d["A"], d["b"], d["c"], d["x"], d["s"], d["y"])
+    (out, _), (g, *_r) = e.forward_reverse(d["dx"], d["dA"], d["db"], d["dc"], want_dA=False)
+    nr = e.lsqr_norms()
+    st = e.lsqr_stats()
+    e.close()
+    assert (st["istop"] == 7).all() and (st["fwd_istop"] == 7).all()
+    keys = ("rnorm", "arnorm", "xnorm", "anorm")
+    lines = []
+    for b in range(2):
+        cache = ocn.Cache(d["A"][b], d["b"][b], d["c"][b], d["x"][b], d["s"][b], d["y"][b], cones)
+        M = cache.M()
+        frhs = ocn.forward_rhs(cache, d["dA"][b], d["db"][b], d["dc"][b])
+        rrhs = np.concatenate([d["dx"][b], np.zeros(cache.m), [-(cache.x @ d["dx"][b])]])
+        for name, rhs, x, est in (("fwd", frhs, out[b], nr["fwd"][b]), ("rev", rrhs, g[b], nr["last"][b])):
+            rng = np.random.default_rng(7)
+            runs = []
+            for t in range(5):
+                rr = rhs if t == 0 else rhs * (1.0 + 2.0 ** -52 * rng.standard_normal(rhs.shape))
+                stt = {}
+                from oracle.lsqr import lsqr
+                xo, it, istop = lsqr(cache.matvec, cache.rmatvec, rr, len(rr), return_info=True, stats=stt)
+                assert (it, istop) == (1001, 7)
+                runs.append([stt[k] for k in keys] + list(_ls_quality(M, rhs, xo)))
+            runs = np.array(runs)
+            lo, hi = runs.min(0), runs.max(0)
+            sp = hi - lo
+            q = _ls_quality(M, rhs, x)
+            got = list(est) + list(q)
+            lines.append(f"problem {b} {name}: engine {np.array2string(np.array(got), precision=4)}; "
+                         f"oracle min {np.array2string(lo, precision=4)} max {np.array2string(hi, precision=4)}")
+            for j in (0, 2, 3, 4):   # rnorm, xnorm, anorm, true ‖Mx − b‖
+                assert lo[j] - 2 * sp[j] <= got[j] <= hi[j] + 2 * sp[j], (b, name, j, got[j], lo[j], hi[j])
+            assert lo[1] / 4 <= got[1] <= hi[1] * 4, (b, name, "arnorm", got[1], lo[1], hi[1])
+            assert got[5] <= 2 * hi[5], (b, name, "normal residual", got[5], hi[5])
+    print("[parity] config-4 maxiter quality:\n  " + "\n  ".join(lines))
 
 
 def test_config5_full_shape(ConicBatch):
