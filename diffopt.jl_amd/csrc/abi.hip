@@ -116,6 +116,7 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
       if (e[0] == '0' || e[0] == '1') h->conic_split = e[0] - '0';
     }
     if (const char* e = getenv("DOPT_LU")) h->lu_mode = atoi(e) != 0;
+    if (const char* e = getenv("DOPT_SYM")) h->sym_mode = atoi(e) != 0;
     if (kind == DOPT_KIND_QP) {
       // largest supported system: the generic solve stages an nmax vector in
       // LDS (64 KB); the blocked route takes reduced systems up to BLOCKED_MAX
@@ -132,6 +133,7 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
       h->kls.ensure((size_t)2 * batch * std::max(m, 1) * sizeof(double));
       h->gk.ensure((size_t)batch * std::max(n, 1) * std::max(m, 1) * sizeof(double));
       h->meta.ensure((size_t)std::max<int64_t>(batch, 1) * sizeof(dopt::QPMeta));
+      h->kamax.ensure((size_t)std::max<int64_t>(batch, 1) * sizeof(double));
       // rhs: [reverse RHS | full forward RHS | reduced forward RHS]; x: [reverse | forward]
       h->rhs.ensure((size_t)3 * batch * std::max(h->nmax, 1) * sizeof(double));
       h->x.ensure((size_t)2 * batch * std::max(h->nmax, 1) * sizeof(double));
@@ -152,7 +154,7 @@ int dopt_destroy(dopt_handle* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   DevBuf* bufs[] = {&h->dinv, &h->plist, &h->lsqr_ws, &h->binv, &h->fwdw, &h->K, &h->ipiv, &h->s, &h->kidx, &h->meta, &h->rhs,
                     &h->x, &h->cone_dev, &h->vp, &h->dpi, &h->cwork, &h->cinfo, &h->cnorm, &h->csplit, &h->krhs, &h->kx,
-                    &h->kfull, &h->nlp_map, &h->nlp_shift, &h->nlp_scale};
+                    &h->kfull, &h->kamax, &h->nlp_map, &h->nlp_shift, &h->nlp_scale};
   for (auto* b : bufs) b->release();
   for (auto& b : h->own_nin) b.release();
   for (auto& b : h->own_in) b.release();

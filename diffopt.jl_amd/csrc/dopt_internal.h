@@ -61,7 +61,10 @@ struct QPMeta {
   int32_t info;      // 0 ok, k>0 zero pivot at column k of the reduced system
   int32_t lu;        // QPLu: which factors K holds
   int32_t gk_ok;     // assembly: the speculative G_k copy (kept = λ ≠ 0 rows) is the kept set
-  int32_t pad[2];
+  int32_t sym;       // 1: P·K is symmetric (P = diag(1, λ_k, 1): every kept λ finite and non-zero, Q
+                     // symmetric) — the no-pivot LU computes only the lower trailing tiles and takes
+                     // U12 from L21 (qp_nopiv.hip); 0: every tile
+  int32_t pad;
 };
 
 constexpr int ASM_WPP = 16;          // assembly tile workgroups per problem (qp_assemble.hip)
@@ -84,7 +87,20 @@ __host__ __device__ inline int qp_route(int iterative, int nsys) {
 // pivot tolerance (the reference's `LHS \ RHS`, QuadraticProgram.jl:490);
 // otherwise the problem is re-assembled and factorised with partial pivoting.
 constexpr double NOPIV_LMAX = 10.0;
+// ... and only while the factor shows no element growth: every pivot and every
+// entry of U within NOPIV_GROWTH·max|K| (max|K| of the assembled system,
+// `kamax`); a larger one rejects the problem as above (the
+// multiplier bound alone lets growth of order 11^k through).
+constexpr double NOPIV_GROWTH = 1e8;
 
+// P-symmetric no-pivot LU (QPMeta::sym): the row scale p_r of the reduced
+// system's row r — λ of a kept inequality row, 1 for the z and ν rows
+// (kl = the problem's compacted λ_k, null for non-QP systems).
+struct PScale {
+  const double* kl;
+  int n, nk;
+  __device__ double operator()(int r) const { return (kl && r >= n && r < n + nk) ? kl[r - n] : 1.0; }
+};
 // QP problem inputs / forward tangents as seen by the kernels (device pointers)
 struct QPIn {
   const double *Q, *G, *h, *A, *z, *lam, *nu;
@@ -112,6 +128,7 @@ struct Handle {
   int32_t nmax = 0, ld = 0;  // max system size, K row stride (doubles)
   DevBuf K, ipiv, s, kidx, meta, rhs, x;
   DevBuf kls;                // kept rows' λ_k and s_k, compacted (assembly tiles)
+  DevBuf kamax;              // per problem: max |K| of the assembled system (no-pivot growth bound)
   DevBuf gk;                 // kept rows of G, compacted column-major (n × m per problem; assembly tiles)
   DevBuf dinv;               // per-problem diagonal-block inverses (L11⁻¹ | U11⁻¹ per 32-block)
   DevBuf plist;              // problem indices of the partial-pivoting re-factorisation
@@ -127,6 +144,9 @@ struct Handle {
   // partial-pivoting re-factorisation of rejected problems (default);
   // 0 = partial pivoting for every problem (env DOPT_LU=0)
   int32_t lu_mode = 1;
+  // P-symmetric no-pivot LU for the problems that qualify (QPMeta::sym); 0:
+  // the general no-pivot LU for every problem (env DOPT_SYM=0)
+  int32_t sym_mode = 1;
   int32_t blocked_npmax = 0;       // largest padded blocked system of the current factorisation
   bool has_generic = true;         // some problem exceeds BLOCKED_MAX
   int32_t n_generic = 0;           // problems factorised by the generic LU (last factorisation)

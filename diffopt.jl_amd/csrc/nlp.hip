@@ -79,7 +79,7 @@ __global__ __launch_bounds__(NT) void nlp_assemble_kernel(NLPDims d, NLPMap mp, 
                                                           int ld, int nmax, QPMeta* __restrict__ meta,
                                                           const int32_t* __restrict__ shift,
                                                           const int32_t* __restrict__ plist,
-                                                          double* __restrict__ partial) {
+                                                          double* __restrict__ partial, double* __restrict__ kamax) {
   __shared__ double red[NT / 64];
   double amax = 0.0;
   const int b = plist ? plist[blockIdx.y] : (int)blockIdx.y;
@@ -145,6 +145,9 @@ __global__ __launch_bounds__(NT) void nlp_assemble_kernel(NLPDims d, NLPMap mp, 
     double m = red[0];
     for (int w = 1; w < NT / 64; ++w) m = fmax(m, red[w]);
     partial[bb * gridDim.x + blockIdx.x] = m;
+    // max |M| of the problem: the no-pivot LU's growth bound (non-negative
+    // doubles order as their bit patterns)
+    atomicMax(reinterpret_cast<unsigned long long*>(kamax) + bb, (unsigned long long)__double_as_longlong(m));
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     QPMeta mm = {};
@@ -360,7 +363,7 @@ void assemble(Handle& h, const int32_t* plist, int count) {
   if (count == 0) return;
   hipLaunchKernelGGL(nlp_assemble_kernel, dim3(row_blocks(h), count), dim3(NT), 0, h.stream, dims(h), map_of(h),
                      inputs(h), h.K.as<double>(), h.ld, h.nmax, h.meta.as<QPMeta>(), h.nlp_shift.as<int32_t>(),
-                     plist, h.nlp_scale.as<double>());
+                     plist, h.nlp_scale.as<double>(), h.kamax.as<double>());
   DOPT_CHECK_HIP(hipGetLastError());
 }
 
@@ -397,6 +400,7 @@ void nlp_configure(Handle& h) {
   h.K.ensure((size_t)B * h.nmax * h.ld * sizeof(double));
   h.ipiv.ensure((size_t)B * h.nmax * sizeof(int32_t));
   h.meta.ensure((size_t)std::max<int64_t>(B, 1) * sizeof(QPMeta));
+  h.kamax.ensure((size_t)std::max<int64_t>(B, 1) * sizeof(double));
   h.rhs.ensure((size_t)2 * B * h.nmax * sizeof(double));
   h.x.ensure((size_t)2 * B * h.nmax * sizeof(double));
   h.nlp_shift.ensure((size_t)std::max<int64_t>(B, 1) * sizeof(int32_t));
@@ -413,6 +417,7 @@ void nlp_factor(Handle& h) {
   if (!h.nset) throw Error(-1, "dopt_nlp_factor: the NLP point has not been set");
   const int B = (int)h.batch;
   DOPT_CHECK_HIP(hipMemsetAsync(h.nlp_shift.p, 0, (size_t)B * sizeof(int32_t), h.stream));
+  DOPT_CHECK_HIP(hipMemsetAsync(h.kamax.p, 0, (size_t)B * sizeof(double), h.stream));
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
     assemble(h, nullptr, B);

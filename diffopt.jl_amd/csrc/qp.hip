@@ -716,9 +716,9 @@ static void check_launch() { DOPT_CHECK_HIP(hipGetLastError()); }
 // qp_assemble.hip
 template <int RPT>
 __global__ void qp_prep_kernel(QPIn, double*, int32_t*, int32_t*, double*, double*, int64_t, QPMeta*,
-                               const int32_t*);
-__global__ void qp_asm_tile_kernel(QPIn, const int32_t*, const double*, const double*, int64_t, const QPMeta*, double*,
-                                   int, int, const int32_t*);
+                               const int32_t*, double*, int);
+__global__ void qp_asm_tile_kernel(QPIn, const int32_t*, const double*, const double*, int64_t, QPMeta*, double*,
+                                   int, int, const int32_t*, int, double*);
 int prep_rows_per_thread(int m);
 int prep_threads(int m);
 size_t prep_lds(int n);
@@ -751,29 +751,30 @@ static int32_t* rpos_of(Handle& h) { return h.kidx.as<int32_t>() + (size_t)h.bat
 // prepare (s, kept rows, metadata) + assembly of `count` problems (plist:
 // their indices; null = all).  `after_prep` runs between the two launches
 // (the metadata read-back: it only needs the prepare kernel, so the host's
-// wait overlaps the tile kernel).
+// wait overlaps the tile kernel).  `full`: every tile, also for P-symmetric
+// problems (the partial-pivoting paths read the whole K).
 template <class F>
-static void prep_assemble(Handle& h, const int32_t* plist, int count, F&& after_prep) {
+static void prep_assemble(Handle& h, const int32_t* plist, int count, bool full, F&& after_prep) {
   if (count == 0) return;
   const QPIn P = qp_inputs(h);
   const dim3 pg(count), pb(prep_threads(h.m));
   if (prep_rows_per_thread(h.m) == 2)
     hipLaunchKernelGGL(qp_prep_kernel<2>, pg, pb, prep_lds(h.n), h.stream, P, h.s.as<double>(),
                        h.kidx.as<int32_t>(), rpos_of(h), h.kls.as<double>(), h.gk.as<double>(), h.batch, h.meta.as<QPMeta>(),
-                       plist);
+                       plist, h.kamax.as<double>(), h.sym_mode);
   else
     hipLaunchKernelGGL(qp_prep_kernel<1>, pg, pb, prep_lds(h.n), h.stream, P, h.s.as<double>(),
                        h.kidx.as<int32_t>(), rpos_of(h), h.kls.as<double>(), h.gk.as<double>(), h.batch, h.meta.as<QPMeta>(),
-                       plist);
+                       plist, h.kamax.as<double>(), h.sym_mode);
   check_launch();
   after_prep();
   hipLaunchKernelGGL(qp_asm_tile_kernel, dim3((unsigned)count * ASM_WPP), dim3(512), 0, h.stream, P,
                      h.kidx.as<int32_t>(), h.kls.as<double>(), h.gk.as<double>(), h.batch, h.meta.as<QPMeta>(),
                      h.K.as<double>(), h.ld,
-                     h.nmax, plist);
+                     h.nmax, plist, full ? 1 : 0, h.kamax.as<double>());
   check_launch();
 }
-static void prep_assemble(Handle& h, const int32_t* plist, int count) { prep_assemble(h, plist, count, [] {}); }
+static void prep_assemble(Handle& h, const int32_t* plist, int count) { prep_assemble(h, plist, count, true, [] {}); }
 
 // Asynchronous read-back of the per-problem metadata into pinned memory; the
 // caller may queue independent kernels before waiting (meta_wait), so the
@@ -915,7 +916,7 @@ void qp_factor(Handle& h) {
   if (!h.set) throw Error(-1, "dopt_qp_factor: dopt_qp_set has not been called");
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
-    prep_assemble(h, nullptr, (int)h.batch, [&] { meta_copy(h); });
+    prep_assemble(h, nullptr, (int)h.batch, h.lu_mode == 0, [&] { meta_copy(h); });
   }
   meta_sizes(h);
   factor_blocked(h, [] {}, nullptr, nullptr, qp_reasm(h));
@@ -1141,7 +1142,7 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
   const FwdTangents T = tangents(h, dQ, dq, dG, dh, dA, db);
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
-    prep_assemble(h, nullptr, (int)h.batch, [&] { meta_copy(h); });
+    prep_assemble(h, nullptr, (int)h.batch, h.lu_mode == 0, [&] { meta_copy(h); });
   }
   // no-pivot LU: both right-hand sides ride along as a bordering column / row
   // and come out forward-swept (w0, w1, written by the RHS kernels next to

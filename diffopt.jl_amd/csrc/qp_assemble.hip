@@ -61,10 +61,11 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
                                                             int32_t* __restrict__ kidx, int32_t* __restrict__ rpos,
                                                             double* __restrict__ kls, double* __restrict__ gk,
                                                             int64_t B, QPMeta* __restrict__ meta,
-                                                            const int32_t* __restrict__ plist) {
+                                                            const int32_t* __restrict__ plist,
+                                                            double* __restrict__ kamax, int sym_mode) {
   extern __shared__ __attribute__((aligned(16))) double zdyn[];
   __shared__ int cnt[PREP_MAXT / 64 + 1], scnt[PREP_MAXT / 64 + 1];
-  __shared__ int extra;
+  __shared__ int extra, asym;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int T = (int)blockDim.x, NW = T >> 6;
   const int b = plist ? plist[blockIdx.x] : (int)blockIdx.x;
@@ -96,6 +97,7 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
     cnt[NW] = 0;
     scnt[NW] = 0;
     extra = 0;
+    asym = 0;
   }
   __syncthreads();
   const double* Gb = P.G + (size_t)b * m * n;
@@ -209,6 +211,8 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
         s_out[(size_t)b * m + i + q] = si[q];
         keep[q] = iterative ? 1 : !(li[q] == 0.0 && si[q] != 0.0);
         if (keep[q] && !spec[q]) atomicAdd(&extra, 1);
+        // a kept row with λ = 0 (s = 0) or a non-finite λ breaks the P-symmetry
+        if (keep[q] && !(fabs(li[q]) > 0.0 && fabs(li[q]) <= 1.7976931348623157e308)) asym = 1;
       }
     }
     // ascending compaction of the kept rows: ballot prefixes within the wave
@@ -259,12 +263,15 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
     meta[b].info = 0;
     meta[b].lu = LU_NONE;
     meta[b].gk_ok = extra == 0;
+    // P·K symmetric up to Q's own symmetry, which the tile kernel checks
+    meta[b].sym = sym_mode && !asym && qp_route(iterative, n + nk + p) == ROUTE_BLOCKED;
+    kamax[b] = 0.0;
   }
 }
 template __global__ void qp_prep_kernel<1>(QPIn, double*, int32_t*, int32_t*, double*, double*, int64_t, QPMeta*,
-                                           const int32_t*);
+                                           const int32_t*, double*, int);
 template __global__ void qp_prep_kernel<2>(QPIn, double*, int32_t*, int32_t*, double*, double*, int64_t, QPMeta*,
-                                           const int32_t*);
+                                           const int32_t*, double*, int);
 
 int prep_rows_per_thread(int m) { return (m % 2 == 0) ? 2 : 1; }
 int prep_threads(int m) {
@@ -280,14 +287,21 @@ size_t prep_lds(int n) { return n <= ZLDS_MAX ? (size_t)std::max(n, 1) * sizeof(
 // Per pair: the kept rows' (index, λ, s) of both tile ranges staged in LDS;
 // every load of both tiles issued (column-major sources transposed into the
 // LDS tiles, the rest written in place); one barrier; 16-byte row stores.
+// P-symmetric problems (meta.sym, unless `full`): the no-pivot LU reads only
+// the diagonal and lower tiles, so an upper tile is neither stored nor, where
+// it holds no Q entries, loaded; where it does, it is loaded to check Q's
+// symmetry against its mirror — a mismatch stores it after all and marks the
+// problem LU_REJECT (re-assembled in full and factorised with partial
+// pivoting).  max |K| over the stored tiles → kamax (the growth bound).
 constexpr int AT = 64, ATLD = AT + 2, ATH = 512;
 constexpr int AK1 = AT * AT / ATH;   // elements per thread per tile (8)
 
 __global__ __launch_bounds__(ATH) void qp_asm_tile_kernel(QPIn P, const int32_t* __restrict__ kidx,
                                                           const double* __restrict__ kls,
                                                           const double* __restrict__ gk, int64_t B,
-                                                          const QPMeta* __restrict__ meta, double* __restrict__ Kper,
-                                                          int ld, int nmax, const int32_t* __restrict__ plist) {
+                                                          QPMeta* __restrict__ meta, double* __restrict__ Kper,
+                                                          int ld, int nmax, const int32_t* __restrict__ plist,
+                                                          int full, double* __restrict__ kamax) {
   __shared__ __attribute__((aligned(16))) double Ts[2][AT * ATLD];
   __shared__ int kid_s[2][AT];
   __shared__ double lam_s[2][AT], s_s[2][AT];
@@ -297,6 +311,7 @@ __global__ __launch_bounds__(ATH) void qp_asm_tile_kernel(QPIn P, const int32_t*
   const int n = P.n, m = P.m, p = P.p;
   const int nk = meta[b].nk;
   const bool gk_ok = meta[b].gk_ok != 0;
+  const bool half = !full && meta[b].sym != 0;   // lower + diagonal tiles only
   const int N = n + nk + p, Np = (N + 31) & ~31, TT = (Np + AT - 1) / AT;
   const int npairs = TT * (TT + 1) / 2;
   if (g >= npairs) return;
@@ -395,15 +410,18 @@ __global__ __launch_bounds__(ATH) void qp_asm_tile_kernel(QPIn P, const int32_t*
       }
     }
   };
+  double vmax = 0.0;   // max |K| over this thread's stores
   auto tile_store = [&](int r0, int c0, const double* Tl) {
     const int cp = 2 * (t & 31), rw = t >> 5;
     if (c0 + cp >= Np) return;
 #pragma unroll
     for (int k = 0; k < AT / 16; ++k) {
       const int rr = rw + 16 * k, r = r0 + rr;
-      if (r < Np)
-        *reinterpret_cast<double2*>(K + (size_t)r * ld + c0 + cp) =
-            *reinterpret_cast<const double2*>(Tl + rr * ATLD + cp);
+      if (r < Np) {
+        const double2 v = *reinterpret_cast<const double2*>(Tl + rr * ATLD + cp);
+        *reinterpret_cast<double2*>(K + (size_t)r * ld + c0 + cp) = v;
+        vmax = fmax(vmax, fmax(fabs(v.x), fabs(v.y)));
+      }
     }
   };
 
@@ -421,13 +439,32 @@ __global__ __launch_bounds__(ATH) void qp_asm_tile_kernel(QPIn P, const int32_t*
       s_s[which][e] = ok ? skb[ci] : 0.0;
     }
     __syncthreads();
-    tile_load(R * AT, C * AT, 0, 1, Ts[0]);
+    // upper tile (R, C), R < C: skipped for P-symmetric problems, loaded only
+    // to check Q's symmetry where it overlaps Q
+    const bool qpart = R * AT < n && C * AT < n;
+    const bool up_load = R == C || !half || qpart;
+    if (up_load) tile_load(R * AT, C * AT, 0, 1, Ts[0]);
     if (R != C) tile_load(C * AT, R * AT, 1, 0, Ts[1]);
     __syncthreads();
-    tile_store(R * AT, C * AT, Ts[0]);
+    bool up_store = !half || R == C;
+    if (half && R != C && qpart) {
+      int bad = 0;
+      for (int e = t; e < AT * AT; e += ATH) {
+        const int i = e >> 6, j = e & 63;   // upper (R·64 + i, C·64 + j) vs lower (C·64 + j, R·64 + i)
+        if (R * AT + i < n && C * AT + j < n) bad |= Ts[0][i * ATLD + j] != Ts[1][j * ATLD + i];
+      }
+      if (__syncthreads_or(bad)) {
+        up_store = true;
+        if (t == 0) meta[b].lu = LU_REJECT;
+      }
+    }
+    if (up_store) tile_store(R * AT, C * AT, Ts[0]);
     if (R != C) tile_store(C * AT, R * AT, Ts[1]);
     __syncthreads();   // Ts and the staged ranges are reused by the next pair
   }
+  for (int o = 32; o > 0; o >>= 1) vmax = fmax(vmax, __shfl_xor(vmax, o));
+  if ((t & 63) == 0)
+    atomicMax(reinterpret_cast<unsigned long long*>(kamax) + b, (unsigned long long)__double_as_longlong(vmax));
 }
 
 size_t dinv_stride(int nmax) { return (size_t)((nmax + 31) / 32) * 2 * 32 * 32; }

@@ -104,6 +104,29 @@ __device__ __forceinline__ int nlu_np(const QPMeta& mm) {
   return (mm.nsys + 31) & ~31;
 }
 
+// the growth bound of a problem (no bound when its max |K| is unknown: 0)
+__device__ __forceinline__ double growth_bound(double amax) {
+  return amax > 0.0 ? NOPIV_GROWTH * amax : 1.7976931348623157e308;
+}
+
+// row scales of problem b (QP: the compacted λ_k; null kls: all 1)
+__device__ __forceinline__ PScale pscale(const double* kls, int b, int n, int m, const QPMeta& mm) {
+  PScale ps;
+  ps.kl = kls ? kls + (size_t)b * m : nullptr;
+  ps.n = n;
+  ps.nk = mm.nk;
+  return ps;
+}
+
+// Tile of a per-problem grid: `tiles` per problem in the full grid, or the
+// lower triangle (rt ≥ ct) of an nrt × nrt grid when `lower`.
+__device__ __forceinline__ void lower_tile(int tile, int& rt, int& ct) {
+  rt = (int)((sqrtf(8.0f * tile + 1.0f) - 1.0f) * 0.5f);
+  while ((rt + 1) * (rt + 2) / 2 <= tile) ++rt;
+  while (rt * (rt + 1) / 2 > tile) --rt;
+  ct = tile - rt * (rt + 1) / 2;
+}
+
 // ---------------------------------------------------------------------------
 // Single-wave LU (no pivoting) of the 32×32 block at rows / columns o..o+31
 // of the LDS image S: lane = 4×4 tile (ti = lane >> 3, tj = lane & 7); the
@@ -118,7 +141,7 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double* colb, double* trash) {
+__device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double* colb, double* trash, double bound) {
   const int lane = threadIdx.x & 63, ti = lane >> 3, tj = lane & 7;
   double a[4][4];
 #pragma unroll
@@ -178,7 +201,8 @@ __device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double*
   // L and U from the registers to S (K's 32×32 diagonal blocks are never
   // read again: the solves use their inverses, dinv); the threshold test once, on the final values
   // (a pivot and a multiplier never change after their step): every pivot
-  // non-zero and finite, every |l| ≤ NOPIV_LMAX (NaN fails)
+  // non-zero and within the growth bound (finite), every |l| ≤ NOPIV_LMAX
+  // (NaN fails)
   int bad = 0;
 #pragma unroll
   for (int r = 0; r < 4; ++r)
@@ -186,7 +210,7 @@ __device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double*
     for (int c = 0; c < 4; ++c) {
       const int gi = 4 * ti + r, gj = 4 * tj + c;
       S[(o + gi) * SLD + o + gj] = a[r][c];
-      if (gi == gj) bad |= !(fabs(a[r][c]) > 0.0) || !(fabs(a[r][c]) <= 1.7976931348623157e308);
+      if (gi == gj) bad |= !(fabs(a[r][c]) > 0.0) || !(fabs(a[r][c]) <= bound);
       if (gi > gj) bad |= !(fabs(a[r][c]) <= NOPIV_LMAX);
     }
   return __any(bad) ? 1 : 0;
@@ -347,7 +371,8 @@ __device__ __forceinline__ d4n tile32(int tr, int tc, FA A, FB Bm, int ns = 8) {
 // Writes U_ab / L_ba to K, perm = identity, the 32×32 diagonal-block inverses to
 // dinv and, when a trailing step follows, the packed 64×64 inverse (L11⁻¹
 // strictly below the diagonal, U11⁻¹ on and above it) to `Bg`.  A failed
-// threshold test marks the problem LU_REJECT and stops.  Called by the whole
+// threshold test (|l| > NOPIV_LMAX, or a pivot / U_ab entry beyond `bound` =
+// NOPIV_GROWTH·max|K|) marks the problem LU_REJECT and stops.  Called by the whole
 // 256-thread workgroup (workgroup-uniform arguments).
 // ---------------------------------------------------------------------------
 struct DiagLds {
@@ -401,7 +426,7 @@ __device__ __forceinline__ void fwd_block(const DiagLds& L, double* __restrict__
 __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__ Kb, int ld,
                                           int32_t* __restrict__ permb, double* __restrict__ Db,
                                           QPMeta* __restrict__ mb, int c0, int Np, int N, double* __restrict__ Bg,
-                                          double* __restrict__ w0b, double* __restrict__ w1b) {
+                                          double* __restrict__ w0b, double* __restrict__ w1b, double bound) {
   double* S = L.S;
   const int Wv = min(NB64, Np - c0);   // 32 or 64
   const bool trsm = Np - c0 > NB64;    // a trailing step follows
@@ -417,7 +442,7 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
 
   // ---- A. LU of block a
   if (wv == 0) {
-    const int bad = wave_lu32(S, 0, L.rowb, L.colb, L.trash);
+    const int bad = wave_lu32(S, 0, L.rowb, L.colb, L.trash, bound);
     if (lane == 0 && bad) *L.sbad = 1;
   }
   __syncthreads();
@@ -460,7 +485,7 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
       Kb[(size_t)(c0 + i) * ld + c0 + 32 + j] = au[rr];
       S[(32 + i) * SLD + j] = al[rr];
       Kb[(size_t)(c0 + 32 + i) * ld + c0 + j] = al[rr];
-      bad |= !(fabs(al[rr]) <= NOPIV_LMAX);
+      bad |= !(fabs(al[rr]) <= NOPIV_LMAX) || !(fabs(au[rr]) <= bound);
     }
     if (__any(bad) && lane == 0) *L.sbad = 1;   // every writer stores the same value
   }
@@ -489,7 +514,7 @@ __device__ __forceinline__ void diag_core(const DiagLds& L, double* __restrict__
 
   // ---- D. LU of block b
   if (wv == 0) {
-    const int bad = wave_lu32(S, 32, L.rowb, L.colb, L.trash);
+    const int bad = wave_lu32(S, 32, L.rowb, L.colb, L.trash, bound);
     if (lane == 0 && bad) *L.sbad = 1;
   }
   __syncthreads();
@@ -591,8 +616,11 @@ static_assert((NB64 * SLD + 200) % 2 == 0, "trash slots 16-byte aligned");
 // an inverse are skipped.  nlu_cross_kernel, which computes the other strips
 // of the step, reads these two as its shared operands.  sw: strip width (32
 // or 64); no barrier follows, so inactive waves return at once.
+// P-symmetric problems (sym): U12(0) is not computed but taken from L21(0),
+// U_kj = (u_kk / p_k)·L_jk·p_j (P·K symmetric ⇒ U = D_u·P⁻¹·Lᵀ·P), u_kk from
+// the packed inverse's diagonal.  Every U12 entry is held to the growth bound.
 __device__ __forceinline__ void diag_strip0(const double* S, double* __restrict__ Kb, int ld, int c0, int sw,
-                                            QPMeta* __restrict__ mb) {
+                                            QPMeta* __restrict__ mb, double bound, bool sym, PScale ps) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
   if (16 * wv >= sw) return;   // wave-uniform
   const int r0 = c0 + NB64;
@@ -618,6 +646,23 @@ __device__ __forceinline__ void diag_strip0(const double* S, double* __restrict_
       Kb[(size_t)(r0 + 16 * wv + g + 4 * rr) * ld + c0 + 16 * ct + l16] = acc[ct][rr];
       over |= !(fabs(acc[ct][rr]) <= NOPIV_LMAX);
     }
+  if (sym) {
+    // U12(0)[k][j], k = 16ct + l16 (the block row), j = r0 + 16wv + g + 4rr
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int k = 16 * ct + l16;
+      const double uk = 1.0 / (S[k * SLD + k] * ps(c0 + k));   // u_kk / p_k (S: U11⁻¹ on the diagonal)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int j = r0 + 16 * wv + g + 4 * rr;
+        const double u = uk * acc[ct][rr] * ps(j);
+        Kb[(size_t)(c0 + k) * ld + j] = u;
+        over |= !(fabs(u) <= bound);
+      }
+    }
+    if (__any(over) && lane == 0) mb->lu = LU_REJECT;
+    return;
+  }
   if (__any(over) && lane == 0) mb->lu = LU_REJECT;   // every writer stores the same value
   const double* bsrc = Kb + (size_t)(c0 + g) * ld + r0 + 16 * wv + l16;
 #pragma unroll
@@ -632,10 +677,15 @@ __device__ __forceinline__ void diag_strip0(const double* S, double* __restrict_
       acc[it] = nmfma(k == i ? 1.0 : (k < i ? S[i * SLD + k] : 0.0), bv[s], acc[it]);
     }
   }
+  over = 0;
 #pragma unroll
   for (int it = 0; it < 4; ++it)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) Kb[(size_t)(c0 + 16 * it + g + 4 * rr) * ld + r0 + 16 * wv + l16] = acc[it][rr];
+    for (int rr = 0; rr < 4; ++rr) {
+      Kb[(size_t)(c0 + 16 * it + g + 4 * rr) * ld + r0 + 16 * wv + l16] = acc[it][rr];
+      over |= !(fabs(acc[it][rr]) <= bound);
+    }
+  if (__any(over) && lane == 0) mb->lu = LU_REJECT;
 }
 
 // Diagonal block of step c0 of every problem: one 256-thread workgroup per
@@ -645,7 +695,7 @@ template <bool STRIP0>
 __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_diag_kernel(
     double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
     size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv, double* __restrict__ w0,
-    double* __restrict__ w1) {
+    double* __restrict__ w1, const double* __restrict__ kamax, const double* __restrict__ kls, int n, int m) {
   __shared__ double S[STEP_LDS];
   const int b = blockIdx.x;
   const QPMeta mm = meta[b];
@@ -673,15 +723,16 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
   }
   if (t == 0 && c0 == 0) meta[b].lu = LU_NOPIV;   // LU_REJECT below if a test fails
   NLU_MARK(0);
+  const double bound = growth_bound(kamax[b]);
   diag_core(DiagLds(S), Kb, ld, perm + (size_t)b * nmax, dinv + (size_t)b * dstride + (size_t)(c0 / 32) * DBLK,
             meta + b, c0, Np, mm.nsys, binv + (size_t)b * NB64 * NB64, w0 ? w0 + (size_t)b * nmax : nullptr,
-            w0 ? w1 + (size_t)b * nmax : nullptr);
+            w0 ? w1 + (size_t)b * nmax : nullptr, bound);
   if constexpr (STRIP0) {
     const int sw = min(NB64, Np - c0 - NB64);
     if (sw <= 0) return;   // no trailing step for this problem
     __syncthreads();       // S final (and the threshold verdicts of diag_core)
     if (*DiagLds(S).sbad) return;
-    diag_strip0(S, Kb, ld, c0, sw, meta + b);
+    diag_strip0(S, Kb, ld, c0, sw, meta + b, bound, mm.sym != 0, pscale(kls, b, n, m, mm));
   }
 }
 
@@ -693,30 +744,35 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
 // columns; the operand shared by the four waves (U11⁻¹, or the A12 strip) is
 // staged in LDS.  The k-steps that meet only the zero triangle of an inverse
 // are skipped at compile time (40 of 64 per wave on average).  XCD-aware
-// order: one problem's strips are consecutive.
+// order: one problem's strips are consecutive.  P-symmetric problems: side 1
+// does nothing, side 0 writes U12 = D_u·P⁻¹·L21ᵀ·P beside L21 (transposed
+// through LDS).  Every U12 entry is held to the growth bound.
 // ---------------------------------------------------------------------------
 constexpr int TLD = 64 + 16;   // LDS row stride (doubles) of a staged 64×64 operand
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_trsm_kernel(double* __restrict__ K, int ld, int nmax,
                                                        QPMeta* __restrict__ meta, int c0,
                                                        const double* __restrict__ binv, int nst,
-                                                       int total) {
+                                                       int total, const double* __restrict__ kamax,
+                                                       const double* __restrict__ kls, int n, int m, int nsides) {
   __shared__ double X[NB64 * TLD];
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
   const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
-  const int b = logical / (2 * nst);
-  const int rem = logical - b * 2 * nst;
+  const int b = logical / (nsides * nst);   // nsides 1: side 0 only (every problem P-symmetric)
+  const int rem = logical - b * nsides * nst;
   const int side = rem / nst, st = rem - side * nst;
   const QPMeta mm = meta[b];
   const int Np = nlu_np(mm);
   const int R2 = Np - c0 - NB64;
-  if (mm.lu == LU_REJECT || st * 64 >= R2) return;   // workgroup-uniform
+  const bool sym = mm.sym != 0;
+  if (mm.lu == LU_REJECT || st * 64 >= R2 || (sym && side == 1)) return;   // workgroup-uniform
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
   double* Kb = K + (size_t)b * nmax * ld;
   const double* Bg = binv + (size_t)b * NB64 * NB64;
   const int s0 = c0 + NB64 + 64 * st;          // first row (side 0) / column (side 1) of the strip
   const int sw = min(64, R2 - 64 * st);        // 32 or 64
+  const double bound = growth_bound(kamax[b]);
   if (side == 0) {
     // every global load of the workgroup in flight before the first LDS
     // store: U11⁻¹ (the packed inverse, L2-resident) and the A21 rows (HBM)
@@ -737,22 +793,50 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
       X[k * TLD + c] = k <= c ? v[q] : 0.0;
     }
     __syncthreads();
-    if (!wact) return;
+    if (!sym && !wact) return;
     d4n acc[4];
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      acc[ct] = (d4n){0, 0, 0, 0};
-#pragma unroll
-      for (int s = 0; s < 4 * (ct + 1); ++s)
-        acc[ct] = nmfma(av[s], X[(4 * s + g) * TLD + 16 * ct + l16], acc[ct]);
-    }
     int over = 0;
+    if (wact) {
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
+      for (int ct = 0; ct < 4; ++ct) {
+        acc[ct] = (d4n){0, 0, 0, 0};
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        Kb[(size_t)(row + g + 4 * rr) * ld + c0 + 16 * ct + l16] = acc[ct][rr];
-        over |= !(fabs(acc[ct][rr]) <= NOPIV_LMAX);
+        for (int s = 0; s < 4 * (ct + 1); ++s)
+          acc[ct] = nmfma(av[s], X[(4 * s + g) * TLD + 16 * ct + l16], acc[ct]);
+      }
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          Kb[(size_t)(row + g + 4 * rr) * ld + c0 + 16 * ct + l16] = acc[ct][rr];
+          over |= !(fabs(acc[ct][rr]) <= NOPIV_LMAX);
+        }
+      }
+    }
+    if (sym) {
+      // U12[k][j] = (u_kk / p_k)·L21[j][k]·p_j, k = 16ct + l16, j = row + g + 4rr:
+      // through LDS (X free once every wave's MFMAs are done), then row stores
+      const PScale ps = pscale(kls, b, n, m, mm);
+      __syncthreads();
+      if (wact) {
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          const int k = 16 * ct + l16;
+          const double uk = 1.0 / (Bg[k * NB64 + k] * ps(c0 + k));
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int jl = 16 * wv + g + 4 * rr;
+            const double u = uk * acc[ct][rr] * ps(s0 + jl);
+            X[k * TLD + jl] = u;
+            over |= !(fabs(u) <= bound);
+          }
+        }
+      }
+      __syncthreads();
+      const int k = t >> 2, cq = (t & 3) * 16;   // row k of the block, 16 columns
+      if (cq < sw) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) Kb[(size_t)(c0 + k) * ld + s0 + cq + u] = X[k * TLD + cq + u];
       }
     }
     if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;   // every writer stores the same value
@@ -795,13 +879,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
         for (int q = 0; q < 4; ++q) acc[q] = nmfma(av[s], X[(4 * s + g) * TLD + 16 * q + l16], acc[q]);
       }
     }
+    int over = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (16 * q < sw) {
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) Kb[(size_t)(c0 + 16 * wv + g + 4 * rr) * ld + s0 + 16 * q + l16] = acc[q][rr];
+        for (int rr = 0; rr < 4; ++rr) {
+          Kb[(size_t)(c0 + 16 * wv + g + 4 * rr) * ld + s0 + 16 * q + l16] = acc[q][rr];
+          over |= !(fabs(acc[q][rr]) <= bound);
+        }
       }
     }
+    if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;
   }
 }
 
@@ -823,23 +912,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 // update's B operand.  Wave w owns the tile's rows 16w..16w+15.  XCD-aware
 // order: one problem's tiles are consecutive.  The fused forward sweeps of
 // step c0 ride on tiles (0, J) (c −= c′U12) and (I, 0) (b −= L21 b′).
+// P-symmetric problems take only the tiles (I, 0): tile (I ≥ 1, 0) writes
+// U12(I) = D_u·P⁻¹·L21(I)ᵀ·P beside L21(I) and carries the forward sweep of
+// Kᵀ for those columns as c_j −= p_j·Σ_k (c′_k u_kk / p_k)·L21[j][k]
+// (`lower`: every problem of the batch is P-symmetric, the grid holds those
+// tiles only).  Every U12 entry is held to the growth bound.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_cross_kernel(
     double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
-    int nt, int total, double* __restrict__ w0, double* __restrict__ w1) {
+    int nt, int total, double* __restrict__ w0, double* __restrict__ w1, const double* __restrict__ kamax,
+    const double* __restrict__ kls, int n, int m, int lower) {
   __shared__ double X[NB64 * TLD];
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
   const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
-  const int tiles = 2 * nt - 1;
+  const int tiles = lower ? nt : 2 * nt - 1;
   const int b = logical / tiles;
   const int tile = logical - b * tiles;
-  const int I = tile < nt ? 0 : tile - nt + 1;   // row strip (L21, C rows)
-  const int J = tile < nt ? tile : 0;            // column strip (U12, C columns)
+  const int I = lower ? tile : (tile < nt ? 0 : tile - nt + 1);   // row strip (L21, C rows)
+  const int J = lower ? 0 : (tile < nt ? tile : 0);              // column strip (U12, C columns)
   const QPMeta mm = meta[b];
   const int Np = nlu_np(mm);
   const int R2 = Np - c0 - NB64;                 // trailing rows = columns (multiple of 32)
-  if (mm.lu == LU_REJECT || I * 64 >= R2 || J * 64 >= R2) return;   // workgroup-uniform
+  const bool sym = mm.sym != 0;
+  if (mm.lu == LU_REJECT || I * 64 >= R2 || J * 64 >= R2 || (sym && J > 0)) return;   // workgroup-uniform
+  const double bound = growth_bound(kamax[b]);
+  const PScale ps = pscale(kls, b, n, m, mm);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
   double* Kb = K + (size_t)b * nmax * ld;
   const double* Bg = binv + (size_t)b * NB64 * NB64;
@@ -902,6 +1000,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
           a[4 * ct + rr] = -lt[rr];
         }
       }
+      if (sym) {   // U12(I)[k][j] = (u_kk / p_k)·L21[j][k]·p_j, k = 16ct + g + 4rr, j = row + l16
+        const double pj = ps(row + l16);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const int k = 4 * s + g;
+          const double u = -a[s] * pj / (Bg[k * NB64 + k] * ps(c0 + k));
+          Kb[(size_t)(c0 + k) * ld + row + l16] = u;
+          over |= !(fabs(u) <= bound);
+        }
+      }
       if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;   // every writer stores the same value
     }
     __syncthreads();   // every wave is done with U11⁻¹
@@ -935,14 +1043,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
       for (int s = 0; s < 16; ++s) a[s] = -Kb[(size_t)(row + l16) * ld + c0 + 4 * s + g];
     }
     __syncthreads();   // every wave is done with A12(J)
+    int over = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         X[(16 * wv + g + 4 * rr) * TLD + 16 * q + l16] = um[q][rr];
-        if (16 * q < swJ) Kb[(size_t)(c0 + 16 * wv + g + 4 * rr) * ld + s0 + 16 * q + l16] = um[q][rr];
+        if (16 * q < swJ) {
+          Kb[(size_t)(c0 + 16 * wv + g + 4 * rr) * ld + s0 + 16 * q + l16] = um[q][rr];
+          over |= !(fabs(um[q][rr]) <= bound);
+        }
       }
     }
+    if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;
   } else {
     double u[16];
     load_strip(u);   // U12(0)
@@ -972,12 +1085,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
   if (!wact) return;
   if (w0 && J == 0) {   // fused forward sweep of K: b_I −= L21(I) b′ (a = −L21)
     const double* bp = w0 + (size_t)b * nmax + c0;
-    double ps = 0.0;
+    double sm = 0.0;
 #pragma unroll
-    for (int s = 0; s < 16; ++s) ps = fma(a[s], bp[4 * s + g], ps);
-    ps += __shfl_xor(ps, 16);
-    ps += __shfl_xor(ps, 32);
-    if (g == 0) w0[(size_t)b * nmax + row + l16] += ps;
+    for (int s = 0; s < 16; ++s) sm = fma(a[s], bp[4 * s + g], sm);
+    sm += __shfl_xor(sm, 16);
+    sm += __shfl_xor(sm, 32);
+    if (g == 0) w0[(size_t)b * nmax + row + l16] += sm;
+  }
+  if (w1 && sym && I > 0) {   // fused forward sweep of Kᵀ through L21 (the tile (0, I) is not run)
+    const double* cp = w1 + (size_t)b * nmax + c0;
+    double sm = 0.0;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = 4 * s + g;
+      sm = fma(a[s], cp[k] / (Bg[k * NB64 + k] * ps(c0 + k)), sm);
+    }
+    sm += __shfl_xor(sm, 16);
+    sm += __shfl_xor(sm, 32);
+    if (g == 0) w1[(size_t)b * nmax + row + l16] += sm * ps(row + l16);
   }
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
@@ -1004,24 +1129,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 // diagonal block and TRSM of step c0+64 — so the trailing matrix is read and
 // written once per two steps.  U12⁽ᵏ⁾ / U12⁽ᵏ⁺¹⁾ are staged in turn through
 // one 40 KB LDS tile.  Tiles (I, 0) / (0, J) of this grid also carry the
-// fused forward sweeps of step c0+64.
+// fused forward sweeps of step c0+64.  P-symmetric problems take only the
+// tiles rt ≥ ct (`lower`: the grid holds only those, every problem being
+// P-symmetric), the forward sweep of Kᵀ riding on tiles (rt, 0) through
+// L21⁽ᵏ⁺¹⁾ as in nlu_cross_kernel (binv: step c0+64's packed inverse).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_update2_kernel(double* __restrict__ K, int ld, int nmax,
                                                           const QPMeta* __restrict__ meta, int c0, int nrt,
                                                           int nct, int total, double* __restrict__ w0,
-                                                          double* __restrict__ w1) {
+                                                          double* __restrict__ w1, const double* __restrict__ binv,
+                                                          const double* __restrict__ kls, int n, int m, int lower) {
   __shared__ double U[NB64 * ULD];
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
   const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
-  const int tiles = nrt * nct;
+  const int tiles = lower ? nrt * (nrt + 1) / 2 : nrt * nct;
   const int b = logical / tiles;
   const int tile = logical - b * tiles;
-  const int rt = tile / nct, ct = tile - rt * nct;
+  int rt, ct;
+  if (lower) lower_tile(tile, rt, ct);
+  else {
+    rt = tile / nct;
+    ct = tile - rt * nct;
+  }
   const QPMeta mm = meta[b];
   const int Np = nlu_np(mm);
   const int R2 = Np - c0 - 2 * NB64;   // rows = columns after both steps (multiple of 32)
-  if (mm.lu == LU_REJECT || rt * 64 >= R2 || ct * 64 >= R2) return;   // workgroup-uniform
+  const bool sym = mm.sym != 0;
+  if (mm.lu == LU_REJECT || rt * 64 >= R2 || ct * 64 >= R2 || (sym && rt < ct)) return;   // workgroup-uniform
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
   double* Kb = K + (size_t)b * nmax * ld;
   const int cbase = c0 + 2 * NB64 + ct * 64;
@@ -1090,12 +1225,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
   if (!wact) return;
   if (w0 && ct == 0) {
     const double* bp = w0 + (size_t)b * nmax + c0 + NB64;
-    double ps = 0.0;
+    double sm = 0.0;
 #pragma unroll
-    for (int s = 0; s < NB64 / 4; ++s) ps = fma(a[s], bp[4 * s + g], ps);
-    ps += __shfl_xor(ps, 16);
-    ps += __shfl_xor(ps, 32);
-    if (g == 0) w0[(size_t)b * nmax + rbase + l16] += ps;
+    for (int s = 0; s < NB64 / 4; ++s) sm = fma(a[s], bp[4 * s + g], sm);
+    sm += __shfl_xor(sm, 16);
+    sm += __shfl_xor(sm, 32);
+    if (g == 0) w0[(size_t)b * nmax + rbase + l16] += sm;
+  }
+  if (w1 && sym && ct == 0 && rt > 0) {   // Kᵀ sweep through L21⁽ᵏ⁺¹⁾ (tile (0, rt) is not run)
+    const PScale ps = pscale(kls, b, n, m, mm);
+    const double* Bg = binv + (size_t)b * NB64 * NB64;
+    const double* cp = w1 + (size_t)b * nmax + c0 + NB64;
+    double sm = 0.0;
+#pragma unroll
+    for (int s = 0; s < NB64 / 4; ++s) {
+      const int k = 4 * s + g;
+      sm = fma(a[s], cp[k] / (Bg[k * NB64 + k] * ps(c0 + NB64 + k)), sm);
+    }
+    sm += __shfl_xor(sm, 16);
+    sm += __shfl_xor(sm, 32);
+    if (g == 0) w1[(size_t)b * nmax + rbase + l16] += sm * ps(rbase + l16);
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -1124,6 +1273,20 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   const int npmax = h.blocked_npmax;
   if (npmax == 0) return;
   const int B = (int)h.batch;
+  // P-symmetric route: the QP back-end's problems (kls: their λ_k); `lower`
+  // when every blocked problem of the batch qualifies (tile grids halved)
+  const bool qp = h.kind == DOPT_KIND_QP;
+  const double* kls = qp ? h.kls.as<double>() : nullptr;
+  const double* kamax = h.kamax.as<double>();
+  int lower = qp && h.meta_host ? 1 : 0;
+  if (lower)
+    for (int64_t b = 0; b < h.batch; ++b) {
+      const QPMeta& mm = h.meta_host[b];
+      if (qp_route(mm.iterative, mm.nsys) == ROUTE_BLOCKED && !mm.sym) {
+        lower = 0;
+        break;
+      }
+    }
   const size_t dstride = dinv_stride(h.nmax);
   double* K = h.K.as<double>();
   int32_t* perm = h.ipiv.as<int32_t>();
@@ -1137,16 +1300,16 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   auto diag = [&](int c0, bool strip0) {
     if (strip0)
       hipLaunchKernelGGL(nlu_diag_kernel<true>, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv, dstride,
-                         meta, c0, binv, w0, w1);
+                         meta, c0, binv, w0, w1, kamax, kls, h.n, h.m);
     else
       hipLaunchKernelGGL(nlu_diag_kernel<false>, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv,
-                         dstride, meta, c0, binv, w0, w1);
+                         dstride, meta, c0, binv, w0, w1, kamax, kls, h.n, h.m);
     DOPT_CHECK_HIP(hipGetLastError());
   };
   auto cross = [&](int c0, int nt) {
-    const long long tot = (2LL * nt - 1) * B;
+    const long long tot = (lower ? (long long)nt : 2LL * nt - 1) * B;
     hipLaunchKernelGGL(nlu_cross_kernel, grid(tot), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0, binv, nt,
-                       (int)tot, w0, w1);
+                       (int)tot, w0, w1, kamax, kls, h.n, h.m, lower);
     DOPT_CHECK_HIP(hipGetLastError());
   };
   for (int c0 = 0; c0 < npmax;) {
@@ -1165,13 +1328,13 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
     // step c0+64: diagonal block, TRSM, both rank-64 updates of the rest in one pass
     diag(c0 + NB64, false);
     const int nt2 = (R2 - NB64 + 63) / 64;
-    const long long tt = 2LL * nt2 * B;
+    const long long tt = (lower ? 1LL : 2LL) * nt2 * B;
     hipLaunchKernelGGL(nlu_trsm_kernel, grid(tt), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0 + NB64, binv,
-                       nt2, (int)tt);
+                       nt2, (int)tt, kamax, kls, h.n, h.m, lower ? 1 : 2);
     DOPT_CHECK_HIP(hipGetLastError());
-    const long long tot = (long long)nt2 * nt2 * B;
+    const long long tot = (lower ? (long long)nt2 * (nt2 + 1) / 2 : (long long)nt2 * nt2) * B;
     hipLaunchKernelGGL(nlu_update2_kernel, grid(tot), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0, nt2, nt2,
-                       (int)tot, w0, w1);
+                       (int)tot, w0, w1, binv, kls, h.n, h.m, lower);
     DOPT_CHECK_HIP(hipGetLastError());
     c0 += 2 * NB64;
   }

@@ -37,6 +37,7 @@ def qp_numpy(batch, n, m, p, phi, seed, dense_tangents=False, lam_eps=0.0):
     for _ in range(batch):
         L = rng.standard_normal((n, n))
         Q = L @ L.T / n + 0.1 * np.eye(n)
+        Q = 0.5 * (Q + Q.T)   # exactly symmetric (the reference's Q always is)
         G = rng.standard_normal((m, n)) / math.sqrt(n)
         A = rng.standard_normal((p, n)) / math.sqrt(n)
         z = rng.standard_normal(n)
@@ -81,6 +82,9 @@ def qp_torch(batch, n, m, p, phi, seed, device="cuda", rank_offset=0, lam_eps=0.
     L = torch.randn(batch, n, n, generator=g, **f64)
     Q = L @ L.transpose(1, 2) / n + 0.1 * torch.eye(n, **f64)
     del L
+    # exactly symmetric, as the reference's Q always is (its quadratic terms
+    # are mirrored): a batched GEMM sums Q_ij and Q_ji in different orders
+    Q = 0.5 * (Q + Q.transpose(1, 2))
     G = torch.randn(batch, m, n, generator=g, **f64) / math.sqrt(n)
     A = torch.randn(batch, p, n, generator=g, **f64) / math.sqrt(n)
     z = torch.randn(batch, n, generator=g, **f64)

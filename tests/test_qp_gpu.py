@@ -221,6 +221,108 @@ def test_pivot_fallback_every_problem(QPBatch):
     _check_batch(QPBatch, d, kinds=[PIVOT] * 3)
 
 
+@pytest.fixture(params=["sym", "general"])
+def sym_mode(request, monkeypatch):
+    """The no-pivot LU's route for P-symmetric problems (read by dopt_create):
+    the P-symmetric one (lower tiles, U12 from L21; default) or the general
+    one for every problem (DOPT_SYM=0)."""
+    if request.param == "general":
+        monkeypatch.setenv("DOPT_SYM", "0")
+    else:
+        monkeypatch.delenv("DOPT_SYM", raising=False)
+    monkeypatch.delenv("DOPT_LU", raising=False)
+    return request.param
+
+
+def test_sym_route_cfg2_shape(QPBatch, sym_mode):
+    """The config-2 shape through the P-symmetric route (P = diag(1, λ_k, 1)
+    makes P·K symmetric: only the lower trailing tiles are updated, U12 is
+    taken from L21) and through the general no-pivot LU: both at the oracle
+    bar, and the two agree to rounding."""
+    d = _synthetic(4, 200, 300, 0, 0.3, 20250309 + 7)
+    e = _check_batch(QPBatch, d, kinds=[NOPIV] * 4)
+    np.testing.assert_array_equal(e.info(), 0)
+
+
+def test_sym_and_general_routes_agree(QPBatch, monkeypatch):
+    """Same problems (multi-block, with equality rows) through both no-pivot
+    routes: equal to ~1e-12 (different rounding, same factors)."""
+    d = _synthetic(3, 300, 400, 20, 0.6, 12)
+    outs = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DOPT_SYM", mode)
+        B, n = d["z"].shape
+        e = QPBatch(B, n, d["lam"].shape[1], d["nu"].shape[1])
+        e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+        outs.append(e.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"]))
+        np.testing.assert_array_equal(e.lu_kind(), [NOPIV] * B)
+    for a, b in zip(outs[0], outs[1]):
+        assert relfro(a, b) <= 1e-11
+
+
+def _wilkinson_c(n, c):
+    """Wilkinson's growth matrix with multipliers −c: 1 on the diagonal, −c
+    below it, 1 in the last column.  Its no-pivot LU keeps every |l| = c but
+    the last column grows as (1 + c)^k."""
+    W = np.eye(n) - c * np.tril(np.ones((n, n)), -1)
+    W[:, -1] = 1.0
+    return W
+
+
+def test_growth_bound_rejects_small_multiplier_growth(QPBatch, monkeypatch):
+    """a KKT whose no-pivot LU has small multipliers
+    (|l| = 8 ≤ 10, the threshold test passes) but element growth 9^15 ≈ 2e14:
+    Q = the Wilkinson-type matrix above (n = 16).  The growth bound |u| ≤
+    1e8·max|K| must reject it → partial pivoting, at the oracle bar; a
+    well-conditioned neighbour keeps the no-pivot route.  Run on the general
+    route (DOPT_SYM=0: Q is not symmetric, so the P-symmetric route would
+    reject it earlier, at the assembly's symmetry check — tested below)."""
+    d = _synthetic(2, 16, 8, 0, 0.5, 71)
+    d["Q"][1] = _wilkinson_c(16, 8.0)
+    monkeypatch.setenv("DOPT_SYM", "0")
+    monkeypatch.delenv("DOPT_LU", raising=False)
+    _check_batch(QPBatch, d, kinds=[NOPIV, PIVOT])
+
+
+def test_asymmetric_Q_leaves_sym_route(QPBatch, monkeypatch):
+    """An asymmetric Q (the reference's Q is always symmetric — its
+    quadratic terms are mirrored — but the C-ABI takes any dense Q) under the
+    default P-symmetric route: the assembly's symmetry check rejects it and it
+    is re-assembled in full and factorised with partial pivoting; results at
+    the oracle bar, the symmetric neighbours unaffected."""
+    monkeypatch.delenv("DOPT_SYM", raising=False)
+    monkeypatch.delenv("DOPT_LU", raising=False)
+    d = _synthetic(3, 70, 90, 4, 0.4, 72)
+    rng = np.random.default_rng(3)
+    d["Q"][1] = d["Q"][1] + 1e-3 * np.triu(rng.standard_normal((70, 70)), 1)
+    _check_batch(QPBatch, d, kinds=[NOPIV, PIVOT, NOPIV])
+
+
+def test_ill_conditioned_Q(QPBatch, sym_mode):
+    """Q with condition number 1e8 (eigenvalues log-spaced in [1e-8, 1]).
+    Q's own no-pivot LU is harmless (|l| ≤ 1.4), but the kept G rows then
+    take multipliers ~ G·U⁻¹ up to 7e6 (measured in numpy on these problems):
+    the threshold test rejects every problem — as UMFPACK's threshold pivoting
+    would move off those pivots — and partial pivoting matches the oracle at
+    1e-6, on both no-pivot routes."""
+    d = _synthetic(3, 120, 150, 6, 0.3, 73)
+    rng = np.random.default_rng(4)
+    for b in range(3):
+        V, _ = np.linalg.qr(rng.standard_normal((120, 120)))
+        Q = (V * np.logspace(0, -8, 120)) @ V.T
+        d["Q"][b] = (Q + Q.T) / 2
+    _check_batch(QPBatch, d, kinds=[PIVOT] * 3)
+
+
+def test_lam_eps_1e12(QPBatch, sym_mode):
+    """bench.py --lam-eps at 1e-12: every inactive row kept with λ = 1e-12
+    (N' = n + m; the P-symmetric route scales those rows by 1e-12); no-pivot
+    route, oracle bar."""
+    d = _synthetic(3, 200, 300, 0, 0.3, 20250312, lam_eps=1e-12)
+    e = _check_batch(QPBatch, d, kinds=[NOPIV] * 3)
+    assert (e.system_size() == 500).all()
+
+
 def test_reverse_grads_materialised(QPBatch):
     """dopt_qp_reverse_grads: ReverseObjectiveFunction / ReverseConstraintFunction
     of every problem (QuadraticProgram.jl:448-473, :307-314) against the

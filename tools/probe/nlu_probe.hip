@@ -37,6 +37,9 @@ int main(int argc, char** argv) {
   hipMalloc(&meta, B * sizeof(QPMeta));
   hipMemcpy(K, hK.data(), hK.size() * 8, hipMemcpyHostToDevice);
   hipMemcpy(meta, hm.data(), B * sizeof(QPMeta), hipMemcpyHostToDevice);
+  double* kamax;   // zeros: no growth bound
+  hipMalloc(&kamax, B * sizeof(double));
+  hipMemset(kamax, 0, B * sizeof(double));
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
@@ -62,29 +65,29 @@ int main(int argc, char** argv) {
   };
   timeit("diag", [&] {
     hipLaunchKernelGGL(nlu_diag_kernel<false>, dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
-                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr);
+                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr, kamax, nullptr, 0, 0);
   });
   if (NLU_STOP == 99) {
     // diag once more so binv holds this data's inverse for the step
     hipLaunchKernelGGL(nlu_diag_kernel<false>, dim3(B), dim3(PNT), 0, 0, K0, ld, nmax, perm, dinv,
-                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr);
+                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr, kamax, nullptr, 0, 0);
     for (int c0 = 0; c0 + 64 < Np; c0 += 64) {
       const int nt = (Np - c0 - 64 + 63) / 64;
       char nm[32];
       snprintf(nm, sizeof nm, "diag+s0 c0=%d", c0);
       timeit(nm, [&] {
         hipLaunchKernelGGL(nlu_diag_kernel<true>, dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
-                           dinv_stride(nmax), meta, c0, binv, nullptr, nullptr);
+                           dinv_stride(nmax), meta, c0, binv, nullptr, nullptr, kamax, nullptr, 0, 0);
       });
       snprintf(nm, sizeof nm, "trsm c0=%d", c0);
       timeit(nm, [&] {
         hipLaunchKernelGGL(nlu_trsm_kernel, dim3(2 * nt * B), dim3(256), 0, 0, K, ld, nmax, meta, c0, binv, nt,
-                           2 * nt * B);
+                           2 * nt * B, kamax, nullptr, 0, 0, 2);
       });
       snprintf(nm, sizeof nm, "cross c0=%d", c0);
       timeit(nm, [&] {
         hipLaunchKernelGGL(nlu_cross_kernel, dim3((2 * nt - 1) * B), dim3(256), 0, 0, K, ld, nmax, meta, c0, binv,
-                           nt, (2 * nt - 1) * B, nullptr, nullptr);
+                           nt, (2 * nt - 1) * B, nullptr, nullptr, kamax, nullptr, 0, 0, 0);
       });
     }
   }
@@ -95,7 +98,7 @@ int main(int argc, char** argv) {
     hipMemcpy(K, K0, hK.size() * 8, hipMemcpyDeviceToDevice);
     hipMemcpy(meta, hm.data(), B * sizeof(QPMeta), hipMemcpyHostToDevice);
     hipLaunchKernelGGL(nlu_diag_kernel<false>, dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
-                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr);
+                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr, kamax, nullptr, 0, 0);
     hipDeviceSynchronize();
     hipMemcpyFromSymbol(st, HIP_SYMBOL(nlu_stamps), sizeof(st));
     const char* nm[11] = {"load", "A lu_a", "B stores", "C schur", "D lu_b", "E inv_b/T", "F offdiag", "G binv",
