@@ -635,6 +635,33 @@ int dopt_nlp_kkt_solve(dopt_handle* h, int32_t k, const double* rhs, double* x) 
   });
 }
 
+int dopt_lhs_solve(dopt_handle* h, int32_t rows, const double* M, int32_t k, const double* rhs, double* x,
+                   int32_t iterative) {
+  if (!h) return -1;
+  {
+    const int rc = dopt_nlp_set_kkt(h, rows, rows, 0, M);
+    if (rc) return rc;
+  }
+  std::vector<int32_t> info(h->batch, 0);
+  const int rc = guarded(h, [&]() {
+    if (k <= 0) throw Error(-1, "k must be positive");
+    if (!rhs || !x) throw Error(-1, "rhs and x are required");
+    Timer tm;
+    const size_t cnt = (size_t)k * h->batch * rows;
+    const double* r = stage_in(*h, h->tin[0], rhs, cnt);
+    double* o = out_ptr(*h, h->tout[0], x, cnt);
+    dopt::lhs_solve(*h, k, r, o, iterative != 0, info.data());
+    copy_out(*h, x, o, cnt);
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    h->last_time = tm.s();
+    return 0;
+  });
+  if (rc) return rc;
+  for (int32_t v : info)
+    if (v > 0) return v;   // LHS \ RHS raises SingularException(info)
+  return 0;
+}
+
 int dopt_nlp_get_corrections(dopt_handle* h, int32_t* corr) {
   return guarded(h, [&]() {
     if (!corr) throw Error(-1, "corr is required");
@@ -705,6 +732,19 @@ int dopt_qp_get_lu_kind(dopt_handle* h, int8_t* kinds) {
                  : r == dopt::ROUTE_GENERIC ? DOPT_LU_KIND_PIVOT
                  : mm.lu == dopt::LU_NOPIV ? DOPT_LU_KIND_NOPIV : DOPT_LU_KIND_PIVOT;
     }
+    return 0;
+  });
+}
+
+int dopt_qp_get_sym(dopt_handle* h, int8_t* flags) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "QP only");
+    if (!flags) throw Error(-1, "flags is required");
+    std::vector<dopt::QPMeta> meta(h->batch);
+    DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h->meta.p, h->batch * sizeof(dopt::QPMeta),
+                                  hipMemcpyDeviceToHost, h->stream));
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    for (int64_t i = 0; i < h->batch; ++i) flags[i] = meta[i].sym && meta[i].lu == dopt::LU_NOPIV ? 1 : 0;
     return 0;
   });
 }
@@ -800,7 +840,7 @@ static void conic_set_common(Handle* h, const double* A, const double* b, const 
       int d = 0;
       while (d * (d + 1) / 2 < dim) ++d;
       if (d * (d + 1) / 2 != dim) throw Error(-1, "PSD triangle dimension is not triangular");
-      if (d > 256) throw Error(-1, "PSD cones larger than 256×256 are not supported");
+      if (d > 4096) throw Error(-1, "PSD cones larger than 4096×4096 are not supported");
     }
     rows += dim;
   }

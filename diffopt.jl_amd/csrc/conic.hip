@@ -20,7 +20,9 @@ namespace dopt {
 
 constexpr int CTPB = 256;
 constexpr int PSD_MAX = 64;       // PSD sides up to this: eigensolver and Dπ apply in LDS
-constexpr int PSD_BIG_MAX = 256;  // larger sides (≤ this): the same code on global scratch
+constexpr int PSD_BIG_MAX = 256;  // larger sides: the same code on global scratch; the Jacobi rotation
+                                  // table holds this many columns' pairs (larger sides, up to 4096
+                                  // (abi.hip): in chunks, the eigenvalue order past V in the scratch)
 
 struct ConeDesc {
   int32_t code, dim, row, poff;  // poff: offset into the per-problem param block
@@ -140,11 +142,15 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
       }
       off = cblock_sum(off, red);
       if (off <= 1e-32 * nrm2 || off == 0.0) break;
-      for (int step = 0; step < de - 1; ++step) {
-        // round-robin pairs: position 0 fixed, others rotate
-        if (t < de / 2) {
+      for (int step = 0; step < de - 1; ++step)
+      for (int p0 = 0; p0 < de / 2; p0 += PSD_BIG_MAX / 2) {
+        // round-robin pairs: position 0 fixed, others rotate; above PSD_BIG_MAX
+        // the step's disjoint rotations in chunks of PSD_BIG_MAX / 2 (they
+        // commute: no chunk touches another's pivots)
+        const int np = min(PSD_BIG_MAX / 2, de / 2 - p0);
+        if (t < np) {
           auto at = [&](int pos) { return pos == 0 ? 0 : 1 + ((pos - 1 + step) % (de - 1)); };
-          int a = at(t), c = at(de - 1 - t);
+          int a = at(p0 + t), c = at(de - 1 - p0 - t);
           if (a > c) { const int tmp = a; a = c; c = tmp; }
           pp[t] = a;
           qq[t] = c;
@@ -164,7 +170,7 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
         }
         __syncthreads();
         // rows: X ← Jᵀ X
-        for (int e = t; e < (de / 2) * d; e += CTPB) {
+        for (int e = t; e < np * d; e += CTPB) {
           const int r = e / d, col = e % d;
           const int a = pp[r], c = qq[r];
           if (c < d) {
@@ -176,7 +182,7 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
         }
         __syncthreads();
         // columns: X ← X J ; V ← V J
-        for (int e = t; e < (de / 2) * d; e += CTPB) {
+        for (int e = t; e < np * d; e += CTPB) {
           const int r = e / d, row = e % d;
           const int a = pp[r], c = qq[r];
           if (c < d) {
@@ -192,14 +198,17 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
         __syncthreads();
       }
     }
-    // sort eigenpairs ascending (as LAPACK) — selection sort by one thread
+    // sort eigenpairs ascending (as LAPACK) — selection sort by one thread;
+    // the permutation in LDS, or past V in the global scratch above PSD_BIG_MAX
+    int* gperm = reinterpret_cast<int*>(Vp + (size_t)d * d);
+    auto PRM = [&](int i) -> int& { return d > PSD_BIG_MAX ? gperm[i] : perm[i]; };
     if (t == 0) {
-      for (int i = 0; i < d; ++i) perm[i] = i;
+      for (int i = 0; i < d; ++i) PRM(i) = i;
       for (int i = 0; i < d; ++i) {
         int mi = i;
         for (int j = i + 1; j < d; ++j)
-          if (X(perm[j], perm[j]) < X(perm[mi], perm[mi])) mi = j;
-        const int tmp = perm[i]; perm[i] = perm[mi]; perm[mi] = tmp;
+          if (X(PRM(j), PRM(j)) < X(PRM(mi), PRM(mi))) mi = j;
+        const int tmp = PRM(i); PRM(i) = PRM(mi); PRM(mi) = tmp;
       }
     }
     __syncthreads();
@@ -208,13 +217,13 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
     double* Bm = P + d * d;
     for (int e = t; e < d * d; e += CTPB) {
       const int i = e / d, j = e % d;
-      U[i * d + j] = V(i, perm[j]);
+      U[i * d + j] = V(i, PRM(j));
     }
     int allpos = 1;
-    for (int i = 0; i < d; ++i) allpos &= (X(perm[i], perm[i]) >= 0.0);
+    for (int i = 0; i < d; ++i) allpos &= (X(PRM(i), PRM(i)) >= 0.0);
     for (int e = t; e < d * d; e += CTPB) {
       const int i = e / d, j = e % d;
-      const double li = X(perm[i], perm[i]), lj = X(perm[j], perm[j]);
+      const double li = X(PRM(i), PRM(i)), lj = X(PRM(j), PRM(j));
       double w;
       if (li == lj) w = (li > 0.0) ? 1.0 : 0.0;
       else w = (fmax(li, 0.0) - fmax(lj, 0.0)) / (li - lj);
@@ -228,7 +237,7 @@ __global__ __launch_bounds__(CTPB) void conic_cone_kernel(
       while ((j + 1) * (j + 2) / 2 <= e) ++j;
       const int i = e - j * (j + 1) / 2;
       double acc = 0.0;
-      for (int q = 0; q < d; ++q) acc = fma(V(i, perm[q]) * fmax(X(perm[q], perm[q]), 0.0), V(j, perm[q]), acc);
+      for (int q = 0; q < d; ++q) acc = fma(V(i, PRM(q)) * fmax(X(PRM(q), PRM(q)), 0.0), V(j, PRM(q)), acc);
       vpb[e] = acc;
     }
 #undef X

@@ -176,6 +176,7 @@ struct Handle {
   int32_t nlp_rows = 0;            // size of M
   int32_t nlp_num_w = 0, nlp_ng = 0, nlp_nl = 0, nlp_nlo = 0, nlp_nup = 0, nlp_nlowp = 0, nlp_nupp = 0;
   int32_t nlp_ncons = 0;           // constraint rows of M (KKT mode: as given)
+  int32_t nlp_max_corr = 50;       // inertia corrections tried (0: a singular M is reported, dopt_lhs_solve)
   bool nlp_kkt = false;
   DevBuf nlp_map;                  // int32 index maps (nlp.hip NLPMap)
   const double* nin[12] = {};      // Hxx, Hxp, Jx, Jp, x, cval, crhs, y, xl, xu, yl, yu (KKT mode: nin[0] = M)
@@ -278,6 +279,8 @@ size_t dinv_stride(int nmax);
 using ReasmFn = std::function<void(const int32_t*, int)>;
 void factor_dense(Handle& h, const ReasmFn& reasm);
 double* dense_dinv(Handle& h);
+void lsqr_slabs(Handle& h, int trans, const double* rhs, double* x);
+void lhs_solve(Handle& h, int k, const double* rhs, double* x, bool iterative, int32_t* info);
 void nlp_configure(Handle& h);
 void nlp_factor(Handle& h);
 void nlp_forward(Handle& h, const double* dp, double* dx, double* ddual);

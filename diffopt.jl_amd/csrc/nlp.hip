@@ -444,7 +444,7 @@ void nlp_factor(Handle& h) {
   std::vector<int32_t> sing = singular_list(h, all);
   h.nlp_corr.assign(B, 0);
   std::vector<int32_t> shift(B, 0);
-  for (int k = 1; k <= NLP_MAX_CORR && !sing.empty(); ++k) {
+  for (int k = 1; k <= std::min(NLP_MAX_CORR, h.nlp_max_corr) && !sing.empty(); ++k) {
     PhaseTimer pt(h, DOPT_PHASE_QP_LU_PIVOT);
     for (int32_t b : sing) shift[b] = k;
     DOPT_CHECK_HIP(hipMemcpyAsync(h.nlp_shift.p, shift.data(), (size_t)B * sizeof(int32_t), hipMemcpyHostToDevice,
@@ -566,6 +566,58 @@ void nlp_kkt_solve(Handle& h, int k, const double* rhs, double* x) {
     if (h.nlp_corr[b] < 0)
       for (int j = 0; j < k; ++j)
         DOPT_CHECK_HIP(hipMemsetAsync(x + ((size_t)j * B + b) * R, 0, R * sizeof(double), h.stream));
+}
+
+// The reference's QuadraticProgram.LinearAlgebraSolver plug point
+// (QuadraticProgram.jl:475-502): solve_system(solver, LHS, RHS, iterative) =
+// iterative ? lsqr(LHS, RHS) : LHS \ RHS, for the matrix set in KKT mode
+// (dopt_lhs_solve).  LU: the shared blocked LU without inertia correction,
+// info[b] the column of a zero pivot (1-based; 0 = regular), then the k
+// solves; LSQR: the QP back-end's LSQR kernel (IterativeSolvers defaults) per
+// right-hand side on the assembled slabs.  rhs / x seed-major, stride rows.
+void lhs_solve(Handle& h, int k, const double* rhs, double* x, bool iterative, int32_t* info) {
+  const int B = (int)h.batch, R = h.nlp_rows;
+  std::fill(info, info + B, 0);
+  if (!iterative) {
+    h.nlp_max_corr = 0;
+    try {
+      nlp_factor(h);
+    } catch (...) {
+      h.nlp_max_corr = NLP_MAX_CORR;
+      throw;
+    }
+    h.nlp_max_corr = NLP_MAX_CORR;
+    std::vector<QPMeta> meta(B);
+    DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h.meta.p, B * sizeof(QPMeta), hipMemcpyDeviceToHost, h.stream));
+    DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+    for (int b = 0; b < B; ++b) info[b] = h.nlp_corr[b] < 0 ? std::max(meta[b].info, 1) : 0;
+    nlp_kkt_solve(h, k, rhs, x);
+    return;
+  }
+  // LSQR: M into the slabs, every problem on the `iterative` branch
+  DOPT_CHECK_HIP(hipMemsetAsync(h.nlp_shift.p, 0, (size_t)B * sizeof(int32_t), h.stream));
+  DOPT_CHECK_HIP(hipMemsetAsync(h.kamax.p, 0, (size_t)B * sizeof(double), h.stream));
+  assemble(h, nullptr, B);
+  std::vector<QPMeta> meta(B);
+  for (auto& mm : meta) {
+    mm = QPMeta{};
+    mm.nsys = R;
+    mm.iterative = 1;
+  }
+  DOPT_CHECK_HIP(hipMemcpyAsync(h.meta.p, meta.data(), B * sizeof(QPMeta), hipMemcpyHostToDevice, h.stream));
+  const size_t blk = (size_t)B * h.nmax;
+  h.krhs.ensure(blk * sizeof(double));
+  h.kx.ensure(blk * sizeof(double));
+  for (int j = 0; j < k; ++j) {
+    DOPT_CHECK_HIP(hipMemsetAsync(h.krhs.p, 0, blk * sizeof(double), h.stream));
+    DOPT_CHECK_HIP(hipMemcpy2DAsync(h.krhs.p, h.nmax * sizeof(double), rhs + (size_t)j * B * R, R * sizeof(double),
+                                    R * sizeof(double), B, hipMemcpyDeviceToDevice, h.stream));
+    lsqr_slabs(h, 0, h.krhs.as<double>(), h.kx.as<double>());
+    DOPT_CHECK_HIP(hipMemcpy2DAsync(x + (size_t)j * B * R, R * sizeof(double), h.kx.p, h.nmax * sizeof(double),
+                                    R * sizeof(double), B, hipMemcpyDeviceToDevice, h.stream));
+  }
+  DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));   // `meta` outlives the upload
+  h.nfactored = false;   // the slabs hold M, not factors
 }
 
 }  // namespace dopt

@@ -719,6 +719,8 @@ __global__ void qp_prep_kernel(QPIn, double*, int32_t*, int32_t*, double*, doubl
                                const int32_t*, double*, int);
 __global__ void qp_asm_tile_kernel(QPIn, const int32_t*, const double*, const double*, int64_t, QPMeta*, double*,
                                    int, int, const int32_t*, int, double*);
+__global__ void qp_qsym_kernel(QPIn, QPMeta*, double*, const int32_t*);
+int qsym_pairs(int n);
 int prep_rows_per_thread(int m);
 int prep_threads(int m);
 size_t prep_lds(int n);
@@ -768,6 +770,11 @@ static void prep_assemble(Handle& h, const int32_t* plist, int count, bool full,
                        plist, h.kamax.as<double>(), h.sym_mode);
   check_launch();
   after_prep();
+  if (!full && h.n > 0) {   // P-symmetric problems: Q's symmetry (they skip the tile kernel)
+    hipLaunchKernelGGL(qp_qsym_kernel, dim3((unsigned)qsym_pairs(h.n), (unsigned)count), dim3(256), 0, h.stream, P,
+                       h.meta.as<QPMeta>(), h.kamax.as<double>(), plist);
+    check_launch();
+  }
   hipLaunchKernelGGL(qp_asm_tile_kernel, dim3((unsigned)count * ASM_WPP), dim3(512), 0, h.stream, P,
                      h.kidx.as<int32_t>(), h.kls.as<double>(), h.gk.as<double>(), h.batch, h.meta.as<QPMeta>(),
                      h.K.as<double>(), h.ld,
@@ -933,6 +940,15 @@ void factor_dense(Handle& h, const ReasmFn& reasm) {
 }
 
 double* dense_dinv(Handle& h) { return dinv_of(h); }
+
+// LSQR (IterativeSolvers defaults) on the K slabs of the problems whose
+// meta.iterative is set: rhs / x stride nmax per problem (dopt_lhs_solve)
+void lsqr_slabs(Handle& h, int trans, const double* rhs, double* x) {
+  h.lsqr_ws.ensure((size_t)h.batch * 5 * h.nmax * sizeof(double));
+  hipLaunchKernelGGL(qp_lsqr_kernel, dim3((unsigned)h.batch), dim3(TPB), 0, h.stream, h.K.as<double>(),
+                     h.meta.as<QPMeta>(), h.nmax, h.ld, trans, rhs, x, h.lsqr_ws.as<double>());
+  check_launch();
+}
 
 // Per-direction work buffers (trans 0 = reverse, 1 = forward): reduced RHS,
 // solution, and the full-length forward RHS.

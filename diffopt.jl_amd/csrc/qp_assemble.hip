@@ -1,26 +1,37 @@
 // QP prepare + KKT assembly, two launches.
 //
 //   qp_prep_kernel       one workgroup per problem, two inequality rows per
-//                        thread (one 16-byte load per column): branch flag `iterative = norm(Q) ≈ 0` (exact
-//                        zero test), s = Gz − h in Julia's sparse mul! order
-//                        (bit-exact with the oracle), the kept rows (λ_i ≠ 0 or
-//                        s_i == 0: exact elimination of the decoupled rows, in
-//                        ascending order, with their λ_k / s_k compacted),
-//                        per-problem metadata.  Reads G once, PREP_U loads in
-//                        flight per thread, no K writes.
-//   qp_asm_tile_kernel   ASM_WPP workgroups per problem, each taking 64×64
-//                        tiles of the reduced KKT
+//                        thread (one 16-byte load per column): branch flag
+//                        `iterative = norm(Q) ≈ 0` (exact zero test), s = Gz − h
+//                        in Julia's sparse mul! order (bit-exact with the
+//                        oracle), the kept rows (λ_i ≠ 0 or s_i == 0: exact
+//                        elimination of the decoupled rows, in ascending order,
+//                        with their λ_k / s_k compacted), a column-major
+//                        compacted copy of the speculatively kept rows of G
+//                        (λ ≠ 0: G_k, stride m),
+//                        per-problem metadata, max |K| over the G / λ / s
+//                        entries (the growth bound).  Reads G once, no K writes.
+//   qp_asm_tile_kernel   ASM_WPP workgroups per problem over 64×64 tiles of
 //                          K = [Q, G_kᵀD(λ_k), Aᵀ; G_k, D(s_k), 0; A, 0, 0]
-//                        (row-major, identity-padded to Np = round_up(N, 32))
-//                        in mirrored pairs (R, C) / (C, R): the pair reads the
-//                        same lines of G (the G_k row band and the G_kᵀΛ column
-//                        band), the second time from L2.  Columns c < n come
-//                        from column-major sources (Q, G_k, A rows): loaded with
-//                        the lanes along r and transposed through LDS; columns
-//                        c ≥ n (G_kᵀΛ, Aᵀ, the diagonal, the padding) are loaded
-//                        in place.  Both tiles of a pair are loaded before
-//                        either is stored (a wave's vmcnt counts stores and
-//                        loads in one order), stores are 16 bytes per lane.
+//                        (row-major, identity-padded to Np = round_up(N, 32)),
+//                        in mirrored pairs (R, C) / (C, R), both tiles loaded
+//                        before either is stored (a wave's vmcnt counts stores
+//                        and loads in one order), 16-byte row stores; columns
+//                        c < n come from column-major sources (Q, G, A rows),
+//                        loaded with the lanes along r and transposed through
+//                        LDS, columns c ≥ n in place.
+//                        P-symmetric problems (QPMeta::sym) are not written at
+//                        all: the no-pivot LU's first block step reads Q and
+//                        G_k straight from the sources (qp_nopiv.hip, QSrc), so
+//                        K makes no round trip through HBM before the LU.
+//                        Every other problem, and every re-assembly (`full`),
+//                        is written in full.
+//   qp_qsym_kernel       for the P-symmetric problems: Q exactly symmetric
+//                        (the source reads take Q(r, c) as Q(c, r)), 64×64
+//                        tile pairs of Q, both read coalesced and compared
+//                        through LDS; max |Q| and |A| into the growth bound.  A
+//                        mismatch marks the problem LU_REJECT (re-assembled in
+//                        full, partial pivoting).
 //
 // The single-workgroup-per-problem predecessor (prepare and tile loop in one
 // workgroup, G blocks written from the s-loop registers) measured 527 µs on
@@ -66,6 +77,8 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
   extern __shared__ __attribute__((aligned(16))) double zdyn[];
   __shared__ int cnt[PREP_MAXT / 64 + 1], scnt[PREP_MAXT / 64 + 1];
   __shared__ int extra, asym;
+  __shared__ double kred[PREP_MAXT / 64];
+  double kmx = 0.0;   // max |K| over this thread's kept rows: |G_ij|, |λ_i G_ij|, |s_i|
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int T = (int)blockDim.x, NW = T >> 6;
   const int b = plist ? plist[blockIdx.x] : (int)blockIdx.x;
@@ -121,6 +134,9 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
     // every row in the iterative branch): their G rows are copied to gk
     // (column-major, compacted) from the registers that form s
     int sci[RPT];
+    double gm[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) gm[q] = 0.0;
     {
       int sbelow = 0, scount = 0;
 #pragma unroll
@@ -138,7 +154,7 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
     }
     {
       const double* gp = Gb + (valid[RPT - 1] ? i : 0);
-      double* gw0 = gkb + sci[0];
+      double* gw0 = gkb + sci[0];   // column-major G_k (stride m per column)
       int j = 0;
       if constexpr (RPT == 2) {
         // buffer accesses with 32-bit offsets (few address registers); a
@@ -167,6 +183,8 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
           for (int u = 0; u < PREP_U2; ++u) {
             acc[0] = __dadd_rn(acc[0], __dmul_rn(cur[u].x, zs[j + u]));
             acc[1] = __dadd_rn(acc[1], __dmul_rn(cur[u].y, zs[j + u]));
+            gm[0] = fmax(gm[0], fabs(cur[u].x));
+            gm[1] = fmax(gm[1], fabs(cur[u].y));
             bstore1(wr, so0 + (unsigned)(j + u) * mb, cur[u].x);
             bstore1(wr, so1 + (unsigned)(j + u) * mb, cur[u].y);
           }
@@ -179,6 +197,8 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
           const dv2 g2 = bload2(gr, lo + (unsigned)j * mb);
           acc[0] = __dadd_rn(acc[0], __dmul_rn(g2.x, zs[j]));
           acc[1] = __dadd_rn(acc[1], __dmul_rn(g2.y, zs[j]));
+          gm[0] = fmax(gm[0], fabs(g2.x));
+          gm[1] = fmax(gm[1], fabs(g2.y));
           bstore1(wr, so0 + (unsigned)j * mb, g2.x);
           bstore1(wr, so1 + (unsigned)j * mb, g2.y);
         }
@@ -190,12 +210,14 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
 #pragma unroll
           for (int u = 0; u < PREP_U; ++u) {
             acc[0] = __dadd_rn(acc[0], __dmul_rn(gv[u], zs[j + u]));
+            gm[0] = fmax(gm[0], fabs(gv[u]));
             if (spec[0]) gw0[(size_t)(j + u) * m] = gv[u];
           }
         }
         for (; j < n; ++j) {
           const double g = gp[(size_t)j * m];
           acc[0] = __dadd_rn(acc[0], __dmul_rn(g, zs[j]));
+          gm[0] = fmax(gm[0], fabs(g));
           if (spec[0]) gw0[(size_t)j * m] = g;
         }
       }
@@ -213,6 +235,7 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
         if (keep[q] && !spec[q]) atomicAdd(&extra, 1);
         // a kept row with λ = 0 (s = 0) or a non-finite λ breaks the P-symmetry
         if (keep[q] && !(fabs(li[q]) > 0.0 && fabs(li[q]) <= 1.7976931348623157e308)) asym = 1;
+        if (keep[q]) kmx = fmax(kmx, fmax(fmax(gm[q], gm[q] * fabs(li[q])), fabs(si[q])));
       }
     }
     // ascending compaction of the kept rows: ballot prefixes within the wave
@@ -255,7 +278,11 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
     }
     __syncthreads();
   }
+  for (int o = 32; o > 0; o >>= 1) kmx = fmax(kmx, __shfl_xor(kmx, o));
+  if (lane == 0) kred[wv] = kmx;
+  __syncthreads();
   if (t == 0) {
+    for (int w = 1; w < NW; ++w) kmx = fmax(kmx, kred[w]);
     const int nk = cnt[NW];
     meta[b].nk = nk;
     meta[b].nsys = n + nk + p;
@@ -265,7 +292,7 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
     meta[b].gk_ok = extra == 0;
     // P·K symmetric up to Q's own symmetry, which the tile kernel checks
     meta[b].sym = sym_mode && !asym && qp_route(iterative, n + nk + p) == ROUTE_BLOCKED;
-    kamax[b] = 0.0;
+    kamax[b] = kmx;   // the tile kernel folds in max |Q| and |A|
   }
 }
 template __global__ void qp_prep_kernel<1>(QPIn, double*, int32_t*, int32_t*, double*, double*, int64_t, QPMeta*,
@@ -287,12 +314,11 @@ size_t prep_lds(int n) { return n <= ZLDS_MAX ? (size_t)std::max(n, 1) * sizeof(
 // Per pair: the kept rows' (index, λ, s) of both tile ranges staged in LDS;
 // every load of both tiles issued (column-major sources transposed into the
 // LDS tiles, the rest written in place); one barrier; 16-byte row stores.
-// P-symmetric problems (meta.sym, unless `full`): the no-pivot LU reads only
-// the diagonal and lower tiles, so an upper tile is neither stored nor, where
-// it holds no Q entries, loaded; where it does, it is loaded to check Q's
-// symmetry against its mirror — a mismatch stores it after all and marks the
-// problem LU_REJECT (re-assembled in full and factorised with partial
-// pivoting).  max |K| over the stored tiles → kamax (the growth bound).
+// G_k rows from the compacted copy (contiguous over ci, stride m per column)
+// when the speculative set is the kept set, else row kid[ci] of G.
+// P-symmetric problems (meta.sym, unless `full`) are skipped (qp_qsym_kernel
+// checks them).  max |K| of what is stored → kamax (the growth bound; the
+// prepare kernel set G / λ / s).
 constexpr int AT = 64, ATLD = AT + 2, ATH = 512;
 constexpr int AK1 = AT * AT / ATH;   // elements per thread per tile (8)
 
@@ -311,7 +337,7 @@ __global__ __launch_bounds__(ATH) void qp_asm_tile_kernel(QPIn P, const int32_t*
   const int n = P.n, m = P.m, p = P.p;
   const int nk = meta[b].nk;
   const bool gk_ok = meta[b].gk_ok != 0;
-  const bool half = !full && meta[b].sym != 0;   // lower + diagonal tiles only
+  if (!full && meta[b].sym != 0) return;   // P-symmetric: not assembled (workgroup-uniform)
   const int N = n + nk + p, Np = (N + 31) & ~31, TT = (Np + AT - 1) / AT;
   const int npairs = TT * (TT + 1) / 2;
   if (g >= npairs) return;
@@ -439,32 +465,81 @@ __global__ __launch_bounds__(ATH) void qp_asm_tile_kernel(QPIn P, const int32_t*
       s_s[which][e] = ok ? skb[ci] : 0.0;
     }
     __syncthreads();
-    // upper tile (R, C), R < C: skipped for P-symmetric problems, loaded only
-    // to check Q's symmetry where it overlaps Q
-    const bool qpart = R * AT < n && C * AT < n;
-    const bool up_load = R == C || !half || qpart;
-    if (up_load) tile_load(R * AT, C * AT, 0, 1, Ts[0]);
+    tile_load(R * AT, C * AT, 0, 1, Ts[0]);
     if (R != C) tile_load(C * AT, R * AT, 1, 0, Ts[1]);
     __syncthreads();
-    bool up_store = !half || R == C;
-    if (half && R != C && qpart) {
-      int bad = 0;
-      for (int e = t; e < AT * AT; e += ATH) {
-        const int i = e >> 6, j = e & 63;   // upper (R·64 + i, C·64 + j) vs lower (C·64 + j, R·64 + i)
-        if (R * AT + i < n && C * AT + j < n) bad |= Ts[0][i * ATLD + j] != Ts[1][j * ATLD + i];
-      }
-      if (__syncthreads_or(bad)) {
-        up_store = true;
-        if (t == 0) meta[b].lu = LU_REJECT;
-      }
-    }
-    if (up_store) tile_store(R * AT, C * AT, Ts[0]);
+    tile_store(R * AT, C * AT, Ts[0]);
     if (R != C) tile_store(C * AT, R * AT, Ts[1]);
     __syncthreads();   // Ts and the staged ranges are reused by the next pair
   }
   for (int o = 32; o > 0; o >>= 1) vmax = fmax(vmax, __shfl_xor(vmax, o));
   if ((t & 63) == 0)
     atomicMax(reinterpret_cast<unsigned long long*>(kamax) + b, (unsigned long long)__double_as_longlong(vmax));
+}
+
+// ---------------------------------------------------------------------------
+// Q symmetry check of the P-symmetric problems (the LU's source reads take
+// Q(r, c) as Q(c, r)): grid (tile pairs R ≤ C of Q's ⌈n/64⌉² grid, problems),
+// 256 threads.  Tile (R, C) is read with the lanes along its rows (Q is
+// column-major) into LDS, tile (C, R) the same way into registers, and
+// Q(R·64 + i, C·64 + j) is compared with Q(C·64 + j, R·64 + i) bit for bit.
+// max |Q| (and, pair 0, max |A|) folds into kamax.
+// ---------------------------------------------------------------------------
+constexpr int QS = 64, QSLD = QS + 1, QST = 256;
+
+__global__ __launch_bounds__(QST) void qp_qsym_kernel(QPIn P, QPMeta* __restrict__ meta, double* __restrict__ kamax,
+                                                      const int32_t* __restrict__ plist) {
+  __shared__ double T[QS * QSLD];
+  const int b = plist ? plist[blockIdx.y] : (int)blockIdx.y;
+  if (!meta[b].sym) return;   // workgroup-uniform
+  const int n = P.n, t = threadIdx.x;
+  const int TQ = (n + QS - 1) / QS;
+  int R = 0, rem = (int)blockIdx.x;
+  while (R < TQ && rem >= TQ - R) { rem -= TQ - R; ++R; }
+  if (R >= TQ) return;
+  const int C = R + rem;
+  const double* Qb = P.Q + (size_t)b * n * n;
+  const int i = t & 63, j0 = t >> 6;   // lane ↔ row i of a tile, 16 columns j0 + 4k per thread
+  double vmax = 0.0;
+  double mine[16];
+  // tile (R, C): Q(R·64 + i, C·64 + j) at Q[(C·64 + j)·n + R·64 + i] → T[j][i]
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int j = j0 + 4 * k, r = R * QS + i, c = C * QS + j;
+    const bool in = r < n && c < n;
+    mine[k] = in ? Qb[(size_t)c * n + r] : 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    T[(j0 + 4 * k) * QSLD + i] = mine[k];
+    vmax = fmax(vmax, fabs(mine[k]));
+  }
+  // tile (C, R): Q(C·64 + i, R·64 + j) — compared with T[i][j] = Q(R·64 + j, C·64 + i)
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int j = j0 + 4 * k, r = C * QS + i, c = R * QS + j;
+    const bool in = r < n && c < n;
+    mine[k] = in ? Qb[(size_t)c * n + r] : 0.0;
+  }
+  __syncthreads();
+  int bad = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int j = j0 + 4 * k;
+    bad |= mine[k] != T[i * QSLD + j];   // NaN never compares equal: rejected as well
+    vmax = fmax(vmax, fabs(mine[k]));
+  }
+  if (blockIdx.x == 0)
+    for (size_t e = t; e < (size_t)P.p * n; e += QST) vmax = fmax(vmax, fabs(P.A[(size_t)b * P.p * n + e]));
+  if (__syncthreads_or(bad) && t == 0) meta[b].lu = LU_REJECT;
+  for (int o = 32; o > 0; o >>= 1) vmax = fmax(vmax, __shfl_xor(vmax, o));
+  if ((t & 63) == 0)
+    atomicMax(reinterpret_cast<unsigned long long*>(kamax) + b, (unsigned long long)__double_as_longlong(vmax));
+}
+
+int qsym_pairs(int n) {
+  const int TQ = (n + QS - 1) / QS;
+  return TQ * (TQ + 1) / 2;
 }
 
 size_t dinv_stride(int nmax) { return (size_t)((nmax + 31) / 32) * 2 * 32 * 32; }

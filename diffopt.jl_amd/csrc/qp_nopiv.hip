@@ -94,6 +94,10 @@ constexpr int NB64 = 64;           // diagonal block width
 constexpr int SLD = NB64 + 1;      // LDS row stride of the 64×64 block
 constexpr int PNT = 256;           // panel threads
 constexpr int DBLK = 2 * 32 * 32;  // doubles per 32-block in dinv (L⁻¹ | U⁻¹)
+// binv per problem: the packed 64×64 inverse of the current diagonal block,
+// then (P-symmetric problems) its 64 ratios u_kk / p_k
+constexpr int BUKP = NB64 * NB64;
+constexpr int BSTR = NB64 * NB64 + NB64;
 
 __device__ __forceinline__ d4n nmfma(double a, double b, d4n c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -116,6 +120,57 @@ __device__ __forceinline__ PScale pscale(const double* kls, int b, int n, int m,
   ps.n = n;
   ps.nk = mm.nk;
   return ps;
+}
+
+// ---------------------------------------------------------------------------
+// Source reads of the first block step.  P-symmetric QP problems (QPMeta::sym)
+// are not assembled into K (qp_assemble.hip only checks Q's symmetry): the
+// launches of step 0 — the diagonal block, TRSM strip 0, the cross band and
+// the first rank-128 update — read K's entries from the inputs, each entry
+// computed exactly as the assembly would (λ·G products included), and write
+// only factor / updated tiles.  Q(r, c) is read as Q(c, r) (row r of the
+// column-major Q, contiguous along c: Q is exactly symmetric for these
+// problems, qp_qsym_kernel), G_k from the prepare kernel's column-major
+// compacted copy (stride m).
+// ---------------------------------------------------------------------------
+struct QSrc {          // batch bases (kernel argument)
+  const double *Q, *gk, *kls, *A;
+  int n, m, p;
+  int64_t B;
+};
+struct QSrcB {         // one problem
+  const double *Q, *gk, *lk, *sk, *A;
+  int n, m, p, nk, N;
+};
+__device__ __forceinline__ QSrcB qsrc(const QSrc& s, int b, const QPMeta& mm) {
+  QSrcB v;
+  v.Q = s.Q + (size_t)b * s.n * s.n;
+  v.gk = s.gk + (size_t)b * s.n * s.m;
+  v.lk = s.kls + (size_t)b * s.m;
+  v.sk = s.kls + ((size_t)s.B + b) * s.m;
+  v.A = s.A + (size_t)b * s.p * s.n;
+  v.n = s.n;
+  v.m = s.m;
+  v.p = s.p;
+  v.nk = mm.nk;
+  v.N = mm.nsys;
+  return v;
+}
+// K[r][c] of the reduced system [Q, G_kᵀΛ, Aᵀ; G_k, D(s_k), 0; A, 0, 0]
+// (identity padding past N)
+__device__ __forceinline__ double kval(const QSrcB& v, int r, int c) {
+  const int n = v.n, nk = v.nk;
+  if (r >= v.N || c >= v.N) return r == c ? 1.0 : 0.0;
+  if (r < n) {
+    if (c < n) return v.Q[(size_t)r * n + c];
+    if (c < n + nk) return v.gk[(size_t)r * v.m + (c - n)] * v.lk[c - n];
+    return v.A[(size_t)r * v.p + (c - n - nk)];
+  }
+  if (r < n + nk) {
+    if (c < n) return v.gk[(size_t)c * v.m + (r - n)];
+    return r == c ? v.sk[r - n] : 0.0;
+  }
+  return c < n ? v.A[(size_t)c * v.p + (r - n - nk)] : 0.0;
 }
 
 // Tile of a per-problem grid: `tiles` per problem in the full grid, or the
@@ -620,13 +675,16 @@ static_assert((NB64 * SLD + 200) % 2 == 0, "trash slots 16-byte aligned");
 // U_kj = (u_kk / p_k)·L_jk·p_j (P·K symmetric ⇒ U = D_u·P⁻¹·Lᵀ·P), u_kk from
 // the packed inverse's diagonal.  Every U12 entry is held to the growth bound.
 __device__ __forceinline__ void diag_strip0(const double* S, double* __restrict__ Kb, int ld, int c0, int sw,
-                                            QPMeta* __restrict__ mb, double bound, bool sym, PScale ps) {
+                                            QPMeta* __restrict__ mb, double bound, bool sym, PScale ps,
+                                            bool src_on, const QSrcB& sv) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
   if (16 * wv >= sw) return;   // wave-uniform
   const int r0 = c0 + NB64;
   double av[16], bv[16];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) av[s] = Kb[(size_t)(r0 + 16 * wv + l16) * ld + c0 + 4 * s + g];
+  for (int s = 0; s < 16; ++s)
+    av[s] = src_on ? kval(sv, r0 + 16 * wv + l16, c0 + 4 * s + g)
+                   : Kb[(size_t)(r0 + 16 * wv + l16) * ld + c0 + 4 * s + g];
   d4n acc[4];
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct) {   // U11⁻¹ is upper: k ≤ 16ct + 15
@@ -695,7 +753,8 @@ template <bool STRIP0>
 __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_diag_kernel(
     double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
     size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv, double* __restrict__ w0,
-    double* __restrict__ w1, const double* __restrict__ kamax, const double* __restrict__ kls, int n, int m) {
+    double* __restrict__ w1, const double* __restrict__ kamax, const double* __restrict__ kls, int n, int m,
+    QSrc src, int srcmode) {
   __shared__ double S[STEP_LDS];
   const int b = blockIdx.x;
   const QPMeta mm = meta[b];
@@ -704,6 +763,8 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
   const int Wv = min(NB64, Np - c0);
   const int t = threadIdx.x;
   double* Kb = K + (size_t)b * nmax * ld;
+  const bool src_on = srcmode && c0 == 0 && mm.sym;   // step 0 of a P-symmetric problem: K not assembled
+  const QSrcB sv = qsrc(src, b, mm);
   NLU_MARK_INIT;
   // the block → LDS (identity beyond Wv); all 16 loads in flight
   {
@@ -712,7 +773,7 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
     for (int q = 0; q < NB64 * NB64 / PNT; ++q) {
       const int e = t + PNT * q, i = e >> 6, j = e & 63;
       const bool in = i < Wv && j < Wv;
-      v[q] = Kb[(size_t)(c0 + (in ? i : 0)) * ld + c0 + (in ? j : 0)];
+      v[q] = src_on ? (in ? kval(sv, c0 + i, c0 + j) : 0.0) : Kb[(size_t)(c0 + (in ? i : 0)) * ld + c0 + (in ? j : 0)];
     }
 #pragma unroll
     for (int q = 0; q < NB64 * NB64 / PNT; ++q) {
@@ -725,14 +786,18 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
   NLU_MARK(0);
   const double bound = growth_bound(kamax[b]);
   diag_core(DiagLds(S), Kb, ld, perm + (size_t)b * nmax, dinv + (size_t)b * dstride + (size_t)(c0 / 32) * DBLK,
-            meta + b, c0, Np, mm.nsys, binv + (size_t)b * NB64 * NB64, w0 ? w0 + (size_t)b * nmax : nullptr,
+            meta + b, c0, Np, mm.nsys, binv + (size_t)b * BSTR, w0 ? w0 + (size_t)b * nmax : nullptr,
             w0 ? w1 + (size_t)b * nmax : nullptr, bound);
+  if (mm.sym && Np - c0 > NB64) {   // u_kk / p_k of the block for the P-symmetric TRSM / cross / update
+    __syncthreads();                // S final (the packed inverse: U11⁻¹ on the diagonal)
+    if (t < NB64) binv[(size_t)b * BSTR + BUKP + t] = 1.0 / (S[t * SLD + t] * pscale(kls, b, n, m, mm)(c0 + t));
+  }
   if constexpr (STRIP0) {
     const int sw = min(NB64, Np - c0 - NB64);
     if (sw <= 0) return;   // no trailing step for this problem
     __syncthreads();       // S final (and the threshold verdicts of diag_core)
     if (*DiagLds(S).sbad) return;
-    diag_strip0(S, Kb, ld, c0, sw, meta + b, bound, mm.sym != 0, pscale(kls, b, n, m, mm));
+    diag_strip0(S, Kb, ld, c0, sw, meta + b, bound, mm.sym != 0, pscale(kls, b, n, m, mm), src_on, sv);
   }
 }
 
@@ -769,7 +834,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
   if (mm.lu == LU_REJECT || st * 64 >= R2 || (sym && side == 1)) return;   // workgroup-uniform
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
   double* Kb = K + (size_t)b * nmax * ld;
-  const double* Bg = binv + (size_t)b * NB64 * NB64;
+  const double* Bg = binv + (size_t)b * BSTR;
   const int s0 = c0 + NB64 + 64 * st;          // first row (side 0) / column (side 1) of the strip
   const int sw = min(64, R2 - 64 * st);        // 32 or 64
   const double bound = growth_bound(kamax[b]);
@@ -822,7 +887,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) {
           const int k = 16 * ct + l16;
-          const double uk = 1.0 / (Bg[k * NB64 + k] * ps(c0 + k));
+          const double uk = Bg[BUKP + k];
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int jl = 16 * wv + g + 4 * rr;
@@ -921,7 +986,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_cross_kernel(
     double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
     int nt, int total, double* __restrict__ w0, double* __restrict__ w1, const double* __restrict__ kamax,
-    const double* __restrict__ kls, int n, int m, int lower) {
+    const double* __restrict__ kls, int n, int m, int lower, QSrc src, int srcmode) {
   __shared__ double X[NB64 * TLD];
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
@@ -938,9 +1003,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
   if (mm.lu == LU_REJECT || I * 64 >= R2 || J * 64 >= R2 || (sym && J > 0)) return;   // workgroup-uniform
   const double bound = growth_bound(kamax[b]);
   const PScale ps = pscale(kls, b, n, m, mm);
+  const bool src_on = srcmode && c0 == 0 && sym;   // step 0: A21 / C from the sources (not assembled)
+  const QSrcB sv = qsrc(src, b, mm);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
   double* Kb = K + (size_t)b * nmax * ld;
-  const double* Bg = binv + (size_t)b * NB64 * NB64;
+  const double* Bg = binv + (size_t)b * BSTR;
   const int swI = min(64, R2 - 64 * I), swJ = min(64, R2 - 64 * J);   // 32 or 64
   const int r0 = c0 + NB64 + 64 * I;   // first row of strip I
   const int s0 = c0 + NB64 + 64 * J;   // first column of strip J
@@ -974,7 +1041,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
     for (int q = 0; q < 16; ++q) v[q] = Bg[t + 256 * q];
     if (wact) {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) av[s] = Kb[(size_t)(row + l16) * ld + c0 + 4 * s + g];
+      for (int s = 0; s < 16; ++s)
+        av[s] = src_on ? kval(sv, row + l16, c0 + 4 * s + g) : Kb[(size_t)(row + l16) * ld + c0 + 4 * s + g];
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -1005,7 +1073,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
           const int k = 4 * s + g;
-          const double u = -a[s] * pj / (Bg[k * NB64 + k] * ps(c0 + k));
+          const double u = -a[s] * pj * Bg[BUKP + k];
           Kb[(size_t)(c0 + k) * ld + row + l16] = u;
           over |= !(fabs(u) <= bound);
         }
@@ -1071,7 +1139,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
     for (int q = 0; q < 4; ++q) {
       const int cq = s0 + 16 * min(q, nq - 1) + l16;
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) acc[q][rr] = Kb[(size_t)(row + g + 4 * rr) * ld + cq];
+      for (int rr = 0; rr < 4; ++rr)
+        acc[q][rr] = src_on ? kval(sv, row + g + 4 * rr, cq) : Kb[(size_t)(row + g + 4 * rr) * ld + cq];
     }
   }
   __syncthreads();   // the U12 tile is in X
@@ -1098,7 +1167,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const int k = 4 * s + g;
-      sm = fma(a[s], cp[k] / (Bg[k * NB64 + k] * ps(c0 + k)), sm);
+      sm = fma(a[s], cp[k] * Bg[BUKP + k], sm);
     }
     sm += __shfl_xor(sm, 16);
     sm += __shfl_xor(sm, 32);
@@ -1138,7 +1207,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
                                                           const QPMeta* __restrict__ meta, int c0, int nrt,
                                                           int nct, int total, double* __restrict__ w0,
                                                           double* __restrict__ w1, const double* __restrict__ binv,
-                                                          const double* __restrict__ kls, int n, int m, int lower) {
+                                                          const double* __restrict__ kls, int n, int m, int lower,
+                                                          QSrc src, int srcmode) {
   __shared__ double U[NB64 * ULD];
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
@@ -1184,11 +1254,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
     const double* arow = Kb + (size_t)(rbase + l16) * ld + c0;
 #pragma unroll
     for (int s = 0; s < NB64 / 4; ++s) a[s] = -arow[4 * s + g];
+    const bool src_on = srcmode && c0 == 0 && sym;   // step 0: C from the sources (not assembled)
+    const QSrcB sv = qsrc(src, b, mm);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int cq = cbase + 16 * min(q, nq - 1) + l16;
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) acc[q][rr] = Kb[(size_t)(rbase + g + 4 * rr) * ld + cq];
+      for (int rr = 0; rr < 4; ++rr)
+        acc[q][rr] = src_on ? kval(sv, rbase + g + 4 * rr, cq) : Kb[(size_t)(rbase + g + 4 * rr) * ld + cq];
     }
   }
   __syncthreads();
@@ -1234,13 +1307,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
   }
   if (w1 && sym && ct == 0 && rt > 0) {   // Kᵀ sweep through L21⁽ᵏ⁺¹⁾ (tile (0, rt) is not run)
     const PScale ps = pscale(kls, b, n, m, mm);
-    const double* Bg = binv + (size_t)b * NB64 * NB64;
+    const double* ukp = binv + (size_t)b * BSTR + BUKP;
     const double* cp = w1 + (size_t)b * nmax + c0 + NB64;
     double sm = 0.0;
 #pragma unroll
     for (int s = 0; s < NB64 / 4; ++s) {
       const int k = 4 * s + g;
-      sm = fma(a[s], cp[k] / (Bg[k * NB64 + k] * ps(c0 + NB64 + k)), sm);
+      sm = fma(a[s], cp[k] * ukp[k], sm);
     }
     sm += __shfl_xor(sm, 16);
     sm += __shfl_xor(sm, 32);
@@ -1279,6 +1352,18 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   const double* kls = qp ? h.kls.as<double>() : nullptr;
   const double* kamax = h.kamax.as<double>();
   int lower = qp && h.meta_host ? 1 : 0;
+  // step 0 of the P-symmetric problems reads the QP inputs (no K assembly)
+  static const double zero = 0.0;
+  QSrc src;
+  src.Q = qp ? h.Q : &zero;
+  src.gk = qp ? h.gk.as<double>() : &zero;
+  src.kls = qp ? h.kls.as<double>() : &zero;
+  src.A = qp && h.p ? h.A : &zero;
+  src.n = h.n;
+  src.m = h.m;
+  src.p = h.p;
+  src.B = h.batch;
+  const int srcmode = qp ? 1 : 0;
   if (lower)
     for (int64_t b = 0; b < h.batch; ++b) {
       const QPMeta& mm = h.meta_host[b];
@@ -1291,7 +1376,7 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   double* K = h.K.as<double>();
   int32_t* perm = h.ipiv.as<int32_t>();
   QPMeta* meta = h.meta.as<QPMeta>();
-  h.binv.ensure((size_t)B * NB64 * NB64 * sizeof(double));
+  h.binv.ensure((size_t)B * BSTR * sizeof(double));
   double* binv = h.binv.as<double>();
   auto grid = [](long long g) {
     if (g > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
@@ -1300,16 +1385,16 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   auto diag = [&](int c0, bool strip0) {
     if (strip0)
       hipLaunchKernelGGL(nlu_diag_kernel<true>, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv, dstride,
-                         meta, c0, binv, w0, w1, kamax, kls, h.n, h.m);
+                         meta, c0, binv, w0, w1, kamax, kls, h.n, h.m, src, srcmode);
     else
       hipLaunchKernelGGL(nlu_diag_kernel<false>, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv,
-                         dstride, meta, c0, binv, w0, w1, kamax, kls, h.n, h.m);
+                         dstride, meta, c0, binv, w0, w1, kamax, kls, h.n, h.m, src, srcmode);
     DOPT_CHECK_HIP(hipGetLastError());
   };
   auto cross = [&](int c0, int nt) {
     const long long tot = (lower ? (long long)nt : 2LL * nt - 1) * B;
     hipLaunchKernelGGL(nlu_cross_kernel, grid(tot), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0, binv, nt,
-                       (int)tot, w0, w1, kamax, kls, h.n, h.m, lower);
+                       (int)tot, w0, w1, kamax, kls, h.n, h.m, lower, src, srcmode);
     DOPT_CHECK_HIP(hipGetLastError());
   };
   for (int c0 = 0; c0 < npmax;) {
@@ -1334,7 +1419,7 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
     DOPT_CHECK_HIP(hipGetLastError());
     const long long tot = (lower ? (long long)nt2 * (nt2 + 1) / 2 : (long long)nt2 * nt2) * B;
     hipLaunchKernelGGL(nlu_update2_kernel, grid(tot), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0, nt2, nt2,
-                       (int)tot, w0, w1, binv, kls, h.n, h.m, lower);
+                       (int)tot, w0, w1, binv, kls, h.n, h.m, lower, src, srcmode);
     DOPT_CHECK_HIP(hipGetLastError());
     c0 += 2 * NB64;
   }

@@ -49,6 +49,8 @@ SIGNATURES = {
     "dopt_conic_forward_reverse": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 10),
     "dopt_conic_lsqr_stats": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_conic_lsqr_norms": (ctypes.c_int, [_h, ctypes.c_void_p]),
+    "dopt_lhs_solve": (ctypes.c_int, [_h, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_int32]),
     "dopt_qp_params_reverse": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64]
                                + [ctypes.c_void_p] * 5),
     "dopt_qp_params_forward": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64]
@@ -72,6 +74,7 @@ SIGNATURES = {
     "dopt_get_iterative": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_qp_get_kept": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_qp_get_lu_kind": (ctypes.c_int, [_h, ctypes.c_void_p]),
+    "dopt_qp_get_sym": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_get_system_size": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_last_time": (ctypes.c_double, [_h]),
     "dopt_set_profiling": (ctypes.c_int, [_h, ctypes.c_int32]),

@@ -318,6 +318,13 @@ class QPBatch:
         _lib.check(self.lib.dopt_qp_get_lu_kind(self.h, buf.ctypes.data), self.h)
         return buf
 
+    def sym_route(self):
+        """Per problem: 1 when the last factorisation took the P-symmetric
+        no-pivot route (lower trailing tiles, U from L), else 0."""
+        buf = np.zeros(self.batch, dtype=np.int8)
+        _lib.check(self.lib.dopt_qp_get_sym(self.h, buf.ctypes.data), self.h)
+        return buf
+
     def set_profiling(self, on=True, phases=None):
         """Per-phase HIP-event timing on (all phases, or only the phase names
         in `phases`) or off."""
@@ -335,6 +342,47 @@ class QPBatch:
     def split(self, out):
         n, m = self.n, self.m
         return out[:, :n], out[:, n:n + m], out[:, n + m:]
+
+
+def solve_system(LHS, RHS, iterative=False, device=0):
+    """``QuadraticProgram.solve_system(solver, LHS, RHS, iterative)`` for the
+    MI355X solver of the reference's ``LinearAlgebraSolver`` plug point
+    (QuadraticProgram.jl:475-502): ``iterative ? lsqr(LHS, RHS) : LHS \\ RHS``
+    on the device (dopt_lhs_solve).  LHS (rows, rows) or a batch (B, rows,
+    rows); RHS (rows,) / (rows, k) or batched (B, rows) / (B, rows, k).  A
+    singular LHS raises SingularException(info), as ``\\`` does."""
+    lib = _lib.load()
+    M = np.asarray(LHS, dtype=np.float64)
+    single = M.ndim == 2
+    if single:
+        M = M[None]
+    B, rows = M.shape[0], M.shape[-1]
+    if M.shape != (B, rows, rows):
+        raise TypeError("LHS must be square")
+    R = np.asarray(RHS, dtype=np.float64)
+    if single:
+        R = R[None]
+    vec = R.ndim == 2
+    Rk = R[..., None] if vec else R                     # (B, rows, k)
+    if Rk.shape[:2] != (B, rows):
+        raise TypeError("RHS does not match LHS")
+    k = Rk.shape[2]
+    rhs = np.ascontiguousarray(np.transpose(Rk, (2, 0, 1)))   # seed-major (k, B, rows)
+    Mc = np.ascontiguousarray(np.swapaxes(M, 1, 2))            # column-major per problem
+    out = np.empty_like(rhs)
+    h = ctypes.c_void_p()
+    rc = lib.dopt_create(ctypes.byref(h), device, B, rows, 0, 0, _lib.DOPT_KIND_NLP)
+    if rc != 0:
+        raise _lib.EngineError(rc, "dopt_create failed (no HIP device?)")
+    try:
+        rc = lib.dopt_lhs_solve(h, rows, Mc.ctypes.data, k, rhs.ctypes.data, out.ctypes.data, int(bool(iterative)))
+        _lib.check(rc, h)
+    finally:
+        lib.dopt_destroy(h)
+    X = np.transpose(out, (1, 2, 0))                           # (B, rows, k)
+    if vec:
+        X = X[..., 0]
+    return X[0] if single else X
 
 
 class Model:

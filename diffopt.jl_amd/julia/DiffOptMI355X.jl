@@ -227,6 +227,37 @@ function DiffOpt.forward_differentiate!(m::QPModel)
     return
 end
 
+# ------------------------------------------------ LinearAlgebraSolver ----
+# The reference's narrow plug point for users who keep the stock
+# QuadraticProgram.Model (QuadraticProgram.jl:475-502; exercised at
+# test/moi_wrapper.jl:74-98): after `_diff`,
+#   MOI.set(optimizer.diff.model, DiffOpt.QuadraticProgram.LinearAlgebraSolver(),
+#           DiffOptMI355X.MI355XSolver())
+# makes every `solve_system(solver, LHS, RHS, iterative)` (:335 reverse with
+# LHS, :438 forward with LHS') run on the MI355X (dopt_lhs_solve): the blocked
+# LU, or LSQR with IterativeSolvers' defaults when `iterative`.  A singular
+# LHS raises SingularException(info) as `LHS \ RHS` does.  Per problem, like
+# the plug point itself; QPModel above is the batched, assembly-on-device path.
+struct MI355XSolver
+    device::Int
+end
+MI355XSolver(; device::Integer = 0) = MI355XSolver(device)
+
+function QP.solve_system(s::MI355XSolver, LHS, RHS, iterative)
+    M = Matrix{Float64}(LHS)                 # LHS, or LHS' materialised (column-major)
+    rows = size(M, 1)
+    rhs = Vector{Float64}(RHS)
+    x = Vector{Float64}(undef, rows)
+    h = Handle(rows, 0, 0; device = s.device, kind = KIND_NLP)
+    GC.@preserve M rhs x begin
+        rc = ccall((:dopt_lhs_solve, LIB), Cint,
+                   (Ptr{Cvoid}, Int32, Ptr{Float64}, Int32, Ptr{Float64}, Ptr{Float64}, Int32),
+                   h.ptr, rows, M, 1, rhs, x, Int32(iterative))
+        _check(rc, h.ptr)                    # rc > 0: SingularException(rc)
+    end
+    return x
+end
+
 # ------------------------------------------------------------ conic model ----
 const CP = DiffOpt.ConicProgram
 
@@ -246,33 +277,27 @@ mutable struct ConicModel <: DiffOpt.AbstractModel
     s::Vector{Float64}                   # === inner.s
     y::Vector{Float64}                   # === inner.y
     handle::Union{Nothing,Handle}
-    factored::Bool
+    staged::Any                          # (A, b, c, x, s, y, cones) the handle holds, or nothing
     device::Int
 end
 
 function ConicModel(; device::Integer = 0)
     inner = CP.Model()
-    return ConicModel(inner, inner.model, inner.input_cache, inner.x, inner.s, inner.y, nothing, false, device)
+    return ConicModel(inner, inner.model, inner.input_cache, inner.x, inner.s, inner.y, nothing, nothing, device)
 end
 
 MOI.is_empty(m::ConicModel) = MOI.is_empty(m.inner)
 function MOI.empty!(m::ConicModel)
     MOI.empty!(m.inner)
     m.handle = nothing
-    m.factored = false
+    m.staged = nothing
     return
 end
 MOI.supports_constraint(m::ConicModel, F::Type{MOI.VectorAffineFunction{Float64}},
                         S::Type{<:MOI.AbstractVectorSet}) = MOI.supports_constraint(m.inner, F, S)
 MOI.get(m::ConicModel, a::DiffOpt.DifferentiateTimeSec) = MOI.get(m.inner, a)
-function MOI.set(m::ConicModel, a::MOI.ConstraintPrimalStart, ci::MOI.ConstraintIndex, v)
-    m.factored = false
-    return MOI.set(m.inner, a, ci, v)
-end
-function MOI.set(m::ConicModel, a::MOI.ConstraintDualStart, ci::MOI.ConstraintIndex, v)
-    m.factored = false
-    return MOI.set(m.inner, a, ci, v)
-end
+MOI.set(m::ConicModel, a::MOI.ConstraintPrimalStart, ci::MOI.ConstraintIndex, v) = MOI.set(m.inner, a, ci, v)
+MOI.set(m::ConicModel, a::MOI.ConstraintDualStart, ci::MOI.ConstraintIndex, v) = MOI.set(m.inner, a, ci, v)
 MOI.get(m::ConicModel, a::DiffOpt.ForwardVariablePrimal, vi::MOI.VariableIndex) = MOI.get(m.inner, a, vi)
 MOI.get(m::ConicModel, a::DiffOpt.ReverseObjectiveFunction) = MOI.get(m.inner, a)
 MOI.get(m::ConicModel, a::MOI.ConstraintFunction, ci::MOI.ConstraintIndex) = MOI.get(m.inner, a, ci)
@@ -296,9 +321,12 @@ end
 
 # the engine's counterpart of `_gradient_cache` (ConicProgram.jl:172-255): A_moi
 # as the MOI matrix (the diffcp sign flip is applied on the device), c negated
-# for MAX_SENSE (:206-208), the NaN-start guard (:186-196) raised by the engine
+# for MAX_SENSE (:206-208), the NaN-start guard (:186-196) raised by the engine.
+# Keyed on the full data and primal-dual point, as QPModel: any change — a new
+# VariablePrimalStart (diff_opt.jl:362-370 writes m.x, which is inner.x),
+# ConstraintPrimalStart / ConstraintDualStart, or a model edit — re-stages and
+# re-factors; an unchanged model reuses the device factorisation.
 function _ensure!(m::ConicModel)
-    m.factored && return m.handle
     inner = m.inner
     Amoi = convert(SparseArrays.SparseMatrixCSC{Float64,Int64}, m.model.constraints.coefficients)
     b = Vector{Float64}(m.model.constraints.constants)
@@ -320,7 +348,10 @@ function _ensure!(m::ConicModel)
     h = m.handle
     if h === nothing || (h.n, h.m) != (n, mr)
         h = m.handle = Handle(n, mr, 0; device = m.device, kind = KIND_CONIC)
+        m.staged = nothing
     end
+    key = (Amoi, b, c, copy(inner.x), copy(inner.s), copy(inner.y), desc)
+    m.staged !== nothing && isequal(m.staged, key) && return h
     colptr, rowval, nzval, nnz = _csc(Amoi)
     GC.@preserve Amoi b c inner desc begin
         _check(ccall((:dopt_conic_set_csc, LIB), Cint,
@@ -331,7 +362,7 @@ function _ensure!(m::ConicModel)
                      _ptr(inner.s), _ptr(inner.y), desc, Int32(length(desc) ÷ 2)), h.ptr)
         _check(ccall((:dopt_conic_factor, LIB), Cint, (Ptr{Cvoid},), h.ptr), h.ptr)
     end
-    m.factored = true
+    m.staged = key
     return h
 end
 

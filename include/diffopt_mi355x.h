@@ -53,7 +53,7 @@ extern "C" {
 #define DOPT_CONE_NONNEG 1       /* MOI.Nonnegatives                          */
 #define DOPT_CONE_NONPOS 2       /* MOI.Nonpositives                          */
 #define DOPT_CONE_SOC 3          /* MOI.SecondOrderCone                       */
-#define DOPT_CONE_PSD_TRI 4      /* MOI.PositiveSemidefiniteConeTriangle (side ≤ 256; > 64 on global scratch) */
+#define DOPT_CONE_PSD_TRI 4      /* MOI.PositiveSemidefiniteConeTriangle (side ≤ 4096; > 64 on global scratch) */
 
 #define DOPT_ABI_VERSION 2
 
@@ -306,6 +306,18 @@ int dopt_nlp_get_layout(dopt_handle* h, int32_t* layout);
  * per problem, rhs / x seed-major (k × batch × rows). */
 int dopt_nlp_set_kkt(dopt_handle* h, int32_t rows, int32_t num_w, int32_t num_cons, const double* M);
 int dopt_nlp_kkt_solve(dopt_handle* h, int32_t k, const double* rhs, double* x);
+/* The reference's narrow QP plug point, QuadraticProgram.LinearAlgebraSolver
+ * (QuadraticProgram.jl:475-502; exercised at test/moi_wrapper.jl:74-98):
+ * solve_system(solver, LHS, RHS, iterative) = iterative ? lsqr(LHS, RHS) :
+ * LHS \ RHS, for a given square matrix per problem — the reference passes its
+ * assembled KKT LHS for reverse and LHS' for forward (:335, :438).  On a
+ * DOPT_KIND_NLP handle: M column-major rows × rows × batch, k right-hand sides
+ * seed-major (k × batch × rows), x the same shape.  LU: the blocked LU
+ * without inertia correction; returns > 0 (a zero-pivot column, 1-based) for
+ * a singular LHS — the Julia shim raises SingularException as `\` does.
+ * iterative: LSQR with IterativeSolvers' defaults, as the reference. */
+int dopt_lhs_solve(dopt_handle* h, int32_t rows, const double* M, int32_t k, const double* rhs, double* x,
+                   int32_t iterative);
 
 int dopt_get_info(dopt_handle* h, int32_t* info);
 /* per-problem `iterative` branch flags (QP; 1 = LSQR branch). */
@@ -320,6 +332,11 @@ int dopt_qp_get_kept(dopt_handle* h, int8_t* kept);
 #define DOPT_LU_KIND_NOPIV 1     /* no-pivot LU passed the threshold test        */
 #define DOPT_LU_KIND_PIVOT 2     /* partial pivoting                             */
 int dopt_qp_get_lu_kind(dopt_handle* h, int8_t* kinds);
+/* per-problem flag: 1 when the last factorisation took the P-symmetric
+ * no-pivot route (P = diag(1, λ_k, 1) makes P·K symmetric: lower trailing
+ * tiles only, U from L, ≈ N'³/3 flops instead of 2N'³/3), 0 otherwise.
+ * Introspection for tests and the bench. */
+int dopt_qp_get_sym(dopt_handle* h, int8_t* flags);
 /* per-problem size of the factorised (reduced) KKT system (QP) or LSQR
  * iteration count of the last solve (CONIC). */
 int dopt_get_system_size(dopt_handle* h, int32_t* sizes);

@@ -50,17 +50,28 @@ def tri_indices(d):
     return out
 
 
+_TRI_IJ = {}
+
+
+def _tri_ij(d):
+    """Row / column index arrays of tri_indices(d) (cached)."""
+    if d not in _TRI_IJ:
+        ij = np.array(tri_indices(d), dtype=np.int64).reshape(-1, 2)
+        _TRI_IJ[d] = (ij[:, 0], ij[:, 1])
+    return _TRI_IJ[d]
+
+
 def smat(v, d):
+    i, j = _tri_ij(d)
     X = np.zeros((d, d))
-    for k, (i, j) in enumerate(tri_indices(d)):
-        X[i, j] = v[k]
-        X[j, i] = v[k]
+    X[i, j] = v
+    X[j, i] = v
     return X
 
 
 def tri(X):
-    d = X.shape[0]
-    return np.array([X[i, j] for (i, j) in tri_indices(d)])
+    i, j = _tri_ij(X.shape[0])
+    return X[i, j].copy()
 
 
 def psd_scale(d):
@@ -119,6 +130,59 @@ def psd_jacobian_unscaled(v):
     return J
 
 
+class PSDStructured:
+    """Dπ of a PSD-triangle cone without its dense k × k Jacobian (k = d(d+1)/2,
+    e.g. 45 150 at d = 300 — 16 GB dense): J·w = tri(U (B ∘ (Uᵀ smat(w) U)) Uᵀ)
+    with the eigendecomposition smat(v) = U Λ Uᵀ and the Daleckii–Krein
+    weights B of psd_jacobian_unscaled (the same J, column by column:
+    J e_c = tri(dP(E_c)), and smat(w) = Σ_c w_c E_c).  `convention` S2JSm2:
+    Dπ·w = S² J (S⁻² w) and Dπᵀ·w = J w (S J S⁻¹ is symmetric).  Used by
+    dpi_blocks for sides above STRUCTURED_MIN; equal to the dense blocks to
+    rounding (tests/test_oracle_golden.py)."""
+
+    def __init__(self, v, psd_convention="S2JSm2"):
+        if psd_convention != "S2JSm2":
+            raise ValueError("structured PSD Dπ implements the S2JSm2 convention")
+        v = np.asarray(v, dtype=np.float64)
+        self.k = v.shape[0]
+        self.shape = (self.k, self.k)
+        self.d = d = psd_side(self.k)
+        lam, self.U = np.linalg.eigh(smat(v, d))
+        self.ident = bool(np.all(lam >= 0))
+        lp = np.maximum(lam, 0.0)
+        dl = lam[:, None] - lam[None, :]
+        same = dl == 0.0
+        with np.errstate(divide="ignore", invalid="ignore"):
+            B = (lp[:, None] - lp[None, :]) / np.where(same, 1.0, dl)
+        self.B = np.where(same, (lam[:, None] > 0).astype(float) * np.ones_like(B), B)
+        s = psd_scale(d)
+        self.s2 = s * s
+
+    def jvec(self, w):
+        w = np.asarray(w, dtype=np.float64)
+        if self.ident:
+            return w.copy()
+        U = self.U
+        return tri(U @ (self.B * (U.T @ smat(w, self.d) @ U)) @ U.T)
+
+    def __matmul__(self, w):
+        return self.s2 * self.jvec(np.asarray(w, dtype=np.float64) / self.s2)
+
+    @property
+    def T(self):
+        outer = self
+
+        class _T:
+            shape = outer.shape
+
+            def __matmul__(self, w):
+                return outer.jvec(w)
+        return _T()
+
+
+STRUCTURED_MIN = 128   # PSD sides from here on: PSDStructured instead of a dense block (k > 8256)
+
+
 def dproj(code, v, psd_convention="S2JSm2"):
     v = np.asarray(v, dtype=np.float64)
     k = v.shape[0]
@@ -174,11 +238,19 @@ def pi(v, cones):
     return out
 
 
-def dpi_blocks(v, cones, psd_convention="S2JSm2"):
-    """``DiffOpt.Dπ`` (diff_opt.jl:509-519): list of dense diagonal blocks."""
+def dpi_blocks(v, cones, psd_convention="S2JSm2", structured_min=STRUCTURED_MIN):
+    """``DiffOpt.Dπ`` (diff_opt.jl:509-519): list of diagonal blocks — dense,
+    except PSD cones of side ≥ structured_min (PSDStructured: same operator,
+    applied through the eigendecomposition)."""
     off = cone_offsets(cones)
-    return [dproj(code, v[off[k]:off[k + 1]], psd_convention)
-            for k, (code, dim) in enumerate(cones)]
+    out = []
+    for k, (code, dim) in enumerate(cones):
+        vk = v[off[k]:off[k + 1]]
+        if code == PSD and psd_side(dim) >= structured_min and psd_convention == "S2JSm2":
+            out.append(PSDStructured(vk, psd_convention))
+        else:
+            out.append(dproj(code, vk, psd_convention))
+    return out
 
 
 def blockdiag(blocks):
@@ -187,6 +259,6 @@ def blockdiag(blocks):
     o = 0
     for b in blocks:
         k = b.shape[0]
-        D[o:o + k, o:o + k] = b
+        D[o:o + k, o:o + k] = b if isinstance(b, np.ndarray) else np.stack([b @ e for e in np.eye(k)], axis=1)
         o += k
     return D

@@ -353,11 +353,15 @@ def test_config5_full_shape(ConicBatch):
 @pytest.mark.parametrize("shape", [
     ("large PSD (d = 66) + small cones", 2, 60, [(4, 2211), (4, 15), (1, 5)], 17, 2),   # converged at √eps: 2 of 12 in (1e-6, 3.2e-6] (r02)
     ("large PSD (d = 100)", 1, 60, [(4, 5050)], 18, 0),
-], ids=["d66_mixed", "d100"])
+    ("large PSD (d = 300)", 1, 40, [(4, 45150)], 19, 1),   # converged at √eps (istop 2 / 1): 1 of 6 at 1.6e-5, inside the 1-ulp envelope (r03)
+], ids=["d66_mixed", "d100", "d300"])
 def test_large_psd_sides(ConicBatch, shape):
     """PSD sides above 64 (the LDS eigensolver / Dπ apply limit): the same code
-    on global scratch, split LSQR path; reference: any MOI PSD triangle
-    (ConicProgram.jl:132-142, diff_opt.jl:491-519)."""
+    on global scratch, split LSQR path; d = 300 exceeds the Jacobi rotation
+    table (256: chunked rotations, the eigenvalue order in the scratch) and the
+    oracle's dense Jacobian (45 150², 16 GB: oracle.cones.PSDStructured).
+    Reference: any MOI PSD triangle (ConicProgram.jl:132-142,
+    diff_opt.jl:491-519)."""
     name, B, n, cones, seed, cap = shape
     _synthetic_check(ConicBatch, B, n, cones, seed, name, cap=cap)
 

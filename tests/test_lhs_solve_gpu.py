@@ -1,0 +1,66 @@
+"""The reference's narrow QP plug point, ``QuadraticProgram.LinearAlgebraSolver``
+(QuadraticProgram.jl:475-502; test/moi_wrapper.jl:74-98 plugs a custom
+solver): ``solve_system(solver, LHS, RHS, iterative)`` =
+``iterative ? lsqr(LHS, RHS) : LHS \\ RHS`` on the device (dopt_lhs_solve,
+diffopt_amd.qp.solve_system).  Checked on the reference's own use: the
+assembled KKT LHS of a QP (reverse) and its adjoint (forward), against the
+oracle's full-KKT solve; LSQR against the oracle's IterativeSolvers
+restatement; a singular LHS raises SingularException."""
+
+import numpy as np
+import pytest
+
+from oracle import lsqr as olsqr
+from oracle import qp as oqp
+
+pytestmark = pytest.mark.gpu
+
+
+def _kkt(seed, n=40, m=60, p=5):
+    from diffopt_amd.synthetic import qp_numpy
+    d = qp_numpy(1, n, m, p, 0.4, seed)
+    Q, G, h, A, z, lam = (d[k][0] for k in ["Q", "G", "h", "A", "z", "lam"])
+    return d, (Q, G, h, A, z, lam), oqp.create_LHS_matrix(z, lam, Q, G, h, A)
+
+
+def test_reverse_and_forward_systems():
+    from diffopt_amd.qp import solve_system
+    d, a, LHS = _kkt(5)
+    L = np.asarray(LHS.todense() if hasattr(LHS, "todense") else LHS)
+    N = L.shape[0]
+    rng = np.random.default_rng(1)
+    rhs = rng.standard_normal(N)
+    x = solve_system(L, rhs)
+    np.testing.assert_allclose(x, np.linalg.solve(L, rhs), rtol=1e-10, atol=1e-12)
+    xt = solve_system(L.T, rhs)                                   # LHS' (forward, :438)
+    np.testing.assert_allclose(xt, np.linalg.solve(L.T, rhs), rtol=1e-10, atol=1e-12)
+    R = rng.standard_normal((N, 3))                               # several right-hand sides
+    np.testing.assert_allclose(solve_system(L, R), np.linalg.solve(L, R), rtol=1e-10, atol=1e-12)
+    # batched: two problems at once
+    _, _, L2 = _kkt(6)
+    L2 = np.asarray(L2.todense() if hasattr(L2, "todense") else L2)
+    if L2.shape == L.shape:
+        Xb = solve_system(np.stack([L, L2]), np.stack([rhs, rhs]))
+        np.testing.assert_allclose(Xb[1], np.linalg.solve(L2, rhs), rtol=1e-10, atol=1e-12)
+
+
+def test_iterative_branch_is_lsqr():
+    from diffopt_amd.qp import solve_system
+    rng = np.random.default_rng(2)
+    # well-conditioned (σ ∈ ≈[0.9, 1.1]): LSQR stops at its √eps tests within a
+    # few iterations, so the two runs agree far below north_star's 1e-6 bar
+    A = np.eye(30) + 0.1 * rng.standard_normal((30, 30)) / np.sqrt(30)
+    b = rng.standard_normal(30)
+    x = solve_system(A, b, iterative=True)
+    ref = olsqr.lsqr_dense(A, b)
+    assert np.linalg.norm(x - ref) / np.linalg.norm(ref) <= 1e-6
+
+
+def test_singular_raises():
+    from diffopt_amd import _lib
+    from diffopt_amd.qp import solve_system
+    rng = np.random.default_rng(3)
+    A = rng.standard_normal((20, 20))
+    A[:, 7] = 0.0                                                 # a zero column: exactly singular
+    with pytest.raises(_lib.SingularException):
+        solve_system(A, rng.standard_normal(20))

@@ -175,3 +175,19 @@ def test_conic_matrix_free_products_match_dense_M():
     v = rng.standard_normal(M.shape[0])
     np.testing.assert_allclose(cache.matvec(v), M @ v, atol=1e-12)
     np.testing.assert_allclose(cache.rmatvec(v), M.T @ v, atol=1e-12)
+
+
+def test_structured_psd_matches_dense():
+    """oracle.cones.PSDStructured (large PSD sides: Dπ through the
+    eigendecomposition, no dense k × k Jacobian) equals the dense S²JS⁻²
+    block and its transpose to rounding, including a PSD (identity) point."""
+    from oracle import cones as C
+    rng = np.random.default_rng(3)
+    for d in (3, 12, 30):
+        k = d * (d + 1) // 2
+        for v in (rng.standard_normal(k), C.tri(np.eye(d) * 2.0)):
+            Dd = C.dproj(C.PSD, v)
+            S = C.PSDStructured(v)
+            w = rng.standard_normal(k)
+            np.testing.assert_allclose(S @ w, Dd @ w, rtol=1e-12, atol=1e-13)
+            np.testing.assert_allclose(S.T @ w, Dd.T @ w, rtol=1e-12, atol=1e-13)

@@ -32,7 +32,7 @@ int main(int argc, char** argv) {
   QPMeta* meta;
   hipMalloc(&K, hK.size() * 8);
   hipMalloc(&dinv, (size_t)B * dinv_stride(nmax) * 8);
-  hipMalloc(&binv, (size_t)B * 64 * 64 * 8);
+  hipMalloc(&binv, (size_t)B * (64 * 64 + 64) * 8);
   hipMalloc(&perm, (size_t)B * nmax * 4);
   hipMalloc(&meta, B * sizeof(QPMeta));
   hipMemcpy(K, hK.data(), hK.size() * 8, hipMemcpyHostToDevice);
@@ -65,19 +65,19 @@ int main(int argc, char** argv) {
   };
   timeit("diag", [&] {
     hipLaunchKernelGGL(nlu_diag_kernel<false>, dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
-                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr, kamax, nullptr, 0, 0);
+                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr, kamax, nullptr, 0, 0, QSrc{}, 0);
   });
   if (NLU_STOP == 99) {
     // diag once more so binv holds this data's inverse for the step
     hipLaunchKernelGGL(nlu_diag_kernel<false>, dim3(B), dim3(PNT), 0, 0, K0, ld, nmax, perm, dinv,
-                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr, kamax, nullptr, 0, 0);
+                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr, kamax, nullptr, 0, 0, QSrc{}, 0);
     for (int c0 = 0; c0 + 64 < Np; c0 += 64) {
       const int nt = (Np - c0 - 64 + 63) / 64;
       char nm[32];
       snprintf(nm, sizeof nm, "diag+s0 c0=%d", c0);
       timeit(nm, [&] {
         hipLaunchKernelGGL(nlu_diag_kernel<true>, dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
-                           dinv_stride(nmax), meta, c0, binv, nullptr, nullptr, kamax, nullptr, 0, 0);
+                           dinv_stride(nmax), meta, c0, binv, nullptr, nullptr, kamax, nullptr, 0, 0, QSrc{}, 0);
       });
       snprintf(nm, sizeof nm, "trsm c0=%d", c0);
       timeit(nm, [&] {
@@ -87,7 +87,7 @@ int main(int argc, char** argv) {
       snprintf(nm, sizeof nm, "cross c0=%d", c0);
       timeit(nm, [&] {
         hipLaunchKernelGGL(nlu_cross_kernel, dim3((2 * nt - 1) * B), dim3(256), 0, 0, K, ld, nmax, meta, c0, binv,
-                           nt, (2 * nt - 1) * B, nullptr, nullptr, kamax, nullptr, 0, 0, 0);
+                           nt, (2 * nt - 1) * B, nullptr, nullptr, kamax, nullptr, 0, 0, 0, QSrc{}, 0);
       });
     }
   }
@@ -98,7 +98,7 @@ int main(int argc, char** argv) {
     hipMemcpy(K, K0, hK.size() * 8, hipMemcpyDeviceToDevice);
     hipMemcpy(meta, hm.data(), B * sizeof(QPMeta), hipMemcpyHostToDevice);
     hipLaunchKernelGGL(nlu_diag_kernel<false>, dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
-                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr, kamax, nullptr, 0, 0);
+                       dinv_stride(nmax), meta, 0, binv, nullptr, nullptr, kamax, nullptr, 0, 0, QSrc{}, 0);
     hipDeviceSynchronize();
     hipMemcpyFromSymbol(st, HIP_SYMBOL(nlu_stamps), sizeof(st));
     const char* nm[11] = {"load", "A lu_a", "B stores", "C schur", "D lu_b", "E inv_b/T", "F offdiag", "G binv",
