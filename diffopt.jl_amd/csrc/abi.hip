@@ -152,6 +152,12 @@ int dopt_destroy(dopt_handle* h) {
   if (!h) return 0;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->aux) {
+    (void)hipStreamSynchronize(h->aux);
+    (void)hipStreamDestroy(h->aux);
+  }
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   DevBuf* bufs[] = {&h->dinv, &h->plist, &h->lsqr_ws, &h->binv, &h->fwdw, &h->K, &h->ipiv, &h->s, &h->kidx, &h->meta, &h->rhs,
                     &h->x, &h->cone_dev, &h->vp, &h->dpi, &h->cwork, &h->cinfo, &h->cnorm, &h->csplit, &h->krhs, &h->kx,
                     &h->kfull, &h->kamax, &h->nlp_map, &h->nlp_shift, &h->nlp_scale};

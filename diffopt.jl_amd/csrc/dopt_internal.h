@@ -134,7 +134,9 @@ struct Handle {
   DevBuf plist;              // problem indices of the partial-pivoting re-factorisation
   DevBuf glist;              // problem indices of the generic LU
   DevBuf lsqr_ws;            // LSQR vectors of the `iterative` branch (5 per problem)
-  DevBuf binv;               // no-pivot LU: packed 64×64 inverse of the current diagonal block
+  DevBuf binv;               // no-pivot LU: packed 64×64 inverses of the diagonal blocks (two, by step parity)
+  hipStream_t aux = nullptr;       // no-pivot LU, P-symmetric batches: second stream (off the critical chain)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   DevBuf fwdw;               // fused call: both right-hand sides, forward-swept inside the no-pivot LU
   DevBuf krhs, kx, kfull;    // multi-RHS calls: k seeds' reduced RHS, solutions, full forward RHS
   DevBuf mws;                // multi-RHS: per-workgroup vectors of tall systems (qp_multi.hip)

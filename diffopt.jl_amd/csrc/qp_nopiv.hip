@@ -173,13 +173,15 @@ __device__ __forceinline__ double kval(const QSrcB& v, int r, int c) {
   return c < n ? v.A[(size_t)c * v.p + (r - n - nk)] : 0.0;
 }
 
-// Tile of a per-problem grid: `tiles` per problem in the full grid, or the
-// lower triangle (rt ≥ ct) of an nrt × nrt grid when `lower`.
-__device__ __forceinline__ void lower_tile(int tile, int& rt, int& ct) {
-  rt = (int)((sqrtf(8.0f * tile + 1.0f) - 1.0f) * 0.5f);
-  while ((rt + 1) * (rt + 2) / 2 <= tile) ++rt;
-  while (rt * (rt + 1) / 2 > tile) --rt;
-  ct = tile - rt * (rt + 1) / 2;
+// Tile `tile` of the lower triangle (rt ≥ ct) of an nrt × nrt grid, column by
+// column: column 0's nrt tiles first.
+__device__ __forceinline__ void col_lower_tile(int tile, int nrt, int& rt, int& ct) {
+  ct = 0;
+  while (tile >= nrt - ct) {
+    tile -= nrt - ct;
+    ++ct;
+  }
+  rt = ct + tile;
 }
 
 // ---------------------------------------------------------------------------
@@ -986,15 +988,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_cross_kernel(
     double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
     int nt, int total, double* __restrict__ w0, double* __restrict__ w1, const double* __restrict__ kamax,
-    const double* __restrict__ kls, int n, int m, int lower, QSrc src, int srcmode) {
+    const double* __restrict__ kls, int n, int m, int lower, QSrc src, int srcmode, int toff, int tsub) {
   __shared__ double X[NB64 * TLD];
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
   const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
-  const int tiles = lower ? nt : 2 * nt - 1;
+  const int tiles = lower ? tsub : 2 * nt - 1;   // lower: tiles (I, 0), I = toff .. toff + tsub − 1
   const int b = logical / tiles;
   const int tile = logical - b * tiles;
-  const int I = lower ? tile : (tile < nt ? 0 : tile - nt + 1);   // row strip (L21, C rows)
+  const int I = lower ? toff + tile : (tile < nt ? 0 : tile - nt + 1);   // row strip (L21, C rows)
   const int J = lower ? 0 : (tile < nt ? tile : 0);              // column strip (U12, C columns)
   const QPMeta mm = meta[b];
   const int Np = nlu_np(mm);
@@ -1208,16 +1210,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
                                                           int nct, int total, double* __restrict__ w0,
                                                           double* __restrict__ w1, const double* __restrict__ binv,
                                                           const double* __restrict__ kls, int n, int m, int lower,
-                                                          QSrc src, int srcmode) {
+                                                          QSrc src, int srcmode, int toff, int tsub) {
   __shared__ double U[NB64 * ULD];
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
   const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
-  const int tiles = lower ? nrt * (nrt + 1) / 2 : nrt * nct;
+  // lower: tiles toff .. toff + tsub − 1 of the column-major lower triangle
+  // (column 0 first: the next diagonal block and strip 0 need only those)
+  const int tiles = lower ? tsub : nrt * nct;
   const int b = logical / tiles;
   const int tile = logical - b * tiles;
   int rt, ct;
-  if (lower) lower_tile(tile, rt, ct);
+  if (lower) col_lower_tile(toff + tile, nrt, rt, ct);
   else {
     rt = tile / nct;
     ct = tile - rt * nct;
@@ -1376,27 +1380,58 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   double* K = h.K.as<double>();
   int32_t* perm = h.ipiv.as<int32_t>();
   QPMeta* meta = h.meta.as<QPMeta>();
-  h.binv.ensure((size_t)B * BSTR * sizeof(double));
-  double* binv = h.binv.as<double>();
+  // the packed inverse of step c lives in binv buffer (c / 64) & 1: a diagonal
+  // launch may then run while the previous step's cross tiles still read theirs
+  h.binv.ensure((size_t)2 * B * BSTR * sizeof(double));
+  auto binv_of = [&](int c) { return h.binv.as<double>() + (size_t)((c / NB64) & 1) * B * BSTR; };
   auto grid = [](long long g) {
     if (g > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
     return dim3((unsigned)g);
   };
+  // P-symmetric batches (`lower`) run two streams: the main one carries the
+  // critical chain (diagonal blocks, the tiles they need), `aux` the rest of
+  // each band / trailing update, joined by events before their consumers
+  hipStream_t S = h.stream, T = h.stream;
+  if (lower) {
+    if (!h.aux) {
+      DOPT_CHECK_HIP(hipStreamCreateWithFlags(&h.aux, hipStreamNonBlocking));
+      DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_fork, hipEventDisableTiming));
+      DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_join, hipEventDisableTiming));
+    }
+    T = h.aux;
+  }
+  auto fork = [&] {   // T starts after everything queued on S so far
+    DOPT_CHECK_HIP(hipEventRecord(h.ev_fork, S));
+    DOPT_CHECK_HIP(hipStreamWaitEvent(T, h.ev_fork, 0));
+  };
+  auto join = [&] {   // S continues after everything queued on T so far
+    DOPT_CHECK_HIP(hipEventRecord(h.ev_join, T));
+    DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_join, 0));
+  };
   auto diag = [&](int c0, bool strip0) {
     if (strip0)
-      hipLaunchKernelGGL(nlu_diag_kernel<true>, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv, dstride,
-                         meta, c0, binv, w0, w1, kamax, kls, h.n, h.m, src, srcmode);
+      hipLaunchKernelGGL(nlu_diag_kernel<true>, dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv, dstride,
+                         meta, c0, binv_of(c0), w0, w1, kamax, kls, h.n, h.m, src, srcmode);
     else
-      hipLaunchKernelGGL(nlu_diag_kernel<false>, dim3(B), dim3(PNT), 0, h.stream, K, h.ld, h.nmax, perm, dinv,
-                         dstride, meta, c0, binv, w0, w1, kamax, kls, h.n, h.m, src, srcmode);
+      hipLaunchKernelGGL(nlu_diag_kernel<false>, dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv,
+                         dstride, meta, c0, binv_of(c0), w0, w1, kamax, kls, h.n, h.m, src, srcmode);
     DOPT_CHECK_HIP(hipGetLastError());
   };
-  auto cross = [&](int c0, int nt) {
-    const long long tot = (lower ? (long long)nt : 2LL * nt - 1) * B;
-    hipLaunchKernelGGL(nlu_cross_kernel, grid(tot), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0, binv, nt,
-                       (int)tot, w0, w1, kamax, kls, h.n, h.m, lower, src, srcmode);
+  // cross band of step c0: lower — tiles (I, 0), I in [i0, i0 + cnt); else all
+  auto cross = [&](hipStream_t st, int c0, int nt, int i0, int cnt) {
+    const long long tot = (lower ? (long long)cnt : 2LL * nt - 1) * B;
+    hipLaunchKernelGGL(nlu_cross_kernel, grid(tot), dim3(256), 0, st, K, h.ld, h.nmax, meta, c0, binv_of(c0), nt,
+                       (int)tot, w0, w1, kamax, kls, h.n, h.m, lower, src, srcmode, i0, cnt);
     DOPT_CHECK_HIP(hipGetLastError());
   };
+  // paired update of steps c0, c0+64: lower — column-major tiles [t0, t0 + cnt)
+  auto update2 = [&](hipStream_t st, int c0, int nt2, int t0, int cnt) {
+    const long long tot = (lower ? (long long)cnt : (long long)nt2 * nt2) * B;
+    hipLaunchKernelGGL(nlu_update2_kernel, grid(tot), dim3(256), 0, st, K, h.ld, h.nmax, meta, c0, nt2, nt2,
+                       (int)tot, w0, w1, binv_of(c0 + NB64), kls, h.n, h.m, lower, src, srcmode, t0, cnt);
+    DOPT_CHECK_HIP(hipGetLastError());
+  };
+  bool pending = false;   // T holds work S must wait for before the next band
   for (int c0 = 0; c0 < npmax;) {
     const int R2 = npmax - c0 - NB64;
     if (R2 <= 0) {   // the last diagonal block
@@ -1405,24 +1440,41 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
     }
     const int nt = (R2 + 63) / 64;
     diag(c0, true);
-    cross(c0, nt);
-    if (R2 <= NB64) {   // one trailing block: the cross launch was its whole update
+    if (pending) {   // the previous trailing update's other tiles (they feed this band)
+      join();
+      pending = false;
+    }
+    if (R2 <= NB64) {   // one trailing block: the cross launch is its whole update
+      cross(S, c0, nt, 0, 1);
       c0 += NB64;
       continue;
     }
+    if (lower) {   // tile (0, 0) → diagonal block c0+64 on S; the band's other tiles on T
+      fork();
+      cross(S, c0, nt, 0, 1);
+      cross(T, c0, nt, 1, nt - 1);
+    } else {
+      cross(S, c0, nt, 0, 0);
+    }
     // step c0+64: diagonal block, TRSM, both rank-64 updates of the rest in one pass
     diag(c0 + NB64, false);
+    if (lower) join();
     const int nt2 = (R2 - NB64 + 63) / 64;
     const long long tt = (lower ? 1LL : 2LL) * nt2 * B;
-    hipLaunchKernelGGL(nlu_trsm_kernel, grid(tt), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0 + NB64, binv,
-                       nt2, (int)tt, kamax, kls, h.n, h.m, lower ? 1 : 2);
+    hipLaunchKernelGGL(nlu_trsm_kernel, grid(tt), dim3(256), 0, S, K, h.ld, h.nmax, meta, c0 + NB64,
+                       binv_of(c0 + NB64), nt2, (int)tt, kamax, kls, h.n, h.m, lower ? 1 : 2);
     DOPT_CHECK_HIP(hipGetLastError());
-    const long long tot = (lower ? (long long)nt2 * (nt2 + 1) / 2 : (long long)nt2 * nt2) * B;
-    hipLaunchKernelGGL(nlu_update2_kernel, grid(tot), dim3(256), 0, h.stream, K, h.ld, h.nmax, meta, c0, nt2, nt2,
-                       (int)tot, w0, w1, binv, kls, h.n, h.m, lower, src, srcmode);
-    DOPT_CHECK_HIP(hipGetLastError());
+    if (lower && nt2 > 1) {   // column 0 (next diagonal block, strip 0) on S, the rest on T
+      fork();
+      update2(S, c0, nt2, 0, nt2);
+      update2(T, c0, nt2, nt2, nt2 * (nt2 + 1) / 2 - nt2);
+      pending = true;
+    } else {
+      update2(S, c0, nt2, 0, lower ? nt2 * (nt2 + 1) / 2 : 0);
+    }
     c0 += 2 * NB64;
   }
+  if (pending) join();
 }
 
 }  // namespace dopt

@@ -87,7 +87,7 @@ int main(int argc, char** argv) {
       snprintf(nm, sizeof nm, "cross c0=%d", c0);
       timeit(nm, [&] {
         hipLaunchKernelGGL(nlu_cross_kernel, dim3((2 * nt - 1) * B), dim3(256), 0, 0, K, ld, nmax, meta, c0, binv,
-                           nt, (2 * nt - 1) * B, nullptr, nullptr, kamax, nullptr, 0, 0, 0, QSrc{}, 0);
+                           nt, (2 * nt - 1) * B, nullptr, nullptr, kamax, nullptr, 0, 0, 0, QSrc{}, 0, 0, 0);
       });
     }
   }
