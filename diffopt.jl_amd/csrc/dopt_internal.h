@@ -135,8 +135,13 @@ struct Handle {
   DevBuf glist;              // problem indices of the generic LU
   DevBuf lsqr_ws;            // LSQR vectors of the `iterative` branch (5 per problem)
   DevBuf binv;               // no-pivot LU: packed 64×64 inverses of the diagonal blocks (two, by step parity)
-  hipStream_t aux = nullptr;       // no-pivot LU, P-symmetric batches: second stream (off the critical chain)
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipStream_t aux = nullptr;       // second stream: Q's symmetry check beside the prepare kernel; the
+                                   // P-symmetric no-pivot LU's work off the critical chain
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_qsym = nullptr, ev_crit = nullptr;
+  hipStream_t crit = nullptr;      // high-priority stream of the LU's critical chain (prio_mode)
+  int32_t prio_mode = 1;           // env DOPT_PRIO=0: the chain stays on the handle's stream
+  DevBuf qsy;                // Q symmetry check: max |Q|, |A| (B doubles), then the asymmetry flags (B int32)
+  bool qsym_pending = false; // the check is queued on `aux`; the LU waits for ev_qsym first
   DevBuf fwdw;               // fused call: both right-hand sides, forward-swept inside the no-pivot LU
   DevBuf krhs, kx, kfull;    // multi-RHS calls: k seeds' reduced RHS, solutions, full forward RHS
   DevBuf mws;                // multi-RHS: per-workgroup vectors of tall systems (qp_multi.hip)
@@ -222,6 +227,30 @@ struct Handle {
     ev_pending.clear();
   }
 };
+
+// the handle's second stream and its fork / join events (created on first
+// use); with prio_mode, also the high-priority stream of the no-pivot LU's
+// critical chain (`crit`), so that the diagonal launches are dispatched ahead
+// of the bulk tiles queued on `aux`
+inline void ensure_aux(Handle& h) {
+  if (h.aux) return;
+  int least = 0, greatest = 0;
+  DOPT_CHECK_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  DOPT_CHECK_HIP(hipStreamCreateWithPriority(&h.aux, hipStreamNonBlocking, least));
+  if (h.prio_mode) DOPT_CHECK_HIP(hipStreamCreateWithPriority(&h.crit, hipStreamNonBlocking, greatest));
+  DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_fork, hipEventDisableTiming));
+  DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_join, hipEventDisableTiming));
+  DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_qsym, hipEventDisableTiming));
+  DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_crit, hipEventDisableTiming));
+}
+inline double* qsy_max(Handle& h) { return h.qsy.as<double>(); }
+inline int32_t* qsy_flag(Handle& h) { return reinterpret_cast<int32_t*>(h.qsy.as<double>() + h.batch); }
+// the handle's stream waits for the pending Q symmetry check
+inline void qsym_join(Handle& h) {
+  if (!h.qsym_pending) return;
+  DOPT_CHECK_HIP(hipStreamWaitEvent(h.stream, h.ev_qsym, 0));
+  h.qsym_pending = false;
+}
 
 // RAII phase bracket: records a start/stop event pair around the kernels
 // launched in its scope when profiling is enabled.

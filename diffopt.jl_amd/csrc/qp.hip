@@ -719,7 +719,7 @@ __global__ void qp_prep_kernel(QPIn, double*, int32_t*, int32_t*, double*, doubl
                                const int32_t*, double*, int);
 __global__ void qp_asm_tile_kernel(QPIn, const int32_t*, const double*, const double*, int64_t, QPMeta*, double*,
                                    int, int, const int32_t*, int, double*);
-__global__ void qp_qsym_kernel(QPIn, QPMeta*, double*, const int32_t*);
+__global__ void qp_qsym_kernel(QPIn, double*, int32_t*, const int32_t*);
 int qsym_pairs(int n);
 int prep_rows_per_thread(int m);
 int prep_threads(int m);
@@ -759,6 +759,21 @@ template <class F>
 static void prep_assemble(Handle& h, const int32_t* plist, int count, bool full, F&& after_prep) {
   if (count == 0) return;
   const QPIn P = qp_inputs(h);
+  if (!full && h.n > 0) {
+    // Q's symmetry check (P-symmetric route) beside the prepare kernel, on the
+    // second stream: it reads only Q / A, its verdict goes to qsy (consumed
+    // by the LU's first diagonal launch, which waits for it: qsym_join)
+    ensure_aux(h);
+    h.qsy.ensure((size_t)h.batch * (sizeof(double) + sizeof(int32_t)));
+    DOPT_CHECK_HIP(hipEventRecord(h.ev_fork, h.stream));
+    DOPT_CHECK_HIP(hipStreamWaitEvent(h.aux, h.ev_fork, 0));
+    DOPT_CHECK_HIP(hipMemsetAsync(h.qsy.p, 0, h.qsy.bytes, h.aux));
+    hipLaunchKernelGGL(qp_qsym_kernel, dim3((unsigned)qsym_pairs(h.n), (unsigned)count), dim3(256), 0, h.aux, P,
+                       qsy_max(h), qsy_flag(h), plist);
+    check_launch();
+    DOPT_CHECK_HIP(hipEventRecord(h.ev_qsym, h.aux));
+    h.qsym_pending = true;
+  }
   const dim3 pg(count), pb(prep_threads(h.m));
   if (prep_rows_per_thread(h.m) == 2)
     hipLaunchKernelGGL(qp_prep_kernel<2>, pg, pb, prep_lds(h.n), h.stream, P, h.s.as<double>(),
@@ -770,11 +785,6 @@ static void prep_assemble(Handle& h, const int32_t* plist, int count, bool full,
                        plist, h.kamax.as<double>(), h.sym_mode);
   check_launch();
   after_prep();
-  if (!full && h.n > 0) {   // P-symmetric problems: Q's symmetry (they skip the tile kernel)
-    hipLaunchKernelGGL(qp_qsym_kernel, dim3((unsigned)qsym_pairs(h.n), (unsigned)count), dim3(256), 0, h.stream, P,
-                       h.meta.as<QPMeta>(), h.kamax.as<double>(), plist);
-    check_launch();
-  }
   hipLaunchKernelGGL(qp_asm_tile_kernel, dim3((unsigned)count * ASM_WPP), dim3(512), 0, h.stream, P,
                      h.kidx.as<int32_t>(), h.kls.as<double>(), h.gk.as<double>(), h.batch, h.meta.as<QPMeta>(),
                      h.K.as<double>(), h.ld,

@@ -26,12 +26,14 @@
 //                        K makes no round trip through HBM before the LU.
 //                        Every other problem, and every re-assembly (`full`),
 //                        is written in full.
-//   qp_qsym_kernel       for the P-symmetric problems: Q exactly symmetric
+//   qp_qsym_kernel       for the P-symmetric route: Q exactly symmetric
 //                        (the source reads take Q(r, c) as Q(c, r)), 64×64
 //                        tile pairs of Q, both read coalesced and compared
-//                        through LDS; max |Q| and |A| into the growth bound.  A
-//                        mismatch marks the problem LU_REJECT (re-assembled in
-//                        full, partial pivoting).
+//                        through LDS; max |Q| and |A| for the growth bound.
+//                        Runs on the handle's second stream beside the prepare
+//                        kernel (it reads only Q and A); the LU's first
+//                        diagonal launch waits for it and rejects a mismatch
+//                        (re-assembled in full, partial pivoting).
 //
 // The single-workgroup-per-problem predecessor (prepare and tile loop in one
 // workgroup, G blocks written from the s-loop registers) measured 527 µs on
@@ -478,20 +480,24 @@ __global__ __launch_bounds__(ATH) void qp_asm_tile_kernel(QPIn P, const int32_t*
 }
 
 // ---------------------------------------------------------------------------
-// Q symmetry check of the P-symmetric problems (the LU's source reads take
+// Q symmetry check for the P-symmetric route (the LU's source reads take
 // Q(r, c) as Q(c, r)): grid (tile pairs R ≤ C of Q's ⌈n/64⌉² grid, problems),
 // 256 threads.  Tile (R, C) is read with the lanes along its rows (Q is
 // column-major) into LDS, tile (C, R) the same way into registers, and
 // Q(R·64 + i, C·64 + j) is compared with Q(C·64 + j, R·64 + i) bit for bit.
-// max |Q| (and, pair 0, max |A|) folds into kamax.
+// Independent of the prepare kernel (it runs beside it, on the handle's
+// second stream): every problem is checked, the verdict goes to qflag[b] (1:
+// asymmetric) and max |Q| (and, pair 0, max |A|) to qmax[b] (both zeroed
+// before the launch); the no-pivot LU's first diagonal launch consumes them
+// (a P-symmetric problem with qflag set is rejected to partial pivoting,
+// qmax folds into kamax for the growth bound).
 // ---------------------------------------------------------------------------
 constexpr int QS = 64, QSLD = QS + 1, QST = 256;
 
-__global__ __launch_bounds__(QST) void qp_qsym_kernel(QPIn P, QPMeta* __restrict__ meta, double* __restrict__ kamax,
+__global__ __launch_bounds__(QST) void qp_qsym_kernel(QPIn P, double* __restrict__ qmax, int32_t* __restrict__ qflag,
                                                       const int32_t* __restrict__ plist) {
   __shared__ double T[QS * QSLD];
   const int b = plist ? plist[blockIdx.y] : (int)blockIdx.y;
-  if (!meta[b].sym) return;   // workgroup-uniform
   const int n = P.n, t = threadIdx.x;
   const int TQ = (n + QS - 1) / QS;
   int R = 0, rem = (int)blockIdx.x;
@@ -531,10 +537,10 @@ __global__ __launch_bounds__(QST) void qp_qsym_kernel(QPIn P, QPMeta* __restrict
   }
   if (blockIdx.x == 0)
     for (size_t e = t; e < (size_t)P.p * n; e += QST) vmax = fmax(vmax, fabs(P.A[(size_t)b * P.p * n + e]));
-  if (__syncthreads_or(bad) && t == 0) meta[b].lu = LU_REJECT;
+  if (__syncthreads_or(bad) && t == 0) qflag[b] = 1;
   for (int o = 32; o > 0; o >>= 1) vmax = fmax(vmax, __shfl_xor(vmax, o));
   if ((t & 63) == 0)
-    atomicMax(reinterpret_cast<unsigned long long*>(kamax) + b, (unsigned long long)__double_as_longlong(vmax));
+    atomicMax(reinterpret_cast<unsigned long long*>(qmax) + b, (unsigned long long)__double_as_longlong(vmax));
 }
 
 int qsym_pairs(int n) {

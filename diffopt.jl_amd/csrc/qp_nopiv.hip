@@ -49,10 +49,15 @@
 //    the memory-bound update needs.
 //
 // Factor format: K row-major, L strictly below / U on and above the diagonal
-// outside the 32×32 diagonal blocks (those keep the assembled values: the
-// solves never read them, they use the blocks' inverses in dinv), perm =
-// identity, dinv as the partial-pivoting path writes it — the solves of
-// qp_blocked.hip serve both.
+// outside the 32×32 diagonal blocks.  Those blocks are NOT factor entries:
+// they hold whatever the earlier block steps' trailing updates left there (or,
+// for P-symmetric problems, nothing written at all), because the solves never
+// read them — they use the blocks' inverses in dinv.  perm = identity, dinv as
+// the partial-pivoting path writes it — the solves of qp_blocked.hip serve
+// both.  Allowed consumers of K are therefore the solves and multi-RHS solves
+// (off-diagonal tiles) only; anything that needs U's pivots (singularity
+// verdicts, determinants, inertia) reads u_ii = 1 / (U11⁻¹)_ii from dinv, as
+// nlp_pivot_check_kernel does.
 //
 // Reference: QuadraticProgram.jl create_LHS_matrix :256-282 and solve_system
 // :486-496 (reverse :316-351, forward :357-446).
@@ -135,6 +140,8 @@ __device__ __forceinline__ PScale pscale(const double* kls, int b, int n, int m,
 // ---------------------------------------------------------------------------
 struct QSrc {          // batch bases (kernel argument)
   const double *Q, *gk, *kls, *A;
+  const double* qmax;     // Q symmetry check (qp_qsym_kernel): max |Q|, |A| per problem
+  const int32_t* qflag;   // ... and its verdict (1: Q not exactly symmetric)
   int n, m, p;
   int64_t B;
 };
@@ -198,7 +205,133 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// 1/d: v_rcp_f64 + two Newton steps
+__device__ __forceinline__ double rcp_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(fma(-d, r, 1.0), r, r);
+  return fma(fma(-d, r, 1.0), r, r);
+}
+
+// Blocked by 4 columns (default): step j4 factorises the 4×4 diagonal tile in
+// its owner lane (j4, j4), the panel lanes (j4, tj > j4) / (ti > j4, j4) then
+// form their U / L pieces locally from it (U = L_dd⁻¹·A, L = A·U_dd⁻¹), and
+// every trailing lane applies the rank-4 update from the pieces — two wave
+// syncs per 4 columns instead of eight, every piece written to S as it is
+// final.  The unblocked form (one column per step, kept below as
+// wave_lu32_cols) is the same factorisation with a different rounding order.
 __device__ __forceinline__ int wave_lu32(double* S, int o, double* rowb, double* colb, double* trash, double bound) {
+  (void)colb;
+  (void)trash;
+  const int lane = threadIdx.x & 63, ti = lane >> 3, tj = lane & 7;
+  double a[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a[r][c] = S[(o + 4 * ti + r) * SLD + o + 4 * tj + c];
+  double* rc = rowb;   // the current step's 4 pivot reciprocals
+#pragma unroll 1
+  for (int j4 = 0; j4 < 8; ++j4) {
+    const int d = o + 4 * j4;
+    // 1. the diagonal tile, in its owner lane
+    if (ti == j4 && tj == j4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double r = rcp_nr(a[k][k]);
+        rc[k] = r;
+#pragma unroll
+        for (int i = k + 1; i < 4; ++i) a[i][k] *= r;
+#pragma unroll
+        for (int i = k + 1; i < 4; ++i)
+#pragma unroll
+          for (int c = k + 1; c < 4; ++c) a[i][c] = fma(-a[i][k], a[k][c], a[i][c]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) S[(d + r) * SLD + d + c] = a[r][c];
+    }
+    wave_sync();
+    // 2. the panels: L pieces below (column by column through U_dd), U pieces
+    // to the right (row by row through the unit-lower L_dd)
+    if (tj == j4 && ti > j4) {
+      double u[4][4], r[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        r[q] = rc[q];
+#pragma unroll
+        for (int k = q + 1; k < 4; ++k) u[q][k] = S[(d + q) * SLD + d + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          double v = a[i][k];
+#pragma unroll
+          for (int q = 0; q < k; ++q) v = fma(-a[i][q], u[q][k], v);
+          a[i][k] = v * r[k];
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) S[(o + 4 * ti + i) * SLD + d + k] = a[i][k];
+    } else if (ti == j4 && tj > j4) {
+      double l[4][4];
+#pragma unroll
+      for (int k = 1; k < 4; ++k)
+#pragma unroll
+        for (int q = 0; q < k; ++q) l[k][q] = S[(d + k) * SLD + d + q];
+#pragma unroll
+      for (int k = 1; k < 4; ++k)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          double v = a[k][c];
+#pragma unroll
+          for (int q = 0; q < k; ++q) v = fma(-l[k][q], a[q][c], v);
+          a[k][c] = v;
+        }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) S[(d + k) * SLD + o + 4 * tj + c] = a[k][c];
+    }
+    wave_sync();
+    // 3. the rank-4 update of the trailing tiles (no sync after it: the next
+    // step writes only its own diagonal tile and panels, which no lane reads here)
+    if (ti > j4 && tj > j4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {   // one k-column at a time (8 operands live)
+        double lp[4], up[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          lp[i] = S[(o + 4 * ti + i) * SLD + d + q];
+          up[i] = S[(d + q) * SLD + o + 4 * tj + i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) a[i][c] = fma(-lp[i], up[c], a[i][c]);
+      }
+    }
+  }
+  // the threshold test once, on the final values (S already holds them): every
+  // pivot non-zero and within the growth bound (finite), every |l| ≤
+  // NOPIV_LMAX (NaN fails)
+  int bad = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int gi = 4 * ti + r, gj = 4 * tj + c;
+      if (gi == gj) bad |= !(fabs(a[r][c]) > 0.0) || !(fabs(a[r][c]) <= bound);
+      if (gi > gj) bad |= !(fabs(a[r][c]) <= NOPIV_LMAX);
+    }
+  return __any(bad) ? 1 : 0;
+}
+
+// The unblocked single-wave LU (one column per step; two wave syncs per
+// column).  Kept for comparison probes (tools/probe).
+__device__ __forceinline__ int wave_lu32_cols(double* S, int o, double* rowb, double* colb, double* trash,
+                                              double bound) {
   const int lane = threadIdx.x & 63, ti = lane >> 3, tj = lane & 7;
   double a[4][4];
 #pragma unroll
@@ -755,7 +888,7 @@ template <bool STRIP0>
 __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_diag_kernel(
     double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
     size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv, double* __restrict__ w0,
-    double* __restrict__ w1, const double* __restrict__ kamax, const double* __restrict__ kls, int n, int m,
+    double* __restrict__ w1, double* __restrict__ kamax, const double* __restrict__ kls, int n, int m,
     QSrc src, int srcmode) {
   __shared__ double S[STEP_LDS];
   const int b = blockIdx.x;
@@ -767,6 +900,18 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
   double* Kb = K + (size_t)b * nmax * ld;
   const bool src_on = srcmode && c0 == 0 && mm.sym;   // step 0 of a P-symmetric problem: K not assembled
   const QSrcB sv = qsrc(src, b, mm);
+  double amax = kamax[b];
+  if (src_on) {
+    // the Q symmetry check's verdict: an asymmetric Q leaves the P-symmetric
+    // route (partial pivoting); max |Q|, |A| joins max |K| for the growth
+    // bound of this and every later launch
+    if (src.qflag[b]) {
+      if (t == 0) meta[b].lu = LU_REJECT;
+      return;
+    }
+    amax = fmax(amax, src.qmax[b]);
+    if (t == 0) kamax[b] = amax;
+  }
   NLU_MARK_INIT;
   // the block → LDS (identity beyond Wv); all 16 loads in flight
   {
@@ -786,7 +931,7 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
   }
   if (t == 0 && c0 == 0) meta[b].lu = LU_NOPIV;   // LU_REJECT below if a test fails
   NLU_MARK(0);
-  const double bound = growth_bound(kamax[b]);
+  const double bound = growth_bound(amax);
   diag_core(DiagLds(S), Kb, ld, perm + (size_t)b * nmax, dinv + (size_t)b * dstride + (size_t)(c0 / 32) * DBLK,
             meta + b, c0, Np, mm.nsys, binv + (size_t)b * BSTR, w0 ? w0 + (size_t)b * nmax : nullptr,
             w0 ? w1 + (size_t)b * nmax : nullptr, bound);
@@ -1347,6 +1492,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 // w0 / w1 (both or neither): the reverse / forward right-hand sides,
 // forward-swept in place along the way (fwd_block).
 void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
+  qsym_join(h);   // the first diagonal launch reads the Q symmetry check
   const int npmax = h.blocked_npmax;
   if (npmax == 0) return;
   const int B = (int)h.batch;
@@ -1354,7 +1500,7 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   // when every blocked problem of the batch qualifies (tile grids halved)
   const bool qp = h.kind == DOPT_KIND_QP;
   const double* kls = qp ? h.kls.as<double>() : nullptr;
-  const double* kamax = h.kamax.as<double>();
+  double* kamax = h.kamax.as<double>();
   int lower = qp && h.meta_host ? 1 : 0;
   // step 0 of the P-symmetric problems reads the QP inputs (no K assembly)
   static const double zero = 0.0;
@@ -1363,6 +1509,11 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   src.gk = qp ? h.gk.as<double>() : &zero;
   src.kls = qp ? h.kls.as<double>() : &zero;
   src.A = qp && h.p ? h.A : &zero;
+  // the check's results exist only when a prepare of the P-symmetric route ran
+  static const int32_t zflag = 0;
+  const bool qchk = qp && h.qsy.p && h.n > 0;
+  src.qmax = qchk ? qsy_max(h) : &zero;
+  src.qflag = qchk ? qsy_flag(h) : &zflag;
   src.n = h.n;
   src.m = h.m;
   src.p = h.p;
@@ -1393,12 +1544,13 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   // each band / trailing update, joined by events before their consumers
   hipStream_t S = h.stream, T = h.stream;
   if (lower) {
-    if (!h.aux) {
-      DOPT_CHECK_HIP(hipStreamCreateWithFlags(&h.aux, hipStreamNonBlocking));
-      DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_fork, hipEventDisableTiming));
-      DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_join, hipEventDisableTiming));
-    }
+    ensure_aux(h);
     T = h.aux;
+    if (h.crit) {   // the chain on the high-priority stream, forked from / joined back into h.stream
+      S = h.crit;
+      DOPT_CHECK_HIP(hipEventRecord(h.ev_crit, h.stream));
+      DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_crit, 0));
+    }
   }
   auto fork = [&] {   // T starts after everything queued on S so far
     DOPT_CHECK_HIP(hipEventRecord(h.ev_fork, S));
@@ -1475,6 +1627,10 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
     c0 += 2 * NB64;
   }
   if (pending) join();
+  if (S != h.stream) {
+    DOPT_CHECK_HIP(hipEventRecord(h.ev_crit, S));
+    DOPT_CHECK_HIP(hipStreamWaitEvent(h.stream, h.ev_crit, 0));
+  }
 }
 
 }  // namespace dopt

@@ -343,8 +343,9 @@ int dopt_get_system_size(dopt_handle* h, int32_t* sizes);
 /* Per-phase GPU time, measured with HIP events on the handle's stream around
  * each phase's kernels while profiling is on (off by default). */
 #define DOPT_PHASE_QP_ASSEMBLE 0  /* branch flag, s = Gz − h, elimination, KKT   */
-#define DOPT_PHASE_QP_LU 1        /* no-pivot blocked LU (+ generic LU)          */
-#define DOPT_PHASE_QP_LU_PIVOT 2  /* partial-pivoting LU (rejected problems)     */
+#define DOPT_PHASE_QP_LU 1        /* no-pivot blocked LU                         */
+#define DOPT_PHASE_QP_LU_PIVOT 2  /* partial-pivoting LU (rejected problems, the
+                                     generic unblocked LU, NLP factorisations)  */
 #define DOPT_PHASE_QP_RHS 3       /* forward/reverse right-hand sides            */
 #define DOPT_PHASE_QP_SOLVE 4     /* triangular solves                           */
 #define DOPT_PHASE_QP_LSQR 5      /* LSQR (norm(Q) == 0 branch)                  */
@@ -366,7 +367,11 @@ int dopt_get_phase_times(dopt_handle* h, double* ms, int32_t* counts,
                          int32_t nphases);
 const char* dopt_phase_name(int32_t phase);
 /* wall time (s) of the last forward/reverse call, incl. any factorisation it
- * triggered — the DifferentiateTimeSec analogue (diff_opt.jl:256-266). */
+ * triggered — the DifferentiateTimeSec analogue (diff_opt.jl:256-266).
+ * Exception: a device-mode dopt_qp_forward_reverse that returned
+ * stream-ordered (see above) records only the time to queue its work; call
+ * hipStreamSynchronize on the handle's stream and time around it for the
+ * completed solve. */
 double dopt_last_time(const dopt_handle* h);
 
 #ifdef __cplusplus
