@@ -118,6 +118,8 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
     if (const char* e = getenv("DOPT_LU")) h->lu_mode = atoi(e) != 0;
     if (const char* e = getenv("DOPT_SYM")) h->sym_mode = atoi(e) != 0;
     if (const char* e = getenv("DOPT_PRIO")) h->prio_mode = atoi(e) != 0;
+    if (const char* e = getenv("DOPT_LEFT")) h->left_mode = atoi(e) != 0;
+    if (const char* e = getenv("DOPT_LSTREAMS")) h->lstreams = atoi(e) != 0;
     if (kind == DOPT_KIND_QP) {
       // largest supported system: the generic solve stages an nmax vector in
       // LDS (64 KB); the blocked route takes reduced systems up to BLOCKED_MAX
@@ -168,7 +170,7 @@ int dopt_destroy(dopt_handle* h) {
   DevBuf* bufs[] = {&h->dinv, &h->plist, &h->lsqr_ws, &h->binv, &h->fwdw, &h->K, &h->ipiv, &h->s, &h->kidx, &h->meta, &h->rhs,
                     &h->x, &h->cone_dev, &h->vp, &h->dpi, &h->cwork, &h->cinfo, &h->cnorm, &h->csplit, &h->krhs, &h->kx,
                     &h->kfull, &h->kamax, &h->nlp_map, &h->nlp_shift, &h->nlp_scale, &h->kls, &h->gk, &h->glist,
-                    &h->mws, &h->qsy, &h->psd_eig, &h->psd_app};
+                    &h->mws, &h->qsy, &h->psd_eig, &h->psd_app, &h->ukp};
   for (auto* b : bufs) b->release();
   for (auto& b : h->own_nin) b.release();
   for (auto& b : h->own_in) b.release();

@@ -140,6 +140,11 @@ struct Handle {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_qsym = nullptr, ev_crit = nullptr;
   hipStream_t crit = nullptr;      // high-priority stream of the LU's critical chain (prio_mode)
   int32_t prio_mode = 1;           // env DOPT_PRIO=0: the chain stays on the handle's stream
+  int32_t left_mode = 1;           // P-symmetric batches: left-looking LU (env DOPT_LEFT=0: right-looking)
+  int32_t lstreams = 0;            // left-looking LU: column tiles I ≥ J+2 on `aux` (env DOPT_LSTREAMS=1)
+  DevBuf ukp;                      // left-looking LU: u_kk / p_k of every finished diagonal block (nmax per problem)
+  bool ukp_valid = false;          // the last no-pivot factorisation was left-looking (ukp holds its u_kk / p_k)
+  bool u_missing = false;          // ... and stored only L for its P-symmetric problems (U from L on demand)
   DevBuf qsy;                // Q symmetry check: max |Q|, |A| (B doubles), then the asymmetry flags (B int32)
   bool qsym_pending = false; // the check is queued on `aux`; the LU waits for ev_qsym first
   DevBuf fwdw;               // fused call: both right-hand sides, forward-swept inside the no-pivot LU
@@ -291,6 +296,9 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
 //                   and the triangular solves shared by both
 void qp_nopiv_factor(Handle& h, double* dinv, double* w0 = nullptr, double* w1 = nullptr);
 void qp_blocked_factor(Handle& h, double* dinv, const int32_t* plist, int count);
+// U of the left-looking route's P-symmetric factors, from L (before any solve
+// that reads U: single-direction and multi-RHS solves); no-op unless u_missing
+void qp_nopiv_materialize_u(Handle& h);
 void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rhs, double* x, int sel);
 void qp_blocked_solve_multi(Handle& h, const double* dinv, int trans, int k, const double* rhs, double* x,
                             int sel);

@@ -474,6 +474,13 @@ constexpr int SOLVE_STATIC = 3 * PT + BNB;
 __host__ __device__ inline int solve_lds_np(int nmax) { return nmax < BLOCKED_MAX ? nmax : BLOCKED_MAX; }
 __host__ inline size_t solve_lds_bytes(int nmax) { return (size_t)solve_lds_np(nmax) * (2 * sizeof(double) + sizeof(int)); }
 
+// P-symmetric no-pivot factors (qp_nopiv.hip left-looking route): u_kk / p_k
+// per row (ukp, nmax per problem) and the row scales (kls: λ_k, m per problem)
+struct SymSweep {
+  const double *ukp, *kls;
+  int n, m;
+};
+
 template <int ENT, bool TALL = false>
 __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict__ K, int ld, int nmax,
                                                 const int32_t* __restrict__ perm,
@@ -481,7 +488,7 @@ __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict_
                                                 const QPMeta* __restrict__ meta, int trans, int sel,
                                                 const double* __restrict__ rhs,
                                                 double* __restrict__ xout, double* v, double* y, int* ps,
-                                                double* part, int sweep0 = 0) {
+                                                double* part, int sweep0 = 0, const SymSweep* sym = nullptr) {
   const QPMeta mm = meta[b];
   const int Np = blocked_np(mm);
   if (Np == 0 || !((sel >> mm.lu) & 1)) return;
@@ -491,9 +498,13 @@ __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict_
   const int32_t* pb = perm + (size_t)b * nmax;
   const double* Dbase = dinv + (size_t)b * dstride;
   const double* rb = rhs + (size_t)b * nmax;
+  // sym: the reverse backward sweep U x = y of a P-symmetric factor as
+  // Lᵀ (P x) = y ./ (u/p) (U = D_u·P⁻¹·Lᵀ·P), x = (P x) ./ p after the sweep
+  const double* udb = sym ? sym->ukp + (size_t)b * nmax : nullptr;
+  const PScale psc = sym ? PScale{sym->kls + (size_t)b * sym->m, sym->n, mm.nk} : PScale{nullptr, 0, 0};
   for (int i = t; i < Np; i += PT) {
     ps[i] = pb[i];
-    y[i] = i < N ? rb[i] : 0.0;
+    y[i] = i < N ? (udb ? rb[i] / udb[i] : rb[i]) : 0.0;
   }
   __syncthreads();
   for (int i = t; i < Np; i += PT) v[i] = trans ? y[i] : y[ps[i]];
@@ -601,7 +612,7 @@ __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict_
   } else {
     for (int i = t; i < Np; i += PT) y[ps[i]] = v[i];
     __syncthreads();
-    for (int i = t; i < N; i += PT) xb[i] = y[i];
+    for (int i = t; i < N; i += PT) xb[i] = udb ? y[i] / psc(i) : y[i];
   }
 }
 
@@ -744,7 +755,7 @@ __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict
                                                         double* __restrict__ x_rev,
                                                         double* __restrict__ x_fwd,
                                                         const double* __restrict__ w_rev,
-                                                        const double* __restrict__ w_fwd) {
+                                                        const double* __restrict__ w_fwd, SymSweep sym) {
   SOLVE_LDS(TALL);
   int L = blockIdx.x;
   if (B % 8 == 0) {   // workgroups 16g+j (rows) and 16g+8+j (columns) solve problem 8g+j
@@ -753,7 +764,10 @@ __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict
   }
   const int pb = L < B ? L : L - B;
   const bool swept = w_rev && meta[pb].lu == LU_NOPIV;
-  if (L < B)
+  if (L < B && swept && sym.ukp && meta[pb].sym)   // both directions sweep Lᵀ: U is not read
+    solve_cols_body<ENT, TALL>(L, K, ld, nmax, perm, dinv, dstride, meta, 1, sel, w_rev, x_rev, v, y, ps, part, 1,
+                               &sym);
+  else if (L < B)
     solve_rows_body(L, K, ld, nmax, perm, dinv, dstride, meta, sel, swept ? w_rev : rhs_rev, x_rev, v, ps, part,
                     swept ? 1 : 0);
   else
@@ -829,6 +843,7 @@ static void solve_lds_optin(KF kf, size_t lds) {
 }
 
 void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rhs, double* x, int sel) {
+  qp_nopiv_materialize_u(h);
   const int npmax = h.blocked_npmax;
   if (npmax == 0) return;
   const int B = (int)h.batch;
@@ -870,10 +885,12 @@ void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, con
   const QPMeta* meta = h.meta.as<QPMeta>();
   const int ent = (npmax + PT - 1) / PT;
   const size_t lds = solve_lds_bytes(h.nmax);
+  // the left-looking LU's u_kk / p_k: the P-symmetric problems' reverse sweep through Lᵀ
+  SymSweep sym{h.ukp_valid ? h.ukp.as<double>() : nullptr, h.kls.as<double>(), h.n, h.m};
 #define DOPT_SOLVE2(E, T)                                                                         \
   solve_lds_optin(blu_solve2_kernel<E, T>, T ? lds : 0);                                          \
   hipLaunchKernelGGL((blu_solve2_kernel<E, T>), dim3(2 * B), dim3(PT), T ? lds : 0, h.stream, K, h.ld, h.nmax, perm, \
-                     dinv, dstride, meta, B, sel, rhs_rev, rhs_fwd, x_rev, x_fwd, w_rev, w_fwd)
+                     dinv, dstride, meta, B, sel, rhs_rev, rhs_fwd, x_rev, x_fwd, w_rev, w_fwd, sym)
   if (ent <= 1) { DOPT_SOLVE2(1, false); }
   else if (ent == 2) { DOPT_SOLVE2(2, false); }
   else if (npmax <= SOLVE_STATIC) { DOPT_SOLVE2(3, false); }

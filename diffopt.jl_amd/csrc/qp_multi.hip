@@ -142,6 +142,7 @@ __global__ __launch_bounds__(MT) void blu_solve_multi_kernel(const double* __res
 // factor kind is in `sel`, one launch.
 void qp_blocked_solve_multi(Handle& h, const double* dinv, int trans, int k, const double* rhs, double* x,
                             int sel) {
+  qp_nopiv_materialize_u(h);
   const int npmax = h.blocked_npmax;
   if (npmax == 0 || k <= 0) return;
   const int B = (int)h.batch;

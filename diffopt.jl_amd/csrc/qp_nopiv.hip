@@ -180,6 +180,21 @@ __device__ __forceinline__ double kval(const QSrcB& v, int r, int c) {
   return c < n ? v.A[(size_t)c * v.p + (r - n - nk)] : 0.0;
 }
 
+// kval for r > c (strictly lower part): the same values, with Q(r, c) read
+// as stored (column-major, Q[c·n + r]) — lanes along r then coalesce on every
+// source (Q, G_k's column-major copy, A)
+__device__ __forceinline__ double kval_lower(const QSrcB& v, int r, int c) {
+  const int n = v.n, nk = v.nk;
+  if (r >= v.N || c >= v.N) return r == c ? 1.0 : 0.0;
+  if (c < n) {
+    if (r < n) return v.Q[(size_t)c * n + r];
+    if (r < n + nk) return v.gk[(size_t)c * v.m + (r - n)];
+    return v.A[(size_t)c * v.p + (r - n - nk)];
+  }
+  if (r < n + nk) return r == c ? v.sk[r - n] : 0.0;
+  return 0.0;
+}
+
 // Tile `tile` of the lower triangle (rt ≥ ct) of an nrt × nrt grid, column by
 // column: column 0's nrt tiles first.
 __device__ __forceinline__ void col_lower_tile(int tile, int nrt, int& rt, int& ct) {
@@ -1477,6 +1492,311 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
   }
 }
 
+// ===========================================================================
+// Left-looking no-pivot LU of P-symmetric batches (default for those).
+//
+// With P·K symmetric, U(k, J) = D_k·L(J, k)ᵀ·P_J (D_k = diag(u_kk / p_k) of
+// block k, P_J = diag(p) of block J's columns), so every tile of block
+// column J is formed once, from the sources, as
+//   C(I, J) = A(I, J) − [Σ_{k<J} L(I, k)·D_k·L(J, k)ᵀ]·P_J,      I ≥ J,
+// and then factorised (I = J) or solved against U_JJ (I > J).  No tile is
+// read and written back per step (the right-looking passes moved 3.5 GB per
+// config-2 factorisation, PMC), the forward sweeps of the fused call become
+// GEMVs over the same row strip L(J, <J), and a column takes two launches:
+//   nlu_ldiag_kernel  one 256-thread WG per problem: C(J, J) by MFMA over
+//                     the staged row strip L(J, k); the sweeps; diag_core
+//                     (LU, inverses, dinv, the packed inverse for the TRSM);
+//                     u_kk / p_k of the block (ukp)
+//   nlu_lcol_kernel   one 256-thread WG per tile (I ≥ J+1, J): its C, then
+//                     L(I, J) = C·U_JJ⁻¹ and U(J, I) = D_J·L(I, J)ᵀ·P_I
+// (Tile (J+1, J) computed inside ldiag(J) — so that ldiag(J+1) would not
+// wait for lcol(J) — spilled 53 VGPRs there and measured slower.)
+// ===========================================================================
+
+// stage the row strip L(J, k): rows c0 .. c0+63 (zero from row `rows` on),
+// columns k0 .. k0+63 of K, transposed: X[kk·TLD + j] = L[c0 + j][k0 + kk]
+__device__ __forceinline__ void stage_rowstrip(double* X, const double* Kb, int ld, int c0, int k0, int rows) {
+  const int t = threadIdx.x, j = t >> 2, kq = (t & 3) * 16;
+  double v[16];
+  const double* src = Kb + (size_t)(c0 + (j < rows ? j : 0)) * ld + k0 + kq;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) v[u] = src[u];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) X[(kq + u) * TLD + j] = j < rows ? v[u] : 0.0;
+}
+
+__global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_ldiag_kernel(
+    double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
+    size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv, double* __restrict__ ukp,
+    double* __restrict__ w0, double* __restrict__ w1, double* __restrict__ kamax, const double* __restrict__ kls,
+    int n, int m, QSrc src) {
+  __shared__ double S[STEP_LDS];
+  const int b = blockIdx.x;
+  const QPMeta mm = meta[b];
+  const int Np = nlu_np(mm);
+  if (c0 >= Np || mm.lu == LU_REJECT) return;   // workgroup-uniform
+  const int Wv = min(NB64, Np - c0);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
+  double* Kb = K + (size_t)b * nmax * ld;
+  const QSrcB sv = qsrc(src, b, mm);
+  const PScale ps = pscale(kls, b, n, m, mm);
+  double* ud = ukp + (size_t)b * nmax;
+  double* w0b = w0 ? w0 + (size_t)b * nmax : nullptr;
+  double* w1b = w0 ? w1 + (size_t)b * nmax : nullptr;
+  double amax = kamax[b];
+  if (c0 == 0) {
+    // the Q symmetry check's verdict (partial pivoting for an asymmetric Q),
+    // max |Q|, |A| into the growth bound
+    if (src.qflag[b]) {
+      if (t == 0) meta[b].lu = LU_REJECT;
+      return;
+    }
+    amax = fmax(amax, src.qmax[b]);
+    if (t == 0) kamax[b] = amax;
+  }
+  // ---- the left-looking update of C(J, J) over k < J
+  d4n accd[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) accd[q] = (d4n){0, 0, 0, 0};
+  double sweep = 0.0;   // t < 64: Σ L(J, <J)[t]·y (w0); 64 ≤ t < 128: Σ L(J, <J)[t − 64]·(d∘z) (w1)
+  const bool dact = 16 * wv < Wv;   // wave-uniform
+  for (int k0 = 0; k0 < c0; k0 += NB64) {
+    double dk[16];   // D_k, for the A operand
+#pragma unroll
+    for (int s = 0; s < 16; ++s) dk[s] = ud[k0 + 4 * s + g];
+    __syncthreads();   // the previous strip is consumed
+    stage_rowstrip(S, Kb, ld, c0, k0, Wv);
+    __syncthreads();
+    if (dact) {
+      // A operand: this wave's rows of the same staged strip, times D_k
+      double a[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) a[s] = S[(4 * s + g) * TLD + 16 * wv + l16] * dk[s];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        double bq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bq[q] = S[(4 * s + g) * TLD + 16 * q + l16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) accd[q] = nmfma(a[s], bq[q], accd[q]);
+      }
+    }
+    if (w0b && t < 2 * NB64) {   // forward sweeps: the row strip times the finished blocks of y / z
+      const int j = t & 63;
+      double sm = 0.0;
+      if (t < NB64) {
+#pragma unroll 8
+        for (int kk = 0; kk < NB64; ++kk) sm = fma(S[kk * TLD + j], w0b[k0 + kk], sm);
+      } else {
+#pragma unroll 8
+        for (int kk = 0; kk < NB64; ++kk) sm = fma(S[kk * TLD + j], ud[k0 + kk] * w1b[k0 + kk], sm);
+      }
+      sweep += sm;
+    }
+  }
+  __syncthreads();   // the staging is consumed: S becomes the diagonal image
+  // C(J, J) = A(J, J) − acc·P_J → S (identity beyond Wv)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = 16 * q + l16;
+    const double pj = ps(c0 + j);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int i = 16 * wv + g + 4 * rr;
+      const bool in = i < Wv && j < Wv;
+      S[i * SLD + j] = in ? kval(sv, c0 + i, c0 + j) - accd[q][rr] * pj : (i == j ? 1.0 : 0.0);
+    }
+  }
+  if (w0b && t < 2 * NB64) {   // block J of b / c minus the finished blocks' contributions
+    const int j = t & 63;
+    if (j < Wv && c0 + j < mm.nsys) {
+      if (t < NB64) w0b[c0 + j] -= sweep;
+      else w1b[c0 + j] -= ps(c0 + j) * sweep;
+    }
+  }
+  if (t == 0 && c0 == 0) meta[b].lu = LU_NOPIV;   // LU_REJECT below if a test fails
+  const double bound = growth_bound(amax);
+  // diag_core's first barrier orders the S image and the sweep stores above
+  diag_core(DiagLds(S), Kb, ld, perm + (size_t)b * nmax, dinv + (size_t)b * dstride + (size_t)(c0 / 32) * DBLK,
+            meta + b, c0, Np, mm.nsys, binv + (size_t)b * BSTR, w0b, w1b, bound);
+  __syncthreads();   // S final (U11⁻¹ on the diagonal, every exit of diag_core) + verdicts
+  if (*DiagLds(S).sbad) return;
+  // u_kk / p_k: the later blocks' updates, and the solves' reverse sweep through Lᵀ
+  if (t < Wv) ud[c0 + t] = 1.0 / (S[t * SLD + t] * ps(c0 + t));
+}
+
+// Tiles (I, J), I ≥ J+1, of block column J = c0 / 64 (one 256-thread WG per
+// tile, XCD-aware order: one problem's tiles are consecutive): C(I, J) by
+// MFMA over the staged row strips L(J, k) (B operand) and this tile's row
+// strips L(I, k)·D_k (A operand), then the TRSM by the packed inverse of the
+// diagonal block (binv) with the threshold test, L(I, J) → K, and
+// U(J, I) = D_J·L(I, J)ᵀ·P_I beside it (transposed through LDS; growth bound).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_lcol_kernel(
+    double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
+    const double* __restrict__ ukp, int ntile, int toff, int total, const double* __restrict__ kamax,
+    const double* __restrict__ kls, int n, int m, QSrc src, int wr_u) {
+  __shared__ double X[NB64 * TLD];
+  const int L = blockIdx.x;
+  const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
+  const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
+  const int b = logical / ntile;
+  const int it = logical - b * ntile;
+  const QPMeta mm = meta[b];
+  const int Np = nlu_np(mm);
+  const int r0 = c0 + NB64 + 64 * (toff + it);   // first row of tile I
+  if (mm.lu == LU_REJECT || r0 >= Np) return;    // workgroup-uniform
+  const int sw = min(NB64, Np - r0);             // 32 or 64 rows
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
+  const bool wact = 16 * wv < sw;                // wave-uniform
+  double* Kb = K + (size_t)b * nmax * ld;
+  const double* ud = ukp + (size_t)b * nmax;
+  const double* Bg = binv + (size_t)b * BSTR;
+  const QSrcB sv = qsrc(src, b, mm);
+  const PScale ps = pscale(kls, b, n, m, mm);
+  const double bound = growth_bound(kamax[b]);
+  d4n acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = (d4n){0, 0, 0, 0};
+  for (int k0 = 0; k0 < c0; k0 += NB64) {
+    double a[16];   // loaded with the staging loads (one round trip per k-block)
+    if (wact) {
+      const double* ar = Kb + (size_t)(r0 + 16 * wv + l16) * ld + k0;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) a[s] = ar[4 * s + g] * ud[k0 + 4 * s + g];
+    }
+    __syncthreads();
+    stage_rowstrip(X, Kb, ld, c0, k0, NB64);   // block J is full (tiles follow it)
+    __syncthreads();
+    if (wact) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        double bq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bq[q] = X[(4 * s + g) * TLD + 16 * q + l16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = nmfma(a[s], bq[q], acc[q]);
+      }
+    }
+  }
+  // C = A − acc·P_J in the TRSM's A-operand layout (lane ↔ row 16wv + l16,
+  // k-step s ↔ column 4s + g): the sources read with the lanes along the
+  // rows, the update transposed through LDS
+  double av[16];
+  if (wact) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) av[s] = kval_lower(sv, r0 + 16 * wv + l16, c0 + 4 * s + g);
+  }
+  __syncthreads();
+  if (wact && c0 > 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = 16 * q + l16;
+      const double pj = ps(c0 + j);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) X[(16 * wv + g + 4 * rr) * TLD + j] = acc[q][rr] * pj;
+    }
+  }
+  __syncthreads();
+  if (wact && c0 > 0) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) av[s] -= X[(16 * wv + l16) * TLD + 4 * s + g];
+  }
+  {   // U11⁻¹ (upper triangle, zero below) staged once every wave holds its C rows
+    double v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = Bg[t + 256 * q];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = t + 256 * q, k = e >> 6, c = e & 63;
+      X[k * TLD + c] = k <= c ? v[q] : 0.0;
+    }
+  }
+  __syncthreads();
+  d4n lt[4];
+  int over = 0;
+  if (wact) {
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {   // U11⁻¹ is upper: k ≤ 16ct + 15
+      lt[ct] = (d4n){0, 0, 0, 0};
+#pragma unroll
+      for (int s = 0; s < 4 * (ct + 1); ++s) lt[ct] = nmfma(av[s], X[(4 * s + g) * TLD + 16 * ct + l16], lt[ct]);
+    }
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        Kb[(size_t)(r0 + 16 * wv + g + 4 * rr) * ld + c0 + 16 * ct + l16] = lt[ct][rr];
+        over |= !(fabs(lt[ct][rr]) <= NOPIV_LMAX);
+      }
+  }
+  if (wr_u) __syncthreads();   // every wave is done with U11⁻¹
+  if (wact) {   // U(J, I)[k][jl] = (u_kk / p_k)·L[jl][k]·p_jl: the growth bound; stored when wr_u
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int k = 16 * ct + l16;
+      const double uk = ud[c0 + k];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int jl = 16 * wv + g + 4 * rr;
+        const double u = uk * lt[ct][rr] * ps(r0 + jl);
+        if (wr_u) X[k * TLD + jl] = u;
+        over |= !(fabs(u) <= bound);
+      }
+    }
+  }
+  if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;   // every writer stores the same value
+  if (!wr_u) return;   // workgroup-uniform
+  __syncthreads();
+  const int k = t >> 2, cq = (t & 3) * 16;   // row k of block J, 16 columns
+  if (cq < sw) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) Kb[(size_t)(c0 + k) * ld + r0 + cq + u] = X[k * TLD + cq + u];
+  }
+}
+
+// U of the left-looking route's P-symmetric factors, materialised from L for
+// the solves that read it (single-direction and multi-RHS solves; the fused
+// call's solves sweep Lᵀ both ways and the LU does not store U): every tile
+// (I > J) of the 64-grid, U(J, I)[k][j] = (u_kk / p_k)·L(I, J)[j][k]·p_j —
+// what nlu_lcol_kernel writes when wr_u is set.  One 256-thread WG per (tile,
+// problem); problems that are not P-symmetric no-pivot factors are skipped.
+__global__ __launch_bounds__(256) void nlu_sym_u_kernel(double* __restrict__ K, int ld, int nmax,
+                                                        const QPMeta* __restrict__ meta,
+                                                        const double* __restrict__ ukp,
+                                                        const double* __restrict__ kls, int n, int m, int nb) {
+  __shared__ double X[NB64 * TLD];
+  const int b = blockIdx.y;
+  const QPMeta mm = meta[b];
+  if (mm.lu != LU_NOPIV || !mm.sym) return;   // workgroup-uniform
+  int I, J;
+  col_lower_tile((int)blockIdx.x, nb - 1, I, J);   // strictly lower: I − 1 ≥ J
+  ++I;
+  const int Np = nlu_np(mm);
+  const int r0 = 64 * I, c0 = 64 * J;
+  if (r0 >= Np) return;
+  const int sw = min(NB64, Np - r0);
+  const int t = threadIdx.x, j = t >> 2, kq = (t & 3) * 16;
+  double* Kb = K + (size_t)b * nmax * ld;
+  const double* ud = ukp + (size_t)b * nmax;
+  const PScale ps = pscale(kls, b, n, m, mm);
+  if (j < sw) {   // L(I, J) row j, 16 columns → X[k][j] scaled
+    const double pj = ps(r0 + j);
+    const double* src = Kb + (size_t)(r0 + j) * ld + c0 + kq;
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = src[u];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) X[(kq + u) * TLD + j] = ud[c0 + kq + u] * v[u] * pj;
+  }
+  __syncthreads();
+  const int k = t >> 2, cq = (t & 3) * 16;
+  if (cq < sw) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) Kb[(size_t)(c0 + k) * ld + r0 + cq + u] = X[k * TLD + cq + u];
+  }
+}
+
 }  // namespace
 
 // No-pivot blocked LU of every ROUTE_BLOCKED problem, by pairs of 64-column
@@ -1493,6 +1813,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 // forward-swept in place along the way (fwd_block).
 void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   qsym_join(h);   // the first diagonal launch reads the Q symmetry check
+  h.ukp_valid = false;
+  h.u_missing = false;
   const int npmax = h.blocked_npmax;
   if (npmax == 0) return;
   const int B = (int)h.batch;
@@ -1531,6 +1853,61 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   double* K = h.K.as<double>();
   int32_t* perm = h.ipiv.as<int32_t>();
   QPMeta* meta = h.meta.as<QPMeta>();
+  if (lower && h.left_mode) {
+    // P-symmetric batch: the left-looking LU, per block column J the diagonal
+    // launch and the column's tiles.  Two streams (lstreams): the tiles
+    // I ≥ J+2 of column J run on `aux` beside ldiag(J+1) (which needs only
+    // tile (J+1, J) of this column, on the main stream); the main stream
+    // joins them before the next column's first tile (it reads (J+2, J)).
+    h.binv.ensure((size_t)2 * B * BSTR * sizeof(double));
+    h.ukp.ensure((size_t)B * h.nmax * sizeof(double));
+    h.ukp_valid = true;
+    h.u_missing = true;   // U is not stored (qp_nopiv_materialize_u when a solve needs it)
+    double* ukp = h.ukp.as<double>();
+    hipStream_t S = h.stream, T = h.stream;
+    if (h.lstreams) {
+      ensure_aux(h);
+      T = h.aux;
+    }
+    auto lcol = [&](hipStream_t st, int c0, double* bv, int toff, int cnt) {
+      if (cnt <= 0) return;
+      const long long tot = (long long)cnt * B;
+      if (tot > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
+      hipLaunchKernelGGL(nlu_lcol_kernel, dim3((unsigned)tot), dim3(256), 0, st, K, h.ld, h.nmax, meta, c0, bv, ukp,
+                         cnt, toff, (int)tot, kamax, kls, h.n, h.m, src, 0);
+      DOPT_CHECK_HIP(hipGetLastError());
+    };
+    bool pending = false;   // T holds column tiles S must wait for
+    for (int c0 = 0; c0 < npmax; c0 += NB64) {
+      double* bv = h.binv.as<double>() + (size_t)((c0 / NB64) & 1) * B * BSTR;
+      hipLaunchKernelGGL(nlu_ldiag_kernel, dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv, dstride, meta,
+                         c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src);
+      DOPT_CHECK_HIP(hipGetLastError());
+      const int ntile = (npmax - c0 - NB64 + 63) / 64;
+      if (ntile <= 0) break;
+      if (T == S) {
+        lcol(S, c0, bv, 0, ntile);
+        continue;
+      }
+      if (pending) {   // column J−1's tiles I ≥ J+1 (tile (J+1, J−1) feeds this column)
+        DOPT_CHECK_HIP(hipEventRecord(h.ev_join, T));
+        DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_join, 0));
+        pending = false;
+      }
+      DOPT_CHECK_HIP(hipEventRecord(h.ev_fork, S));   // T: after ldiag(J) (and, in S order, all before it)
+      DOPT_CHECK_HIP(hipStreamWaitEvent(T, h.ev_fork, 0));
+      lcol(S, c0, bv, 0, 1);
+      if (ntile > 1) {
+        lcol(T, c0, bv, 1, ntile - 1);
+        pending = true;
+      }
+    }
+    if (pending) {
+      DOPT_CHECK_HIP(hipEventRecord(h.ev_join, T));
+      DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_join, 0));
+    }
+    return;
+  }
   // the packed inverse of step c lives in binv buffer (c / 64) & 1: a diagonal
   // launch may then run while the previous step's cross tiles still read theirs
   h.binv.ensure((size_t)2 * B * BSTR * sizeof(double));
@@ -1631,6 +2008,17 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
     DOPT_CHECK_HIP(hipEventRecord(h.ev_crit, S));
     DOPT_CHECK_HIP(hipStreamWaitEvent(h.stream, h.ev_crit, 0));
   }
+}
+
+void qp_nopiv_materialize_u(Handle& h) {
+  if (!h.u_missing) return;
+  h.u_missing = false;
+  const int nb = (h.blocked_npmax + 63) / 64;
+  if (nb < 2) return;
+  hipLaunchKernelGGL(nlu_sym_u_kernel, dim3((unsigned)(nb * (nb - 1) / 2), (unsigned)h.batch), dim3(256), 0, h.stream,
+                     h.K.as<double>(), h.ld, h.nmax, h.meta.as<QPMeta>(), h.ukp.as<double>(), h.kls.as<double>(), h.n,
+                     h.m, nb);
+  DOPT_CHECK_HIP(hipGetLastError());
 }
 
 }  // namespace dopt
