@@ -616,6 +616,81 @@ __device__ __forceinline__ void solve_cols_body(int b, const double* __restrict_
   }
 }
 
+// Both backward sweeps of a P-symmetric no-pivot factor of the fused call in
+// one workgroup and one pass over L: reverse Lᵀ (P x) = y ./ (u/p), forward
+// Lᵀ x = z (y, z: the forward-swept right-hand sides w_rev / w_fwd; perm is
+// the identity).  Each column slice of L is read once for both vectors.
+template <int ENT>
+__device__ __forceinline__ void solve_sym2_body(int b, const double* __restrict__ K, int ld, int nmax,
+                                                const double* __restrict__ dinv, size_t dstride,
+                                                const QPMeta& mm, const double* __restrict__ w_rev,
+                                                const double* __restrict__ w_fwd, double* __restrict__ x_rev,
+                                                double* __restrict__ x_fwd, double* v, double* y, double* part,
+                                                double* part2, const SymSweep& sym) {
+  const int Np = blocked_np(mm), N = mm.nsys;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const double* Kb = K + (size_t)b * nmax * ld;
+  const double* Dbase = dinv + (size_t)b * dstride;
+  const double* udb = sym.ukp + (size_t)b * nmax;
+  const PScale psc{sym.kls + (size_t)b * sym.m, sym.n, mm.nk};
+  const double* rb = w_rev + (size_t)b * nmax;
+  const double* fb = w_fwd + (size_t)b * nmax;
+  for (int i = t; i < Np; i += PT) {
+    v[i] = i < N ? rb[i] / udb[i] : 0.0;
+    y[i] = i < N ? fb[i] : 0.0;
+  }
+  __syncthreads();
+  const int nblk = Np / BNB;
+  for (int s = 0; s < nblk; ++s) {
+    const int bk = nblk - 1 - s;
+    const int i0 = bk * BNB;
+    double f[ENT][BNB];
+    int ev[ENT];
+    bool has[ENT];
+#pragma unroll
+    for (int q = 0; q < ENT; ++q) {   // column e < i0 of the slice L[i0 .. i0+31][·]
+      const int e = t + PT * q;
+      has[q] = e < i0;
+      ev[q] = e;
+      const int ec = has[q] ? e : i0;
+      if (!__any(has[q])) continue;
+#pragma unroll
+      for (int j = 0; j < BNB; ++j) f[q][j] = Kb[(size_t)(i0 + j) * ld + ec];
+    }
+    if (wv < 2 && lane < BNB) {   // wave 0: L_kk⁻ᵀ v_k, wave 1: L_kk⁻ᵀ y_k
+      const double* Dk = Dbase + (size_t)bk * BDINV;   // L⁻¹ of the 32-block
+      const double* vv = wv ? y : v;
+      double acc = 0.0;
+#pragma unroll 8
+      for (int j = 0; j < BNB; ++j) acc = fma(Dk[lane + j * BNB], vv[i0 + j], acc);
+      (wv ? part2 : part)[lane] = acc;
+    }
+    __syncthreads();
+    if (wv == 0 && lane < BNB) v[i0 + lane] = part[lane];
+    if (wv == 1 && lane < BNB) y[i0 + lane] = part2[lane];
+#pragma unroll
+    for (int q = 0; q < ENT; ++q) {
+      if (has[q]) {
+        double a1 = v[ev[q]], a2 = y[ev[q]];
+#pragma unroll
+        for (int j = 0; j < BNB; ++j) {
+          a1 = fma(-f[q][j], part[j], a1);
+          a2 = fma(-f[q][j], part2[j], a2);
+        }
+        v[ev[q]] = a1;
+        y[ev[q]] = a2;
+      }
+    }
+    __syncthreads();
+  }
+  double* xr = x_rev + (size_t)b * nmax;
+  double* xf = x_fwd + (size_t)b * nmax;
+  for (int i = t; i < N; i += PT) {
+    xr[i] = v[i] / psc(i);
+    xf[i] = y[i];
+  }
+}
+
 template <int ENT, bool TALL = false>
 __global__ __launch_bounds__(PT) void blu_solve_kernel(const double* __restrict__ K, int ld, int nmax,
                                                        const int32_t* __restrict__ perm,
@@ -757,17 +832,31 @@ __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict
                                                         const double* __restrict__ w_rev,
                                                         const double* __restrict__ w_fwd, SymSweep sym) {
   SOLVE_LDS(TALL);
+  __shared__ double part2[BNB];
   int L = blockIdx.x;
   if (B % 8 == 0) {   // workgroups 16g+j (rows) and 16g+8+j (columns) solve problem 8g+j
     const int g = L >> 4, j = L & 7;
     L = (L & 8) ? B + 8 * g + j : 8 * g + j;
   }
   const int pb = L < B ? L : L - B;
-  const bool swept = w_rev && meta[pb].lu == LU_NOPIV;
-  if (L < B && swept && sym.ukp && meta[pb].sym)   // both directions sweep Lᵀ: U is not read
-    solve_cols_body<ENT, TALL>(L, K, ld, nmax, perm, dinv, dstride, meta, 1, sel, w_rev, x_rev, v, y, ps, part, 1,
-                               &sym);
-  else if (L < B)
+  const QPMeta mm = meta[pb];
+  const bool swept = w_rev && mm.lu == LU_NOPIV;
+  if (swept && sym.ukp && mm.sym && ((sel >> mm.lu) & 1) && blocked_np(mm) > 0) {
+    // P-symmetric factor: both directions sweep Lᵀ (U is not stored)
+    if constexpr (!TALL) {
+      if (L < B)   // one pass over L for both vectors; the forward workgroup has nothing to do
+        solve_sym2_body<ENT>(pb, K, ld, nmax, dinv, dstride, mm, w_rev, w_fwd, x_rev, x_fwd, v, y, part, part2, sym);
+    } else {
+      if (L < B)
+        solve_cols_body<ENT, TALL>(L, K, ld, nmax, perm, dinv, dstride, meta, 1, sel, w_rev, x_rev, v, y, ps, part, 1,
+                                   &sym);
+      else
+        solve_cols_body<ENT, TALL>(L - B, K, ld, nmax, perm, dinv, dstride, meta, 1, sel, w_fwd, x_fwd, v, y, ps, part,
+                                   1);
+    }
+    return;
+  }
+  if (L < B)
     solve_rows_body(L, K, ld, nmax, perm, dinv, dstride, meta, sel, swept ? w_rev : rhs_rev, x_rev, v, ps, part,
                     swept ? 1 : 0);
   else
