@@ -201,16 +201,17 @@ def run_nlp(args, world, rank, local_rank):
         elapsed = float(tt.item())
     corr = eng.corrections()
     kinds = eng.lu_kind()
+    sizes = eng.system_size().astype(np.float64)   # R (n + c) on the reduced route, M's rows on the full one
     if rank == 0:
         ms_tot, cnt = phases[name]   # live, over the timed region
         avg_s = ms_tot / cnt / 1e3
         if name in ("qp_lu", "qp_lu_pivot"):
-            work = B * 2.0 / 3.0 * rows ** 3
+            work = float((2.0 / 3.0 * sizes ** 3).sum())   # the general (non-symmetric) LU of each factorised system
             achieved = work / avg_s / 1e12
             roof = dict(bound="mfma", achieved=round(achieved, 3), peak=PEAK_FP64_TFLOPS, unit="TFLOP/s",
                         frac=round(achieved / PEAK_FP64_TFLOPS, 4))
         else:
-            work = B * 8.0 * rows * rows   # one read of the factors
+            work = float((8.0 * sizes * sizes).sum())   # one read of the factors
             achieved = work / avg_s / 1e9
             roof = dict(bound="hbm", achieved=round(achieved, 1), peak=PEAK_HBM_GBS, unit="GB/s",
                         frac=round(achieved / PEAK_HBM_GBS, 4))
@@ -233,6 +234,7 @@ def run_nlp(args, world, rank, local_rank):
             "data": "synthetic (seeded strictly complementary NLP KKT point, diffopt_amd.synthetic.nlp_numpy)",
             "config": {"workload": "config 6: NLP KKT batch (sIpopt system + inertia correction), fwd+rev",
                        "problems_per_gpu": B, "n": n, "constraints": c, "params": P, "kkt_rows": rows,
+                       "factorised_size_mean": round(float(sizes.mean()), 1),
                        "inertia_corrections": int((corr != 0).sum()),
                        "factorisation": {"no_pivot": int((kinds == 1).sum()),
                                          "partial_pivoting": int((kinds == 2).sum())},

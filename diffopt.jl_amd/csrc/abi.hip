@@ -120,6 +120,7 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
     if (const char* e = getenv("DOPT_PRIO")) h->prio_mode = atoi(e) != 0;
     if (const char* e = getenv("DOPT_LEFT")) h->left_mode = atoi(e) != 0;
     if (const char* e = getenv("DOPT_LSTREAMS")) h->lstreams = atoi(e) != 0;
+    if (const char* e = getenv("DOPT_NLP_REDUCE")) h->nlp_reduce = atoi(e) != 0;
     if (kind == DOPT_KIND_QP) {
       // largest supported system: the generic solve stages an nmax vector in
       // LDS (64 KB); the blocked route takes reduced systems up to BLOCKED_MAX
@@ -170,7 +171,7 @@ int dopt_destroy(dopt_handle* h) {
   DevBuf* bufs[] = {&h->dinv, &h->plist, &h->lsqr_ws, &h->binv, &h->fwdw, &h->K, &h->ipiv, &h->s, &h->kidx, &h->meta, &h->rhs,
                     &h->x, &h->cone_dev, &h->vp, &h->dpi, &h->cwork, &h->cinfo, &h->cnorm, &h->csplit, &h->krhs, &h->kx,
                     &h->kfull, &h->kamax, &h->nlp_map, &h->nlp_shift, &h->nlp_scale, &h->kls, &h->gk, &h->glist,
-                    &h->mws, &h->qsy, &h->psd_eig, &h->psd_app, &h->ukp};
+                    &h->mws, &h->qsy, &h->psd_eig, &h->psd_app, &h->ukp, &h->nlp_rd, &h->nlp_ri, &h->nlp_t1, &h->nlp_t2};
   for (auto* b : bufs) b->release();
   for (auto& b : h->own_nin) b.release();
   for (auto& b : h->own_in) b.release();
@@ -781,7 +782,8 @@ int dopt_get_iterative(dopt_handle* h, int8_t* flags) {
 int dopt_get_system_size(dopt_handle* h, int32_t* sizes) {
   return guarded(h, [&]() {
     if (!sizes) throw Error(-1, "sizes is required");
-    if (h->kind == DOPT_KIND_QP) {
+    if (h->kind == DOPT_KIND_QP || h->kind == DOPT_KIND_NLP) {
+      if (h->kind == DOPT_KIND_NLP && !h->nfactored) throw Error(-1, "no NLP factorisation has run");
       std::vector<dopt::QPMeta> meta(h->batch);
       DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h->meta.p, h->batch * sizeof(dopt::QPMeta),
                                     hipMemcpyDeviceToHost, h->stream));

@@ -196,6 +196,13 @@ struct Handle {
   DevBuf nlp_shift;                // per problem: inertia corrections applied (int32); −1: failed
   DevBuf nlp_scale;                // per problem × assembly row block: max |M| (the pivot test's scale)
   std::vector<int32_t> nlp_corr;   // host copy of nlp_shift after the factorisation
+  // reduced KKT route (nlp.hip, structured mode): the bound and slack rows
+  // eliminated exactly, R = [H + diag(δ), Jᵀ; J, −diag(ρ)] over [x; y] factorised
+  // instead of M; env DOPT_NLP_REDUCE=0 keeps the full sIpopt M
+  int32_t nlp_reduce = 1;
+  DevBuf nlp_rd;                   // per problem: δ (num_w), ρ (c) doubles
+  DevBuf nlp_ri;                   // per problem: active bound of each w index (num_w), row state (c); then B ok flags
+  DevBuf nlp_t1, nlp_t2;           // reduced right-hand sides / solutions (max(2, P) × B × nmax)
   bool nstruct = false, nset = false, nfactored = false;
 
   // scratch for host-mode tangents / outputs

@@ -74,17 +74,133 @@ __device__ __forceinline__ double nlp_VU(const NLPDims& d, const NLPMap& mp, con
   return v * (-d.sense);
 }
 
+// ---------------------------------------------------------------------------
+// Reduced KKT route (structured mode).  The bound rows and the slacks are
+// eliminated exactly (tests/test_nlp_reduce_cpu.py restates the algebra and
+// checks it against the full solves with M and Mᵀ):
+//   bound row i on w_j, a·z_j + d·z_ν = r (row j carries b·z_ν):
+//     M: (a, b) = (V, ∓1), Mᵀ: (a, b) = (∓1, V);
+//     d ≠ 0: z_ν eliminated, row j gains δ_j = −a·b/d (the same for M and Mᵀ),
+//            r_j −= b·r/d;
+//     d = 0: z_j = r/a is known (a = 0, or two active bounds on one variable:
+//            the problem keeps the full M);
+//   slack t of row k (W is zero there): known → row k reads J_k x = r_k + z_t;
+//     else row t reads δ_t z_t − y_k = r̃_t: δ_t = 0 → y_k = −r̃_t known;
+//     δ_t ≠ 0 → row k reads J_k x − ρ_k y_k = r_k + ρ_k r̃_t (ρ_k = 1/δ_t).
+// R = [H + diag(δ_x), Jᵀ; J, −diag(ρ)] over [x; y], the known unknowns as
+// identity rows / columns, n + c rows whatever the active set — the same
+// matrix for both directions (Rᵀ for Mᵀ).  det M = ±Π(pivots)·det R, so M is
+// singular exactly when R is (or a = 0 above): the singularity verdict and
+// the inertia correction (on the full M) keep the reference's semantics.
+// ---------------------------------------------------------------------------
+struct NLPRed {
+  int on;
+  double* delta;   // B × num_w
+  double* rho;     // B × c
+  int32_t* kx;     // B × num_w: the active bound of w_j (lower i → i, upper i → nlo + i), −1 none
+  int32_t* yst;    // B × c: 0 kept, 1 y_k known, 2 regularised (ρ)
+  int32_t* ok;     // B: 1 when the reduction applies
+};
+
+__device__ __forceinline__ bool red_use(const NLPRed& R, const int32_t* shift, int b) {
+  return R.on && R.ok[b] && shift[b] == 0;
+}
+
+// R[r][col] of problem b (identity padding past n + c)
+__device__ __forceinline__ double nlp_R(const NLPDims& d, const NLPIn& in, const NLPRed& R, size_t b, int r,
+                                        int col) {
+  const int n = d.n, N = n + d.c;
+  if (r >= N || col >= N) return r == col ? 1.0 : 0.0;
+  const int32_t* kx = R.kx + b * d.num_w;
+  const int32_t* ys = R.yst + b * d.c;
+  if (r < n) {
+    if (kx[r] >= 0) return r == col ? 1.0 : 0.0;
+    if (col < n) {
+      if (kx[col] >= 0) return 0.0;
+      double v = in.Hxx[b * n * n + (size_t)col * n + r];
+      if (col == r) v += R.delta[b * d.num_w + r];
+      return v;
+    }
+    const int k = col - n;
+    return ys[k] == 1 ? 0.0 : in.Jx[b * d.c * n + (size_t)r * d.c + k];
+  }
+  const int k = r - n;
+  if (ys[k] == 1) return r == col ? 1.0 : 0.0;
+  if (col < n) return kx[col] >= 0 ? 0.0 : in.Jx[b * d.c * n + (size_t)col * d.c + k];
+  if (col != r) return 0.0;
+  return ys[k] == 2 ? -R.rho[b * d.c + k] : 0.0;
+}
+
+// Per problem: δ, the active bounds, the constraint rows' states, and whether
+// the reduction applies (one workgroup per problem)
+__global__ __launch_bounds__(NT) void nlp_red_prep_kernel(NLPDims d, NLPMap mp, NLPIn in, NLPRed R) {
+  __shared__ int bad;
+  const size_t b = blockIdx.x;
+  const int t = threadIdx.x;
+  double* delta = R.delta + b * d.num_w;
+  int32_t* kx = R.kx + b * d.num_w;
+  if (t == 0) bad = 0;
+  for (int j = t; j < d.num_w; j += NT) {
+    delta[j] = 0.0;
+    kx[j] = -1;
+  }
+  __syncthreads();
+  // lower bounds (at most one per w index): a = V, b = −1
+  for (int i = t; i < d.nlo; i += NT) {
+    const int j = mp.low_idx[i];
+    const double xl = j < d.n ? in.xl[b * d.n + j] : 0.0;
+    const double dd = nlp_X(d, mp, in, b, j) - xl, V = nlp_VL(d, mp, in, b, j);
+    if (!isfinite(dd) || !isfinite(V)) bad = 1;
+    else if (dd != 0.0) delta[j] += V / dd;
+    else if (V == 0.0) bad = 1;
+    else kx[j] = i;
+  }
+  __syncthreads();
+  // upper bounds: a = V, b = +1
+  for (int i = t; i < d.nup; i += NT) {
+    const int j = mp.up_idx[i];
+    const double xu = j < d.n ? in.xu[b * d.n + j] : 0.0;
+    const double dd = xu - nlp_X(d, mp, in, b, j), V = nlp_VU(d, mp, in, b, j);
+    if (!isfinite(dd) || !isfinite(V)) bad = 1;
+    else if (dd != 0.0) delta[j] -= V / dd;
+    else if (V == 0.0 || kx[j] >= 0) bad = 1;
+    else kx[j] = d.nlo + i;
+  }
+  __syncthreads();
+  for (int k = t; k < d.c; k += NT) {
+    const int s = mp.slack_of_row[k];
+    int st = 0;
+    double rho = 0.0;
+    if (s >= 0 && kx[s] < 0) {
+      const double dl = delta[s];
+      if (dl == 0.0) {
+        st = 1;
+      } else {
+        st = 2;
+        rho = 1.0 / dl;
+      }
+    }
+    R.yst[b * d.c + k] = st;
+    R.rho[b * d.c + k] = rho;
+  }
+  __syncthreads();
+  if (t == 0) R.ok[b] = bad ? 0 : 1;
+}
+
 // M (+ k·st·D) of the listed problems into K; grid (row blocks, count)
 __global__ __launch_bounds__(NT) void nlp_assemble_kernel(NLPDims d, NLPMap mp, NLPIn in, double* __restrict__ K,
                                                           int ld, int nmax, QPMeta* __restrict__ meta,
                                                           const int32_t* __restrict__ shift,
                                                           const int32_t* __restrict__ plist,
-                                                          double* __restrict__ partial, double* __restrict__ kamax) {
+                                                          double* __restrict__ partial, double* __restrict__ kamax,
+                                                          NLPRed Rd) {
   __shared__ double red[NT / 64];
   double amax = 0.0;
   const int b = plist ? plist[blockIdx.y] : (int)blockIdx.y;
   const size_t bb = (size_t)b;
-  const int Np = (d.rows + 31) & ~31;
+  const bool reduced = red_use(Rd, shift, b);   // workgroup-uniform
+  const int rows = reduced ? d.n + d.c : d.rows;
+  const int Np = (rows + 31) & ~31;
   const int kc = max(shift[b], 0);
   const int lo0 = d.num_w + d.c, up0 = lo0 + d.nlo;
   double* Kb = K + bb * nmax * ld;
@@ -94,7 +210,9 @@ __global__ __launch_bounds__(NT) void nlp_assemble_kernel(NLPDims d, NLPMap mp, 
     const double dshift = kc * NLP_ST * ((r >= d.num_w && r < d.num_w + d.c) ? -1.0 : 1.0);
     for (int col = threadIdx.x; col < Np; col += NT) {
       double v = 0.0;
-      if (r >= d.rows || col >= d.rows) {
+      if (reduced) {
+        v = nlp_R(d, in, Rd, bb, r, col);
+      } else if (r >= d.rows || col >= d.rows) {
         v = r == col ? 1.0 : 0.0;   // identity padding
       } else if (d.kkt) {
         v = in.Hxx[bb * d.rows * d.rows + (size_t)col * d.rows + r];
@@ -132,8 +250,8 @@ __global__ __launch_bounds__(NT) void nlp_assemble_kernel(NLPDims d, NLPMap mp, 
           v = xu - nlp_X(d, mp, in, bb, j);
         }
       }
-      if (col == r && r < d.rows) v += dshift;
-      if (r < d.rows && col < d.rows) amax = fmax(amax, fabs(v));
+      if (col == r && r < d.rows && !reduced) v += dshift;
+      if (r < rows && col < rows) amax = fmax(amax, fabs(v));
       Kb[(size_t)r * ld + col] = v;
     }
   }
@@ -151,7 +269,7 @@ __global__ __launch_bounds__(NT) void nlp_assemble_kernel(NLPDims d, NLPMap mp, 
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     QPMeta mm = {};
-    mm.nsys = d.rows;
+    mm.nsys = rows;
     mm.lu = LU_NONE;
     meta[b] = mm;
   }
@@ -185,6 +303,7 @@ __global__ __launch_bounds__(NT) void nlp_pivot_check_kernel(const double* __res
   if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = sc;
   __syncthreads();
   sc = fmax(fmax(sred[0], sred[1]), fmax(sred[2], sred[3]));
+  rows = mm.nsys;   // the factorised system: M, or R on the reduced route
   const double tol = rows * 2.220446049250313e-16 * sc;
   const double* Kb = K + (size_t)b * nmax * ld;
   const int32_t* pb = perm + (size_t)b * nmax;
@@ -317,6 +436,167 @@ __global__ __launch_bounds__(NT) void nlp_jac_out_kernel(NLPDims d, const double
   }
 }
 
+// The reduced route's right-hand sides: the full one r (rows of M, stride
+// nmax) → R's (n + c), per direction (trans: Mᵀ); full-route problems copy r.
+// Grid (B, k): right-hand side j of problem b at (j·B + b)·nmax.
+// Dynamic LDS: rr (num_w), known z (num_w), known y (c).
+__device__ __forceinline__ void red_rr(const NLPDims& d, const NLPMap& mp, const NLPIn& in, size_t b, int trans,
+                                       const double* r, double* rr, double* zk) {
+  const int lo0 = d.num_w + d.c, up0 = lo0 + d.nlo;
+  for (int j = threadIdx.x; j < d.num_w; j += NT) {
+    double rj = r[j], z = 0.0;
+    const int lp = mp.lowpos[j], up = mp.uppos[j];
+    if (lp >= 0) {
+      const double xl = j < d.n ? in.xl[b * d.n + j] : 0.0;
+      const double dd = nlp_X(d, mp, in, b, j) - xl, V = nlp_VL(d, mp, in, b, j);
+      const double a = trans ? -1.0 : V, bc = trans ? V : -1.0;
+      if (dd != 0.0) rj -= bc * r[lo0 + lp] / dd;
+      else z = r[lo0 + lp] / a;
+    }
+    if (up >= 0) {
+      const double xu = j < d.n ? in.xu[b * d.n + j] : 0.0;
+      const double dd = xu - nlp_X(d, mp, in, b, j), V = nlp_VU(d, mp, in, b, j);
+      const double a = trans ? 1.0 : V, bc = trans ? V : 1.0;
+      if (dd != 0.0) rj -= bc * r[up0 + up] / dd;
+      else z = r[up0 + up] / a;
+    }
+    rr[j] = rj;
+    zk[j] = z;
+  }
+}
+
+__global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, NLPIn in, NLPRed Rd,
+                                                         const int32_t* __restrict__ shift, int trans,
+                                                         const double* __restrict__ rfull,
+                                                         double* __restrict__ rred, int nmax) {
+  extern __shared__ double sm[];
+  const size_t b = blockIdx.x, off = ((size_t)blockIdx.y * gridDim.x + b) * nmax;
+  const double* r = rfull + off;
+  double* o = rred + off;
+  const int t = threadIdx.x;
+  if (!red_use(Rd, shift, (int)b)) {
+    for (int i = t; i < nmax; i += NT) o[i] = r[i];
+    return;
+  }
+  const int n = d.n, c = d.c, w = d.num_w, N = n + c;
+  double *rr = sm, *zk = sm + w, *yv = sm + 2 * w;
+  const int32_t* kx = Rd.kx + b * w;
+  const int32_t* ys = Rd.yst + b * c;
+  const double* rho = Rd.rho + b * c;
+  red_rr(d, mp, in, b, trans, r, rr, zk);
+  __syncthreads();
+  for (int k = t; k < c; k += NT) yv[k] = ys[k] == 1 ? -rr[mp.slack_of_row[k]] : 0.0;
+  __syncthreads();
+  const double* H = in.Hxx + b * n * n;
+  const double* J = in.Jx + b * c * n;
+  for (int i = t; i < nmax; i += NT) {
+    double v = 0.0;
+    if (i < n) {
+      if (kx[i] >= 0) {
+        v = zk[i];
+      } else {
+        v = rr[i];
+        for (int j = 0; j < n; ++j)   // known x (W, or Wᵀ for Mᵀ)
+          if (kx[j] >= 0) v -= (trans ? H[(size_t)i * n + j] : H[(size_t)j * n + i]) * zk[j];
+        for (int k = 0; k < c; ++k)
+          if (ys[k] == 1) v -= J[(size_t)i * c + k] * yv[k];
+      }
+    } else if (i < N) {
+      const int k = i - n;
+      if (ys[k] == 1) {
+        v = yv[k];
+      } else {
+        v = r[w + k];
+        const int s = mp.slack_of_row[k];
+        if (s >= 0 && kx[s] >= 0) v += zk[s];
+        if (ys[k] == 2) v += rho[k] * rr[s];
+        for (int j = 0; j < n; ++j)
+          if (kx[j] >= 0) v -= J[(size_t)j * c + k] * zk[j];
+      }
+    }
+    o[i] = v;
+  }
+}
+
+// The reduced route's solution of R (x, stride nmax) → the full one of M /
+// Mᵀ (rows); full-route problems copy.  Grid (B, k) as above.  Dynamic LDS:
+// rr (num_w), known z (num_w), z over w (num_w).
+__global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap mp, NLPIn in, NLPRed Rd,
+                                                             const int32_t* __restrict__ shift, int trans,
+                                                             const double* __restrict__ rfull,
+                                                             const double* __restrict__ xred,
+                                                             double* __restrict__ zfull, int nmax) {
+  extern __shared__ double sm[];
+  const size_t b = blockIdx.x, off = ((size_t)blockIdx.y * gridDim.x + b) * nmax;
+  const double* r = rfull + off;
+  const double* xr = xred + off;
+  double* z = zfull + off;
+  const int t = threadIdx.x;
+  if (!red_use(Rd, shift, (int)b)) {
+    for (int i = t; i < nmax; i += NT) z[i] = xr[i];
+    return;
+  }
+  const int n = d.n, c = d.c, w = d.num_w;
+  double *rr = sm, *zk = sm + w, *zw = sm + 2 * w;
+  const int32_t* kx = Rd.kx + b * w;
+  const int32_t* ys = Rd.yst + b * c;
+  const double* rho = Rd.rho + b * c;
+  const double* dl = Rd.delta + b * w;
+  const double* H = in.Hxx + b * n * n;
+  const double* J = in.Jx + b * c * n;
+  red_rr(d, mp, in, b, trans, r, rr, zk);
+  for (int i = t; i < n; i += NT) zw[i] = xr[i];
+  for (int k = t; k < c; k += NT) z[w + k] = xr[n + k];
+  __syncthreads();
+  for (int s = n + t; s < w; s += NT) {   // slacks
+    const int k = mp.row_of_slack[s - n];
+    double v;
+    if (kx[s] >= 0) {
+      v = zk[s];
+    } else if (ys[k] == 1) {
+      v = -r[w + k];
+      for (int j = 0; j < n; ++j) v += J[(size_t)j * c + k] * zw[j];
+    } else {
+      v = (rr[s] + xr[n + k]) * rho[k];
+    }
+    zw[s] = v;
+  }
+  __syncthreads();
+  for (int j = t; j < w; j += NT) z[j] = zw[j];
+  // the bound rows' unknowns
+  const int lo0 = w + c, up0 = lo0 + d.nlo;
+  for (int q = t; q < d.nlo + d.nup; q += NT) {
+    const bool low = q < d.nlo;
+    const int i = low ? q : q - d.nlo;
+    const int j = low ? mp.low_idx[i] : mp.up_idx[i];
+    const int row = low ? lo0 + i : up0 + i;
+    double dd, V;
+    if (low) {
+      const double xl = j < n ? in.xl[b * n + j] : 0.0;
+      dd = nlp_X(d, mp, in, b, j) - xl;
+      V = nlp_VL(d, mp, in, b, j);
+    } else {
+      const double xu = j < n ? in.xu[b * n + j] : 0.0;
+      dd = xu - nlp_X(d, mp, in, b, j);
+      V = nlp_VU(d, mp, in, b, j);
+    }
+    const double cf = low ? -1.0 : 1.0;
+    const double a = trans ? cf : V, bc = trans ? V : cf;
+    double v;
+    if (dd != 0.0) {
+      v = (r[row] - a * zw[j]) / dd;
+    } else if (j < n) {   // row j: (W x)_j + δ_j x_j + (Jᵀ y)_j + b·z_ν = r̃_j
+      double acc = rr[j] - dl[j] * zw[j];
+      for (int jj = 0; jj < n; ++jj) acc -= (trans ? H[(size_t)j * n + jj] : H[(size_t)jj * n + j]) * zw[jj];
+      for (int k = 0; k < c; ++k) acc -= J[(size_t)j * c + k] * xr[n + k];
+      v = acc / bc;
+    } else {              // slack row: −y_k + b·z_ν = r̃_t
+      v = (rr[j] + xr[n + mp.row_of_slack[j - n]]) / bc;
+    }
+    z[row] = v;
+  }
+}
+
 NLPDims dims(const Handle& h) {
   NLPDims d;
   d.n = h.n;
@@ -359,12 +639,53 @@ NLPIn inputs(const Handle& h) {
 
 int row_blocks(const Handle& h) { return (((h.nlp_rows + 31) & ~31) + ROWS_PER_WG - 1) / ROWS_PER_WG; }
 
+// the reduced route's per-problem data (on: structured mode and nlp_reduce)
+NLPRed red_of(Handle& h) {
+  NLPRed R{};
+  R.on = (!h.nlp_kkt && h.nlp_reduce) ? 1 : 0;
+  if (!R.on) return R;
+  const size_t B = h.batch, w = h.nlp_num_w, c = h.m;
+  h.nlp_rd.ensure(std::max<size_t>(B * (w + c), 1) * sizeof(double));
+  h.nlp_ri.ensure((B * (w + c) + B) * sizeof(int32_t));
+  R.delta = h.nlp_rd.as<double>();
+  R.rho = R.delta + B * w;
+  R.kx = h.nlp_ri.as<int32_t>();
+  R.yst = R.kx + B * w;
+  R.ok = R.yst + B * c;
+  return R;
+}
+
 void assemble(Handle& h, const int32_t* plist, int count) {
   if (count == 0) return;
   hipLaunchKernelGGL(nlp_assemble_kernel, dim3(row_blocks(h), count), dim3(NT), 0, h.stream, dims(h), map_of(h),
                      inputs(h), h.K.as<double>(), h.ld, h.nmax, h.meta.as<QPMeta>(), h.nlp_shift.as<int32_t>(),
-                     plist, h.nlp_scale.as<double>(), h.kamax.as<double>());
+                     plist, h.nlp_scale.as<double>(), h.kamax.as<double>(), red_of(h));
   DOPT_CHECK_HIP(hipGetLastError());
+}
+
+// full right-hand sides (k per problem) → the system each problem factorised
+void red_rhs(Handle& h, int trans, int k, const double* rfull, double* rred) {
+  const size_t lds = (size_t)(2 * h.nlp_num_w + h.m) * sizeof(double);
+  hipLaunchKernelGGL(nlp_red_rhs_kernel, dim3((unsigned)h.batch, (unsigned)k), dim3(NT), lds, h.stream, dims(h),
+                     map_of(h), inputs(h), red_of(h), h.nlp_shift.as<int32_t>(), trans, rfull, rred, h.nmax);
+  DOPT_CHECK_HIP(hipGetLastError());
+}
+void red_recover(Handle& h, int trans, int k, const double* rfull, const double* xred, double* zfull) {
+  const size_t lds = (size_t)3 * h.nlp_num_w * sizeof(double);
+  hipLaunchKernelGGL(nlp_red_recover_kernel, dim3((unsigned)h.batch, (unsigned)k), dim3(NT), lds, h.stream,
+                     dims(h), map_of(h), inputs(h), red_of(h), h.nlp_shift.as<int32_t>(), trans, rfull, xred, zfull,
+                     h.nmax);
+  DOPT_CHECK_HIP(hipGetLastError());
+}
+bool reduced_on(const Handle& h) { return !h.nlp_kkt && h.nlp_reduce; }
+// reduced right-hand sides / solutions for k per problem
+double* red_t1(Handle& h, int k) {
+  h.nlp_t1.ensure((size_t)k * h.batch * h.nmax * sizeof(double));
+  return h.nlp_t1.as<double>();
+}
+double* red_t2(Handle& h, int k) {
+  h.nlp_t2.ensure((size_t)k * h.batch * h.nmax * sizeof(double));
+  return h.nlp_t2.as<double>();
 }
 
 void pivot_check(Handle& h, const int32_t* plist, int count) {
@@ -420,6 +741,9 @@ void nlp_factor(Handle& h) {
   DOPT_CHECK_HIP(hipMemsetAsync(h.kamax.p, 0, (size_t)B * sizeof(double), h.stream));
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
+    if (reduced_on(h))
+      hipLaunchKernelGGL(nlp_red_prep_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), map_of(h), inputs(h),
+                         red_of(h));
     assemble(h, nullptr, B);
   }
   h.blocked_npmax = h.nmax;
@@ -427,10 +751,12 @@ void nlp_factor(Handle& h) {
   // (slacks are absent from the Hessian) and at the dual rows: the no-pivot
   // LU's threshold test rejects every problem with a slack or bound row
   // (measured: config 6, all 1024 rejected, 3.5 ms of 16.2 ms per step
-  // wasted), so such systems go straight to partial pivoting.
+  // wasted), so such systems go straight to partial pivoting — unless they
+  // take the reduced route (R has no such rows; a problem kept on the full M
+  // there is rejected by the no-pivot LU and re-factorised with pivoting).
   const bool saddle_only = !h.nlp_kkt && h.nlp_ng + h.nlp_nl + h.nlp_nlo + h.nlp_nup == 0;
   const int32_t lu_mode = h.lu_mode;
-  if (!saddle_only) h.lu_mode = 0;
+  if (!saddle_only && !reduced_on(h)) h.lu_mode = 0;
   try {
     factor_dense(h, [&h](const int32_t* pl, int count) { assemble(h, pl, count); });
   } catch (...) {
@@ -475,15 +801,18 @@ void nlp_forward(Handle& h, const double* dp, double* dx, double* ddual) {
   const int B = (int)h.batch;
   double* rhs = h.rhs.as<double>();
   double* x = h.x.as<double>();
+  const bool red = reduced_on(h);
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
     hipLaunchKernelGGL(nlp_fwd_rhs_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), inputs(h), dp, h.nmax, rhs);
     DOPT_CHECK_HIP(hipGetLastError());
+    if (red) red_rhs(h, 0, 1, rhs, red_t1(h, 1));
   }
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
-    qp_blocked_solve(h, dense_dinv(h), 0, rhs, x, LU_SEL_ALL);
+    qp_blocked_solve(h, dense_dinv(h), 0, red ? red_t1(h, 1) : rhs, red ? red_t2(h, 1) : x, LU_SEL_ALL);
   }
+  if (red) red_recover(h, 0, 1, rhs, red_t2(h, 1), x);
   PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
   hipLaunchKernelGGL(nlp_fwd_out_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), x, h.nmax,
                      h.nlp_shift.as<int32_t>(), dx, ddual);
@@ -496,15 +825,18 @@ void nlp_reverse(Handle& h, const double* dx, const double* ddual, double* dp) {
   const int B = (int)h.batch;
   double* rhs = h.rhs.as<double>() + (size_t)B * h.nmax;
   double* u = h.x.as<double>() + (size_t)B * h.nmax;
+  const bool red = reduced_on(h);
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
     hipLaunchKernelGGL(nlp_rev_rhs_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), dx, ddual, h.nmax, rhs);
     DOPT_CHECK_HIP(hipGetLastError());
+    if (red) red_rhs(h, 1, 1, rhs, red_t1(h, 1));
   }
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
-    qp_blocked_solve(h, dense_dinv(h), 1, rhs, u, LU_SEL_ALL);
+    qp_blocked_solve(h, dense_dinv(h), 1, red ? red_t1(h, 1) : rhs, red ? red_t2(h, 1) : u, LU_SEL_ALL);
   }
+  if (red) red_recover(h, 1, 1, rhs, red_t2(h, 1), u);
   PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
   if (h.p)
     hipLaunchKernelGGL(nlp_rev_out_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), inputs(h), u, h.nmax,
@@ -526,16 +858,20 @@ void nlp_jacobian(Handle& h, double* ds) {
   const size_t blk = (size_t)B * h.nmax;
   h.krhs.ensure(blk * P * sizeof(double));
   h.kx.ensure(blk * P * sizeof(double));
+  const bool red = reduced_on(h);
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
     hipLaunchKernelGGL(nlp_jac_rhs_kernel, dim3(B, P), dim3(NT), 0, h.stream, dims(h), inputs(h), B, h.nmax,
                        h.krhs.as<double>());
     DOPT_CHECK_HIP(hipGetLastError());
+    if (red) red_rhs(h, 0, P, h.krhs.as<double>(), red_t1(h, P));
   }
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
-    solve_multi(h, 0, P, h.krhs.as<double>(), h.kx.as<double>());
+    if (red) solve_multi(h, 0, P, red_t1(h, P), red_t2(h, P));
+    else solve_multi(h, 0, P, h.krhs.as<double>(), h.kx.as<double>());
   }
+  if (red) red_recover(h, 0, P, h.krhs.as<double>(), red_t2(h, P), h.kx.as<double>());
   PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
   hipLaunchKernelGGL(nlp_jac_out_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), h.kx.as<double>(), B, h.nmax,
                      h.nlp_shift.as<int32_t>(), ds);

@@ -128,6 +128,14 @@ class NLPBatch:
         lay = self.layout()
         return self.c + lay["nlow_primal"] + lay["nup_primal"]
 
+    def system_size(self):
+        """Per-problem size of the factorised system: n + c on the reduced
+        route (bounds and slacks eliminated exactly), the rows of M on the
+        full one (inertia corrections, degenerate bounds, DOPT_NLP_REDUCE=0)."""
+        buf = np.zeros(self.batch, dtype=np.int32)
+        _lib.check(self.lib.dopt_get_system_size(self.h, buf.ctypes.data), self.h)
+        return buf
+
     def lu_kind(self):
         """Per-problem factorisation kind (the shared blocked LU):
         _lib.LU_KIND_NOPIV / LU_KIND_PIVOT."""

@@ -337,8 +337,9 @@ int dopt_qp_get_lu_kind(dopt_handle* h, int8_t* kinds);
  * tiles only, U from L, ≈ N'³/3 flops instead of 2N'³/3), 0 otherwise.
  * Introspection for tests and the bench. */
 int dopt_qp_get_sym(dopt_handle* h, int8_t* flags);
-/* per-problem size of the factorised (reduced) KKT system (QP) or LSQR
- * iteration count of the last solve (CONIC). */
+/* per-problem size of the factorised (reduced) KKT system (QP; NLP: n + c on
+ * the reduced route, the rows of M on the full one) or LSQR iteration count
+ * of the last solve (CONIC). */
 int dopt_get_system_size(dopt_handle* h, int32_t* sizes);
 /* Per-phase GPU time, measured with HIP events on the handle's stream around
  * each phase's kernels while profiling is on (off by default). */

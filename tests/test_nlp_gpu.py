@@ -305,3 +305,57 @@ def test_argument_errors():
         e.set_structure([0, 5])
     with pytest.raises(EngineError, match="sense"):
         e.set_structure([0, 1], sense=0)
+
+
+# ---- the reduced KKT route (bounds and slacks eliminated exactly) ----------
+@pytest.mark.parametrize("sense", [1, -1])
+def test_reduced_route_sizes_and_parity(sense, monkeypatch):
+    """Every strictly complementary problem takes the reduced route (system
+    size n + c, no-pivot LU) and matches the oracle's full-M sensitivities;
+    DOPT_NLP_REDUCE=0 (the full M) gives the same outputs to 1e-9."""
+    from diffopt_amd.synthetic import nlp_numpy
+    B, n, c, P = 6, 40, 25, 5
+    st, pt, dp, dx, dd = nlp_numpy(B, n, c, P, 7100 + sense, sense=sense)
+    monkeypatch.delenv("DOPT_NLP_REDUCE", raising=False)
+    e = engine(st, pt, B)
+    assert (e.system_size() == n + c).all()
+    fx, fd, rp, J = check_against_oracle(e, st, pt, dp, dx, dd, range(B))
+    e.close()
+    monkeypatch.setenv("DOPT_NLP_REDUCE", "0")
+    f = engine(st, pt, B)
+    assert (f.system_size() == f.layout()["rows"]).all()
+    gx, gd = f.forward(dp)
+    assert relfro(np.concatenate([gx, gd], axis=1), np.concatenate([fx, fd], axis=1)) <= 1e-9
+    assert relfro(f.reverse(dx, dd), rp) <= 1e-9
+    assert relfro(f.jacobian(), J) <= 1e-9
+    f.close()
+
+
+def test_reduced_route_mixed_with_full_route():
+    """One batch mixing problems the elimination cannot take — an active bound
+    with a zero dual (M singular: the inertia correction on the full M), and a
+    primal variable pinned by both bounds — with reduced ones: the reduced
+    problems keep n + c, the others the full M, all match the oracle."""
+    from diffopt_amd.synthetic import nlp_numpy
+    B, n, c, P = 4, 30, 18, 4
+    st, pt, dp, dx, dd = nlp_numpy(B, n, c, P, 7300)
+    low = np.flatnonzero(st["has_low"])
+    both = np.flatnonzero(st["has_low"].astype(bool) & st["has_up"].astype(bool))
+    j = int(low[0])
+    pt["xl"][1, j], pt["yl"][1, j] = pt["x"][1, j], 0.0   # problem 1: active lower bound, zero dual
+    if len(both):
+        k = int(both[0])                                   # problem 2: both bounds active on k
+        pt["xl"][2, k] = pt["xu"][2, k] = pt["x"][2, k]
+        pt["yl"][2, k], pt["yu"][2, k] = 0.7, -0.4
+    e = engine(st, pt, B)
+    sizes = e.system_size()
+    rows = e.layout()["rows"]
+    assert sizes[0] == n + c and sizes[3] == n + c
+    assert sizes[1] == rows
+    if len(both):
+        assert sizes[2] == rows
+    corr = e.corrections()
+    for b in range(B):
+        assert corr[b] == oracle_problem(st, pt, b)[4]
+    check_against_oracle(e, st, pt, dp, dx, dd, range(B))
+    e.close()
