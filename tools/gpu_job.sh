@@ -43,6 +43,6 @@ case "$mode" in
         || { tail -20 gpurun_out/pmc_${tag}_$c.log; exit 1; }
     done
     python3 tools/pmc_summary.py gpurun_out/pmc_${tag}_FETCH_SIZE gpurun_out/pmc_${tag}_WRITE_SIZE \
-      gpurun_out/pmc_${tag}.json ;;
+      gpurun_out/pmc_${tag}.json ${PMC_SUFFIX:-} ;;
   *) echo "unknown mode $mode"; exit 2 ;;
 esac

@@ -11,7 +11,8 @@ per-lane streaming loads and the LU's 4-row × 128-B pattern all read as 0.500
 of the streamed bytes, 4-, 8- and 16-byte stores as 1.000 — one factor each.
 FETCH_SIZE/WRITE_SIZE are in KB (rocprofv3 derived counters) → ×1024.
 
-  python tools/pmc_summary.py <fetch_dir> <write_dir> <out.json>   (merges into out.json)
+  python tools/pmc_summary.py <fetch_dir> <write_dir> <out.json> [key_suffix]   (merges into out.json;
+         key_suffix, e.g. @cfg3, is appended to every kernel key — the keys bench.py looks up)
 """
 import csv
 import glob
@@ -36,12 +37,14 @@ KERNEL_PHASE = {
 # the per-step qp_prep_kernel dispatch
 QP_GROUPS = {"qp_assemble": ("qp_prep_kernel", "qp_asm_tile_kernel"),
              "qp_lu": ("nlu_diag_kernel", "nlu_trsm_kernel", "nlu_cross_kernel", "nlu_update2_kernel",
-                       "blu_panel_kernel", "blu_update_kernel"),
+                       "nlu_ldiag_kernel", "nlu_lcol_kernel", "blu_panel_kernel", "blu_update_kernel"),
              "qp_solve": ("blu_solve_kernel", "blu_solve_rows_kernel", "blu_solve2_kernel")}
 QP_STEP = "qp_prep_kernel"
 # NLP back-end (bench config 6): the step is counted by the assembly; its LU
 # is the partial-pivoting blocked LU, its solves the blocked solve kernels
-NLP_GROUPS = {"qp_assemble": ("nlp_assemble_kernel",),
+NLP_GROUPS = {"qp_assemble": ("nlp_assemble_kernel", "nlp_red_prep_kernel"),
+              "qp_lu": ("nlu_diag_kernel", "nlu_trsm_kernel", "nlu_cross_kernel", "nlu_update2_kernel",
+                        "nlu_ldiag_kernel", "nlu_lcol_kernel"),
               "qp_lu_pivot": ("blu_panel_kernel", "blu_update_kernel"),
               "qp_solve": ("blu_solve_kernel", "blu_solve_rows_kernel")}
 NLP_STEP = "nlp_assemble_kernel"
@@ -100,6 +103,7 @@ def per_launch(d, counter):
 
 def main():
     fdir, wdir, out = sys.argv[1:4]
+    suffix = sys.argv[4] if len(sys.argv) > 4 else ""
     fetch = per_launch(fdir, "FETCH_SIZE")
     write = per_launch(wdir, "WRITE_SIZE")
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes",
@@ -108,7 +112,7 @@ def main():
     for ph in sorted(set(fetch) | set(write)):
         rb = fetch.get(ph, 0.0) * 2 * 1024
         wb = write.get(ph, 0.0) * 1024
-        res["kernels"][ph] = {"read_bytes_per_launch": rb, "write_bytes_per_launch": wb,
+        res["kernels"][ph + suffix] = {"read_bytes_per_launch": rb, "write_bytes_per_launch": wb,
                               "hbm_bytes_per_launch": rb + wb}
     if os.path.exists(out):          # merge: other configs' kernels stay
         with open(out) as f:
