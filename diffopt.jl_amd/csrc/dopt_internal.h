@@ -200,6 +200,8 @@ struct Handle {
   // eliminated exactly, R = [H + diag(δ), Jᵀ; J, −diag(ρ)] over [x; y] factorised
   // instead of M; env DOPT_NLP_REDUCE=0 keeps the full sIpopt M
   int32_t nlp_reduce = 1;
+  bool nlp_left = false;           // this factorisation: every problem reduced and P-symmetric (H symmetric) —
+                                   // the left-looking LU reads R from the inputs (no assembly)
   DevBuf nlp_rd;                   // per problem: δ (num_w), ρ (c) doubles
   DevBuf nlp_ri;                   // per problem: active bound of each w index (num_w), row state (c); then B ok flags
   DevBuf nlp_t1, nlp_t2;           // reduced right-hand sides / solutions (max(2, P) × B × nmax)

@@ -26,7 +26,7 @@
 // assembled densely (identity padding to the 32-multiple the LU works on),
 // one value per element computed by gather — no zero-then-scatter pass.
 // Inertia correction adds k·st·D, D = +1 except −1 on the constraint rows.
-#include "dopt_internal.h"
+#include "nlp_defs.h"
 
 #include <algorithm>
 
@@ -39,102 +39,13 @@ constexpr int ROWS_PER_WG = 8;
 constexpr double NLP_ST = 1e-6;        // _inertia_correction st (NonLinearProgram.jl:397)
 constexpr int NLP_MAX_CORR = 50;       // max_corrections (:398)
 
-struct NLPDims {
-  int n, c, P, num_w, ng, nl, nlo, nup, nlowp, nupp, rows, sense, kkt;
-};
-
-// device index maps (one int32 buffer), built on the host from the structure
-struct NLPMap {
-  const int32_t* slack_of_row;   // c: slack column of an inequality row (w index), −1 for EqualTo
-  const int32_t* row_of_slack;   // ng + nl: the constraint row of a slack column (n + i)
-  const int32_t* lowpos;         // num_w: position in the lower block, −1 if unbounded below
-  const int32_t* uppos;          // num_w: position in the upper block
-  const int32_t* low_idx;        // nlo: w index of each lower-bound row
-  const int32_t* up_idx;         // nup
-};
-
-struct NLPIn {
-  const double *Hxx, *Hxp, *Jx, *Jp, *x, *cval, *crhs, *y, *xl, *xu, *yl, *yu;
-};
-
-__device__ __forceinline__ double nlp_X(const NLPDims& d, const NLPMap& mp, const NLPIn& in, size_t b, int j) {
-  if (j < d.n) return in.x[b * d.n + j];
-  const int k = mp.row_of_slack[j - d.n];   // slack = c(x) − b (nlp_utilities.jl:202-206)
-  return in.cval[b * d.c + k] - in.crhs[b * d.c + k];
-}
-
-// V_L / V_U of bounded w index j (nlp_utilities.jl:213-267): primal bounds take
-// the bound duals, slacks the row dual; ×sense (lower) / ×(−sense) (upper)
-__device__ __forceinline__ double nlp_VL(const NLPDims& d, const NLPMap& mp, const NLPIn& in, size_t b, int j) {
-  const double v = j < d.n ? in.yl[b * d.n + j] : in.y[b * d.c + mp.row_of_slack[j - d.n]];
-  return v * d.sense;
-}
-__device__ __forceinline__ double nlp_VU(const NLPDims& d, const NLPMap& mp, const NLPIn& in, size_t b, int j) {
-  const double v = j < d.n ? in.yu[b * d.n + j] : in.y[b * d.c + mp.row_of_slack[j - d.n]];
-  return v * (-d.sense);
-}
-
-// ---------------------------------------------------------------------------
-// Reduced KKT route (structured mode).  The bound rows and the slacks are
-// eliminated exactly (tests/test_nlp_reduce_cpu.py restates the algebra and
-// checks it against the full solves with M and Mᵀ):
-//   bound row i on w_j, a·z_j + d·z_ν = r (row j carries b·z_ν):
-//     M: (a, b) = (V, ∓1), Mᵀ: (a, b) = (∓1, V);
-//     d ≠ 0: z_ν eliminated, row j gains δ_j = −a·b/d (the same for M and Mᵀ),
-//            r_j −= b·r/d;
-//     d = 0: z_j = r/a is known (a = 0, or two active bounds on one variable:
-//            the problem keeps the full M);
-//   slack t of row k (W is zero there): known → row k reads J_k x = r_k + z_t;
-//     else row t reads δ_t z_t − y_k = r̃_t: δ_t = 0 → y_k = −r̃_t known;
-//     δ_t ≠ 0 → row k reads J_k x − ρ_k y_k = r_k + ρ_k r̃_t (ρ_k = 1/δ_t).
-// R = [H + diag(δ_x), Jᵀ; J, −diag(ρ)] over [x; y], the known unknowns as
-// identity rows / columns, n + c rows whatever the active set — the same
-// matrix for both directions (Rᵀ for Mᵀ).  det M = ±Π(pivots)·det R, so M is
-// singular exactly when R is (or a = 0 above): the singularity verdict and
-// the inertia correction (on the full M) keep the reference's semantics.
-// ---------------------------------------------------------------------------
-struct NLPRed {
-  int on;
-  double* delta;   // B × num_w
-  double* rho;     // B × c
-  int32_t* kx;     // B × num_w: the active bound of w_j (lower i → i, upper i → nlo + i), −1 none
-  int32_t* yst;    // B × c: 0 kept, 1 y_k known, 2 regularised (ρ)
-  int32_t* ok;     // B: 1 when the reduction applies
-};
-
-__device__ __forceinline__ bool red_use(const NLPRed& R, const int32_t* shift, int b) {
-  return R.on && R.ok[b] && shift[b] == 0;
-}
-
-// R[r][col] of problem b (identity padding past n + c)
-__device__ __forceinline__ double nlp_R(const NLPDims& d, const NLPIn& in, const NLPRed& R, size_t b, int r,
-                                        int col) {
-  const int n = d.n, N = n + d.c;
-  if (r >= N || col >= N) return r == col ? 1.0 : 0.0;
-  const int32_t* kx = R.kx + b * d.num_w;
-  const int32_t* ys = R.yst + b * d.c;
-  if (r < n) {
-    if (kx[r] >= 0) return r == col ? 1.0 : 0.0;
-    if (col < n) {
-      if (kx[col] >= 0) return 0.0;
-      double v = in.Hxx[b * n * n + (size_t)col * n + r];
-      if (col == r) v += R.delta[b * d.num_w + r];
-      return v;
-    }
-    const int k = col - n;
-    return ys[k] == 1 ? 0.0 : in.Jx[b * d.c * n + (size_t)r * d.c + k];
-  }
-  const int k = r - n;
-  if (ys[k] == 1) return r == col ? 1.0 : 0.0;
-  if (col < n) return kx[col] >= 0 ? 0.0 : in.Jx[b * d.c * n + (size_t)col * d.c + k];
-  if (col != r) return 0.0;
-  return ys[k] == 2 ? -R.rho[b * d.c + k] : 0.0;
-}
-
 // Per problem: δ, the active bounds, the constraint rows' states, and whether
 // the reduction applies (one workgroup per problem)
-__global__ __launch_bounds__(NT) void nlp_red_prep_kernel(NLPDims d, NLPMap mp, NLPIn in, NLPRed R) {
+__global__ __launch_bounds__(NT) void nlp_red_prep_kernel(NLPDims d, NLPMap mp, NLPIn in, NLPRed R,
+                                                          QPMeta* __restrict__ meta, double* __restrict__ kamax,
+                                                          const int32_t* __restrict__ hasym) {
   __shared__ int bad;
+  __shared__ double red[NT / 64];
   const size_t b = blockIdx.x;
   const int t = threadIdx.x;
   double* delta = R.delta + b * d.num_w;
@@ -183,8 +94,26 @@ __global__ __launch_bounds__(NT) void nlp_red_prep_kernel(NLPDims d, NLPMap mp, 
     R.yst[b * d.c + k] = st;
     R.rho[b * d.c + k] = rho;
   }
+  // max |R| without H (J, δ, ρ, the identity rows; qp_qsym_kernel gives max |H|):
+  // the growth bound of the left-looking LU, which reads R from the inputs
+  double amax = 1.0;
+  for (size_t e = t; e < (size_t)d.c * d.n; e += NT) amax = fmax(amax, fabs(in.Jx[b * d.c * d.n + e]));
+  for (int j = t; j < d.n; j += NT) amax = fmax(amax, fabs(delta[j]));
+  for (int k = t; k < d.c; k += NT) amax = fmax(amax, fabs(R.rho[b * d.c + k]));
+  for (int o = 32; o > 0; o >>= 1) amax = fmax(amax, __shfl_xor(amax, o));
+  if ((t & 63) == 0) red[t >> 6] = amax;
   __syncthreads();
-  if (t == 0) R.ok[b] = bad ? 0 : 1;
+  if (t == 0) {
+    for (int w = 1; w < NT / 64; ++w) amax = fmax(amax, red[w]);
+    const bool ok = !bad;
+    R.ok[b] = ok ? 1 : 0;
+    kamax[b] = amax;
+    QPMeta mm = {};
+    mm.nsys = ok ? d.n + d.c : d.rows;
+    mm.lu = LU_NONE;
+    mm.sym = ok && hasym && !hasym[b];   // R symmetric: H exactly symmetric
+    meta[b] = mm;
+  }
 }
 
 // M (+ k·st·D) of the listed problems into K; grid (row blocks, count)
@@ -291,7 +220,8 @@ __global__ __launch_bounds__(NT) void nlp_pivot_check_kernel(const double* __res
                                                              const double* __restrict__ dinv, size_t dstride,
                                                              QPMeta* __restrict__ meta,
                                                              const double* __restrict__ partial, int nparts,
-                                                             int rows, const int32_t* __restrict__ plist) {
+                                                             int rows, const int32_t* __restrict__ plist,
+                                                             const double* __restrict__ kamax) {
   __shared__ double sred[NT / 64];
   __shared__ int ired[NT / 64];
   const int b = plist ? plist[blockIdx.x] : (int)blockIdx.x;
@@ -302,7 +232,7 @@ __global__ __launch_bounds__(NT) void nlp_pivot_check_kernel(const double* __res
   for (int o = 32; o > 0; o >>= 1) sc = fmax(sc, __shfl_xor(sc, o));
   if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = sc;
   __syncthreads();
-  sc = fmax(fmax(sred[0], sred[1]), fmax(sred[2], sred[3]));
+  sc = fmax(fmax(fmax(sred[0], sred[1]), fmax(sred[2], sred[3])), kamax[b]);   // kamax: max |R| of the left route
   rows = mm.nsys;   // the factorised system: M, or R on the reduced route
   const double tol = rows * 2.220446049250313e-16 * sc;
   const double* Kb = K + (size_t)b * nmax * ld;
@@ -468,7 +398,8 @@ __device__ __forceinline__ void red_rr(const NLPDims& d, const NLPMap& mp, const
 __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, NLPIn in, NLPRed Rd,
                                                          const int32_t* __restrict__ shift, int trans,
                                                          const double* __restrict__ rfull,
-                                                         double* __restrict__ rred, int nmax) {
+                                                         double* __restrict__ rred, int nmax,
+                                                         const QPMeta* __restrict__ meta) {
   extern __shared__ double sm[];
   const size_t b = blockIdx.x, off = ((size_t)blockIdx.y * gridDim.x + b) * nmax;
   const double* r = rfull + off;
@@ -480,15 +411,20 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
   }
   const int n = d.n, c = d.c, w = d.num_w, N = n + c;
   double *rr = sm, *zk = sm + w, *yv = sm + 2 * w;
-  const int32_t* kx = Rd.kx + b * w;
-  const int32_t* ys = Rd.yst + b * c;
+  int* kx = reinterpret_cast<int*>(sm + 2 * w + c);   // the masks, staged
+  int* ys = kx + w;
   const double* rho = Rd.rho + b * c;
+  for (int j = t; j < w; j += NT) kx[j] = Rd.kx[b * w + j];
+  for (int k = t; k < c; k += NT) ys[k] = Rd.yst[b * c + k];
   red_rr(d, mp, in, b, trans, r, rr, zk);
   __syncthreads();
   for (int k = t; k < c; k += NT) yv[k] = ys[k] == 1 ? -rr[mp.slack_of_row[k]] : 0.0;
   __syncthreads();
   const double* H = in.Hxx + b * n * n;
   const double* J = in.Jx + b * c * n;
+  // W for M, Wᵀ for Mᵀ — column-major H read with the lanes along i whenever
+  // H is exactly symmetric (meta.sym: the two coincide)
+  const bool hcol = !trans || meta[b].sym;
   for (int i = t; i < nmax; i += NT) {
     double v = 0.0;
     if (i < n) {
@@ -496,8 +432,8 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
         v = zk[i];
       } else {
         v = rr[i];
-        for (int j = 0; j < n; ++j)   // known x (W, or Wᵀ for Mᵀ)
-          if (kx[j] >= 0) v -= (trans ? H[(size_t)i * n + j] : H[(size_t)j * n + i]) * zk[j];
+        for (int j = 0; j < n; ++j)   // known x
+          if (kx[j] >= 0) v -= (hcol ? H[(size_t)j * n + i] : H[(size_t)i * n + j]) * zk[j];
         for (int k = 0; k < c; ++k)
           if (ys[k] == 1) v -= J[(size_t)i * c + k] * yv[k];
       }
@@ -525,7 +461,8 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
                                                              const int32_t* __restrict__ shift, int trans,
                                                              const double* __restrict__ rfull,
                                                              const double* __restrict__ xred,
-                                                             double* __restrict__ zfull, int nmax) {
+                                                             double* __restrict__ zfull, int nmax,
+                                                             const QPMeta* __restrict__ meta) {
   extern __shared__ double sm[];
   const size_t b = blockIdx.x, off = ((size_t)blockIdx.y * gridDim.x + b) * nmax;
   const double* r = rfull + off;
@@ -537,16 +474,23 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
     return;
   }
   const int n = d.n, c = d.c, w = d.num_w;
-  double *rr = sm, *zk = sm + w, *zw = sm + 2 * w;
-  const int32_t* kx = Rd.kx + b * w;
-  const int32_t* ys = Rd.yst + b * c;
+  double *rr = sm, *zk = sm + w, *zw = sm + 2 * w, *yl = sm + 3 * w;
+  int* kx = reinterpret_cast<int*>(sm + 3 * w + c);   // the masks, staged
+  int* ys = kx + w;
+  for (int j = t; j < w; j += NT) kx[j] = Rd.kx[b * w + j];
+  for (int k = t; k < c; k += NT) ys[k] = Rd.yst[b * c + k];
   const double* rho = Rd.rho + b * c;
   const double* dl = Rd.delta + b * w;
   const double* H = in.Hxx + b * n * n;
   const double* J = in.Jx + b * c * n;
+  // row j of W (Wᵀ for Mᵀ) contiguous when H is exactly symmetric
+  const bool hrow = trans || meta[b].sym;
   red_rr(d, mp, in, b, trans, r, rr, zk);
   for (int i = t; i < n; i += NT) zw[i] = xr[i];
-  for (int k = t; k < c; k += NT) z[w + k] = xr[n + k];
+  for (int k = t; k < c; k += NT) {
+    yl[k] = xr[n + k];
+    z[w + k] = xr[n + k];
+  }
   __syncthreads();
   for (int s = n + t; s < w; s += NT) {   // slacks
     const int k = mp.row_of_slack[s - n];
@@ -557,7 +501,7 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
       v = -r[w + k];
       for (int j = 0; j < n; ++j) v += J[(size_t)j * c + k] * zw[j];
     } else {
-      v = (rr[s] + xr[n + k]) * rho[k];
+      v = (rr[s] + yl[k]) * rho[k];
     }
     zw[s] = v;
   }
@@ -587,11 +531,11 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
       v = (r[row] - a * zw[j]) / dd;
     } else if (j < n) {   // row j: (W x)_j + δ_j x_j + (Jᵀ y)_j + b·z_ν = r̃_j
       double acc = rr[j] - dl[j] * zw[j];
-      for (int jj = 0; jj < n; ++jj) acc -= (trans ? H[(size_t)j * n + jj] : H[(size_t)jj * n + j]) * zw[jj];
-      for (int k = 0; k < c; ++k) acc -= J[(size_t)j * c + k] * xr[n + k];
+      for (int jj = 0; jj < n; ++jj) acc -= (hrow ? H[(size_t)j * n + jj] : H[(size_t)jj * n + j]) * zw[jj];
+      for (int k = 0; k < c; ++k) acc -= J[(size_t)j * c + k] * yl[k];
       v = acc / bc;
     } else {              // slack row: −y_k + b·z_ν = r̃_t
-      v = (rr[j] + xr[n + mp.row_of_slack[j - n]]) / bc;
+      v = (rr[j] + yl[mp.row_of_slack[j - n]]) / bc;
     }
     z[row] = v;
   }
@@ -665,16 +609,19 @@ void assemble(Handle& h, const int32_t* plist, int count) {
 
 // full right-hand sides (k per problem) → the system each problem factorised
 void red_rhs(Handle& h, int trans, int k, const double* rfull, double* rred) {
-  const size_t lds = (size_t)(2 * h.nlp_num_w + h.m) * sizeof(double);
+  const size_t w = h.nlp_num_w, c = h.m;
+  const size_t lds = (2 * w + c) * sizeof(double) + (w + c) * sizeof(int);
   hipLaunchKernelGGL(nlp_red_rhs_kernel, dim3((unsigned)h.batch, (unsigned)k), dim3(NT), lds, h.stream, dims(h),
-                     map_of(h), inputs(h), red_of(h), h.nlp_shift.as<int32_t>(), trans, rfull, rred, h.nmax);
+                     map_of(h), inputs(h), red_of(h), h.nlp_shift.as<int32_t>(), trans, rfull, rred, h.nmax,
+                     h.meta.as<QPMeta>());
   DOPT_CHECK_HIP(hipGetLastError());
 }
 void red_recover(Handle& h, int trans, int k, const double* rfull, const double* xred, double* zfull) {
-  const size_t lds = (size_t)3 * h.nlp_num_w * sizeof(double);
+  const size_t w = h.nlp_num_w, c = h.m;
+  const size_t lds = (3 * w + c) * sizeof(double) + (w + c) * sizeof(int);
   hipLaunchKernelGGL(nlp_red_recover_kernel, dim3((unsigned)h.batch, (unsigned)k), dim3(NT), lds, h.stream,
                      dims(h), map_of(h), inputs(h), red_of(h), h.nlp_shift.as<int32_t>(), trans, rfull, xred, zfull,
-                     h.nmax);
+                     h.nmax, h.meta.as<QPMeta>());
   DOPT_CHECK_HIP(hipGetLastError());
 }
 bool reduced_on(const Handle& h) { return !h.nlp_kkt && h.nlp_reduce; }
@@ -693,7 +640,7 @@ void pivot_check(Handle& h, const int32_t* plist, int count) {
   hipLaunchKernelGGL(nlp_pivot_check_kernel, dim3(count), dim3(NT), 0, h.stream, h.K.as<double>(), h.ld, h.nmax,
                      h.ipiv.as<int32_t>(), dense_dinv(h), dinv_stride(h.nmax), h.meta.as<QPMeta>(),
                      h.nlp_scale.as<double>(), row_blocks(h),
-                     h.nlp_rows, plist);
+                     h.nlp_rows, plist, h.kamax.as<double>());
   DOPT_CHECK_HIP(hipGetLastError());
 }
 
@@ -709,6 +656,13 @@ std::vector<int32_t> singular_list(Handle& h, const std::vector<int32_t>& among)
 }
 
 }  // namespace
+
+NLPDims nlp_dims(const Handle& h) { return dims(h); }
+__global__ void qp_qsym_kernel(QPIn, double*, int32_t*, const int32_t*);
+int qsym_pairs(int n);
+NLPMap nlp_map_of(const Handle& h) { return map_of(h); }
+NLPIn nlp_inputs(const Handle& h) { return inputs(h); }
+NLPRed nlp_red_of(Handle& h) { return red_of(h); }
 
 // Buffers and sizes once the structure is known (dopt_nlp_set_structure /
 // dopt_nlp_set_kkt have filled the nlp_* counts and nlp_map).
@@ -739,14 +693,46 @@ void nlp_factor(Handle& h) {
   const int B = (int)h.batch;
   DOPT_CHECK_HIP(hipMemsetAsync(h.nlp_shift.p, 0, (size_t)B * sizeof(int32_t), h.stream));
   DOPT_CHECK_HIP(hipMemsetAsync(h.kamax.p, 0, (size_t)B * sizeof(double), h.stream));
+  h.nlp_left = false;
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
-    if (reduced_on(h))
+    if (reduced_on(h)) {
+      // H's exact symmetry (R is then symmetric: the left-looking LU reads it
+      // from the inputs, no assembly), then the per-problem elimination data
+      const int32_t* hasym = nullptr;
+      if (h.n > 0 && h.left_mode && h.lu_mode == 1) {   // (partial pivoting everywhere reads the assembled K)
+        h.qsy.ensure((size_t)B * (sizeof(double) + sizeof(int32_t)));
+        DOPT_CHECK_HIP(hipMemsetAsync(h.qsy.p, 0, h.qsy.bytes, h.stream));
+        static const double dummy = 0.0;
+        QPIn P{};
+        P.Q = h.nin[0];
+        P.G = P.h = P.A = P.z = P.lam = P.nu = &dummy;
+        P.n = h.n;
+        hipLaunchKernelGGL(qp_qsym_kernel, dim3((unsigned)qsym_pairs(h.n), (unsigned)B), dim3(256), 0, h.stream, P,
+                           qsy_max(h), qsy_flag(h), nullptr);
+        DOPT_CHECK_HIP(hipGetLastError());
+        hasym = qsy_flag(h);
+      }
       hipLaunchKernelGGL(nlp_red_prep_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), map_of(h), inputs(h),
-                         red_of(h));
-    assemble(h, nullptr, B);
+                         red_of(h), h.meta.as<QPMeta>(), h.kamax.as<double>(), hasym);
+      DOPT_CHECK_HIP(hipGetLastError());
+      // the factorised sizes (n + c, or the rows of M for a problem kept on
+      // the full route) size the LU and solve launches; every problem reduced
+      // and symmetric: the left-looking route
+      std::vector<QPMeta> mh(B);
+      DOPT_CHECK_HIP(hipMemcpyAsync(mh.data(), h.meta.p, B * sizeof(QPMeta), hipMemcpyDeviceToHost, h.stream));
+      DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+      int npmax = 0;
+      for (const QPMeta& mm : mh) npmax = std::max(npmax, (mm.nsys + 31) & ~31);
+      h.blocked_npmax = npmax;
+      h.nlp_left = hasym && std::all_of(mh.begin(), mh.end(), [](const QPMeta& mm) { return mm.sym != 0; });
+    }
+    if (h.nlp_left)   // the pivot check's per-block scales: kamax alone
+      DOPT_CHECK_HIP(hipMemsetAsync(h.nlp_scale.p, 0, h.nlp_scale.bytes, h.stream));
+    else
+      assemble(h, nullptr, B);
   }
-  h.blocked_npmax = h.nmax;
+  if (!reduced_on(h)) h.blocked_npmax = h.nmax;
   // The sIpopt ordering puts an exactly zero diagonal at every slack column
   // (slacks are absent from the Hessian) and at the dual rows: the no-pivot
   // LU's threshold test rejects every problem with a slack or bound row
@@ -778,6 +764,7 @@ void nlp_factor(Handle& h) {
     h.plist.ensure(sing.size() * sizeof(int32_t));
     DOPT_CHECK_HIP(hipMemcpyAsync(h.plist.p, sing.data(), sing.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                                   h.stream));
+    h.blocked_npmax = h.nmax;   // the corrected problems are the full M
     assemble(h, h.plist.as<int32_t>(), (int)sing.size());
     qp_blocked_factor(h, dense_dinv(h), h.plist.as<int32_t>(), (int)sing.size());
     pivot_check(h, h.plist.as<int32_t>(), (int)sing.size());

@@ -61,7 +61,7 @@
 //
 // Reference: QuadraticProgram.jl create_LHS_matrix :256-282 and solve_system
 // :486-496 (reverse :316-351, forward :357-446).
-#include "dopt_internal.h"
+#include "nlp_defs.h"
 
 // tools/probe/nlu_probe.hip builds this file with -DNLU_STOP=k to time the
 // diagonal kernel up to phase k; the product build never stops early
@@ -194,6 +194,32 @@ __device__ __forceinline__ double kval_lower(const QSrcB& v, int r, int c) {
   if (r < n + nk) return r == c ? v.sk[r - n] : 0.0;
   return 0.0;
 }
+
+// The left-looking LU's source of K's entries: the QP inputs (QSrc, kval /
+// kval_lower above) or the NLP inputs through the reduced route's R (NSrc,
+// nlp_R) — overloads found at instantiation.
+__device__ __forceinline__ QSrcB src_bind(const QSrc& s, int b, const QPMeta& mm) { return qsrc(s, b, mm); }
+__device__ __forceinline__ double src_val(const QSrcB& v, int r, int c) { return kval(v, r, c); }
+__device__ __forceinline__ double src_val_lower(const QSrcB& v, int r, int c) { return kval_lower(v, r, c); }
+
+struct NSrc {          // NLP, reduced route (kernel argument)
+  NLPDims d;
+  NLPIn in;
+  NLPRed R;
+  const double* qmax;     // H's symmetry check (qp_qsym_kernel on Hxx): max |H| per problem
+  const int32_t* qflag;   // ... and its verdict
+};
+struct NSrcB {
+  const NSrc* s;
+  size_t b;
+};
+__device__ __forceinline__ NSrcB src_bind(const NSrc& s, int b, const QPMeta&) { return NSrcB{&s, (size_t)b}; }
+__device__ __forceinline__ double src_val(const NSrcB& v, int r, int c) {
+  return nlp_R(v.s->d, v.s->in, v.s->R, v.b, r, c);
+}
+// R's lower part reads H column-major (H[c·n + r]) and J's column-major copy
+// with the lanes along r: coalesced as is
+__device__ __forceinline__ double src_val_lower(const NSrcB& v, int r, int c) { return src_val(v, r, c); }
 
 // Tile `tile` of the lower triangle (rt ≥ ct) of an nrt × nrt grid, column by
 // column: column 0's nrt tiles first.
@@ -1525,11 +1551,12 @@ __device__ __forceinline__ void stage_rowstrip(double* X, const double* Kb, int 
   for (int u = 0; u < 16; ++u) X[(kq + u) * TLD + j] = j < rows ? v[u] : 0.0;
 }
 
+template <class SRC>
 __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_ldiag_kernel(
     double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
     size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv, double* __restrict__ ukp,
     double* __restrict__ w0, double* __restrict__ w1, double* __restrict__ kamax, const double* __restrict__ kls,
-    int n, int m, QSrc src) {
+    int n, int m, SRC src) {
   __shared__ double S[STEP_LDS];
   const int b = blockIdx.x;
   const QPMeta mm = meta[b];
@@ -1538,7 +1565,7 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
   const int Wv = min(NB64, Np - c0);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
   double* Kb = K + (size_t)b * nmax * ld;
-  const QSrcB sv = qsrc(src, b, mm);
+  const auto sv = src_bind(src, b, mm);
   const PScale ps = pscale(kls, b, n, m, mm);
   double* ud = ukp + (size_t)b * nmax;
   double* w0b = w0 ? w0 + (size_t)b * nmax : nullptr;
@@ -1604,7 +1631,7 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
     for (int rr = 0; rr < 4; ++rr) {
       const int i = 16 * wv + g + 4 * rr;
       const bool in = i < Wv && j < Wv;
-      S[i * SLD + j] = in ? kval(sv, c0 + i, c0 + j) - accd[q][rr] * pj : (i == j ? 1.0 : 0.0);
+      S[i * SLD + j] = in ? src_val(sv, c0 + i, c0 + j) - accd[q][rr] * pj : (i == j ? 1.0 : 0.0);
     }
   }
   if (w0b && t < 2 * NB64) {   // block J of b / c minus the finished blocks' contributions
@@ -1631,10 +1658,11 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
 // strips L(I, k)·D_k (A operand), then the TRSM by the packed inverse of the
 // diagonal block (binv) with the threshold test, L(I, J) → K, and
 // U(J, I) = D_J·L(I, J)ᵀ·P_I beside it (transposed through LDS; growth bound).
+template <class SRC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_lcol_kernel(
     double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
     const double* __restrict__ ukp, int ntile, int toff, int total, const double* __restrict__ kamax,
-    const double* __restrict__ kls, int n, int m, QSrc src, int wr_u) {
+    const double* __restrict__ kls, int n, int m, SRC src, int wr_u) {
   __shared__ double X[NB64 * TLD];
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
@@ -1651,7 +1679,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
   double* Kb = K + (size_t)b * nmax * ld;
   const double* ud = ukp + (size_t)b * nmax;
   const double* Bg = binv + (size_t)b * BSTR;
-  const QSrcB sv = qsrc(src, b, mm);
+  const auto sv = src_bind(src, b, mm);
   const PScale ps = pscale(kls, b, n, m, mm);
   const double bound = growth_bound(kamax[b]);
   d4n acc[4];
@@ -1684,7 +1712,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
   double av[16];
   if (wact) {
 #pragma unroll
-    for (int s = 0; s < 16; ++s) av[s] = kval_lower(sv, r0 + 16 * wv + l16, c0 + 4 * s + g);
+    for (int s = 0; s < 16; ++s) av[s] = src_val_lower(sv, r0 + 16 * wv + l16, c0 + 4 * s + g);
   }
   __syncthreads();
   if (wact && c0 > 0) {
@@ -1799,6 +1827,71 @@ __global__ __launch_bounds__(256) void nlu_sym_u_kernel(double* __restrict__ K, 
 
 }  // namespace
 
+// The left-looking LU of a P-symmetric batch (every blocked problem sym), its
+// entries read from `src` (QP inputs, or the NLP inputs through R): per block
+// column J the diagonal launch and the column's tiles.  Two streams
+// (lstreams): the tiles I ≥ J+2 of column J run on `aux` beside ldiag(J+1)
+// (which needs only tile (J+1, J) of this column, on the main stream); the
+// main stream joins them before the next column's first tile (it reads
+// (J+2, J)).
+template <class SRC>
+static void left_lu(Handle& h, const SRC& src, double* dinv, double* w0, double* w1, const double* kls,
+                    double* kamax) {
+  const int npmax = h.blocked_npmax;
+  const int B = (int)h.batch;
+  const size_t dstride = dinv_stride(h.nmax);
+  double* K = h.K.as<double>();
+  int32_t* perm = h.ipiv.as<int32_t>();
+  QPMeta* meta = h.meta.as<QPMeta>();
+  h.binv.ensure((size_t)2 * B * BSTR * sizeof(double));
+  h.ukp.ensure((size_t)B * h.nmax * sizeof(double));
+  h.ukp_valid = true;
+  h.u_missing = true;   // U is not stored (qp_nopiv_materialize_u when a solve needs it)
+  double* ukp = h.ukp.as<double>();
+  hipStream_t S = h.stream, T = h.stream;
+  if (h.lstreams) {
+    ensure_aux(h);
+    T = h.aux;
+  }
+  auto lcol = [&](hipStream_t st, int c0, double* bv, int toff, int cnt) {
+    if (cnt <= 0) return;
+    const long long tot = (long long)cnt * B;
+    if (tot > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
+    hipLaunchKernelGGL(nlu_lcol_kernel<SRC>, dim3((unsigned)tot), dim3(256), 0, st, K, h.ld, h.nmax, meta, c0, bv, ukp,
+                       cnt, toff, (int)tot, kamax, kls, h.n, h.m, src, 0);
+    DOPT_CHECK_HIP(hipGetLastError());
+  };
+  bool pending = false;   // T holds column tiles S must wait for
+  for (int c0 = 0; c0 < npmax; c0 += NB64) {
+    double* bv = h.binv.as<double>() + (size_t)((c0 / NB64) & 1) * B * BSTR;
+    hipLaunchKernelGGL(nlu_ldiag_kernel<SRC>, dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv, dstride, meta,
+                       c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src);
+    DOPT_CHECK_HIP(hipGetLastError());
+    const int ntile = (npmax - c0 - NB64 + 63) / 64;
+    if (ntile <= 0) break;
+    if (T == S) {
+      lcol(S, c0, bv, 0, ntile);
+      continue;
+    }
+    if (pending) {   // column J−1's tiles I ≥ J+1 (tile (J+1, J−1) feeds this column)
+      DOPT_CHECK_HIP(hipEventRecord(h.ev_join, T));
+      DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_join, 0));
+      pending = false;
+    }
+    DOPT_CHECK_HIP(hipEventRecord(h.ev_fork, S));   // T: after ldiag(J) (and, in S order, all before it)
+    DOPT_CHECK_HIP(hipStreamWaitEvent(T, h.ev_fork, 0));
+    lcol(S, c0, bv, 0, 1);
+    if (ntile > 1) {
+      lcol(T, c0, bv, 1, ntile - 1);
+      pending = true;
+    }
+  }
+  if (pending) {
+    DOPT_CHECK_HIP(hipEventRecord(h.ev_join, T));
+    DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_join, 0));
+  }
+}
+
 // No-pivot blocked LU of every ROUTE_BLOCKED problem, by pairs of 64-column
 // block steps (rank 64 per step measured slower):
 //   step c0:     diagonal block + TRSM strip 0 (one launch), then the cross
@@ -1853,59 +1946,20 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   double* K = h.K.as<double>();
   int32_t* perm = h.ipiv.as<int32_t>();
   QPMeta* meta = h.meta.as<QPMeta>();
+  if (h.kind == DOPT_KIND_NLP && h.nlp_left) {
+    // NLP reduced route, every problem P-symmetric (H exactly symmetric, p = 1):
+    // R read straight from the NLP inputs
+    NSrc ns;
+    ns.d = nlp_dims(h);
+    ns.in = nlp_inputs(h);
+    ns.R = nlp_red_of(h);
+    ns.qmax = qsy_max(h);
+    ns.qflag = qsy_flag(h);
+    left_lu(h, ns, dinv, w0, w1, nullptr, kamax);
+    return;
+  }
   if (lower && h.left_mode) {
-    // P-symmetric batch: the left-looking LU, per block column J the diagonal
-    // launch and the column's tiles.  Two streams (lstreams): the tiles
-    // I ≥ J+2 of column J run on `aux` beside ldiag(J+1) (which needs only
-    // tile (J+1, J) of this column, on the main stream); the main stream
-    // joins them before the next column's first tile (it reads (J+2, J)).
-    h.binv.ensure((size_t)2 * B * BSTR * sizeof(double));
-    h.ukp.ensure((size_t)B * h.nmax * sizeof(double));
-    h.ukp_valid = true;
-    h.u_missing = true;   // U is not stored (qp_nopiv_materialize_u when a solve needs it)
-    double* ukp = h.ukp.as<double>();
-    hipStream_t S = h.stream, T = h.stream;
-    if (h.lstreams) {
-      ensure_aux(h);
-      T = h.aux;
-    }
-    auto lcol = [&](hipStream_t st, int c0, double* bv, int toff, int cnt) {
-      if (cnt <= 0) return;
-      const long long tot = (long long)cnt * B;
-      if (tot > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
-      hipLaunchKernelGGL(nlu_lcol_kernel, dim3((unsigned)tot), dim3(256), 0, st, K, h.ld, h.nmax, meta, c0, bv, ukp,
-                         cnt, toff, (int)tot, kamax, kls, h.n, h.m, src, 0);
-      DOPT_CHECK_HIP(hipGetLastError());
-    };
-    bool pending = false;   // T holds column tiles S must wait for
-    for (int c0 = 0; c0 < npmax; c0 += NB64) {
-      double* bv = h.binv.as<double>() + (size_t)((c0 / NB64) & 1) * B * BSTR;
-      hipLaunchKernelGGL(nlu_ldiag_kernel, dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv, dstride, meta,
-                         c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src);
-      DOPT_CHECK_HIP(hipGetLastError());
-      const int ntile = (npmax - c0 - NB64 + 63) / 64;
-      if (ntile <= 0) break;
-      if (T == S) {
-        lcol(S, c0, bv, 0, ntile);
-        continue;
-      }
-      if (pending) {   // column J−1's tiles I ≥ J+1 (tile (J+1, J−1) feeds this column)
-        DOPT_CHECK_HIP(hipEventRecord(h.ev_join, T));
-        DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_join, 0));
-        pending = false;
-      }
-      DOPT_CHECK_HIP(hipEventRecord(h.ev_fork, S));   // T: after ldiag(J) (and, in S order, all before it)
-      DOPT_CHECK_HIP(hipStreamWaitEvent(T, h.ev_fork, 0));
-      lcol(S, c0, bv, 0, 1);
-      if (ntile > 1) {
-        lcol(T, c0, bv, 1, ntile - 1);
-        pending = true;
-      }
-    }
-    if (pending) {
-      DOPT_CHECK_HIP(hipEventRecord(h.ev_join, T));
-      DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_join, 0));
-    }
+    left_lu(h, src, dinv, w0, w1, kls, kamax);
     return;
   }
   // the packed inverse of step c lives in binv buffer (c / 64) & 1: a diagonal
