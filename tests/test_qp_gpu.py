@@ -614,3 +614,43 @@ def test_profiling_restricted_to_named_phases(QPBatch):
     np.testing.assert_array_equal(f_one, f_all)
     with pytest.raises(ValueError):
         e.set_profiling(True, phases=["no_such_phase"])
+
+
+@pytest.mark.parametrize("shape", [(6, 40, 60, 4), (3, 150, 200, 10)], ids=["small", "multi-block"])
+def test_left_looking_factors_serve_every_solve(QPBatch, monkeypatch, shape):
+    """The left-looking P-symmetric route stores only L (U = D·P⁻¹·Lᵀ·P): the
+    fused call's backward sweeps go through Lᵀ, later single-direction and
+    multi-RHS solves on the same factors materialise U first.  Every result
+    against the oracle, and the routes agree with the right-looking LU
+    (DOPT_LEFT=0) to rounding."""
+    monkeypatch.delenv("DOPT_LEFT", raising=False)
+    monkeypatch.delenv("DOPT_LU", raising=False)
+    monkeypatch.delenv("DOPT_SYM", raising=False)
+    B, n, m, p = shape
+    d = _synthetic(B, n, m, p, 0.35, 4242 + n)
+    e = QPBatch(B, n, m, p)
+    e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    fkw = dict(dq=d["dq"], dh=d["dh"], db=d["db"])
+    r1, f1 = e.forward_reverse(d["dl_dz"], **fkw)
+    assert e.sym_route().all()
+    r2 = e.reverse(d["dl_dz"])              # U materialised from L here
+    f2 = e.forward(**fkw)
+    seeds = np.stack([d["dl_dz"], d["dl_dz"][::-1].copy(), 2.0 * d["dl_dz"]])
+    rk = e.reverse_k(seeds)
+    for b in range(B):
+        args = [d[k][b] for k in ["Q", "G", "h", "A", "z", "lam", "nu"]]
+        ref_r = np.concatenate(oqp.reverse_differentiate(*args, d["dl_dz"][b]))
+        ref_f = np.concatenate(oqp.forward_differentiate(*args, **{k: v[b] for k, v in fkw.items()}))
+        for got in (r1[b], r2[b], rk[0, b], 0.5 * rk[2, b]):
+            assert relfro(got, ref_r) <= RTOL
+        assert relfro(rk[1, b], np.concatenate(oqp.reverse_differentiate(*args, seeds[1, b]))) <= RTOL
+        for got in (f1[b], f2[b]):
+            assert relfro(got, ref_f) <= RTOL
+    assert relfro(r2, r1) <= 1e-10
+    e.close()
+    monkeypatch.setenv("DOPT_LEFT", "0")
+    g = QPBatch(B, n, m, p)
+    g.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    r3, f3 = g.forward_reverse(d["dl_dz"], **fkw)
+    assert relfro(r3, r1) <= 1e-9 and relfro(f3, f1) <= 1e-9
+    g.close()
