@@ -1709,36 +1709,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
   // C = A − acc·P_J in the TRSM's A-operand layout (lane ↔ row 16wv + l16,
   // k-step s ↔ column 4s + g): the sources read with the lanes along the
   // rows, the update transposed through LDS
-  double av[16];
+  // U11⁻¹ (L2) loaded together with the sources: one round trip
+  double av[16], v[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = Bg[t + 256 * q];
   if (wact) {
 #pragma unroll
     for (int s = 0; s < 16; ++s) av[s] = src_val_lower(sv, r0 + 16 * wv + l16, c0 + 4 * s + g);
   }
-  __syncthreads();
-  if (wact && c0 > 0) {
+  if (c0 > 0) {   // workgroup-uniform
+    __syncthreads();   // every wave is done with the last staged strip
+    if (wact) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = 16 * q + l16;
-      const double pj = ps(c0 + j);
+      for (int q = 0; q < 4; ++q) {
+        const int j = 16 * q + l16;
+        const double pj = ps(c0 + j);
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) X[(16 * wv + g + 4 * rr) * TLD + j] = acc[q][rr] * pj;
+        for (int rr = 0; rr < 4; ++rr) X[(16 * wv + g + 4 * rr) * TLD + j] = acc[q][rr] * pj;
+      }
     }
-  }
-  __syncthreads();
-  if (wact && c0 > 0) {
-#pragma unroll
-    for (int s = 0; s < 16; ++s) av[s] -= X[(16 * wv + l16) * TLD + 4 * s + g];
-  }
-  {   // U11⁻¹ (upper triangle, zero below) staged once every wave holds its C rows
-    double v[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = Bg[t + 256 * q];
     __syncthreads();
+    if (wact) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + 256 * q, k = e >> 6, c = e & 63;
-      X[k * TLD + c] = k <= c ? v[q] : 0.0;
+      for (int s = 0; s < 16; ++s) av[s] -= X[(16 * wv + l16) * TLD + 4 * s + g];
     }
+    __syncthreads();   // every wave holds its C rows before U11⁻¹ overwrites X
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {   // U11⁻¹: upper triangle, zero below
+    const int e = t + 256 * q, k = e >> 6, c = e & 63;
+    X[k * TLD + c] = k <= c ? v[q] : 0.0;
   }
   __syncthreads();
   d4n lt[4];
