@@ -864,6 +864,95 @@ __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict
                          y, ps, part, swept ? 1 : 0);
 }
 
+// The P-symmetric fused sweeps (solve_sym2_body's algebra) as their own lean
+// launch: one workgroup per problem, the column slices read in two halves of
+// 16 rows (the first half in flight across the diagonal solve).  At 96 VGPRs
+// (5 waves per SIMD) config 2's sweep takes 0.16 ms against 0.21 ms inside
+// blu_solve2_kernel (124 VGPRs, whose other paths set the count); forcing 8
+// waves per SIMD (64 VGPRs, 22 spilled) measured 0.32 ms (DOPT_SYM_LEAN=2).
+template <int ENT, int WPE>
+__global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(WPE))) void blu_sym2_kernel(const double* __restrict__ K, int ld, int nmax,
+                                                      const double* __restrict__ dinv, size_t dstride,
+                                                      const QPMeta* __restrict__ meta,
+                                                      const double* __restrict__ w_rev,
+                                                      const double* __restrict__ w_fwd, double* __restrict__ x_rev,
+                                                      double* __restrict__ x_fwd, SymSweep sym) {
+  __shared__ double v[SOLVE_STATIC], y[SOLVE_STATIC], part[BNB], part2[BNB];
+  const int b = blockIdx.x;
+  const QPMeta mm = meta[b];
+  const int Np = blocked_np(mm);
+  if (Np == 0 || mm.lu != LU_NOPIV || !mm.sym) return;   // workgroup-uniform
+  const int N = mm.nsys;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const double* Kb = K + (size_t)b * nmax * ld;
+  const double* Dbase = dinv + (size_t)b * dstride;
+  const double* udb = sym.ukp + (size_t)b * nmax;
+  const PScale psc{sym.kls + (size_t)b * sym.m, sym.n, mm.nk};
+  const double* rb = w_rev + (size_t)b * nmax;
+  const double* fb = w_fwd + (size_t)b * nmax;
+  for (int i = t; i < Np; i += PT) {
+    v[i] = i < N ? rb[i] / udb[i] : 0.0;
+    y[i] = i < N ? fb[i] : 0.0;
+  }
+  __syncthreads();
+  const int nblk = Np / BNB;
+  for (int s = 0; s < nblk; ++s) {
+    const int bk = nblk - 1 - s;
+    const int i0 = bk * BNB;
+    double f[ENT][16];
+#pragma unroll
+    for (int q = 0; q < ENT; ++q) {   // rows i0 .. i0+15 of column e < i0
+      const int e = t + PT * q;
+      const int ec = e < i0 ? e : 0;
+      if (q * PT >= i0) continue;   // workgroup-uniform: no entries left
+#pragma unroll
+      for (int j = 0; j < 16; ++j) f[q][j] = Kb[(size_t)(i0 + j) * ld + ec];
+    }
+    if (wv < 2 && lane < BNB) {   // wave 0: L_kk⁻ᵀ v_k, wave 1: L_kk⁻ᵀ y_k
+      const double* Dk = Dbase + (size_t)bk * BDINV;
+      const double* vv = wv ? y : v;
+      double acc = 0.0;
+#pragma unroll 8
+      for (int j = 0; j < BNB; ++j) acc = fma(Dk[lane + j * BNB], vv[i0 + j], acc);
+      (wv ? part2 : part)[lane] = acc;
+    }
+    __syncthreads();
+    if (wv == 0 && lane < BNB) v[i0 + lane] = part[lane];
+    if (wv == 1 && lane < BNB) y[i0 + lane] = part2[lane];
+#pragma unroll
+    for (int q = 0; q < ENT; ++q) {
+      const int e = t + PT * q;
+      if (q * PT >= i0) continue;
+      const bool has = e < i0;
+      const int ec = has ? e : 0;
+      double a1 = has ? v[e] : 0.0, a2 = has ? y[e] : 0.0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        a1 = fma(-f[q][j], part[j], a1);
+        a2 = fma(-f[q][j], part2[j], a2);
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) f[q][j] = Kb[(size_t)(i0 + 16 + j) * ld + ec];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        a1 = fma(-f[q][j], part[16 + j], a1);
+        a2 = fma(-f[q][j], part2[16 + j], a2);
+      }
+      if (has) {
+        v[e] = a1;
+        y[e] = a2;
+      }
+    }
+    __syncthreads();
+  }
+  double* xr = x_rev + (size_t)b * nmax;
+  double* xf = x_fwd + (size_t)b * nmax;
+  for (int i = t; i < N; i += PT) {
+    xr[i] = v[i] / psc(i);
+    xf[i] = y[i];
+  }
+}
+
 }  // namespace
 
 // Partial-pivoting blocked LU of `count` problems (plist: their indices; null
@@ -976,6 +1065,24 @@ void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, con
   const size_t lds = solve_lds_bytes(h.nmax);
   // the left-looking LU's u_kk / p_k: the P-symmetric problems' reverse sweep through Lᵀ
   SymSweep sym{h.ukp_valid ? h.ukp.as<double>() : nullptr, h.kls.as<double>(), h.n, h.m};
+  if (sym.ukp && w_rev && (sel & LU_SEL_NOPIV) && npmax <= SOLVE_STATIC && h.sym_lean) {
+    // the left-looking route's factors (every blocked problem P-symmetric): the lean sweep kernel
+    if (ent <= 1 && h.sym_lean == 2)   // every workgroup of a 1024-problem batch resident (spills 22 VGPRs)
+      hipLaunchKernelGGL((blu_sym2_kernel<1, 8>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, meta,
+                         w_rev, w_fwd, x_rev, x_fwd, sym);
+    else if (ent <= 1)
+      hipLaunchKernelGGL((blu_sym2_kernel<1, 5>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, meta,
+                         w_rev, w_fwd, x_rev, x_fwd, sym);
+    else if (ent == 2)
+      hipLaunchKernelGGL((blu_sym2_kernel<2, 2>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, meta,
+                         w_rev, w_fwd, x_rev, x_fwd, sym);
+    else
+      hipLaunchKernelGGL((blu_sym2_kernel<3, 2>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, meta,
+                         w_rev, w_fwd, x_rev, x_fwd, sym);
+    DOPT_CHECK_HIP(hipGetLastError());
+    sel &= ~LU_SEL_NOPIV;
+    if (!sel) return;
+  }
 #define DOPT_SOLVE2(E, T)                                                                         \
   solve_lds_optin(blu_solve2_kernel<E, T>, T ? lds : 0);                                          \
   hipLaunchKernelGGL((blu_solve2_kernel<E, T>), dim3(2 * B), dim3(PT), T ? lds : 0, h.stream, K, h.ld, h.nmax, perm, \
