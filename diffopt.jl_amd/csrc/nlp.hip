@@ -369,7 +369,27 @@ __global__ __launch_bounds__(NT) void nlp_jac_out_kernel(NLPDims d, const double
 // The reduced route's right-hand sides: the full one r (rows of M, stride
 // nmax) → R's (n + c), per direction (trans: Mᵀ); full-route problems copy r.
 // Grid (B, k): right-hand side j of problem b at (j·B + b)·nmax.
-// Dynamic LDS: rr (num_w), known z (num_w), known y (c).
+// Dynamic LDS: rr (num_w), known z (num_w), known y (c); the masks and their
+// compacted lists (ints).
+// Deterministic compaction by wave 0: out[0..*cnt) = the indices i < len with
+// pred(i), ascending (ballot + prefix popcount; the order, and so every
+// summation over the list, is the same run to run).  Caller syncs after.
+template <class F>
+__device__ __forceinline__ void wave_compact(int len, F pred, int* out, int* cnt) {
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int base = 0;
+  for (int i0 = 0; i0 < len; i0 += 64) {
+    const int i = i0 + lane;
+    const bool p = i < len && pred(i);
+    const unsigned long long m = __ballot(p);
+    if (p) out[base + __popcll(m & below)] = i;
+    base += __popcll(m);
+  }
+  if (lane == 0) *cnt = base;
+}
+
 __device__ __forceinline__ void red_rr(const NLPDims& d, const NLPMap& mp, const NLPIn& in, size_t b, int trans,
                                        const double* r, double* rr, double* zk) {
   const int lo0 = d.num_w + d.c, up0 = lo0 + d.nlo;
@@ -413,17 +433,25 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
   double *rr = sm, *zk = sm + w, *yv = sm + 2 * w;
   int* kx = reinterpret_cast<int*>(sm + 2 * w + c);   // the masks, staged
   int* ys = kx + w;
+  int* kl = ys + c;    // known x, compacted (n)
+  int* yl1 = kl + n;   // rows with y known, compacted (c)
+  int* cnt = yl1 + c;  // [#known x, #known y]
   const double* rho = Rd.rho + b * c;
   for (int j = t; j < w; j += NT) kx[j] = Rd.kx[b * w + j];
   for (int k = t; k < c; k += NT) ys[k] = Rd.yst[b * c + k];
   red_rr(d, mp, in, b, trans, r, rr, zk);
   __syncthreads();
   for (int k = t; k < c; k += NT) yv[k] = ys[k] == 1 ? -rr[mp.slack_of_row[k]] : 0.0;
+  wave_compact(n, [&](int j) { return kx[j] >= 0; }, kl, cnt);
+  wave_compact(c, [&](int k) { return ys[k] == 1; }, yl1, cnt + 1);
   __syncthreads();
+  const int nkx = cnt[0], nky = cnt[1];
   const double* H = in.Hxx + b * n * n;
   const double* J = in.Jx + b * c * n;
   // W for M, Wᵀ for Mᵀ — column-major H read with the lanes along i whenever
-  // H is exactly symmetric (meta.sym: the two coincide)
+  // H is exactly symmetric (meta.sym: the two coincide); only the known
+  // columns are visited (the compacted lists: no per-column branch, the
+  // loads of several columns in flight)
   const bool hcol = !trans || meta[b].sym;
   for (int i = t; i < nmax; i += NT) {
     double v = 0.0;
@@ -432,10 +460,14 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
         v = zk[i];
       } else {
         v = rr[i];
-        for (int j = 0; j < n; ++j)   // known x
-          if (kx[j] >= 0) v -= (hcol ? H[(size_t)j * n + i] : H[(size_t)i * n + j]) * zk[j];
-        for (int k = 0; k < c; ++k)
-          if (ys[k] == 1) v -= J[(size_t)i * c + k] * yv[k];
+        if (hcol) {
+#pragma unroll 4
+          for (int q = 0; q < nkx; ++q) v -= H[(size_t)kl[q] * n + i] * zk[kl[q]];
+        } else {
+#pragma unroll 4
+          for (int q = 0; q < nkx; ++q) v -= H[(size_t)i * n + kl[q]] * zk[kl[q]];
+        }
+        for (int q = 0; q < nky; ++q) v -= J[(size_t)i * c + yl1[q]] * yv[yl1[q]];
       }
     } else if (i < N) {
       const int k = i - n;
@@ -446,8 +478,8 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
         const int s = mp.slack_of_row[k];
         if (s >= 0 && kx[s] >= 0) v += zk[s];
         if (ys[k] == 2) v += rho[k] * rr[s];
-        for (int j = 0; j < n; ++j)
-          if (kx[j] >= 0) v -= J[(size_t)j * c + k] * zk[j];
+#pragma unroll 4
+        for (int q = 0; q < nkx; ++q) v -= J[(size_t)kl[q] * c + k] * zk[kl[q]];
       }
     }
     o[i] = v;
@@ -456,7 +488,8 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
 
 // The reduced route's solution of R (x, stride nmax) → the full one of M /
 // Mᵀ (rows); full-route problems copy.  Grid (B, k) as above.  Dynamic LDS:
-// rr (num_w), known z (num_w), z over w (num_w).
+// rr (num_w), known z (num_w), z over w (num_w), y (c); the masks and the
+// compacted active primal bounds (ints).
 __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap mp, NLPIn in, NLPRed Rd,
                                                              const int32_t* __restrict__ shift, int trans,
                                                              const double* __restrict__ rfull,
@@ -477,6 +510,8 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
   double *rr = sm, *zk = sm + w, *zw = sm + 2 * w, *yl = sm + 3 * w;
   int* kx = reinterpret_cast<int*>(sm + 3 * w + c);   // the masks, staged
   int* ys = kx + w;
+  int* al = ys + c;    // primal variables fixed by an active bound, compacted (n)
+  int* cnt = al + n;
   for (int j = t; j < w; j += NT) kx[j] = Rd.kx[b * w + j];
   for (int k = t; k < c; k += NT) ys[k] = Rd.yst[b * c + k];
   const double* rho = Rd.rho + b * c;
@@ -492,6 +527,7 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
     z[w + k] = xr[n + k];
   }
   __syncthreads();
+  wave_compact(n, [&](int j) { return kx[j] >= 0; }, al, cnt);   // wave 0
   for (int s = n + t; s < w; s += NT) {   // slacks
     const int k = mp.row_of_slack[s - n];
     double v;
@@ -507,13 +543,12 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
   }
   __syncthreads();
   for (int j = t; j < w; j += NT) z[j] = zw[j];
-  // the bound rows' unknowns
-  const int lo0 = w + c, up0 = lo0 + d.nlo;
+  // the bound rows' unknowns (lower block then upper: row lo0 + q for bound q)
+  const int lo0 = w + c;
   for (int q = t; q < d.nlo + d.nup; q += NT) {
     const bool low = q < d.nlo;
     const int i = low ? q : q - d.nlo;
     const int j = low ? mp.low_idx[i] : mp.up_idx[i];
-    const int row = low ? lo0 + i : up0 + i;
     double dd, V;
     if (low) {
       const double xl = j < n ? in.xl[b * n + j] : 0.0;
@@ -526,18 +561,30 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
     }
     const double cf = low ? -1.0 : 1.0;
     const double a = trans ? cf : V, bc = trans ? V : cf;
-    double v;
-    if (dd != 0.0) {
-      v = (r[row] - a * zw[j]) / dd;
-    } else if (j < n) {   // row j: (W x)_j + δ_j x_j + (Jᵀ y)_j + b·z_ν = r̃_j
-      double acc = rr[j] - dl[j] * zw[j];
-      for (int jj = 0; jj < n; ++jj) acc -= (hrow ? H[(size_t)j * n + jj] : H[(size_t)jj * n + j]) * zw[jj];
-      for (int k = 0; k < c; ++k) acc -= J[(size_t)j * c + k] * yl[k];
-      v = acc / bc;
-    } else {              // slack row: −y_k + b·z_ν = r̃_t
-      v = (rr[j] + yl[mp.row_of_slack[j - n]]) / bc;
+    if (dd != 0.0)
+      z[lo0 + q] = (r[lo0 + q] - a * zw[j]) / dd;
+    else if (j >= n)   // slack row: −y_k + b·z_ν = r̃_t
+      z[lo0 + q] = (rr[j] + yl[mp.row_of_slack[j - n]]) / bc;
+    // an active bound on a primal variable: below
+  }
+  // row j of an active primal bound q = kx[j]:
+  //   (W x)_j + δ_j x_j + (Jᵀ y)_j + b·z_ν = r̃_j,
+  // 16 lanes per row (one 128-byte line per group load), 16 rows at a time
+  const int na = cnt[0], g = t >> 4, gl = t & 15;
+  for (int e = g; e < na; e += NT / 16) {
+    const int j = al[e], q = kx[j];
+    const bool low = q < d.nlo;
+    double acc = 0.0;
+#pragma unroll 4
+    for (int jj = gl; jj < n; jj += 16) acc = fma(hrow ? H[(size_t)j * n + jj] : H[(size_t)jj * n + j], zw[jj], acc);
+#pragma unroll 4
+    for (int k = gl; k < c; k += 16) acc = fma(J[(size_t)j * c + k], yl[k], acc);
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    if (gl == 0) {
+      const double bc = trans ? (low ? nlp_VL(d, mp, in, b, j) : nlp_VU(d, mp, in, b, j)) : (low ? -1.0 : 1.0);
+      z[lo0 + q] = (rr[j] - dl[j] * zw[j] - acc) / bc;
     }
-    z[row] = v;
   }
 }
 
@@ -610,7 +657,7 @@ void assemble(Handle& h, const int32_t* plist, int count) {
 // full right-hand sides (k per problem) → the system each problem factorised
 void red_rhs(Handle& h, int trans, int k, const double* rfull, double* rred) {
   const size_t w = h.nlp_num_w, c = h.m;
-  const size_t lds = (2 * w + c) * sizeof(double) + (w + c) * sizeof(int);
+  const size_t lds = (2 * w + c) * sizeof(double) + (w + c + h.n + c + 2) * sizeof(int);
   hipLaunchKernelGGL(nlp_red_rhs_kernel, dim3((unsigned)h.batch, (unsigned)k), dim3(NT), lds, h.stream, dims(h),
                      map_of(h), inputs(h), red_of(h), h.nlp_shift.as<int32_t>(), trans, rfull, rred, h.nmax,
                      h.meta.as<QPMeta>());
@@ -618,7 +665,7 @@ void red_rhs(Handle& h, int trans, int k, const double* rfull, double* rred) {
 }
 void red_recover(Handle& h, int trans, int k, const double* rfull, const double* xred, double* zfull) {
   const size_t w = h.nlp_num_w, c = h.m;
-  const size_t lds = (3 * w + c) * sizeof(double) + (w + c) * sizeof(int);
+  const size_t lds = (3 * w + c) * sizeof(double) + (w + c + h.n + 1) * sizeof(int);
   hipLaunchKernelGGL(nlp_red_recover_kernel, dim3((unsigned)h.batch, (unsigned)k), dim3(NT), lds, h.stream,
                      dims(h), map_of(h), inputs(h), red_of(h), h.nlp_shift.as<int32_t>(), trans, rfull, xred, zfull,
                      h.nmax, h.meta.as<QPMeta>());

@@ -953,6 +953,131 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   }
 }
 
+// One direction through a P-symmetric no-pivot factor (only L stored): with
+// P·K symmetric, U = D_u·P⁻¹·Lᵀ·P, so
+//   K w = r:   L y = r,  Lᵀ (P w) = y ./ (u/p),  w = (P w) ./ p;
+//   Kᵀ x = c:  Kᵀ = P·K·P⁻¹, so x = p .* w with K w = c ./ p.
+// Forward sweep by row segments of L (contiguous per entry), backward by
+// column segments (contiguous across entries), both in halves of 16 rows /
+// columns; no U, no permutation.
+template <int ENT, int WPE>
+__global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(WPE))) void blu_symsolve_kernel(
+    const double* __restrict__ K, int ld, int nmax, const double* __restrict__ dinv, size_t dstride,
+    const QPMeta* __restrict__ meta, int trans, const double* __restrict__ rhs, double* __restrict__ xout,
+    SymSweep sym) {
+  __shared__ double v[SOLVE_STATIC], part[BNB];
+  const int b = blockIdx.x;
+  const QPMeta mm = meta[b];
+  const int Np = blocked_np(mm);
+  if (Np == 0 || mm.lu != LU_NOPIV || !mm.sym) return;   // workgroup-uniform
+  const int N = mm.nsys;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const double* Kb = K + (size_t)b * nmax * ld;
+  const double* Dbase = dinv + (size_t)b * dstride;
+  const double* udb = sym.ukp + (size_t)b * nmax;
+  const PScale psc{sym.kls ? sym.kls + (size_t)b * sym.m : nullptr, sym.n, mm.nk};
+  const double* rb = rhs + (size_t)b * nmax;
+  for (int i = t; i < Np; i += PT) v[i] = i < N ? (trans ? rb[i] / psc(i) : rb[i]) : 0.0;
+  __syncthreads();
+  const int nblk = Np / BNB;
+  // forward: L y = r (block k: y_k = L_kk⁻¹ v_k, then v_e −= L[e][k-block]·y_k
+  // for e past it): row segments, 8 lanes per row × 4 doubles (one wave load
+  // touches 8 rows' lines), 64 rows per pass, up to SCH passes in flight
+  // across the diagonal solve
+  {
+    constexpr int SCH = 4;   // passes per chunk: 16 doubles in flight, no spill at WPE 5
+    const int g8 = t & 7, rid = t >> 3;
+    for (int bk = 0; bk < nblk; ++bk) {
+      const int i0 = bk * BNB, e0 = i0 + BNB, ecnt = Np - e0;
+      const int npass = (ecnt + RPASS - 1) / RPASS;
+      double f[SCH][4];
+      auto load_chunk = [&](int c) {
+#pragma unroll
+        for (int p = 0; p < SCH; ++p) {
+          if ((c * SCH + p) * RPASS >= ecnt) break;   // uniform
+          const int li = (c * SCH + p) * RPASS + rid;
+          const int ec = li < ecnt ? e0 + li : i0;
+          const double* row = Kb + (size_t)ec * ld + i0 + 4 * g8;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) f[p][u] = row[u];
+        }
+      };
+      if (npass > 0) load_chunk(0);
+      if (wv == 0 && lane < BNB) {
+        const double* Dk = Dbase + (size_t)bk * BDINV + lane * BNB;   // row `lane` of L⁻¹
+        double acc = 0.0;
+#pragma unroll 8
+        for (int j = 0; j < BNB; ++j) acc = fma(Dk[j], v[i0 + j], acc);
+        part[lane] = acc;
+      }
+      __syncthreads();
+      if (wv == 0 && lane < BNB) v[i0 + lane] = part[lane];
+      double xk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xk[u] = part[4 * g8 + u];
+      for (int c = 0; c * SCH < npass; ++c) {
+        if (c > 0) load_chunk(c);
+#pragma unroll
+        for (int p = 0; p < SCH; ++p) {
+          if ((c * SCH + p) * RPASS >= ecnt) break;
+          double d = f[p][0] * xk[0];
+#pragma unroll
+          for (int u = 1; u < 4; ++u) d = fma(f[p][u], xk[u], d);
+          d += __shfl_xor(d, 1);
+          d += __shfl_xor(d, 2);
+          d += __shfl_xor(d, 4);
+          const int li = (c * SCH + p) * RPASS + rid;
+          if (g8 == 0 && li < ecnt) v[e0 + li] -= d;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = t; i < Np; i += PT) v[i] /= udb[i];   // y ./ (u/p)
+  __syncthreads();
+  // backward: Lᵀ (P w) = v
+  for (int s = 0; s < nblk; ++s) {
+    const int bk = nblk - 1 - s;
+    const int i0 = bk * BNB;
+    double f[ENT][16];
+#pragma unroll
+    for (int q = 0; q < ENT; ++q) {
+      const int e = t + PT * q;
+      const int ec = e < i0 ? e : 0;
+      if (q * PT >= i0) continue;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) f[q][j] = Kb[(size_t)(i0 + j) * ld + ec];
+    }
+    if (wv == 0 && lane < BNB) {
+      const double* Dk = Dbase + (size_t)bk * BDINV;
+      double acc = 0.0;
+#pragma unroll 8
+      for (int j = 0; j < BNB; ++j) acc = fma(Dk[lane + j * BNB], v[i0 + j], acc);
+      part[lane] = acc;
+    }
+    __syncthreads();
+    if (wv == 0 && lane < BNB) v[i0 + lane] = part[lane];
+#pragma unroll
+    for (int q = 0; q < ENT; ++q) {
+      const int e = t + PT * q;
+      if (q * PT >= i0) continue;
+      const bool has = e < i0;
+      const int ec = has ? e : 0;
+      double a = has ? v[e] : 0.0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) a = fma(-f[q][j], part[j], a);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) f[q][j] = Kb[(size_t)(i0 + 16 + j) * ld + ec];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) a = fma(-f[q][j], part[16 + j], a);
+      if (has) v[e] = a;
+    }
+    __syncthreads();
+  }
+  double* xb = xout + (size_t)b * nmax;
+  for (int i = t; i < N; i += PT) xb[i] = trans ? v[i] : v[i] / psc(i);   // Kᵀ: p .* w = (P w); K: w = (P w) ./ p
+}
+
 }  // namespace
 
 // Partial-pivoting blocked LU of `count` problems (plist: their indices; null
@@ -1021,7 +1146,6 @@ static void solve_lds_optin(KF kf, size_t lds) {
 }
 
 void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rhs, double* x, int sel) {
-  qp_nopiv_materialize_u(h);
   const int npmax = h.blocked_npmax;
   if (npmax == 0) return;
   const int B = (int)h.batch;
@@ -1030,6 +1154,22 @@ void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rh
   const int32_t* perm = h.ipiv.as<int32_t>();
   const QPMeta* meta = h.meta.as<QPMeta>();
   const size_t lds = solve_lds_bytes(h.nmax);
+  if (h.ukp_valid && h.sym_lean && (sel & LU_SEL_NOPIV) && npmax <= SOLVE_STATIC) {
+    // the left-looking route's P-symmetric factors: through L alone (no U)
+    SymSweep sym{h.ukp.as<double>(), h.kind == DOPT_KIND_QP ? h.kls.as<double>() : nullptr, h.n, h.m};
+    const int ent = (npmax + PT - 1) / PT;
+#define DOPT_SYMSOLVE(E, W)                                                                                   \
+  hipLaunchKernelGGL((blu_symsolve_kernel<E, W>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, \
+                     meta, trans, rhs, x, sym)
+    if (ent <= 1) { DOPT_SYMSOLVE(1, 5); }
+    else if (ent == 2) { DOPT_SYMSOLVE(2, 2); }
+    else { DOPT_SYMSOLVE(3, 2); }
+#undef DOPT_SYMSOLVE
+    DOPT_CHECK_HIP(hipGetLastError());
+    sel &= ~LU_SEL_NOPIV;   // every no-pivot problem of the route is P-symmetric
+    if (!sel) return;
+  }
+  if (sel & LU_SEL_NOPIV) qp_nopiv_materialize_u(h);   // the general sweeps read U
   if (!trans) {
     solve_lds_optin(blu_solve_rows_kernel, lds);
     hipLaunchKernelGGL(blu_solve_rows_kernel, dim3(B), dim3(PT), lds, h.stream, K, h.ld, h.nmax, perm,
