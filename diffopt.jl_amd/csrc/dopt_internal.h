@@ -143,6 +143,7 @@ struct Handle {
   int32_t left_mode = 1;           // P-symmetric batches: left-looking LU (env DOPT_LEFT=0: right-looking)
   int32_t lstreams = 0;            // left-looking LU: column tiles I ≥ J+2 on `aux` (env DOPT_LSTREAMS=1)
   DevBuf ukp;                      // left-looking LU: u_kk / p_k of every finished diagonal block (nmax per problem)
+  int32_t lcol_tw = 1;             // left-looking LU column tiles per workgroup (env DOPT_LCOL_TW: 1 or 2)
   int32_t sym_lean = 1;            // fused P-symmetric sweeps in their own lean kernel (env DOPT_SYM_LEAN=0: inside
                                    // blu_solve2_kernel)
   bool ukp_valid = false;          // the last no-pivot factorisation was left-looking (ukp holds its u_kk / p_k)

@@ -1652,30 +1652,50 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
   if (t < Wv) ud[c0 + t] = 1.0 / (S[t * SLD + t] * ps(c0 + t));
 }
 
-// Tiles (I, J), I ≥ J+1, of block column J = c0 / 64 (one 256-thread WG per
-// tile, XCD-aware order: one problem's tiles are consecutive): C(I, J) by
-// MFMA over the staged row strips L(J, k) (B operand) and this tile's row
-// strips L(I, k)·D_k (A operand), then the TRSM by the packed inverse of the
-// diagonal block (binv) with the threshold test, L(I, J) → K, and
-// U(J, I) = D_J·L(I, J)ᵀ·P_I beside it (transposed through LDS; growth bound).
-template <class SRC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_lcol_kernel(
+// stage_rowstrip by NTH threads (NTH = 256 or 512): 16·256/NTH columns each
+template <int NTH>
+__device__ __forceinline__ void stage_rowstrip_n(double* X, const double* Kb, int ld, int c0, int k0) {
+  constexpr int CW = 16 * 256 / NTH, PR = NB64 / CW;   // columns per thread, threads per row
+  const int t = threadIdx.x, j = t / PR, kq = (t % PR) * CW;
+  double v[CW];
+  const double* src = Kb + (size_t)(c0 + j) * ld + k0 + kq;
+#pragma unroll
+  for (int u = 0; u < CW; ++u) v[u] = src[u];
+#pragma unroll
+  for (int u = 0; u < CW; ++u) X[(kq + u) * TLD + j] = v[u];
+}
+
+// Tiles (I, J), I ≥ J+1, of block column J = c0 / 64: TW tiles per workgroup
+// (256 threads each, tiles I and I+1 when TW = 2, sharing the staged row strip
+// L(J, k) and the U11⁻¹ load; XCD-aware order: one problem's tiles are
+// consecutive).  C(I, J) by MFMA over the staged strips L(J, k) (B operand)
+// and the tile's own row strips L(I, k)·D_k (A operand), then the TRSM by the
+// packed inverse of the diagonal block (binv) with the threshold test and the
+// growth bound on U(J, I) = D_J·L(I, J)ᵀ·P_I; L(I, J) → K (U is not stored:
+// nlu_sym_u_kernel when a solve needs it).  `ngrp` workgroups per problem,
+// `cnt` tiles per problem from tile `toff` on.
+template <class SRC, int TW>
+__global__ __launch_bounds__(256 * TW) __attribute__((amdgpu_waves_per_eu(4))) void nlu_lcol_kernel(
     double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
-    const double* __restrict__ ukp, int ntile, int toff, int total, const double* __restrict__ kamax,
-    const double* __restrict__ kls, int n, int m, SRC src, int wr_u) {
-  __shared__ double X[NB64 * TLD];
+    const double* __restrict__ ukp, int ngrp, int cnt, int toff, int total, const double* __restrict__ kamax,
+    const double* __restrict__ kls, int n, int m, SRC src) {
+  constexpr int NTH = 256 * TW;
+  __shared__ double X[TW][NB64 * TLD];   // X[0]: staged strip / U11⁻¹ (shared); X[h]: tile h's transposes
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
   const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
-  const int b = logical / ntile;
-  const int it = logical - b * ntile;
+  const int b = logical / ngrp;
+  const int it0 = (logical - b * ngrp) * TW;
   const QPMeta mm = meta[b];
   const int Np = nlu_np(mm);
-  const int r0 = c0 + NB64 + 64 * (toff + it);   // first row of tile I
-  if (mm.lu == LU_REJECT || r0 >= Np) return;    // workgroup-uniform
-  const int sw = min(NB64, Np - r0);             // 32 or 64 rows
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
+  if (mm.lu == LU_REJECT || c0 + NB64 + 64 * (toff + it0) >= Np) return;   // workgroup-uniform
+  const int T = threadIdx.x, half = T >> 8, t = T & 255;
+  const int it = it0 + half;
+  const int r0 = c0 + NB64 + 64 * (toff + it);   // first row of this half's tile I
+  const int sw = it < cnt && r0 < Np ? min(NB64, Np - r0) : 0;   // 0, 32 or 64 rows
+  const int lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
   const bool wact = 16 * wv < sw;                // wave-uniform
+  double* Xh = X[half];
   double* Kb = K + (size_t)b * nmax * ld;
   const double* ud = ukp + (size_t)b * nmax;
   const double* Bg = binv + (size_t)b * BSTR;
@@ -1693,14 +1713,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
       for (int s = 0; s < 16; ++s) a[s] = ar[4 * s + g] * ud[k0 + 4 * s + g];
     }
     __syncthreads();
-    stage_rowstrip(X, Kb, ld, c0, k0, NB64);   // block J is full (tiles follow it)
+    stage_rowstrip_n<NTH>(X[0], Kb, ld, c0, k0);   // block J is full (tiles follow it)
     __syncthreads();
     if (wact) {
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         double bq[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) bq[q] = X[(4 * s + g) * TLD + 16 * q + l16];
+        for (int q = 0; q < 4; ++q) bq[q] = X[0][(4 * s + g) * TLD + 16 * q + l16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] = nmfma(a[s], bq[q], acc[q]);
       }
@@ -1710,9 +1730,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
   // k-step s ↔ column 4s + g): the sources read with the lanes along the
   // rows, the update transposed through LDS
   // U11⁻¹ (L2) loaded together with the sources: one round trip
-  double av[16], v[16];
+  constexpr int VQ = 16 / TW;
+  double av[16], v[VQ];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) v[q] = Bg[t + 256 * q];
+  for (int q = 0; q < VQ; ++q) v[q] = Bg[T + NTH * q];
   if (wact) {
 #pragma unroll
     for (int s = 0; s < 16; ++s) av[s] = src_val_lower(sv, r0 + 16 * wv + l16, c0 + 4 * s + g);
@@ -1725,69 +1746,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
         const int j = 16 * q + l16;
         const double pj = ps(c0 + j);
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) X[(16 * wv + g + 4 * rr) * TLD + j] = acc[q][rr] * pj;
+        for (int rr = 0; rr < 4; ++rr) Xh[(16 * wv + g + 4 * rr) * TLD + j] = acc[q][rr] * pj;
       }
     }
     __syncthreads();
     if (wact) {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) av[s] -= X[(16 * wv + l16) * TLD + 4 * s + g];
+      for (int s = 0; s < 16; ++s) av[s] -= Xh[(16 * wv + l16) * TLD + 4 * s + g];
     }
-    __syncthreads();   // every wave holds its C rows before U11⁻¹ overwrites X
+    __syncthreads();   // every wave holds its C rows before U11⁻¹ overwrites X[0]
   }
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {   // U11⁻¹: upper triangle, zero below
-    const int e = t + 256 * q, k = e >> 6, c = e & 63;
-    X[k * TLD + c] = k <= c ? v[q] : 0.0;
+  for (int q = 0; q < VQ; ++q) {   // U11⁻¹: upper triangle, zero below
+    const int e = T + NTH * q, k = e >> 6, c = e & 63;
+    X[0][k * TLD + c] = k <= c ? v[q] : 0.0;
   }
   __syncthreads();
+  if (!wact) return;   // no barrier below
   d4n lt[4];
   int over = 0;
-  if (wact) {
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {   // U11⁻¹ is upper: k ≤ 16ct + 15
-      lt[ct] = (d4n){0, 0, 0, 0};
+  for (int ct = 0; ct < 4; ++ct) {   // U11⁻¹ is upper: k ≤ 16ct + 15
+    lt[ct] = (d4n){0, 0, 0, 0};
 #pragma unroll
-      for (int s = 0; s < 4 * (ct + 1); ++s) lt[ct] = nmfma(av[s], X[(4 * s + g) * TLD + 16 * ct + l16], lt[ct]);
-    }
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        Kb[(size_t)(r0 + 16 * wv + g + 4 * rr) * ld + c0 + 16 * ct + l16] = lt[ct][rr];
-        over |= !(fabs(lt[ct][rr]) <= NOPIV_LMAX);
-      }
+    for (int s = 0; s < 4 * (ct + 1); ++s) lt[ct] = nmfma(av[s], X[0][(4 * s + g) * TLD + 16 * ct + l16], lt[ct]);
   }
-  if (wr_u) __syncthreads();   // every wave is done with U11⁻¹
-  if (wact) {   // U(J, I)[k][jl] = (u_kk / p_k)·L[jl][k]·p_jl: the growth bound; stored when wr_u
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      const int k = 16 * ct + l16;
-      const double uk = ud[c0 + k];
+  for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int jl = 16 * wv + g + 4 * rr;
-        const double u = uk * lt[ct][rr] * ps(r0 + jl);
-        if (wr_u) X[k * TLD + jl] = u;
-        over |= !(fabs(u) <= bound);
-      }
+    for (int rr = 0; rr < 4; ++rr) {
+      Kb[(size_t)(r0 + 16 * wv + g + 4 * rr) * ld + c0 + 16 * ct + l16] = lt[ct][rr];
+      over |= !(fabs(lt[ct][rr]) <= NOPIV_LMAX);
     }
+  // U(J, I)[k][jl] = (u_kk / p_k)·L[jl][k]·p_jl: the growth bound
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    const double uk = ud[c0 + 16 * ct + l16];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) over |= !(fabs(uk * lt[ct][rr] * ps(r0 + 16 * wv + g + 4 * rr)) <= bound);
   }
   if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;   // every writer stores the same value
-  if (!wr_u) return;   // workgroup-uniform
-  __syncthreads();
-  const int k = t >> 2, cq = (t & 3) * 16;   // row k of block J, 16 columns
-  if (cq < sw) {
-#pragma unroll
-    for (int u = 0; u < 16; ++u) Kb[(size_t)(c0 + k) * ld + r0 + cq + u] = X[k * TLD + cq + u];
-  }
 }
 
 // U of the left-looking route's P-symmetric factors, materialised from L for
 // the solves that read it (single-direction and multi-RHS solves; the fused
 // call's solves sweep Lᵀ both ways and the LU does not store U): every tile
 // (I > J) of the 64-grid, U(J, I)[k][j] = (u_kk / p_k)·L(I, J)[j][k]·p_j —
-// what nlu_lcol_kernel writes when wr_u is set.  One 256-thread WG per (tile,
+// what the right-looking route's TRSM stores beside L.  One 256-thread WG per (tile,
 // problem); problems that are not P-symmetric no-pivot factors are skipped.
 __global__ __launch_bounds__(256) void nlu_sym_u_kernel(double* __restrict__ K, int ld, int nmax,
                                                         const QPMeta* __restrict__ meta,
@@ -1855,10 +1860,16 @@ static void left_lu(Handle& h, const SRC& src, double* dinv, double* w0, double*
   }
   auto lcol = [&](hipStream_t st, int c0, double* bv, int toff, int cnt) {
     if (cnt <= 0) return;
-    const long long tot = (long long)cnt * B;
+    const int tw = h.lcol_tw == 2 && cnt > 1 ? 2 : 1;   // tiles per workgroup
+    const int ngrp = (cnt + tw - 1) / tw;
+    const long long tot = (long long)ngrp * B;
     if (tot > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
-    hipLaunchKernelGGL(nlu_lcol_kernel<SRC>, dim3((unsigned)tot), dim3(256), 0, st, K, h.ld, h.nmax, meta, c0, bv, ukp,
-                       cnt, toff, (int)tot, kamax, kls, h.n, h.m, src, 0);
+    if (tw == 2)
+      hipLaunchKernelGGL((nlu_lcol_kernel<SRC, 2>), dim3((unsigned)tot), dim3(512), 0, st, K, h.ld, h.nmax, meta, c0,
+                         bv, ukp, ngrp, cnt, toff, (int)tot, kamax, kls, h.n, h.m, src);
+    else
+      hipLaunchKernelGGL((nlu_lcol_kernel<SRC, 1>), dim3((unsigned)tot), dim3(256), 0, st, K, h.ld, h.nmax, meta, c0,
+                         bv, ukp, ngrp, cnt, toff, (int)tot, kamax, kls, h.n, h.m, src);
     DOPT_CHECK_HIP(hipGetLastError());
   };
   bool pending = false;   // T holds column tiles S must wait for
