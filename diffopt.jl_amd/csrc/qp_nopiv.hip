@@ -1541,8 +1541,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
 
 // stage the row strip L(J, k): rows c0 .. c0+63 (zero from row `rows` on),
 // columns k0 .. k0+63 of K, transposed: X[kk·TLD + j] = L[c0 + j][k0 + kk]
+// (lane ↔ row, 16 columns per thread: conflict-free LDS stores)
 __device__ __forceinline__ void stage_rowstrip(double* X, const double* Kb, int ld, int c0, int k0, int rows) {
-  const int t = threadIdx.x, j = t >> 2, kq = (t & 3) * 16;
+  const int t = threadIdx.x, j = t & 63, kq = (t >> 6) * 16;
   double v[16];
   const double* src = Kb + (size_t)(c0 + (j < rows ? j : 0)) * ld + k0 + kq;
 #pragma unroll
@@ -1653,10 +1654,13 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
 }
 
 // stage_rowstrip by NTH threads (NTH = 256 or 512): 16·256/NTH columns each
+// (lane ↔ row: a 16-lane store group writes 16 consecutive rows of one
+// column, conflict-free; a (row, column-quarter) mapping stores 4 rows × 4
+// quarters per group, 4-way)
 template <int NTH>
 __device__ __forceinline__ void stage_rowstrip_n(double* X, const double* Kb, int ld, int c0, int k0) {
-  constexpr int CW = 16 * 256 / NTH, PR = NB64 / CW;   // columns per thread, threads per row
-  const int t = threadIdx.x, j = t / PR, kq = (t % PR) * CW;
+  constexpr int CW = 16 * 256 / NTH;   // columns per thread
+  const int t = threadIdx.x, j = t & 63, kq = (t >> 6) * CW;
   double v[CW];
   const double* src = Kb + (size_t)(c0 + j) * ld + k0 + kq;
 #pragma unroll
