@@ -1582,48 +1582,75 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
     amax = fmax(amax, src.qmax[b]);
     if (t == 0) kamax[b] = amax;
   }
-  // ---- the left-looking update of C(J, J) over k < J
-  d4n accd[4];
+  // ---- the left-looking update of C(J, J) over k < J.  X = Σ_k L(J, k)·D_k·
+  // L(J, k)ᵀ is symmetric: only its ten lower 16×16 tiles are formed (3, 3,
+  // 2, 2 per wave; rows ra / rb = 3 of the 4×4 tile grid), mirrored through
+  // LDS afterwards:
+  //   w0: (0,0) (3,0) (3,1)   w1: (1,0) (1,1) (3,2)   w2: (2,0) (2,1)   w3: (2,2) (3,3)
+  d4n accd[3];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) accd[q] = (d4n){0, 0, 0, 0};
+  for (int q = 0; q < 3; ++q) accd[q] = (d4n){0, 0, 0, 0};
   double sweep = 0.0;   // t < 64: Σ L(J, <J)[t]·y (w0); 64 ≤ t < 128: Σ L(J, <J)[t − 64]·(d∘z) (w1)
-  const bool dact = 16 * wv < Wv;   // wave-uniform
+  const int ra = wv < 3 ? wv : 2;                       // row of tile 0 (and tile 1 on w1 / w2)
+  const int tc0 = wv == 3 ? 2 : 0;                      // column of tile 0 (row ra)
+  const bool t1b = wv == 0 || wv == 3;                  // tile 1 on row 3
+  const int tc1 = wv == 0 ? 0 : (wv == 3 ? 3 : 1);      // column of tile 1
+  const int tc2 = wv == 0 ? 1 : 2;                      // column of tile 2 (row 3; w0, w1 only)
+  const bool dact = 16 * ra < Wv;                       // wave-uniform: tile 0 inside the block
+  const bool bact = Wv > 48 && wv != 2;                 // the row-3 tiles inside the block
   for (int k0 = 0; k0 < c0; k0 += NB64) {
     double dk[16];   // D_k, for the A operand
 #pragma unroll
     for (int s = 0; s < 16; ++s) dk[s] = ud[k0 + 4 * s + g];
+    // the sweeps' vector blocks (y, d∘z) ride in the strip's padding columns
+    // 64 / 65: one load per thread with the others, not a chain of loads
+    // inside the sweep loop
+    const bool swp = w0b && t < 2 * NB64;
+    double sv = 0.0;
+    if (swp) sv = t < NB64 ? w0b[k0 + t] : ud[k0 + t - NB64] * w1b[k0 + t - NB64];
     __syncthreads();   // the previous strip is consumed
     stage_rowstrip(S, Kb, ld, c0, k0, Wv);
+    if (swp) S[(t & 63) * TLD + NB64 + (t >> 6)] = sv;
     __syncthreads();
     if (dact) {
-      // A operand: this wave's rows of the same staged strip, times D_k
-      double a[16];
-#pragma unroll
-      for (int s = 0; s < 16; ++s) a[s] = S[(4 * s + g) * TLD + 16 * wv + l16] * dk[s];
+      // A operands: rows ra / 3 of the same staged strip, times D_k (read per
+      // k-step: two preloaded A sets would spill)
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
-        double bq[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) bq[q] = S[(4 * s + g) * TLD + 16 * q + l16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) accd[q] = nmfma(a[s], bq[q], accd[q]);
+        const double* row = S + (4 * s + g) * TLD + l16;
+        const double aa = row[16 * ra] * dk[s];
+        const double ab = bact ? row[48] * dk[s] : 0.0;
+        accd[0] = nmfma(aa, row[16 * tc0], accd[0]);
+        if (!t1b || bact) accd[1] = nmfma(t1b ? ab : aa, row[16 * tc1], accd[1]);
+        if (wv < 2 && bact) accd[2] = nmfma(ab, row[16 * tc2], accd[2]);
       }
     }
-    if (w0b && t < 2 * NB64) {   // forward sweeps: the row strip times the finished blocks of y / z
-      const int j = t & 63;
+    if (swp) {   // forward sweeps: the row strip times the finished blocks of y / z
+      const int j = t & 63, vc = NB64 + (t >> 6);
       double sm = 0.0;
-      if (t < NB64) {
-#pragma unroll 8
-        for (int kk = 0; kk < NB64; ++kk) sm = fma(S[kk * TLD + j], w0b[k0 + kk], sm);
-      } else {
-#pragma unroll 8
-        for (int kk = 0; kk < NB64; ++kk) sm = fma(S[kk * TLD + j], ud[k0 + kk] * w1b[k0 + kk], sm);
-      }
+#pragma unroll 16
+      for (int kk = 0; kk < NB64; ++kk) sm = fma(S[kk * TLD + j], S[kk * TLD + vc], sm);
       sweep += sm;
     }
   }
   __syncthreads();   // the staging is consumed: S becomes the diagonal image
-  // C(J, J) = A(J, J) − acc·P_J → S (identity beyond Wv)
+  if (c0 > 0) {   // workgroup-uniform: X's tiles and their mirrors → S
+    auto put = [&](int r, int c, const d4n& x) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int i = 16 * r + g + 4 * rr, j = 16 * c + l16;
+        S[i * SLD + j] = x[rr];
+        if (r != c) S[j * SLD + i] = x[rr];
+      }
+    };
+    if (dact) {
+      put(ra, tc0, accd[0]);
+      if (!t1b || bact) put(t1b ? 3 : ra, tc1, accd[1]);
+      if (wv < 2 && bact) put(3, tc2, accd[2]);
+    }
+    __syncthreads();
+  }
+  // C(J, J) = A(J, J) − X·P_J → S (identity beyond Wv)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int j = 16 * q + l16;
@@ -1632,7 +1659,8 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
     for (int rr = 0; rr < 4; ++rr) {
       const int i = 16 * wv + g + 4 * rr;
       const bool in = i < Wv && j < Wv;
-      S[i * SLD + j] = in ? src_val(sv, c0 + i, c0 + j) - accd[q][rr] * pj : (i == j ? 1.0 : 0.0);
+      const double x = c0 > 0 && in ? S[i * SLD + j] : 0.0;
+      S[i * SLD + j] = in ? src_val(sv, c0 + i, c0 + j) - x * pj : (i == j ? 1.0 : 0.0);
     }
   }
   if (w0b && t < 2 * NB64) {   // block J of b / c minus the finished blocks' contributions
@@ -1861,8 +1889,13 @@ static void left_lu(Handle& h, const SRC& src, double* dinv, double* w0, double*
   if (h.lstreams) {
     ensure_aux(h);
     T = h.aux;
+    if (h.crit) {   // the chain on the high-priority stream, forked from / joined back into h.stream
+      S = h.crit;
+      DOPT_CHECK_HIP(hipEventRecord(h.ev_crit, h.stream));
+      DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_crit, 0));
+    }
   }
-  auto lcol = [&](hipStream_t st, int c0, double* bv, int toff, int cnt) {
+  auto lcol =[&](hipStream_t st, int c0, double* bv, int toff, int cnt) {
     if (cnt <= 0) return;
     const int tw = h.lcol_tw == 2 && cnt > 1 ? 2 : 1;   // tiles per workgroup
     const int ngrp = (cnt + tw - 1) / tw;
@@ -1904,6 +1937,10 @@ static void left_lu(Handle& h, const SRC& src, double* dinv, double* w0, double*
   if (pending) {
     DOPT_CHECK_HIP(hipEventRecord(h.ev_join, T));
     DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_join, 0));
+  }
+  if (S != h.stream) {
+    DOPT_CHECK_HIP(hipEventRecord(h.ev_crit, S));
+    DOPT_CHECK_HIP(hipStreamWaitEvent(h.stream, h.ev_crit, 0));
   }
 }
 
