@@ -99,7 +99,14 @@ constexpr double NOPIV_GROWTH = 1e8;
 struct PScale {
   const double* kl;
   int n, nk;
-  __device__ double operator()(int r) const { return (kl && r >= n && r < n + nk) ? kl[r - n] : 1.0; }
+  // the null test is uniform; the row test selects the index of an
+  // unconditional load (a branch per row made the compiler wait on each load)
+  __device__ double operator()(int r) const {
+    if (!kl) return 1.0;
+    const bool in = r >= n && r < n + nk;
+    const double v = kl[in ? r - n : 0];
+    return in ? v : 1.0;
+  }
 };
 // QP problem inputs / forward tangents as seen by the kernels (device pointers)
 struct QPIn {

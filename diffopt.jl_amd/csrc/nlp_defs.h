@@ -73,29 +73,56 @@ __device__ __forceinline__ bool red_use(const NLPRed& R, const int32_t* shift, i
   return R.on && R.ok[b] && shift[b] == 0;
 }
 
-// R[r][col] of problem b (identity padding past n + c)
+// R[r][col] of problem b (identity padding past n + c).  Two rounds of
+// unconditional loads (the index maps kx / yst, then the selected value and
+// δ): with a branch per case the compiler waited for every load in turn.
 __device__ __forceinline__ double nlp_R(const NLPDims& d, const NLPIn& in, const NLPRed& R, size_t b, int r,
                                         int col) {
   const int n = d.n, N = n + d.c;
-  if (r >= N || col >= N) return r == col ? 1.0 : 0.0;
+  const bool pad = r >= N || col >= N;
+  const int rr = pad ? 0 : r, cc = pad ? 0 : col;
+  const bool rq = rr < n, cq = cc < n;
   const int32_t* kx = R.kx + b * d.num_w;
-  const int32_t* ys = R.yst + b * d.c;
-  if (r < n) {
-    if (kx[r] >= 0) return r == col ? 1.0 : 0.0;
-    if (col < n) {
-      if (kx[col] >= 0) return 0.0;
-      double v = in.Hxx[b * n * n + (size_t)col * n + r];
-      if (col == r) v += R.delta[b * d.num_w + r];
-      return v;
+  const int32_t* ys = d.c ? R.yst + b * d.c : kx;   // (no constraints: never a live read)
+  const int kr = kx[rq ? rr : 0], kc = kx[cq ? cc : 0];
+  const int yr = ys[rq ? 0 : rr - n], yc = ys[cq ? 0 : cc - n];
+  const double* dummy = in.Hxx;
+  const double ident = r == col ? 1.0 : 0.0;
+  double cv = 0.0;
+  int mode = 0;   // 0: the constant cv, 1: the loaded value, 2: its negation
+  bool addd = false;
+  const double* p = dummy;
+  if (pad) {
+    cv = ident;
+  } else if (rq) {
+    if (kr >= 0) {
+      cv = ident;
+    } else if (cq) {
+      if (kc < 0) {
+        mode = 1;
+        p = in.Hxx + b * n * n + (size_t)cc * n + rr;
+        addd = cc == rr;
+      }
+    } else if (yc != 1) {
+      mode = 1;
+      p = in.Jx + b * d.c * n + (size_t)rr * d.c + (cc - n);
     }
-    const int k = col - n;
-    return ys[k] == 1 ? 0.0 : in.Jx[b * d.c * n + (size_t)r * d.c + k];
+  } else {
+    if (yr == 1) {
+      cv = ident;
+    } else if (cq) {
+      if (kc < 0) {
+        mode = 1;
+        p = in.Jx + b * d.c * n + (size_t)cc * d.c + (rr - n);
+      }
+    } else if (cc == rr && yr == 2) {
+      mode = 2;
+      p = R.rho + b * d.c + (rr - n);
+    }
   }
-  const int k = r - n;
-  if (ys[k] == 1) return r == col ? 1.0 : 0.0;
-  if (col < n) return kx[col] >= 0 ? 0.0 : in.Jx[b * d.c * n + (size_t)col * d.c + k];
-  if (col != r) return 0.0;
-  return ys[k] == 2 ? -R.rho[b * d.c + k] : 0.0;
+  const double x = *p;
+  const double dl = *(addd ? R.delta + b * d.num_w + rr : dummy);
+  return mode == 0 ? cv : (mode == 2 ? -x : (addd ? x + dl : x));
 }
 
 

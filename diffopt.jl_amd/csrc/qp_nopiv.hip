@@ -164,35 +164,40 @@ __device__ __forceinline__ QSrcB qsrc(const QSrc& s, int b, const QPMeta& mm) {
   return v;
 }
 // K[r][c] of the reduced system [Q, G_kᵀΛ, Aᵀ; G_k, D(s_k), 0; A, 0, 0]
-// (identity padding past N)
+// (identity padding past N).  Branch-free: the source address is selected
+// and loaded unconditionally (a dead entry loads Q[0]), so a thread's 16
+// entries are 16 loads in flight — with one branch per source the compiler
+// waited for each load before the next (16 round trips per tile).
 __device__ __forceinline__ double kval(const QSrcB& v, int r, int c) {
-  const int n = v.n, nk = v.nk;
-  if (r >= v.N || c >= v.N) return r == c ? 1.0 : 0.0;
-  if (r < n) {
-    if (c < n) return v.Q[(size_t)r * n + c];
-    if (c < n + nk) return v.gk[(size_t)r * v.m + (c - n)] * v.lk[c - n];
-    return v.A[(size_t)r * v.p + (c - n - nk)];
-  }
-  if (r < n + nk) {
-    if (c < n) return v.gk[(size_t)c * v.m + (r - n)];
-    return r == c ? v.sk[r - n] : 0.0;
-  }
-  return c < n ? v.A[(size_t)c * v.p + (r - n - nk)] : 0.0;
+  const int n = v.n, nk = v.nk, rn = r - n, cn = c - n;
+  const bool pad = r >= v.N || c >= v.N;
+  const bool rq = r < n, rg = !rq && rn < nk, cq = c < n, cg = !cq && cn < nk;
+  const double* rowq = rq ? (cq ? v.Q + (size_t)r * n + c
+                                : (cg ? v.gk + (size_t)r * v.m + cn : v.A + (size_t)r * v.p + (cn - nk)))
+                          : nullptr;
+  const double* rowg = cq ? v.gk + (size_t)c * v.m + rn : v.sk + rn;
+  const double* rowa = v.A + (size_t)c * v.p + (rn - nk);
+  const bool live = !pad && (rq || cq || (rg && r == c));
+  const double* p = !live ? v.Q : (rq ? rowq : (rg ? rowg : rowa));
+  const bool lam = !pad && rq && cg;   // G_kᵀ·Λ: times λ_c
+  const double* p2 = lam ? v.lk + cn : v.Q;
+  const double x = *p, y = *p2;
+  return live ? (lam ? x * y : x) : (pad && r == c ? 1.0 : 0.0);
 }
 
 // kval for r > c (strictly lower part): the same values, with Q(r, c) read
 // as stored (column-major, Q[c·n + r]) — lanes along r then coalesce on every
-// source (Q, G_k's column-major copy, A)
+// source (Q, G_k's column-major copy, A).  Branch-free as kval.
 __device__ __forceinline__ double kval_lower(const QSrcB& v, int r, int c) {
-  const int n = v.n, nk = v.nk;
-  if (r >= v.N || c >= v.N) return r == c ? 1.0 : 0.0;
-  if (c < n) {
-    if (r < n) return v.Q[(size_t)c * n + r];
-    if (r < n + nk) return v.gk[(size_t)c * v.m + (r - n)];
-    return v.A[(size_t)c * v.p + (r - n - nk)];
-  }
-  if (r < n + nk) return r == c ? v.sk[r - n] : 0.0;
-  return 0.0;
+  const int n = v.n, nk = v.nk, rn = r - n;
+  const bool pad = r >= v.N || c >= v.N;
+  const bool cq = c < n;
+  const double* colp = r < n ? v.Q + (size_t)c * n + r
+                             : (rn < nk ? v.gk + (size_t)c * v.m + rn : v.A + (size_t)c * v.p + (rn - nk));
+  const bool live = !pad && (cq || (rn >= 0 && rn < nk && r == c));
+  const double* p = !live ? v.Q : (cq ? colp : v.sk + rn);
+  const double x = *p;
+  return live ? x : (pad && r == c ? 1.0 : 0.0);
 }
 
 // The left-looking LU's source of K's entries: the QP inputs (QSrc, kval /
