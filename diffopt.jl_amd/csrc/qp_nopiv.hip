@@ -163,40 +163,59 @@ __device__ __forceinline__ QSrcB qsrc(const QSrc& s, int b, const QPMeta& mm) {
   v.N = mm.nsys;
   return v;
 }
+// a load through a global-address-space pointer: selected among the
+// sources, plain pointers become flat loads, which count against the LDS
+// counter too (every LDS wait then drained them)
+typedef const double __attribute__((address_space(1))) gdouble;
+__device__ __forceinline__ double gload(const double* base, int off) { return ((gdouble*)base)[off]; }
+
 // K[r][c] of the reduced system [Q, G_kᵀΛ, Aᵀ; G_k, D(s_k), 0; A, 0, 0]
 // (identity padding past N).  Branch-free: the source address is selected
 // and loaded unconditionally (a dead entry loads Q[0]), so a thread's 16
 // entries are 16 loads in flight — with one branch per source the compiler
 // waited for each load before the next (16 round trips per tile).
-__device__ __forceinline__ double kval(const QSrcB& v, int r, int c) {
+// (32-bit offsets — one problem's arrays hold < 2³¹ entries — selected
+// after all are computed; the sources by value: selecting among the fields
+// of a referenced struct turned into a select of their addresses, which kept
+// the struct in scratch and put a scratch load before every source load.)
+__device__ __forceinline__ double kval(QSrcB v, int r, int c) {
   const int n = v.n, nk = v.nk, rn = r - n, cn = c - n;
   const bool pad = r >= v.N || c >= v.N;
   const bool rq = r < n, rg = !rq && rn < nk, cq = c < n, cg = !cq && cn < nk;
-  const double* rowq = rq ? (cq ? v.Q + (size_t)r * n + c
-                                : (cg ? v.gk + (size_t)r * v.m + cn : v.A + (size_t)r * v.p + (cn - nk)))
-                          : nullptr;
-  const double* rowg = cq ? v.gk + (size_t)c * v.m + rn : v.sk + rn;
-  const double* rowa = v.A + (size_t)c * v.p + (rn - nk);
   const bool live = !pad && (rq || cq || (rg && r == c));
-  const double* p = !live ? v.Q : (rq ? rowq : (rg ? rowg : rowa));
   const bool lam = !pad && rq && cg;   // G_kᵀ·Λ: times λ_c
-  const double* p2 = lam ? v.lk + cn : v.Q;
-  const double x = *p, y = *p2;
-  return live ? (lam ? x * y : x) : (pad && r == c ? 1.0 : 0.0);
+  // every candidate offset computed (no arm does work), then selected
+  const int oq = r * n + c, ogr = r * v.m + cn, oar = r * v.p + (cn - nk);
+  const int ogc = c * v.m + rn, oac = c * v.p + (rn - nk);
+  int off = rq ? (cq ? oq : (cg ? ogr : oar)) : (rg ? (cq ? ogc : rn) : oac);
+  const double* base = rq ? (cq ? v.Q : (cg ? v.gk : v.A)) : (rg ? (cq ? v.gk : v.sk) : v.A);
+  off = live ? off : 0;
+  base = live ? base : v.Q;
+  const double* p2 = lam ? v.lk : v.Q;
+  const double x = gload(base, off), y = gload(p2, lam ? cn : 0);
+  // combined by arithmetic, not selects on the loaded values (the compiler
+  // turned those into branches with the loads sunk into them, each waited
+  // for in turn): a dead entry loads Q[0] and is multiplied by 0 (a problem
+  // whose Q[0] is not finite fails its first pivot and is rejected)
+  const double ml = lam ? 1.0 : 0.0, mv = live ? 1.0 : 0.0;
+  const double cst = !live && pad && r == c ? 1.0 : 0.0;
+  return fma(x * fma(y, ml, 1.0 - ml), mv, cst);
 }
 
 // kval for r > c (strictly lower part): the same values, with Q(r, c) read
 // as stored (column-major, Q[c·n + r]) — lanes along r then coalesce on every
 // source (Q, G_k's column-major copy, A).  Branch-free as kval.
-__device__ __forceinline__ double kval_lower(const QSrcB& v, int r, int c) {
+__device__ __forceinline__ double kval_lower(QSrcB v, int r, int c) {
   const int n = v.n, nk = v.nk, rn = r - n;
   const bool pad = r >= v.N || c >= v.N;
-  const bool cq = c < n;
-  const double* colp = r < n ? v.Q + (size_t)c * n + r
-                             : (rn < nk ? v.gk + (size_t)c * v.m + rn : v.A + (size_t)c * v.p + (rn - nk));
-  const bool live = !pad && (cq || (rn >= 0 && rn < nk && r == c));
-  const double* p = !live ? v.Q : (cq ? colp : v.sk + rn);
-  const double x = *p;
+  const bool cq = c < n, rq = r < n, rg = !rq && rn < nk;
+  const bool live = !pad && (cq || (rg && r == c));
+  const int oq = c * n + r, og = c * v.m + rn, oa = c * v.p + (rn - nk);
+  int off = cq ? (rq ? oq : (rg ? og : oa)) : rn;
+  const double* base = cq ? (rq ? v.Q : (rg ? v.gk : v.A)) : v.sk;
+  off = live ? off : 0;
+  base = live ? base : v.Q;
+  const double x = gload(base, off);
   return live ? x : (pad && r == c ? 1.0 : 0.0);
 }
 
@@ -204,8 +223,8 @@ __device__ __forceinline__ double kval_lower(const QSrcB& v, int r, int c) {
 // kval_lower above) or the NLP inputs through the reduced route's R (NSrc,
 // nlp_R) — overloads found at instantiation.
 __device__ __forceinline__ QSrcB src_bind(const QSrc& s, int b, const QPMeta& mm) { return qsrc(s, b, mm); }
-__device__ __forceinline__ double src_val(const QSrcB& v, int r, int c) { return kval(v, r, c); }
-__device__ __forceinline__ double src_val_lower(const QSrcB& v, int r, int c) { return kval_lower(v, r, c); }
+__device__ __forceinline__ double src_val(QSrcB v, int r, int c) { return kval(v, r, c); }
+__device__ __forceinline__ double src_val_lower(QSrcB v, int r, int c) { return kval_lower(v, r, c); }
 
 struct NSrc {          // NLP, reduced route (kernel argument)
   NLPDims d;
@@ -1655,17 +1674,31 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
     }
     __syncthreads();
   }
-  // C(J, J) = A(J, J) − X·P_J → S (identity beyond Wv)
+  // C(J, J) = A(J, J) − X·P_J → S (identity beyond Wv).  Every source entry
+  // is loaded before the first LDS access (src_val is branch-free and gives
+  // the identity past N, so the loads need no guard): one round trip
+  double av[4][4], pj[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    pj[q] = ps(c0 + 16 * q + l16);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) av[q][rr] = src_val(sv, c0 + 16 * wv + g + 4 * rr, c0 + 16 * q + l16);
+  }
+  // a compiler-only fence: the loads stay issued here (sunk next to their
+  // uses they would wait one by one); it emits no instruction
+  asm volatile("" ::: "memory");
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int j = 16 * q + l16;
-    const double pj = ps(c0 + j);
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int i = 16 * wv + g + 4 * rr;
+      // past Wv (c0 + i or c0 + j ≥ Np ≥ N) src_val is the identity and
+      // p_j = 1: av is used unconditionally (a select on it would become a
+      // branch with the loads sunk into it)
       const bool in = i < Wv && j < Wv;
       const double x = c0 > 0 && in ? S[i * SLD + j] : 0.0;
-      S[i * SLD + j] = in ? src_val(sv, c0 + i, c0 + j) - x * pj : (i == j ? 1.0 : 0.0);
+      S[i * SLD + j] = av[q][rr] - x * pj[q];
     }
   }
   if (w0b && t < 2 * NB64) {   // block J of b / c minus the finished blocks' contributions
@@ -1768,22 +1801,24 @@ __global__ __launch_bounds__(256 * TW) __attribute__((amdgpu_waves_per_eu(4))) v
   // rows, the update transposed through LDS
   // U11⁻¹ (L2) loaded together with the sources: one round trip
   constexpr int VQ = 16 / TW;
-  double av[16], v[VQ];
+  double av[16], v[VQ], pj[4];
 #pragma unroll
   for (int q = 0; q < VQ; ++q) v[q] = Bg[T + NTH * q];
   if (wact) {
 #pragma unroll
     for (int s = 0; s < 16; ++s) av[s] = src_val_lower(sv, r0 + 16 * wv + l16, c0 + 4 * s + g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pj[q] = ps(c0 + 16 * q + l16);
   }
+  asm volatile("" ::: "memory");   // compiler-only fence: the loads above stay issued together
   if (c0 > 0) {   // workgroup-uniform
     __syncthreads();   // every wave is done with the last staged strip
     if (wact) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int j = 16 * q + l16;
-        const double pj = ps(c0 + j);
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) Xh[(16 * wv + g + 4 * rr) * TLD + j] = acc[q][rr] * pj;
+        for (int rr = 0; rr < 4; ++rr) Xh[(16 * wv + g + 4 * rr) * TLD + j] = acc[q][rr] * pj[q];
       }
     }
     __syncthreads();
