@@ -507,25 +507,27 @@ __global__ __launch_bounds__(QST) void qp_qsym_kernel(QPIn P, double* __restrict
   const double* Qb = P.Q + (size_t)b * n * n;
   const int i = t & 63, j0 = t >> 6;   // lane ↔ row i of a tile, 16 columns j0 + 4k per thread
   double vmax = 0.0;
-  double mine[16];
-  // tile (R, C): Q(R·64 + i, C·64 + j) at Q[(C·64 + j)·n + R·64 + i] → T[j][i]
+  double other[16], mine[16];
+  // both tiles' loads issued before the first LDS store (one round trip, not
+  // two): tile (R, C): Q(R·64 + i, C·64 + j) at Q[(C·64 + j)·n + R·64 + i] →
+  // T[j][i]; tile (C, R): Q(C·64 + i, R·64 + j), compared with T[i][j] =
+  // Q(R·64 + j, C·64 + i)
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int j = j0 + 4 * k, r = R * QS + i, c = C * QS + j;
     const bool in = r < n && c < n;
-    mine[k] = in ? Qb[(size_t)c * n + r] : 0.0;
+    other[k] = in ? Qb[(size_t)c * n + r] : 0.0;
   }
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    T[(j0 + 4 * k) * QSLD + i] = mine[k];
-    vmax = fmax(vmax, fabs(mine[k]));
-  }
-  // tile (C, R): Q(C·64 + i, R·64 + j) — compared with T[i][j] = Q(R·64 + j, C·64 + i)
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int j = j0 + 4 * k, r = C * QS + i, c = R * QS + j;
     const bool in = r < n && c < n;
     mine[k] = in ? Qb[(size_t)c * n + r] : 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    T[(j0 + 4 * k) * QSLD + i] = other[k];
+    vmax = fmax(vmax, fabs(other[k]));
   }
   __syncthreads();
   int bad = 0;
