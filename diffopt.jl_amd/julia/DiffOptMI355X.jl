@@ -12,8 +12,12 @@
 # `solve_system` of DiffOpt.QuadraticProgram.Model (QuadraticProgram.jl:256-282,
 # 316-446, 486-496), ConicModel only `_gradient_cache`'s M and the two `lsqr`
 # calls of DiffOpt.ConicProgram.Model (ConicProgram.jl:172-255, 257-394) — so
-# results, sign conventions and getters are the reference's.  Not exercised in CI: the build image has no Julia (SURVEY.md
-# §8(c)); the C-ABI it binds is exercised by the Python ctypes harness.
+# results, sign conventions and getters are the reference's.  For the
+# NonLinearProgram back-end: `mi355x_factorization` (the
+# NonLinearKKTJacobianFactorization plug point) and `NLPBatch` (the batched
+# sensitivity surface).  Not exercised in CI: the build image has no Julia
+# (SURVEY.md §8(c)); the C-ABI it binds is exercised by the Python ctypes
+# harness.
 module DiffOptMI355X
 
 import DiffOpt
@@ -464,6 +468,120 @@ function LinearAlgebra.ldiv!(Y::AbstractMatrix{Float64}, K::KKTFactor, N::Abstra
                                     K.h.ptr, k, Nd, Yd), K.h.ptr)
     copyto!(Y, Yd)
     return Y
+end
+
+# ------------------------------------------------------------ NLP batches ----
+# The batched NonLinearProgram surface: a batch of NLPs sharing one structure
+# (the constraint kinds and which variables are bounded), each with its own
+# derivatives at the solution, does the whole `_compute_sensitivity` on the
+# device — the reference's `_build_sensitivity_matrices`
+# (nlp_utilities.jl:181-396) → dopt_nlp_set_structure / dopt_nlp_set,
+# `_lu_with_inertia_correction` (NonLinearProgram.jl:394-422) → dopt_nlp_factor,
+# `forward_differentiate!` / `reverse_differentiate!` (NonLinearProgram.jl:502-582)
+# → dopt_nlp_forward / dopt_nlp_reverse, ∂s (nlp_utilities.jl:457-500) →
+# dopt_nlp_jacobian.  The caller evaluates the derivatives at the solution as
+# the reference's MOI Nonlinear evaluator does (nlp_utilities.jl:35-92):
+#   Hxx n×n×B, Hxp n×P×B (Hessian of f − sense·yᵀc), Jx c×n×B, Jp c×P×B,
+#   x n×B, cval / crhs / y c×B (c(x), the set constants, MOI ConstraintDual),
+#   xl / xu / yl / yu n×B (bound values and bound duals; ignored where unbounded).
+# Outputs follow the Python NLPBatch (diffopt_amd/nlp.py) and the header:
+#   e = NLPBatch(B, n, c, P); set_structure!(e, …); set!(e, …); factor!(e)
+#   dx, ddual = nlp_forward(e, dp); dp = nlp_reverse(e; dx = seed); ∂s = nlp_jacobian(e)
+mutable struct NLPBatch
+    ptr::Ptr{Cvoid}
+    batch::Int
+    n::Int
+    c::Int
+    P::Int
+end
+
+function NLPBatch(batch::Integer, n::Integer, c::Integer, P::Integer; device::Integer = 0)
+    r = Ref{Ptr{Cvoid}}(C_NULL)
+    rc = ccall((:dopt_create, LIB), Cint,
+               (Ptr{Ptr{Cvoid}}, Cint, Int64, Int32, Int32, Int32, Int32),
+               r, device, batch, n, c, P, KIND_NLP)
+    _check(rc, r[])
+    e = NLPBatch(r[], Int(batch), Int(n), Int(c), Int(P))
+    finalizer(e) do ee
+        ee.ptr == C_NULL || ccall((:dopt_destroy, LIB), Cint, (Ptr{Cvoid},), ee.ptr)
+        ee.ptr = C_NULL
+    end
+    return e
+end
+
+"""
+    set_structure!(e, con_kind, has_low, has_up, sense)
+
+`con_kind[i]`: 0 `EqualTo`, 1 `GreaterThan`, 2 `LessThan` for NLP row i (the
+reference's constraint order); `has_low` / `has_up`: which variables carry a
+`VariableIndex`-in-`GreaterThan` / `LessThan` bound; `sense` = +1 (MIN) / −1 (MAX).
+"""
+function set_structure!(e::NLPBatch, con_kind::AbstractVector{<:Integer}, has_low::AbstractVector{Bool},
+                        has_up::AbstractVector{Bool}, sense::Integer)
+    ck = Int32.(con_kind)
+    lo = Int8.(has_low)
+    up = Int8.(has_up)
+    GC.@preserve ck lo up _check(ccall((:dopt_nlp_set_structure, LIB), Cint,
+                                       (Ptr{Cvoid}, Ptr{Int32}, Ptr{Int8}, Ptr{Int8}, Int32),
+                                       e.ptr, ck, lo, up, sense), e.ptr)
+    return e
+end
+
+_fptr(a) = a === nothing ? Ptr{Float64}(C_NULL) : pointer(a)
+_dense(a) = a === nothing ? nothing : convert(Array{Float64}, a)
+
+function set!(e::NLPBatch, Hxx, Hxp, Jx, Jp, x, cval, crhs, y;
+              xl = nothing, xu = nothing, yl = nothing, yu = nothing)
+    A = map(_dense, (Hxx, Hxp, Jx, Jp, x, cval, crhs, y, xl, xu, yl, yu))
+    GC.@preserve A _check(ccall((:dopt_nlp_set, LIB), Cint, (Ptr{Cvoid}, ntuple(_ -> Ptr{Float64}, 12)...),
+                                e.ptr, map(_fptr, A)...), e.ptr)
+    return e
+end
+
+"Factorise every problem's KKT system; returns the inertia corrections (0 none, k > 0, −1 failed)."
+function factor!(e::NLPBatch)
+    _check(ccall((:dopt_nlp_factor, LIB), Cint, (Ptr{Cvoid},), e.ptr), e.ptr)
+    corr = Vector{Int32}(undef, e.batch)
+    _check(ccall((:dopt_nlp_get_corrections, LIB), Cint, (Ptr{Cvoid}, Ptr{Int32}), e.ptr, corr), e.ptr)
+    return corr
+end
+
+"(rows, num_w, c, nlo, nup, nlow_primal, nup_primal) of the KKT system."
+function nlp_layout(e::NLPBatch)
+    l = Vector{Int32}(undef, 7)
+    _check(ccall((:dopt_nlp_get_layout, LIB), Cint, (Ptr{Cvoid}, Ptr{Int32}), e.ptr, l), e.ptr)
+    return Tuple(Int.(l))
+end
+
+_ndual(e::NLPBatch) = (l = nlp_layout(e); l[3] + l[6] + l[7])
+
+"Forward mode (NonLinearProgram.jl:502-528): dp P×B → (dx n×B, ddual (c+nlow+nup)×B)."
+function nlp_forward(e::NLPBatch, dp::AbstractMatrix)
+    dpd = convert(Matrix{Float64}, dp)
+    dx = Matrix{Float64}(undef, e.n, e.batch)
+    dd = Matrix{Float64}(undef, _ndual(e), e.batch)
+    GC.@preserve dpd dx dd _check(ccall((:dopt_nlp_forward, LIB), Cint,
+                                        (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                                        e.ptr, dpd, dx, dd), e.ptr)
+    return dx, dd
+end
+
+"Reverse mode (NonLinearProgram.jl:530-582): seeds dx n×B and/or ddual → dp P×B."
+function nlp_reverse(e::NLPBatch; dx = nothing, ddual = nothing)
+    a, d = _dense(dx), _dense(ddual)
+    dp = Matrix{Float64}(undef, e.P, e.batch)
+    GC.@preserve a d dp _check(ccall((:dopt_nlp_reverse, LIB), Cint,
+                                     (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                                     e.ptr, _fptr(a), _fptr(d), dp), e.ptr)
+    return dp
+end
+
+"∂s per problem (nlp_utilities.jl:457-500): rows × P × B."
+function nlp_jacobian(e::NLPBatch)
+    rows = nlp_layout(e)[1]
+    ds = Array{Float64}(undef, rows, e.P, e.batch)
+    GC.@preserve ds _check(ccall((:dopt_nlp_jacobian, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}), e.ptr, ds), e.ptr)
+    return ds
 end
 
 end # module
