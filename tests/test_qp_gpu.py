@@ -244,6 +244,19 @@ def test_sym_route_cfg2_shape(QPBatch, sym_mode):
     np.testing.assert_array_equal(e.info(), 0)
 
 
+def test_sym_route_32_wide_tail(QPBatch, sym_mode):
+    """Reduced size 200, padded to 224 = three 64-blocks + a 32-wide tail: the
+    left-looking diagonal launch of the tail block
+    forms only the lower 16×16 tiles inside the block (the row-3 tiles and the
+    waves past the 32 rows idle), the sweep vectors come through the staged
+    strip's padding; every problem at the oracle bar."""
+    d = _synthetic(8, 150, 100, 0, 0.5, 20251017)
+    e = _check_batch(QPBatch, d, kinds=[NOPIV] * 8)
+    np.testing.assert_array_equal(e.info(), 0)
+    pads = [(int(s) + 31) // 32 * 32 for s in e.system_size()]
+    assert any(p % 64 == 32 and p > 64 for p in pads), pads
+
+
 def test_sym_and_general_routes_agree(QPBatch, monkeypatch):
     """Same problems (multi-block, with equality rows) through both no-pivot
     routes: equal to ~1e-12 (different rounding, same factors)."""
