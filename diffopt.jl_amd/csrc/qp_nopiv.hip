@@ -88,6 +88,17 @@ __device__ unsigned long long nlu_stamps[16];
 #define NLU_MARK(k) do {} while (0)
 #define NLU_MARK_INIT do {} while (0)
 #endif
+// probe builds with -DLDIAG_STAMPS: s_memtime of thread 0 at the marks of the
+// left-looking diagonal kernel, per workgroup (plain stores, never waited for)
+#ifdef LDIAG_STAMPS
+__device__ unsigned long long ld_stamps[4096 * 16];
+#define LD_MARK(k)                                                                      \
+  do {                                                                                  \
+    if (threadIdx.x == 0) ld_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define LD_MARK(k) do {} while (0)
+#endif
 
 namespace dopt {
 
@@ -275,6 +286,14 @@ __device__ __forceinline__ double rcp_nr(double d) {
   double r = __builtin_amdgcn_rcp(d);
   r = fma(fma(-d, r, 1.0), r, r);
   return fma(fma(-d, r, 1.0), r, r);
+}
+
+// lane l's x (l wave-uniform): two v_readlane_b32 into an SGPR pair
+__device__ __forceinline__ double readlane_d(double x, int l) {
+  const unsigned long long v = (unsigned long long)__double_as_longlong(x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 // Blocked by 4 columns (default): step j4 factorises the 4×4 diagonal tile in
@@ -1576,13 +1595,189 @@ __device__ __forceinline__ void stage_rowstrip(double* X, const double* Kb, int 
   for (int u = 0; u < 16; ++u) X[(kq + u) * TLD + j] = j < rows ? v[u] : 0.0;
 }
 
-template <class SRC>
+// ---------------------------------------------------------------------------
+// The diagonal block of the left-looking route as ONE symmetric elimination
+// (default; DOPT_LDL=0: diag_core).  S = P_J·C(J, J) is symmetric (P·K
+// symmetric, the update X symmetric), so eliminating the augmented [S | I]
+// without pivoting gives, in one pass, S = L̃·D̃·L̃ᵀ and L̃⁻¹; K's factors
+// and inverses of the block follow by diagonal scalings:
+//   L = P⁻¹L̃P,  U = P⁻¹D̃L̃ᵀ,  L⁻¹ = P⁻¹L̃⁻¹P,  U⁻¹ = L̃⁻ᵀD̃⁻¹P
+// (C = P⁻¹S = L·U; the same factors diag_core forms up to rounding).
+// Lane j holds column j of the augmented matrix — of S while j is not yet
+// eliminated, of the right half once it is — wave w rows 16w..16w+15 (16
+// doubles per lane).  Step k needs only row k of the current
+// matrix, which is register k across the lanes: one ds_write_b64 publishes
+// it and every lane reads it back as broadcasts,
+//   lane j > k  (S):           a_i −= S_ik·(S_kj / d_k)   (S_ik = S_ki: the published row)
+//   lane j = k  (e_k):         a_i  = −S_ik / d_k          (i > k)
+//   lane j < k  (right half):  a_i −= S_ik·(R_kj / d_k)
+// — one formula, a_i = fma(−row_i, f_j, base), f_j = (j == k ? 1 : a_k) / d_k.
+// Only the upper triangle of S is read (column j's rows ≤ j; the rows below
+// are dropped at j's own step).  At the end lane j holds column j of
+//   F:  i < j  d_i·L̃_ji;   i = j  d_j;   i > j  (L̃⁻¹)_ij.
+// Wave w runs steps 16w..16w+15 after applying the 16w rows the waves
+// before it published (four barrier-separated phases; a published row is
+// final, so the image ends as F): 64 single-wave steps plus three rounds of
+// 16 independent rank-1 updates, where diag_core spends ≈55 µs in two
+// single-wave 32×32 LUs, the 16-block inverses and their MFMA products.  The threshold test, the growth bound
+// and every output (K's U_ab / L_ba, dinv, the packed inverse, u_kk / p_k,
+// the fused forward sweeps) come from F, by the whole workgroup.
+// ---------------------------------------------------------------------------
+constexpr int LX = NB64 * SLD;   // the extras past the 64 × SLD image
+static_assert(LX + 5 * 64 + 128 + 2 <= STEP_LDS, "ldl64_core extras must fit 40 KB");
+
+__device__ __forceinline__ void ldl64_core(double* buf, double* __restrict__ Kb, int ld,
+                                           int32_t* __restrict__ permb, double* __restrict__ Db,
+                                           QPMeta* __restrict__ mb, int c0, int Np, int N, double* __restrict__ Bg,
+                                           double* __restrict__ w0b, double* __restrict__ w1b, double bound,
+                                           const PScale& ps, double* __restrict__ ud) {
+  double* S = buf;
+  double* P = buf + LX;        // p_i
+  double* RP = P + 64;         // 1 / p_i
+  double* RD = P + 128;        // 1 / d_i
+  double* vec = P + 192;       // the fused sweeps' right-hand-side blocks
+  int* sbad = reinterpret_cast<int*>(P + 320);
+  const int Wv = min(NB64, Np - c0);   // 32 or 64: identity beyond
+  const bool trsm = Np - c0 > NB64;
+  const int t = threadIdx.x, lane = t & 63, role = ((t >> 6) + NLU_ROT) & 3;
+  if (t < 64) {
+    const double p = ps(c0 + t);
+    P[t] = p;
+    RP[t] = 1.0 / p;
+  }
+  if (t == 0) *sbad = 0;
+  if (t < Wv) permb[c0 + t] = c0 + t;
+  __syncthreads();
+  // wave w holds rows 16w..16w+15 of every column (lane); a lane j < 16w
+  // starts from 0 there (those rows are below its diagonal: its right-half
+  // column, zero until step j)
+  LD_MARK(3);
+  double a[16];
+  const int r0 = __builtin_amdgcn_readfirstlane(16 * role);   // wave-uniform (readlane's lane index)
+  {
+    const double z = lane < r0 ? 0.0 : 1.0;   // a product, not a select on the load (no branch)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a[r] = P[r0 + r] * S[(r0 + r) * SLD + lane] * z;
+  }
+  __syncthreads();   // every wave holds its rows: image row k becomes the published row k
+  // phase q: the waves below apply the rows phase q − 1 published (they never
+  // feed back), then wave q runs steps 16q..16q+15 alone.  A published row is
+  // final (later steps update only rows below it), so the image ends as F.
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q > 0 && role >= q) {
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const int k = 16 * (q - 1) + kk;
+        const double* V = S + k * SLD;
+        // f_j = S_kj/d_k (j ≥ r0, S part), R_kj/d_k (j < k), 1/d_k (j = k), 0
+        // for k < j < r0 (their rows here stay 0 until step j)
+        const double sel = (lane < k || lane >= r0) ? 1.0 : 0.0;
+        const double f = fma(V[lane], sel, lane == k ? 1.0 : 0.0) * RD[k];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a[r] = fma(-V[r0 + r], f, a[r]);
+      }
+    }
+    if (role == q) {
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const int k = r0 + kk;
+        double* V = S + k * SLD;
+        V[lane] = a[kk];   // published for the waves below and as F's row k
+        wave_sync();
+        // the pivot straight from lane k (no LDS round trip on the chain); the
+        // rows below it in this wave read back from the published row
+        const double rd = rcp_nr(readlane_d(a[kk], k));
+        if (lane == 0) RD[k] = rd;
+        // lane k: its rows below k restart from 0 (column k of the right half)
+        const double keep = lane == k ? 0.0 : 1.0;
+        const double f = fma(a[kk], keep, 1.0 - keep) * rd;
+#pragma unroll
+        for (int i = kk + 1; i < 16; ++i) a[i] = fma(-V[r0 + i], f, a[i] * keep);
+      }
+    }
+    __syncthreads();
+    LD_MARK(4 + q);
+  }
+  // One pass over the block, thread ↔ column j = t & 63 and rows i ≡ t >> 6
+  // (mod 4): K's entries of the block, l_ij = L̃_ij·p_j/p_i = F_ji/d_j·p_j/p_i
+  // (i > j) and U_ij = F_ij/p_i (i ≤ j), held to the threshold test
+  // (|l| ≤ NOPIV_LMAX) and the growth bound (|U| ≤ bound, pivots non-zero) as
+  // they are formed; the off-diagonal 32-blocks (U_ab, L_ba) go to K, the
+  // diagonal ones' inverses to dinv — (L⁻¹)_ij = F_ij·p_j/p_i (i > j),
+  // (U⁻¹)_ij = F_ji·p_j/d_j (i < j), p_j/d_j on the diagonal — and the packed
+  // 64×64 inverse (L11⁻¹ below the diagonal, U11⁻¹ on and above) to Bg for
+  // the column tiles' TRSM.  A failed test marks the problem LU_REJECT (its
+  // stores are then overwritten by the partial-pivoting fallback).
+  {
+    const int j = t & 63, i0 = t >> 6;
+    const double pj = P[j], rdj = RD[j], sj = rdj * pj;
+    int bad = 0;
+#pragma unroll 4
+    for (int q = 0; q < 16; ++q) {
+      const int i = i0 + 4 * q;
+      const double fij = S[i * SLD + j], fji = S[j * SLD + i], rpi = RP[i];
+      const bool low = i > j;
+      const double kv = low ? fji * sj * rpi : fij * rpi;                 // l_ij or U_ij
+      const double iv = low ? fij * pj * rpi : (i < j ? fji : 1.0) * sj;  // (L⁻¹)_ij or (U⁻¹)_ij
+      if (i < Wv && j < Wv)
+        bad |= low ? !(fabs(kv) <= NOPIV_LMAX) : (!(fabs(kv) <= bound) || (i == j && !(fabs(kv) > 0.0)));
+      if ((i ^ j) & 32) {   // off-diagonal 32-block (only in a full block)
+        if (Wv == NB64) Kb[(size_t)(c0 + i) * ld + c0 + j] = kv;
+      } else if (i < Wv) {  // diagonal 32-block (i >> 5): its inverses
+        double* D = Db + (i >> 5) * DBLK;
+        const int e = (i & 31) * 32 + (j & 31);
+        D[e] = low ? iv : (i == j ? 1.0 : 0.0);
+        D[32 * 32 + e] = low ? 0.0 : iv;
+      }
+      if (trsm) Bg[i * NB64 + j] = iv;
+    }
+    if (__any(bad) && lane == 0) *sbad = 1;   // every writer stores the same value
+  }
+  __syncthreads();
+  LD_MARK(8);
+  if (*sbad) {
+    if (t == 0) mb->lu = LU_REJECT;
+    return;
+  }
+  LD_MARK(9);
+  // u_kk / p_k = d_k / p_k²: the later blocks' updates and the sweeps through Lᵀ
+  if (t < Wv) ud[c0 + t] = S[t * SLD + t] * RP[t] * RP[t];
+  // fused forward sweeps: block c0 of the reverse RHS ← L11⁻¹·b, of the
+  // forward RHS ← c·U11⁻¹ (entries past N read as 0)
+  if (w0b) {
+    if (t < 128) {
+      const int i = t & 63;
+      const bool in = i < Wv && c0 + i < N;
+      vec[t] = in ? (t < 64 ? w0b : w1b)[c0 + i] : 0.0;
+    }
+    __syncthreads();
+    if (t < 64) {   // b′_t = b_t + Σ_{j<t} F_tj·p_j·b_j / p_t
+      double acc = 0.0;
+#pragma unroll 8
+      for (int j = 0; j < NB64; ++j)
+        if (j < t) acc = fma(S[t * SLD + j], P[j] * vec[j], acc);
+      if (t < Wv) w0b[c0 + t] = fma(acc, RP[t], vec[t]);
+    } else if (t < 128) {   // c′_j = (c_j + Σ_{i<j} c_i·F_ji)·p_j / d_j
+      const int j = t - 64;
+      double acc = vec[64 + j];
+#pragma unroll 8
+      for (int i = 0; i < NB64; ++i)
+        if (i < j) acc = fma(vec[64 + i], S[j * SLD + i], acc);
+      if (j < Wv) w1b[c0 + j] = acc * P[j] * RD[j];
+    }
+  }
+  LD_MARK(10);
+}
+
+template <class SRC, bool LDL>
 __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_ldiag_kernel(
     double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
     size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv, double* __restrict__ ukp,
     double* __restrict__ w0, double* __restrict__ w1, double* __restrict__ kamax, const double* __restrict__ kls,
     int n, int m, SRC src) {
   __shared__ double S[STEP_LDS];
+  LD_MARK(0);
   const int b = blockIdx.x;
   const QPMeta mm = meta[b];
   const int Np = nlu_np(mm);
@@ -1658,6 +1853,7 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
     }
   }
   __syncthreads();   // the staging is consumed: S becomes the diagonal image
+  LD_MARK(1);
   if (c0 > 0) {   // workgroup-uniform: X's tiles and their mirrors → S
     auto put = [&](int r, int c, const d4n& x) {
 #pragma unroll
@@ -1710,6 +1906,12 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
   }
   if (t == 0 && c0 == 0) meta[b].lu = LU_NOPIV;   // LU_REJECT below if a test fails
   const double bound = growth_bound(amax);
+  LD_MARK(2);
+  if (LDL) {   // its first barrier orders the S image and the sweep stores above
+    ldl64_core(S, Kb, ld, perm + (size_t)b * nmax, dinv + (size_t)b * dstride + (size_t)(c0 / 32) * DBLK, meta + b, c0,
+               Np, mm.nsys, binv + (size_t)b * BSTR, w0b, w1b, bound, ps, ud);
+    return;
+  }
   // diag_core's first barrier orders the S image and the sweep stores above
   diag_core(DiagLds(S), Kb, ld, perm + (size_t)b * nmax, dinv + (size_t)b * dstride + (size_t)(c0 / 32) * DBLK,
             meta + b, c0, Np, mm.nsys, binv + (size_t)b * BSTR, w0b, w1b, bound);
@@ -1952,8 +2154,12 @@ static void left_lu(Handle& h, const SRC& src, double* dinv, double* w0, double*
   bool pending = false;   // T holds column tiles S must wait for
   for (int c0 = 0; c0 < npmax; c0 += NB64) {
     double* bv = h.binv.as<double>() + (size_t)((c0 / NB64) & 1) * B * BSTR;
-    hipLaunchKernelGGL(nlu_ldiag_kernel<SRC>, dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv, dstride, meta,
-                       c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src);
+    if (h.ldl_mode)
+      hipLaunchKernelGGL((nlu_ldiag_kernel<SRC, true>), dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv, dstride,
+                         meta, c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src);
+    else
+      hipLaunchKernelGGL((nlu_ldiag_kernel<SRC, false>), dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv, dstride,
+                         meta, c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src);
     DOPT_CHECK_HIP(hipGetLastError());
     const int ntile = (npmax - c0 - NB64 + 63) / 64;
     if (ntile <= 0) break;
