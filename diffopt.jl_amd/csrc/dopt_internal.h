@@ -217,6 +217,7 @@ struct Handle {
   DevBuf nlp_rd;                   // per problem: δ (num_w), ρ (c) doubles
   DevBuf nlp_ri;                   // per problem: active bound of each w index (num_w), row state (c); then B ok flags
   DevBuf nlp_t1, nlp_t2;           // reduced right-hand sides / solutions (max(2, P) × B × nmax)
+  DevBuf nlp_msc;                  // per problem: max |M| of the full M (the reduced route's singularity scale)
   bool nstruct = false, nset = false, nfactored = false;
 
   // scratch for host-mode tangents / outputs

@@ -43,9 +43,11 @@ constexpr int NLP_MAX_CORR = 50;       // max_corrections (:398)
 // the reduction applies (one workgroup per problem)
 __global__ __launch_bounds__(NT) void nlp_red_prep_kernel(NLPDims d, NLPMap mp, NLPIn in, NLPRed R,
                                                           QPMeta* __restrict__ meta, double* __restrict__ kamax,
-                                                          const int32_t* __restrict__ hasym) {
+                                                          const int32_t* __restrict__ hasym,
+                                                          const double* __restrict__ hmax,
+                                                          double* __restrict__ mscale) {
   __shared__ int bad;
-  __shared__ double red[NT / 64];
+  __shared__ double red[NT / 64], mred[NT / 64];
   const size_t b = blockIdx.x;
   const int t = threadIdx.x;
   double* delta = R.delta + b * d.num_w;
@@ -56,11 +58,17 @@ __global__ __launch_bounds__(NT) void nlp_red_prep_kernel(NLPDims d, NLPMap mp, 
     kx[j] = -1;
   }
   __syncthreads();
+  // max |M| over the entries of the full M that R does not carry as such
+  // (the bound rows' V and X − X_B, the ±1 of the slack and bound columns):
+  // the singularity test's scale, as on the full route (max |R|
+  // holds δ = V/d, ~1e9 at an interior-point bound with d ≈ 1e-9)
+  double mmax = d.num_w > d.n || d.nlo + d.nup > 0 ? 1.0 : 0.0;
   // lower bounds (at most one per w index): a = V, b = −1
   for (int i = t; i < d.nlo; i += NT) {
     const int j = mp.low_idx[i];
     const double xl = j < d.n ? in.xl[b * d.n + j] : 0.0;
     const double dd = nlp_X(d, mp, in, b, j) - xl, V = nlp_VL(d, mp, in, b, j);
+    mmax = fmax(mmax, fmax(fabs(dd), fabs(V)));
     if (!isfinite(dd) || !isfinite(V)) bad = 1;
     else if (dd != 0.0) delta[j] += V / dd;
     else if (V == 0.0) bad = 1;
@@ -72,6 +80,7 @@ __global__ __launch_bounds__(NT) void nlp_red_prep_kernel(NLPDims d, NLPMap mp, 
     const int j = mp.up_idx[i];
     const double xu = j < d.n ? in.xu[b * d.n + j] : 0.0;
     const double dd = xu - nlp_X(d, mp, in, b, j), V = nlp_VU(d, mp, in, b, j);
+    mmax = fmax(mmax, fmax(fabs(dd), fabs(V)));
     if (!isfinite(dd) || !isfinite(V)) bad = 1;
     else if (dd != 0.0) delta[j] -= V / dd;
     else if (V == 0.0 || kx[j] >= 0) bad = 1;
@@ -96,18 +105,30 @@ __global__ __launch_bounds__(NT) void nlp_red_prep_kernel(NLPDims d, NLPMap mp, 
   }
   // max |R| without H (J, δ, ρ, the identity rows; qp_qsym_kernel gives max |H|):
   // the growth bound of the left-looking LU, which reads R from the inputs
-  double amax = 1.0;
-  for (size_t e = t; e < (size_t)d.c * d.n; e += NT) amax = fmax(amax, fabs(in.Jx[b * d.c * d.n + e]));
+  for (size_t e = t; e < (size_t)d.c * d.n; e += NT) mmax = fmax(mmax, fabs(in.Jx[b * d.c * d.n + e]));
+  double amax = fmax(1.0, mmax);   // (mmax so far: |J|, the bound rows, the ±1 entries)
   for (int j = t; j < d.n; j += NT) amax = fmax(amax, fabs(delta[j]));
   for (int k = t; k < d.c; k += NT) amax = fmax(amax, fabs(R.rho[b * d.c + k]));
-  for (int o = 32; o > 0; o >>= 1) amax = fmax(amax, __shfl_xor(amax, o));
-  if ((t & 63) == 0) red[t >> 6] = amax;
+  if (!hmax)   // max |H| not known from the symmetry check: scanned here
+    for (size_t e = t; e < (size_t)d.n * d.n; e += NT) mmax = fmax(mmax, fabs(in.Hxx[b * d.n * d.n + e]));
+  for (int o = 32; o > 0; o >>= 1) {
+    amax = fmax(amax, __shfl_xor(amax, o));
+    mmax = fmax(mmax, __shfl_xor(mmax, o));
+  }
+  if ((t & 63) == 0) {
+    red[t >> 6] = amax;
+    mred[t >> 6] = mmax;
+  }
   __syncthreads();
   if (t == 0) {
-    for (int w = 1; w < NT / 64; ++w) amax = fmax(amax, red[w]);
+    for (int w = 1; w < NT / 64; ++w) {
+      amax = fmax(amax, red[w]);
+      mmax = fmax(mmax, mred[w]);
+    }
     const bool ok = !bad;
     R.ok[b] = ok ? 1 : 0;
     kamax[b] = amax;
+    mscale[b] = hmax ? fmax(mmax, hmax[b]) : mmax;
     QPMeta mm = {};
     mm.nsys = ok ? d.n + d.c : d.rows;
     mm.lu = LU_NONE;
@@ -221,7 +242,8 @@ __global__ __launch_bounds__(NT) void nlp_pivot_check_kernel(const double* __res
                                                              QPMeta* __restrict__ meta,
                                                              const double* __restrict__ partial, int nparts,
                                                              int rows, const int32_t* __restrict__ plist,
-                                                             const double* __restrict__ kamax) {
+                                                             NLPRed Rd, const int32_t* __restrict__ shift,
+                                                             const double* __restrict__ mscale) {
   __shared__ double sred[NT / 64];
   __shared__ int ired[NT / 64];
   const int b = plist ? plist[blockIdx.x] : (int)blockIdx.x;
@@ -232,7 +254,12 @@ __global__ __launch_bounds__(NT) void nlp_pivot_check_kernel(const double* __res
   for (int o = 32; o > 0; o >>= 1) sc = fmax(sc, __shfl_xor(sc, o));
   if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = sc;
   __syncthreads();
-  sc = fmax(fmax(fmax(sred[0], sred[1]), fmax(sred[2], sred[3])), kamax[b]);   // kamax: max |R| of the left route
+  sc = fmax(fmax(sred[0], sred[1]), fmax(sred[2], sred[3]));   // the assembly's max |M| per row block
+  // a problem factorised on the reduced route: max |M| of its full M
+  // (nlp_red_prep_kernel), not max |R| — R's δ = V/d is ~1e9 at an interior-
+  // point bound and would turn a regular pivot into a "singular" verdict the
+  // reference (and the full route) would not give
+  if (red_use(Rd, shift, b)) sc = mscale[b];
   rows = mm.nsys;   // the factorised system: M, or R on the reduced route
   const double tol = rows * 2.220446049250313e-16 * sc;
   const double* Kb = K + (size_t)b * nmax * ld;
@@ -672,6 +699,11 @@ void red_recover(Handle& h, int trans, int k, const double* rfull, const double*
   DOPT_CHECK_HIP(hipGetLastError());
 }
 bool reduced_on(const Handle& h) { return !h.nlp_kkt && h.nlp_reduce; }
+// per problem: max |M| of the full M, the singularity test's scale on the reduced route
+double* nlp_mscale(Handle& h) {
+  h.nlp_msc.ensure((size_t)std::max<int64_t>(h.batch, 1) * sizeof(double));
+  return h.nlp_msc.as<double>();
+}
 // reduced right-hand sides / solutions for k per problem
 double* red_t1(Handle& h, int k) {
   h.nlp_t1.ensure((size_t)k * h.batch * h.nmax * sizeof(double));
@@ -687,7 +719,7 @@ void pivot_check(Handle& h, const int32_t* plist, int count) {
   hipLaunchKernelGGL(nlp_pivot_check_kernel, dim3(count), dim3(NT), 0, h.stream, h.K.as<double>(), h.ld, h.nmax,
                      h.ipiv.as<int32_t>(), dense_dinv(h), dinv_stride(h.nmax), h.meta.as<QPMeta>(),
                      h.nlp_scale.as<double>(), row_blocks(h),
-                     h.nlp_rows, plist, h.kamax.as<double>());
+                     h.nlp_rows, plist, red_of(h), h.nlp_shift.as<int32_t>(), nlp_mscale(h));
   DOPT_CHECK_HIP(hipGetLastError());
 }
 
@@ -761,7 +793,8 @@ void nlp_factor(Handle& h) {
         hasym = qsy_flag(h);
       }
       hipLaunchKernelGGL(nlp_red_prep_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), map_of(h), inputs(h),
-                         red_of(h), h.meta.as<QPMeta>(), h.kamax.as<double>(), hasym);
+                         red_of(h), h.meta.as<QPMeta>(), h.kamax.as<double>(), hasym,
+                         hasym ? (const double*)qsy_max(h) : nullptr, nlp_mscale(h));
       DOPT_CHECK_HIP(hipGetLastError());
       // the factorised sizes (n + c, or the rows of M for a problem kept on
       // the full route) size the LU and solve launches; every problem reduced
@@ -774,7 +807,7 @@ void nlp_factor(Handle& h) {
       h.blocked_npmax = npmax;
       h.nlp_left = hasym && std::all_of(mh.begin(), mh.end(), [](const QPMeta& mm) { return mm.sym != 0; });
     }
-    if (h.nlp_left)   // the pivot check's per-block scales: kamax alone
+    if (h.nlp_left)   // no assembly: the pivot check's scale is nlp_mscale alone
       DOPT_CHECK_HIP(hipMemsetAsync(h.nlp_scale.p, 0, h.nlp_scale.bytes, h.stream));
     else
       assemble(h, nullptr, B);

@@ -344,45 +344,88 @@ class QPBatch:
         return out[:, :n], out[:, n:n + m], out[:, n + m:]
 
 
-def solve_system(LHS, RHS, iterative=False, device=0):
-    """``QuadraticProgram.solve_system(solver, LHS, RHS, iterative)`` for the
-    MI355X solver of the reference's ``LinearAlgebraSolver`` plug point
-    (QuadraticProgram.jl:475-502): ``iterative ? lsqr(LHS, RHS) : LHS \\ RHS``
-    on the device (dopt_lhs_solve).  LHS (rows, rows) or a batch (B, rows,
-    rows); RHS (rows,) / (rows, k) or batched (B, rows) / (B, rows, k).  A
-    singular LHS raises SingularException(info), as ``\\`` does."""
-    lib = _lib.load()
-    M = np.asarray(LHS, dtype=np.float64)
-    single = M.ndim == 2
-    if single:
-        M = M[None]
-    B, rows = M.shape[0], M.shape[-1]
-    if M.shape != (B, rows, rows):
-        raise TypeError("LHS must be square")
-    R = np.asarray(RHS, dtype=np.float64)
-    if single:
-        R = R[None]
-    vec = R.ndim == 2
-    Rk = R[..., None] if vec else R                     # (B, rows, k)
-    if Rk.shape[:2] != (B, rows):
-        raise TypeError("RHS does not match LHS")
-    k = Rk.shape[2]
-    rhs = np.ascontiguousarray(np.transpose(Rk, (2, 0, 1)))   # seed-major (k, B, rows)
-    Mc = np.ascontiguousarray(np.swapaxes(M, 1, 2))            # column-major per problem
-    out = np.empty_like(rhs)
-    h = ctypes.c_void_p()
-    rc = lib.dopt_create(ctypes.byref(h), device, B, rows, 0, 0, _lib.DOPT_KIND_NLP)
-    if rc != 0:
-        raise _lib.EngineError(rc, "dopt_create failed (no HIP device?)")
-    try:
-        rc = lib.dopt_lhs_solve(h, rows, Mc.ctypes.data, k, rhs.ctypes.data, out.ctypes.data, int(bool(iterative)))
+class MI355XSolver:
+    """The MI355X solver of the reference's ``LinearAlgebraSolver`` plug point
+    (QuadraticProgram.jl:475-502; the Julia ``DiffOptMI355X.MI355XSolver``):
+    ``solve_system(LHS, RHS, iterative)`` is ``iterative ? lsqr(LHS, RHS) :
+    LHS \\ RHS`` on the device (dopt_lhs_solve).  The reference calls it twice
+    per model (reverse with LHS, :335; forward with LHS', :438) and its
+    callers loop models of one size, so the solver keeps one engine handle
+    per (batch, rows) instead of creating one per call."""
+
+    def __init__(self, device=0):
+        self.device = device
+        self._h = None
+        self._key = None
+        self.lib = _lib.load()
+
+    def close(self):
+        if self._h is not None:
+            self.lib.dopt_destroy(self._h)
+            self._h = None
+            self._key = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _handle(self, B, rows):
+        if self._key != (B, rows):
+            self.close()
+            h = ctypes.c_void_p()
+            rc = self.lib.dopt_create(ctypes.byref(h), self.device, B, rows, 0, 0, _lib.DOPT_KIND_NLP)
+            if rc != 0:
+                raise _lib.EngineError(rc, "dopt_create failed (no HIP device?)")
+            self._h, self._key = h, (B, rows)
+        return self._h
+
+    def solve_system(self, LHS, RHS, iterative=False):
+        """LHS (rows, rows) or a batch (B, rows, rows); RHS (rows,) / (rows, k)
+        or batched (B, rows) / (B, rows, k).  A singular LHS raises
+        SingularException(info), as ``\\`` does — on the engine's
+        rank-revealing test |u_ii| ≤ rows·ε·max|M| (include/diffopt_mi355x.h,
+        dopt_lhs_solve), which is stricter than ``\\``'s exactly-zero pivot."""
+        M = np.asarray(LHS, dtype=np.float64)
+        single = M.ndim == 2
+        if single:
+            M = M[None]
+        B, rows = M.shape[0], M.shape[-1]
+        if M.shape != (B, rows, rows):
+            raise TypeError("LHS must be square")
+        R = np.asarray(RHS, dtype=np.float64)
+        if single:
+            R = R[None]
+        vec = R.ndim == 2
+        Rk = R[..., None] if vec else R                     # (B, rows, k)
+        if Rk.shape[:2] != (B, rows):
+            raise TypeError("RHS does not match LHS")
+        k = Rk.shape[2]
+        rhs = np.ascontiguousarray(np.transpose(Rk, (2, 0, 1)))   # seed-major (k, B, rows)
+        Mc = np.ascontiguousarray(np.swapaxes(M, 1, 2))            # column-major per problem
+        out = np.empty_like(rhs)
+        h = self._handle(B, rows)
+        rc = self.lib.dopt_lhs_solve(h, rows, Mc.ctypes.data, k, rhs.ctypes.data, out.ctypes.data,
+                                     int(bool(iterative)))
         _lib.check(rc, h)
+        X = np.transpose(out, (1, 2, 0))                           # (B, rows, k)
+        if vec:
+            X = X[..., 0]
+        return X[0] if single else X
+
+
+def solve_system(LHS, RHS, iterative=False, device=0, solver=None):
+    """``QuadraticProgram.solve_system(solver, LHS, RHS, iterative)`` (see
+    MI355XSolver): one call on `solver`'s cached handle, or on a temporary
+    solver when none is given."""
+    if solver is not None:
+        return solver.solve_system(LHS, RHS, iterative)
+    s = MI355XSolver(device)
+    try:
+        return s.solve_system(LHS, RHS, iterative)
     finally:
-        lib.dopt_destroy(h)
-    X = np.transpose(out, (1, 2, 0))                           # (B, rows, k)
-    if vec:
-        X = X[..., 0]
-    return X[0] if single else X
+        s.close()
 
 
 class Model:

@@ -258,14 +258,21 @@ def conic_numpy_wellcond(batch, n, cones, seed, f_interior=0.25, f_dual_interior
     in its null space (M·z = (c − A_moiᵀy, A_moi x + b − s, −(cᵀx + bᵀy)) = 0 by
     feasibility and zero gap) — so LSQR returns the minimum-norm least-squares
     solution, which is unique; "converging" means istop 1–2.  Nonnegatives /
-    Nonpositives / Zeros rows as in ``conic_numpy``; PSD cones are not
-    generated here."""
+    Nonpositives / Zeros rows as in ``conic_numpy`` (Nonneg / Nonpos entries of
+    v = y − s on both sides of 0, |v| ≥ 0.5: the guard band).  PSD triangles
+    (VERDICT r03 item 2): S = V·diag(σ)·Vᵀ, Y = V·diag(ω)·Vᵀ strictly
+    complementary — each eigen-index carries exactly one of σ_i, ω_i, drawn
+    from ``pair_norm``·U(0.5, 1.5), at least one of each — so v = Y − S has
+    eigenvalues of both signs bounded away from 0 and every Daleckii–Krein
+    weight λ⁺/(λ⁺ − λ⁻) lies in [1/4, 3/4]; c uses MOI's set_dot weights (2 on
+    the off-diagonal triangle entries)."""
     rng = np.random.default_rng(seed)
     m = sum(d for _, d in cones)
     out = {k: [] for k in ["A", "b", "c", "x", "s", "y", "dx", "dA", "db", "dc"]}
     for _ in range(batch):
         s = np.zeros(m)
         y = np.zeros(m)
+        wts = np.ones(m)
         o = 0
         for code, dim in cones:
             if code == 0:
@@ -293,6 +300,16 @@ def conic_numpy_wellcond(batch, n, cones, seed, f_interior=0.25, f_dual_interior
                     s[o + 1:o + dim] = al * u
                     y[o] = be * pair_norm
                     y[o + 1:o + dim] = -be * u
+            elif code == 4:
+                d = int((math.isqrt(8 * dim + 1) - 1) // 2)
+                V, _ = np.linalg.qr(rng.standard_normal((d, d)))
+                on_s = rng.random(d) < 0.5
+                on_s[0], on_s[-1] = True, False          # both ranks non-zero
+                mag = pair_norm * rng.uniform(0.5, 1.5, d)
+                sig, om = np.where(on_s, mag, 0.0), np.where(on_s, 0.0, mag)
+                s[o:o + dim] = _tri((V * sig) @ V.T)
+                y[o:o + dim] = _tri((V * om) @ V.T)
+                wts[o:o + dim] = np.array([1.0 if i == j else 2.0 for j in range(d) for i in range(j + 1)])
             else:
                 raise ValueError("conic_numpy_wellcond: cone code %d not generated" % code)
             o += dim
@@ -303,7 +320,7 @@ def conic_numpy_wellcond(batch, n, cones, seed, f_interior=0.25, f_dual_interior
         A = (U[:, :k] * sv) @ V[:, :k].T
         x = rng.standard_normal(n) / math.sqrt(n)
         b = s - A @ x
-        c = A.T @ y
+        c = A.T @ (wts * y)
         out["A"].append(A); out["b"].append(b); out["c"].append(c); out["x"].append(x)
         out["s"].append(s); out["y"].append(y)
         out["dx"].append(rng.standard_normal(n))

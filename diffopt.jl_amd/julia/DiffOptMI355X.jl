@@ -242,17 +242,34 @@ end
 # LU, or LSQR with IterativeSolvers' defaults when `iterative`.  A singular
 # LHS raises SingularException(info) as `LHS \ RHS` does.  Per problem, like
 # the plug point itself; QPModel above is the batched, assembly-on-device path.
-struct MI355XSolver
+# The reference calls solve_system twice per model (LHS, then LHS') and its
+# callers loop models of one size, so the solver keeps one engine handle per
+# system size rather than a dopt_create per call (ADVICE r03).  Singularity is
+# the engine's rank-revealing verdict |u_ii| ≤ rows·ε·max|M|, stricter than
+# `\`'s exactly-zero pivot (include/diffopt_mi355x.h, dopt_lhs_solve).
+mutable struct MI355XSolver
     device::Int
+    handle::Union{Nothing,Handle}
+    rows::Int
 end
-MI355XSolver(; device::Integer = 0) = MI355XSolver(device)
+MI355XSolver(; device::Integer = 0) = MI355XSolver(device, nothing, 0)
+
+function _solver_handle!(s::MI355XSolver, rows::Int)
+    if s.handle === nothing || s.rows != rows
+        s.handle = Handle(rows, 0, 0; device = s.device, kind = KIND_NLP)
+        s.rows = rows
+    end
+    return s.handle
+end
 
 function QP.solve_system(s::MI355XSolver, LHS, RHS, iterative)
-    M = Matrix{Float64}(LHS)                 # LHS, or LHS' materialised (column-major)
-    rows = size(M, 1)
+    rows = size(LHS, 1)
+    # LHS, or LHS' materialised (column-major); a sparse LHS is densified here
+    # (the engine's dense LU: UMFPACK's sparsity is not exploited)
+    M = Matrix{Float64}(LHS)
     rhs = Vector{Float64}(RHS)
     x = Vector{Float64}(undef, rows)
-    h = Handle(rows, 0, 0; device = s.device, kind = KIND_NLP)
+    h = _solver_handle!(s, rows)
     GC.@preserve M rhs x begin
         rc = ccall((:dopt_lhs_solve, LIB), Cint,
                    (Ptr{Cvoid}, Int32, Ptr{Float64}, Int32, Ptr{Float64}, Ptr{Float64}, Int32),

@@ -105,12 +105,31 @@ int dopt_qp_set_csc(dopt_handle* h,
  * select the solve branch per problem (`iterative = norm(Q) ≈ 0`, :333/:436)
  * and LU-factorise it ONCE (the reference re-factorises per call, :490).
  * Rows with λ_i == 0 and (Gz−h)_i != 0 are eliminated exactly (their
- * unknowns decouple).  Pivoting: the factors of a problem are accepted
- * without row interchanges when every multiplier satisfies |l_ij| ≤ 10 (the
- * diagonal passes UMFPACK's threshold test with tolerance 0.1); otherwise the
- * problem is factorised with partial pivoting (env DOPT_LU=0: partial
- * pivoting for every problem).  Optional: dopt_qp_reverse/forward factor on
- * demand. */
+ * unknowns decouple); the rest, N' = n + kept + p rows, is factorised.
+ *
+ * Acceptance of a problem's no-pivot factors (else it is re-assembled and
+ * factorised with partial pivoting, transparently):
+ *   - threshold: every multiplier |l_ij| ≤ 10, i.e. every diagonal pivot
+ *     passes UMFPACK's threshold test with tolerance 0.1;
+ *   - growth: every pivot non-zero and finite, and every entry of U within
+ *     1e8·max|K| (NOPIV_GROWTH, dopt_internal.h).
+ * Which factorisation a problem gets:
+ *   - P-symmetric route (default): when Q is exactly symmetric (checked
+ *     bitwise on the device) and every kept λ is finite and non-zero, P·K is
+ *     symmetric for P = diag(1, λ_k, 1), so U = D·P⁻¹·Lᵀ·P and only L is
+ *     stored (U is materialised from L on demand, for single-direction and
+ *     multi-RHS solves); left-looking by 64-column block columns, each
+ *     diagonal block by a one-pass symmetric elimination of [P·C | I];
+ *   - general no-pivot LU (right-looking, L and U stored) for the other
+ *     problems of the batch;
+ *   - partial pivoting for the problems either one rejects.
+ * Environment switches (read at dopt_create; results agree to rounding):
+ *   DOPT_LU=0    partial pivoting for every problem;
+ *   DOPT_SYM=0   no P-symmetric route (the general no-pivot LU throughout);
+ *   DOPT_LEFT=0  the P-symmetric problems factorised right-looking;
+ *   DOPT_LDL=0   the left-looking route's diagonal blocks by the recursive
+ *                32×32 LU instead of the symmetric elimination.
+ * Optional: dopt_qp_reverse/forward factor on demand. */
 int dopt_qp_factor(dopt_handle* h);
 /* reverse_differentiate! (QuadraticProgram.jl:316-351):
  * out[b] = [dz (n) | dλ (m) | dν (p)] = −LHS \ [dl_dz; 0; 0]. */

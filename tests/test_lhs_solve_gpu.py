@@ -64,3 +64,30 @@ def test_singular_raises():
     A[:, 7] = 0.0                                                 # a zero column: exactly singular
     with pytest.raises(_lib.SingularException):
         solve_system(A, rng.standard_normal(20))
+
+
+def test_cached_solver_handle():
+    """MI355XSolver keeps one engine handle per (batch, rows) across calls
+    (the reference calls solve_system with LHS, then LHS', per
+    model, and loops models): the reverse / forward pair and a loop over
+    models of two sizes on one solver give exactly the fresh-handle results,
+    and a singular system in between does not poison the cached handle."""
+    from diffopt_amd import _lib
+    from diffopt_amd.qp import MI355XSolver, solve_system
+    s = MI355XSolver()
+    rng = np.random.default_rng(11)
+    for seed, shape in ((21, (40, 60, 5)), (22, (40, 60, 5)), (23, (20, 30, 4)), (24, (40, 60, 5))):
+        _, _, LHS = _kkt(seed, *shape)
+        L = np.asarray(LHS.todense() if hasattr(LHS, "todense") else LHS)
+        rhs = rng.standard_normal(L.shape[0])
+        for M in (L, L.T):
+            got = s.solve_system(M, rhs)
+            np.testing.assert_array_equal(got, solve_system(M, rhs))
+            np.testing.assert_allclose(got, np.linalg.solve(M, rhs), rtol=1e-10, atol=1e-12)
+        if seed == 22:
+            Z = L.copy()
+            Z[:, 3] = 0.0
+            with pytest.raises(_lib.SingularException):
+                s.solve_system(Z, rhs)
+    assert s._key == (1, L.shape[0])
+    s.close()

@@ -261,6 +261,40 @@ def test_near_singular_verdict(lu_mode, delta):
     check_against_oracle(e, st, pt, dp, dx, dd, [0, 2])
 
 
+@pytest.mark.parametrize("reduce", ["1", "0"], ids=["reduced", "full"])
+def test_interior_point_bounds_singularity_scale(monkeypatch, reduce):
+    """interior-point duals leave an active bound at
+    d = x − x_L ≈ 1e-9 with V ≈ 1, so the reduced route's eliminated-bound
+    term δ = V/d is ≈ 1e9.  The singularity test's scale must be max |M| of the
+    full M (|H|, |J|, |V|, |d|, 1), not max |R| (which holds δ): with max |R|
+    the tolerance rows·ε·max|R| ≈ 1e-5 flags the regular pivots of a problem
+    with modest curvature (H scaled by 1e-6: pivots ~1e-7) as singular and
+    applies inertia corrections the reference's lu(M) (an exactly zero pivot
+    only, NonLinearProgram.jl:394-422) never would.  Corrections must match the
+    oracle's (0) on both routes, and the sensitivities the oracle."""
+    from diffopt_amd.synthetic import nlp_numpy
+    monkeypatch.setenv("DOPT_NLP_REDUCE", reduce)
+    B, n, c, P = 3, 40, 20, 5
+    st, pt, dp, dx, dd = nlp_numpy(B, n, c, P, 4242, frac_low=0.6, frac_up=0.4, active=0.5)
+    moved = 0
+    for b in range(B):
+        for j in range(n):
+            if st["has_low"][j] and pt["xl"][b, j] == pt["x"][b, j]:
+                pt["xl"][b, j] -= 1e-9
+                moved += 1
+            if st["has_up"][j] and pt["xu"][b, j] == pt["x"][b, j]:
+                pt["xu"][b, j] += 1e-9
+                moved += 1
+    assert moved >= 10
+    pt["Hxx"][1] *= 1e-6
+    for b in range(B):
+        assert oracle_problem(st, pt, b)[4] == 0
+    e = engine(st, pt, B)
+    np.testing.assert_array_equal(e.corrections(), 0)
+    check_against_oracle(e, st, pt, dp, dx, dd, range(B))
+    e.close()
+
+
 def test_config6_shape():
     """bench.py --config 6's shape (n = 200, c = 100, P = 20, 607 rows, partial
     pivoting): two problems of the bench generator vs the oracle at 1e-6."""

@@ -35,10 +35,12 @@ KERNEL_PHASE = {
 # update sequence of one factorisation, the two solve kernels of one step);
 # summed over the dispatches and divided by the number of steps, counted by
 # the per-step qp_prep_kernel dispatch
-QP_GROUPS = {"qp_assemble": ("qp_prep_kernel", "qp_asm_tile_kernel"),
+QP_GROUPS = {"qp_assemble": ("qp_prep_kernel", "qp_asm_tile_kernel", "qp_qsym_kernel"),
              "qp_lu": ("nlu_diag_kernel", "nlu_trsm_kernel", "nlu_cross_kernel", "nlu_update2_kernel",
                        "nlu_ldiag_kernel", "nlu_lcol_kernel", "blu_panel_kernel", "blu_update_kernel"),
-             "qp_solve": ("blu_solve_kernel", "blu_solve_rows_kernel", "blu_solve2_kernel")}
+             "qp_solve": ("blu_solve_kernel", "blu_solve_rows_kernel", "blu_solve2_kernel", "blu_sym2_kernel",
+                          "blu_symsolve_kernel"),
+             "qp_output": ("qp_output_kernel",)}
 QP_STEP = "qp_prep_kernel"
 # NLP back-end (bench config 6): the step is counted by the assembly; its LU
 # is the partial-pivoting blocked LU, its solves the blocked solve kernels
