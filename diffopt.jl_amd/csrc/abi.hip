@@ -190,6 +190,7 @@ int dopt_destroy(dopt_handle* h) {
   }
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->meta_host) (void)hipHostFree(h->meta_host);
+  if (h->pin) (void)hipHostFree(h->pin);
   if (h->meta_ev) (void)hipEventDestroy(h->meta_ev);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -248,6 +249,44 @@ static const int64_t* stage_in_i64(Handle& h, DevBuf& buf, const int64_t* src, s
   return (const int64_t*)buf.p;
 }
 
+// Host-mode inputs of at most PACK_MAX bytes in all: gathered into the
+// handle's pinned buffer (memcpy) and moved by one host→device copy, the
+// device pointers returned in order (null stays null).  Larger inputs keep
+// one copy per array (a host memcpy of gigabytes costs more than it saves).
+constexpr size_t PACK_MAX = (size_t)8 << 20;
+struct PackIn {
+  const void* src;
+  size_t bytes;
+};
+static bool pack_in(Handle& h, const PackIn* in, int k, const void** out) {
+  if (h.mem == DOPT_MEM_DEVICE) return false;
+  size_t tot = 0;
+  for (int i = 0; i < k; ++i) tot += (in[i].bytes + 15) & ~(size_t)15;
+  if (tot == 0 || tot > PACK_MAX) return false;
+  if (h.pin_bytes < tot) {
+    if (h.pin) DOPT_CHECK_HIP(hipHostFree(h.pin));
+    h.pin = nullptr;
+    h.pin_bytes = 0;
+    DOPT_CHECK_HIP(hipHostMalloc(&h.pin, tot, hipHostMallocDefault));
+    h.pin_bytes = tot;
+  }
+  // the previous call's copy out of the pinned buffer is complete: every
+  // host-mode entry point synchronises before it returns
+  h.pack.ensure(tot);
+  size_t off = 0;
+  for (int i = 0; i < k; ++i) {
+    if (!in[i].src) {
+      out[i] = nullptr;
+      continue;
+    }
+    std::memcpy(static_cast<char*>(h.pin) + off, in[i].src, in[i].bytes);
+    out[i] = static_cast<const char*>(h.pack.p) + off;
+    off += (in[i].bytes + 15) & ~(size_t)15;
+  }
+  DOPT_CHECK_HIP(hipMemcpyAsync(h.pack.p, h.pin, off, hipMemcpyHostToDevice, h.stream));
+  return true;
+}
+
 int dopt_qp_set_csc(dopt_handle* h,
                     const int64_t* Q_colptr, const int64_t* Q_rowval, const double* Q_nzval, int64_t Q_nnz,
                     const int64_t* G_colptr, const int64_t* G_rowval, const double* G_nzval, int64_t G_nnz,
@@ -268,13 +307,29 @@ int dopt_qp_set_csc(dopt_handle* h,
                          {G_colptr, G_rowval, G_nzval, G_nnz, m, 1},
                          {A_colptr, A_rowval, A_nzval, A_nnz, p, 3}};
     const double* dense[3] = {nullptr, nullptr, nullptr};
+    // small models (the Julia back-end's batch of one): every array in one copy
+    PackIn pin[13];
+    const void* pdev[13];
+    for (int k = 0; k < 3; ++k) {
+      const Mat& M = mats[k];
+      const bool on = M.rows > 0;
+      pin[3 * k] = {on ? M.cp : nullptr, on ? B * (n + 1) * sizeof(int64_t) : 0};
+      pin[3 * k + 1] = {on && M.nnz ? M.rv : nullptr, on ? (size_t)M.nnz * sizeof(int64_t) : 0};
+      pin[3 * k + 2] = {on && M.nnz ? M.nz : nullptr, on ? (size_t)M.nnz * sizeof(double) : 0};
+    }
+    pin[9] = {m ? hv : nullptr, m ? B * m * sizeof(double) : 0};
+    pin[10] = {z, B * n * sizeof(double)};
+    pin[11] = {m ? lam : nullptr, m ? B * m * sizeof(double) : 0};
+    pin[12] = {p ? nu : nullptr, p ? B * p * sizeof(double) : 0};
+    const bool packed = pack_in(*h, pin, 13, pdev);
     for (int k = 0; k < 3; ++k) {
       const Mat& M = mats[k];
       if (M.rows == 0) continue;
       if (M.nnz > 0 && (!M.rv || !M.nz)) throw Error(-1, "rowval and nzval are required when nnz > 0");
-      const int64_t* cp = stage_in_i64(*h, h->csc_in[3 * k], M.cp, B * (n + 1));
-      const int64_t* rv = stage_in_i64(*h, h->csc_in[3 * k + 1], M.rv, (size_t)M.nnz);
-      const double* nz = stage_in(*h, h->csc_in_val[k], M.nz, (size_t)M.nnz);
+      const int64_t* cp = packed ? (const int64_t*)pdev[3 * k] : stage_in_i64(*h, h->csc_in[3 * k], M.cp, B * (n + 1));
+      const int64_t* rv = packed ? (const int64_t*)pdev[3 * k + 1]
+                                 : stage_in_i64(*h, h->csc_in[3 * k + 1], M.rv, (size_t)M.nnz);
+      const double* nz = packed ? (const double*)pdev[3 * k + 2] : stage_in(*h, h->csc_in_val[k], M.nz, (size_t)M.nnz);
       DevBuf& d = h->own_in[M.slot];
       d.ensure(B * M.rows * n * sizeof(double));
       dopt::csc_to_dense(*h, cp, rv ? rv : cp, nz ? nz : (const double*)d.p, M.nnz, (int)M.rows, (int)n,
@@ -288,11 +343,18 @@ int dopt_qp_set_csc(dopt_handle* h,
                                          : "CSC rowval out of range");
     h->Q = dense[0];
     h->G = m ? dense[1] : nullptr;
-    h->hv = m ? stage_in(*h, h->own_in[2], hv, B * m) : nullptr;
     h->A = p ? dense[2] : nullptr;
-    h->z = stage_in(*h, h->own_in[4], z, B * n);
-    h->lam = m ? stage_in(*h, h->own_in[5], lam, B * m) : nullptr;
-    h->nu = p ? stage_in(*h, h->own_in[6], nu, B * p) : nullptr;
+    if (packed) {   // the pack stays as the inputs' home until the next set
+      h->hv = (const double*)pdev[9];
+      h->z = (const double*)pdev[10];
+      h->lam = (const double*)pdev[11];
+      h->nu = (const double*)pdev[12];
+    } else {
+      h->hv = m ? stage_in(*h, h->own_in[2], hv, B * m) : nullptr;
+      h->z = stage_in(*h, h->own_in[4], z, B * n);
+      h->lam = m ? stage_in(*h, h->own_in[5], lam, B * m) : nullptr;
+      h->nu = p ? stage_in(*h, h->own_in[6], nu, B * p) : nullptr;
+    }
     h->set = true;
     h->factored = false;
     DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));

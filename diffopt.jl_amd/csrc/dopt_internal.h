@@ -131,6 +131,11 @@ struct Handle {
   const double *Q = nullptr, *G = nullptr, *hv = nullptr, *A = nullptr;
   const double *z = nullptr, *lam = nullptr, *nu = nullptr;
   DevBuf own_in[7];          // host-mode copies of the 7 QP inputs (Q, G, A: also the CSC densification)
+  // small host-mode inputs gathered into one pinned buffer and moved by ONE
+  // copy (dopt_qp_set_csc of a batch-1 model: 13 copies → 1)
+  void* pin = nullptr;
+  size_t pin_bytes = 0;
+  DevBuf pack;
   DevBuf csc_in[9], csc_in_val[3], csc_err;   // host-mode copies of CSC colptr / rowval / nzval
   int32_t nmax = 0, ld = 0;  // max system size, K row stride (doubles)
   DevBuf K, ipiv, s, kidx, meta, rhs, x;

@@ -127,7 +127,16 @@ class QPBatch:
         args = []
         for cp, rv, nz, nnz in mats:
             args += [st.ptr(cp), st.ptr(rv if nnz else None), st.ptr(nz if nnz else None), nnz]
-        rc = self.lib.dopt_qp_set_csc(self.h, *args, *[st.ptr(v) for v in vecs])
+        args += [st.ptr(v) for v in vecs]
+        self._csc_keep = (mats, vecs)   # the arrays behind `args`
+        self.set_csc_args(args)
+        return args
+
+    def set_csc_args(self, args):
+        """dopt_qp_set_csc on the ctypes arguments a previous ``set_csc``
+        returned (arrays kept alive by this object): the ABI call alone, as the
+        Julia back-end issues it with the MOI matrix form already in hand."""
+        rc = self.lib.dopt_qp_set_csc(self.h, *args)
         _lib.check(rc, self.h)
 
     def factor(self, singular_ok=False):
