@@ -156,6 +156,8 @@ struct Handle {
   int32_t lstreams = 0;            // left-looking LU: column tiles I ≥ J+2 on `aux` (env DOPT_LSTREAMS=1)
   DevBuf ukp;                      // left-looking LU: u_kk / p_k of every finished diagonal block (nmax per problem)
   int32_t lcol_tw = 1;             // left-looking LU column tiles per workgroup (env DOPT_LCOL_TW: 1 or 2)
+  int32_t lpersist = 0;            // left-looking LU: one workgroup per problem, one launch (env DOPT_LPERSIST=1)
+  int32_t lslices = 1;             // left-looking LU: batch halves as two skewed chains (env DOPT_LSLICE=2)
   int32_t ldl_mode = 1;            // left-looking LU: diagonal blocks by the one-pass symmetric elimination
                                    // (ldl64_core; env DOPT_LDL=0: the recursive 32×32 LU, diag_core)
   int32_t sym_lean = 1;            // fused P-symmetric sweeps in their own lean kernel (env DOPT_SYM_LEAN=0: inside

@@ -1770,15 +1770,16 @@ __device__ __forceinline__ void ldl64_core(double* buf, double* __restrict__ Kb,
   LD_MARK(10);
 }
 
+// The diagonal step of block column J = c0 / 64 for problem b (S: the
+// workgroup's STEP_LDS doubles of LDS); nlu_ldiag_kernel runs it for a batch,
+// nlu_left_all_kernel inside its per-problem loop.
 template <class SRC, bool LDL>
-__global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_ldiag_kernel(
-    double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
-    size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv, double* __restrict__ ukp,
-    double* __restrict__ w0, double* __restrict__ w1, double* __restrict__ kamax, const double* __restrict__ kls,
-    int n, int m, SRC src) {
-  __shared__ double S[STEP_LDS];
+__device__ __forceinline__ void ldiag_body(
+    double* S, int b, double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm,
+    double* __restrict__ dinv, size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv,
+    double* __restrict__ ukp, double* __restrict__ w0, double* __restrict__ w1, double* __restrict__ kamax,
+    const double* __restrict__ kls, int n, int m, const SRC& src) {
   LD_MARK(0);
-  const int b = blockIdx.x;
   const QPMeta mm = meta[b];
   const int Np = nlu_np(mm);
   if (c0 >= Np || mm.lu == LU_REJECT) return;   // workgroup-uniform
@@ -1921,6 +1922,17 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
   if (t < Wv) ud[c0 + t] = 1.0 / (S[t * SLD + t] * ps(c0 + t));
 }
 
+template <class SRC, bool LDL>
+__global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_ldiag_kernel(
+    double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
+    size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv, double* __restrict__ ukp,
+    double* __restrict__ w0, double* __restrict__ w1, double* __restrict__ kamax, const double* __restrict__ kls,
+    int n, int m, SRC src, int b0) {
+  __shared__ double S[STEP_LDS];
+  ldiag_body<SRC, LDL>(S, b0 + (int)blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, c0, binv, ukp, w0, w1,
+                       kamax, kls, n, m, src);
+}
+
 // stage_rowstrip by NTH threads (NTH = 256 or 512): 16·256/NTH columns each
 // (lane ↔ row: a 16-lane store group writes 16 consecutive rows of one
 // column, conflict-free; a (row, column-quarter) mapping stores 4 rows × 4
@@ -1946,18 +1958,15 @@ __device__ __forceinline__ void stage_rowstrip_n(double* X, const double* Kb, in
 // growth bound on U(J, I) = D_J·L(I, J)ᵀ·P_I; L(I, J) → K (U is not stored:
 // nlu_sym_u_kernel when a solve needs it).  `ngrp` workgroups per problem,
 // `cnt` tiles per problem from tile `toff` on.
+// Tiles it0 .. it0+TW−1 (from tile `toff` on) of block column J = c0 / 64 of
+// problem b (X: the workgroup's TW × NB64·TLD doubles of LDS);
+// nlu_lcol_kernel runs them for a batch, nlu_left_all_kernel inside its loop.
 template <class SRC, int TW>
-__global__ __launch_bounds__(256 * TW) __attribute__((amdgpu_waves_per_eu(4))) void nlu_lcol_kernel(
-    double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
-    const double* __restrict__ ukp, int ngrp, int cnt, int toff, int total, const double* __restrict__ kamax,
-    const double* __restrict__ kls, int n, int m, SRC src) {
+__device__ __forceinline__ void lcol_body(
+    double (*X)[NB64 * TLD], int b, int it0, double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta,
+    int c0, const double* __restrict__ binv, const double* __restrict__ ukp, int cnt, int toff,
+    const double* __restrict__ kamax, const double* __restrict__ kls, int n, int m, const SRC& src) {
   constexpr int NTH = 256 * TW;
-  __shared__ double X[TW][NB64 * TLD];   // X[0]: staged strip / U11⁻¹ (shared); X[h]: tile h's transposes
-  const int L = blockIdx.x;
-  const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
-  const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
-  const int b = logical / ngrp;
-  const int it0 = (logical - b * ngrp) * TW;
   const QPMeta mm = meta[b];
   const int Np = nlu_np(mm);
   if (mm.lu == LU_REJECT || c0 + NB64 + 64 * (toff + it0) >= Np) return;   // workgroup-uniform
@@ -2000,7 +2009,12 @@ __global__ __launch_bounds__(256 * TW) __attribute__((amdgpu_waves_per_eu(4))) v
   }
   // C = A − acc·P_J in the TRSM's A-operand layout (lane ↔ row 16wv + l16,
   // k-step s ↔ column 4s + g): the sources read with the lanes along the
-  // rows, the update transposed through LDS
+  // rows, the update transposed through LDS.  The transposing buffer is
+  // XOR-swizzled (column c of row r at c ^ (r & 14)): the read walks 16 rows
+  // of one column, which TLD = 80 (row stride ≡ 32 banks) put on two bank
+  // pairs — an 8-way conflict; swizzled, the 32 lanes of a half-wave hit 64
+  // distinct banks (lds_bank_conflict / lds_idx_active
+  // 0.556 on config 2)
   // U11⁻¹ (L2) loaded together with the sources: one round trip
   constexpr int VQ = 16 / TW;
   double av[16], v[VQ], pj[4];
@@ -2020,13 +2034,16 @@ __global__ __launch_bounds__(256 * TW) __attribute__((amdgpu_waves_per_eu(4))) v
       for (int q = 0; q < 4; ++q) {
         const int j = 16 * q + l16;
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) Xh[(16 * wv + g + 4 * rr) * TLD + j] = acc[q][rr] * pj[q];
+        for (int rr = 0; rr < 4; ++rr) {
+          const int r = 16 * wv + g + 4 * rr;
+          Xh[r * TLD + (j ^ (r & 14))] = acc[q][rr] * pj[q];
+        }
       }
     }
     __syncthreads();
     if (wact) {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) av[s] -= Xh[(16 * wv + l16) * TLD + 4 * s + g];
+      for (int s = 0; s < 16; ++s) av[s] -= Xh[(16 * wv + l16) * TLD + ((4 * s + g) ^ ((16 * wv + l16) & 14))];
     }
     __syncthreads();   // every wave holds its C rows before U11⁻¹ overwrites X[0]
   }
@@ -2060,6 +2077,65 @@ __global__ __launch_bounds__(256 * TW) __attribute__((amdgpu_waves_per_eu(4))) v
     for (int rr = 0; rr < 4; ++rr) over |= !(fabs(uk * lt[ct][rr] * ps(r0 + 16 * wv + g + 4 * rr)) <= bound);
   }
   if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;   // every writer stores the same value
+}
+
+template <class SRC, int TW>
+__global__ __launch_bounds__(256 * TW) __attribute__((amdgpu_waves_per_eu(4))) void nlu_lcol_kernel(
+    double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
+    const double* __restrict__ ukp, int ngrp, int cnt, int toff, int total, const double* __restrict__ kamax,
+    const double* __restrict__ kls, int n, int m, SRC src, int b0) {
+  __shared__ double X[TW][NB64 * TLD];   // X[0]: staged strip / U11⁻¹ (shared); X[h]: tile h's transposes
+  const int L = blockIdx.x;
+  const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
+  const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
+  const int bl = logical / ngrp;
+  lcol_body<SRC, TW>(X, b0 + bl, (logical - bl * ngrp) * TW, K, ld, nmax, meta, c0, binv, ukp, cnt, toff, kamax,
+                     kls, n, m, src);
+}
+
+// The whole left-looking factorisation of one problem per workgroup, block
+// column by block column: the diagonal step, then the column's tiles one
+// after another (env DOPT_LPERSIST=1).  No launch boundary and no
+// inter-workgroup dependence: the four problems a CU holds drift into
+// different phases, so one's latency-bound diagonal elimination (VALU / LDS)
+// shares the CU with another's column tiles (MFMA / memory) instead of every
+// workgroup of a launch being in the same phase.  One packed-inverse buffer
+// per problem (the steps of a problem are ordered within its workgroup).
+// the two steps as separate functions (not inlined: each body gets its own
+// register allocation instead of one spilling allocation for both)
+template <class SRC>
+__device__ __noinline__ void ldiag_call(double* S, int b, double* K, int ld, int nmax, int32_t* perm, double* dinv,
+                                        size_t dstride, QPMeta* meta, int c0, double* binv, double* ukp, double* w0,
+                                        double* w1, double* kamax, const double* kls, int n, int m, const SRC& src) {
+  ldiag_body<SRC, true>(S, b, K, ld, nmax, perm, dinv, dstride, meta, c0, binv, ukp, w0, w1, kamax, kls, n, m, src);
+}
+template <class SRC>
+__device__ __noinline__ void lcol_call(double* S, int b, int it, double* K, int ld, int nmax, QPMeta* meta, int c0,
+                                       const double* binv, const double* ukp, int cnt, const double* kamax,
+                                       const double* kls, int n, int m, const SRC& src) {
+  lcol_body<SRC, 1>(reinterpret_cast<double (*)[NB64 * TLD]>(S), b, it, K, ld, nmax, meta, c0, binv, ukp, cnt, 0,
+                    kamax, kls, n, m, src);
+}
+
+template <class SRC>
+__global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_left_all_kernel(
+    double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
+    size_t dstride, QPMeta* __restrict__ meta, double* __restrict__ binv, double* __restrict__ ukp,
+    double* __restrict__ w0, double* __restrict__ w1, double* __restrict__ kamax, const double* __restrict__ kls,
+    int n, int m, SRC src, int npmax) {
+  static_assert(STEP_LDS == NB64 * TLD, "one LDS buffer serves both steps");
+  __shared__ double S[STEP_LDS];
+  const int b = (int)blockIdx.x;
+  const int Np = nlu_np(meta[b]);   // 0 for a problem off the blocked route: every step returns at once
+  for (int c0 = 0; c0 < npmax && c0 < Np; c0 += NB64) {
+    ldiag_call<SRC>(S, b, K, ld, nmax, perm, dinv, dstride, meta, c0, binv, ukp, w0, w1, kamax, kls, n, m, src);
+    __syncthreads();   // the step's stores (this workgroup's own) before the tiles read them; S reused
+    const int ntile = (Np - c0 - NB64 + 63) / 64;
+    for (int it = 0; it < ntile; ++it) {
+      lcol_call<SRC>(S, b, it, K, ld, nmax, meta, c0, binv, ukp, ntile, kamax, kls, n, m, src);
+      __syncthreads();
+    }
+  }
 }
 
 // U of the left-looking route's P-symmetric factors, materialised from L for
@@ -2137,34 +2213,70 @@ static void left_lu(Handle& h, const SRC& src, double* dinv, double* w0, double*
       DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_crit, 0));
     }
   }
-  auto lcol =[&](hipStream_t st, int c0, double* bv, int toff, int cnt) {
+  auto lcol =[&](hipStream_t st, int c0, double* bv, int toff, int cnt, int b0, int Bs) {
     if (cnt <= 0) return;
     const int tw = h.lcol_tw == 2 && cnt > 1 ? 2 : 1;   // tiles per workgroup
     const int ngrp = (cnt + tw - 1) / tw;
-    const long long tot = (long long)ngrp * B;
+    const long long tot = (long long)ngrp * Bs;
     if (tot > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
     if (tw == 2)
       hipLaunchKernelGGL((nlu_lcol_kernel<SRC, 2>), dim3((unsigned)tot), dim3(512), 0, st, K, h.ld, h.nmax, meta, c0,
-                         bv, ukp, ngrp, cnt, toff, (int)tot, kamax, kls, h.n, h.m, src);
+                         bv, ukp, ngrp, cnt, toff, (int)tot, kamax, kls, h.n, h.m, src, b0);
     else
       hipLaunchKernelGGL((nlu_lcol_kernel<SRC, 1>), dim3((unsigned)tot), dim3(256), 0, st, K, h.ld, h.nmax, meta, c0,
-                         bv, ukp, ngrp, cnt, toff, (int)tot, kamax, kls, h.n, h.m, src);
+                         bv, ukp, ngrp, cnt, toff, (int)tot, kamax, kls, h.n, h.m, src, b0);
     DOPT_CHECK_HIP(hipGetLastError());
   };
+  auto ldiag = [&](hipStream_t st, int c0, double* bv, int b0, int Bs) {
+    if (h.ldl_mode)
+      hipLaunchKernelGGL((nlu_ldiag_kernel<SRC, true>), dim3(Bs), dim3(PNT), 0, st, K, h.ld, h.nmax, perm, dinv,
+                         dstride, meta, c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src, b0);
+    else
+      hipLaunchKernelGGL((nlu_ldiag_kernel<SRC, false>), dim3(Bs), dim3(PNT), 0, st, K, h.ld, h.nmax, perm, dinv,
+                         dstride, meta, c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src, b0);
+    DOPT_CHECK_HIP(hipGetLastError());
+  };
+  auto binv_of = [&](int c0) { return h.binv.as<double>() + (size_t)((c0 / NB64) & 1) * B * BSTR; };
+  if (h.lpersist && T == S) {   // one workgroup per problem for the whole factorisation (env DOPT_LPERSIST=1)
+    hipLaunchKernelGGL(nlu_left_all_kernel<SRC>, dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv, dstride, meta,
+                       h.binv.as<double>(), ukp, w0, w1, kamax, kls, h.n, h.m, src, npmax);
+    DOPT_CHECK_HIP(hipGetLastError());
+    return;
+  }
+  if (h.lslices == 2 && B >= 64 && T == S) {
+    // two batch halves, each its own chain on its own stream, the second one
+    // launch behind the first: a half's diagonal launch (VALU / latency
+    // bound) then shares the CUs with the other half's column tiles (MFMA /
+    // memory bound) instead of running alone (env DOPT_LSLICE=2)
+    ensure_aux(h);
+    const int B0 = B / 2;
+    hipStream_t st2 = h.aux;
+    for (int half = 0; half < 2; ++half) {
+      const int b0 = half ? B0 : 0, Bs = half ? B - B0 : B0;
+      hipStream_t st = half ? st2 : S;
+      for (int c0 = 0; c0 < npmax; c0 += NB64) {
+        ldiag(st, c0, binv_of(c0), b0, Bs);
+        if (half == 0 && c0 == 0) {   // the second half starts after the first half's first diagonal launch
+          DOPT_CHECK_HIP(hipEventRecord(h.ev_fork, S));
+          DOPT_CHECK_HIP(hipStreamWaitEvent(st2, h.ev_fork, 0));
+        }
+        const int ntile = (npmax - c0 - NB64 + 63) / 64;
+        if (ntile <= 0) break;
+        lcol(st, c0, binv_of(c0), 0, ntile, b0, Bs);
+      }
+    }
+    DOPT_CHECK_HIP(hipEventRecord(h.ev_join, st2));
+    DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_join, 0));
+    return;
+  }
   bool pending = false;   // T holds column tiles S must wait for
   for (int c0 = 0; c0 < npmax; c0 += NB64) {
-    double* bv = h.binv.as<double>() + (size_t)((c0 / NB64) & 1) * B * BSTR;
-    if (h.ldl_mode)
-      hipLaunchKernelGGL((nlu_ldiag_kernel<SRC, true>), dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv, dstride,
-                         meta, c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src);
-    else
-      hipLaunchKernelGGL((nlu_ldiag_kernel<SRC, false>), dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv, dstride,
-                         meta, c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src);
-    DOPT_CHECK_HIP(hipGetLastError());
+    double* bv = binv_of(c0);
+    ldiag(S, c0, bv, 0, B);
     const int ntile = (npmax - c0 - NB64 + 63) / 64;
     if (ntile <= 0) break;
     if (T == S) {
-      lcol(S, c0, bv, 0, ntile);
+      lcol(S, c0, bv, 0, ntile, 0, B);
       continue;
     }
     if (pending) {   // column J−1's tiles I ≥ J+1 (tile (J+1, J−1) feeds this column)
@@ -2174,9 +2286,9 @@ static void left_lu(Handle& h, const SRC& src, double* dinv, double* w0, double*
     }
     DOPT_CHECK_HIP(hipEventRecord(h.ev_fork, S));   // T: after ldiag(J) (and, in S order, all before it)
     DOPT_CHECK_HIP(hipStreamWaitEvent(T, h.ev_fork, 0));
-    lcol(S, c0, bv, 0, 1);
+    lcol(S, c0, bv, 0, 1, 0, B);
     if (ntile > 1) {
-      lcol(T, c0, bv, 1, ntile - 1);
+      lcol(T, c0, bv, 1, ntile - 1, 0, B);
       pending = true;
     }
   }

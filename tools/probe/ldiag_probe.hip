@@ -82,10 +82,10 @@ int main(int argc, char** argv) {
       double* bv = binv + (size_t)(J & 1) * B * BSTR;
       if (ldl)
         hipLaunchKernelGGL((nlu_ldiag_kernel<QSrc, true>), dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
-                           dinv_stride(nmax), meta, c0, bv, ukp, nullptr, nullptr, kamax, nullptr, n, 0, src);
+                           dinv_stride(nmax), meta, c0, bv, ukp, nullptr, nullptr, kamax, nullptr, n, 0, src, 0);
       else
         hipLaunchKernelGGL((nlu_ldiag_kernel<QSrc, false>), dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
-                           dinv_stride(nmax), meta, c0, bv, ukp, nullptr, nullptr, kamax, nullptr, n, 0, src);
+                           dinv_stride(nmax), meta, c0, bv, ukp, nullptr, nullptr, kamax, nullptr, n, 0, src, 0);
       hipEventRecord(ev[e++]);
 #ifdef LDIAG_STAMPS
       if (r == reps) {
@@ -102,7 +102,7 @@ int main(int argc, char** argv) {
       if (ntile > 0) {
         const int tot = ntile * B;
         hipLaunchKernelGGL((nlu_lcol_kernel<QSrc, 1>), dim3(tot), dim3(256), 0, 0, K, ld, nmax, meta, c0, bv, ukp,
-                           ntile, ntile, 0, tot, kamax, nullptr, n, 0, src);
+                           ntile, ntile, 0, tot, kamax, nullptr, n, 0, src, 0);
       }
       hipEventRecord(ev[e++]);
     }
