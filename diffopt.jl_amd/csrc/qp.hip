@@ -493,14 +493,23 @@ __global__ __launch_bounds__(TPB) void qp_fwd_rhs_kernel(
 //   eliminated rows (λ_i == 0, s_i != 0):
 //     reverse:  x_λi = (0 − G_i·x_z)/s_i          (row n+i of LHS)
 //     forward:  x_λi = r_i / s_i                   (row n+i of LHSᵀ)
+// x1 / out1 non-null: one launch for both directions of the fused call,
+// grid 2B — workgroups b < B the reverse outputs (x, out), b ≥ B the forward
+// ones of problem b − B (x1, out1): the light forward recovery rides beside the
+// reverse one's G reads instead of a launch of its own
 __global__ __launch_bounds__(TPB) void qp_output_kernel(
-    const double* __restrict__ x, const double* __restrict__ G,
+    const double* __restrict__ x0, const double* __restrict__ G,
     const double* __restrict__ s, const int32_t* __restrict__ rpos,
     const QPMeta* __restrict__ meta, const double* __restrict__ full, int n,
-    int m, int p, int nmax, int zcap, int trans, double* __restrict__ out) {
+    int m, int p, int nmax, int zcap, int trans0, double* __restrict__ out0, const double* __restrict__ x1,
+    double* __restrict__ out1, int B) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int nel;
-  const int b = blockIdx.x, t = threadIdx.x;
+  const bool second = x1 && (int)blockIdx.x >= B;   // workgroup-uniform
+  const int b = second ? (int)blockIdx.x - B : (int)blockIdx.x, t = threadIdx.x;
+  const double* __restrict__ x = second ? x1 : x0;
+  double* __restrict__ out = second ? out1 : out0;
+  const int trans = second ? 1 : trans0;
   const int nk = meta[b].nk;
   const double* xb = x + (size_t)b * nmax;
   double* ob = out + (size_t)b * (n + m + p);
@@ -973,7 +982,8 @@ static double* x_of(Handle& h, int trans) {
 // generic solves, LSQR and output recovery for one direction (the blocked
 // solves are launched by the callers); rhs / x / full: this direction's work
 // vectors (stride nmax per problem)
-static void finish_into(Handle& h, int trans, double* rhs, double* x, const double* full, double* out) {
+static void finish_into(Handle& h, int trans, double* rhs, double* x, const double* full, double* out,
+                        const double* pair_x = nullptr, double* pair_out = nullptr, bool solves_only = false) {
   const int B = (int)h.batch, n = h.n, m = h.m, p = h.p;
   const int nmax = h.nmax, ld = h.ld;
   QPMeta* meta = h.meta.as<QPMeta>();
@@ -991,17 +1001,29 @@ static void finish_into(Handle& h, int trans, double* rhs, double* x, const doub
                        trans, rhs, x, h.lsqr_ws.as<double>());
     check_launch();
   }
+  if (solves_only) return;
   static const double dummy = 0.0;
   PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
   const size_t olds = (n <= ZCAP ? (size_t)n * sizeof(double) : 0) +
                       (!trans && m <= OUT_LCAP ? (size_t)m * sizeof(int) : 0);
-  hipLaunchKernelGGL(qp_output_kernel, dim3(B), dim3(TPB), olds,
-                     h.stream, x, m ? h.G : &dummy, h.s.as<double>(), rpos_of(h), meta, full, n, m, p,
-                     nmax, ZCAP, trans, out);
+  if (pair_x) {   // the forward direction's outputs in the same launch (trans = 0 here)
+    hipLaunchKernelGGL(qp_output_kernel, dim3(2 * B), dim3(TPB), olds, h.stream, x, m ? h.G : &dummy,
+                       h.s.as<double>(), rpos_of(h), meta, full, n, m, p, nmax, ZCAP, 0, out, pair_x, pair_out, B);
+  } else {
+    hipLaunchKernelGGL(qp_output_kernel, dim3(B), dim3(TPB), olds, h.stream, x, m ? h.G : &dummy,
+                       h.s.as<double>(), rpos_of(h), meta, full, n, m, p, nmax, ZCAP, trans, out,
+                       (const double*)nullptr, (double*)nullptr, B);
+  }
   check_launch();
 }
 static void finish(Handle& h, int trans, double* out) {
   finish_into(h, trans, rhs_of(h, trans), x_of(h, trans), full_of(h), out);
+}
+// both directions of the fused call: the generic / LSQR solves per direction,
+// then one output launch for both
+static void finish_pair(Handle& h, double* out_rev, double* out_fwd) {
+  finish_into(h, 1, rhs_of(h, 1), x_of(h, 1), full_of(h), nullptr, nullptr, nullptr, true);
+  finish_into(h, 0, rhs_of(h, 0), x_of(h, 0), full_of(h), out_rev, x_of(h, 1), out_fwd);
 }
 
 static void rev_rhs(Handle& h, const double* dl_dz, double* copy = nullptr) {
@@ -1191,8 +1213,7 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
   };
   factor_blocked(h, [&] { solve2(h.lu_mode == 1 ? LU_SEL_NOPIV : LU_SEL_ALL, w0, w1); }, w0, w1, qp_reasm(h));
   if (h.n_pivot > 0) solve2(LU_SEL_PIVOT, nullptr, nullptr);
-  finish(h, 0, out_rev);
-  finish(h, 1, out_fwd);
+  finish_pair(h, out_rev, out_fwd);
   h.factored = true;   // the factors stay valid for later reverse / forward calls
   // the host already knows every info: the no-pivot LU accepted every blocked
   // problem (an accepted factor has no zero pivot) and no fallback or generic
