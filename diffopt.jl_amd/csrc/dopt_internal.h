@@ -156,6 +156,7 @@ struct Handle {
   int32_t lstreams = 0;            // left-looking LU: column tiles I ≥ J+2 on `aux` (env DOPT_LSTREAMS=1)
   DevBuf ukp;                      // left-looking LU: u_kk / p_k of every finished diagonal block (nmax per problem)
   int32_t lcol_tw = 1;             // left-looking LU column tiles per workgroup (env DOPT_LCOL_TW: 1 or 2)
+  int32_t lcol_pf = 0;             // left-looking column tiles: next strip prefetched (env DOPT_LCOL_PF=1; measured slower)
   int32_t lpersist = 0;            // left-looking LU: one workgroup per problem, one launch (env DOPT_LPERSIST=1)
   int32_t lslices = 1;             // left-looking LU: batch halves as two skewed chains (env DOPT_LSLICE=2)
   int32_t ldl_mode = 1;            // left-looking LU: diagonal blocks by the one-pass symmetric elimination

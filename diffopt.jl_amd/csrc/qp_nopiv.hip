@@ -1961,7 +1961,7 @@ __device__ __forceinline__ void stage_rowstrip_n(double* X, const double* Kb, in
 // Tiles it0 .. it0+TW−1 (from tile `toff` on) of block column J = c0 / 64 of
 // problem b (X: the workgroup's TW × NB64·TLD doubles of LDS);
 // nlu_lcol_kernel runs them for a batch, nlu_left_all_kernel inside its loop.
-template <class SRC, int TW>
+template <class SRC, int TW, bool PF = true>
 __device__ __forceinline__ void lcol_body(
     double (*X)[NB64 * TLD], int b, int it0, double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta,
     int c0, const double* __restrict__ binv, const double* __restrict__ ukp, int cnt, int toff,
@@ -1986,6 +1986,19 @@ __device__ __forceinline__ void lcol_body(
   d4n acc[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = (d4n){0, 0, 0, 0};
+  // the staged strip L(J, k) of the next k-block is loaded into registers
+  // while this one's MFMAs run (plain loads survive the barriers; stored to
+  // LDS after the barrier that retires this one): the stage is one LDS write
+  // pass, not a global round trip, per k-block (env DOPT_LCOL_PF=1; measured
+  // slower: config 3 LU 34.4 -> 37.3 ms, config 2 0.81 -> 0.83 ms — off)
+  constexpr int CW = 16 * 256 / NTH;   // strip columns per thread
+  const int sj = T & 63, skq = (T >> 6) * CW;
+  const double* srow = Kb + (size_t)(c0 + sj) * ld + skq;
+  double snx[CW];
+  if (PF && c0 > 0) {
+#pragma unroll
+    for (int u = 0; u < CW; ++u) snx[u] = srow[u];
+  }
   for (int k0 = 0; k0 < c0; k0 += NB64) {
     double a[16];   // loaded with the staging loads (one round trip per k-block)
     if (wact) {
@@ -1994,7 +2007,16 @@ __device__ __forceinline__ void lcol_body(
       for (int s = 0; s < 16; ++s) a[s] = ar[4 * s + g] * ud[k0 + 4 * s + g];
     }
     __syncthreads();
-    stage_rowstrip_n<NTH>(X[0], Kb, ld, c0, k0);   // block J is full (tiles follow it)
+    if (PF) {
+#pragma unroll
+      for (int u = 0; u < CW; ++u) X[0][(skq + u) * TLD + sj] = snx[u];
+      if (k0 + NB64 < c0) {
+#pragma unroll
+        for (int u = 0; u < CW; ++u) snx[u] = srow[k0 + NB64 + u];
+      }
+    } else {
+      stage_rowstrip_n<NTH>(X[0], Kb, ld, c0, k0);   // block J is full (tiles follow it)
+    }
     __syncthreads();
     if (wact) {
 #pragma unroll
@@ -2079,7 +2101,7 @@ __device__ __forceinline__ void lcol_body(
   if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;   // every writer stores the same value
 }
 
-template <class SRC, int TW>
+template <class SRC, int TW, bool PF>
 __global__ __launch_bounds__(256 * TW) __attribute__((amdgpu_waves_per_eu(4))) void nlu_lcol_kernel(
     double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
     const double* __restrict__ ukp, int ngrp, int cnt, int toff, int total, const double* __restrict__ kamax,
@@ -2089,8 +2111,8 @@ __global__ __launch_bounds__(256 * TW) __attribute__((amdgpu_waves_per_eu(4))) v
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
   const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
   const int bl = logical / ngrp;
-  lcol_body<SRC, TW>(X, b0 + bl, (logical - bl * ngrp) * TW, K, ld, nmax, meta, c0, binv, ukp, cnt, toff, kamax,
-                     kls, n, m, src);
+  lcol_body<SRC, TW, PF>(X, b0 + bl, (logical - bl * ngrp) * TW, K, ld, nmax, meta, c0, binv, ukp, cnt, toff,
+                         kamax, kls, n, m, src);
 }
 
 // The whole left-looking factorisation of one problem per workgroup, block
@@ -2220,11 +2242,14 @@ static void left_lu(Handle& h, const SRC& src, double* dinv, double* w0, double*
     const long long tot = (long long)ngrp * Bs;
     if (tot > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
     if (tw == 2)
-      hipLaunchKernelGGL((nlu_lcol_kernel<SRC, 2>), dim3((unsigned)tot), dim3(512), 0, st, K, h.ld, h.nmax, meta, c0,
-                         bv, ukp, ngrp, cnt, toff, (int)tot, kamax, kls, h.n, h.m, src, b0);
+      hipLaunchKernelGGL((nlu_lcol_kernel<SRC, 2, true>), dim3((unsigned)tot), dim3(512), 0, st, K, h.ld, h.nmax, meta,
+                         c0, bv, ukp, ngrp, cnt, toff, (int)tot, kamax, kls, h.n, h.m, src, b0);
+    else if (h.lcol_pf)
+      hipLaunchKernelGGL((nlu_lcol_kernel<SRC, 1, true>), dim3((unsigned)tot), dim3(256), 0, st, K, h.ld, h.nmax, meta,
+                         c0, bv, ukp, ngrp, cnt, toff, (int)tot, kamax, kls, h.n, h.m, src, b0);
     else
-      hipLaunchKernelGGL((nlu_lcol_kernel<SRC, 1>), dim3((unsigned)tot), dim3(256), 0, st, K, h.ld, h.nmax, meta, c0,
-                         bv, ukp, ngrp, cnt, toff, (int)tot, kamax, kls, h.n, h.m, src, b0);
+      hipLaunchKernelGGL((nlu_lcol_kernel<SRC, 1, false>), dim3((unsigned)tot), dim3(256), 0, st, K, h.ld, h.nmax,
+                         meta, c0, bv, ukp, ngrp, cnt, toff, (int)tot, kamax, kls, h.n, h.m, src, b0);
     DOPT_CHECK_HIP(hipGetLastError());
   };
   auto ldiag = [&](hipStream_t st, int c0, double* bv, int b0, int Bs) {

@@ -101,7 +101,7 @@ int main(int argc, char** argv) {
       const int ntile = (Np - c0 - 64 + 63) / 64;
       if (ntile > 0) {
         const int tot = ntile * B;
-        hipLaunchKernelGGL((nlu_lcol_kernel<QSrc, 1>), dim3(tot), dim3(256), 0, 0, K, ld, nmax, meta, c0, bv, ukp,
+        hipLaunchKernelGGL((nlu_lcol_kernel<QSrc, 1, true>), dim3(tot), dim3(256), 0, 0, K, ld, nmax, meta, c0, bv, ukp,
                            ntile, ntile, 0, tot, kamax, nullptr, n, 0, src, 0);
       }
       hipEventRecord(ev[e++]);
