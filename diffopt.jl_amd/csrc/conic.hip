@@ -338,6 +338,168 @@ __device__ __forceinline__ void psd_apply_cone(const ConeDesc cd, const double* 
   __syncthreads();
 }
 
+// One PSD cone of side d ≤ PSD_MAX with the images in LDS, on
+// v_mfma_f64_16x16x4f64: the four d×d products as 16×16 output tiles (up to
+// 4 × 4), tile idx ≡ wave (mod 4), the k-sum in steps of 4 over round_up(d, 4)
+// with reads outside [0, d) returning 0 (so the images need no zero padding and
+// the padded rows / columns of a product are never stored).  Every global load
+// of the cone (the identity flag, U, the input triangle, this lane's 16 entries
+// of B for the Hadamard product) is issued before the first use.  The middle
+// product UᵀXU is symmetric, so only its upper tiles are computed and mirrored;
+// the last one is stored as the upper triangle (MOI order) only.
+typedef double d4c __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ d4c cmfma(double a, double b, d4c c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+template <class FA, class FB, class FS>
+__device__ __forceinline__ void psd_mfma(int d, bool upper, FA a, FB b, FS st) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, l16 = lane & 15, g = lane >> 4;
+  const int nT = (d + 15) >> 4;
+  int ti[4], tj[4];
+  bool on[4];
+  {
+    int idx = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) on[s] = false;
+    for (int r = 0; r < nT; ++r)
+      for (int c = upper ? r : 0; c < nT; ++c, ++idx)
+        if ((idx & 3) == wv) {
+          const int s = idx >> 2;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (k == s) { ti[k] = r; tj[k] = c; on[k] = true; }
+        }
+  }
+  if (!on[0]) return;   // wave-uniform; no barrier inside
+  d4c acc[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc[s] = (d4c){0.0, 0.0, 0.0, 0.0};
+  const int dp = (d + 3) & ~3;
+  for (int q0 = 0; q0 < dp; q0 += 4) {
+    const int q = q0 + g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      if (on[s]) acc[s] = cmfma(a(16 * ti[s] + l16, q), b(q, 16 * tj[s] + l16), acc[s]);
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    if (on[s])
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) st(16 * ti[s] + g + 4 * rr, 16 * tj[s] + l16, acc[s][rr], s, rr);
+}
+
+__device__ __forceinline__ void psd_apply_cone_lds(const ConeDesc cd, const double* __restrict__ P,
+                                                   const double* in, double* out, int trans, double* Xs,
+                                                   double* Ys, double* Us) {
+  const int t = threadIdx.x;
+  const int d = psd_side(cd.dim);
+  const int ld = ((d + 3) & ~3) + 1;
+  const int dd = d * d;
+  const double* U = P + cd.poff;
+  const double* Bm = U + dd;
+  const double* w = in + cd.row;
+  double* o = out + cd.row;
+  constexpr int UR = (PSD_MAX * PSD_MAX + CTPB - 1) / CTPB;                    // 16
+  constexpr int WR = (PSD_MAX * (PSD_MAX + 1) / 2 + CTPB - 1) / CTPB;          // 9
+  const double identf = U[2 * dd];
+  double ur[UR], wr[WR];
+#pragma unroll
+  for (int k = 0; k < UR; ++k) {
+    const int e = t + CTPB * k;
+    ur[k] = U[e < dd ? e : 0];
+  }
+#pragma unroll
+  for (int k = 0; k < WR; ++k) {
+    const int e = t + CTPB * k;
+    wr[k] = w[e < cd.dim ? e : 0];
+  }
+  if (identf != 0.0) {   // Dπ = I (every eigenvalue ≥ 0)
+#pragma unroll
+    for (int k = 0; k < WR; ++k) {
+      const int e = t + CTPB * k;
+      if (e < cd.dim) o[e] = wr[k];
+    }
+    return;
+  }
+  // this lane's entries of B at the middle product's output positions: the
+  // upper tiles of psd_mfma's enumeration for this wave (mirrored below)
+  const int lane = t & 63, wv = t >> 6, l16 = lane & 15, g = lane >> 4;
+  const int nT = (d + 15) >> 4;
+  double br[4][4];
+  {
+    int idx = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) br[s][rr] = 0.0;
+    for (int r = 0; r < nT; ++r)
+      for (int c = r; c < nT; ++c, ++idx)
+        if ((idx & 3) == wv) {
+          const int s = idx >> 2;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (k == s)
+#pragma unroll
+              for (int rr = 0; rr < 4; ++rr) {
+                const int i = 16 * r + g + 4 * rr, j = 16 * c + l16;
+                const bool ok = i < d && j < d;
+                const double bv = Bm[ok ? i * d + j : 0];
+                br[k][rr] = ok ? bv : 0.0;
+              }
+        }
+  }
+#pragma unroll
+  for (int k = 0; k < UR; ++k) {
+    const int e = t + CTPB * k;
+    if (e < dd) Us[(e / d) * ld + e % d] = ur[k];
+  }
+  // X = smat(S⁻² w) for Dπ (= Jᵀ = S²JS⁻²), smat(w) for Dπᵀ (= J)
+#pragma unroll
+  for (int k = 0; k < WR; ++k) {
+    const int e = t + CTPB * k;
+    if (e < cd.dim) {
+      int c = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+      if (c * (c + 1) / 2 > e) --c;
+      if ((c + 1) * (c + 2) / 2 <= e) ++c;
+      const int a = e - c * (c + 1) / 2;
+      const double val = (!trans && a != c) ? 0.5 * wr[k] : wr[k];
+      Xs[a * ld + c] = val;
+      Xs[c * ld + a] = val;
+    }
+  }
+  __syncthreads();
+  auto rd = [&](const double* img, int i, int j) {
+    const bool ok = i < d && j < d;
+    const double v = img[ok ? i * ld + j : 0];
+    return ok ? v : 0.0;
+  };
+  // Y = Uᵀ X
+  psd_mfma(d, false, [&](int i, int q) { return rd(Us, q, i); }, [&](int q, int j) { return rd(Xs, q, j); },
+           [&](int i, int j, double v, int, int) { if (i < d && j < d) Ys[i * ld + j] = v; });
+  __syncthreads();
+  // X = (Y U) ∘ B, upper tiles, mirrored
+  psd_mfma(d, true, [&](int i, int q) { return rd(Ys, i, q); }, [&](int q, int j) { return rd(Us, q, j); },
+           [&](int i, int j, double v, int s, int rr) {
+             if (i < d && j < d) {
+               const double x = v * br[s][rr];
+               Xs[i * ld + j] = x;
+               Xs[j * ld + i] = x;
+             }
+           });
+  __syncthreads();
+  // Y = U X
+  psd_mfma(d, false, [&](int i, int q) { return rd(Us, i, q); }, [&](int q, int j) { return rd(Xs, q, j); },
+           [&](int i, int j, double v, int, int) { if (i < d && j < d) Ys[i * ld + j] = v; });
+  __syncthreads();
+  // out = tri(Y Uᵀ) (upper tiles; S² for Dπ)
+  psd_mfma(d, true, [&](int i, int q) { return rd(Ys, i, q); }, [&](int q, int j) { return rd(Us, j, q); },
+           [&](int i, int j, double v, int, int) {
+             if (i <= j && j < d) o[tri_idx(i, j)] = (!trans && i != j) ? 2.0 * v : v;
+           });
+  __syncthreads();
+}
+
 template <bool BIG = false>
 __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, const double* __restrict__ v,
                           const double* __restrict__ P, const double* in, double* out,
@@ -396,7 +558,11 @@ __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, con
       psd_apply_cone(cd, P, in, out, trans, g, g + img, g + 2 * img);
     } else {
       const size_t img = (size_t)((d + 3) & ~3) * (((d + 3) & ~3) + 1);   // this cone's image: dp × (dp+1)
-      psd_apply_cone(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
+      // the MFMA form in the split path's Dπ kernel; the persistent LSQR
+      // kernels keep the register-tile form (the MFMA form's prefetched
+      // operands push conic_lsqr2_kernel from 42 to 141 VGPR spills)
+      if (BIG) psd_apply_cone_lds(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
+      else psd_apply_cone(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
     }
   }
   __syncthreads();
@@ -424,14 +590,14 @@ constexpr int PAIR_ROWS = 64 * PAIR_K;
 // NV = 1 summation order exactly (the column chunk NC only groups loads), so
 // the co-iterated sequences are bit-identical to separate ones.  NC = 2 for
 // NV = 2 keeps two waves per SIMD.  ys: NV·4·PAIR_ROWS doubles.
-template <int NV, int PK = PAIR_K, int NC = (NV == 1 ? PAIR_NC : 2)>
+template <int NV, int PK = PAIR_K, int NC = (NV == 1 ? PAIR_NC : 2), int NW = 4>
 __device__ __forceinline__ void gemv_multi(const double* __restrict__ A, int ld, int m, int n,
                                            const double* const* x, const double* const* w, double* const* y,
                                            double* const* g, double* __restrict__ ys) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (m <= 0) {
     for (int q = 0; q < NV; ++q)
-      for (int j = threadIdx.x; j < n; j += CTPB) g[q][j] = 0.0;
+      for (int j = threadIdx.x; j < n; j += 64 * NW) g[q][j] = 0.0;
     __syncthreads();
     return;
   }
@@ -450,11 +616,11 @@ __device__ __forceinline__ void gemv_multi(const double* __restrict__ A, int ld,
     }
     const double* Ar = A + r0 + lane;
     int j = wv;
-    for (; j + 4 * (NC - 1) < n; j += 4 * NC) {
+    for (; j + NW * (NC - 1) < n; j += NW * NC) {
       double a[NC][PK];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        const double* cc = Ar + (size_t)(j + 4 * c) * ld;
+        const double* cc = Ar + (size_t)(j + NW * c) * ld;
 #pragma unroll
         for (int k = 0; k < PK; ++k) a[c][k] = ok[k] ? cc[64 * k] : 0.0;
       }
@@ -463,7 +629,7 @@ __device__ __forceinline__ void gemv_multi(const double* __restrict__ A, int ld,
       for (int q = 0; q < NV; ++q) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-          const double xc = x[q][j + 4 * c];
+          const double xc = x[q][j + NW * c];
           double acc = 0.0;
 #pragma unroll
           for (int k = 0; k < PK; ++k) {
@@ -484,10 +650,10 @@ __device__ __forceinline__ void gemv_multi(const double* __restrict__ A, int ld,
 #pragma unroll
         for (int q = 0; q < NV; ++q)
 #pragma unroll
-          for (int c = 0; c < NC; ++c) g[q][j + 4 * c] = r0 ? g[q][j + 4 * c] + sc[q][c] : sc[q][c];
+          for (int c = 0; c < NC; ++c) g[q][j + NW * c] = r0 ? g[q][j + NW * c] + sc[q][c] : sc[q][c];
       }
     }
-    for (; j < n; j += 4) {
+    for (; j < n; j += NW) {
       const double* c0 = Ar + (size_t)j * ld;
       double a0[PK];
 #pragma unroll
@@ -508,12 +674,16 @@ __device__ __forceinline__ void gemv_multi(const double* __restrict__ A, int ld,
 #pragma unroll
     for (int q = 0; q < NV; ++q)
 #pragma unroll
-      for (int k = 0; k < PK; ++k) ys[(q * 4 + wv) * (64 * PK) + lane + 64 * k] = ya[q][k];
+      for (int k = 0; k < PK; ++k) ys[(q * NW + wv) * (64 * PK) + lane + 64 * k] = ya[q][k];
     __syncthreads();
     for (int q = 0; q < NV; ++q) {
-      const double* yq = ys + q * 4 * (64 * PK);
-      for (int r = threadIdx.x; r < (64 * PK) && r0 + r < m; r += CTPB)
-        y[q][r0 + r] = (yq[r] + yq[(64 * PK) + r]) + (yq[2 * (64 * PK) + r] + yq[3 * (64 * PK) + r]);
+      const double* yq = ys + q * NW * (64 * PK);
+      for (int r = threadIdx.x; r < (64 * PK) && r0 + r < m; r += 64 * NW) {
+        double s = (yq[r] + yq[(64 * PK) + r]) + (yq[2 * (64 * PK) + r] + yq[3 * (64 * PK) + r]);
+        if (NW == 8)
+          s += (yq[4 * (64 * PK) + r] + yq[5 * (64 * PK) + r]) + (yq[6 * (64 * PK) + r] + yq[7 * (64 * PK) + r]);
+        y[q][r0 + r] = s;
+      }
     }
     __syncthreads();
   }
@@ -1127,6 +1297,7 @@ constexpr int SPLIT_CHUNK = 8;
 #endif
 constexpr int SPLIT_K = DOPT_SPLIT_K;            // rows per lane of a split row block
 constexpr int SPLIT_ROWS = 64 * SPLIT_K;
+constexpr int SPLIT_FUSE_NMAX = 4096;   // fused form: u_n / v'_n of a sequence in LDS
 
 struct LsqrState {
   double alpha, beta, rhobar, phibar, anorm, ddnorm, xxnorm, zz, sn2, cs2, bnorm;
@@ -1180,10 +1351,11 @@ __global__ __launch_bounds__(CTPB) void conic_split_init_kernel(
 // 1: Mᵀ·u (x = u_n, w = u_m)
 // grid (row blocks, problems): every live sequence of problem b (nq of them)
 // from one sweep over the row block
-__global__ __launch_bounds__(CTPB) void conic_split_pass_kernel(
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void conic_split_pass_kernel(
     int dir, const double* __restrict__ A, const double* __restrict__ bvec, SplitWS ws,
     const LsqrState* __restrict__ stv, int nq) {
-  __shared__ double ys[2 * 4 * SPLIT_ROWS];
+  __shared__ double ys[2 * NW * SPLIT_ROWS];
   const int rb = blockIdx.x, b = blockIdx.y;
   int sq[2], cnt = 0;
   for (int q = 0; q < nq; ++q) {
@@ -1206,8 +1378,8 @@ __global__ __launch_bounds__(CTPB) void conic_split_pass_kernel(
     yb[c] = ws.mvec(ws.yb, bv) + r0;
     gp[c] = ws.gpart + ((size_t)bv * ws.RB + rb) * n;
   }
-  if (cnt == 2) gemv_multi<2, SPLIT_K>(Ab, m, rows, n, src, wv, yb, gp, ys);
-  else gemv_multi<1, SPLIT_K>(Ab, m, rows, n, src, wv, yb, gp, ys);
+  if (cnt == 2) gemv_multi<2, SPLIT_K, 2, NW>(Ab, m, rows, n, src, wv, yb, gp, ys);
+  else gemv_multi<1, SPLIT_K, PAIR_NC, NW>(Ab, m, rows, n, src, wv, yb, gp, ys);
   const double* bb = bvec + (size_t)b * m + r0;
   for (int c = 0; c < cnt; ++c) {
     const int bv = sq[c];
@@ -1216,11 +1388,11 @@ __global__ __launch_bounds__(CTPB) void conic_split_pass_kernel(
       double* o = ws.vec(ws.out, bv) + n + r0;
       const double* vm = src[c] + n + r0;
       const double* Dv = ws.mvec(ws.Dv, bv) + r0;
-      for (int i = threadIdx.x; i < rows; i += CTPB) o[i] = yb[c][i] + vm[i] - Dv[i] + bb[i] * last;
+      for (int i = threadIdx.x; i < rows; i += 64 * NW) o[i] = yb[c][i] + vm[i] - Dv[i] + bb[i] * last;
     } else {
       double* tm = ws.mvec(ws.tmpm, bv) + r0;
       const double* um = src[c] + n + r0;
-      for (int i = threadIdx.x; i < rows; i += CTPB) tm[i] = -yb[c][i] - um[i] - bb[i] * last;
+      for (int i = threadIdx.x; i < rows; i += 64 * NW) tm[i] = -yb[c][i] - um[i] - bb[i] * last;
     }
   }
 }
@@ -1360,6 +1532,70 @@ __global__ __launch_bounds__(VT) void conic_split_upd_u_kernel(
   }
 }
 
+// One LSQR step's plane rotation (IterativeSolvers lsqr!, the loop body after
+// the bidiagonalisation) and, after the x / w update, its estimates and
+// stopping tests — shared by the split kernels so both forms compute the same
+// expressions.
+struct LsqrStep {
+  double rho, theta, rhobar, phi, phibar, tau, t1, t2;
+};
+__device__ __forceinline__ LsqrStep lsqr_rotate(const LsqrState& st, double alpha, double beta) {
+  LsqrStep g;
+  const double rhobar1 = st.rhobar;
+  g.rho = hypot(rhobar1, beta);
+  const double cs = rhobar1 / g.rho, sn = beta / g.rho;
+  g.theta = sn * alpha;
+  g.rhobar = -cs * alpha;
+  g.phi = cs * st.phibar;
+  g.phibar = sn * st.phibar;
+  g.tau = sn * g.phi;
+  g.t1 = g.phi / g.rho;
+  g.t2 = -g.theta / g.rho;
+  return g;
+}
+
+// updates st's recurrences and estimates; returns istop (0: go on)
+__device__ __forceinline__ int lsqr_tests(LsqrState& st, const LsqrStep& g, double alpha, double ddnorm,
+                                          int maxiter) {
+  const double eps = 2.220446049250313e-16;
+  const double atol = sqrt(eps), btol = sqrt(eps), ctol = sqrt(eps);
+  const double anorm = st.anorm, bnorm = st.bnorm;
+  const double delta = st.sn2 * g.rho, gambar = -st.cs2 * g.rho;
+  const double rhs_ = g.phi - delta * st.zz;
+  const double zbar = rhs_ / gambar;
+  const double xnorm = sqrt(st.xxnorm + zbar * zbar);
+  const double gamma = hypot(gambar, g.theta);
+  st.cs2 = gambar / gamma;
+  st.sn2 = g.theta / gamma;
+  st.zz = rhs_ / gamma;
+  st.xxnorm += st.zz * st.zz;
+  const double acond = anorm * sqrt(ddnorm);
+  const double rnorm = sqrt(g.phibar * g.phibar);
+  const double arnorm = alpha * fabs(g.tau);
+  const double test1 = rnorm / bnorm;
+  const double test2 = (anorm * rnorm != 0.0) ? arnorm / (anorm * rnorm) : 0.0;
+  const double test3 = (acond != 0.0) ? 1.0 / acond : 0.0;
+  const double t1r = test1 / (1.0 + anorm * xnorm / bnorm);
+  const double rtol = btol + atol * anorm * xnorm / bnorm;
+  int istop = 0;
+  if (st.it >= maxiter) istop = 7;
+  if (1.0 + test3 <= 1.0) istop = 6;
+  if (1.0 + test2 <= 1.0) istop = 5;
+  if (1.0 + t1r <= 1.0) istop = 4;
+  if (test3 <= ctol) istop = 3;
+  if (test2 <= atol) istop = 2;
+  if (test1 <= rtol) istop = 1;
+  st.alpha = alpha;
+  st.rhobar = g.rhobar;
+  st.phibar = g.phibar;
+  st.ddnorm = ddnorm;
+  st.istop = istop;
+  st.rnorm = rnorm;
+  st.arnorm = arnorm;
+  st.xnorm = xnorm;
+  return istop;
+}
+
 // finish Mᵀ·u into out: out_n = Σ_rb gpart − c·u_last, out_m += u_m,
 // out_end = c·u_n + b·u_m
 __device__ __forceinline__ void split_finish_T(const SplitWS& ws, int b, const double* bvec,
@@ -1400,9 +1636,11 @@ __device__ __forceinline__ void split_finish_T(const SplitWS& ws, int b, const d
 }
 
 // first Mᵀ·u: v = Mᵀu/α, w = v, recurrence initial values
+// pw (fused path, else null): this sequence's Σw² slots (nc of them, stride
+// PL per sequence) get Σw² in slot 0 and zeros
 __global__ __launch_bounds__(VT) void conic_split_init2_kernel(
     const double* __restrict__ bvec, const double* __restrict__ cvec, SplitWS ws,
-    LsqrState* __restrict__ stv, int32_t* __restrict__ active) {
+    LsqrState* __restrict__ stv, int32_t* __restrict__ active, double* __restrict__ pw, int PL, int nc) {
   __shared__ double red[VT / 64];
   const int b = blockIdx.x, t = threadIdx.x, N = ws.N;
   LsqrState st = stv[b];
@@ -1414,8 +1652,18 @@ __global__ __launch_bounds__(VT) void conic_split_init2_kernel(
   double aa = 0.0;
   for (int i = t; i < N; i += VT) aa = fma(out[i], out[i], aa);
   const double alpha = sqrt(vblock_sum(aa, red));
+  double ww = 0.0;
   if (alpha > 0.0)
-    for (int i = t; i < N; i += VT) { const double vi = out[i] / alpha; v[i] = vi; w[i] = vi; }
+    for (int i = t; i < N; i += VT) {
+      const double vi = out[i] / alpha;
+      v[i] = vi;
+      w[i] = vi;
+      ww = fma(vi, vi, ww);
+    }
+  if (pw) {
+    ww = vblock_sum(ww, red);
+    for (int r = t; r < nc; r += VT) pw[(size_t)b * PL + r] = r == 0 ? ww : 0.0;
+  }
   if (t == 0) {
     st.alpha = alpha;
     st.anorm = st.ddnorm = st.xxnorm = st.zz = st.sn2 = 0.0;
@@ -1446,15 +1694,8 @@ __global__ __launch_bounds__(VT) void conic_split_upd_v_kernel(
     if (alpha > 0.0) vscale(v, N, alpha);
     __syncthreads();
   }
-  const double rhobar1 = st.rhobar;
-  const double rho = hypot(rhobar1, beta);
-  const double cs = rhobar1 / rho, sn = beta / rho;
-  const double theta = sn * alpha;
-  const double rhobar = -cs * alpha;
-  const double phi = cs * st.phibar;
-  const double phibar = sn * st.phibar;
-  const double tau = sn * phi;
-  const double t1 = phi / rho, t2 = -theta / rho;
+  const LsqrStep gs = lsqr_rotate(st, alpha, beta);
+  const double t1 = gs.t1, t2 = gs.t2;
   double* x = ws.vec(ws.x, b);
   double* w = ws.vec(ws.w, b);
   double sw = 0.0;
@@ -1477,44 +1718,9 @@ __global__ __launch_bounds__(VT) void conic_split_upd_v_kernel(
       }
     }
   }
-  const double ddnorm = st.ddnorm + vblock_sum(sw, red) / (rho * rho);
+  const double ddnorm = st.ddnorm + vblock_sum(sw, red) / (gs.rho * gs.rho);
   if (t != 0) return;
-  const double eps = 2.220446049250313e-16;
-  const double atol = sqrt(eps), btol = sqrt(eps), ctol = sqrt(eps);
-  const double anorm = st.anorm, bnorm = st.bnorm;
-  const double delta = st.sn2 * rho, gambar = -st.cs2 * rho;
-  const double rhs_ = phi - delta * st.zz;
-  const double zbar = rhs_ / gambar;
-  const double xnorm = sqrt(st.xxnorm + zbar * zbar);
-  const double gamma = hypot(gambar, theta);
-  st.cs2 = gambar / gamma;
-  st.sn2 = theta / gamma;
-  st.zz = rhs_ / gamma;
-  st.xxnorm += st.zz * st.zz;
-  const double acond = anorm * sqrt(ddnorm);
-  const double rnorm = sqrt(phibar * phibar);
-  const double arnorm = alpha * fabs(tau);
-  const double test1 = rnorm / bnorm;
-  const double test2 = (anorm * rnorm != 0.0) ? arnorm / (anorm * rnorm) : 0.0;
-  const double test3 = (acond != 0.0) ? 1.0 / acond : 0.0;
-  const double t1r = test1 / (1.0 + anorm * xnorm / bnorm);
-  const double rtol = btol + atol * anorm * xnorm / bnorm;
-  int istop = 0;
-  if (st.it >= maxiter) istop = 7;
-  if (1.0 + test3 <= 1.0) istop = 6;
-  if (1.0 + test2 <= 1.0) istop = 5;
-  if (1.0 + t1r <= 1.0) istop = 4;
-  if (test3 <= ctol) istop = 3;
-  if (test2 <= atol) istop = 2;
-  if (test1 <= rtol) istop = 1;
-  st.alpha = alpha;
-  st.rhobar = rhobar;
-  st.phibar = phibar;
-  st.ddnorm = ddnorm;
-  st.istop = istop;
-  st.rnorm = rnorm;
-  st.arnorm = arnorm;
-  st.xnorm = xnorm;
+  const int istop = lsqr_tests(st, gs, alpha, ddnorm, maxiter);
   if (istop) {
     st.done = 1;
     atomicSub(active, 1);
@@ -1542,6 +1748,345 @@ __global__ __launch_bounds__(CTPB) void conic_split_out_kernel(
     const LsqrState& st = stv[bv];
     norms[(size_t)4 * b + t] = t == 0 ? st.rnorm : t == 1 ? st.arnorm : t == 2 ? st.xnorm : st.anorm;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Fused split LSQR (default; DOPT_SPLIT_FUSE=0 → the six-launch form above):
+// the per-sequence vector kernels folded into the passes and the Dπ launches,
+// four launches per iteration:
+//   passM (row blocks × problems): rows of A·v_n and the block's partial
+//         Aᵀ·Dv (gpM); on its rows u' = M·v − αu, and the block's Σu'², Σb·Dv
+//   passT (row blocks × problems): prologue u'_n = −Σ_rb gpM + c·v_end − αu_n,
+//         u'_end, β = ‖u'‖ from the partials, u = u'/β (u_n in LDS for the
+//         block's own sweep; row block 0 writes it and the step's scalars);
+//         then rows of A·u_n, the partial Aᵀ·u_m (gpT), the block's Σb·u_m
+//   dpiU  (cones × sequences): the cone's rows of v' = Dπᵀ(…) + u_m − βv, Σv'²
+//   dpiV  (cones × sequences): prologue v'_n = Σ_rb gpT − c·u_end − βv_n,
+//         v'_end, α = ‖v'‖, the rotation, x and w on the cone's rows (cone 0:
+//         the n part and the end as well), Σw² of the new w, the stopping
+//         tests; then Dv = Dπ v_m on the cone for the next iteration.
+// Every workgroup recomputes a step's shared scalars from the same partials in
+// the same order, so they agree bit for bit.  What one workgroup writes while
+// another of the same launch still reads the previous value — u, v, the
+// state and the Σw² slots — is double-buffered by iteration parity `par`;
+// each workgroup writes only its own rows (and block 0 / cone 0 the shared
+// n part and end), so no value is read and written by different workgroups
+// of one launch.
+// ---------------------------------------------------------------------------
+struct FSplit {
+  double *x, *w, *Dv, *tmpm, *yb, *gpM, *gpT, *part;
+  double *u0, *u1, *v0, *v1;
+  LsqrState *s0, *s1;
+  int N, m, n, RB, B, nc, PL;
+  __device__ int phys(int bv) const { return bv % B; }
+  __device__ double* U(int p, int bv) const { return (p ? u1 : u0) + (size_t)bv * N; }
+  __device__ double* V(int p, int bv) const { return (p ? v1 : v0) + (size_t)bv * N; }
+  __device__ LsqrState* S(int p) const { return p ? s1 : s0; }
+  // partial slots per sequence: Σu'² [RB] | Σb·Dv [RB] | Σb·u_m [RB] | Σv'² [nc] | Σw² [2][nc]
+  __device__ double* P(int bv) const { return part + (size_t)bv * PL; }
+  __device__ int oPbd() const { return RB; }
+  __device__ int oPbu() const { return 2 * RB; }
+  __device__ int oPv() const { return 3 * RB; }
+  __device__ int oPw(int p) const { return 3 * RB + nc + p * nc; }
+};
+
+// K block sums at once (fixed order: every workgroup of a launch that reduces
+// the same values gets the same bits); red: K·TPB/64 doubles
+template <int TPB, int K>
+__device__ __forceinline__ void bsumk(double (&v)[K], double* red) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = cwave_sum(v[k]);
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) red[K * wv + k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < TPB / 64; ++q) s += red[K * q + k];
+    v[k] = s;
+  }
+}
+
+// Σ_rb gp[rb·n + j], eight loads in flight
+__device__ __forceinline__ double gsum8(const double* __restrict__ gp, int RB, int n, int j) {
+  double s[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = 0.0;
+  int r = 0;
+  for (; r + 8 <= RB; r += 8)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] += gp[(size_t)(r + k) * n + j];
+  for (; r < RB; ++r) s[0] += gp[(size_t)r * n + j];
+  return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
+
+// DIR 0: passM, DIR 1: passT (see above).  Dynamic LDS (passT): u_n of the
+// (up to two) live sequences, 2·n doubles.
+template <int NW, int DIR>
+__global__ __launch_bounds__(64 * NW) void conic_fsplit_pass_kernel(
+    const double* __restrict__ A, const double* __restrict__ bvec, const double* __restrict__ cvec, FSplit fs,
+    int par, int nq) {
+  constexpr int TPB = 64 * NW;
+  __shared__ double ys[2 * NW * SPLIT_ROWS];
+  __shared__ double red[4 * NW];
+  extern __shared__ __attribute__((aligned(16))) double ul[];
+  const int rb = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  LsqrState* S = fs.S(par);
+  int sq[2], cnt = 0;
+  for (int q = 0; q < nq; ++q)
+    if (!S[q * fs.B + b].done) sq[cnt++] = q * fs.B + b;
+  if (cnt == 0) return;   // workgroup-uniform
+  const int m = fs.m, n = fs.n, N = fs.N, RB = fs.RB;
+  const int r0 = rb * SPLIT_ROWS;
+  const int rows = min(SPLIT_ROWS, m - r0);
+  const double* Ab = A + (size_t)b * m * n + r0;
+  const double* bb = bvec + (size_t)b * m + r0;
+  const double* xs[2];
+  const double* wv[2];
+  double* yv[2];
+  double* gv[2];
+  int live[2], nl = 0;
+  double uen[2] = {0.0, 0.0};   // DIR 1: the live sequences' u_end (normalised)
+  if (DIR == 0) {
+    for (int c = 0; c < cnt; ++c) {
+      const int bv = sq[c];
+      xs[c] = fs.V(par, bv);
+      wv[c] = fs.Dv + (size_t)bv * m + r0;
+      yv[c] = fs.yb + (size_t)bv * m + r0;
+      gv[c] = fs.gpM + ((size_t)bv * RB + rb) * n;
+      live[c] = bv;
+    }
+    nl = cnt;
+  } else {
+    // prologue: u' on the n part and the end, β, u = u'/β
+    const double* c = cvec + (size_t)b * n;
+    double al[2] = {0.0, 0.0}, ve[2] = {0.0, 0.0}, acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int ci = 0; ci < cnt; ++ci) {
+      al[ci] = S[sq[ci]].alpha;
+      ve[ci] = fs.V(par, sq[ci])[N - 1];
+    }
+    for (int j = t; j < n; j += TPB) {
+      const double cj = c[j];
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci)
+        if (ci < cnt) {
+          const int bv = sq[ci];
+          const double g = gsum8(fs.gpM + (size_t)bv * RB * n, RB, n, j);
+          const double val = (-g + cj * ve[ci]) - al[ci] * fs.U(par, bv)[j];
+          ul[ci * n + j] = val;
+          acc[2 * ci] = fma(val, val, acc[2 * ci]);
+          acc[2 * ci + 1] = fma(cj, fs.V(par, bv)[j], acc[2 * ci + 1]);
+        }
+    }
+    for (int ci = 0; ci < cnt; ++ci) {
+      const double* Pq = fs.P(sq[ci]);
+      for (int r = t; r < RB; r += TPB) {
+        acc[2 * ci] += Pq[r];
+        acc[2 * ci + 1] += Pq[fs.oPbd() + r];
+      }
+    }
+    bsumk<TPB, 4>(acc, red);
+    for (int ci = 0; ci < cnt; ++ci) {
+      const int bv = sq[ci];
+      const double* uo = fs.U(par, bv);
+      double* un = fs.U(par ^ 1, bv);
+      const double uend = -acc[2 * ci + 1] - al[ci] * uo[N - 1];
+      const double beta = sqrt(acc[2 * ci] + uend * uend);
+      if (rb == 0 && t == 0) {
+        LsqrState& st = S[bv];   // fields no other workgroup of this launch reads
+        st.it += 1;
+        st.beta = beta;
+        st.skipT = !(beta > 0.0);
+        if (beta > 0.0) st.anorm = sqrt(st.anorm * st.anorm + al[ci] * al[ci] + beta * beta);
+      }
+      const double dv = beta > 0.0 ? beta : 1.0;   // β = 0: u stays u' (skipT), as upd_u
+      for (int j = t; j < n; j += TPB) {
+        const double x = ul[ci * n + j] / dv;
+        ul[ci * n + j] = x;
+        if (rb == 0) un[j] = x;
+      }
+      if (rb == 0 && t == 0) un[N - 1] = uend / dv;
+      for (int i = t; i < rows; i += TPB) un[n + r0 + i] /= dv;
+      if (beta > 0.0) {
+        xs[nl] = ul + ci * n;
+        wv[nl] = un + n + r0;
+        yv[nl] = fs.yb + (size_t)bv * m + r0;
+        gv[nl] = fs.gpT + ((size_t)bv * RB + rb) * n;
+        uen[nl] = uend / dv;
+        live[nl++] = bv;
+      }
+    }
+    __syncthreads();   // u_n in LDS and this block's rows of u (global) before the sweep
+  }
+  if (nl == 0) return;
+  if (nl == 2) gemv_multi<2, SPLIT_K, 2, NW>(Ab, m, rows, n, xs, wv, yv, gv, ys);
+  else gemv_multi<1, SPLIT_K, PAIR_NC, NW>(Ab, m, rows, n, xs, wv, yv, gv, ys);
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int c = 0; c < nl; ++c) {
+    const int bv = live[c];
+    const double* y = yv[c];
+    if (DIR == 0) {
+      const double alpha = S[bv].alpha;
+      const double* v = fs.V(par, bv);
+      const double vend = v[N - 1];
+      const double* vm = v + n + r0;
+      const double* Dv = wv[c];
+      const double* uo = fs.U(par, bv) + n + r0;
+      double* un = fs.U(par ^ 1, bv) + n + r0;
+      for (int i = t; i < rows; i += TPB) {
+        const double o = y[i] + vm[i] - Dv[i] + bb[i] * vend;
+        const double u = o - alpha * uo[i];
+        un[i] = u;
+        acc[2 * c] = fma(u, u, acc[2 * c]);
+        acc[2 * c + 1] = fma(bb[i], Dv[i], acc[2 * c + 1]);
+      }
+    } else {
+      const double* um = wv[c];
+      const double ue = uen[c];
+      double* tm = fs.tmpm + (size_t)bv * m + r0;
+      for (int i = t; i < rows; i += TPB) {
+        tm[i] = -y[i] - um[i] - bb[i] * ue;
+        acc[2 * c] = fma(bb[i], um[i], acc[2 * c]);
+      }
+    }
+  }
+  bsumk<TPB, 4>(acc, red);
+  if (t == 0)
+    for (int c = 0; c < nl; ++c) {
+      double* Pq = fs.P(live[c]);
+      if (DIR == 0) {
+        Pq[rb] = acc[2 * c];
+        Pq[fs.oPbd() + rb] = acc[2 * c + 1];
+      } else {
+        Pq[fs.oPbu() + rb] = acc[2 * c];
+      }
+    }
+}
+
+// dpiU: one cone per workgroup; v' = Dπᵀ(tmpm) + u_m − βv on the cone's rows
+__global__ __launch_bounds__(CTPB) void conic_fsplit_dpiU_kernel(
+    const ConeDesc* __restrict__ cones_g, const double* __restrict__ vcone, const double* __restrict__ P,
+    int plen, FSplit fs, int par, double* __restrict__ gws, int wlen) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ double red[4];
+  const int k = blockIdx.x, bv = blockIdx.y, t = threadIdx.x;
+  const LsqrState& st = fs.S(par)[bv];
+  if (st.done || st.skipT) return;
+  const ConeDesc cd = cones_g[k];
+  const int n = fs.n, m = fs.m;
+  const double* pv = vcone + (size_t)fs.phys(bv) * m;
+  const double* pp = P + (size_t)fs.phys(bv) * plen;
+  double* vn = fs.V(par ^ 1, bv);
+  dpi_apply<true>(&cd, 1, pv, pp, fs.tmpm + (size_t)bv * m, vn + n, 1, lds, red, gws + (size_t)bv * wlen);
+  const double beta = st.beta;
+  const double* vo = fs.V(par, bv);
+  const double* un = fs.U(par ^ 1, bv);
+  double acc = 0.0;
+  for (int r = t; r < cd.dim; r += CTPB) {
+    const int i = n + cd.row + r;
+    const double val = (vn[i] + un[i]) - beta * vo[i];
+    vn[i] = val;
+    acc = fma(val, val, acc);
+  }
+  acc = cblock_sum(acc, red);
+  if (t == 0) fs.P(bv)[fs.oPv() + k] = acc;
+}
+
+// dpiV: finish the iteration (first = 0), then Dv = Dπ v_m on the cone.
+// Dynamic LDS: the Dπ images (img doubles), then v'_n (n doubles).
+__global__ __launch_bounds__(CTPB) void conic_fsplit_dpiV_kernel(
+    const ConeDesc* __restrict__ cones_g, const double* __restrict__ vcone, const double* __restrict__ P,
+    int plen, const double* __restrict__ cvec, FSplit fs, int par, int first, int maxiter,
+    int32_t* __restrict__ active, double* __restrict__ gws, int wlen, int img) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ double red[8];
+  const int k = blockIdx.x, bv = blockIdx.y, t = threadIdx.x;
+  const ConeDesc cd = cones_g[k];
+  const int n = fs.n, m = fs.m, N = fs.N, RB = fs.RB;
+  int vp = par;   // buffer of the v the Dπ apply reads
+  if (!first) {
+    LsqrState st = fs.S(par)[bv];
+    LsqrState* Sn = fs.S(par ^ 1);
+    if (st.done) {   // carried into the next parity's buffer
+      if (k == 0 && t == 0) Sn[bv] = st;
+      return;
+    }
+    const double beta = st.beta;
+    double alpha = st.alpha;
+    const double* vo = fs.V(par, bv);
+    double* vn = fs.V(par ^ 1, bv);
+    double* Pq = fs.P(bv);
+    const int rlo = n + cd.row, rhi = n + cd.row + cd.dim;
+    if (!st.skipT) {
+      const double* un = fs.U(par ^ 1, bv);
+      const double* c = cvec + (size_t)fs.phys(bv) * n;
+      double* vl = lds + img;
+      const double ue = un[N - 1];
+      double acc[2] = {0.0, 0.0};
+      for (int j = t; j < n; j += CTPB) {
+        const double cj = c[j];
+        const double val = (gsum8(fs.gpT + (size_t)bv * RB * n, RB, n, j) - cj * ue) - beta * vo[j];
+        vl[j] = val;
+        acc[0] = fma(val, val, acc[0]);
+        acc[1] = fma(cj, un[j], acc[1]);
+      }
+      for (int r = t; r < fs.nc; r += CTPB) acc[0] += Pq[fs.oPv() + r];
+      for (int r = t; r < RB; r += CTPB) acc[1] += Pq[fs.oPbu() + r];
+      bsumk<CTPB, 2>(acc, red);
+      const double vend = acc[1] - beta * vo[N - 1];
+      alpha = sqrt(acc[0] + vend * vend);
+      const double dv = alpha > 0.0 ? alpha : 1.0;   // α = 0: v stays v', as upd_v
+      for (int i = rlo + t; i < rhi; i += CTPB) vn[i] /= dv;
+      if (k == 0) {
+        for (int j = t; j < n; j += CTPB) vn[j] = vl[j] / dv;
+        if (t == 0) vn[N - 1] = vend / dv;
+      }
+    } else {   // no Mᵀ·u this step: v unchanged
+      for (int i = rlo + t; i < rhi; i += CTPB) vn[i] = vo[i];
+      if (k == 0) {
+        for (int j = t; j < n; j += CTPB) vn[j] = vo[j];
+        if (t == 0) vn[N - 1] = vo[N - 1];
+      }
+    }
+    const LsqrStep gs = lsqr_rotate(st, alpha, beta);
+    double* x = fs.x + (size_t)bv * N;
+    double* w = fs.w + (size_t)bv * N;
+    // each thread reads back only the v entries it wrote above
+    double acc[2] = {0.0, 0.0};
+    auto upd = [&](int i) {
+      const double wo = w[i];
+      x[i] = x[i] + gs.t1 * wo;
+      const double wn = vn[i] + gs.t2 * wo;
+      w[i] = wn;
+      acc[0] = fma(wn, wn, acc[0]);
+    };
+    for (int i = rlo + t; i < rhi; i += CTPB) upd(i);
+    if (k == 0) {
+      for (int j = t; j < n; j += CTPB) upd(j);
+      if (t == 0) upd(N - 1);
+    }
+    for (int r = t; r < fs.nc; r += CTPB) acc[1] += Pq[fs.oPw(par) + r];   // Σ of the old w²
+    bsumk<CTPB, 2>(acc, red);
+    if (t == 0) Pq[fs.oPw(par ^ 1) + k] = acc[0];
+    const double ddnorm = st.ddnorm + acc[1] / (gs.rho * gs.rho);
+    const int istop = lsqr_tests(st, gs, alpha, ddnorm, maxiter);
+    if (k == 0 && t == 0) {
+      if (istop) st.done = 1;
+      Sn[bv] = st;
+      if (istop) atomicSub(active, 1);
+    }
+    if (istop) return;   // workgroup-uniform
+    __syncthreads();     // the cone's rows of v before the Dπ apply's loads
+    vp = par ^ 1;
+  } else if (fs.S(par)[bv].done) {
+    return;
+  }
+  dpi_apply<true>(&cd, 1, vcone + (size_t)fs.phys(bv) * m, P + (size_t)fs.phys(bv) * plen,
+                  fs.V(vp, bv) + n, fs.Dv + (size_t)bv * m, 0, lds, red, gws + (size_t)bv * wlen);
 }
 
 // ---------------------------------------------------------------------------
@@ -1629,26 +2174,69 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
   const int nc = (int)h.cones.size() / 2;
   const int N = n + m + 1;
   const int RB = std::max(1, (m + SPLIT_ROWS - 1) / SPLIT_ROWS);
-  const size_t per = (size_t)5 * N + 4 * (size_t)std::max(m, 1) + (size_t)RB * n;
-  h.csplit.ensure((size_t)V * per * sizeof(double) + (size_t)V * sizeof(LsqrState) + 64);
+  const size_t M1 = (size_t)std::max(m, 1);
+  // fused form: u_n of two sequences in the pass kernel's LDS, v'_n in dpiV's
+  const bool fuse = h.split_fuse && nc > 0 && n <= SPLIT_FUSE_NMAX;
+  const int PL = 3 * RB + 3 * nc;
+  const size_t per = fuse ? (size_t)6 * N + 3 * M1 + (size_t)2 * RB * n + PL
+                          : (size_t)5 * N + 4 * M1 + (size_t)RB * n;
+  h.csplit.ensure((size_t)V * per * sizeof(double) + (size_t)2 * V * sizeof(LsqrState) + 64);
   SplitWS ws;
+  FSplit fs;
   double* base = h.csplit.as<double>();
-  ws.x = base;
-  ws.u = ws.x + (size_t)V * N;
-  ws.v = ws.u + (size_t)V * N;
-  ws.w = ws.v + (size_t)V * N;
-  ws.out = ws.w + (size_t)V * N;
-  ws.Dv = ws.out + (size_t)V * N;
-  ws.tmpm = ws.Dv + (size_t)V * std::max(m, 1);
-  ws.yb = ws.tmpm + (size_t)V * std::max(m, 1);
-  ws.gpart = ws.yb + (size_t)V * std::max(m, 1);
+  LsqrState* st;
+  if (fuse) {
+    fs.x = base;
+    fs.w = fs.x + (size_t)V * N;
+    fs.u0 = fs.w + (size_t)V * N;
+    fs.u1 = fs.u0 + (size_t)V * N;
+    fs.v0 = fs.u1 + (size_t)V * N;
+    fs.v1 = fs.v0 + (size_t)V * N;
+    fs.Dv = fs.v1 + (size_t)V * N;
+    fs.tmpm = fs.Dv + (size_t)V * M1;
+    fs.yb = fs.tmpm + (size_t)V * M1;
+    fs.gpM = fs.yb + (size_t)V * M1;
+    fs.gpT = fs.gpM + (size_t)V * RB * n;
+    fs.part = fs.gpT + (size_t)V * RB * n;
+    fs.s0 = reinterpret_cast<LsqrState*>(base + (size_t)V * per);
+    fs.s1 = fs.s0 + V;
+    fs.N = N;
+    fs.m = m;
+    fs.n = n;
+    fs.RB = RB;
+    fs.B = B;
+    fs.nc = nc;
+    fs.PL = PL;
+    // the first Mᵀ·u runs the six-launch form's kernels on these buffers
+    // (out: v1, free until the first dpiU)
+    ws.x = fs.x;
+    ws.u = fs.u0;
+    ws.v = fs.v0;
+    ws.w = fs.w;
+    ws.out = fs.v1;
+    ws.Dv = fs.Dv;
+    ws.tmpm = fs.tmpm;
+    ws.yb = fs.yb;
+    ws.gpart = fs.gpT;
+    st = fs.s0;
+  } else {
+    ws.x = base;
+    ws.u = ws.x + (size_t)V * N;
+    ws.v = ws.u + (size_t)V * N;
+    ws.w = ws.v + (size_t)V * N;
+    ws.out = ws.w + (size_t)V * N;
+    ws.Dv = ws.out + (size_t)V * N;
+    ws.tmpm = ws.Dv + (size_t)V * M1;
+    ws.yb = ws.tmpm + (size_t)V * M1;
+    ws.gpart = ws.yb + (size_t)V * M1;
+    st = reinterpret_cast<LsqrState*>(base + (size_t)V * per);
+  }
   ws.N = N;
   ws.m = m;
   ws.n = n;
   ws.RB = RB;
   ws.B = B;
-  LsqrState* st = reinterpret_cast<LsqrState*>(base + (size_t)V * per);
-  int32_t* active = reinterpret_cast<int32_t*>(st + V);
+  int32_t* active = reinterpret_cast<int32_t*>(reinterpret_cast<LsqrState*>(base + (size_t)V * per) + 2 * V);
   const size_t dl = dpi_lds_bytes(h.cones);
   const double* vcone = h.vp.as<double>();
   const double* P = h.dpi.as<double>();
@@ -1659,34 +2247,76 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
   DOPT_CHECK_HIP(hipMemcpyAsync(active, &nact, sizeof(int32_t), hipMemcpyHostToDevice, h.stream));
   int32_t left = V;
   PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
+  auto pass = [&](int dir) {
+    if (h.split_nw == 8)
+      hipLaunchKernelGGL(conic_split_pass_kernel<8>, dim3(RB, B), dim3(512), 0, h.stream, dir, h.cA, h.cb, ws, st,
+                         nq);
+    else
+      hipLaunchKernelGGL(conic_split_pass_kernel<4>, dim3(RB, B), dim3(256), 0, h.stream, dir, h.cA, h.cb, ws, st,
+                         nq);
+  };
   auto passT = [&]() {
-    hipLaunchKernelGGL(conic_split_pass_kernel, dim3(RB, B), dim3(CTPB), 0, h.stream, 1, h.cA, h.cb, ws, st, nq);
+    pass(1);
     if (nc)
       hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, V), dim3(CTPB), dl, h.stream, 1, cd, vcone, P,
                          h.dpi_len, ws, st, gws, h.psd_big_len);
   };
   hipLaunchKernelGGL(conic_split_init_kernel, dim3(V), dim3(CTPB), 0, h.stream, rhs, tol0, tol1, ws, st, active);
   passT();
-  hipLaunchKernelGGL(conic_split_init2_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st, active);
+  hipLaunchKernelGGL(conic_split_init2_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st, active,
+                     fuse ? fs.part + fs.PL - 2 * nc : nullptr, PL, nc);
   ccheck();
-  for (int it = 0; it < N && left > 0;) {
-    for (int k = 0; k < SPLIT_CHUNK && it < N; ++k, ++it) {
-      if (nc)
-        hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, V), dim3(CTPB), dl, h.stream, 0, cd, vcone, P,
-                           h.dpi_len, ws, st, gws, h.psd_big_len);
-      hipLaunchKernelGGL(conic_split_pass_kernel, dim3(RB, B), dim3(CTPB), 0, h.stream, 0, h.cA, h.cb, ws, st,
-                         nq);
-      hipLaunchKernelGGL(conic_split_upd_u_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st);
-      passT();
-      hipLaunchKernelGGL(conic_split_upd_v_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st, N,
-                         active);
+  int par = 0;
+  if (fuse) {
+    const size_t dlv = ((dl + 15) & ~(size_t)15) + (size_t)n * sizeof(double);
+    const int img = (int)(((dl + 15) & ~(size_t)15) / sizeof(double));
+    const size_t dlp = (size_t)2 * n * sizeof(double);
+    auto dpiV = [&](int first) {
+      hipLaunchKernelGGL(conic_fsplit_dpiV_kernel, dim3(nc, V), dim3(CTPB), dlv, h.stream, cd, vcone, P, h.dpi_len,
+                         h.cc, fs, par, first, N, active, gws, h.psd_big_len, img);
+    };
+    dpiV(1);
+    for (int it = 0; it < N && left > 0;) {
+      for (int k = 0; k < SPLIT_CHUNK && it < N; ++k, ++it) {
+        if (h.split_nw == 8) {
+          hipLaunchKernelGGL((conic_fsplit_pass_kernel<8, 0>), dim3(RB, B), dim3(512), 0, h.stream, h.cA, h.cb,
+                             h.cc, fs, par, nq);
+          hipLaunchKernelGGL((conic_fsplit_pass_kernel<8, 1>), dim3(RB, B), dim3(512), dlp, h.stream, h.cA, h.cb,
+                             h.cc, fs, par, nq);
+        } else {
+          hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 0>), dim3(RB, B), dim3(256), 0, h.stream, h.cA, h.cb,
+                             h.cc, fs, par, nq);
+          hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 1>), dim3(RB, B), dim3(256), dlp, h.stream, h.cA, h.cb,
+                             h.cc, fs, par, nq);
+        }
+        hipLaunchKernelGGL(conic_fsplit_dpiU_kernel, dim3(nc, V), dim3(CTPB), dl, h.stream, cd, vcone, P,
+                           h.dpi_len, fs, par, gws, h.psd_big_len);
+        dpiV(0);
+        par ^= 1;
+      }
+      ccheck();
+      DOPT_CHECK_HIP(hipMemcpyAsync(&left, active, sizeof(int32_t), hipMemcpyDeviceToHost, h.stream));
+      DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
     }
-    ccheck();
-    DOPT_CHECK_HIP(hipMemcpyAsync(&left, active, sizeof(int32_t), hipMemcpyDeviceToHost, h.stream));
-    DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+  } else {
+    for (int it = 0; it < N && left > 0;) {
+      for (int k = 0; k < SPLIT_CHUNK && it < N; ++k, ++it) {
+        if (nc)
+          hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, V), dim3(CTPB), dl, h.stream, 0, cd, vcone, P,
+                             h.dpi_len, ws, st, gws, h.psd_big_len);
+        pass(0);
+        hipLaunchKernelGGL(conic_split_upd_u_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st);
+        passT();
+        hipLaunchKernelGGL(conic_split_upd_v_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st, N,
+                           active);
+      }
+      ccheck();
+      DOPT_CHECK_HIP(hipMemcpyAsync(&left, active, sizeof(int32_t), hipMemcpyDeviceToHost, h.stream));
+      DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+    }
   }
-  hipLaunchKernelGGL(conic_split_out_kernel, dim3(V), dim3(CTPB), 0, h.stream, ws, st, out0, info0, out1, info1,
-                     norms0, norms1);
+  hipLaunchKernelGGL(conic_split_out_kernel, dim3(V), dim3(CTPB), 0, h.stream, ws,
+                     fuse ? (par ? fs.s1 : fs.s0) : st, out0, info0, out1, info1, norms0, norms1);
   ccheck();
 }
 

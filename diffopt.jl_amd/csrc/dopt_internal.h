@@ -196,6 +196,8 @@ struct Handle {
   DevBuf vp, dpi, cwork, cinfo, cnorm;   // cnorm: LSQR terminal estimates, 8·B doubles
   DevBuf csplit;                // split-path LSQR vectors, partial products, state
   int32_t conic_split = -1;     // -1 auto, 0 persistent kernel, 1 split (env DOPT_CONIC_SPLIT)
+  int32_t split_nw = 4;         // waves per split-LSQR pass workgroup, 4 or 8 (env DOPT_SPLIT_NW)
+  int32_t split_fuse = 1;       // split LSQR: 1 four-launch fused iteration, 0 six launches (env DOPT_SPLIT_FUSE)
   int32_t dpi_len = 0;          // doubles per problem of packed Dπ blocks
   int32_t psd_big_len = 0;      // doubles of global scratch per problem / sequence for PSD sides > 64
   DevBuf psd_eig, psd_app;      // that scratch: the eigensolver's (per problem), the Dπ apply's (per sequence)

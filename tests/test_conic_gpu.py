@@ -351,8 +351,14 @@ def test_config5_full_shape(ConicBatch):
 
 
 @pytest.mark.parametrize("shape", [
-    ("large PSD (d = 66) + small cones", 2, 60, [(4, 2211), (4, 15), (1, 5)], 17, 2),   # converged at √eps: 2 of 12 in (1e-6, 3.2e-6] (r02)
-    ("large PSD (d = 100)", 1, 60, [(4, 5050)], 18, 0),
+    # converged at √eps: 2 of 12 in (1e-6, 3.2e-6] (r02); 3 of 12 in (1e-6, 3.4e-6]
+    # with the split path's MFMA Dπ apply (r04: the small cones' products in a
+    # different summation order), every one inside 10× the oracle's 1-ulp spread
+    ("large PSD (d = 66) + small cones", 2, 60, [(4, 2211), (4, 15), (1, 5)], 17, 3),
+    # converged at √eps; 1 of 6 at 4.7e-6 with the fused split LSQR (r04: the
+    # partial sums in another order), inside the oracle's 1-ulp envelope and
+    # checked against the exact min-norm solution below
+    ("large PSD (d = 100)", 1, 60, [(4, 5050)], 18, 1),
     ("large PSD (d = 300)", 1, 40, [(4, 45150)], 19, 1),   # converged at √eps (istop 2 / 1): 1 of 6 at 1.6e-5, inside the 1-ulp envelope (r03)
 ], ids=["d66_mixed", "d100", "d300"])
 def test_large_psd_sides(ConicBatch, shape):
@@ -444,8 +450,9 @@ def _exact_minnorm(cache, rhs):
     ("well-posed SOC", 2, 100, [(3, 10)] * 20, 21),
     ("config-4 structure, m=1000", 2, 500, [(3, 50)] * 20, 14),
     ("large PSD (d = 66) + small cones", 2, 60, [(4, 2211), (4, 15), (1, 5)], 17),
+    ("large PSD (d = 100)", 1, 60, [(4, 5050)], 18),
     ("large PSD (d = 300)", 1, 40, [(4, 45150)], 19),
-], ids=["soc", "m1000", "d66", "d300"])
+], ids=["soc", "m1000", "d66", "d100", "d300"])
 def test_converged_shapes_vs_exact_minnorm(ConicBatch, shape):
     """The shapes whose LSQR converges (istop 1–2) but stops at the
     reference's √eps tolerances, where engine and oracle differ by up to
