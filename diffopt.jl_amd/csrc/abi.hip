@@ -127,8 +127,11 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
     if (const char* e = getenv("DOPT_LSLICE")) h->lslices = atoi(e);
     if (const char* e = getenv("DOPT_LPERSIST")) h->lpersist = atoi(e) != 0;
     if (const char* e = getenv("DOPT_LCOL_PF")) h->lcol_pf = atoi(e) != 0;
+    if (const char* e = getenv("DOPT_SYM_TPB")) h->sym_tpb = atoi(e);
     if (const char* e = getenv("DOPT_SPLIT_NW")) h->split_nw = atoi(e) == 8 ? 8 : 4;
     if (const char* e = getenv("DOPT_SPLIT_FUSE")) h->split_fuse = atoi(e) != 0;
+    if (const char* e = getenv("DOPT_SPLIT_NC")) h->split_nc = atoi(e) == 4 ? 4 : 2;
+    if (const char* e = getenv("DOPT_PSD_MFMA")) h->psd_mfma = atoi(e) != 0;
     if (kind == DOPT_KIND_QP) {
       // largest supported system: the generic solve stages an nmax vector in
       // LDS (64 KB); the blocked route takes reduced systems up to BLOCKED_MAX

@@ -352,35 +352,65 @@ __device__ __forceinline__ d4c cmfma(double a, double b, d4c c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+// slot s of wave wv holds tile idx = wv + 4s of the nT × nT grid (row-major;
+// `upper`: of its upper triangle); false past the end.  Closed form, no loop
+// over the grid: the slots' loads can be issued together.
+__device__ __forceinline__ bool psd_tile(int idx, int nT, bool upper, int& r, int& c) {
+  if (!upper) {
+    r = idx / nT;
+    c = idx - r * nT;
+    return idx < nT * nT;
+  }
+  r = c = 0;
+  int k = idx;
+  bool found = false;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int len = nT - rr;
+    if (!found && len > 0) {
+      if (k < len) {
+        r = rr;
+        c = rr + k;
+        found = true;
+      } else {
+        k -= len;
+      }
+    }
+  }
+  return found;
+}
+
 template <class FA, class FB, class FS>
 __device__ __forceinline__ void psd_mfma(int d, bool upper, FA a, FB b, FS st) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, l16 = lane & 15, g = lane >> 4;
   const int nT = (d + 15) >> 4;
   int ti[4], tj[4];
   bool on[4];
-  {
-    int idx = 0;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) on[s] = false;
-    for (int r = 0; r < nT; ++r)
-      for (int c = upper ? r : 0; c < nT; ++c, ++idx)
-        if ((idx & 3) == wv) {
-          const int s = idx >> 2;
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (k == s) { ti[k] = r; tj[k] = c; on[k] = true; }
-        }
-  }
+  for (int s = 0; s < 4; ++s) on[s] = psd_tile(wv + 4 * s, nT, upper, ti[s], tj[s]);
   if (!on[0]) return;   // wave-uniform; no barrier inside
   d4c acc[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) acc[s] = (d4c){0.0, 0.0, 0.0, 0.0};
   const int dp = (d + 3) & ~3;
-  for (int q0 = 0; q0 < dp; q0 += 4) {
-    const int q = q0 + g;
+  // two k-steps per trip, every operand of the trip read before its MFMAs (a
+  // step past dp reads zeros: a(…) / b(…) give 0 outside [0, d))
+  for (int q0 = 0; q0 < dp; q0 += 8) {
+    double av[2][4], bv[2][4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
-      if (on[s]) acc[s] = cmfma(a(16 * ti[s] + l16, q), b(q, 16 * tj[s] + l16), acc[s]);
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        if (on[s]) {
+          const int q = q0 + 4 * h + g;
+          av[h][s] = a(16 * ti[s] + l16, q);
+          bv[h][s] = b(q, 16 * tj[s] + l16);
+        }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        if (on[s]) acc[s] = cmfma(av[h][s], bv[h][s], acc[s]);
   }
 #pragma unroll
   for (int s = 0; s < 4; ++s)
@@ -422,32 +452,23 @@ __device__ __forceinline__ void psd_apply_cone_lds(const ConeDesc cd, const doub
     }
     return;
   }
-  // this lane's entries of B at the middle product's output positions: the
-  // upper tiles of psd_mfma's enumeration for this wave (mirrored below)
+  // this lane's entries of B at the middle product's output positions (the
+  // upper tiles of psd_mfma's enumeration for this wave, mirrored below):
+  // loaded from clamped addresses, masked only where used
   const int lane = t & 63, wv = t >> 6, l16 = lane & 15, g = lane >> 4;
   const int nT = (d + 15) >> 4;
   double br[4][4];
-  {
-    int idx = 0;
+  bool bk[4][4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+  for (int s = 0; s < 4; ++s) {
+    int r, c;
+    const bool on = psd_tile(wv + 4 * s, nT, true, r, c);
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) br[s][rr] = 0.0;
-    for (int r = 0; r < nT; ++r)
-      for (int c = r; c < nT; ++c, ++idx)
-        if ((idx & 3) == wv) {
-          const int s = idx >> 2;
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (k == s)
-#pragma unroll
-              for (int rr = 0; rr < 4; ++rr) {
-                const int i = 16 * r + g + 4 * rr, j = 16 * c + l16;
-                const bool ok = i < d && j < d;
-                const double bv = Bm[ok ? i * d + j : 0];
-                br[k][rr] = ok ? bv : 0.0;
-              }
-        }
+    for (int rr = 0; rr < 4; ++rr) {
+      const int i = 16 * r + g + 4 * rr, j = 16 * c + l16;
+      bk[s][rr] = on && i < d && j < d;
+      br[s][rr] = Bm[bk[s][rr] ? i * d + j : 0];
+    }
   }
 #pragma unroll
   for (int k = 0; k < UR; ++k) {
@@ -482,7 +503,7 @@ __device__ __forceinline__ void psd_apply_cone_lds(const ConeDesc cd, const doub
   psd_mfma(d, true, [&](int i, int q) { return rd(Ys, i, q); }, [&](int q, int j) { return rd(Us, q, j); },
            [&](int i, int j, double v, int s, int rr) {
              if (i < d && j < d) {
-               const double x = v * br[s][rr];
+               const double x = v * (bk[s][rr] ? br[s][rr] : 0.0);
                Xs[i * ld + j] = x;
                Xs[j * ld + i] = x;
              }
@@ -500,7 +521,7 @@ __device__ __forceinline__ void psd_apply_cone_lds(const ConeDesc cd, const doub
   __syncthreads();
 }
 
-template <bool BIG = false>
+template <bool BIG = false, bool MF = false>
 __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, const double* __restrict__ v,
                           const double* __restrict__ P, const double* in, double* out,
                           int trans, double* lds, double* red, double* gws) {
@@ -558,10 +579,10 @@ __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, con
       psd_apply_cone(cd, P, in, out, trans, g, g + img, g + 2 * img);
     } else {
       const size_t img = (size_t)((d + 3) & ~3) * (((d + 3) & ~3) + 1);   // this cone's image: dp × (dp+1)
-      // the MFMA form in the split path's Dπ kernel; the persistent LSQR
-      // kernels keep the register-tile form (the MFMA form's prefetched
-      // operands push conic_lsqr2_kernel from 42 to 141 VGPR spills)
-      if (BIG) psd_apply_cone_lds(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
+      // the register-tile form (the MFMA form, psd_apply_cone_lds, measured
+      // slower in the split Dπ kernel: 47.9 vs 38.1 µs per launch at config 5,
+      // and it pushes conic_lsqr2_kernel from 42 to 141 VGPR spills)
+      if (MF) psd_apply_cone_lds(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
       else psd_apply_cone(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
     }
   }
@@ -1398,6 +1419,8 @@ __global__ __launch_bounds__(64 * NW) void conic_split_pass_kernel(
 }
 
 // Dπ (dir 0: Dv = Dπ v_m) or Dπᵀ (dir 1: out_m = Dπᵀ tmpm), one cone per WG
+// (MF: the PSD cones' products on MFMA, env DOPT_PSD_MFMA=1)
+template <bool MF>
 __global__ __launch_bounds__(CTPB) void conic_split_dpi_kernel(
     int dir, const ConeDesc* __restrict__ cones_g, const double* __restrict__ vcone,
     const double* __restrict__ P, int plen, SplitWS ws, const LsqrState* __restrict__ stv,
@@ -1412,9 +1435,9 @@ __global__ __launch_bounds__(CTPB) void conic_split_dpi_kernel(
   const double* pp = P + (size_t)ws.phys(b) * plen;
   double* g = gws + (size_t)b * wlen;
   if (dir == 0)
-    dpi_apply<true>(&cd, 1, pv, pp, ws.vec(ws.v, b) + ws.n, ws.mvec(ws.Dv, b), 0, lds, red, g);
+    dpi_apply<true, MF>(&cd, 1, pv, pp, ws.vec(ws.v, b) + ws.n, ws.mvec(ws.Dv, b), 0, lds, red, g);
   else
-    dpi_apply<true>(&cd, 1, pv, pp, ws.mvec(ws.tmpm, b), ws.vec(ws.out, b) + ws.n, 1, lds, red, g);
+    dpi_apply<true, MF>(&cd, 1, pv, pp, ws.mvec(ws.tmpm, b), ws.vec(ws.out, b) + ws.n, 1, lds, red, g);
 }
 
 // The per-problem vector kernels below run 1024-thread workgroups and issue
@@ -1826,7 +1849,7 @@ __device__ __forceinline__ double gsum8(const double* __restrict__ gp, int RB, i
 
 // DIR 0: passM, DIR 1: passT (see above).  Dynamic LDS (passT): u_n of the
 // (up to two) live sequences, 2·n doubles.
-template <int NW, int DIR>
+template <int NW, int DIR, int NC2 = 2>
 __global__ __launch_bounds__(64 * NW) void conic_fsplit_pass_kernel(
     const double* __restrict__ A, const double* __restrict__ bvec, const double* __restrict__ cvec, FSplit fs,
     int par, int nq) {
@@ -1923,8 +1946,11 @@ __global__ __launch_bounds__(64 * NW) void conic_fsplit_pass_kernel(
     __syncthreads();   // u_n in LDS and this block's rows of u (global) before the sweep
   }
   if (nl == 0) return;
-  if (nl == 2) gemv_multi<2, SPLIT_K, 2, NW>(Ab, m, rows, n, xs, wv, yv, gv, ys);
-  else gemv_multi<1, SPLIT_K, PAIR_NC, NW>(Ab, m, rows, n, xs, wv, yv, gv, ys);
+  // NC2 columns in flight per wave for two sequences (NC2 + 2 for one): the
+  // grid holds ≤ 2 workgroups per CU, so registers are not what limits the
+  // loads in flight
+  if (nl == 2) gemv_multi<2, SPLIT_K, NC2, NW>(Ab, m, rows, n, xs, wv, yv, gv, ys);
+  else gemv_multi<1, SPLIT_K, (NC2 == 2 ? PAIR_NC : NC2 + 2), NW>(Ab, m, rows, n, xs, wv, yv, gv, ys);
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   for (int c = 0; c < nl; ++c) {
     const int bv = live[c];
@@ -1968,6 +1994,7 @@ __global__ __launch_bounds__(64 * NW) void conic_fsplit_pass_kernel(
 }
 
 // dpiU: one cone per workgroup; v' = Dπᵀ(tmpm) + u_m − βv on the cone's rows
+template <bool MF>
 __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiU_kernel(
     const ConeDesc* __restrict__ cones_g, const double* __restrict__ vcone, const double* __restrict__ P,
     int plen, FSplit fs, int par, double* __restrict__ gws, int wlen) {
@@ -1981,7 +2008,7 @@ __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiU_kernel(
   const double* pv = vcone + (size_t)fs.phys(bv) * m;
   const double* pp = P + (size_t)fs.phys(bv) * plen;
   double* vn = fs.V(par ^ 1, bv);
-  dpi_apply<true>(&cd, 1, pv, pp, fs.tmpm + (size_t)bv * m, vn + n, 1, lds, red, gws + (size_t)bv * wlen);
+  dpi_apply<true, MF>(&cd, 1, pv, pp, fs.tmpm + (size_t)bv * m, vn + n, 1, lds, red, gws + (size_t)bv * wlen);
   const double beta = st.beta;
   const double* vo = fs.V(par, bv);
   const double* un = fs.U(par ^ 1, bv);
@@ -1998,6 +2025,7 @@ __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiU_kernel(
 
 // dpiV: finish the iteration (first = 0), then Dv = Dπ v_m on the cone.
 // Dynamic LDS: the Dπ images (img doubles), then v'_n (n doubles).
+template <bool MF>
 __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiV_kernel(
     const ConeDesc* __restrict__ cones_g, const double* __restrict__ vcone, const double* __restrict__ P,
     int plen, const double* __restrict__ cvec, FSplit fs, int par, int first, int maxiter,
@@ -2085,7 +2113,7 @@ __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiV_kernel(
   } else if (fs.S(par)[bv].done) {
     return;
   }
-  dpi_apply<true>(&cd, 1, vcone + (size_t)fs.phys(bv) * m, P + (size_t)fs.phys(bv) * plen,
+  dpi_apply<true, MF>(&cd, 1, vcone + (size_t)fs.phys(bv) * m, P + (size_t)fs.phys(bv) * plen,
                   fs.V(vp, bv) + n, fs.Dv + (size_t)bv * m, 0, lds, red, gws + (size_t)bv * wlen);
 }
 
@@ -2258,8 +2286,8 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
   auto passT = [&]() {
     pass(1);
     if (nc)
-      hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, V), dim3(CTPB), dl, h.stream, 1, cd, vcone, P,
-                         h.dpi_len, ws, st, gws, h.psd_big_len);
+      hipLaunchKernelGGL(h.psd_mfma ? conic_split_dpi_kernel<true> : conic_split_dpi_kernel<false>, dim3(nc, V),
+                         dim3(CTPB), dl, h.stream, 1, cd, vcone, P, h.dpi_len, ws, st, gws, h.psd_big_len);
   };
   hipLaunchKernelGGL(conic_split_init_kernel, dim3(V), dim3(CTPB), 0, h.stream, rhs, tol0, tol1, ws, st, active);
   passT();
@@ -2272,16 +2300,17 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
     const int img = (int)(((dl + 15) & ~(size_t)15) / sizeof(double));
     const size_t dlp = (size_t)2 * n * sizeof(double);
     auto dpiV = [&](int first) {
-      hipLaunchKernelGGL(conic_fsplit_dpiV_kernel, dim3(nc, V), dim3(CTPB), dlv, h.stream, cd, vcone, P, h.dpi_len,
-                         h.cc, fs, par, first, N, active, gws, h.psd_big_len, img);
+      hipLaunchKernelGGL(h.psd_mfma ? conic_fsplit_dpiV_kernel<true> : conic_fsplit_dpiV_kernel<false>, dim3(nc, V),
+                         dim3(CTPB), dlv, h.stream, cd, vcone, P, h.dpi_len, h.cc, fs, par, first, N, active, gws,
+                         h.psd_big_len, img);
     };
     dpiV(1);
     for (int it = 0; it < N && left > 0;) {
       for (int k = 0; k < SPLIT_CHUNK && it < N; ++k, ++it) {
-        if (h.split_nw == 8) {
-          hipLaunchKernelGGL((conic_fsplit_pass_kernel<8, 0>), dim3(RB, B), dim3(512), 0, h.stream, h.cA, h.cb,
+        if (h.split_nc == 4) {
+          hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 0, 4>), dim3(RB, B), dim3(256), 0, h.stream, h.cA, h.cb,
                              h.cc, fs, par, nq);
-          hipLaunchKernelGGL((conic_fsplit_pass_kernel<8, 1>), dim3(RB, B), dim3(512), dlp, h.stream, h.cA, h.cb,
+          hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 1, 4>), dim3(RB, B), dim3(256), dlp, h.stream, h.cA, h.cb,
                              h.cc, fs, par, nq);
         } else {
           hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 0>), dim3(RB, B), dim3(256), 0, h.stream, h.cA, h.cb,
@@ -2289,8 +2318,9 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
           hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 1>), dim3(RB, B), dim3(256), dlp, h.stream, h.cA, h.cb,
                              h.cc, fs, par, nq);
         }
-        hipLaunchKernelGGL(conic_fsplit_dpiU_kernel, dim3(nc, V), dim3(CTPB), dl, h.stream, cd, vcone, P,
-                           h.dpi_len, fs, par, gws, h.psd_big_len);
+        hipLaunchKernelGGL(h.psd_mfma ? conic_fsplit_dpiU_kernel<true> : conic_fsplit_dpiU_kernel<false>,
+                           dim3(nc, V), dim3(CTPB), dl, h.stream, cd, vcone, P, h.dpi_len, fs, par, gws,
+                           h.psd_big_len);
         dpiV(0);
         par ^= 1;
       }
@@ -2302,8 +2332,9 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
     for (int it = 0; it < N && left > 0;) {
       for (int k = 0; k < SPLIT_CHUNK && it < N; ++k, ++it) {
         if (nc)
-          hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, V), dim3(CTPB), dl, h.stream, 0, cd, vcone, P,
-                             h.dpi_len, ws, st, gws, h.psd_big_len);
+          hipLaunchKernelGGL(h.psd_mfma ? conic_split_dpi_kernel<true> : conic_split_dpi_kernel<false>,
+                             dim3(nc, V), dim3(CTPB), dl, h.stream, 0, cd, vcone, P, h.dpi_len, ws, st, gws,
+                             h.psd_big_len);
         pass(0);
         hipLaunchKernelGGL(conic_split_upd_u_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st);
         passT();

@@ -196,7 +196,10 @@ struct Handle {
   DevBuf vp, dpi, cwork, cinfo, cnorm;   // cnorm: LSQR terminal estimates, 8·B doubles
   DevBuf csplit;                // split-path LSQR vectors, partial products, state
   int32_t conic_split = -1;     // -1 auto, 0 persistent kernel, 1 split (env DOPT_CONIC_SPLIT)
+  int32_t sym_tpb = 256;        // P-symmetric sweep kernel's workgroup size, 256 or 512 (env DOPT_SYM_TPB)
   int32_t split_nw = 4;         // waves per split-LSQR pass workgroup, 4 or 8 (env DOPT_SPLIT_NW)
+  int32_t split_nc = 2;         // fused split pass: columns in flight per wave for two sequences, 2 or 4 (env DOPT_SPLIT_NC)
+  int32_t psd_mfma = 0;         // split LSQR: PSD Dπ products on MFMA (env DOPT_PSD_MFMA=1)
   int32_t split_fuse = 1;       // split LSQR: 1 four-launch fused iteration, 0 six launches (env DOPT_SPLIT_FUSE)
   int32_t dpi_len = 0;          // doubles per problem of packed Dπ blocks
   int32_t psd_big_len = 0;      // doubles of global scratch per problem / sequence for PSD sides > 64

@@ -870,8 +870,8 @@ __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict
 // (5 waves per SIMD) config 2's sweep takes 0.16 ms against 0.21 ms inside
 // blu_solve2_kernel (124 VGPRs, whose other paths set the count); forcing 8
 // waves per SIMD (64 VGPRs, 22 spilled) measured 0.32 ms (DOPT_SYM_LEAN=2).
-template <int ENT, int WPE>
-__global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(WPE))) void blu_sym2_kernel(const double* __restrict__ K, int ld, int nmax,
+template <int ENT, int WPE, int TPB = PT, int RH = 16>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void blu_sym2_kernel(const double* __restrict__ K, int ld, int nmax,
                                                       const double* __restrict__ dinv, size_t dstride,
                                                       const QPMeta* __restrict__ meta,
                                                       const double* __restrict__ w_rev,
@@ -890,7 +890,7 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   const PScale psc{sym.kls + (size_t)b * sym.m, sym.n, mm.nk};
   const double* rb = w_rev + (size_t)b * nmax;
   const double* fb = w_fwd + (size_t)b * nmax;
-  for (int i = t; i < Np; i += PT) {
+  for (int i = t; i < Np; i += TPB) {
     v[i] = i < N ? rb[i] / udb[i] : 0.0;
     y[i] = i < N ? fb[i] : 0.0;
   }
@@ -899,14 +899,14 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   for (int s = 0; s < nblk; ++s) {
     const int bk = nblk - 1 - s;
     const int i0 = bk * BNB;
-    double f[ENT][16];
+    double f[ENT][RH];
 #pragma unroll
-    for (int q = 0; q < ENT; ++q) {   // rows i0 .. i0+15 of column e < i0
-      const int e = t + PT * q;
+    for (int q = 0; q < ENT; ++q) {   // rows i0 .. i0+RH−1 of column e < i0
+      const int e = t + TPB * q;
       const int ec = e < i0 ? e : 0;
-      if (q * PT >= i0) continue;   // workgroup-uniform: no entries left
+      if (q * TPB >= i0) continue;   // workgroup-uniform: no entries left
 #pragma unroll
-      for (int j = 0; j < 16; ++j) f[q][j] = Kb[(size_t)(i0 + j) * ld + ec];
+      for (int j = 0; j < RH; ++j) f[q][j] = Kb[(size_t)(i0 + j) * ld + ec];
     }
     if (wv < 2 && lane < BNB) {   // wave 0: L_kk⁻ᵀ v_k, wave 1: L_kk⁻ᵀ y_k
       const double* Dk = Dbase + (size_t)bk * BDINV;
@@ -919,35 +919,47 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     __syncthreads();
     if (wv == 0 && lane < BNB) v[i0 + lane] = part[lane];
     if (wv == 1 && lane < BNB) y[i0 + lane] = part2[lane];
+    double a1[ENT], a2[ENT];
+    int ec[ENT];
 #pragma unroll
     for (int q = 0; q < ENT; ++q) {
-      const int e = t + PT * q;
-      if (q * PT >= i0) continue;
+      const int e = t + TPB * q;
       const bool has = e < i0;
-      const int ec = has ? e : 0;
-      double a1 = has ? v[e] : 0.0, a2 = has ? y[e] : 0.0;
+      ec[q] = has ? e : 0;
+      a1[q] = has ? v[e] : 0.0;
+      a2[q] = has ? y[e] : 0.0;
+    }
+    // the rows in groups of RH, every entry's group together (group h+1's
+    // loads after group h's FMAs in source order)
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        a1 = fma(-f[q][j], part[j], a1);
-        a2 = fma(-f[q][j], part2[j], a2);
+    for (int h = 0; h < BNB / RH; ++h) {
+#pragma unroll
+      for (int q = 0; q < ENT; ++q) {
+        if (q * TPB >= i0) continue;   // workgroup-uniform
+        if (h) {
+#pragma unroll
+          for (int j = 0; j < RH; ++j) f[q][j] = Kb[(size_t)(i0 + RH * h + j) * ld + ec[q]];
+        }
+#pragma unroll
+        for (int j = 0; j < RH; ++j) {
+          a1[q] = fma(-f[q][j], part[RH * h + j], a1[q]);
+          a2[q] = fma(-f[q][j], part2[RH * h + j], a2[q]);
+        }
       }
+    }
 #pragma unroll
-      for (int j = 0; j < 16; ++j) f[q][j] = Kb[(size_t)(i0 + 16 + j) * ld + ec];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        a1 = fma(-f[q][j], part[16 + j], a1);
-        a2 = fma(-f[q][j], part2[16 + j], a2);
-      }
-      if (has) {
-        v[e] = a1;
-        y[e] = a2;
+    for (int q = 0; q < ENT; ++q) {
+      const int e = t + TPB * q;
+      if (q * TPB < i0 && e < i0) {
+        v[e] = a1[q];
+        y[e] = a2[q];
       }
     }
     __syncthreads();
   }
   double* xr = x_rev + (size_t)b * nmax;
   double* xf = x_fwd + (size_t)b * nmax;
-  for (int i = t; i < N; i += PT) {
+  for (int i = t; i < N; i += TPB) {
     xr[i] = v[i] / psc(i);
     xf[i] = y[i];
   }
@@ -1207,7 +1219,10 @@ void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, con
   SymSweep sym{h.ukp_valid ? h.ukp.as<double>() : nullptr, h.kls.as<double>(), h.n, h.m};
   if (sym.ukp && w_rev && (sel & LU_SEL_NOPIV) && npmax <= SOLVE_STATIC && h.sym_lean) {
     // the left-looking route's factors (every blocked problem P-symmetric): the lean sweep kernel
-    if (ent <= 1 && h.sym_lean == 2)   // every workgroup of a 1024-problem batch resident (spills 22 VGPRs)
+    if (ent <= 1 && h.sym_tpb == 256)   // 256 threads, two entries each: four workgroups per CU (env DOPT_SYM_TPB=256)
+      hipLaunchKernelGGL((blu_sym2_kernel<2, 4, 256, 8>), dim3(B), dim3(256), 0, h.stream, K, h.ld, h.nmax, dinv,
+                         dstride, meta, w_rev, w_fwd, x_rev, x_fwd, sym);
+    else if (ent <= 1 && h.sym_lean == 2)   // every workgroup of a 1024-problem batch resident (spills 22 VGPRs)
       hipLaunchKernelGGL((blu_sym2_kernel<1, 8>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, meta,
                          w_rev, w_fwd, x_rev, x_fwd, sym);
     else if (ent <= 1)

@@ -1791,7 +1791,9 @@ __device__ __forceinline__ void ldiag_body(
   double* ud = ukp + (size_t)b * nmax;
   double* w0b = w0 ? w0 + (size_t)b * nmax : nullptr;
   double* w1b = w0 ? w1 + (size_t)b * nmax : nullptr;
-  double amax = kamax[b];
+  // a vector (agent-scope) load, never the scalar cache: written by this
+  // problem's step 0 (and by the prepare kernel)
+  double amax = __hip_atomic_load(kamax + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (c0 == 0) {
     // the Q symmetry check's verdict (partial pivoting for an asymmetric Q),
     // max |Q|, |A| into the growth bound
@@ -1982,7 +1984,7 @@ __device__ __forceinline__ void lcol_body(
   const double* Bg = binv + (size_t)b * BSTR;
   const auto sv = src_bind(src, b, mm);
   const PScale ps = pscale(kls, b, n, m, mm);
-  const double bound = growth_bound(kamax[b]);
+  const double bound = growth_bound(__hip_atomic_load(kamax + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   d4n acc[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = (d4n){0, 0, 0, 0};

@@ -53,7 +53,7 @@ NLP_STEP = "nlp_assemble_kernel"
 # split-path LSQR: every conic_split_* dispatch belongs to the LSQR call opened
 # by the preceding conic_split_init_kernel; reported per LSQR call under the
 # bench's phase name "conic_lsqr" (key "conic_lsqr_split")
-SPLIT_FRAG, SPLIT_OPEN = "conic_split_", "conic_split_init_kernel"
+SPLIT_FRAGS, SPLIT_OPEN = ("conic_split_", "conic_fsplit_"), "conic_split_init_kernel"
 
 
 def per_launch(d, counter):
@@ -78,7 +78,7 @@ def per_launch(d, counter):
                 if row.get("Counter_Name") != counter:
                     continue
                 kn = row.get("Kernel_Name", "")
-                if SPLIT_FRAG in kn:
+                if any(fr in kn for fr in SPLIT_FRAGS):
                     tot += float(row["Counter_Value"])
                     if SPLIT_OPEN in kn:
                         calls.add(row.get("Dispatch_Id"))
