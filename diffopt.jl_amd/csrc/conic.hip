@@ -35,6 +35,26 @@ __device__ __forceinline__ double cwave_sum(double v) {
   return v;
 }
 
+// wave sum by DPP (VALU lane moves, no LDS crossbar): quad xor 1 / 2, the
+// half-row and row mirrors, then row_bcast:15 / 31 carry the rows' totals up;
+// the full sum lands in lane 63 (the other lanes hold partial sums)
+template <int CTRL, int ROWMASK, bool ZERO>
+__device__ __forceinline__ double cdpp(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(ZERO ? 0 : (int)b, (int)b, CTRL, ROWMASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(ZERO ? 0 : (int)(b >> 32), (int)(b >> 32), CTRL, ROWMASK, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double wave_sum63(double v) {
+  v += cdpp<0xB1, 0xF, false>(v);    // quad_perm [1,0,3,2]
+  v += cdpp<0x4E, 0xF, false>(v);    // quad_perm [2,3,0,1]
+  v += cdpp<0x141, 0xF, false>(v);   // row_half_mirror
+  v += cdpp<0x140, 0xF, false>(v);   // row_mirror
+  v += cdpp<0x142, 0xA, true>(v);    // row_bcast:15 → rows 1, 3
+  v += cdpp<0x143, 0xC, true>(v);    // row_bcast:31 → rows 2, 3
+  return v;
+}
+
 __device__ __forceinline__ double cblock_sum(double v, double* red) {
   v = cwave_sum(v);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -394,23 +414,23 @@ __device__ __forceinline__ void psd_mfma(int d, bool upper, FA a, FB b, FS st) {
   for (int s = 0; s < 4; ++s) acc[s] = (d4c){0.0, 0.0, 0.0, 0.0};
   const int dp = (d + 3) & ~3;
   // two k-steps per trip, every operand of the trip read before its MFMAs (a
-  // step past dp reads zeros: a(…) / b(…) give 0 outside [0, d))
+  // step past dp reads zeros: a(…) / b(…) give 0 outside [0, d)).  No branch
+  // per slot: an empty slot (r = c = 0) repeats tile (0, 0) and is not stored
+  // — per-slot branches put an LDS wait in front of every MFMA
   for (int q0 = 0; q0 < dp; q0 += 8) {
     double av[2][4], bv[2][4];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        if (on[s]) {
-          const int q = q0 + 4 * h + g;
-          av[h][s] = a(16 * ti[s] + l16, q);
-          bv[h][s] = b(q, 16 * tj[s] + l16);
-        }
+      for (int s = 0; s < 4; ++s) {
+        const int q = q0 + 4 * h + g;
+        av[h][s] = a(16 * ti[s] + l16, q);
+        bv[h][s] = b(q, 16 * tj[s] + l16);
+      }
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        if (on[s]) acc[s] = cmfma(av[h][s], bv[h][s], acc[s]);
+      for (int s = 0; s < 4; ++s) acc[s] = cmfma(av[h][s], bv[h][s], acc[s]);
   }
 #pragma unroll
   for (int s = 0; s < 4; ++s)
@@ -419,6 +439,7 @@ __device__ __forceinline__ void psd_mfma(int d, bool upper, FA a, FB b, FS st) {
       for (int rr = 0; rr < 4; ++rr) st(16 * ti[s] + g + 4 * rr, 16 * tj[s] + l16, acc[s][rr], s, rr);
 }
 
+template <bool MFMA>
 __device__ __forceinline__ void psd_apply_cone_lds(const ConeDesc cd, const double* __restrict__ P,
                                                    const double* in, double* out, int trans, double* Xs,
                                                    double* Ys, double* Us) {
@@ -490,6 +511,36 @@ __device__ __forceinline__ void psd_apply_cone_lds(const ConeDesc cd, const doub
     }
   }
   __syncthreads();
+  if constexpr (!MFMA) {
+    // the products on 4×4 register tiles (psd_gemm4) over images padded to
+    // dp: zero the padding (rows / columns d..dp−1) first
+    const int dp = (d + 3) & ~3;
+    if (dp != d) {
+      for (int e = t; e < dp * dp; e += CTPB) {
+        const int i = e / dp, j = e - (e / dp) * dp;
+        if (i >= d || j >= d) {
+          Xs[i * ld + j] = 0.0;
+          Us[i * ld + j] = 0.0;
+        }
+      }
+    }
+    __syncthreads();
+    psd_gemm4(d, dp, false, [&](int i, int q) { return Us[q * ld + i]; }, [&](int q, int j) { return Xs[q * ld + j]; },
+              [&](int i, int j, double v) { Ys[i * ld + j] = v; });
+    __syncthreads();
+    psd_gemm4(d, dp, false, [&](int i, int q) { return Ys[i * ld + q]; }, [&](int q, int j) { return Us[q * ld + j]; },
+              [&](int i, int j, double v) { Xs[i * ld + j] = (i < d && j < d) ? v * Bm[i * d + j] : 0.0; });
+    __syncthreads();
+    psd_gemm4(d, dp, false, [&](int i, int q) { return Us[i * ld + q]; }, [&](int q, int j) { return Xs[q * ld + j]; },
+              [&](int i, int j, double v) { Ys[i * ld + j] = v; });
+    __syncthreads();
+    psd_gemm4(d, dp, true, [&](int i, int q) { return Ys[i * ld + q]; }, [&](int q, int j) { return Us[j * ld + q]; },
+              [&](int i, int j, double v) {
+                if (i <= j && j < d) o[tri_idx(i, j)] = (!trans && i != j) ? 2.0 * v : v;
+              });
+    __syncthreads();
+    return;
+  }
   auto rd = [&](const double* img, int i, int j) {
     const bool ok = i < d && j < d;
     const double v = img[ok ? i * ld + j : 0];
@@ -579,10 +630,13 @@ __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, con
       psd_apply_cone(cd, P, in, out, trans, g, g + img, g + 2 * img);
     } else {
       const size_t img = (size_t)((d + 3) & ~3) * (((d + 3) & ~3) + 1);   // this cone's image: dp × (dp+1)
-      // the register-tile form (the MFMA form, psd_apply_cone_lds, measured
-      // slower in the split Dπ kernel: 47.9 vs 38.1 µs per launch at config 5,
-      // and it pushes conic_lsqr2_kernel from 42 to 141 VGPR spills)
-      if (MF) psd_apply_cone_lds(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
+      // split path: every load of the cone issued up front, the products on
+      // 4×4 register tiles (MF: on MFMA, env DOPT_PSD_MFMA=1 — measured no
+      // faster, 42 vs 43 µs per dpiU launch at config 5); the persistent LSQR
+      // kernels keep psd_apply_cone (the up-front operands would push
+      // conic_lsqr2_kernel from 42 to 141 VGPR spills)
+      if (MF) psd_apply_cone_lds<true>(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
+      else if (BIG) psd_apply_cone_lds<false>(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
       else psd_apply_cone(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
     }
   }
@@ -660,14 +714,12 @@ __device__ __forceinline__ void gemv_multi(const double* __restrict__ A, int ld,
           sc[q][c] = acc;
         }
       }
+      // the rows' sum by DPP into lane 63 (no LDS round trips)
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
+      for (int q = 0; q < NV; ++q)
 #pragma unroll
-        for (int q = 0; q < NV; ++q)
-#pragma unroll
-          for (int c = 0; c < NC; ++c) sc[q][c] += __shfl_xor(sc[q][c], o);
-      }
-      if (lane == 0) {
+        for (int c = 0; c < NC; ++c) sc[q][c] = wave_sum63(sc[q][c]);
+      if (lane == 63) {
 #pragma unroll
         for (int q = 0; q < NV; ++q)
 #pragma unroll
@@ -688,8 +740,8 @@ __device__ __forceinline__ void gemv_multi(const double* __restrict__ A, int ld,
           s0 = fma(a0[k], wr[q][k], s0);
           ya[q][k] = fma(a0[k], x0, ya[q][k]);
         }
-        s0 = cwave_sum(s0);
-        if (lane == 0) g[q][j] = r0 ? g[q][j] + s0 : s0;
+        s0 = wave_sum63(s0);
+        if (lane == 63) g[q][j] = r0 ? g[q][j] + s0 : s0;
       }
     }
 #pragma unroll
@@ -1834,6 +1886,26 @@ __device__ __forceinline__ void bsumk(double (&v)[K], double* red) {
   }
 }
 
+// Σ_rb gp[rb·n + j], the row blocks in chunks of 32 with every load of a chunk
+// issued before the first add (clamped addresses, masked after the load): one
+// round trip per chunk instead of one per 8 loads plus a serial remainder
+__device__ __forceinline__ double gsum32(const double* __restrict__ gp, int RB, int n, int j) {
+  double tot = 0.0;
+  for (int r0 = 0; r0 < RB; r0 += 32) {
+    double v[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) v[k] = gp[(size_t)(r0 + k < RB ? r0 + k : r0) * n + j];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) v[k] = r0 + k < RB ? v[k] : 0.0;
+#pragma unroll
+    for (int w = 16; w > 0; w >>= 1)
+#pragma unroll
+      for (int k = 0; k < w; ++k) v[k] += v[k + w];
+    tot += v[0];
+  }
+  return tot;
+}
+
 // Σ_rb gp[rb·n + j], eight loads in flight
 __device__ __forceinline__ double gsum8(const double* __restrict__ gp, int RB, int n, int j) {
   double s[8];
@@ -1898,7 +1970,7 @@ __global__ __launch_bounds__(64 * NW) void conic_fsplit_pass_kernel(
       for (int ci = 0; ci < 2; ++ci)
         if (ci < cnt) {
           const int bv = sq[ci];
-          const double g = gsum8(fs.gpM + (size_t)bv * RB * n, RB, n, j);
+          const double g = gsum32(fs.gpM + (size_t)bv * RB * n, RB, n, j);
           const double val = (-g + cj * ve[ci]) - al[ci] * fs.U(par, bv)[j];
           ul[ci * n + j] = val;
           acc[2 * ci] = fma(val, val, acc[2 * ci]);
@@ -2013,11 +2085,28 @@ __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiU_kernel(
   const double* vo = fs.V(par, bv);
   const double* un = fs.U(par ^ 1, bv);
   double acc = 0.0;
-  for (int r = t; r < cd.dim; r += CTPB) {
-    const int i = n + cd.row + r;
-    const double val = (vn[i] + un[i]) - beta * vo[i];
-    vn[i] = val;
-    acc = fma(val, val, acc);
+  // RU rows per thread per round, every load of a round issued first (one
+  // round trip per RU·CTPB rows, not one per CTPB)
+  constexpr int RU = 8;
+  const int lo = n + cd.row, hi = lo + cd.dim;
+  for (int i0 = lo + t; i0 < hi; i0 += RU * CTPB) {
+    double a[RU], b[RU], c[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int i = i0 + u * CTPB < hi ? i0 + u * CTPB : lo;
+      a[u] = vn[i];
+      b[u] = un[i];
+      c[u] = vo[i];
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int i = i0 + u * CTPB;
+      if (i < hi) {
+        const double val = (a[u] + b[u]) - beta * c[u];
+        vn[i] = val;
+        acc = fma(val, val, acc);
+      }
+    }
   }
   acc = cblock_sum(acc, red);
   if (t == 0) fs.P(bv)[fs.oPv() + k] = acc;
@@ -2049,15 +2138,16 @@ __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiV_kernel(
     double* vn = fs.V(par ^ 1, bv);
     double* Pq = fs.P(bv);
     const int rlo = n + cd.row, rhi = n + cd.row + cd.dim;
+    double* vl = lds + img;
+    double dvs = 1.0, vend_n = 0.0;
     if (!st.skipT) {
       const double* un = fs.U(par ^ 1, bv);
       const double* c = cvec + (size_t)fs.phys(bv) * n;
-      double* vl = lds + img;
       const double ue = un[N - 1];
       double acc[2] = {0.0, 0.0};
       for (int j = t; j < n; j += CTPB) {
         const double cj = c[j];
-        const double val = (gsum8(fs.gpT + (size_t)bv * RB * n, RB, n, j) - cj * ue) - beta * vo[j];
+        const double val = (gsum32(fs.gpT + (size_t)bv * RB * n, RB, n, j) - cj * ue) - beta * vo[j];
         vl[j] = val;
         acc[0] = fma(val, val, acc[0]);
         acc[1] = fma(cj, un[j], acc[1]);
@@ -2067,35 +2157,55 @@ __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiV_kernel(
       bsumk<CTPB, 2>(acc, red);
       const double vend = acc[1] - beta * vo[N - 1];
       alpha = sqrt(acc[0] + vend * vend);
-      const double dv = alpha > 0.0 ? alpha : 1.0;   // α = 0: v stays v', as upd_v
-      for (int i = rlo + t; i < rhi; i += CTPB) vn[i] /= dv;
-      if (k == 0) {
-        for (int j = t; j < n; j += CTPB) vn[j] = vl[j] / dv;
-        if (t == 0) vn[N - 1] = vend / dv;
-      }
-    } else {   // no Mᵀ·u this step: v unchanged
-      for (int i = rlo + t; i < rhi; i += CTPB) vn[i] = vo[i];
-      if (k == 0) {
-        for (int j = t; j < n; j += CTPB) vn[j] = vo[j];
-        if (t == 0) vn[N - 1] = vo[N - 1];
-      }
+      dvs = alpha > 0.0 ? alpha : 1.0;   // α = 0: v stays v', as upd_v
+      vend_n = vend / dvs;
+    } else {   // no Mᵀ·u this step: v unchanged (carried into this parity's buffer)
+      vend_n = vo[N - 1];
     }
     const LsqrStep gs = lsqr_rotate(st, alpha, beta);
     double* x = fs.x + (size_t)bv * N;
     double* w = fs.w + (size_t)bv * N;
-    // each thread reads back only the v entries it wrote above
     double acc[2] = {0.0, 0.0};
-    auto upd = [&](int i) {
-      const double wo = w[i];
-      x[i] = x[i] + gs.t1 * wo;
-      const double wn = vn[i] + gs.t2 * wo;
-      w[i] = wn;
-      acc[0] = fma(wn, wn, acc[0]);
+    // v ← v'/α on this workgroup's rows (the cone's; cone 0 also the n part,
+    // from LDS, and the end), then x += t1·w, w ← v + t2·w there: RU rows per
+    // thread per round, every load of a round issued first
+    constexpr int RU = 8;
+    const double* vsrc = st.skipT ? vo : vn;   // v' (dpiU's rows) or the unchanged v
+    auto rows = [&](int lo, int hi, bool from_lds) {
+      for (int i0 = lo + t; i0 < hi; i0 += RU * CTPB) {
+        double vv[RU], wo[RU], xo[RU];
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          const int i = i0 + u * CTPB < hi ? i0 + u * CTPB : lo;
+          vv[u] = from_lds ? vl[i] : vsrc[i];
+          wo[u] = w[i];
+          xo[u] = x[i];
+        }
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          const int i = i0 + u * CTPB;
+          if (i < hi) {
+            const double v = st.skipT ? vv[u] : vv[u] / dvs;
+            vn[i] = v;
+            x[i] = xo[u] + gs.t1 * wo[u];
+            const double wn = v + gs.t2 * wo[u];
+            w[i] = wn;
+            acc[0] = fma(wn, wn, acc[0]);
+          }
+        }
+      }
     };
-    for (int i = rlo + t; i < rhi; i += CTPB) upd(i);
+    rows(rlo, rhi, false);
     if (k == 0) {
-      for (int j = t; j < n; j += CTPB) upd(j);
-      if (t == 0) upd(N - 1);
+      rows(0, n, !st.skipT);
+      if (t == 0) {   // the end
+        const double wo = w[N - 1];
+        vn[N - 1] = vend_n;
+        x[N - 1] = x[N - 1] + gs.t1 * wo;
+        const double wn = vend_n + gs.t2 * wo;
+        w[N - 1] = wn;
+        acc[0] = fma(wn, wn, acc[0]);
+      }
     }
     for (int r = t; r < fs.nc; r += CTPB) acc[1] += Pq[fs.oPw(par) + r];   // Σ of the old w²
     bsumk<CTPB, 2>(acc, red);
