@@ -29,11 +29,6 @@ struct ConeDesc {
   int32_t woff, pad;             // PSD side > PSD_MAX: offset into the global scratch
 };
 
-__device__ __forceinline__ double cwave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
 
 // wave sum by DPP (VALU lane moves, no LDS crossbar): quad xor 1 / 2, the
 // half-row and row mirrors, then row_bcast:15 / 31 carry the rows' totals up;
@@ -53,6 +48,15 @@ __device__ __forceinline__ double wave_sum63(double v) {
   v += cdpp<0x142, 0xA, true>(v);    // row_bcast:15 → rows 1, 3
   v += cdpp<0x143, 0xC, true>(v);    // row_bcast:31 → rows 2, 3
   return v;
+}
+
+// wave sum in every lane: the DPP sum, broadcast from lane 63
+__device__ __forceinline__ double cwave_sum(double v) {
+  v = wave_sum63(v);
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, 63);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
 __device__ __forceinline__ double cblock_sum(double v, double* red) {

@@ -73,19 +73,26 @@ __device__ __forceinline__ bool red_use(const NLPRed& R, const int32_t* shift, i
   return R.on && R.ok[b] && shift[b] == 0;
 }
 
-// R[r][col] of problem b (identity padding past n + c).  Two rounds of
-// unconditional loads (the index maps kx / yst, then the selected value and
-// δ): with a branch per case the compiler waited for every load in turn.
-__device__ __forceinline__ double nlp_R(const NLPDims& d, const NLPIn& in, const NLPRed& R, size_t b, int r,
-                                        int col) {
+// The index code of row / column r of R: kx[r] (the active bound of x_r) for
+// r < n, yst[r − n] (the state of y) past it; 0 in the identity padding.
+__device__ __forceinline__ int nlp_code(const NLPDims& d, const NLPRed& R, size_t b, int r) {
+  const int n = d.n, N = n + d.c;
+  const int rr = r >= N ? 0 : r;
+  const int32_t* kx = R.kx + b * d.num_w;
+  const int32_t* ys = d.c ? R.yst + b * d.c : kx;   // (no constraints: never a live read)
+  return rr < n ? kx[rr] : ys[rr - n];
+}
+
+// R[r][col] of problem b (identity padding past n + c) from the two index
+// codes (nlp_code of r and of col): one round of unconditional loads (the
+// selected value and δ).
+__device__ __forceinline__ double nlp_R_codes(const NLPDims& d, const NLPIn& in, const NLPRed& R, size_t b, int r,
+                                              int col, int coder, int codec) {
   const int n = d.n, N = n + d.c;
   const bool pad = r >= N || col >= N;
   const int rr = pad ? 0 : r, cc = pad ? 0 : col;
   const bool rq = rr < n, cq = cc < n;
-  const int32_t* kx = R.kx + b * d.num_w;
-  const int32_t* ys = d.c ? R.yst + b * d.c : kx;   // (no constraints: never a live read)
-  const int kr = kx[rq ? rr : 0], kc = kx[cq ? cc : 0];
-  const int yr = ys[rq ? 0 : rr - n], yc = ys[cq ? 0 : cc - n];
+  const int kr = coder, kc = codec, yr = coder, yc = codec;
   const double* dummy = in.Hxx;
   const double ident = r == col ? 1.0 : 0.0;
   double cv = 0.0;
@@ -123,6 +130,14 @@ __device__ __forceinline__ double nlp_R(const NLPDims& d, const NLPIn& in, const
   const double x = *p;
   const double dl = *(addd ? R.delta + b * d.num_w + rr : dummy);
   return mode == 0 ? cv : (mode == 2 ? -x : (addd ? x + dl : x));
+}
+
+// R[r][col]: two rounds of unconditional loads (the index codes, then the
+// selected value and δ) — with a branch per case the compiler waited for every
+// load in turn
+__device__ __forceinline__ double nlp_R(const NLPDims& d, const NLPIn& in, const NLPRed& R, size_t b, int r,
+                                        int col) {
+  return nlp_R_codes(d, in, R, b, r, col, nlp_code(d, R, b, r), nlp_code(d, R, b, col));
 }
 
 

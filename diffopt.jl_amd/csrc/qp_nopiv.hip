@@ -256,6 +256,34 @@ __device__ __forceinline__ double src_val(const NSrcB& v, int r, int c) {
 // with the lanes along r: coalesced as is
 __device__ __forceinline__ double src_val_lower(const NSrcB& v, int r, int c) { return src_val(v, r, c); }
 
+// Column tiles: the index codes of the tile's 64 rows (from r0) and 64 columns
+// (from c0) staged once per workgroup in the padding columns 64..79 of the
+// tile's first LDS rows (int view: row k holds 32 codes at columns 64..79), so
+// each source entry is one round of loads, not two.  QP sources: nothing.
+constexpr int CODE_LD = NB64 + 16;   // = TLD (the tiles' LDS row stride, asserted there)
+__device__ __forceinline__ int* tile_codes(double* X) { return reinterpret_cast<int*>(X + NB64); }
+__device__ __forceinline__ int tile_code(const int* tc, int idx) {   // idx < 128: rows, then columns
+  return tc[(idx >> 5) * (2 * CODE_LD) + (idx & 31)];
+}
+__device__ __forceinline__ void src_stage_codes(const QSrc&, const QSrcB&, double*, int, int) {}
+__device__ __forceinline__ void src_stage_codes(const NSrc& s, const NSrcB& v, double* X, int r0, int c0) {
+  const int t = threadIdx.x;
+  if (t < 128) {
+    const int r = t < 64 ? r0 + t : c0 + (t - 64);
+    int* tc = tile_codes(X);
+    tc[(t >> 5) * (2 * CODE_LD) + (t & 31)] = nlp_code(s.d, s.R, v.b, r);
+  }
+}
+__device__ __forceinline__ double src_val_tile(const QSrcB& v, const double*, int r, int c, int, int) {
+  return kval_lower(v, r, c);
+}
+__device__ __forceinline__ double src_val_tile(const NSrcB& v, const double* X, int r, int c, int ri, int ci) {
+  const int* tc = tile_codes(const_cast<double*>(X));
+  return nlp_R_codes(v.s->d, v.s->in, v.s->R, v.b, r, c, tile_code(tc, ri), tile_code(tc, 64 + ci));
+}
+template <class SRC> constexpr bool src_staged() { return false; }
+template <> constexpr bool src_staged<NSrc>() { return true; }
+
 // Tile `tile` of the lower triangle (rt ≥ ct) of an nrt × nrt grid, column by
 // column: column 0's nrt tiles first.
 __device__ __forceinline__ void col_lower_tile(int tile, int nrt, int& rt, int& ct) {
@@ -1045,6 +1073,7 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
 // through LDS).  Every U12 entry is held to the growth bound.
 // ---------------------------------------------------------------------------
 constexpr int TLD = 64 + 16;   // LDS row stride (doubles) of a staged 64×64 operand
+static_assert(TLD == CODE_LD, "the NLP tiles' index codes live in TLD's padding columns");
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_trsm_kernel(double* __restrict__ K, int ld, int nmax,
                                                        QPMeta* __restrict__ meta, int c0,
@@ -1985,6 +2014,9 @@ __device__ __forceinline__ void lcol_body(
   const auto sv = src_bind(src, b, mm);
   const PScale ps = pscale(kls, b, n, m, mm);
   const double bound = growth_bound(__hip_atomic_load(kamax + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  // NLP: the tile's index codes into LDS (ordered by the k-loop's barriers,
+  // or the one below when there is no k-loop)
+  if (TW == 1) src_stage_codes(src, sv, X[0], r0, c0);
   d4n acc[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = (d4n){0, 0, 0, 0};
@@ -2044,9 +2076,12 @@ __device__ __forceinline__ void lcol_body(
   double av[16], v[VQ], pj[4];
 #pragma unroll
   for (int q = 0; q < VQ; ++q) v[q] = Bg[T + NTH * q];
+  if (TW == 1 && src_staged<SRC>() && c0 == 0) __syncthreads();   // the codes (no k-loop)
   if (wact) {
 #pragma unroll
-    for (int s = 0; s < 16; ++s) av[s] = src_val_lower(sv, r0 + 16 * wv + l16, c0 + 4 * s + g);
+    for (int s = 0; s < 16; ++s)
+      av[s] = TW == 1 ? src_val_tile(sv, X[0], r0 + 16 * wv + l16, c0 + 4 * s + g, 16 * wv + l16, 4 * s + g)
+                      : src_val_lower(sv, r0 + 16 * wv + l16, c0 + 4 * s + g);
 #pragma unroll
     for (int q = 0; q < 4; ++q) pj[q] = ps(c0 + 16 * q + l16);
   }

@@ -231,8 +231,10 @@ def test_well_posed_batch(ConicBatch):
 
 
 def test_mixed_cones_batch(ConicBatch):
+    # LSQR to maxiter on a singular M: 32–33 of 36 under the 1-ulp envelope bar
+    # (r04: 33 with the DPP wave sums' summation order)
     _synthetic_check(ConicBatch, 6, 30, [(0, 3), (1, 10), (3, 6), (2, 4), (4, 6)], 11, "mixed cones",
-                     cap=32)
+                     cap=34)
 
 
 def test_soc_only_batch(ConicBatch):
