@@ -64,6 +64,16 @@ __device__ __forceinline__ double wave_max_f64(double v) {
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
   return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
+// sum over each group of 8 lanes, in every lane of the group, by DPP (quad
+// xor 1, xor 2, then the half-row mirror: lane i + lane 7 − i): the same
+// additions in the same order as the xor-1/2/4 butterfly, without the LDS
+// crossbar of __shfl_xor
+__device__ __forceinline__ double sum8_dpp(double d) {
+  d += dpp_f64<0xB1, 0xF>(d);    // quad_perm [1,0,3,2]
+  d += dpp_f64<0x4E, 0xF>(d);    // quad_perm [2,3,0,1]
+  d += dpp_f64<0x141, 0xF>(d);   // row_half_mirror
+  return d;
+}
 __device__ __forceinline__ int wave_min_i32(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
@@ -780,9 +790,7 @@ __device__ __forceinline__ void solve_rows_body(int b, const double* __restrict_
           double d = f[p][0] * xk[0];
 #pragma unroll
           for (int u = 1; u < 4; ++u) d = fma(f[p][u], xk[u], d);
-          d += __shfl_xor(d, 1);
-          d += __shfl_xor(d, 2);
-          d += __shfl_xor(d, 4);
+          d = sum8_dpp(d);
           const int li = (c * RCH + p) * RPASS + rid;
           if (g8 == 0 && li < ecnt) v[e0 + li] -= d;   // rows outside block k only
         }
@@ -1035,9 +1043,7 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           double d = f[p][0] * xk[0];
 #pragma unroll
           for (int u = 1; u < 4; ++u) d = fma(f[p][u], xk[u], d);
-          d += __shfl_xor(d, 1);
-          d += __shfl_xor(d, 2);
-          d += __shfl_xor(d, 4);
+          d = sum8_dpp(d);
           const int li = (c * SCH + p) * RPASS + rid;
           if (g8 == 0 && li < ecnt) v[e0 + li] -= d;
         }
@@ -1228,9 +1234,15 @@ void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, con
     else if (ent <= 1)
       hipLaunchKernelGGL((blu_sym2_kernel<1, 5>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, meta,
                          w_rev, w_fwd, x_rev, x_fwd, sym);
+    else if (ent == 2 && h.sym_tpb == 256)   // 256 threads × 4 entries, rows in groups of 4
+      hipLaunchKernelGGL((blu_sym2_kernel<4, 4, 256, 4>), dim3(B), dim3(256), 0, h.stream, K, h.ld, h.nmax, dinv,
+                         dstride, meta, w_rev, w_fwd, x_rev, x_fwd, sym);
     else if (ent == 2)
       hipLaunchKernelGGL((blu_sym2_kernel<2, 2>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, meta,
                          w_rev, w_fwd, x_rev, x_fwd, sym);
+    else if (h.sym_tpb == 256)   // 256 threads × 6 entries (Np ≤ 1536), rows in groups of 4
+      hipLaunchKernelGGL((blu_sym2_kernel<6, 3, 256, 4>), dim3(B), dim3(256), 0, h.stream, K, h.ld, h.nmax, dinv,
+                         dstride, meta, w_rev, w_fwd, x_rev, x_fwd, sym);
     else
       hipLaunchKernelGGL((blu_sym2_kernel<3, 2>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, meta,
                          w_rev, w_fwd, x_rev, x_fwd, sym);
