@@ -175,8 +175,7 @@ def run_nlp(args, world, rank, local_rank):
 
     def step():
         eng.factor()
-        eng.forward(dp_t)
-        eng.reverse(dx_t, dd_t)
+        eng.forward_reverse(dp_t, dx_t, dd_t)   # forward + reverse, one pass over the factors for both
 
     for _ in range(args.warmup):
         step()

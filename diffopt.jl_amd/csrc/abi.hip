@@ -697,6 +697,31 @@ int dopt_nlp_reverse(dopt_handle* h, const double* dx, const double* ddual, doub
   });
 }
 
+int dopt_nlp_forward_reverse(dopt_handle* h, const double* dp, const double* dx_seed, const double* ddual_seed,
+                             double* dx_out, double* ddual_out, double* dp_out) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_forward_reverse on a non-NLP handle");
+    if (!dx_out || !ddual_out) throw Error(-1, "dx_out and ddual_out are required");
+    if (h->p && (!dp || !dp_out)) throw Error(-1, "dp and dp_out are required");
+    Timer tm;
+    const size_t B = h->batch, nd = (size_t)h->m + h->nlp_nlowp + h->nlp_nupp;
+    static const double zero = 0.0;
+    const double* d = h->p ? stage_in(*h, h->tin[0], dp, B * h->p) : &zero;
+    const double* ix = stage_in(*h, h->tin[1], dx_seed, B * h->n);
+    const double* id = stage_in(*h, h->tin[2], ddual_seed, B * nd);
+    double* ox = out_ptr(*h, h->tout[0], dx_out, B * h->n);
+    double* od = out_ptr(*h, h->tout[1], ddual_out, B * nd);
+    double* op = out_ptr(*h, h->tout[2], dp_out, B * h->p);
+    dopt::nlp_forward_reverse(*h, d, ix, id, ox, od, op);
+    copy_out(*h, dx_out, ox, B * h->n);
+    copy_out(*h, ddual_out, od, B * nd);
+    copy_out(*h, dp_out, op, B * h->p);
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    h->last_time = tm.s();
+    return 0;
+  });
+}
+
 int dopt_nlp_jacobian(dopt_handle* h, double* ds) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_jacobian on a non-NLP handle");

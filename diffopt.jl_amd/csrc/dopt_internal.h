@@ -335,6 +335,8 @@ void qp_blocked_factor(Handle& h, double* dinv, const int32_t* plist, int count)
 // that reads U: single-direction and multi-RHS solves); no-op unless u_missing
 void qp_nopiv_materialize_u(Handle& h);
 void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rhs, double* x, int sel);
+void qp_blocked_solve_pair(Handle& h, const double* dinv, const double* rhs0, const double* rhs1, double* x0,
+                           double* x1, int sel);
 void qp_blocked_solve_multi(Handle& h, const double* dinv, int trans, int k, const double* rhs, double* x,
                             int sel);
 void qp_reverse_k(Handle& h, int k, const double* dl_dz, double* out);
@@ -359,6 +361,8 @@ void nlp_configure(Handle& h);
 void nlp_factor(Handle& h);
 void nlp_forward(Handle& h, const double* dp, double* dx, double* ddual);
 void nlp_reverse(Handle& h, const double* dx, const double* ddual, double* dp);
+void nlp_forward_reverse(Handle& h, const double* dp, const double* dxs, const double* dds, double* dx,
+                         double* ddual, double* dpo);
 void nlp_jacobian(Handle& h, double* ds);
 void nlp_kkt_solve(Handle& h, int k, const double* rhs, double* x);
 void conic_factor(Handle& h);

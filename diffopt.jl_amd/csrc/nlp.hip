@@ -911,6 +911,51 @@ void nlp_reverse(Handle& h, const double* dx, const double* ddual, double* dp) {
   DOPT_CHECK_HIP(hipGetLastError());
 }
 
+// nlp_forward then nlp_reverse, the two solves as one pair launch (one pass
+// over the factors for both directions; the same arithmetic per direction)
+void nlp_forward_reverse(Handle& h, const double* dp, const double* dxs, const double* dds, double* dx,
+                         double* ddual, double* dpo) {
+  if (!h.nfactored) nlp_factor(h);
+  if (h.nlp_kkt) throw Error(-1, "dopt_nlp_forward_reverse: the handle holds a KKT matrix (use dopt_nlp_kkt_solve)");
+  const int B = (int)h.batch;
+  const size_t blk = (size_t)B * h.nmax;
+  double* rf = h.rhs.as<double>();
+  double* rr = rf + blk;
+  double* x = h.x.as<double>();
+  double* u = x + blk;
+  const bool red = reduced_on(h);
+  double* t1 = red ? red_t1(h, 2) : nullptr;
+  double* t2 = red ? red_t2(h, 2) : nullptr;
+  {
+    PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
+    hipLaunchKernelGGL(nlp_fwd_rhs_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), inputs(h), dp, h.nmax, rf);
+    DOPT_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(nlp_rev_rhs_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), dxs, dds, h.nmax, rr);
+    DOPT_CHECK_HIP(hipGetLastError());
+    if (red) {
+      red_rhs(h, 0, 1, rf, t1);
+      red_rhs(h, 1, 1, rr, t1 + blk);
+    }
+  }
+  {
+    PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
+    qp_blocked_solve_pair(h, dense_dinv(h), red ? t1 : rf, red ? t1 + blk : rr, red ? t2 : x, red ? t2 + blk : u,
+                          LU_SEL_ALL);
+  }
+  if (red) {
+    red_recover(h, 0, 1, rf, t2, x);
+    red_recover(h, 1, 1, rr, t2 + blk, u);
+  }
+  PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
+  hipLaunchKernelGGL(nlp_fwd_out_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), x, h.nmax,
+                     h.nlp_shift.as<int32_t>(), dx, ddual);
+  DOPT_CHECK_HIP(hipGetLastError());
+  if (h.p)
+    hipLaunchKernelGGL(nlp_rev_out_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), inputs(h), u, h.nmax,
+                       h.nlp_shift.as<int32_t>(), dpo);
+  DOPT_CHECK_HIP(hipGetLastError());
+}
+
 // k right-hand sides per problem (seed-major, stride B·nmax) through the
 // blocked factors, one multi-RHS launch
 static void solve_multi(Handle& h, int trans, int k, double* rk, double* xk) {

@@ -979,13 +979,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
 //   Kᵀ x = c:  Kᵀ = P·K·P⁻¹, so x = p .* w with K w = c ./ p.
 // Forward sweep by row segments of L (contiguous per entry), backward by
 // column segments (contiguous across entries), both in halves of 16 rows /
-// columns; no U, no permutation.
-template <int ENT, int WPE>
-__global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(WPE))) void blu_symsolve_kernel(
+// columns; no U, no permutation.  NV = 2: both directions in one pass over L
+// (vector 0 through K, vector 1 through Kᵀ; `trans` unused) — the NLP
+// forward + reverse pair; each vector's arithmetic is the NV = 1 kernel's, in
+// the same order, so the pair's results equal two single-direction launches.
+template <int ENT, int WPE, int TPB = PT, int RH = 16, int NV = 1>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void blu_symsolve_kernel(
     const double* __restrict__ K, int ld, int nmax, const double* __restrict__ dinv, size_t dstride,
     const QPMeta* __restrict__ meta, int trans, const double* __restrict__ rhs, double* __restrict__ xout,
-    SymSweep sym) {
-  __shared__ double v[SOLVE_STATIC], part[BNB];
+    const double* __restrict__ rhs1, double* __restrict__ xout1, SymSweep sym) {
+  static_assert(NV == 1 || NV == 2, "one or two directions");
+  __shared__ double v[NV][SOLVE_STATIC], part[NV][BNB];
   const int b = blockIdx.x;
   const QPMeta mm = meta[b];
   const int Np = blocked_np(mm);
@@ -996,26 +1000,31 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   const double* Dbase = dinv + (size_t)b * dstride;
   const double* udb = sym.ukp + (size_t)b * nmax;
   const PScale psc{sym.kls ? sym.kls + (size_t)b * sym.m : nullptr, sym.n, mm.nk};
-  const double* rb = rhs + (size_t)b * nmax;
-  for (int i = t; i < Np; i += PT) v[i] = i < N ? (trans ? rb[i] / psc(i) : rb[i]) : 0.0;
+  auto tr = [&](int k) { return NV == 2 ? k : trans; };
+  constexpr int RP = TPB / 8;   // rows per pass of the forward sweep
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const double* rb = (k ? rhs1 : rhs) + (size_t)b * nmax;
+    for (int i = t; i < Np; i += TPB) v[k][i] = i < N ? (tr(k) ? rb[i] / psc(i) : rb[i]) : 0.0;
+  }
   __syncthreads();
   const int nblk = Np / BNB;
   // forward: L y = r (block k: y_k = L_kk⁻¹ v_k, then v_e −= L[e][k-block]·y_k
   // for e past it): row segments, 8 lanes per row × 4 doubles (one wave load
-  // touches 8 rows' lines), 64 rows per pass, up to SCH passes in flight
-  // across the diagonal solve
+  // touches 8 rows' lines), RP rows per pass, up to SCH passes in flight
+  // across the diagonal solve (wave k: vector k's)
   {
     constexpr int SCH = 4;   // passes per chunk: 16 doubles in flight, no spill at WPE 5
     const int g8 = t & 7, rid = t >> 3;
     for (int bk = 0; bk < nblk; ++bk) {
       const int i0 = bk * BNB, e0 = i0 + BNB, ecnt = Np - e0;
-      const int npass = (ecnt + RPASS - 1) / RPASS;
+      const int npass = (ecnt + RP - 1) / RP;
       double f[SCH][4];
       auto load_chunk = [&](int c) {
 #pragma unroll
         for (int p = 0; p < SCH; ++p) {
-          if ((c * SCH + p) * RPASS >= ecnt) break;   // uniform
-          const int li = (c * SCH + p) * RPASS + rid;
+          if ((c * SCH + p) * RP >= ecnt) break;   // uniform
+          const int li = (c * SCH + p) * RP + rid;
           const int ec = li < ecnt ? e0 + li : i0;
           const double* row = Kb + (size_t)ec * ld + i0 + 4 * g8;
 #pragma unroll
@@ -1023,77 +1032,106 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         }
       };
       if (npass > 0) load_chunk(0);
-      if (wv == 0 && lane < BNB) {
+      if (wv < NV && lane < BNB) {
         const double* Dk = Dbase + (size_t)bk * BDINV + lane * BNB;   // row `lane` of L⁻¹
+        const double* vv = v[wv];
         double acc = 0.0;
 #pragma unroll 8
-        for (int j = 0; j < BNB; ++j) acc = fma(Dk[j], v[i0 + j], acc);
-        part[lane] = acc;
+        for (int j = 0; j < BNB; ++j) acc = fma(Dk[j], vv[i0 + j], acc);
+        part[wv][lane] = acc;
       }
       __syncthreads();
-      if (wv == 0 && lane < BNB) v[i0 + lane] = part[lane];
-      double xk[4];
+      if (wv < NV && lane < BNB) v[wv][i0 + lane] = part[wv][lane];
+      double xk[NV][4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) xk[u] = part[4 * g8 + u];
+      for (int k = 0; k < NV; ++k)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) xk[k][u] = part[k][4 * g8 + u];
       for (int c = 0; c * SCH < npass; ++c) {
         if (c > 0) load_chunk(c);
 #pragma unroll
         for (int p = 0; p < SCH; ++p) {
-          if ((c * SCH + p) * RPASS >= ecnt) break;
-          double d = f[p][0] * xk[0];
+          if ((c * SCH + p) * RP >= ecnt) break;
+          const int li = (c * SCH + p) * RP + rid;
 #pragma unroll
-          for (int u = 1; u < 4; ++u) d = fma(f[p][u], xk[u], d);
-          d = sum8_dpp(d);
-          const int li = (c * SCH + p) * RPASS + rid;
-          if (g8 == 0 && li < ecnt) v[e0 + li] -= d;
+          for (int k = 0; k < NV; ++k) {
+            double d = f[p][0] * xk[k][0];
+#pragma unroll
+            for (int u = 1; u < 4; ++u) d = fma(f[p][u], xk[k][u], d);
+            d = sum8_dpp(d);
+            if (g8 == 0 && li < ecnt) v[k][e0 + li] -= d;
+          }
         }
       }
       __syncthreads();
     }
   }
-  for (int i = t; i < Np; i += PT) v[i] /= udb[i];   // y ./ (u/p)
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+    for (int i = t; i < Np; i += TPB) v[k][i] /= udb[i];   // y ./ (u/p)
   __syncthreads();
   // backward: Lᵀ (P w) = v
   for (int s = 0; s < nblk; ++s) {
     const int bk = nblk - 1 - s;
     const int i0 = bk * BNB;
-    double f[ENT][16];
+    double f[ENT][RH];
 #pragma unroll
     for (int q = 0; q < ENT; ++q) {
-      const int e = t + PT * q;
+      const int e = t + TPB * q;
       const int ec = e < i0 ? e : 0;
-      if (q * PT >= i0) continue;
+      if (q * TPB >= i0) continue;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) f[q][j] = Kb[(size_t)(i0 + j) * ld + ec];
+      for (int j = 0; j < RH; ++j) f[q][j] = Kb[(size_t)(i0 + j) * ld + ec];
     }
-    if (wv == 0 && lane < BNB) {
+    if (wv < NV && lane < BNB) {
       const double* Dk = Dbase + (size_t)bk * BDINV;
+      const double* vv = v[wv];
       double acc = 0.0;
 #pragma unroll 8
-      for (int j = 0; j < BNB; ++j) acc = fma(Dk[lane + j * BNB], v[i0 + j], acc);
-      part[lane] = acc;
+      for (int j = 0; j < BNB; ++j) acc = fma(Dk[lane + j * BNB], vv[i0 + j], acc);
+      part[wv][lane] = acc;
     }
     __syncthreads();
-    if (wv == 0 && lane < BNB) v[i0 + lane] = part[lane];
+    if (wv < NV && lane < BNB) v[wv][i0 + lane] = part[wv][lane];
+    double a[NV][ENT];
+    int ec[ENT];
 #pragma unroll
     for (int q = 0; q < ENT; ++q) {
-      const int e = t + PT * q;
-      if (q * PT >= i0) continue;
+      const int e = t + TPB * q;
       const bool has = e < i0;
-      const int ec = has ? e : 0;
-      double a = has ? v[e] : 0.0;
+      ec[q] = has ? e : 0;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) a = fma(-f[q][j], part[j], a);
+      for (int k = 0; k < NV; ++k) a[k][q] = has ? v[k][e] : 0.0;
+    }
 #pragma unroll
-      for (int j = 0; j < 16; ++j) f[q][j] = Kb[(size_t)(i0 + 16 + j) * ld + ec];
+    for (int h = 0; h < BNB / RH; ++h) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) a = fma(-f[q][j], part[16 + j], a);
-      if (has) v[e] = a;
+      for (int q = 0; q < ENT; ++q) {
+        if (q * TPB >= i0) continue;   // workgroup-uniform
+        if (h) {
+#pragma unroll
+          for (int j = 0; j < RH; ++j) f[q][j] = Kb[(size_t)(i0 + RH * h + j) * ld + ec[q]];
+        }
+#pragma unroll
+        for (int j = 0; j < RH; ++j)
+#pragma unroll
+          for (int k = 0; k < NV; ++k) a[k][q] = fma(-f[q][j], part[k][RH * h + j], a[k][q]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < ENT; ++q) {
+      const int e = t + TPB * q;
+      if (q * TPB < i0 && e < i0)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k][e] = a[k][q];
     }
     __syncthreads();
   }
-  double* xb = xout + (size_t)b * nmax;
-  for (int i = t; i < N; i += PT) xb[i] = trans ? v[i] : v[i] / psc(i);   // Kᵀ: p .* w = (P w); K: w = (P w) ./ p
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double* xb = (k ? xout1 : xout) + (size_t)b * nmax;
+    for (int i = t; i < N; i += TPB) xb[i] = tr(k) ? v[k][i] : v[k][i] / psc(i);   // Kᵀ: p .* w = (P w); K: w = (P w) ./ p
+  }
 }
 
 }  // namespace
@@ -1178,10 +1216,18 @@ void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rh
     const int ent = (npmax + PT - 1) / PT;
 #define DOPT_SYMSOLVE(E, W)                                                                                   \
   hipLaunchKernelGGL((blu_symsolve_kernel<E, W>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, \
-                     meta, trans, rhs, x, sym)
-    if (ent <= 1) { DOPT_SYMSOLVE(1, 5); }
+                     meta, trans, rhs, x, nullptr, nullptr, sym)
+#define DOPT_SYMSOLVE256(E, W, R)                                                                            \
+  hipLaunchKernelGGL((blu_symsolve_kernel<E, W, 256, R>), dim3(B), dim3(256), 0, h.stream, K, h.ld, h.nmax, dinv,   \
+                     dstride, meta, trans, rhs, x, nullptr, nullptr, sym)
+    if (h.sym_tpb == 256) {   // 256-thread workgroups, 2 / 4 / 6 entries per thread (as blu_sym2_kernel)
+      if (ent <= 1) { DOPT_SYMSOLVE256(2, 4, 8); }
+      else if (ent == 2) { DOPT_SYMSOLVE256(4, 4, 4); }
+      else { DOPT_SYMSOLVE256(6, 3, 4); }
+    } else if (ent <= 1) { DOPT_SYMSOLVE(1, 5); }
     else if (ent == 2) { DOPT_SYMSOLVE(2, 2); }
     else { DOPT_SYMSOLVE(3, 2); }
+#undef DOPT_SYMSOLVE256
 #undef DOPT_SYMSOLVE
     DOPT_CHECK_HIP(hipGetLastError());
     sel &= ~LU_SEL_NOPIV;   // every no-pivot problem of the route is P-symmetric
@@ -1207,6 +1253,39 @@ void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rh
 #undef DOPT_SOLVE1
   }
   DOPT_CHECK_HIP(hipGetLastError());
+}
+
+// Both directions (rhs0 through K, rhs1 through Kᵀ) from factors already in
+// place: the P-symmetric problems in one NV = 2 sweep launch (one pass over L
+// for the pair), anything else through the single-direction solves.
+void qp_blocked_solve_pair(Handle& h, const double* dinv, const double* rhs0, const double* rhs1, double* x0,
+                           double* x1, int sel) {
+  const int npmax = h.blocked_npmax;
+  if (npmax == 0) return;
+  if (h.ukp_valid && h.sym_lean && (sel & LU_SEL_NOPIV) && npmax <= SOLVE_STATIC) {
+    const int B = (int)h.batch;
+    const size_t dstride = dinv_stride(h.nmax);
+    const double* K = h.K.as<double>();
+    const QPMeta* meta = h.meta.as<QPMeta>();
+    SymSweep sym{h.ukp.as<double>(), h.kind == DOPT_KIND_QP ? h.kls.as<double>() : nullptr, h.n, h.m};
+    const int ent = (npmax + PT - 1) / PT;
+#define DOPT_SYMPAIR(E, W, T, R)                                                                               \
+  hipLaunchKernelGGL((blu_symsolve_kernel<E, W, T, R, 2>), dim3(B), dim3(T), 0, h.stream, K, h.ld, h.nmax, dinv, \
+                     dstride, meta, 0, rhs0, x0, rhs1, x1, sym)
+    if (h.sym_tpb == 256) {
+      if (ent <= 1) { DOPT_SYMPAIR(2, 4, 256, 8); }
+      else if (ent == 2) { DOPT_SYMPAIR(4, 4, 256, 4); }
+      else { DOPT_SYMPAIR(6, 3, 256, 4); }
+    } else if (ent <= 1) { DOPT_SYMPAIR(1, 5, PT, 16); }
+    else if (ent == 2) { DOPT_SYMPAIR(2, 2, PT, 16); }
+    else { DOPT_SYMPAIR(3, 2, PT, 16); }
+#undef DOPT_SYMPAIR
+    DOPT_CHECK_HIP(hipGetLastError());
+    sel &= ~LU_SEL_NOPIV;
+    if (!sel) return;
+  }
+  qp_blocked_solve(h, dinv, 0, rhs0, x0, sel);
+  qp_blocked_solve(h, dinv, 1, rhs1, x1, sel);
 }
 
 void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, const double* rhs_fwd,

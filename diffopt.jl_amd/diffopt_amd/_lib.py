@@ -65,6 +65,7 @@ SIGNATURES = {
     "dopt_nlp_factor": (ctypes.c_int, [_h]),
     "dopt_nlp_forward": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 3),
     "dopt_nlp_reverse": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 3),
+    "dopt_nlp_forward_reverse": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 6),
     "dopt_nlp_jacobian": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_nlp_get_corrections": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_nlp_get_layout": (ctypes.c_int, [_h, ctypes.c_void_p]),

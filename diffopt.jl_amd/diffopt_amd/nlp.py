@@ -182,6 +182,24 @@ class NLPBatch:
         _lib.check(rc, self.h)
         return out
 
+    def forward_reverse(self, dp, dx=None, ddual=None):
+        """forward(dp) and reverse(dx, ddual) against the same factors in one
+        call (dopt_nlp_forward_reverse: one pass over the factors for both
+        directions) → (Δx, Δdual, Δp)."""
+        B = self.batch
+        st = self._stage([dp, dx, ddual])
+        dev = st.mem == _lib.DOPT_MEM_DEVICE
+        d = vector(dp, (B, self.P)) if self.P else None
+        a = vector(dx, (B, self.n)) if dx is not None else None
+        b = vector(ddual, (B, self.ndual)) if ddual is not None else None
+        ox = Staged.empty((B, self.n), dev)
+        od = Staged.empty((B, self.ndual), dev)
+        op = Staged.empty((B, self.P), dev)
+        rc = self.lib.dopt_nlp_forward_reverse(self.h, st.ptr(d), st.ptr(a), st.ptr(b), st.ptr(ox), st.ptr(od),
+                                               st.ptr(op))
+        _lib.check(rc, self.h)
+        return ox, od, op
+
     def jacobian(self, device=False):
         """∂s (B, rows, P) — the reference's Δs per problem."""
         rows = self.layout()["rows"]

@@ -593,6 +593,20 @@ function nlp_reverse(e::NLPBatch; dx = nothing, ddual = nothing)
     return dp
 end
 
+"Both modes against the same factors in one call (one pass over them): dp, seeds → (dx, ddual, dp_out)."
+function nlp_forward_reverse(e::NLPBatch, dp::AbstractMatrix; dx = nothing, ddual = nothing)
+    dpd = convert(Matrix{Float64}, dp)
+    a, d = _dense(dx), _dense(ddual)
+    ox = Matrix{Float64}(undef, e.n, e.batch)
+    od = Matrix{Float64}(undef, _ndual(e), e.batch)
+    op = Matrix{Float64}(undef, e.P, e.batch)
+    GC.@preserve dpd a d ox od op _check(ccall((:dopt_nlp_forward_reverse, LIB), Cint,
+                                               (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                                                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                                               e.ptr, dpd, _fptr(a), _fptr(d), ox, od, op), e.ptr)
+    return ox, od, op
+end
+
 "∂s per problem (nlp_utilities.jl:457-500): rows × P × B."
 function nlp_jacobian(e::NLPBatch)
     rows = nlp_layout(e)[1]

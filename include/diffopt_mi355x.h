@@ -311,6 +311,14 @@ int dopt_nlp_factor(dopt_handle* h);
 int dopt_nlp_forward(dopt_handle* h, const double* dp, double* dx, double* ddual);
 /* dx[n], ddual[c + nlow + nup] (either may be NULL = 0) → dp[P] = ∂sᵀΔw. */
 int dopt_nlp_reverse(dopt_handle* h, const double* dx, const double* ddual, double* dp);
+/* Both of the above against the same factors in one call (forward_differentiate!
+ * then reverse_differentiate!, NonLinearProgram.jl:502-582): dp → dx_out,
+ * ddual_out and dx_seed, ddual_seed (either may be NULL = 0) → dp_out; one
+ * pass over the factors serves both directions.  Results equal
+ * dopt_nlp_forward + dopt_nlp_reverse. */
+int dopt_nlp_forward_reverse(dopt_handle* h, const double* dp, const double* dx_seed,
+                             const double* ddual_seed, double* dx_out, double* ddual_out,
+                             double* dp_out);
 /* ∂s itself: ds[rows × P] per problem (column-major), rows = the size of M
  * (dopt_nlp_get_layout). */
 int dopt_nlp_jacobian(dopt_handle* h, double* ds);

@@ -393,3 +393,49 @@ def test_reduced_route_mixed_with_full_route():
         assert corr[b] == oracle_problem(st, pt, b)[4]
     check_against_oracle(e, st, pt, dp, dx, dd, range(B))
     e.close()
+
+
+# ---- forward + reverse in one call (dopt_nlp_forward_reverse) ---------------
+@pytest.mark.parametrize("case", ["synthetic", "full_route", "mixed_routes", "config6", "device", "no_seeds"])
+def test_forward_reverse_equals_separate_calls(case, lu_mode, monkeypatch):
+    """One call for both directions (the P-symmetric problems' solves as one
+    pair launch over the factors) gives exactly the separate forward and
+    reverse calls' outputs — the pair kernel does each direction's arithmetic
+    in the same order — on the reduced and the full route, a batch mixing the
+    two, config 6's shape, device-mode tensors and absent reverse seeds; and
+    the outputs match the oracle at north_star's 1e-6."""
+    import torch
+    from diffopt_amd.synthetic import SEED0, nlp_numpy
+    if case == "full_route":
+        monkeypatch.setenv("DOPT_NLP_REDUCE", "0")
+    shape = {"config6": (2, 200, 100, 20)}.get(case, (5, 40, 25, 6))
+    B = shape[0]
+    st, pt, dp, dx, dd = nlp_numpy(*shape, SEED0 + 6 if case == "config6" else 8100)
+    if case == "mixed_routes":
+        j = int(np.flatnonzero(st["has_low"])[0])
+        pt["xl"][1, j], pt["yl"][1, j] = pt["x"][1, j], 0.0   # problem 1 leaves the reduced route
+    if case == "no_seeds":
+        dx = dd = None
+    e = engine(st, pt, B)
+    fx, fd = e.forward(dp)
+    rp = e.reverse(dx, dd)
+    if case == "device":
+        from diffopt_amd.nlp import NLPBatch
+        t = lambda a: torch.as_tensor(a, device="cuda")
+        ed = NLPBatch(*shape)
+        ed.set_structure(st["con_kind"], st["has_low"], st["has_up"], st["sense"])
+        ed.set(*[t(pt[k]) for k in KEYS])
+        ed.factor()
+        gx, gd, gp = (a.cpu().numpy() for a in ed.forward_reverse(t(dp), t(dx), t(dd)))
+    else:
+        gx, gd, gp = e.forward_reverse(dp, dx, dd)
+    np.testing.assert_array_equal(gx, fx)
+    np.testing.assert_array_equal(gd, fd)
+    np.testing.assert_array_equal(gp, rp)
+    zx = np.zeros_like(fx) if dx is None else dx
+    zd = np.zeros_like(fd) if dd is None else dd
+    for b in range(min(B, 2)):
+        ds, L, *_ = oracle_problem(st, pt, b)
+        ox, od = onlp.forward(ds, L, dp[b])
+        assert relfro(np.concatenate([gx[b], gd[b]]), np.concatenate([ox, od])) <= RTOL
+        assert relfro(gp[b], onlp.reverse(ds, L, zx[b], zd[b])) <= RTOL
