@@ -442,23 +442,43 @@ __device__ __forceinline__ void red_rr(const NLPDims& d, const NLPMap& mp, const
   }
 }
 
+// NV = 1: right-hand side blockIdx.y, through M (trans 0) or Mᵀ (trans 1);
+// NV = 2 (grid (B, 1)): the forward / reverse pair of dopt_nlp_forward_reverse,
+// vector k at (k·B + b)·nmax through M (k = 0) and Mᵀ (k = 1), reading H and J
+// once for both.  (Jᵀ y)_i over the rows with y known is formed first, 16
+// lanes per column of J (contiguous), instead of one lane per column walking
+// a row of J (a 64-line gather per load).
+template <int NV>
 __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, NLPIn in, NLPRed Rd,
                                                          const int32_t* __restrict__ shift, int trans,
                                                          const double* __restrict__ rfull,
                                                          double* __restrict__ rred, int nmax,
                                                          const QPMeta* __restrict__ meta) {
   extern __shared__ double sm[];
-  const size_t b = blockIdx.x, off = ((size_t)blockIdx.y * gridDim.x + b) * nmax;
-  const double* r = rfull + off;
-  double* o = rred + off;
+  const size_t b = blockIdx.x, B = gridDim.x;
+  const double* r[NV];
+  double* o[NV];
+  int tr[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const size_t off = ((NV == 2 ? (size_t)k : (size_t)blockIdx.y) * B + b) * nmax;
+    r[k] = rfull + off;
+    o[k] = rred + off;
+    tr[k] = NV == 2 ? k : trans;
+  }
   const int t = threadIdx.x;
   if (!red_use(Rd, shift, (int)b)) {
-    for (int i = t; i < nmax; i += NT) o[i] = r[i];
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+      for (int i = t; i < nmax; i += NT) o[k][i] = r[k][i];
     return;
   }
   const int n = d.n, c = d.c, w = d.num_w, N = n + c;
-  double *rr = sm, *zk = sm + w, *yv = sm + 2 * w;
-  int* kx = reinterpret_cast<int*>(sm + 2 * w + c);   // the masks, staged
+  double* rr = sm;                      // [NV][w]
+  double* zk = sm + NV * w;             // [NV][w]
+  double* yv = sm + 2 * NV * w;         // [NV][c]
+  double* jy = yv + NV * c;             // [NV][n]
+  int* kx = reinterpret_cast<int*>(jy + NV * n);   // the masks, staged
   int* ys = kx + w;
   int* kl = ys + c;    // known x, compacted (n)
   int* yl1 = kl + n;   // rows with y known, compacted (c)
@@ -466,57 +486,112 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
   const double* rho = Rd.rho + b * c;
   for (int j = t; j < w; j += NT) kx[j] = Rd.kx[b * w + j];
   for (int k = t; k < c; k += NT) ys[k] = Rd.yst[b * c + k];
-  red_rr(d, mp, in, b, trans, r, rr, zk);
+#pragma unroll
+  for (int k = 0; k < NV; ++k) red_rr(d, mp, in, b, tr[k], r[k], rr + k * w, zk + k * w);
   __syncthreads();
-  for (int k = t; k < c; k += NT) yv[k] = ys[k] == 1 ? -rr[mp.slack_of_row[k]] : 0.0;
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+    for (int q = t; q < c; q += NT) yv[k * c + q] = ys[q] == 1 ? -rr[k * w + mp.slack_of_row[q]] : 0.0;
   wave_compact(n, [&](int j) { return kx[j] >= 0; }, kl, cnt);
-  wave_compact(c, [&](int k) { return ys[k] == 1; }, yl1, cnt + 1);
+  wave_compact(c, [&](int q) { return ys[q] == 1; }, yl1, cnt + 1);
   __syncthreads();
   const int nkx = cnt[0], nky = cnt[1];
   const double* H = in.Hxx + b * n * n;
   const double* J = in.Jx + b * c * n;
+  {   // jy_i = Σ over the rows q with y known of J[q][i]·y_q (column i of J: contiguous)
+    const int g = t >> 4, gl = t & 15;
+    for (int i = g; i < n; i += NT / 16) {
+      if (kx[i] >= 0) continue;   // group-uniform
+      double acc[NV];
+#pragma unroll
+      for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+      for (int q = gl; q < nky; q += 16) {
+        const int row = yl1[q];
+        const double jq = J[(size_t)i * c + row];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = fma(jq, yv[k * c + row], acc[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+#pragma unroll
+        for (int m = 8; m >= 1; m >>= 1) acc[k] += __shfl_xor(acc[k], m);
+        if (gl == 0) jy[k * n + i] = acc[k];
+      }
+    }
+  }
+  __syncthreads();
   // W for M, Wᵀ for Mᵀ — column-major H read with the lanes along i whenever
   // H is exactly symmetric (meta.sym: the two coincide); only the known
   // columns are visited (the compacted lists: no per-column branch, the
   // loads of several columns in flight)
-  const bool hcol = !trans || meta[b].sym;
+  const bool sym = meta[b].sym;
   for (int i = t; i < nmax; i += NT) {
-    double v = 0.0;
+    double v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = 0.0;
     if (i < n) {
       if (kx[i] >= 0) {
-        v = zk[i];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = zk[k * w + i];
       } else {
-        v = rr[i];
-        if (hcol) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = rr[k * w + i];
+        if (sym || (NV == 1 && !tr[0])) {   // every vector's W by columns
 #pragma unroll 4
-          for (int q = 0; q < nkx; ++q) v -= H[(size_t)kl[q] * n + i] * zk[kl[q]];
+          for (int q = 0; q < nkx; ++q) {
+            const int col = kl[q];
+            const double hq = H[(size_t)col * n + i];
+#pragma unroll
+            for (int k = 0; k < NV; ++k) v[k] -= hq * zk[k * w + col];
+          }
         } else {
+#pragma unroll
+          for (int k = 0; k < NV; ++k) {
+            if (!tr[k]) {
 #pragma unroll 4
-          for (int q = 0; q < nkx; ++q) v -= H[(size_t)i * n + kl[q]] * zk[kl[q]];
+              for (int q = 0; q < nkx; ++q) v[k] -= H[(size_t)kl[q] * n + i] * zk[k * w + kl[q]];
+            } else {
+#pragma unroll 4
+              for (int q = 0; q < nkx; ++q) v[k] -= H[(size_t)i * n + kl[q]] * zk[k * w + kl[q]];
+            }
+          }
         }
-        for (int q = 0; q < nky; ++q) v -= J[(size_t)i * c + yl1[q]] * yv[yl1[q]];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] -= jy[k * n + i];
       }
     } else if (i < N) {
-      const int k = i - n;
-      if (ys[k] == 1) {
-        v = yv[k];
+      const int row = i - n;
+      if (ys[row] == 1) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = yv[k * c + row];
       } else {
-        v = r[w + k];
-        const int s = mp.slack_of_row[k];
-        if (s >= 0 && kx[s] >= 0) v += zk[s];
-        if (ys[k] == 2) v += rho[k] * rr[s];
+        const int s = mp.slack_of_row[row];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          v[k] = r[k][w + row];
+          if (s >= 0 && kx[s] >= 0) v[k] += zk[k * w + s];
+          if (ys[row] == 2) v[k] += rho[row] * rr[k * w + s];
+        }
 #pragma unroll 4
-        for (int q = 0; q < nkx; ++q) v -= J[(size_t)kl[q] * c + k] * zk[kl[q]];
+        for (int q = 0; q < nkx; ++q) {
+          const int col = kl[q];
+          const double jq = J[(size_t)col * c + row];
+#pragma unroll
+          for (int k = 0; k < NV; ++k) v[k] -= jq * zk[k * w + col];
+        }
       }
     }
-    o[i] = v;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) o[k][i] = v[k];
   }
 }
 
 // The reduced route's solution of R (x, stride nmax) → the full one of M /
-// Mᵀ (rows); full-route problems copy.  Grid (B, k) as above.  Dynamic LDS:
-// rr (num_w), known z (num_w), z over w (num_w), y (c); the masks and the
-// compacted active primal bounds (ints).
+// Mᵀ (rows); full-route problems copy.  Grid (B, k) as above (NV = 2: the
+// forward / reverse pair, H and J read once for both).  Dynamic LDS per
+// vector: rr (num_w), known z (num_w), z over w (num_w), y (c); then the masks
+// and the compacted active primal bounds (ints).
+template <int NV>
 __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap mp, NLPIn in, NLPRed Rd,
                                                              const int32_t* __restrict__ shift, int trans,
                                                              const double* __restrict__ rfull,
@@ -524,52 +599,79 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
                                                              double* __restrict__ zfull, int nmax,
                                                              const QPMeta* __restrict__ meta) {
   extern __shared__ double sm[];
-  const size_t b = blockIdx.x, off = ((size_t)blockIdx.y * gridDim.x + b) * nmax;
-  const double* r = rfull + off;
-  const double* xr = xred + off;
-  double* z = zfull + off;
+  const size_t b = blockIdx.x, B = gridDim.x;
+  const double* r[NV];
+  const double* xr[NV];
+  double* z[NV];
+  int tr[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const size_t off = ((NV == 2 ? (size_t)k : (size_t)blockIdx.y) * B + b) * nmax;
+    r[k] = rfull + off;
+    xr[k] = xred + off;
+    z[k] = zfull + off;
+    tr[k] = NV == 2 ? k : trans;
+  }
   const int t = threadIdx.x;
   if (!red_use(Rd, shift, (int)b)) {
-    for (int i = t; i < nmax; i += NT) z[i] = xr[i];
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+      for (int i = t; i < nmax; i += NT) z[k][i] = xr[k][i];
     return;
   }
   const int n = d.n, c = d.c, w = d.num_w;
-  double *rr = sm, *zk = sm + w, *zw = sm + 2 * w, *yl = sm + 3 * w;
-  int* kx = reinterpret_cast<int*>(sm + 3 * w + c);   // the masks, staged
+  double* rr = sm;                  // [NV][w]
+  double* zk = sm + NV * w;         // [NV][w]
+  double* zw = sm + 2 * NV * w;     // [NV][w]
+  double* yl = sm + 3 * NV * w;     // [NV][c]
+  int* kx = reinterpret_cast<int*>(yl + NV * c);   // the masks, staged
   int* ys = kx + w;
   int* al = ys + c;    // primal variables fixed by an active bound, compacted (n)
   int* cnt = al + n;
   for (int j = t; j < w; j += NT) kx[j] = Rd.kx[b * w + j];
-  for (int k = t; k < c; k += NT) ys[k] = Rd.yst[b * c + k];
+  for (int q = t; q < c; q += NT) ys[q] = Rd.yst[b * c + q];
   const double* rho = Rd.rho + b * c;
   const double* dl = Rd.delta + b * w;
   const double* H = in.Hxx + b * n * n;
   const double* J = in.Jx + b * c * n;
   // row j of W (Wᵀ for Mᵀ) contiguous when H is exactly symmetric
-  const bool hrow = trans || meta[b].sym;
-  red_rr(d, mp, in, b, trans, r, rr, zk);
-  for (int i = t; i < n; i += NT) zw[i] = xr[i];
-  for (int k = t; k < c; k += NT) {
-    yl[k] = xr[n + k];
-    z[w + k] = xr[n + k];
+  const bool sym = meta[b].sym;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    red_rr(d, mp, in, b, tr[k], r[k], rr + k * w, zk + k * w);
+    for (int i = t; i < n; i += NT) zw[k * w + i] = xr[k][i];
+    for (int q = t; q < c; q += NT) {
+      yl[k * c + q] = xr[k][n + q];
+      z[k][w + q] = xr[k][n + q];
+    }
   }
   __syncthreads();
   wave_compact(n, [&](int j) { return kx[j] >= 0; }, al, cnt);   // wave 0
   for (int s = n + t; s < w; s += NT) {   // slacks
-    const int k = mp.row_of_slack[s - n];
-    double v;
+    const int row = mp.row_of_slack[s - n];
+    double v[NV];
     if (kx[s] >= 0) {
-      v = zk[s];
-    } else if (ys[k] == 1) {
-      v = -r[w + k];
-      for (int j = 0; j < n; ++j) v += J[(size_t)j * c + k] * zw[j];
+#pragma unroll
+      for (int k = 0; k < NV; ++k) v[k] = zk[k * w + s];
+    } else if (ys[row] == 1) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) v[k] = -r[k][w + row];
+      for (int j = 0; j < n; ++j) {
+        const double jv = J[(size_t)j * c + row];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] += jv * zw[k * w + j];
+      }
     } else {
-      v = (rr[s] + yl[k]) * rho[k];
+#pragma unroll
+      for (int k = 0; k < NV; ++k) v[k] = (rr[k * w + s] + yl[k * c + row]) * rho[row];
     }
-    zw[s] = v;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) zw[k * w + s] = v[k];
   }
   __syncthreads();
-  for (int j = t; j < w; j += NT) z[j] = zw[j];
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+    for (int j = t; j < w; j += NT) z[k][j] = zw[k * w + j];
   // the bound rows' unknowns (lower block then upper: row lo0 + q for bound q)
   const int lo0 = w + c;
   for (int q = t; q < d.nlo + d.nup; q += NT) {
@@ -587,12 +689,15 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
       V = nlp_VU(d, mp, in, b, j);
     }
     const double cf = low ? -1.0 : 1.0;
-    const double a = trans ? cf : V, bc = trans ? V : cf;
-    if (dd != 0.0)
-      z[lo0 + q] = (r[lo0 + q] - a * zw[j]) / dd;
-    else if (j >= n)   // slack row: −y_k + b·z_ν = r̃_t
-      z[lo0 + q] = (rr[j] + yl[mp.row_of_slack[j - n]]) / bc;
-    // an active bound on a primal variable: below
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const double a = tr[k] ? cf : V, bc = tr[k] ? V : cf;
+      if (dd != 0.0)
+        z[k][lo0 + q] = (r[k][lo0 + q] - a * zw[k * w + j]) / dd;
+      else if (j >= n)   // slack row: −y_k + b·z_ν = r̃_t
+        z[k][lo0 + q] = (rr[k * w + j] + yl[k * c + mp.row_of_slack[j - n]]) / bc;
+      // an active bound on a primal variable: below
+    }
   }
   // row j of an active primal bound q = kx[j]:
   //   (W x)_j + δ_j x_j + (Jᵀ y)_j + b·z_ν = r̃_j,
@@ -601,16 +706,42 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
   for (int e = g; e < na; e += NT / 16) {
     const int j = al[e], q = kx[j];
     const bool low = q < d.nlo;
-    double acc = 0.0;
-#pragma unroll 4
-    for (int jj = gl; jj < n; jj += 16) acc = fma(hrow ? H[(size_t)j * n + jj] : H[(size_t)jj * n + j], zw[jj], acc);
-#pragma unroll 4
-    for (int k = gl; k < c; k += 16) acc = fma(J[(size_t)j * c + k], yl[k], acc);
+    double acc[NV];
 #pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+    if (sym || (NV == 1 && tr[0])) {   // every vector's row j of W contiguous
+#pragma unroll 4
+      for (int jj = gl; jj < n; jj += 16) {
+        const double hv = H[(size_t)j * n + jj];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = fma(hv, zw[k * w + jj], acc[k]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const bool hrow = tr[k];
+#pragma unroll 4
+        for (int jj = gl; jj < n; jj += 16)
+          acc[k] = fma(hrow ? H[(size_t)j * n + jj] : H[(size_t)jj * n + j], zw[k * w + jj], acc[k]);
+      }
+    }
+#pragma unroll 4
+    for (int kk = gl; kk < c; kk += 16) {
+      const double jv = J[(size_t)j * c + kk];
+#pragma unroll
+      for (int k = 0; k < NV; ++k) acc[k] = fma(jv, yl[k * c + kk], acc[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) acc[k] += __shfl_xor(acc[k], o);
+    }
     if (gl == 0) {
-      const double bc = trans ? (low ? nlp_VL(d, mp, in, b, j) : nlp_VU(d, mp, in, b, j)) : (low ? -1.0 : 1.0);
-      z[lo0 + q] = (rr[j] - dl[j] * zw[j] - acc) / bc;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const double bc = tr[k] ? (low ? nlp_VL(d, mp, in, b, j) : nlp_VU(d, mp, in, b, j)) : (low ? -1.0 : 1.0);
+        z[k][lo0 + q] = (rr[k * w + j] - dl[j] * zw[k * w + j] - acc[k]) / bc;
+      }
     }
   }
 }
@@ -682,20 +813,58 @@ void assemble(Handle& h, const int32_t* plist, int count) {
 }
 
 // full right-hand sides (k per problem) → the system each problem factorised
+// dynamic LDS above the default 64 KB: opt in (gfx950: 160 KB per workgroup)
+template <class KF>
+static bool red_lds_ok(KF kf, size_t lds) {
+  if (lds > 160 * 1024) return false;
+  if (lds > 64 * 1024)
+    DOPT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kf), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds));
+  return true;
+}
+
+// k right-hand sides through M (trans 0) / Mᵀ (1); k = 0: the forward /
+// reverse pair (rfull, rred: the forward vector, the reverse one B·nmax on)
 void red_rhs(Handle& h, int trans, int k, const double* rfull, double* rred) {
-  const size_t w = h.nlp_num_w, c = h.m;
-  const size_t lds = (2 * w + c) * sizeof(double) + (w + c + h.n + c + 2) * sizeof(int);
-  hipLaunchKernelGGL(nlp_red_rhs_kernel, dim3((unsigned)h.batch, (unsigned)k), dim3(NT), lds, h.stream, dims(h),
-                     map_of(h), inputs(h), red_of(h), h.nlp_shift.as<int32_t>(), trans, rfull, rred, h.nmax,
-                     h.meta.as<QPMeta>());
+  const size_t w = h.nlp_num_w, c = h.m, n = h.n;
+  const size_t nv = k ? 1 : 2;
+  const size_t lds = nv * (2 * w + c + n) * sizeof(double) + (w + c + n + c + 2) * sizeof(int);
+  if (!k && !red_lds_ok(nlp_red_rhs_kernel<2>, lds)) {   // the pair does not fit: one direction at a time
+    const size_t blk = (size_t)h.batch * h.nmax;
+    red_rhs(h, 0, 1, rfull, rred);
+    red_rhs(h, 1, 1, rfull + blk, rred + blk);
+    return;
+  }
+  if (k && !red_lds_ok(nlp_red_rhs_kernel<1>, lds)) throw Error(-1, "NLP reduced route: problem too large");
+  if (k)
+    hipLaunchKernelGGL(nlp_red_rhs_kernel<1>, dim3((unsigned)h.batch, (unsigned)k), dim3(NT), lds, h.stream, dims(h),
+                       map_of(h), inputs(h), red_of(h), h.nlp_shift.as<int32_t>(), trans, rfull, rred, h.nmax,
+                       h.meta.as<QPMeta>());
+  else
+    hipLaunchKernelGGL(nlp_red_rhs_kernel<2>, dim3((unsigned)h.batch), dim3(NT), lds, h.stream, dims(h), map_of(h),
+                       inputs(h), red_of(h), h.nlp_shift.as<int32_t>(), 0, rfull, rred, h.nmax, h.meta.as<QPMeta>());
   DOPT_CHECK_HIP(hipGetLastError());
 }
+// k = 0: the forward / reverse pair, as red_rhs
 void red_recover(Handle& h, int trans, int k, const double* rfull, const double* xred, double* zfull) {
   const size_t w = h.nlp_num_w, c = h.m;
-  const size_t lds = (3 * w + c) * sizeof(double) + (w + c + h.n + 1) * sizeof(int);
-  hipLaunchKernelGGL(nlp_red_recover_kernel, dim3((unsigned)h.batch, (unsigned)k), dim3(NT), lds, h.stream,
-                     dims(h), map_of(h), inputs(h), red_of(h), h.nlp_shift.as<int32_t>(), trans, rfull, xred, zfull,
-                     h.nmax, h.meta.as<QPMeta>());
+  const size_t nv = k ? 1 : 2;
+  const size_t lds = nv * (3 * w + c) * sizeof(double) + (w + c + h.n + 1) * sizeof(int);
+  if (!k && !red_lds_ok(nlp_red_recover_kernel<2>, lds)) {   // the pair does not fit: one direction at a time
+    const size_t blk = (size_t)h.batch * h.nmax;
+    red_recover(h, 0, 1, rfull, xred, zfull);
+    red_recover(h, 1, 1, rfull + blk, xred + blk, zfull + blk);
+    return;
+  }
+  if (k && !red_lds_ok(nlp_red_recover_kernel<1>, lds)) throw Error(-1, "NLP reduced route: problem too large");
+  if (k)
+    hipLaunchKernelGGL(nlp_red_recover_kernel<1>, dim3((unsigned)h.batch, (unsigned)k), dim3(NT), lds, h.stream,
+                       dims(h), map_of(h), inputs(h), red_of(h), h.nlp_shift.as<int32_t>(), trans, rfull, xred, zfull,
+                       h.nmax, h.meta.as<QPMeta>());
+  else
+    hipLaunchKernelGGL(nlp_red_recover_kernel<2>, dim3((unsigned)h.batch), dim3(NT), lds, h.stream, dims(h),
+                       map_of(h), inputs(h), red_of(h), h.nlp_shift.as<int32_t>(), 0, rfull, xred, zfull, h.nmax,
+                       h.meta.as<QPMeta>());
   DOPT_CHECK_HIP(hipGetLastError());
 }
 bool reduced_on(const Handle& h) { return !h.nlp_kkt && h.nlp_reduce; }
@@ -932,20 +1101,14 @@ void nlp_forward_reverse(Handle& h, const double* dp, const double* dxs, const d
     DOPT_CHECK_HIP(hipGetLastError());
     hipLaunchKernelGGL(nlp_rev_rhs_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), dxs, dds, h.nmax, rr);
     DOPT_CHECK_HIP(hipGetLastError());
-    if (red) {
-      red_rhs(h, 0, 1, rf, t1);
-      red_rhs(h, 1, 1, rr, t1 + blk);
-    }
+    if (red) red_rhs(h, 0, 0, rf, t1);   // the pair: rr = rf + blk → t1 + blk
   }
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     qp_blocked_solve_pair(h, dense_dinv(h), red ? t1 : rf, red ? t1 + blk : rr, red ? t2 : x, red ? t2 + blk : u,
                           LU_SEL_ALL);
   }
-  if (red) {
-    red_recover(h, 0, 1, rf, t2, x);
-    red_recover(h, 1, 1, rr, t2 + blk, u);
-  }
+  if (red) red_recover(h, 0, 0, rf, t2, x);   // the pair (rr, t2 + blk → u = x + blk)
   PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
   hipLaunchKernelGGL(nlp_fwd_out_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), x, h.nmax,
                      h.nlp_shift.as<int32_t>(), dx, ddual);

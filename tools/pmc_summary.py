@@ -42,14 +42,19 @@ QP_GROUPS = {"qp_assemble": ("qp_prep_kernel", "qp_asm_tile_kernel", "qp_qsym_ke
                           "blu_symsolve_kernel"),
              "qp_output": ("qp_output_kernel",)}
 QP_STEP = "qp_prep_kernel"
-# NLP back-end (bench config 6): the step is counted by the assembly; its LU
-# is the partial-pivoting blocked LU, its solves the blocked solve kernels
-NLP_GROUPS = {"qp_assemble": ("nlp_assemble_kernel", "nlp_red_prep_kernel"),
+# NLP back-end (bench config 6): the step is counted by its assembly launch
+# (nlp_red_prep_kernel on the reduced route, nlp_assemble_kernel on the full
+# one — the first of the two found); the LU is the left-looking no-pivot LU
+# (or the partial-pivoting blocked LU), the solves the P-symmetric pair /
+# single-direction sweeps (with the blocked solve kernels for pivoted problems)
+NLP_GROUPS = {"qp_assemble": ("nlp_assemble_kernel", "nlp_red_prep_kernel", "qp_qsym_kernel", "nlp_pivot_check_kernel"),
               "qp_lu": ("nlu_diag_kernel", "nlu_trsm_kernel", "nlu_cross_kernel", "nlu_update2_kernel",
                         "nlu_ldiag_kernel", "nlu_lcol_kernel"),
               "qp_lu_pivot": ("blu_panel_kernel", "blu_update_kernel"),
-              "qp_solve": ("blu_solve_kernel", "blu_solve_rows_kernel")}
-NLP_STEP = "nlp_assemble_kernel"
+              "qp_rhs": ("nlp_fwd_rhs_kernel", "nlp_rev_rhs_kernel", "nlp_red_rhs_kernel"),
+              "qp_solve": ("blu_solve_kernel", "blu_solve_rows_kernel", "blu_symsolve_kernel", "blu_sym2_kernel"),
+              "qp_output": ("nlp_fwd_out_kernel", "nlp_rev_out_kernel", "nlp_red_recover_kernel")}
+NLP_STEP = ("nlp_assemble_kernel", "nlp_red_prep_kernel")
 # split-path LSQR: every conic_split_* dispatch belongs to the LSQR call opened
 # by the preceding conic_split_init_kernel; reported per LSQR call under the
 # bench's phase name "conic_lsqr" (key "conic_lsqr_split")
@@ -84,19 +89,21 @@ def per_launch(d, counter):
                         calls.add(row.get("Dispatch_Id"))
     if calls:
         res["conic_lsqr_split"] = tot / len(calls)
-    for groups, step in ((QP_GROUPS, QP_STEP), (NLP_GROUPS, NLP_STEP)):
-        gtot, steps = defaultdict(float), set()
+    for groups, step in ((QP_GROUPS, (QP_STEP,)), (NLP_GROUPS, NLP_STEP)):
+        gtot, steps = defaultdict(float), defaultdict(set)
         for f in files:
             with open(f) as fh:
                 for row in csv.DictReader(fh):
                     if row.get("Counter_Name") != counter:
                         continue
                     kn = row.get("Kernel_Name", "")
-                    if step in kn:
-                        steps.add(row.get("Dispatch_Id"))
+                    for st in step:
+                        if st in kn:
+                            steps[st].add(row.get("Dispatch_Id"))
                     for ph, frags in groups.items():
                         if any(fr in kn for fr in frags):
                             gtot[ph] += float(row["Counter_Value"])
+        steps = next((steps[st] for st in step if steps[st]), None)   # the first step kernel found
         if steps:
             for ph, v in gtot.items():
                 res[ph] = v / len(steps)
