@@ -221,6 +221,7 @@ struct Handle {
   DevBuf nlp_shift;                // per problem: inertia corrections applied (int32); −1: failed
   DevBuf nlp_scale;                // per problem × assembly row block: max |M| (the pivot test's scale)
   std::vector<int32_t> nlp_corr;   // host copy of nlp_shift after the factorisation
+  bool nlp_pivoted = true;         // some problem's factor is partial-pivoting (rejected, corrected, LU mode 0)
   // reduced KKT route (nlp.hip, structured mode): the bound and slack rows
   // eliminated exactly, R = [H + diag(δ), Jᵀ; J, −diag(ρ)] over [x; y] factorised
   // instead of M; env DOPT_NLP_REDUCE=0 keeps the full sIpopt M

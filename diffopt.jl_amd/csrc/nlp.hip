@@ -105,7 +105,21 @@ __global__ __launch_bounds__(NT) void nlp_red_prep_kernel(NLPDims d, NLPMap mp, 
   }
   // max |R| without H (J, δ, ρ, the identity rows; qp_qsym_kernel gives max |H|):
   // the growth bound of the left-looking LU, which reads R from the inputs
-  for (size_t e = t; e < (size_t)d.c * d.n; e += NT) mmax = fmax(mmax, fabs(in.Jx[b * d.c * d.n + e]));
+  {   // J in 16-byte loads when the problem's slice is 16-byte aligned, several in flight
+    const double* Jb = in.Jx + b * d.c * d.n;
+    const int cn = d.c * d.n;
+    if ((cn & 1) == 0 && (reinterpret_cast<uintptr_t>(Jb) & 15) == 0) {
+      const double2* J2 = reinterpret_cast<const double2*>(Jb);
+#pragma unroll 4
+      for (int e = t; e < cn / 2; e += NT) {
+        const double2 v = J2[e];
+        mmax = fmax(mmax, fmax(fabs(v.x), fabs(v.y)));
+      }
+    } else {
+#pragma unroll 4
+      for (int e = t; e < cn; e += NT) mmax = fmax(mmax, fabs(Jb[e]));
+    }
+  }
   double amax = fmax(1.0, mmax);   // (mmax so far: |J|, the bound rows, the ±1 entries)
   for (int j = t; j < d.n; j += NT) amax = fmax(amax, fabs(delta[j]));
   for (int k = t; k < d.c; k += NT) amax = fmax(amax, fabs(R.rho[b * d.c + k]));
@@ -290,9 +304,11 @@ __global__ __launch_bounds__(NT) void nlp_fwd_rhs_kernel(NLPDims d, NLPIn in, co
     double acc = 0.0;
     if (r < d.n) {
       const double* Hb = in.Hxp + b * d.n * d.P;
+#pragma unroll 4
       for (int j = 0; j < d.P; ++j) acc = fma(Hb[(size_t)j * d.n + r], p[j], acc);
     } else if (r >= d.num_w && r < d.num_w + d.c) {
       const double* Jb = in.Jp + b * d.c * d.P;
+#pragma unroll 4
       for (int j = 0; j < d.P; ++j) acc = fma(Jb[(size_t)j * d.c + (r - d.num_w)], p[j], acc);
     }
     rhs[b * nmax + r] = acc;
@@ -356,13 +372,20 @@ __global__ __launch_bounds__(NT) void nlp_rev_out_kernel(NLPDims d, NLPIn in, co
   const size_t b = blockIdx.x;
   const bool ok = shift[b] >= 0;
   const double* ub = u + b * nmax;
-  for (int j = threadIdx.x; j < d.P; j += NT) {
+  // 8 lanes per column j (contiguous reads of Hxp / Jp's column), 32 columns
+  // at a time
+  const int g = threadIdx.x >> 3, gl = threadIdx.x & 7;
+  for (int j = g; j < d.P; j += NT / 8) {
     double acc = 0.0;
     const double* Hc = in.Hxp + (b * d.P + j) * d.n;   // column j of Hxp
     const double* Jc = in.Jp + (b * d.P + j) * d.c;    // column j of Jp
-    for (int i = 0; i < d.n; ++i) acc = fma(Hc[i], ub[i], acc);
-    for (int k = 0; k < d.c; ++k) acc = fma(Jc[k], ub[d.num_w + k], acc);
-    dp[b * d.P + j] = ok ? -acc : 0.0;
+#pragma unroll 4
+    for (int i = gl; i < d.n; i += 8) acc = fma(Hc[i], ub[i], acc);
+#pragma unroll 4
+    for (int k = gl; k < d.c; k += 8) acc = fma(Jc[k], ub[d.num_w + k], acc);
+#pragma unroll
+    for (int o = 4; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    if (gl == 0) dp[b * d.P + j] = ok ? -acc : 0.0;
   }
 }
 
@@ -537,7 +560,7 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
 #pragma unroll
         for (int k = 0; k < NV; ++k) v[k] = rr[k * w + i];
         if (sym || (NV == 1 && !tr[0])) {   // every vector's W by columns
-#pragma unroll 4
+#pragma unroll 8
           for (int q = 0; q < nkx; ++q) {
             const int col = kl[q];
             const double hq = H[(size_t)col * n + i];
@@ -548,10 +571,10 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
 #pragma unroll
           for (int k = 0; k < NV; ++k) {
             if (!tr[k]) {
-#pragma unroll 4
+#pragma unroll 8
               for (int q = 0; q < nkx; ++q) v[k] -= H[(size_t)kl[q] * n + i] * zk[k * w + kl[q]];
             } else {
-#pragma unroll 4
+#pragma unroll 8
               for (int q = 0; q < nkx; ++q) v[k] -= H[(size_t)i * n + kl[q]] * zk[k * w + kl[q]];
             }
           }
@@ -572,7 +595,7 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
           if (s >= 0 && kx[s] >= 0) v[k] += zk[k * w + s];
           if (ys[row] == 2) v[k] += rho[row] * rr[k * w + s];
         }
-#pragma unroll 4
+#pragma unroll 8
         for (int q = 0; q < nkx; ++q) {
           const int col = kl[q];
           const double jq = J[(size_t)col * c + row];
@@ -656,6 +679,7 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
     } else if (ys[row] == 1) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) v[k] = -r[k][w + row];
+#pragma unroll 8
       for (int j = 0; j < n; ++j) {
         const double jv = J[(size_t)j * c + row];
 #pragma unroll
@@ -710,7 +734,7 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
 #pragma unroll
     for (int k = 0; k < NV; ++k) acc[k] = 0.0;
     if (sym || (NV == 1 && tr[0])) {   // every vector's row j of W contiguous
-#pragma unroll 4
+#pragma unroll 8
       for (int jj = gl; jj < n; jj += 16) {
         const double hv = H[(size_t)j * n + jj];
 #pragma unroll
@@ -720,12 +744,12 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
         const bool hrow = tr[k];
-#pragma unroll 4
+#pragma unroll 8
         for (int jj = gl; jj < n; jj += 16)
           acc[k] = fma(hrow ? H[(size_t)j * n + jj] : H[(size_t)jj * n + j], zw[k * w + jj], acc[k]);
       }
     }
-#pragma unroll 4
+#pragma unroll 8
     for (int kk = gl; kk < c; kk += 16) {
       const double jv = J[(size_t)j * c + kk];
 #pragma unroll
@@ -1028,8 +1052,13 @@ void nlp_factor(Handle& h) {
   DOPT_CHECK_HIP(hipMemcpyAsync(h.nlp_shift.p, shift.data(), (size_t)B * sizeof(int32_t), hipMemcpyHostToDevice,
                                 h.stream));
   DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+  // every factor no-pivot (none rejected, corrected or failed): the solves
+  // skip the partial-pivoting kernels' launches
+  h.nlp_pivoted = h.n_pivot != 0 || std::any_of(h.nlp_corr.begin(), h.nlp_corr.end(), [](int32_t k) { return k != 0; });
   h.nfactored = true;
 }
+
+static int solve_sel(const Handle& h) { return h.nlp_pivoted ? LU_SEL_ALL : LU_SEL_NOPIV; }
 
 void nlp_forward(Handle& h, const double* dp, double* dx, double* ddual) {
   if (!h.nfactored) nlp_factor(h);
@@ -1046,7 +1075,7 @@ void nlp_forward(Handle& h, const double* dp, double* dx, double* ddual) {
   }
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
-    qp_blocked_solve(h, dense_dinv(h), 0, red ? red_t1(h, 1) : rhs, red ? red_t2(h, 1) : x, LU_SEL_ALL);
+    qp_blocked_solve(h, dense_dinv(h), 0, red ? red_t1(h, 1) : rhs, red ? red_t2(h, 1) : x, solve_sel(h));
   }
   if (red) red_recover(h, 0, 1, rhs, red_t2(h, 1), x);
   PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
@@ -1070,7 +1099,7 @@ void nlp_reverse(Handle& h, const double* dx, const double* ddual, double* dp) {
   }
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
-    qp_blocked_solve(h, dense_dinv(h), 1, red ? red_t1(h, 1) : rhs, red ? red_t2(h, 1) : u, LU_SEL_ALL);
+    qp_blocked_solve(h, dense_dinv(h), 1, red ? red_t1(h, 1) : rhs, red ? red_t2(h, 1) : u, solve_sel(h));
   }
   if (red) red_recover(h, 1, 1, rhs, red_t2(h, 1), u);
   PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
@@ -1106,7 +1135,7 @@ void nlp_forward_reverse(Handle& h, const double* dp, const double* dxs, const d
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     qp_blocked_solve_pair(h, dense_dinv(h), red ? t1 : rf, red ? t1 + blk : rr, red ? t2 : x, red ? t2 + blk : u,
-                          LU_SEL_ALL);
+                          solve_sel(h));
   }
   if (red) red_recover(h, 0, 0, rf, t2, x);   // the pair (rr, t2 + blk → u = x + blk)
   PhaseTimer pt(h, DOPT_PHASE_QP_OUTPUT);
@@ -1122,7 +1151,7 @@ void nlp_forward_reverse(Handle& h, const double* dp, const double* dxs, const d
 // k right-hand sides per problem (seed-major, stride B·nmax) through the
 // blocked factors, one multi-RHS launch
 static void solve_multi(Handle& h, int trans, int k, double* rk, double* xk) {
-  qp_blocked_solve_multi(h, dense_dinv(h), trans, k, rk, xk, LU_SEL_ALL);
+  qp_blocked_solve_multi(h, dense_dinv(h), trans, k, rk, xk, solve_sel(h));
 }
 
 void nlp_jacobian(Handle& h, double* ds) {

@@ -872,6 +872,32 @@ __global__ __launch_bounds__(PT) void blu_solve2_kernel(const double* __restrict
                          y, ps, part, swept ? 1 : 0);
 }
 
+// The diagonal blocks' L_kk⁻¹ (dinv's first BNB² entries) for the P-symmetric
+// sweeps: loaded one block ahead into registers (BNB²/TPB per thread, one
+// round trip hidden behind the current block's sweep), staged into LDS with a
+// padded row (DKS_LD: the forward GEMV's row reads and the backward's column
+// reads both conflict-free) — instead of each GEMV lane walking dinv in
+// global memory (4 dependent round trips per block).
+constexpr int DKS_LD = BNB + 1;
+template <int TPB>
+struct DinvPrefetch {
+  static constexpr int DPT = BNB * BNB / TPB;
+  static_assert(DPT * TPB == BNB * BNB, "workgroup size divides BNB²");
+  double r[DPT];
+  __device__ __forceinline__ void load(const double* Dbase, int bk, int t) {
+    const double* Dk = Dbase + (size_t)bk * BDINV;
+#pragma unroll
+    for (int u = 0; u < DPT; ++u) r[u] = Dk[t + u * TPB];
+  }
+  __device__ __forceinline__ void stage(double* dks, int t) const {
+#pragma unroll
+    for (int u = 0; u < DPT; ++u) {
+      const int e = t + u * TPB;
+      dks[(e / BNB) * DKS_LD + (e % BNB)] = r[u];
+    }
+  }
+};
+
 // The P-symmetric fused sweeps (solve_sym2_body's algebra) as their own lean
 // launch: one workgroup per problem, the column slices read in two halves of
 // 16 rows (the first half in flight across the diagonal solve).  At 96 VGPRs
@@ -885,7 +911,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
                                                       const double* __restrict__ w_rev,
                                                       const double* __restrict__ w_fwd, double* __restrict__ x_rev,
                                                       double* __restrict__ x_fwd, SymSweep sym) {
-  __shared__ double v[SOLVE_STATIC], y[SOLVE_STATIC], part[BNB], part2[BNB];
+  __shared__ double v[SOLVE_STATIC], y[SOLVE_STATIC], part[BNB], part2[BNB], dks[BNB * DKS_LD];
   const int b = blockIdx.x;
   const QPMeta mm = meta[b];
   const int Np = blocked_np(mm);
@@ -902,8 +928,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
     v[i] = i < N ? rb[i] / udb[i] : 0.0;
     y[i] = i < N ? fb[i] : 0.0;
   }
-  __syncthreads();
   const int nblk = Np / BNB;
+  DinvPrefetch<TPB> dpf;
+  dpf.load(Dbase, nblk - 1, t);
+  dpf.stage(dks, t);
+  __syncthreads();
   for (int s = 0; s < nblk; ++s) {
     const int bk = nblk - 1 - s;
     const int i0 = bk * BNB;
@@ -916,12 +945,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
       for (int j = 0; j < RH; ++j) f[q][j] = Kb[(size_t)(i0 + j) * ld + ec];
     }
-    if (wv < 2 && lane < BNB) {   // wave 0: L_kk⁻ᵀ v_k, wave 1: L_kk⁻ᵀ y_k
-      const double* Dk = Dbase + (size_t)bk * BDINV;
+    if (bk > 0) dpf.load(Dbase, bk - 1, t);   // the next block's L_kk⁻¹, staged after the barrier
+    if (wv < 2 && lane < BNB) {   // wave 0: L_kk⁻ᵀ v_k, wave 1: L_kk⁻ᵀ y_k (L_kk⁻¹ from LDS)
       const double* vv = wv ? y : v;
       double acc = 0.0;
 #pragma unroll 8
-      for (int j = 0; j < BNB; ++j) acc = fma(Dk[lane + j * BNB], vv[i0 + j], acc);
+      for (int j = 0; j < BNB; ++j) acc = fma(dks[j * DKS_LD + lane], vv[i0 + j], acc);
       (wv ? part2 : part)[lane] = acc;
     }
     __syncthreads();
@@ -963,6 +992,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
         y[e] = a2[q];
       }
     }
+    if (bk > 0) dpf.stage(dks, t);   // this block's GEMV read dks before the barrier above
     __syncthreads();
   }
   double* xr = x_rev + (size_t)b * nmax;
@@ -989,7 +1019,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const QPMeta* __restrict__ meta, int trans, const double* __restrict__ rhs, double* __restrict__ xout,
     const double* __restrict__ rhs1, double* __restrict__ xout1, SymSweep sym) {
   static_assert(NV == 1 || NV == 2, "one or two directions");
-  __shared__ double v[NV][SOLVE_STATIC], part[NV][BNB];
+  __shared__ double v[NV][SOLVE_STATIC], part[NV][BNB], dks[BNB * DKS_LD];
   const int b = blockIdx.x;
   const QPMeta mm = meta[b];
   const int Np = blocked_np(mm);
@@ -1007,8 +1037,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const double* rb = (k ? rhs1 : rhs) + (size_t)b * nmax;
     for (int i = t; i < Np; i += TPB) v[k][i] = i < N ? (tr(k) ? rb[i] / psc(i) : rb[i]) : 0.0;
   }
-  __syncthreads();
   const int nblk = Np / BNB;
+  // L_kk⁻¹ of the block in flight in LDS (dks), the next one's loads in
+  // registers across the current block's sweep (staged after its GEMV's
+  // barrier): the forward sweep ends with the last block staged, which is the
+  // backward sweep's first
+  DinvPrefetch<TPB> dpf;
+  dpf.load(Dbase, 0, t);
+  dpf.stage(dks, t);
+  __syncthreads();
   // forward: L y = r (block k: y_k = L_kk⁻¹ v_k, then v_e −= L[e][k-block]·y_k
   // for e past it): row segments, 8 lanes per row × 4 doubles (one wave load
   // touches 8 rows' lines), RP rows per pass, up to SCH passes in flight
@@ -1032,12 +1069,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
       };
       if (npass > 0) load_chunk(0);
+      if (bk + 1 < nblk) dpf.load(Dbase, bk + 1, t);
       if (wv < NV && lane < BNB) {
-        const double* Dk = Dbase + (size_t)bk * BDINV + lane * BNB;   // row `lane` of L⁻¹
         const double* vv = v[wv];
         double acc = 0.0;
 #pragma unroll 8
-        for (int j = 0; j < BNB; ++j) acc = fma(Dk[j], vv[i0 + j], acc);
+        for (int j = 0; j < BNB; ++j) acc = fma(dks[lane * DKS_LD + j], vv[i0 + j], acc);   // row `lane` of L⁻¹
         part[wv][lane] = acc;
       }
       __syncthreads();
@@ -1063,6 +1100,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
           }
         }
       }
+      if (bk + 1 < nblk) dpf.stage(dks, t);
       __syncthreads();
     }
   }
@@ -1083,12 +1121,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
       for (int j = 0; j < RH; ++j) f[q][j] = Kb[(size_t)(i0 + j) * ld + ec];
     }
+    if (bk > 0) dpf.load(Dbase, bk - 1, t);
     if (wv < NV && lane < BNB) {
-      const double* Dk = Dbase + (size_t)bk * BDINV;
       const double* vv = v[wv];
       double acc = 0.0;
 #pragma unroll 8
-      for (int j = 0; j < BNB; ++j) acc = fma(Dk[lane + j * BNB], vv[i0 + j], acc);
+      for (int j = 0; j < BNB; ++j) acc = fma(dks[j * DKS_LD + lane], vv[i0 + j], acc);
       part[wv][lane] = acc;
     }
     __syncthreads();
@@ -1125,6 +1163,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
         for (int k = 0; k < NV; ++k) v[k][e] = a[k][q];
     }
+    if (bk > 0) dpf.stage(dks, t);
     __syncthreads();
   }
 #pragma unroll
@@ -1223,7 +1262,7 @@ void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rh
     if (h.sym_tpb == 256) {   // 256-thread workgroups, 2 / 4 / 6 entries per thread (as blu_sym2_kernel)
       if (ent <= 1) { DOPT_SYMSOLVE256(2, 4, 8); }
       else if (ent == 2) { DOPT_SYMSOLVE256(4, 4, 4); }
-      else { DOPT_SYMSOLVE256(6, 3, 4); }
+      else { DOPT_SYMSOLVE256(6, 4, 4); }
     } else if (ent <= 1) { DOPT_SYMSOLVE(1, 5); }
     else if (ent == 2) { DOPT_SYMSOLVE(2, 2); }
     else { DOPT_SYMSOLVE(3, 2); }
@@ -1275,7 +1314,7 @@ void qp_blocked_solve_pair(Handle& h, const double* dinv, const double* rhs0, co
     if (h.sym_tpb == 256) {
       if (ent <= 1) { DOPT_SYMPAIR(2, 4, 256, 8); }
       else if (ent == 2) { DOPT_SYMPAIR(4, 4, 256, 4); }
-      else { DOPT_SYMPAIR(6, 3, 256, 4); }
+      else { DOPT_SYMPAIR(6, 4, 256, 4); }
     } else if (ent <= 1) { DOPT_SYMPAIR(1, 5, PT, 16); }
     else if (ent == 2) { DOPT_SYMPAIR(2, 2, PT, 16); }
     else { DOPT_SYMPAIR(3, 2, PT, 16); }
@@ -1320,7 +1359,7 @@ void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, con
       hipLaunchKernelGGL((blu_sym2_kernel<2, 2>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, meta,
                          w_rev, w_fwd, x_rev, x_fwd, sym);
     else if (h.sym_tpb == 256)   // 256 threads × 6 entries (Np ≤ 1536), rows in groups of 4
-      hipLaunchKernelGGL((blu_sym2_kernel<6, 3, 256, 4>), dim3(B), dim3(256), 0, h.stream, K, h.ld, h.nmax, dinv,
+      hipLaunchKernelGGL((blu_sym2_kernel<6, 4, 256, 4>), dim3(B), dim3(256), 0, h.stream, K, h.ld, h.nmax, dinv,
                          dstride, meta, w_rev, w_fwd, x_rev, x_fwd, sym);
     else
       hipLaunchKernelGGL((blu_sym2_kernel<3, 2>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, meta,
