@@ -1017,12 +1017,14 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
     // the Q symmetry check's verdict: an asymmetric Q leaves the P-symmetric
     // route (partial pivoting); max |Q|, |A| joins max |K| for the growth
     // bound of this and every later launch
-    if (src.qflag[b]) {
-      if (t == 0) meta[b].lu = LU_REJECT;
-      return;
+    if (src.qflag) {   // null: no check ran (its buffers are device memory only)
+      if (src.qflag[b]) {
+        if (t == 0) meta[b].lu = LU_REJECT;
+        return;
+      }
+      amax = fmax(amax, src.qmax[b]);
+      if (t == 0) kamax[b] = amax;
     }
-    amax = fmax(amax, src.qmax[b]);
-    if (t == 0) kamax[b] = amax;
   }
   NLU_MARK_INIT;
   // the block → LDS (identity beyond Wv); all 16 loads in flight
@@ -1826,12 +1828,14 @@ __device__ __forceinline__ void ldiag_body(
   if (c0 == 0) {
     // the Q symmetry check's verdict (partial pivoting for an asymmetric Q),
     // max |Q|, |A| into the growth bound
-    if (src.qflag[b]) {
-      if (t == 0) meta[b].lu = LU_REJECT;
-      return;
+    if (src.qflag) {   // null: no check ran (its buffers are device memory only)
+      if (src.qflag[b]) {
+        if (t == 0) meta[b].lu = LU_REJECT;
+        return;
+      }
+      amax = fmax(amax, src.qmax[b]);
+      if (t == 0) kamax[b] = amax;
     }
-    amax = fmax(amax, src.qmax[b]);
-    if (t == 0) kamax[b] = amax;
   }
   // ---- the left-looking update of C(J, J) over k < J.  X = Σ_k L(J, k)·D_k·
   // L(J, k)ᵀ is symmetric: only its ten lower 16×16 tiles are formed (3, 3,
@@ -2397,10 +2401,9 @@ void qp_nopiv_factor(Handle& h, double* dinv, double* w0, double* w1) {
   src.kls = qp ? h.kls.as<double>() : &zero;
   src.A = qp && h.p ? h.A : &zero;
   // the check's results exist only when a prepare of the P-symmetric route ran
-  static const int32_t zflag = 0;
   const bool qchk = qp && h.qsy.p && h.n > 0;
-  src.qmax = qchk ? qsy_max(h) : &zero;
-  src.qflag = qchk ? qsy_flag(h) : &zflag;
+  src.qmax = qchk ? qsy_max(h) : nullptr;
+  src.qflag = qchk ? qsy_flag(h) : nullptr;
   src.n = h.n;
   src.m = h.m;
   src.p = h.p;
