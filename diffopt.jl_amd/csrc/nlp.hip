@@ -440,10 +440,11 @@ __device__ __forceinline__ void wave_compact(int len, F pred, int* out, int* cnt
   if (lane == 0) *cnt = base;
 }
 
+template <int TPB = NT>
 __device__ __forceinline__ void red_rr(const NLPDims& d, const NLPMap& mp, const NLPIn& in, size_t b, int trans,
                                        const double* r, double* rr, double* zk) {
   const int lo0 = d.num_w + d.c, up0 = lo0 + d.nlo;
-  for (int j = threadIdx.x; j < d.num_w; j += NT) {
+  for (int j = threadIdx.x; j < d.num_w; j += TPB) {
     double rj = r[j], z = 0.0;
     const int lp = mp.lowpos[j], up = mp.uppos[j];
     if (lp >= 0) {
@@ -471,8 +472,8 @@ __device__ __forceinline__ void red_rr(const NLPDims& d, const NLPMap& mp, const
 // once for both.  (Jᵀ y)_i over the rows with y known is formed first, 16
 // lanes per column of J (contiguous), instead of one lane per column walking
 // a row of J (a 64-line gather per load).
-template <int NV>
-__global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, NLPIn in, NLPRed Rd,
+template <int NV, int TPB = NT>
+__global__ __launch_bounds__(TPB) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, NLPIn in, NLPRed Rd,
                                                          const int32_t* __restrict__ shift, int trans,
                                                          const double* __restrict__ rfull,
                                                          double* __restrict__ rred, int nmax,
@@ -493,7 +494,7 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
   if (!red_use(Rd, shift, (int)b)) {
 #pragma unroll
     for (int k = 0; k < NV; ++k)
-      for (int i = t; i < nmax; i += NT) o[k][i] = r[k][i];
+      for (int i = t; i < nmax; i += TPB) o[k][i] = r[k][i];
     return;
   }
   const int n = d.n, c = d.c, w = d.num_w, N = n + c;
@@ -507,14 +508,14 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
   int* yl1 = kl + n;   // rows with y known, compacted (c)
   int* cnt = yl1 + c;  // [#known x, #known y]
   const double* rho = Rd.rho + b * c;
-  for (int j = t; j < w; j += NT) kx[j] = Rd.kx[b * w + j];
-  for (int k = t; k < c; k += NT) ys[k] = Rd.yst[b * c + k];
+  for (int j = t; j < w; j += TPB) kx[j] = Rd.kx[b * w + j];
+  for (int k = t; k < c; k += TPB) ys[k] = Rd.yst[b * c + k];
 #pragma unroll
-  for (int k = 0; k < NV; ++k) red_rr(d, mp, in, b, tr[k], r[k], rr + k * w, zk + k * w);
+  for (int k = 0; k < NV; ++k) red_rr<TPB>(d, mp, in, b, tr[k], r[k], rr + k * w, zk + k * w);
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < NV; ++k)
-    for (int q = t; q < c; q += NT) yv[k * c + q] = ys[q] == 1 ? -rr[k * w + mp.slack_of_row[q]] : 0.0;
+    for (int q = t; q < c; q += TPB) yv[k * c + q] = ys[q] == 1 ? -rr[k * w + mp.slack_of_row[q]] : 0.0;
   wave_compact(n, [&](int j) { return kx[j] >= 0; }, kl, cnt);
   wave_compact(c, [&](int q) { return ys[q] == 1; }, yl1, cnt + 1);
   __syncthreads();
@@ -523,7 +524,7 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
   const double* J = in.Jx + b * c * n;
   {   // jy_i = Σ over the rows q with y known of J[q][i]·y_q (column i of J: contiguous)
     const int g = t >> 4, gl = t & 15;
-    for (int i = g; i < n; i += NT / 16) {
+    for (int i = g; i < n; i += TPB / 16) {
       if (kx[i] >= 0) continue;   // group-uniform
       double acc[NV];
 #pragma unroll
@@ -548,7 +549,7 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
   // columns are visited (the compacted lists: no per-column branch, the
   // loads of several columns in flight)
   const bool sym = meta[b].sym;
-  for (int i = t; i < nmax; i += NT) {
+  for (int i = t; i < nmax; i += TPB) {
     double v[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) v[k] = 0.0;
@@ -614,8 +615,8 @@ __global__ __launch_bounds__(NT) void nlp_red_rhs_kernel(NLPDims d, NLPMap mp, N
 // forward / reverse pair, H and J read once for both).  Dynamic LDS per
 // vector: rr (num_w), known z (num_w), z over w (num_w), y (c); then the masks
 // and the compacted active primal bounds (ints).
-template <int NV>
-__global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap mp, NLPIn in, NLPRed Rd,
+template <int NV, int TPB = NT>
+__global__ __launch_bounds__(TPB) void nlp_red_recover_kernel(NLPDims d, NLPMap mp, NLPIn in, NLPRed Rd,
                                                              const int32_t* __restrict__ shift, int trans,
                                                              const double* __restrict__ rfull,
                                                              const double* __restrict__ xred,
@@ -639,7 +640,7 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
   if (!red_use(Rd, shift, (int)b)) {
 #pragma unroll
     for (int k = 0; k < NV; ++k)
-      for (int i = t; i < nmax; i += NT) z[k][i] = xr[k][i];
+      for (int i = t; i < nmax; i += TPB) z[k][i] = xr[k][i];
     return;
   }
   const int n = d.n, c = d.c, w = d.num_w;
@@ -651,8 +652,8 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
   int* ys = kx + w;
   int* al = ys + c;    // primal variables fixed by an active bound, compacted (n)
   int* cnt = al + n;
-  for (int j = t; j < w; j += NT) kx[j] = Rd.kx[b * w + j];
-  for (int q = t; q < c; q += NT) ys[q] = Rd.yst[b * c + q];
+  for (int j = t; j < w; j += TPB) kx[j] = Rd.kx[b * w + j];
+  for (int q = t; q < c; q += TPB) ys[q] = Rd.yst[b * c + q];
   const double* rho = Rd.rho + b * c;
   const double* dl = Rd.delta + b * w;
   const double* H = in.Hxx + b * n * n;
@@ -661,16 +662,16 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
   const bool sym = meta[b].sym;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    red_rr(d, mp, in, b, tr[k], r[k], rr + k * w, zk + k * w);
-    for (int i = t; i < n; i += NT) zw[k * w + i] = xr[k][i];
-    for (int q = t; q < c; q += NT) {
+    red_rr<TPB>(d, mp, in, b, tr[k], r[k], rr + k * w, zk + k * w);
+    for (int i = t; i < n; i += TPB) zw[k * w + i] = xr[k][i];
+    for (int q = t; q < c; q += TPB) {
       yl[k * c + q] = xr[k][n + q];
       z[k][w + q] = xr[k][n + q];
     }
   }
   __syncthreads();
   wave_compact(n, [&](int j) { return kx[j] >= 0; }, al, cnt);   // wave 0
-  for (int s = n + t; s < w; s += NT) {   // slacks
+  for (int s = n + t; s < w; s += TPB) {   // slacks
     const int row = mp.row_of_slack[s - n];
     double v[NV];
     if (kx[s] >= 0) {
@@ -695,10 +696,10 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < NV; ++k)
-    for (int j = t; j < w; j += NT) z[k][j] = zw[k * w + j];
+    for (int j = t; j < w; j += TPB) z[k][j] = zw[k * w + j];
   // the bound rows' unknowns (lower block then upper: row lo0 + q for bound q)
   const int lo0 = w + c;
-  for (int q = t; q < d.nlo + d.nup; q += NT) {
+  for (int q = t; q < d.nlo + d.nup; q += TPB) {
     const bool low = q < d.nlo;
     const int i = low ? q : q - d.nlo;
     const int j = low ? mp.low_idx[i] : mp.up_idx[i];
@@ -727,7 +728,7 @@ __global__ __launch_bounds__(NT) void nlp_red_recover_kernel(NLPDims d, NLPMap m
   //   (W x)_j + δ_j x_j + (Jᵀ y)_j + b·z_ν = r̃_j,
   // 16 lanes per row (one 128-byte line per group load), 16 rows at a time
   const int na = cnt[0], g = t >> 4, gl = t & 15;
-  for (int e = g; e < na; e += NT / 16) {
+  for (int e = g; e < na; e += TPB / 16) {
     const int j = al[e], q = kx[j];
     const bool low = q < d.nlo;
     double acc[NV];
@@ -1027,6 +1028,7 @@ void nlp_factor(Handle& h) {
   std::vector<int32_t> all(B);
   for (int b = 0; b < B; ++b) all[b] = b;
   std::vector<int32_t> sing = singular_list(h, all);
+  const bool corrected = !sing.empty();   // else nlp_shift stays all zero (the memset above)
   h.nlp_corr.assign(B, 0);
   std::vector<int32_t> shift(B, 0);
   for (int k = 1; k <= std::min(NLP_MAX_CORR, h.nlp_max_corr) && !sing.empty(); ++k) {
@@ -1049,9 +1051,11 @@ void nlp_factor(Handle& h) {
     shift[b] = -1;
     h.nlp_corr[b] = -1;
   }
-  DOPT_CHECK_HIP(hipMemcpyAsync(h.nlp_shift.p, shift.data(), (size_t)B * sizeof(int32_t), hipMemcpyHostToDevice,
-                                h.stream));
-  DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+  if (corrected) {   // the final shifts (−1: correction failed); `shift` must outlive the copy
+    DOPT_CHECK_HIP(hipMemcpyAsync(h.nlp_shift.p, shift.data(), (size_t)B * sizeof(int32_t), hipMemcpyHostToDevice,
+                                  h.stream));
+    DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+  }
   // every factor no-pivot (none rejected, corrected or failed): the solves
   // skip the partial-pivoting kernels' launches
   h.nlp_pivoted = h.n_pivot != 0 || std::any_of(h.nlp_corr.begin(), h.nlp_corr.end(), [](int32_t k) { return k != 0; });
