@@ -354,7 +354,9 @@ void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, con
 size_t dinv_stride(int nmax);
 // re-assembly of a list of problems (plist: device indices, count)
 using ReasmFn = std::function<void(const int32_t*, int)>;
-void factor_dense(Handle& h, const ReasmFn& reasm);
+// pre_copy (optional): launched after the no-pivot LU, before its metadata
+// read-back (so the host's copy carries what it writes)
+void factor_dense(Handle& h, const ReasmFn& reasm, const std::function<void()>* pre_copy = nullptr);
 double* dense_dinv(Handle& h);
 void lsqr_slabs(Handle& h, int trans, const double* rhs, double* x);
 void lhs_solve(Handle& h, int k, const double* rhs, double* x, bool iterative, int32_t* info);

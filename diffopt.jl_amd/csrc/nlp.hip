@@ -1017,17 +1017,32 @@ void nlp_factor(Handle& h) {
   const bool saddle_only = !h.nlp_kkt && h.nlp_ng + h.nlp_nl + h.nlp_nlo + h.nlp_nup == 0;
   const int32_t lu_mode = h.lu_mode;
   if (!saddle_only && !reduced_on(h)) h.lu_mode = 0;
+  // the singularity check rides on the LU's metadata read-back when the
+  // no-pivot LU accepted every problem (one host turnaround instead of two)
+  bool early_check = false;
+  const std::function<void()> pre = [&] {
+    pivot_check(h, nullptr, B);
+    early_check = true;
+  };
+  bool fast = false;
   try {
-    factor_dense(h, [&h](const int32_t* pl, int count) { assemble(h, pl, count); });
+    factor_dense(h, [&h](const int32_t* pl, int count) { assemble(h, pl, count); }, &pre);
+    fast = early_check && h.lu_mode == 1 && h.n_pivot == 0 && h.blocked_npmax > 0 && h.meta_host;
   } catch (...) {
     h.lu_mode = lu_mode;
     throw;
   }
   h.lu_mode = lu_mode;
-  pivot_check(h, nullptr, B);
   std::vector<int32_t> all(B);
   for (int b = 0; b < B; ++b) all[b] = b;
-  std::vector<int32_t> sing = singular_list(h, all);
+  std::vector<int32_t> sing;
+  if (fast) {
+    for (int b = 0; b < B; ++b)
+      if (h.meta_host[b].info > 0) sing.push_back(b);
+  } else {
+    pivot_check(h, nullptr, B);   // (problems already found singular are skipped)
+    sing = singular_list(h, all);
+  }
   const bool corrected = !sing.empty();   // else nlp_shift stays all zero (the memset above)
   h.nlp_corr.assign(B, 0);
   std::vector<int32_t> shift(B, 0);

@@ -875,7 +875,8 @@ static void generic_lu(Handle& h, const std::vector<int32_t>& list) {
 // the rejected list: work that skips rejected problems (the solves of the
 // fused call).
 template <class F>
-static void factor_blocked(Handle& h, F&& spec, double* w0, double* w1, const ReasmFn& reasm) {
+static void factor_blocked(Handle& h, F&& spec, double* w0, double* w1, const ReasmFn& reasm,
+                           const std::function<void()>* pre_copy = nullptr) {
   auto np_of = [](const QPMeta& mm) { return (mm.nsys + 31) & ~31; };
   std::vector<int32_t> glist;   // problems for the generic LU
   if (h.has_generic)
@@ -888,6 +889,7 @@ static void factor_blocked(Handle& h, F&& spec, double* w0, double* w1, const Re
       PhaseTimer pt(h, DOPT_PHASE_QP_LU);
       qp_nopiv_factor(h, dinv_of(h), w0, w1);
     }
+    if (pre_copy) (*pre_copy)();   // kernels whose metadata the read-back below should carry (NLP: the pivot check)
     if (h.blocked_npmax) meta_copy(h);
     spec();
     h.n_pivot = 0;
@@ -952,10 +954,10 @@ void qp_factor(Handle& h) {
 // The blocked factorisation of a batch already assembled into K / meta by a
 // caller (the NLP back-end), with `reasm` re-assembling the problems the
 // no-pivot LU rejects.  Sizes from h.blocked_npmax; blocked route only.
-void factor_dense(Handle& h, const ReasmFn& reasm) {
+void factor_dense(Handle& h, const ReasmFn& reasm, const std::function<void()>* pre_copy) {
   h.has_generic = false;
   h.has_lsqr = false;
-  factor_blocked(h, [] {}, nullptr, nullptr, reasm);
+  factor_blocked(h, [] {}, nullptr, nullptr, reasm, pre_copy);
 }
 
 double* dense_dinv(Handle& h) { return dinv_of(h); }

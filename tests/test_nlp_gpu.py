@@ -417,6 +417,8 @@ def test_forward_reverse_equals_separate_calls(case, lu_mode, monkeypatch):
     if case == "no_seeds":
         dx = dd = None
     e = engine(st, pt, B)
+    if case == "mixed_routes":   # problem 1 on the full M (partial pivoting: the factor's slow path)
+        assert e.system_size()[1] == e.layout()["rows"] and e.corrections()[1] == oracle_problem(st, pt, 1)[4]
     fx, fd = e.forward(dp)
     rp = e.reverse(dx, dd)
     if case == "device":

@@ -1,0 +1,8 @@
+# NLP factor: the singularity check carried on the LU's metadata read-back; NLP / QP tests, config-6 bench twice
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+J=tools/gpu_job.sh
+TEST_PATHS="tests/test_nlp_gpu.py tests/test_qp_gpu.py tests/test_model_api_gpu.py" bash $J test && cp gpurun_out/test.log gpurun_out/test_nlpsync.log && \
+bash $J bench cfg6s --config 6 --steps 20 --warmup 3 --no-cpu-baseline && \
+bash $J bench cfg6s2 --config 6 --steps 20 --warmup 3 --no-cpu-baseline
