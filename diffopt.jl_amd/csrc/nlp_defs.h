@@ -85,7 +85,9 @@ __device__ __forceinline__ int nlp_code(const NLPDims& d, const NLPRed& R, size_
 
 // R[r][col] of problem b (identity padding past n + c) from the two index
 // codes (nlp_code of r and of col): one round of unconditional loads (the
-// selected value and δ).
+// selected value and δ).  LOWER: r > col is known (the column tiles), so no
+// diagonal term — no δ load, no identity entry.
+template <bool LOWER = false>
 __device__ __forceinline__ double nlp_R_codes(const NLPDims& d, const NLPIn& in, const NLPRed& R, size_t b, int r,
                                               int col, int coder, int codec) {
   const int n = d.n, N = n + d.c;
@@ -94,7 +96,7 @@ __device__ __forceinline__ double nlp_R_codes(const NLPDims& d, const NLPIn& in,
   const bool rq = rr < n, cq = cc < n;
   const int kr = coder, kc = codec, yr = coder, yc = codec;
   const double* dummy = in.Hxx;
-  const double ident = r == col ? 1.0 : 0.0;
+  const double ident = !LOWER && r == col ? 1.0 : 0.0;
   double cv = 0.0;
   int mode = 0;   // 0: the constant cv, 1: the loaded value, 2: its negation
   bool addd = false;
@@ -108,7 +110,7 @@ __device__ __forceinline__ double nlp_R_codes(const NLPDims& d, const NLPIn& in,
       if (kc < 0) {
         mode = 1;
         p = in.Hxx + b * n * n + (size_t)cc * n + rr;
-        addd = cc == rr;
+        addd = !LOWER && cc == rr;
       }
     } else if (yc != 1) {
       mode = 1;
@@ -128,7 +130,7 @@ __device__ __forceinline__ double nlp_R_codes(const NLPDims& d, const NLPIn& in,
     }
   }
   const double x = *p;
-  const double dl = *(addd ? R.delta + b * d.num_w + rr : dummy);
+  const double dl = LOWER ? 0.0 : *(addd ? R.delta + b * d.num_w + rr : dummy);
   return mode == 0 ? cv : (mode == 2 ? -x : (addd ? x + dl : x));
 }
 

@@ -277,9 +277,10 @@ __device__ __forceinline__ void src_stage_codes(const NSrc& s, const NSrcB& v, d
 __device__ __forceinline__ double src_val_tile(const QSrcB& v, const double*, int r, int c, int, int) {
   return kval_lower(v, r, c);
 }
+// (column tiles only: every entry strictly below the diagonal)
 __device__ __forceinline__ double src_val_tile(const NSrcB& v, const double* X, int r, int c, int ri, int ci) {
   const int* tc = tile_codes(const_cast<double*>(X));
-  return nlp_R_codes(v.s->d, v.s->in, v.s->R, v.b, r, c, tile_code(tc, ri), tile_code(tc, 64 + ci));
+  return nlp_R_codes<true>(v.s->d, v.s->in, v.s->R, v.b, r, c, tile_code(tc, ri), tile_code(tc, 64 + ci));   // r > c
 }
 template <class SRC> constexpr bool src_staged() { return false; }
 template <> constexpr bool src_staged<NSrc>() { return true; }
