@@ -117,21 +117,9 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
     }
     if (const char* e = getenv("DOPT_LU")) h->lu_mode = atoi(e) != 0;
     if (const char* e = getenv("DOPT_SYM")) h->sym_mode = atoi(e) != 0;
-    if (const char* e = getenv("DOPT_PRIO")) h->prio_mode = atoi(e) != 0;
     if (const char* e = getenv("DOPT_LEFT")) h->left_mode = atoi(e) != 0;
-    if (const char* e = getenv("DOPT_LSTREAMS")) h->lstreams = atoi(e) != 0;
     if (const char* e = getenv("DOPT_NLP_REDUCE")) h->nlp_reduce = atoi(e) != 0;
-    if (const char* e = getenv("DOPT_SYM_LEAN")) h->sym_lean = atoi(e);
-    if (const char* e = getenv("DOPT_LCOL_TW")) h->lcol_tw = atoi(e);
-    if (const char* e = getenv("DOPT_LDL")) h->ldl_mode = atoi(e) != 0;
-    if (const char* e = getenv("DOPT_LSLICE")) h->lslices = atoi(e);
-    if (const char* e = getenv("DOPT_LPERSIST")) h->lpersist = atoi(e) != 0;
-    if (const char* e = getenv("DOPT_LCOL_PF")) h->lcol_pf = atoi(e) != 0;
-    if (const char* e = getenv("DOPT_SYM_TPB")) h->sym_tpb = atoi(e);
-    if (const char* e = getenv("DOPT_SPLIT_NW")) h->split_nw = atoi(e) == 8 ? 8 : 4;
     if (const char* e = getenv("DOPT_SPLIT_FUSE")) h->split_fuse = atoi(e) != 0;
-    if (const char* e = getenv("DOPT_SPLIT_NC")) h->split_nc = atoi(e) == 4 ? 4 : 2;
-    if (const char* e = getenv("DOPT_PSD_MFMA")) h->psd_mfma = atoi(e) != 0;
     if (kind == DOPT_KIND_QP) {
       // largest supported system: the generic solve stages an nmax vector in
       // LDS (64 KB); the blocked route takes reduced systems up to BLOCKED_MAX
@@ -233,6 +221,10 @@ int dopt_qp_set(dopt_handle* h, const double* Q, const double* G, const double* 
     if (!Q || !z) throw Error(-1, "Q and z are required");
     if (m && (!G || !hv || !lam)) throw Error(-1, "G, h and lam are required when m > 0");
     if (p && (!A || !nu)) throw Error(-1, "A and nu are required when p > 0");
+    // the staging below may reallocate the buffers the previous model's
+    // pointers name: the handle holds no model until this call succeeds
+    h->set = false;
+    h->factored = false;
     h->Q = stage_in(*h, h->own_in[0], Q, B * n * n);
     h->G = m ? stage_in(*h, h->own_in[1], G, B * m * n) : nullptr;
     h->hv = m ? stage_in(*h, h->own_in[2], hv, B * m) : nullptr;
@@ -307,6 +299,22 @@ int dopt_qp_set_csc(dopt_handle* h,
     if (m && (!G_colptr || !hv || !lam)) throw Error(-1, "G, h and lam are required when m > 0");
     if (p && (!A_colptr || !nu)) throw Error(-1, "A and nu are required when p > 0");
     if (Q_nnz < 0 || G_nnz < 0 || A_nnz < 0) throw Error(-1, "nnz must be >= 0");
+    if ((Q_nnz > 0 && (!Q_rowval || !Q_nzval)) || (m && G_nnz > 0 && (!G_rowval || !G_nzval)) ||
+        (p && A_nnz > 0 && (!A_rowval || !A_nzval)))
+      throw Error(-1, "rowval and nzval are required when nnz > 0");
+    // every host-side check is done: from here on the staging may reallocate
+    // (or overwrite) the buffers the previous model's pointers name, so the
+    // handle holds no model until this call succeeds
+    h->set = false;
+    h->factored = false;
+    // a throw after a queued copy out of the pinned buffer waits for it, so
+    // the next call's memcpy into that buffer cannot race the DMA
+    struct SyncOnThrow {
+      hipStream_t s;
+      ~SyncOnThrow() {
+        if (std::uncaught_exceptions() > 0) (void)hipStreamSynchronize(s);
+      }
+    } sync_on_throw{h->stream};
     h->csc_err.ensure(sizeof(int));
     DOPT_CHECK_HIP(hipMemsetAsync(h->csc_err.p, 0, sizeof(int), h->stream));
     int* err = h->csc_err.as<int>();
@@ -333,7 +341,6 @@ int dopt_qp_set_csc(dopt_handle* h,
     for (int k = 0; k < 3; ++k) {
       const Mat& M = mats[k];
       if (M.rows == 0) continue;
-      if (M.nnz > 0 && (!M.rv || !M.nz)) throw Error(-1, "rowval and nzval are required when nnz > 0");
       const int64_t* cp = packed ? (const int64_t*)pdev[3 * k] : stage_in_i64(*h, h->csc_in[3 * k], M.cp, B * (n + 1));
       const int64_t* rv = packed ? (const int64_t*)pdev[3 * k + 1]
                                  : stage_in_i64(*h, h->csc_in[3 * k + 1], M.rv, (size_t)M.nnz);

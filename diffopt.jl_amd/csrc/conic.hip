@@ -376,74 +376,6 @@ __device__ __forceinline__ d4c cmfma(double a, double b, d4c c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// slot s of wave wv holds tile idx = wv + 4s of the nT × nT grid (row-major;
-// `upper`: of its upper triangle); false past the end.  Closed form, no loop
-// over the grid: the slots' loads can be issued together.
-__device__ __forceinline__ bool psd_tile(int idx, int nT, bool upper, int& r, int& c) {
-  if (!upper) {
-    r = idx / nT;
-    c = idx - r * nT;
-    return idx < nT * nT;
-  }
-  r = c = 0;
-  int k = idx;
-  bool found = false;
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int len = nT - rr;
-    if (!found && len > 0) {
-      if (k < len) {
-        r = rr;
-        c = rr + k;
-        found = true;
-      } else {
-        k -= len;
-      }
-    }
-  }
-  return found;
-}
-
-template <class FA, class FB, class FS>
-__device__ __forceinline__ void psd_mfma(int d, bool upper, FA a, FB b, FS st) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, l16 = lane & 15, g = lane >> 4;
-  const int nT = (d + 15) >> 4;
-  int ti[4], tj[4];
-  bool on[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) on[s] = psd_tile(wv + 4 * s, nT, upper, ti[s], tj[s]);
-  if (!on[0]) return;   // wave-uniform; no barrier inside
-  d4c acc[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) acc[s] = (d4c){0.0, 0.0, 0.0, 0.0};
-  const int dp = (d + 3) & ~3;
-  // two k-steps per trip, every operand of the trip read before its MFMAs (a
-  // step past dp reads zeros: a(…) / b(…) give 0 outside [0, d)).  No branch
-  // per slot: an empty slot (r = c = 0) repeats tile (0, 0) and is not stored
-  // — per-slot branches put an LDS wait in front of every MFMA
-  for (int q0 = 0; q0 < dp; q0 += 8) {
-    double av[2][4], bv[2][4];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int q = q0 + 4 * h + g;
-        av[h][s] = a(16 * ti[s] + l16, q);
-        bv[h][s] = b(q, 16 * tj[s] + l16);
-      }
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc[s] = cmfma(av[h][s], bv[h][s], acc[s]);
-  }
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-    if (on[s])
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) st(16 * ti[s] + g + 4 * rr, 16 * tj[s] + l16, acc[s][rr], s, rr);
-}
-
-template <bool MFMA>
 __device__ __forceinline__ void psd_apply_cone_lds(const ConeDesc cd, const double* __restrict__ P,
                                                    const double* in, double* out, int trans, double* Xs,
                                                    double* Ys, double* Us) {
@@ -477,24 +409,6 @@ __device__ __forceinline__ void psd_apply_cone_lds(const ConeDesc cd, const doub
     }
     return;
   }
-  // this lane's entries of B at the middle product's output positions (the
-  // upper tiles of psd_mfma's enumeration for this wave, mirrored below):
-  // loaded from clamped addresses, masked only where used
-  const int lane = t & 63, wv = t >> 6, l16 = lane & 15, g = lane >> 4;
-  const int nT = (d + 15) >> 4;
-  double br[4][4];
-  bool bk[4][4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    int r, c;
-    const bool on = psd_tile(wv + 4 * s, nT, true, r, c);
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int i = 16 * r + g + 4 * rr, j = 16 * c + l16;
-      bk[s][rr] = on && i < d && j < d;
-      br[s][rr] = Bm[bk[s][rr] ? i * d + j : 0];
-    }
-  }
 #pragma unroll
   for (int k = 0; k < UR; ++k) {
     const int e = t + CTPB * k;
@@ -515,7 +429,7 @@ __device__ __forceinline__ void psd_apply_cone_lds(const ConeDesc cd, const doub
     }
   }
   __syncthreads();
-  if constexpr (!MFMA) {
+  {
     // the products on 4×4 register tiles (psd_gemm4) over images padded to
     // dp: zero the padding (rows / columns d..dp−1) first
     const int dp = (d + 3) & ~3;
@@ -543,40 +457,10 @@ __device__ __forceinline__ void psd_apply_cone_lds(const ConeDesc cd, const doub
                 if (i <= j && j < d) o[tri_idx(i, j)] = (!trans && i != j) ? 2.0 * v : v;
               });
     __syncthreads();
-    return;
   }
-  auto rd = [&](const double* img, int i, int j) {
-    const bool ok = i < d && j < d;
-    const double v = img[ok ? i * ld + j : 0];
-    return ok ? v : 0.0;
-  };
-  // Y = Uᵀ X
-  psd_mfma(d, false, [&](int i, int q) { return rd(Us, q, i); }, [&](int q, int j) { return rd(Xs, q, j); },
-           [&](int i, int j, double v, int, int) { if (i < d && j < d) Ys[i * ld + j] = v; });
-  __syncthreads();
-  // X = (Y U) ∘ B, upper tiles, mirrored
-  psd_mfma(d, true, [&](int i, int q) { return rd(Ys, i, q); }, [&](int q, int j) { return rd(Us, q, j); },
-           [&](int i, int j, double v, int s, int rr) {
-             if (i < d && j < d) {
-               const double x = v * (bk[s][rr] ? br[s][rr] : 0.0);
-               Xs[i * ld + j] = x;
-               Xs[j * ld + i] = x;
-             }
-           });
-  __syncthreads();
-  // Y = U X
-  psd_mfma(d, false, [&](int i, int q) { return rd(Us, i, q); }, [&](int q, int j) { return rd(Xs, q, j); },
-           [&](int i, int j, double v, int, int) { if (i < d && j < d) Ys[i * ld + j] = v; });
-  __syncthreads();
-  // out = tri(Y Uᵀ) (upper tiles; S² for Dπ)
-  psd_mfma(d, true, [&](int i, int q) { return rd(Ys, i, q); }, [&](int q, int j) { return rd(Us, j, q); },
-           [&](int i, int j, double v, int, int) {
-             if (i <= j && j < d) o[tri_idx(i, j)] = (!trans && i != j) ? 2.0 * v : v;
-           });
-  __syncthreads();
 }
 
-template <bool BIG = false, bool MF = false>
+template <bool BIG = false>
 __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, const double* __restrict__ v,
                           const double* __restrict__ P, const double* in, double* out,
                           int trans, double* lds, double* red, double* gws) {
@@ -635,12 +519,11 @@ __device__ __forceinline__ void dpi_apply(const ConeDesc* cones, int ncones, con
     } else {
       const size_t img = (size_t)((d + 3) & ~3) * (((d + 3) & ~3) + 1);   // this cone's image: dp × (dp+1)
       // split path: every load of the cone issued up front, the products on
-      // 4×4 register tiles (MF: on MFMA, env DOPT_PSD_MFMA=1 — measured no
-      // faster, 42 vs 43 µs per dpiU launch at config 5); the persistent LSQR
-      // kernels keep psd_apply_cone (the up-front operands would push
-      // conic_lsqr2_kernel from 42 to 141 VGPR spills)
-      if (MF) psd_apply_cone_lds<true>(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
-      else if (BIG) psd_apply_cone_lds<false>(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
+      // 4×4 register tiles (an MFMA form measured no faster, 42 vs 43 µs per
+      // dpiU launch at config 5, round 4); the persistent LSQR kernels keep
+      // psd_apply_cone (the up-front operands would push conic_lsqr2_kernel
+      // from 42 to 141 VGPR spills)
+      if (BIG) psd_apply_cone_lds(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
       else psd_apply_cone(cd, P, in, out, trans, lds, lds + img, lds + 2 * img);
     }
   }
@@ -1475,8 +1358,6 @@ __global__ __launch_bounds__(64 * NW) void conic_split_pass_kernel(
 }
 
 // Dπ (dir 0: Dv = Dπ v_m) or Dπᵀ (dir 1: out_m = Dπᵀ tmpm), one cone per WG
-// (MF: the PSD cones' products on MFMA, env DOPT_PSD_MFMA=1)
-template <bool MF>
 __global__ __launch_bounds__(CTPB) void conic_split_dpi_kernel(
     int dir, const ConeDesc* __restrict__ cones_g, const double* __restrict__ vcone,
     const double* __restrict__ P, int plen, SplitWS ws, const LsqrState* __restrict__ stv,
@@ -1491,9 +1372,9 @@ __global__ __launch_bounds__(CTPB) void conic_split_dpi_kernel(
   const double* pp = P + (size_t)ws.phys(b) * plen;
   double* g = gws + (size_t)b * wlen;
   if (dir == 0)
-    dpi_apply<true, MF>(&cd, 1, pv, pp, ws.vec(ws.v, b) + ws.n, ws.mvec(ws.Dv, b), 0, lds, red, g);
+    dpi_apply<true>(&cd, 1, pv, pp, ws.vec(ws.v, b) + ws.n, ws.mvec(ws.Dv, b), 0, lds, red, g);
   else
-    dpi_apply<true, MF>(&cd, 1, pv, pp, ws.mvec(ws.tmpm, b), ws.vec(ws.out, b) + ws.n, 1, lds, red, g);
+    dpi_apply<true>(&cd, 1, pv, pp, ws.mvec(ws.tmpm, b), ws.vec(ws.out, b) + ws.n, 1, lds, red, g);
 }
 
 // The per-problem vector kernels below run 1024-thread workgroups and issue
@@ -1925,7 +1806,7 @@ __device__ __forceinline__ double gsum8(const double* __restrict__ gp, int RB, i
 
 // DIR 0: passM, DIR 1: passT (see above).  Dynamic LDS (passT): u_n of the
 // (up to two) live sequences, 2·n doubles.
-template <int NW, int DIR, int NC2 = 2>
+template <int NW, int DIR>
 __global__ __launch_bounds__(64 * NW) void conic_fsplit_pass_kernel(
     const double* __restrict__ A, const double* __restrict__ bvec, const double* __restrict__ cvec, FSplit fs,
     int par, int nq) {
@@ -2022,11 +1903,10 @@ __global__ __launch_bounds__(64 * NW) void conic_fsplit_pass_kernel(
     __syncthreads();   // u_n in LDS and this block's rows of u (global) before the sweep
   }
   if (nl == 0) return;
-  // NC2 columns in flight per wave for two sequences (NC2 + 2 for one): the
-  // grid holds ≤ 2 workgroups per CU, so registers are not what limits the
-  // loads in flight
-  if (nl == 2) gemv_multi<2, SPLIT_K, NC2, NW>(Ab, m, rows, n, xs, wv, yv, gv, ys);
-  else gemv_multi<1, SPLIT_K, (NC2 == 2 ? PAIR_NC : NC2 + 2), NW>(Ab, m, rows, n, xs, wv, yv, gv, ys);
+  // two columns in flight per wave for two sequences, PAIR_NC for one (four
+  // for two measured no faster, round 4: 170.7 vs 168.0 ms at config 5)
+  if (nl == 2) gemv_multi<2, SPLIT_K, 2, NW>(Ab, m, rows, n, xs, wv, yv, gv, ys);
+  else gemv_multi<1, SPLIT_K, PAIR_NC, NW>(Ab, m, rows, n, xs, wv, yv, gv, ys);
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   for (int c = 0; c < nl; ++c) {
     const int bv = live[c];
@@ -2070,7 +1950,6 @@ __global__ __launch_bounds__(64 * NW) void conic_fsplit_pass_kernel(
 }
 
 // dpiU: one cone per workgroup; v' = Dπᵀ(tmpm) + u_m − βv on the cone's rows
-template <bool MF>
 __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiU_kernel(
     const ConeDesc* __restrict__ cones_g, const double* __restrict__ vcone, const double* __restrict__ P,
     int plen, FSplit fs, int par, double* __restrict__ gws, int wlen) {
@@ -2084,7 +1963,7 @@ __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiU_kernel(
   const double* pv = vcone + (size_t)fs.phys(bv) * m;
   const double* pp = P + (size_t)fs.phys(bv) * plen;
   double* vn = fs.V(par ^ 1, bv);
-  dpi_apply<true, MF>(&cd, 1, pv, pp, fs.tmpm + (size_t)bv * m, vn + n, 1, lds, red, gws + (size_t)bv * wlen);
+  dpi_apply<true>(&cd, 1, pv, pp, fs.tmpm + (size_t)bv * m, vn + n, 1, lds, red, gws + (size_t)bv * wlen);
   const double beta = st.beta;
   const double* vo = fs.V(par, bv);
   const double* un = fs.U(par ^ 1, bv);
@@ -2118,7 +1997,6 @@ __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiU_kernel(
 
 // dpiV: finish the iteration (first = 0), then Dv = Dπ v_m on the cone.
 // Dynamic LDS: the Dπ images (img doubles), then v'_n (n doubles).
-template <bool MF>
 __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiV_kernel(
     const ConeDesc* __restrict__ cones_g, const double* __restrict__ vcone, const double* __restrict__ P,
     int plen, const double* __restrict__ cvec, FSplit fs, int par, int first, int maxiter,
@@ -2227,7 +2105,7 @@ __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiV_kernel(
   } else if (fs.S(par)[bv].done) {
     return;
   }
-  dpi_apply<true, MF>(&cd, 1, vcone + (size_t)fs.phys(bv) * m, P + (size_t)fs.phys(bv) * plen,
+  dpi_apply<true>(&cd, 1, vcone + (size_t)fs.phys(bv) * m, P + (size_t)fs.phys(bv) * plen,
                   fs.V(vp, bv) + n, fs.Dv + (size_t)bv * m, 0, lds, red, gws + (size_t)bv * wlen);
 }
 
@@ -2390,17 +2268,12 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
   int32_t left = V;
   PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
   auto pass = [&](int dir) {
-    if (h.split_nw == 8)
-      hipLaunchKernelGGL(conic_split_pass_kernel<8>, dim3(RB, B), dim3(512), 0, h.stream, dir, h.cA, h.cb, ws, st,
-                         nq);
-    else
-      hipLaunchKernelGGL(conic_split_pass_kernel<4>, dim3(RB, B), dim3(256), 0, h.stream, dir, h.cA, h.cb, ws, st,
-                         nq);
+    hipLaunchKernelGGL(conic_split_pass_kernel<4>, dim3(RB, B), dim3(256), 0, h.stream, dir, h.cA, h.cb, ws, st, nq);
   };
   auto passT = [&]() {
     pass(1);
     if (nc)
-      hipLaunchKernelGGL(h.psd_mfma ? conic_split_dpi_kernel<true> : conic_split_dpi_kernel<false>, dim3(nc, V),
+      hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, V),
                          dim3(CTPB), dl, h.stream, 1, cd, vcone, P, h.dpi_len, ws, st, gws, h.psd_big_len);
   };
   hipLaunchKernelGGL(conic_split_init_kernel, dim3(V), dim3(CTPB), 0, h.stream, rhs, tol0, tol1, ws, st, active);
@@ -2414,25 +2287,18 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
     const int img = (int)(((dl + 15) & ~(size_t)15) / sizeof(double));
     const size_t dlp = (size_t)2 * n * sizeof(double);
     auto dpiV = [&](int first) {
-      hipLaunchKernelGGL(h.psd_mfma ? conic_fsplit_dpiV_kernel<true> : conic_fsplit_dpiV_kernel<false>, dim3(nc, V),
+      hipLaunchKernelGGL(conic_fsplit_dpiV_kernel, dim3(nc, V),
                          dim3(CTPB), dlv, h.stream, cd, vcone, P, h.dpi_len, h.cc, fs, par, first, N, active, gws,
                          h.psd_big_len, img);
     };
     dpiV(1);
     for (int it = 0; it < N && left > 0;) {
       for (int k = 0; k < SPLIT_CHUNK && it < N; ++k, ++it) {
-        if (h.split_nc == 4) {
-          hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 0, 4>), dim3(RB, B), dim3(256), 0, h.stream, h.cA, h.cb,
-                             h.cc, fs, par, nq);
-          hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 1, 4>), dim3(RB, B), dim3(256), dlp, h.stream, h.cA, h.cb,
-                             h.cc, fs, par, nq);
-        } else {
-          hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 0>), dim3(RB, B), dim3(256), 0, h.stream, h.cA, h.cb,
-                             h.cc, fs, par, nq);
-          hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 1>), dim3(RB, B), dim3(256), dlp, h.stream, h.cA, h.cb,
-                             h.cc, fs, par, nq);
-        }
-        hipLaunchKernelGGL(h.psd_mfma ? conic_fsplit_dpiU_kernel<true> : conic_fsplit_dpiU_kernel<false>,
+        hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 0>), dim3(RB, B), dim3(256), 0, h.stream, h.cA, h.cb, h.cc,
+                           fs, par, nq);
+        hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 1>), dim3(RB, B), dim3(256), dlp, h.stream, h.cA, h.cb, h.cc,
+                           fs, par, nq);
+        hipLaunchKernelGGL(conic_fsplit_dpiU_kernel,
                            dim3(nc, V), dim3(CTPB), dl, h.stream, cd, vcone, P, h.dpi_len, fs, par, gws,
                            h.psd_big_len);
         dpiV(0);
@@ -2446,7 +2312,7 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
     for (int it = 0; it < N && left > 0;) {
       for (int k = 0; k < SPLIT_CHUNK && it < N; ++k, ++it) {
         if (nc)
-          hipLaunchKernelGGL(h.psd_mfma ? conic_split_dpi_kernel<true> : conic_split_dpi_kernel<false>,
+          hipLaunchKernelGGL(conic_split_dpi_kernel,
                              dim3(nc, V), dim3(CTPB), dl, h.stream, 0, cd, vcone, P, h.dpi_len, ws, st, gws,
                              h.psd_big_len);
         pass(0);

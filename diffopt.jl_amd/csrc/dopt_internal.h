@@ -150,19 +150,9 @@ struct Handle {
   hipStream_t aux = nullptr;       // second stream: Q's symmetry check beside the prepare kernel; the
                                    // P-symmetric no-pivot LU's work off the critical chain
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_qsym = nullptr, ev_crit = nullptr;
-  hipStream_t crit = nullptr;      // high-priority stream of the LU's critical chain (prio_mode)
-  int32_t prio_mode = 1;           // env DOPT_PRIO=0: the chain stays on the handle's stream
+  hipStream_t crit = nullptr;      // high-priority stream of the right-looking LU's critical chain
   int32_t left_mode = 1;           // P-symmetric batches: left-looking LU (env DOPT_LEFT=0: right-looking)
-  int32_t lstreams = 0;            // left-looking LU: column tiles I ≥ J+2 on `aux` (env DOPT_LSTREAMS=1)
   DevBuf ukp;                      // left-looking LU: u_kk / p_k of every finished diagonal block (nmax per problem)
-  int32_t lcol_tw = 1;             // left-looking LU column tiles per workgroup (env DOPT_LCOL_TW: 1 or 2)
-  int32_t lcol_pf = 0;             // left-looking column tiles: next strip prefetched (env DOPT_LCOL_PF=1; measured slower)
-  int32_t lpersist = 0;            // left-looking LU: one workgroup per problem, one launch (env DOPT_LPERSIST=1)
-  int32_t lslices = 1;             // left-looking LU: batch halves as two skewed chains (env DOPT_LSLICE=2)
-  int32_t ldl_mode = 1;            // left-looking LU: diagonal blocks by the one-pass symmetric elimination
-                                   // (ldl64_core; env DOPT_LDL=0: the recursive 32×32 LU, diag_core)
-  int32_t sym_lean = 1;            // fused P-symmetric sweeps in their own lean kernel (env DOPT_SYM_LEAN=0: inside
-                                   // blu_solve2_kernel)
   bool ukp_valid = false;          // the last no-pivot factorisation was left-looking (ukp holds its u_kk / p_k)
   bool u_missing = false;          // ... and stored only L for its P-symmetric problems (U from L on demand)
   DevBuf qsy;                // Q symmetry check: max |Q|, |A| (B doubles), then the asymmetry flags (B int32)
@@ -196,10 +186,6 @@ struct Handle {
   DevBuf vp, dpi, cwork, cinfo, cnorm;   // cnorm: LSQR terminal estimates, 8·B doubles
   DevBuf csplit;                // split-path LSQR vectors, partial products, state
   int32_t conic_split = -1;     // -1 auto, 0 persistent kernel, 1 split (env DOPT_CONIC_SPLIT)
-  int32_t sym_tpb = 256;        // P-symmetric sweep kernel's workgroup size, 256 or 512 (env DOPT_SYM_TPB)
-  int32_t split_nw = 4;         // waves per split-LSQR pass workgroup, 4 or 8 (env DOPT_SPLIT_NW)
-  int32_t split_nc = 2;         // fused split pass: columns in flight per wave for two sequences, 2 or 4 (env DOPT_SPLIT_NC)
-  int32_t psd_mfma = 0;         // split LSQR: PSD Dπ products on MFMA (env DOPT_PSD_MFMA=1)
   int32_t split_fuse = 1;       // split LSQR: 1 four-launch fused iteration, 0 six launches (env DOPT_SPLIT_FUSE)
   int32_t dpi_len = 0;          // doubles per problem of packed Dπ blocks
   int32_t psd_big_len = 0;      // doubles of global scratch per problem / sequence for PSD sides > 64
@@ -270,7 +256,7 @@ struct Handle {
 };
 
 // the handle's second stream and its fork / join events (created on first
-// use); with prio_mode, also the high-priority stream of the no-pivot LU's
+// use), and the high-priority stream of the right-looking no-pivot LU's
 // critical chain (`crit`), so that the diagonal launches are dispatched ahead
 // of the bulk tiles queued on `aux`
 inline void ensure_aux(Handle& h) {
@@ -278,7 +264,7 @@ inline void ensure_aux(Handle& h) {
   int least = 0, greatest = 0;
   DOPT_CHECK_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
   DOPT_CHECK_HIP(hipStreamCreateWithPriority(&h.aux, hipStreamNonBlocking, least));
-  if (h.prio_mode) DOPT_CHECK_HIP(hipStreamCreateWithPriority(&h.crit, hipStreamNonBlocking, greatest));
+  DOPT_CHECK_HIP(hipStreamCreateWithPriority(&h.crit, hipStreamNonBlocking, greatest));
   DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_fork, hipEventDisableTiming));
   DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_join, hipEventDisableTiming));
   DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_qsym, hipEventDisableTiming));

@@ -1249,25 +1249,18 @@ void qp_blocked_solve(Handle& h, const double* dinv, int trans, const double* rh
   const int32_t* perm = h.ipiv.as<int32_t>();
   const QPMeta* meta = h.meta.as<QPMeta>();
   const size_t lds = solve_lds_bytes(h.nmax);
-  if (h.ukp_valid && h.sym_lean && (sel & LU_SEL_NOPIV) && npmax <= SOLVE_STATIC) {
+  if (h.ukp_valid && (sel & LU_SEL_NOPIV) && npmax <= SOLVE_STATIC) {
     // the left-looking route's P-symmetric factors: through L alone (no U)
     SymSweep sym{h.ukp.as<double>(), h.kind == DOPT_KIND_QP ? h.kls.as<double>() : nullptr, h.n, h.m};
     const int ent = (npmax + PT - 1) / PT;
-#define DOPT_SYMSOLVE(E, W)                                                                                   \
-  hipLaunchKernelGGL((blu_symsolve_kernel<E, W>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, \
-                     meta, trans, rhs, x, nullptr, nullptr, sym)
 #define DOPT_SYMSOLVE256(E, W, R)                                                                            \
   hipLaunchKernelGGL((blu_symsolve_kernel<E, W, 256, R>), dim3(B), dim3(256), 0, h.stream, K, h.ld, h.nmax, dinv,   \
                      dstride, meta, trans, rhs, x, nullptr, nullptr, sym)
-    if (h.sym_tpb == 256) {   // 256-thread workgroups, 2 / 4 / 6 entries per thread (as blu_sym2_kernel)
-      if (ent <= 1) { DOPT_SYMSOLVE256(2, 4, 8); }
-      else if (ent == 2) { DOPT_SYMSOLVE256(4, 4, 4); }
-      else { DOPT_SYMSOLVE256(6, 4, 4); }
-    } else if (ent <= 1) { DOPT_SYMSOLVE(1, 5); }
-    else if (ent == 2) { DOPT_SYMSOLVE(2, 2); }
-    else { DOPT_SYMSOLVE(3, 2); }
+    // 256-thread workgroups, 2 / 4 / 6 entries per thread (as blu_sym2_kernel)
+    if (ent <= 1) { DOPT_SYMSOLVE256(2, 4, 8); }
+    else if (ent == 2) { DOPT_SYMSOLVE256(4, 4, 4); }
+    else { DOPT_SYMSOLVE256(6, 4, 4); }
 #undef DOPT_SYMSOLVE256
-#undef DOPT_SYMSOLVE
     DOPT_CHECK_HIP(hipGetLastError());
     sel &= ~LU_SEL_NOPIV;   // every no-pivot problem of the route is P-symmetric
     if (!sel) return;
@@ -1301,7 +1294,7 @@ void qp_blocked_solve_pair(Handle& h, const double* dinv, const double* rhs0, co
                            double* x1, int sel) {
   const int npmax = h.blocked_npmax;
   if (npmax == 0) return;
-  if (h.ukp_valid && h.sym_lean && (sel & LU_SEL_NOPIV) && npmax <= SOLVE_STATIC) {
+  if (h.ukp_valid && (sel & LU_SEL_NOPIV) && npmax <= SOLVE_STATIC) {
     const int B = (int)h.batch;
     const size_t dstride = dinv_stride(h.nmax);
     const double* K = h.K.as<double>();
@@ -1311,13 +1304,9 @@ void qp_blocked_solve_pair(Handle& h, const double* dinv, const double* rhs0, co
 #define DOPT_SYMPAIR(E, W, T, R)                                                                               \
   hipLaunchKernelGGL((blu_symsolve_kernel<E, W, T, R, 2>), dim3(B), dim3(T), 0, h.stream, K, h.ld, h.nmax, dinv, \
                      dstride, meta, 0, rhs0, x0, rhs1, x1, sym)
-    if (h.sym_tpb == 256) {
-      if (ent <= 1) { DOPT_SYMPAIR(2, 4, 256, 8); }
-      else if (ent == 2) { DOPT_SYMPAIR(4, 4, 256, 4); }
-      else { DOPT_SYMPAIR(6, 4, 256, 4); }
-    } else if (ent <= 1) { DOPT_SYMPAIR(1, 5, PT, 16); }
-    else if (ent == 2) { DOPT_SYMPAIR(2, 2, PT, 16); }
-    else { DOPT_SYMPAIR(3, 2, PT, 16); }
+    if (ent <= 1) { DOPT_SYMPAIR(2, 4, 256, 8); }
+    else if (ent == 2) { DOPT_SYMPAIR(4, 4, 256, 4); }
+    else { DOPT_SYMPAIR(6, 4, 256, 4); }
 #undef DOPT_SYMPAIR
     DOPT_CHECK_HIP(hipGetLastError());
     sel &= ~LU_SEL_NOPIV;
@@ -1341,29 +1330,19 @@ void qp_blocked_solve2(Handle& h, const double* dinv, const double* rhs_rev, con
   const size_t lds = solve_lds_bytes(h.nmax);
   // the left-looking LU's u_kk / p_k: the P-symmetric problems' reverse sweep through Lᵀ
   SymSweep sym{h.ukp_valid ? h.ukp.as<double>() : nullptr, h.kls.as<double>(), h.n, h.m};
-  if (sym.ukp && w_rev && (sel & LU_SEL_NOPIV) && npmax <= SOLVE_STATIC && h.sym_lean) {
+  if (sym.ukp && w_rev && (sel & LU_SEL_NOPIV) && npmax <= SOLVE_STATIC) {
     // the left-looking route's factors (every blocked problem P-symmetric): the lean sweep kernel
-    if (ent <= 1 && h.sym_tpb == 256)   // 256 threads, two entries each: four workgroups per CU (env DOPT_SYM_TPB=256)
+    // 256 threads, 2 / 4 / 6 entries each (Np ≤ 512 / 1024 / 1536), rows in
+    // groups of 8 / 4 / 4: four workgroups per CU
+    if (ent <= 1)
       hipLaunchKernelGGL((blu_sym2_kernel<2, 4, 256, 8>), dim3(B), dim3(256), 0, h.stream, K, h.ld, h.nmax, dinv,
                          dstride, meta, w_rev, w_fwd, x_rev, x_fwd, sym);
-    else if (ent <= 1 && h.sym_lean == 2)   // every workgroup of a 1024-problem batch resident (spills 22 VGPRs)
-      hipLaunchKernelGGL((blu_sym2_kernel<1, 8>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, meta,
-                         w_rev, w_fwd, x_rev, x_fwd, sym);
-    else if (ent <= 1)
-      hipLaunchKernelGGL((blu_sym2_kernel<1, 5>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, meta,
-                         w_rev, w_fwd, x_rev, x_fwd, sym);
-    else if (ent == 2 && h.sym_tpb == 256)   // 256 threads × 4 entries, rows in groups of 4
+    else if (ent == 2)
       hipLaunchKernelGGL((blu_sym2_kernel<4, 4, 256, 4>), dim3(B), dim3(256), 0, h.stream, K, h.ld, h.nmax, dinv,
                          dstride, meta, w_rev, w_fwd, x_rev, x_fwd, sym);
-    else if (ent == 2)
-      hipLaunchKernelGGL((blu_sym2_kernel<2, 2>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, meta,
-                         w_rev, w_fwd, x_rev, x_fwd, sym);
-    else if (h.sym_tpb == 256)   // 256 threads × 6 entries (Np ≤ 1536), rows in groups of 4
+    else
       hipLaunchKernelGGL((blu_sym2_kernel<6, 4, 256, 4>), dim3(B), dim3(256), 0, h.stream, K, h.ld, h.nmax, dinv,
                          dstride, meta, w_rev, w_fwd, x_rev, x_fwd, sym);
-    else
-      hipLaunchKernelGGL((blu_sym2_kernel<3, 2>), dim3(B), dim3(PT), 0, h.stream, K, h.ld, h.nmax, dinv, dstride, meta,
-                         w_rev, w_fwd, x_rev, x_fwd, sym);
     DOPT_CHECK_HIP(hipGetLastError());
     sel &= ~LU_SEL_NOPIV;
     if (!sel) return;

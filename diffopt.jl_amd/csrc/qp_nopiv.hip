@@ -1805,7 +1805,7 @@ __device__ __forceinline__ void ldl64_core(double* buf, double* __restrict__ Kb,
 // The diagonal step of block column J = c0 / 64 for problem b (S: the
 // workgroup's STEP_LDS doubles of LDS); nlu_ldiag_kernel runs it for a batch,
 // nlu_left_all_kernel inside its per-problem loop.
-template <class SRC, bool LDL>
+template <class SRC>
 __device__ __forceinline__ void ldiag_body(
     double* S, int b, double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm,
     double* __restrict__ dinv, size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv,
@@ -1944,28 +1944,19 @@ __device__ __forceinline__ void ldiag_body(
   if (t == 0 && c0 == 0) meta[b].lu = LU_NOPIV;   // LU_REJECT below if a test fails
   const double bound = growth_bound(amax);
   LD_MARK(2);
-  if (LDL) {   // its first barrier orders the S image and the sweep stores above
-    ldl64_core(S, Kb, ld, perm + (size_t)b * nmax, dinv + (size_t)b * dstride + (size_t)(c0 / 32) * DBLK, meta + b, c0,
-               Np, mm.nsys, binv + (size_t)b * BSTR, w0b, w1b, bound, ps, ud);
-    return;
-  }
-  // diag_core's first barrier orders the S image and the sweep stores above
-  diag_core(DiagLds(S), Kb, ld, perm + (size_t)b * nmax, dinv + (size_t)b * dstride + (size_t)(c0 / 32) * DBLK,
-            meta + b, c0, Np, mm.nsys, binv + (size_t)b * BSTR, w0b, w1b, bound);
-  __syncthreads();   // S final (U11⁻¹ on the diagonal, every exit of diag_core) + verdicts
-  if (*DiagLds(S).sbad) return;
-  // u_kk / p_k: the later blocks' updates, and the solves' reverse sweep through Lᵀ
-  if (t < Wv) ud[c0 + t] = 1.0 / (S[t * SLD + t] * ps(c0 + t));
+  // ldl64_core's first barrier orders the S image and the sweep stores above
+  ldl64_core(S, Kb, ld, perm + (size_t)b * nmax, dinv + (size_t)b * dstride + (size_t)(c0 / 32) * DBLK, meta + b, c0,
+             Np, mm.nsys, binv + (size_t)b * BSTR, w0b, w1b, bound, ps, ud);
 }
 
-template <class SRC, bool LDL>
+template <class SRC>
 __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_ldiag_kernel(
     double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
     size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv, double* __restrict__ ukp,
     double* __restrict__ w0, double* __restrict__ w1, double* __restrict__ kamax, const double* __restrict__ kls,
     int n, int m, SRC src, int b0) {
   __shared__ double S[STEP_LDS];
-  ldiag_body<SRC, LDL>(S, b0 + (int)blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, c0, binv, ukp, w0, w1,
+  ldiag_body<SRC>(S, b0 + (int)blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, c0, binv, ukp, w0, w1,
                        kamax, kls, n, m, src);
 }
 
@@ -1997,7 +1988,7 @@ __device__ __forceinline__ void stage_rowstrip_n(double* X, const double* Kb, in
 // Tiles it0 .. it0+TW−1 (from tile `toff` on) of block column J = c0 / 64 of
 // problem b (X: the workgroup's TW × NB64·TLD doubles of LDS);
 // nlu_lcol_kernel runs them for a batch, nlu_left_all_kernel inside its loop.
-template <class SRC, int TW, bool PF = true>
+template <class SRC, int TW = 1, bool PF = false>
 __device__ __forceinline__ void lcol_body(
     double (*X)[NB64 * TLD], int b, int it0, double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta,
     int c0, const double* __restrict__ binv, const double* __restrict__ ukp, int cnt, int toff,
@@ -2143,7 +2134,7 @@ __device__ __forceinline__ void lcol_body(
   if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;   // every writer stores the same value
 }
 
-template <class SRC, int TW, bool PF>
+template <class SRC, int TW = 1, bool PF = false>
 __global__ __launch_bounds__(256 * TW) __attribute__((amdgpu_waves_per_eu(4))) void nlu_lcol_kernel(
     double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
     const double* __restrict__ ukp, int ngrp, int cnt, int toff, int total, const double* __restrict__ kamax,
@@ -2155,51 +2146,6 @@ __global__ __launch_bounds__(256 * TW) __attribute__((amdgpu_waves_per_eu(4))) v
   const int bl = logical / ngrp;
   lcol_body<SRC, TW, PF>(X, b0 + bl, (logical - bl * ngrp) * TW, K, ld, nmax, meta, c0, binv, ukp, cnt, toff,
                          kamax, kls, n, m, src);
-}
-
-// The whole left-looking factorisation of one problem per workgroup, block
-// column by block column: the diagonal step, then the column's tiles one
-// after another (env DOPT_LPERSIST=1).  No launch boundary and no
-// inter-workgroup dependence: the four problems a CU holds drift into
-// different phases, so one's latency-bound diagonal elimination (VALU / LDS)
-// shares the CU with another's column tiles (MFMA / memory) instead of every
-// workgroup of a launch being in the same phase.  One packed-inverse buffer
-// per problem (the steps of a problem are ordered within its workgroup).
-// the two steps as separate functions (not inlined: each body gets its own
-// register allocation instead of one spilling allocation for both)
-template <class SRC>
-__device__ __noinline__ void ldiag_call(double* S, int b, double* K, int ld, int nmax, int32_t* perm, double* dinv,
-                                        size_t dstride, QPMeta* meta, int c0, double* binv, double* ukp, double* w0,
-                                        double* w1, double* kamax, const double* kls, int n, int m, const SRC& src) {
-  ldiag_body<SRC, true>(S, b, K, ld, nmax, perm, dinv, dstride, meta, c0, binv, ukp, w0, w1, kamax, kls, n, m, src);
-}
-template <class SRC>
-__device__ __noinline__ void lcol_call(double* S, int b, int it, double* K, int ld, int nmax, QPMeta* meta, int c0,
-                                       const double* binv, const double* ukp, int cnt, const double* kamax,
-                                       const double* kls, int n, int m, const SRC& src) {
-  lcol_body<SRC, 1>(reinterpret_cast<double (*)[NB64 * TLD]>(S), b, it, K, ld, nmax, meta, c0, binv, ukp, cnt, 0,
-                    kamax, kls, n, m, src);
-}
-
-template <class SRC>
-__global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_left_all_kernel(
-    double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
-    size_t dstride, QPMeta* __restrict__ meta, double* __restrict__ binv, double* __restrict__ ukp,
-    double* __restrict__ w0, double* __restrict__ w1, double* __restrict__ kamax, const double* __restrict__ kls,
-    int n, int m, SRC src, int npmax) {
-  static_assert(STEP_LDS == NB64 * TLD, "one LDS buffer serves both steps");
-  __shared__ double S[STEP_LDS];
-  const int b = (int)blockIdx.x;
-  const int Np = nlu_np(meta[b]);   // 0 for a problem off the blocked route: every step returns at once
-  for (int c0 = 0; c0 < npmax && c0 < Np; c0 += NB64) {
-    ldiag_call<SRC>(S, b, K, ld, nmax, perm, dinv, dstride, meta, c0, binv, ukp, w0, w1, kamax, kls, n, m, src);
-    __syncthreads();   // the step's stores (this workgroup's own) before the tiles read them; S reused
-    const int ntile = (Np - c0 - NB64 + 63) / 64;
-    for (int it = 0; it < ntile; ++it) {
-      lcol_call<SRC>(S, b, it, K, ld, nmax, meta, c0, binv, ukp, ntile, kamax, kls, n, m, src);
-      __syncthreads();
-    }
-  }
 }
 
 // U of the left-looking route's P-symmetric factors, materialised from L for
@@ -2248,11 +2194,11 @@ __global__ __launch_bounds__(256) void nlu_sym_u_kernel(double* __restrict__ K, 
 
 // The left-looking LU of a P-symmetric batch (every blocked problem sym), its
 // entries read from `src` (QP inputs, or the NLP inputs through R): per block
-// column J the diagonal launch and the column's tiles.  Two streams
-// (lstreams): the tiles I ≥ J+2 of column J run on `aux` beside ldiag(J+1)
-// (which needs only tile (J+1, J) of this column, on the main stream); the
-// main stream joins them before the next column's first tile (it reads
-// (J+2, J)).
+// column J the diagonal launch and the column's tiles, on the handle's stream.
+// (Round 4 measured and dropped: the column tiles I ≥ J+2 on a second stream
+// beside ldiag(J+1); one workgroup per problem for the whole factorisation;
+// two skewed half-batch chains; two tiles per workgroup; the next strip
+// prefetched into registers — DESIGN.md §6.)
 template <class SRC>
 static void left_lu(Handle& h, const SRC& src, double* dinv, double* w0, double* w1, const double* kls,
                     double* kamax) {
@@ -2267,105 +2213,20 @@ static void left_lu(Handle& h, const SRC& src, double* dinv, double* w0, double*
   h.ukp_valid = true;
   h.u_missing = true;   // U is not stored (qp_nopiv_materialize_u when a solve needs it)
   double* ukp = h.ukp.as<double>();
-  hipStream_t S = h.stream, T = h.stream;
-  if (h.lstreams) {
-    ensure_aux(h);
-    T = h.aux;
-    if (h.crit) {   // the chain on the high-priority stream, forked from / joined back into h.stream
-      S = h.crit;
-      DOPT_CHECK_HIP(hipEventRecord(h.ev_crit, h.stream));
-      DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_crit, 0));
-    }
-  }
-  auto lcol =[&](hipStream_t st, int c0, double* bv, int toff, int cnt, int b0, int Bs) {
-    if (cnt <= 0) return;
-    const int tw = h.lcol_tw == 2 && cnt > 1 ? 2 : 1;   // tiles per workgroup
-    const int ngrp = (cnt + tw - 1) / tw;
-    const long long tot = (long long)ngrp * Bs;
-    if (tot > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
-    if (tw == 2)
-      hipLaunchKernelGGL((nlu_lcol_kernel<SRC, 2, true>), dim3((unsigned)tot), dim3(512), 0, st, K, h.ld, h.nmax, meta,
-                         c0, bv, ukp, ngrp, cnt, toff, (int)tot, kamax, kls, h.n, h.m, src, b0);
-    else if (h.lcol_pf)
-      hipLaunchKernelGGL((nlu_lcol_kernel<SRC, 1, true>), dim3((unsigned)tot), dim3(256), 0, st, K, h.ld, h.nmax, meta,
-                         c0, bv, ukp, ngrp, cnt, toff, (int)tot, kamax, kls, h.n, h.m, src, b0);
-    else
-      hipLaunchKernelGGL((nlu_lcol_kernel<SRC, 1, false>), dim3((unsigned)tot), dim3(256), 0, st, K, h.ld, h.nmax,
-                         meta, c0, bv, ukp, ngrp, cnt, toff, (int)tot, kamax, kls, h.n, h.m, src, b0);
-    DOPT_CHECK_HIP(hipGetLastError());
-  };
-  auto ldiag = [&](hipStream_t st, int c0, double* bv, int b0, int Bs) {
-    if (h.ldl_mode)
-      hipLaunchKernelGGL((nlu_ldiag_kernel<SRC, true>), dim3(Bs), dim3(PNT), 0, st, K, h.ld, h.nmax, perm, dinv,
-                         dstride, meta, c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src, b0);
-    else
-      hipLaunchKernelGGL((nlu_ldiag_kernel<SRC, false>), dim3(Bs), dim3(PNT), 0, st, K, h.ld, h.nmax, perm, dinv,
-                         dstride, meta, c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src, b0);
-    DOPT_CHECK_HIP(hipGetLastError());
-  };
+  hipStream_t S = h.stream;
   auto binv_of = [&](int c0) { return h.binv.as<double>() + (size_t)((c0 / NB64) & 1) * B * BSTR; };
-  if (h.lpersist && T == S) {   // one workgroup per problem for the whole factorisation (env DOPT_LPERSIST=1)
-    hipLaunchKernelGGL(nlu_left_all_kernel<SRC>, dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv, dstride, meta,
-                       h.binv.as<double>(), ukp, w0, w1, kamax, kls, h.n, h.m, src, npmax);
-    DOPT_CHECK_HIP(hipGetLastError());
-    return;
-  }
-  if (h.lslices == 2 && B >= 64 && T == S) {
-    // two batch halves, each its own chain on its own stream, the second one
-    // launch behind the first: a half's diagonal launch (VALU / latency
-    // bound) then shares the CUs with the other half's column tiles (MFMA /
-    // memory bound) instead of running alone (env DOPT_LSLICE=2)
-    ensure_aux(h);
-    const int B0 = B / 2;
-    hipStream_t st2 = h.aux;
-    for (int half = 0; half < 2; ++half) {
-      const int b0 = half ? B0 : 0, Bs = half ? B - B0 : B0;
-      hipStream_t st = half ? st2 : S;
-      for (int c0 = 0; c0 < npmax; c0 += NB64) {
-        ldiag(st, c0, binv_of(c0), b0, Bs);
-        if (half == 0 && c0 == 0) {   // the second half starts after the first half's first diagonal launch
-          DOPT_CHECK_HIP(hipEventRecord(h.ev_fork, S));
-          DOPT_CHECK_HIP(hipStreamWaitEvent(st2, h.ev_fork, 0));
-        }
-        const int ntile = (npmax - c0 - NB64 + 63) / 64;
-        if (ntile <= 0) break;
-        lcol(st, c0, binv_of(c0), 0, ntile, b0, Bs);
-      }
-    }
-    DOPT_CHECK_HIP(hipEventRecord(h.ev_join, st2));
-    DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_join, 0));
-    return;
-  }
-  bool pending = false;   // T holds column tiles S must wait for
   for (int c0 = 0; c0 < npmax; c0 += NB64) {
     double* bv = binv_of(c0);
-    ldiag(S, c0, bv, 0, B);
+    hipLaunchKernelGGL((nlu_ldiag_kernel<SRC>), dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv, dstride, meta,
+                       c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src, 0);
+    DOPT_CHECK_HIP(hipGetLastError());
     const int ntile = (npmax - c0 - NB64 + 63) / 64;
     if (ntile <= 0) break;
-    if (T == S) {
-      lcol(S, c0, bv, 0, ntile, 0, B);
-      continue;
-    }
-    if (pending) {   // column J−1's tiles I ≥ J+1 (tile (J+1, J−1) feeds this column)
-      DOPT_CHECK_HIP(hipEventRecord(h.ev_join, T));
-      DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_join, 0));
-      pending = false;
-    }
-    DOPT_CHECK_HIP(hipEventRecord(h.ev_fork, S));   // T: after ldiag(J) (and, in S order, all before it)
-    DOPT_CHECK_HIP(hipStreamWaitEvent(T, h.ev_fork, 0));
-    lcol(S, c0, bv, 0, 1, 0, B);
-    if (ntile > 1) {
-      lcol(T, c0, bv, 1, ntile - 1, 0, B);
-      pending = true;
-    }
-  }
-  if (pending) {
-    DOPT_CHECK_HIP(hipEventRecord(h.ev_join, T));
-    DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_join, 0));
-  }
-  if (S != h.stream) {
-    DOPT_CHECK_HIP(hipEventRecord(h.ev_crit, S));
-    DOPT_CHECK_HIP(hipStreamWaitEvent(h.stream, h.ev_crit, 0));
+    const long long tot = (long long)ntile * B;
+    if (tot > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
+    hipLaunchKernelGGL((nlu_lcol_kernel<SRC>), dim3((unsigned)tot), dim3(256), 0, S, K, h.ld, h.nmax, meta, c0, bv,
+                       ukp, ntile, ntile, 0, (int)tot, kamax, kls, h.n, h.m, src, 0);
+    DOPT_CHECK_HIP(hipGetLastError());
   }
 }
 

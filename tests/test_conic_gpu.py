@@ -629,6 +629,18 @@ def test_split_psd_blocks_batch(SplitConicBatch):
     _synthetic_check(SplitConicBatch, 3, 25, [(4, 10), (4, 15), (1, 5)], 13, "split: PSD blocks", cap=18)
 
 
+@pytest.mark.parametrize("shape", [
+    ("split six-launch: well-posed SOC", 2, 100, [(3, 10)] * 20, 21, None),
+    ("split six-launch: PSD blocks", 3, 25, [(4, 10), (4, 15), (1, 5)], 13, 18),
+], ids=lambda s: s[0])
+def test_split_six_launch_form(SplitConicBatch, monkeypatch, shape):
+    """DOPT_SPLIT_FUSE=0: the six-launch split iteration (separate u / v
+    update kernels) against the oracle, as the fused form is held above."""
+    monkeypatch.setenv("DOPT_SPLIT_FUSE", "0")
+    label, B, n, cones, seed, cap = shape
+    _synthetic_check(SplitConicBatch, B, n, cones, seed, label, cap=cap, minnorm=cap is None)
+
+
 def test_split_zero_rhs_gives_zero(SplitConicBatch):
     test_zero_rhs_gives_zero(SplitConicBatch)
 

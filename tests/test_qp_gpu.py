@@ -399,6 +399,23 @@ def test_csc_staging_matches_dense_and_oracle(QPBatch):
     bad.indices[0] = 99                   # row index out of range
     with pytest.raises(EngineError):
         e2.set_csc(sp.csc_matrix(d["Q"][0]), bad, h, sp.csc_matrix(A[0]), d["z"], d["lam"], d["nu"])
+    # a failed set leaves no model behind: a larger rejected
+    # model (dense G: the packed staging buffer grows, freeing the one the
+    # previous model's inputs lived in) must not be solved with stale inputs
+    big = sp.csc_matrix(d["G"][0] + 1.0)
+    big.indices[5] = 99
+    with pytest.raises(EngineError):
+        e2.set_csc(sp.csc_matrix(d["Q"][0]), big, h, sp.csc_matrix(A[0]), d["z"], d["lam"], d["nu"])
+    with pytest.raises(EngineError):
+        e2.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
+    with pytest.raises(EngineError):
+        e2.reverse(d["dl_dz"])
+    # and a good set afterwards works as before
+    e2.set_csc([sp.csc_matrix(q) for q in d["Q"]], [sp.csc_matrix(g) for g in G], h,
+               [sp.csc_matrix(a) for a in A], d["z"], d["lam"], d["nu"])
+    r3, f3 = e2.forward_reverse(d["dl_dz"], dq=d["dq"], dh=d["dh"], db=d["db"])
+    np.testing.assert_array_equal(r3, r2)
+    np.testing.assert_array_equal(f3, f2)
 
 
 def test_factor_then_reverse_forward(QPBatch, lu_mode):
