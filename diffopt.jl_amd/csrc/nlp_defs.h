@@ -83,6 +83,41 @@ __device__ __forceinline__ int nlp_code(const NLPDims& d, const NLPRed& R, size_
   return rr < n ? kx[rr] : ys[rr - n];
 }
 
+// nlp_R_codes<true> (below) in two steps, for the column tiles that issue all
+// of a tile's loads before any is used: the address of R[r][col] (r > col)
+// and what its loaded value x stands for — 0: the entry is 0 (p is a valid
+// dummy), 1: x, 2: −x.
+__device__ __forceinline__ int nlp_R_ref_lower(const NLPDims& d, const NLPIn& in, const NLPRed& R, size_t b, int r,
+                                               int col, int coder, int codec, const double*& p) {
+  const int n = d.n, N = n + d.c;
+  const bool pad = r >= N || col >= N;
+  const int rr = pad ? 0 : r, cc = pad ? 0 : col;
+  const bool rq = rr < n, cq = cc < n;
+  int mode = 0;
+  p = in.Hxx;
+  if (pad) {
+  } else if (rq) {
+    if (coder < 0 && cq && codec < 0) {
+      mode = 1;
+      p = in.Hxx + b * n * n + (size_t)cc * n + rr;
+    } else if (coder < 0 && !cq && codec != 1) {
+      mode = 1;
+      p = in.Jx + b * d.c * n + (size_t)rr * d.c + (cc - n);
+    }
+  } else if (coder != 1) {
+    if (cq) {
+      if (codec < 0) {
+        mode = 1;
+        p = in.Jx + b * d.c * n + (size_t)cc * d.c + (rr - n);
+      }
+    } else if (cc == rr && coder == 2) {
+      mode = 2;
+      p = R.rho + b * d.c + (rr - n);
+    }
+  }
+  return mode;
+}
+
 // R[r][col] of problem b (identity padding past n + c) from the two index
 // codes (nlp_code of r and of col): one round of unconditional loads (the
 // selected value and δ).  LOWER: r > col is known (the column tiles), so no

@@ -256,35 +256,6 @@ __device__ __forceinline__ double src_val(const NSrcB& v, int r, int c) {
 // with the lanes along r: coalesced as is
 __device__ __forceinline__ double src_val_lower(const NSrcB& v, int r, int c) { return src_val(v, r, c); }
 
-// Column tiles: the index codes of the tile's 64 rows (from r0) and 64 columns
-// (from c0) staged once per workgroup in the padding columns 64..79 of the
-// tile's first LDS rows (int view: row k holds 32 codes at columns 64..79), so
-// each source entry is one round of loads, not two.  QP sources: nothing.
-constexpr int CODE_LD = NB64 + 16;   // = TLD (the tiles' LDS row stride, asserted there)
-__device__ __forceinline__ int* tile_codes(double* X) { return reinterpret_cast<int*>(X + NB64); }
-__device__ __forceinline__ int tile_code(const int* tc, int idx) {   // idx < 128: rows, then columns
-  return tc[(idx >> 5) * (2 * CODE_LD) + (idx & 31)];
-}
-__device__ __forceinline__ void src_stage_codes(const QSrc&, const QSrcB&, double*, int, int) {}
-__device__ __forceinline__ void src_stage_codes(const NSrc& s, const NSrcB& v, double* X, int r0, int c0) {
-  const int t = threadIdx.x;
-  if (t < 128) {
-    const int r = t < 64 ? r0 + t : c0 + (t - 64);
-    int* tc = tile_codes(X);
-    tc[(t >> 5) * (2 * CODE_LD) + (t & 31)] = nlp_code(s.d, s.R, v.b, r);
-  }
-}
-__device__ __forceinline__ double src_val_tile(const QSrcB& v, const double*, int r, int c, int, int) {
-  return kval_lower(v, r, c);
-}
-// (column tiles only: every entry strictly below the diagonal)
-__device__ __forceinline__ double src_val_tile(const NSrcB& v, const double* X, int r, int c, int ri, int ci) {
-  const int* tc = tile_codes(const_cast<double*>(X));
-  return nlp_R_codes<true>(v.s->d, v.s->in, v.s->R, v.b, r, c, tile_code(tc, ri), tile_code(tc, 64 + ci));   // r > c
-}
-template <class SRC> constexpr bool src_staged() { return false; }
-template <> constexpr bool src_staged<NSrc>() { return true; }
-
 // Tile `tile` of the lower triangle (rt ≥ ct) of an nrt × nrt grid, column by
 // column: column 0's nrt tiles first.
 __device__ __forceinline__ void col_lower_tile(int tile, int nrt, int& rt, int& ct) {
@@ -1076,7 +1047,6 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
 // through LDS).  Every U12 entry is held to the growth bound.
 // ---------------------------------------------------------------------------
 constexpr int TLD = 64 + 16;   // LDS row stride (doubles) of a staged 64×64 operand
-static_assert(TLD == CODE_LD, "the NLP tiles' index codes live in TLD's padding columns");
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_trsm_kernel(double* __restrict__ K, int ld, int nmax,
                                                        QPMeta* __restrict__ meta, int c0,
@@ -1627,6 +1597,20 @@ __device__ __forceinline__ void stage_rowstrip(double* X, const double* Kb, int 
   for (int u = 0; u < 16; ++u) X[(kq + u) * TLD + j] = j < rows ? v[u] : 0.0;
 }
 
+typedef __attribute__((address_space(3))) void lds_void;
+// s_waitcnt vmcnt(0) as the compiler's own instruction (an inline-asm wait is
+// opaque to its wait-count tracking, which then still counts the DMA pieces
+// as in flight and drains with vmcnt(0) at every later use of a plain load)
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// one 1-KB LDS-DMA piece: lane l's 16 bytes from g (per lane) to lds + 16·l
+__device__ __forceinline__ void glds16(const double* g, double* lds) {
+  __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)lds, 16, 0, 0);
+}
+// stage image offset of (row r, column k), k < 16
+__device__ __forceinline__ int lc_off(int r, int k) { return r * 16 + ((((k >> 1) ^ (r >> 1)) & 7) << 1) + (k & 1); }
+// U_JJ⁻¹ image offset of (row j, column c)
+__device__ __forceinline__ int lc_uoff(int j, int c) { return j * NB64 + (c ^ ((j & 1) << 4)); }
+
 // ---------------------------------------------------------------------------
 // The diagonal block of the left-looking route as ONE symmetric elimination
 // (default; DOPT_LDL=0: diag_core).  S = P_J·C(J, J) is symmetric (P·K
@@ -1718,7 +1702,9 @@ __device__ __forceinline__ void ldl64_core(double* buf, double* __restrict__ Kb,
         V[lane] = a[kk];   // published for the waves below and as F's row k
         wave_sync();
         // the pivot straight from lane k (no LDS round trip on the chain); the
-        // rows below it in this wave read back from the published row
+        // rows below it in this wave read back from the published row (round
+        // 5 measured the column-k entries by v_readlane from lane k instead —
+        // 15 readlane pairs per step: every diagonal launch 7–15 µs slower)
         const double rd = rcp_nr(readlane_d(a[kk], k));
         if (lane == 0) RD[k] = rd;
         // lane k: its rows below k restart from 0 (column k of the right half)
@@ -1762,7 +1748,7 @@ __device__ __forceinline__ void ldl64_core(double* buf, double* __restrict__ Kb,
         D[e] = low ? iv : (i == j ? 1.0 : 0.0);
         D[32 * 32 + e] = low ? 0.0 : iv;
       }
-      if (trsm) Bg[i * NB64 + j] = iv;
+      if (trsm && i <= j) Bg[i * NB64 + j] = iv;   // the column tiles read U11⁻¹ only
     }
     if (__any(bad) && lane == 0) *sbad = 1;   // every writer stores the same value
   }
@@ -1960,192 +1946,255 @@ __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void n
                        kamax, kls, n, m, src);
 }
 
-// stage_rowstrip by NTH threads (NTH = 256 or 512): 16·256/NTH columns each
-// (lane ↔ row: a 16-lane store group writes 16 consecutive rows of one
-// column, conflict-free; a (row, column-quarter) mapping stores 4 rows × 4
-// quarters per group, 4-way)
-template <int NTH>
-__device__ __forceinline__ void stage_rowstrip_n(double* X, const double* Kb, int ld, int c0, int k0) {
-  constexpr int CW = 16 * 256 / NTH;   // columns per thread
-  const int t = threadIdx.x, j = t & 63, kq = (t >> 6) * CW;
-  double v[CW];
-  const double* src = Kb + (size_t)(c0 + j) * ld + k0 + kq;
-#pragma unroll
-  for (int u = 0; u < CW; ++u) v[u] = src[u];
-#pragma unroll
-  for (int u = 0; u < CW; ++u) X[(kq + u) * TLD + j] = v[u];
+// ---------------------------------------------------------------------------
+// Column tiles (I, J), I ≥ J+1, of block column J = c0 / 64: one 256-thread
+// workgroup per tile (XCD-aware order: one problem's tiles are consecutive on
+// an XCD).  Round 5 form — the update computed transposed, with its operands
+// streamed into LDS by LDS-DMA while the previous stage's MFMAs run:
+//
+//   Xᵀ(J, I) = Σ_{k<J} L(J, k)·D_k·L(I, k)ᵀ          (wave w: columns i of 16w..16w+15)
+//   Cᵀ       = A(I, J)ᵀ − P_J·Xᵀ                       (sources read in the accumulator layout)
+//   L(I, J)ᵀ = U_JJ⁻ᵀ·Cᵀ                               (the accumulators ARE the B operands)
+//
+// The k-loop runs in stages of 16 columns: the stage's 64 tile rows L(I, k)
+// and 64 strip rows L(J, k) (8 KB each) and its 16 entries of D come into
+// one of two LDS buffers by global_load_lds_dwordx4 (no VGPR destination),
+// issued right after the barrier that frees the buffer, so stage s+1 is in
+// flight during stage s's MFMAs.  Both images are row-major 64 × 16 with the
+// 16-byte granule of column pair k/2 of row r at (k/2) ^ ((r/2) & 7): the
+// MFMA operand reads (lane ↔ row, four k per step) hit 64 distinct banks per
+// half-wave, and the swizzle is applied to the per-lane DMA SOURCE address
+// (the DMA destination is lane-linear).  Transposed, the update's
+// accumulator layout (lane (g, l16), register r ↔ row 4r + g of a 16-row
+// block, column l16) is exactly the TRSM's B-operand layout for its four
+// k-steps, so C needs no transposition through LDS; U_JJ⁻¹ (upper triangle,
+// binv) is DMA'd into LDS after the loop (row stride 64, odd rows shifted by
+// 16 columns: conflict-free A-operand reads).  The sources of the tile are
+// issued during the last stage's MFMAs.  L(I, J) → K with the threshold test
+// and the growth bound on U(J, I) = D_J·L(I, J)ᵀ·P_I (U is not stored:
+// nlu_sym_u_kernel when a solve needs it).
+// ---------------------------------------------------------------------------
+constexpr int LC_IMG = NB64 * 16;        // one 64-row × 16-column stage image (doubles)
+constexpr int LC_STAGE = 2 * LC_IMG;     // tile rows' image, then the strip's
+constexpr int LC_DS = 2 * LC_STAGE;      // D slices of the two buffers (128 doubles each: one DMA piece)
+constexpr int LC_P = LC_DS + 256;        // p_j of block J
+constexpr int LC_UD = LC_P + NB64;       // u_jj / p_j of block J
+constexpr int LC_CODES = LC_UD + NB64;   // NLP: the tile's 128 index codes (int)
+constexpr int LC_LDS = LC_CODES + 64;
+static_assert(NB64 * NB64 <= LC_DS, "U_JJ⁻¹'s image reuses the stage buffers");
+static_assert(LC_LDS * 8 <= 40 * 1024, "four workgroups per CU");
+
+
+template <class SRC> constexpr bool src_staged() { return false; }   // the tile's sources need its index codes
+template <> constexpr bool src_staged<NSrc>() { return true; }
+__device__ __forceinline__ const int* lc_codes(const double* X) {
+  return reinterpret_cast<const int*>(X + LC_CODES);
+}
+__device__ __forceinline__ void src_stage_codes(const QSrc&, const QSrcB&, double*, int, int) {}
+__device__ __forceinline__ void src_stage_codes(const NSrc& s, const NSrcB& v, double* X, int r0, int c0) {
+  const int t = threadIdx.x;
+  if (t < 128) reinterpret_cast<int*>(X + LC_CODES)[t] = nlp_code(s.d, s.R, v.b, t < 64 ? r0 + t : c0 + (t - 64));
+}
+// A column tile's source entry (r > c) in two steps, so that every load of the
+// tile is issued before any is used: its address, and what the loaded value x
+// stands for — 0: zero (p a valid dummy), 1: x, 2: −x
+// (the sources by value, base and offset selected separately: kval's notes)
+__device__ __forceinline__ int src_ref_tile(QSrcB v, const double*, int r, int c, int, int, const double*& p) {
+  const int n = v.n, nk = v.nk, rn = r - n;
+  const bool pad = r >= v.N || c >= v.N;
+  const bool cq = c < n, rq = r < n, rg = !rq && rn < nk;
+  const bool live = !pad && (cq || (rg && r == c));   // (r == c never holds in a column tile)
+  const int oq = c * n + r, og = c * v.m + rn, oa = c * v.p + (rn - nk);
+  int off = cq ? (rq ? oq : (rg ? og : oa)) : rn;
+  const double* base = cq ? (rq ? v.Q : (rg ? v.gk : v.A)) : v.sk;
+  off = live ? off : 0;
+  base = live ? base : v.Q;
+  p = base + off;
+  return live ? 1 : 0;
+}
+__device__ __forceinline__ int src_ref_tile(const NSrcB& v, const double* X, int r, int c, int ri, int ci,
+                                            const double*& p) {
+  const int* tc = lc_codes(X);
+  return nlp_R_ref_lower(v.s->d, v.s->in, v.s->R, v.b, r, c, tc[ri], tc[64 + ci], p);
 }
 
-// Tiles (I, J), I ≥ J+1, of block column J = c0 / 64: TW tiles per workgroup
-// (256 threads each, tiles I and I+1 when TW = 2, sharing the staged row strip
-// L(J, k) and the U11⁻¹ load; XCD-aware order: one problem's tiles are
-// consecutive).  C(I, J) by MFMA over the staged strips L(J, k) (B operand)
-// and the tile's own row strips L(I, k)·D_k (A operand), then the TRSM by the
-// packed inverse of the diagonal block (binv) with the threshold test and the
-// growth bound on U(J, I) = D_J·L(I, J)ᵀ·P_I; L(I, J) → K (U is not stored:
-// nlu_sym_u_kernel when a solve needs it).  `ngrp` workgroups per problem,
-// `cnt` tiles per problem from tile `toff` on.
-// Tiles it0 .. it0+TW−1 (from tile `toff` on) of block column J = c0 / 64 of
-// problem b (X: the workgroup's TW × NB64·TLD doubles of LDS);
-// nlu_lcol_kernel runs them for a batch, nlu_left_all_kernel inside its loop.
-template <class SRC, int TW = 1, bool PF = false>
-__device__ __forceinline__ void lcol_body(
-    double (*X)[NB64 * TLD], int b, int it0, double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta,
-    int c0, const double* __restrict__ binv, const double* __restrict__ ukp, int cnt, int toff,
-    const double* __restrict__ kamax, const double* __restrict__ kls, int n, int m, const SRC& src) {
-  constexpr int NTH = 256 * TW;
+template <class SRC>
+__device__ __forceinline__ void lcol_body(double* X, int b, int it, double* __restrict__ K, int ld, int nmax,
+                                          QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
+                                          const double* __restrict__ ukp, int cnt,
+                                          const double* __restrict__ kamax, const double* __restrict__ kls, int n,
+                                          int m, const SRC& src) {
   const QPMeta mm = meta[b];
   const int Np = nlu_np(mm);
-  if (mm.lu == LU_REJECT || c0 + NB64 + 64 * (toff + it0) >= Np) return;   // workgroup-uniform
-  const int T = threadIdx.x, half = T >> 8, t = T & 255;
-  const int it = it0 + half;
-  const int r0 = c0 + NB64 + 64 * (toff + it);   // first row of this half's tile I
-  const int sw = it < cnt && r0 < Np ? min(NB64, Np - r0) : 0;   // 0, 32 or 64 rows
-  const int lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
-  const bool wact = 16 * wv < sw;                // wave-uniform
-  double* Xh = X[half];
+  const int r0 = c0 + NB64 + 64 * it;   // first row of tile I
+  if (mm.lu == LU_REJECT || it >= cnt || r0 >= Np) return;   // workgroup-uniform
+  const int sw = min(NB64, Np - r0);   // 32 or 64 rows
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
+  const bool wact = 16 * wv < sw;      // wave-uniform: this wave's 16 columns i of Xᵀ are tile rows
   double* Kb = K + (size_t)b * nmax * ld;
   const double* ud = ukp + (size_t)b * nmax;
   const double* Bg = binv + (size_t)b * BSTR;
   const auto sv = src_bind(src, b, mm);
   const PScale ps = pscale(kls, b, n, m, mm);
-  const double bound = growth_bound(__hip_atomic_load(kamax + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  // NLP: the tile's index codes into LDS (ordered by the k-loop's barriers,
-  // or the one below when there is no k-loop)
-  if (TW == 1) src_stage_codes(src, sv, X[0], r0, c0);
+  // stage s's DMA pieces: wave w fills chunks 2w, 2w+1 (rows 8c..8c+7) of
+  // both images; wave 0 also the 16-entry slice of D (one 128-byte copy per
+  // 8 lanes: the piece is 1 KB)
+  const int rho = lane >> 3, gam = lane & 7;
+  auto issue = [&](int st) {
+    double* buf = X + (st & 1) * LC_STAGE;
+    const int ks = 16 * st;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = 2 * wv + q, r = 8 * c + rho, col = ks + 2 * (gam ^ ((r >> 1) & 7));
+      const int rt = r < sw ? r0 + r : r0;   // rows past a 32-row tile: any valid row (never read)
+      glds16(Kb + (size_t)rt * ld + col, buf + c * 128);
+      glds16(Kb + (size_t)(c0 + r) * ld + col, buf + LC_IMG + c * 128);
+    }
+    if (wv == 0) glds16(ud + ks + 2 * gam, X + LC_DS + (st & 1) * 128);
+  };
+  // U_JJ⁻¹'s image over the stage buffers: 32 pieces of 1 KB (rows 2c,
+  // 2c+1), 8 per wave; odd rows' granules shifted by 8 (16 columns).  Only
+  // the upper triangle is written by the diagonal step (the lower part is
+  // masked on read).
+  auto issue_uinv = [&]() {
+    const int hr = lane >> 5, gq = lane & 31;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = 8 * wv + q, j = 2 * c + hr, gs = gq ^ (hr << 3);
+      // granules wholly below the diagonal are not loaded (their lines were
+      // not written by the diagonal step: stale, an HBM read)
+      if (2 * gs + 1 >= j) glds16(Bg + j * NB64 + 2 * gs, X + c * 128);
+    }
+  };
+  double av[4][4];   // A(I, J)ᵀ in the accumulator layout
+  uint32_t amode = 0;   // 2 bits per entry: what av stands for (src_ref_tile)
+  auto load_sources = [&]() {
+    if (wact) {
+      const int ri = 16 * wv + l16;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const double* sp;
+          const int md = src_ref_tile(sv, X, r0 + ri, c0 + 16 * c + g + 4 * rr, ri, 16 * c + g + 4 * rr, sp);
+          av[c][rr] = gload(sp, 0);
+          amode |= (uint32_t)md << (2 * (4 * c + rr));
+        }
+    }
+    asm volatile("" ::: "memory");   // compiler-only fence: the loads above stay issued together
+  };
+  const int nst = c0 >> 4;
+  if (nst > 0) {
+    issue(0);
+  } else {   // no k-loop: U_JJ⁻¹, the sources (QP) and the prologue's loads in one round trip
+    issue_uinv();
+    if (!src_staged<SRC>()) load_sources();
+  }
+  // block J's p_j and u_jj / p_j, the NLP tile's index codes (in flight with stage 0)
+  // (every load issued before any is used: p from λ_k by index, selected
+  // after the fence — PScale's select right after its load would wait on each)
+  const double* kl = ps.kl ? ps.kl : ud;   // (a valid dummy when every p is 1)
+  const int ip = c0 + (t & 63) - ps.n, ir = r0 + 16 * wv + l16 - ps.n;
+  const bool inp = ps.kl && ip >= 0 && ip < ps.nk, inr = ps.kl && ir >= 0 && ir < ps.nk;
+  const double rp = t < NB64 ? kl[inp ? ip : 0] : ud[c0 + (t & 63)];
+  const double rr_ = kl[inr ? ir : 0];
+  asm volatile("" ::: "memory");
+  const double pv = t < NB64 ? (inp ? rp : 1.0) : rp;   // p_j | u_jj / p_j of block J
+  const double pr = inr ? rr_ : 1.0;                     // p_i of this lane's tile row (growth bound)
+  src_stage_codes(src, sv, X, r0, c0);
+  if (t < 2 * NB64) X[LC_P + t] = pv;   // LC_UD = LC_P + 64
   d4n acc[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = (d4n){0, 0, 0, 0};
-  // the staged strip L(J, k) of the next k-block is loaded into registers
-  // while this one's MFMAs run (plain loads survive the barriers; stored to
-  // LDS after the barrier that retires this one): the stage is one LDS write
-  // pass, not a global round trip, per k-block (env DOPT_LCOL_PF=1; measured
-  // slower: config 3 LU 34.4 -> 37.3 ms, config 2 0.81 -> 0.83 ms — off)
-  constexpr int CW = 16 * 256 / NTH;   // strip columns per thread
-  const int sj = T & 63, skq = (T >> 6) * CW;
-  const double* srow = Kb + (size_t)(c0 + sj) * ld + skq;
-  double snx[CW];
-  if (PF && c0 > 0) {
+  auto stage = [&](int st) {
+    if (!wact) return;
+    const double* TI = X + (st & 1) * LC_STAGE;
+    const double* SI = TI + LC_IMG;
+    const double* DS = X + LC_DS + (st & 1) * 128;
 #pragma unroll
-    for (int u = 0; u < CW; ++u) snx[u] = srow[u];
+    for (int kk = 0; kk < 4; ++kk) {
+      const int k = 4 * kk + g;
+      const double bo = TI[lc_off(16 * wv + l16, k)] * DS[k];   // L(I)[i][k]·d_k
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = nmfma(SI[lc_off(16 * c + l16, k)], bo, acc[c]);
+    }
+  };
+  for (int st = 0; st + 1 < nst; ++st) {
+    vm_drain();   // this wave's pieces of stage st landed
+    __syncthreads();                                    // everyone's; buffer (st + 1) & 1 is free
+    issue(st + 1);
+    stage(st);
   }
-  for (int k0 = 0; k0 < c0; k0 += NB64) {
-    double a[16];   // loaded with the staging loads (one round trip per k-block)
-    if (wact) {
-      const double* ar = Kb + (size_t)(r0 + 16 * wv + l16) * ld + k0;
-#pragma unroll
-      for (int s = 0; s < 16; ++s) a[s] = ar[4 * s + g] * ud[k0 + 4 * s + g];
-    }
+  if (nst > 0) {   // the last stage: the tile's sources in flight during its MFMAs
+    vm_drain();
     __syncthreads();
-    if (PF) {
-#pragma unroll
-      for (int u = 0; u < CW; ++u) X[0][(skq + u) * TLD + sj] = snx[u];
-      if (k0 + NB64 < c0) {
-#pragma unroll
-        for (int u = 0; u < CW; ++u) snx[u] = srow[k0 + NB64 + u];
-      }
-    } else {
-      stage_rowstrip_n<NTH>(X[0], Kb, ld, c0, k0);   // block J is full (tiles follow it)
-    }
-    __syncthreads();
-    if (wact) {
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        double bq[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) bq[q] = X[0][(4 * s + g) * TLD + 16 * q + l16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = nmfma(a[s], bq[q], acc[q]);
-      }
-    }
+    load_sources();
+    stage(nst - 1);
+    __syncthreads();   // the stage buffers are consumed: U_JJ⁻¹'s image
+    issue_uinv();
+  } else {
+    __syncthreads();   // p / u_jj / the codes visible
+    if (src_staged<SRC>()) load_sources();   // (NLP: by the codes)
   }
-  // C = A − acc·P_J in the TRSM's A-operand layout (lane ↔ row 16wv + l16,
-  // k-step s ↔ column 4s + g): the sources read with the lanes along the
-  // rows, the update transposed through LDS.  The transposing buffer is
-  // XOR-swizzled (column c of row r at c ^ (r & 14)): the read walks 16 rows
-  // of one column, which TLD = 80 (row stride ≡ 32 banks) put on two bank
-  // pairs — an 8-way conflict; swizzled, the 32 lanes of a half-wave hit 64
-  // distinct banks (lds_bank_conflict / lds_idx_active
-  // 0.556 on config 2)
-  // U11⁻¹ (L2) loaded together with the sources: one round trip
-  constexpr int VQ = 16 / TW;
-  double av[16], v[VQ], pj[4];
-#pragma unroll
-  for (int q = 0; q < VQ; ++q) v[q] = Bg[T + NTH * q];
-  if (TW == 1 && src_staged<SRC>() && c0 == 0) __syncthreads();   // the codes (no k-loop)
+  // Cᵀ = A(I, J)ᵀ − P_J·Xᵀ (overwrites the accumulators); the source values
+  // are first used here, after the last stage's MFMAs
   if (wact) {
 #pragma unroll
-    for (int s = 0; s < 16; ++s)
-      av[s] = TW == 1 ? src_val_tile(sv, X[0], r0 + 16 * wv + l16, c0 + 4 * s + g, 16 * wv + l16, 4 * s + g)
-                      : src_val_lower(sv, r0 + 16 * wv + l16, c0 + 4 * s + g);
+    for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) pj[q] = ps(c0 + 16 * q + l16);
-  }
-  asm volatile("" ::: "memory");   // compiler-only fence: the loads above stay issued together
-  if (c0 > 0) {   // workgroup-uniform
-    __syncthreads();   // every wave is done with the last staged strip
-    if (wact) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = 16 * q + l16;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int r = 16 * wv + g + 4 * rr;
-          Xh[r * TLD + (j ^ (r & 14))] = acc[q][rr] * pj[q];
-        }
+      for (int rr = 0; rr < 4; ++rr) {
+        // by arithmetic, not selects on the loaded value (those became
+        // branches): ×1, ×−1 or ×0 (a dead entry loads a finite dummy)
+        const uint32_t md = (amode >> (2 * (4 * c + rr))) & 3;
+        const double mul = (double)(int)(md & 1) - (double)(int)(md >> 1);
+        acc[c][rr] = fma(-acc[c][rr], X[LC_P + 16 * c + g + 4 * rr], av[c][rr] * mul);
       }
-    }
-    __syncthreads();
-    if (wact) {
-#pragma unroll
-      for (int s = 0; s < 16; ++s) av[s] -= Xh[(16 * wv + l16) * TLD + ((4 * s + g) ^ ((16 * wv + l16) & 14))];
-    }
-    __syncthreads();   // every wave holds its C rows before U11⁻¹ overwrites X[0]
   }
-#pragma unroll
-  for (int q = 0; q < VQ; ++q) {   // U11⁻¹: upper triangle, zero below
-    const int e = T + NTH * q, k = e >> 6, c = e & 63;
-    X[0][k * TLD + c] = k <= c ? v[q] : 0.0;
-  }
+  vm_drain();
   __syncthreads();
   if (!wact) return;   // no barrier below
+  // L(I, J)ᵀ block a = Σ_{c ≤ a} U⁻ᵀ(a, c)·Cᵀ(c, w): A operand U⁻¹[j][j'] (j = 16c + 4s + g,
+  // j' = 16a + l16; zero below the diagonal), B operand Cᵀ's register s of block c
   d4n lt[4];
   int over = 0;
+  const double bound = growth_bound(__hip_atomic_load(kamax + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {   // U11⁻¹ is upper: k ≤ 16ct + 15
-    lt[ct] = (d4n){0, 0, 0, 0};
+  for (int a = 0; a < 4; ++a) {
+    lt[a] = (d4n){0, 0, 0, 0};
 #pragma unroll
-    for (int s = 0; s < 4 * (ct + 1); ++s) lt[ct] = nmfma(av[s], X[0][(4 * s + g) * TLD + 16 * ct + l16], lt[ct]);
+    for (int c = 0; c <= a; ++c)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int j = 16 * c + 4 * s + g, jp = 16 * a + l16;
+        const double u = X[lc_uoff(j, jp)];
+        lt[a] = nmfma(c < a || j <= jp ? u : 0.0, acc[c][s], lt[a]);
+      }
   }
+  const int ri = 16 * wv + l16;
+  double* krow = Kb + (size_t)(r0 + ri) * ld + c0;
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct)
+  for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
-      Kb[(size_t)(r0 + 16 * wv + g + 4 * rr) * ld + c0 + 16 * ct + l16] = lt[ct][rr];
-      over |= !(fabs(lt[ct][rr]) <= NOPIV_LMAX);
+      const double l = lt[a][rr], uk = X[LC_UD + 16 * a + g + 4 * rr];
+      krow[16 * a + g + 4 * rr] = l;
+      // |l| ≤ NOPIV_LMAX, and U(J, I)[j'][i] = (u_j'j' / p_j')·l·p_i within the growth bound
+      over |= (int)!(fabs(l) <= NOPIV_LMAX) | (int)!(fabs(uk * l * pr) <= bound);
     }
-  // U(J, I)[k][jl] = (u_kk / p_k)·L[jl][k]·p_jl: the growth bound
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    const double uk = ud[c0 + 16 * ct + l16];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) over |= !(fabs(uk * lt[ct][rr] * ps(r0 + 16 * wv + g + 4 * rr)) <= bound);
-  }
   if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;   // every writer stores the same value
 }
 
-template <class SRC, int TW = 1, bool PF = false>
-__global__ __launch_bounds__(256 * TW) __attribute__((amdgpu_waves_per_eu(4))) void nlu_lcol_kernel(
+template <class SRC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_lcol_kernel(
     double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
-    const double* __restrict__ ukp, int ngrp, int cnt, int toff, int total, const double* __restrict__ kamax,
-    const double* __restrict__ kls, int n, int m, SRC src, int b0) {
-  __shared__ double X[TW][NB64 * TLD];   // X[0]: staged strip / U11⁻¹ (shared); X[h]: tile h's transposes
+    const double* __restrict__ ukp, int ntile, int total, const double* __restrict__ kamax,
+    const double* __restrict__ kls, int n, int m, SRC src) {
+  __shared__ double X[LC_LDS];   // one LDS object (a second one can make the compiler drain the DMA early)
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
   const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
-  const int bl = logical / ngrp;
-  lcol_body<SRC, TW, PF>(X, b0 + bl, (logical - bl * ngrp) * TW, K, ld, nmax, meta, c0, binv, ukp, cnt, toff,
-                         kamax, kls, n, m, src);
+  const int bl = logical / ntile;
+  lcol_body<SRC>(X, bl, logical - bl * ntile, K, ld, nmax, meta, c0, binv, ukp, ntile, kamax, kls, n, m, src);
 }
 
 // U of the left-looking route's P-symmetric factors, materialised from L for
@@ -2225,7 +2274,7 @@ static void left_lu(Handle& h, const SRC& src, double* dinv, double* w0, double*
     const long long tot = (long long)ntile * B;
     if (tot > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
     hipLaunchKernelGGL((nlu_lcol_kernel<SRC>), dim3((unsigned)tot), dim3(256), 0, S, K, h.ld, h.nmax, meta, c0, bv,
-                       ukp, ntile, ntile, 0, (int)tot, kamax, kls, h.n, h.m, src, 0);
+                       ukp, ntile, (int)tot, kamax, kls, h.n, h.m, src);
     DOPT_CHECK_HIP(hipGetLastError());
   }
 }

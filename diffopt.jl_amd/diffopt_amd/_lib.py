@@ -10,6 +10,9 @@ import os
 
 LIB_NAME = "libdiffopt_mi355x.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# A/B builds of the same engine (tools/build_variant.sh): DOPT_LIB names one
+# in place of the default in-tree library (benchmarking only)
+LIB_PATH = os.environ.get("DOPT_LIB") or LIB_PATH
 
 DOPT_KIND_QP = 0
 DOPT_KIND_CONIC = 1

@@ -4,7 +4,7 @@
 // and with -DLDIAG_STAMPS the diagonal kernel's phases (thread 0's s_memtime
 // at LD_MARK k, averaged over the workgroups of each launch).
 //   hipcc --offload-arch=gfx950 -O3 -DLDIAG_STAMPS tools/probe/ldiag_probe.hip -o ldiag
-//   ./ldiag B NP LDL(1|0)
+//   ./ldiag B NP
 #include "../../diffopt.jl_amd/csrc/qp_nopiv.hip"
 #include <cstdio>
 #include <cstdlib>
@@ -22,7 +22,7 @@ using namespace dopt;
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 1024;
   const int Np = argc > 2 ? atoi(argv[2]) : 320;
-  const int ldl = argc > 3 ? atoi(argv[3]) : 1;
+  const int ldl = 1;
   const int nmax = Np, ld = Np, n = Np;
   std::vector<double> hQ((size_t)B * n * n);
   unsigned s = 12345;
@@ -80,12 +80,8 @@ int main(int argc, char** argv) {
     hipEventRecord(ev[e++]);
     for (int c0 = 0, J = 0; c0 < Np; c0 += 64, ++J) {
       double* bv = binv + (size_t)(J & 1) * B * BSTR;
-      if (ldl)
-        hipLaunchKernelGGL((nlu_ldiag_kernel<QSrc, true>), dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
-                           dinv_stride(nmax), meta, c0, bv, ukp, nullptr, nullptr, kamax, nullptr, n, 0, src, 0);
-      else
-        hipLaunchKernelGGL((nlu_ldiag_kernel<QSrc, false>), dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
-                           dinv_stride(nmax), meta, c0, bv, ukp, nullptr, nullptr, kamax, nullptr, n, 0, src, 0);
+      hipLaunchKernelGGL((nlu_ldiag_kernel<QSrc>), dim3(B), dim3(PNT), 0, 0, K, ld, nmax, perm, dinv,
+                         dinv_stride(nmax), meta, c0, bv, ukp, nullptr, nullptr, kamax, nullptr, n, 0, src, 0);
       hipEventRecord(ev[e++]);
 #ifdef LDIAG_STAMPS
       if (r == reps) {
@@ -101,8 +97,8 @@ int main(int argc, char** argv) {
       const int ntile = (Np - c0 - 64 + 63) / 64;
       if (ntile > 0) {
         const int tot = ntile * B;
-        hipLaunchKernelGGL((nlu_lcol_kernel<QSrc, 1, true>), dim3(tot), dim3(256), 0, 0, K, ld, nmax, meta, c0, bv, ukp,
-                           ntile, ntile, 0, tot, kamax, nullptr, n, 0, src, 0);
+        hipLaunchKernelGGL((nlu_lcol_kernel<QSrc>), dim3(tot), dim3(256), 0, 0, K, ld, nmax, meta, c0, bv, ukp,
+                           ntile, tot, kamax, nullptr, n, 0, src);
       }
       hipEventRecord(ev[e++]);
     }
