@@ -1081,6 +1081,15 @@ int dopt_conic_forward_reverse(dopt_handle* h, const double* dA, const double* d
   });
 }
 
+int dopt_conic_set_maxiter(dopt_handle* h, int32_t maxiter) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_CONIC) throw Error(-1, "dopt_conic_set_maxiter on a non-conic handle");
+    if (maxiter < 0) throw Error(-1, "maxiter must be >= 0");
+    h->lsqr_cap = maxiter;
+    return 0;
+  });
+}
+
 int dopt_conic_lsqr_stats(dopt_handle* h, int32_t* stats) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_CONIC) throw Error(-1, "dopt_conic_lsqr_stats on a non-conic handle");

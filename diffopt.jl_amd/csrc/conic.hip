@@ -797,7 +797,7 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
     const double* __restrict__ b, const double* __restrict__ c,
     const double* __restrict__ v, const double* __restrict__ P, int plen, int m, int n,
     const double* __restrict__ rhs, double rhs_zero_tol, double* __restrict__ work,
-    double* __restrict__ xout, int32_t* __restrict__ info, double* __restrict__ norms) {
+    double* __restrict__ xout, int32_t* __restrict__ info, double* __restrict__ norms, int maxiter) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ double red[4];
   __shared__ ConeDesc cones[128];
@@ -853,7 +853,6 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
       double anorm = 0.0, ddnorm = 0.0, res2 = 0.0, xxnorm = 0.0, zz = 0.0;
       double sn2 = 0.0, cs2 = -1.0, rhobar = alpha, phibar = beta;
       const double bnorm = beta;
-      const int maxiter = N;
       while (it < maxiter) {
         ++it;
         M_apply(pr, cn, ncones, vv, tmp, s1, s2, s4, lds, red, ys);
@@ -956,7 +955,7 @@ __global__ __launch_bounds__(CTPB) __attribute__((amdgpu_waves_per_eu(2))) void 
     const double* __restrict__ rhs_f, double tol_f, const double* __restrict__ rhs_r, double tol_r,
     double* __restrict__ work, double* __restrict__ xout_f, double* __restrict__ xout_r,
     int32_t* __restrict__ info_f, int32_t* __restrict__ info_r, double* __restrict__ norms_f,
-    double* __restrict__ norms_r) {
+    double* __restrict__ norms_r, int maxiter) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ double red[4];
   __shared__ ConeDesc cones[128];
@@ -1034,7 +1033,6 @@ __global__ __launch_bounds__(CTPB) __attribute__((amdgpu_waves_per_eu(2))) void 
   }
   const double eps = 2.220446049250313e-16;
   const double atol = sqrt(eps), btol = sqrt(eps), ctol = sqrt(eps);
-  const int maxiter = N;
   while (S[0].live || S[1].live) {
     // M·v of the live sequences
     if (S[0].live && S[1].live)
@@ -2185,11 +2183,21 @@ void conic_factor(Handle& h) {
   h.cfactored = true;
 }
 
+// LSQR's iteration limit: IterativeSolvers' maxiter = max(size(M)) = N
+// (ConicProgram.jl:323, 372), or the handle's cap (dopt_conic_set_maxiter: the
+// parity tests compare iterates before the trajectories of an ill-conditioned
+// M can diverge)
+static int lsqr_maxiter(const Handle& h) {
+  const int N = h.n + h.m + 1;
+  return h.lsqr_cap > 0 && h.lsqr_cap < N ? h.lsqr_cap : N;
+}
+
 // Split-path LSQR (see conic_split_* above) of nq sequences per problem
 // (rhs: nq·B right-hand sides, sequence q·B + b), co-iterated for nq = 2.
 static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const double* rhs, double* out0,
                              int32_t* info0, double* out1, int32_t* info1, double* norms0, double* norms1) {
   const int B = (int)h.batch, m = h.m, n = h.n;
+  const int maxit = lsqr_maxiter(h);
   const int V = nq * B;   // sequences
   const int nc = (int)h.cones.size() / 2;
   const int N = n + m + 1;
@@ -2288,12 +2296,12 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
     const size_t dlp = (size_t)2 * n * sizeof(double);
     auto dpiV = [&](int first) {
       hipLaunchKernelGGL(conic_fsplit_dpiV_kernel, dim3(nc, V),
-                         dim3(CTPB), dlv, h.stream, cd, vcone, P, h.dpi_len, h.cc, fs, par, first, N, active, gws,
+                         dim3(CTPB), dlv, h.stream, cd, vcone, P, h.dpi_len, h.cc, fs, par, first, maxit, active, gws,
                          h.psd_big_len, img);
     };
     dpiV(1);
-    for (int it = 0; it < N && left > 0;) {
-      for (int k = 0; k < SPLIT_CHUNK && it < N; ++k, ++it) {
+    for (int it = 0; it < maxit && left > 0;) {
+      for (int k = 0; k < SPLIT_CHUNK && it < maxit; ++k, ++it) {
         hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 0>), dim3(RB, B), dim3(256), 0, h.stream, h.cA, h.cb, h.cc,
                            fs, par, nq);
         hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 1>), dim3(RB, B), dim3(256), dlp, h.stream, h.cA, h.cb, h.cc,
@@ -2309,8 +2317,8 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
       DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
     }
   } else {
-    for (int it = 0; it < N && left > 0;) {
-      for (int k = 0; k < SPLIT_CHUNK && it < N; ++k, ++it) {
+    for (int it = 0; it < maxit && left > 0;) {
+      for (int k = 0; k < SPLIT_CHUNK && it < maxit; ++k, ++it) {
         if (nc)
           hipLaunchKernelGGL(conic_split_dpi_kernel,
                              dim3(nc, V), dim3(CTPB), dl, h.stream, 0, cd, vcone, P, h.dpi_len, ws, st, gws,
@@ -2318,7 +2326,7 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
         pass(0);
         hipLaunchKernelGGL(conic_split_upd_u_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st);
         passT();
-        hipLaunchKernelGGL(conic_split_upd_v_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st, N,
+        hipLaunchKernelGGL(conic_split_upd_v_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st, maxit,
                            active);
       }
       ccheck();
@@ -2355,7 +2363,7 @@ static void conic_lsqr(Handle& h, double tol, double* out) {
   hipLaunchKernelGGL(conic_lsqr_kernel, dim3(B), dim3(CTPB), dpi_lds_bytes(h.cones), h.stream,
                      h.cone_dev.as<ConeDesc>(), nc, h.cA, h.cb, h.cc, h.vp.as<double>(),
                      h.dpi.as<double>(), h.dpi_len, m, n, rhs, tol, h.cwork.as<double>(), out,
-                     h.cinfo.as<int32_t>(), h.cnorm.as<double>());
+                     h.cinfo.as<int32_t>(), h.cnorm.as<double>(), lsqr_maxiter(h));
   ccheck();
 }
 
@@ -2440,7 +2448,7 @@ void conic_forward_reverse(Handle& h, const double* dA, const double* db, const 
     hipLaunchKernelGGL(conic_lsqr2_kernel, dim3(B), dim3(CTPB), dpi_lds_bytes(h.cones), h.stream,
                        h.cone_dev.as<ConeDesc>(), nc, h.cA, h.cb, h.cc, h.vp.as<double>(), h.dpi.as<double>(),
                        h.dpi_len, m, n, rhs_f, 0.0, rhs_r, 1e-4, h.cwork.as<double>(), out_f, out_g,
-                       info + 2 * B, info, nrm + 4 * (size_t)B, nrm);
+                       info + 2 * B, info, nrm + 4 * (size_t)B, nrm, lsqr_maxiter(h));
     ccheck();
   }
   PhaseTimer pt(h, DOPT_PHASE_CONIC_OUTPUT);

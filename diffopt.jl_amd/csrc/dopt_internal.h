@@ -186,6 +186,7 @@ struct Handle {
   DevBuf vp, dpi, cwork, cinfo, cnorm;   // cnorm: LSQR terminal estimates, 8·B doubles
   DevBuf csplit;                // split-path LSQR vectors, partial products, state
   int32_t conic_split = -1;     // -1 auto, 0 persistent kernel, 1 split (env DOPT_CONIC_SPLIT)
+  int32_t lsqr_cap = 0;         // LSQR iteration cap (0: IterativeSolvers' maxiter = N; dopt_conic_set_maxiter)
   int32_t split_fuse = 1;       // split LSQR: 1 four-launch fused iteration, 0 six launches (env DOPT_SPLIT_FUSE)
   int32_t dpi_len = 0;          // doubles per problem of packed Dπ blocks
   int32_t psd_big_len = 0;      // doubles of global scratch per problem / sequence for PSD sides > 64

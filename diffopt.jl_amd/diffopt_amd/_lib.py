@@ -51,6 +51,7 @@ SIGNATURES = {
     "dopt_qp_forward_k": (ctypes.c_int, [_h, ctypes.c_int32] + [ctypes.c_void_p] * 7),
     "dopt_conic_forward_reverse": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 10),
     "dopt_conic_lsqr_stats": (ctypes.c_int, [_h, ctypes.c_void_p]),
+    "dopt_conic_set_maxiter": (ctypes.c_int, [_h, ctypes.c_int32]),
     "dopt_conic_lsqr_norms": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_lhs_solve": (ctypes.c_int, [_h, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_int32]),

@@ -162,6 +162,11 @@ class ConicBatch:
             rA = rA.transpose(0, 2, 1) if not dev else rA.transpose(1, 2)
         return (out, fdx), (g, rA, rb, rc_)
 
+    def set_maxiter(self, maxiter):
+        """Cap LSQR at ``maxiter`` iterations (0: the reference's default
+        max(size(M))) — dopt_conic_set_maxiter."""
+        _lib.check(self.lib.dopt_conic_set_maxiter(self.h, int(maxiter)), self.h)
+
     def lsqr_stats(self):
         """(istop, iterations) of the last run and, after ``forward_reverse``,
         of its forward run: dict of (B,) arrays."""

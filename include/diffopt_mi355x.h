@@ -255,6 +255,12 @@ int dopt_conic_forward_reverse(dopt_handle* h, const double* dA, const double* d
                                const double* dc, const double* dx, double* out,
                                double* out_dx, double* out_g, double* out_dA,
                                double* out_db, double* out_dc);
+/* Caps LSQR at `maxiter` iterations (0 restores the reference's default,
+ * IterativeSolvers' maxiter = max(size(M)) = n + m + 1: ConicProgram.jl:323,
+ * :372); a run that reaches the cap reports istop 7.  A parity instrument:
+ * on an ill-conditioned M, where the converged outputs depend on rounding,
+ * the iterates at a fixed small k are still comparable to 1e-6. */
+int dopt_conic_set_maxiter(dopt_handle* h, int32_t maxiter);
 /* LSQR statistics of the last conic call, 4·B int32: [istop | iterations] of
  * the last (or, after dopt_conic_forward_reverse, the reverse) run, then
  * [istop | iterations] of the forward run of dopt_conic_forward_reverse. */

@@ -101,11 +101,12 @@ def forward_rhs(cache, dA=None, db=None, dc=None):
                            [-(dc @ u) - (db @ vp)]])
 
 
-def forward_differentiate(cache, dA=None, db=None, dc=None, return_info=False, stats=None):
+def forward_differentiate(cache, dA=None, db=None, dc=None, return_info=False, stats=None, maxiter=None):
     """``forward_differentiate!`` (ConicProgram.jl:257-334).
 
     Returns ``(dx, du, dv, dw)`` where ``dx = −(du − x·dw)`` is
-    ``ForwardVariablePrimal`` (:403-412).
+    ``ForwardVariablePrimal`` (:403-412).  ``maxiter`` caps LSQR (default:
+    IterativeSolvers' max(size(M)); the engine's dopt_conic_set_maxiter).
     """
     RHS = forward_rhs(cache, dA, db, dc)
     N = RHS.shape[0]
@@ -114,7 +115,7 @@ def forward_differentiate(cache, dA=None, db=None, dc=None, return_info=False, s
         dz = np.zeros(N)
     else:
         dz, it, istop = lsqr(cache.matvec, cache.rmatvec, RHS, N,
-                             return_info=True, stats=stats)
+                             return_info=True, stats=stats, maxiter=maxiter)
         info = (it, istop)
     n, m = cache.n, cache.m
     du, dv, dw = dz[:n], dz[n:n + m], dz[-1]
@@ -123,10 +124,11 @@ def forward_differentiate(cache, dA=None, db=None, dc=None, return_info=False, s
     return (out, info) if return_info else out
 
 
-def reverse_differentiate(cache, dx, return_info=False, stats=None):
+def reverse_differentiate(cache, dx, return_info=False, stats=None, maxiter=None):
     """``reverse_differentiate!`` (ConicProgram.jl:336-394) with dy = ds = 0.
 
     Returns ``(g, πz)``; ``lsqr`` is applied to ``M`` (not ``Mᵀ``, :372).
+    ``maxiter`` caps LSQR as in ``forward_differentiate``.
     """
     n, m = cache.n, cache.m
     dx = np.asarray(dx, dtype=np.float64)
@@ -136,7 +138,7 @@ def reverse_differentiate(cache, dx, return_info=False, stats=None):
         g = np.zeros(n + m + 1)
     else:
         g, it, istop = lsqr(cache.matvec, cache.rmatvec, dz, n + m + 1,
-                            return_info=True, stats=stats)
+                            return_info=True, stats=stats, maxiter=maxiter)
         info = (it, istop)
     piz = np.concatenate([cache.x, cache.vp, [1.0]])
     return ((g, piz), info) if return_info else (g, piz)
