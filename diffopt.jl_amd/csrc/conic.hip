@@ -1278,13 +1278,15 @@ __device__ __forceinline__ void split_finish(int b, int32_t* active, LsqrState& 
   if (threadIdx.x == 0) atomicSub(active, 1);
 }
 
+// (a batch slice's sequence b = q·B_s + b' reads right-hand side q·qs + b0 + b'
+// of the whole batch's: qs = B·N, b0 = the slice's first problem)
 __global__ __launch_bounds__(CTPB) void conic_split_init_kernel(
-    const double* __restrict__ rhs, double tol0, double tol1, SplitWS ws, LsqrState* __restrict__ stv,
-    int32_t* __restrict__ active) {
+    const double* __restrict__ rhs, size_t qs, int b0, double tol0, double tol1, SplitWS ws,
+    LsqrState* __restrict__ stv, int32_t* __restrict__ active) {
   __shared__ double red[4];
   const int b = blockIdx.x, t = threadIdx.x, N = ws.N;
   const double tol = b < ws.B ? tol0 : tol1;
-  const double* rb = rhs + (size_t)b * N;
+  const double* rb = rhs + (size_t)(b / ws.B) * qs + (size_t)(b0 + b % ws.B) * N;
   double* u = ws.vec(ws.u, b);
   double* x = ws.vec(ws.x, b);
   double bb = 0.0;
@@ -1687,10 +1689,11 @@ __global__ __launch_bounds__(VT) void conic_split_upd_v_kernel(
 }
 
 // grid nq·B: sequence bv → (xout0, info0) for bv < B, (xout1, info1) after
+// (info arrays of the whole batch: istop at [b], iterations at [istr + b])
 __global__ __launch_bounds__(CTPB) void conic_split_out_kernel(
     SplitWS ws, const LsqrState* __restrict__ stv, double* __restrict__ xout0, int32_t* __restrict__ info0,
     double* __restrict__ xout1, int32_t* __restrict__ info1, double* __restrict__ norms0,
-    double* __restrict__ norms1) {
+    double* __restrict__ norms1, int istr) {
   const int bv = blockIdx.x, t = threadIdx.x, N = ws.N;
   const int b = ws.phys(bv);
   double* xout = bv < ws.B ? xout0 : xout1;
@@ -1699,7 +1702,7 @@ __global__ __launch_bounds__(CTPB) void conic_split_out_kernel(
   for (int i = t; i < N; i += CTPB) xout[(size_t)b * N + i] = x[i];
   if (t == 0 && info) {
     info[b] = stv[bv].istop;
-    info[ws.B + b] = stv[bv].it;
+    info[istr + b] = stv[bv].it;
   }
   double* norms = bv < ws.B ? norms0 : norms1;
   if (t < 4 && norms) {
@@ -2194,148 +2197,218 @@ static int lsqr_maxiter(const Handle& h) {
 
 // Split-path LSQR (see conic_split_* above) of nq sequences per problem
 // (rhs: nq·B right-hand sides, sequence q·B + b), co-iterated for nq = 2.
+//
+// Batch slices (round 5): the fused form runs the batch
+// as two halves, each with its own workspace, on the handle's stream and on
+// `aux`, the second half started one launch behind the first.  Each half's
+// latency-bound Dπ launches (dpiU / dpiV: one workgroup per cone and
+// sequence) then share the GPU with the other half's bandwidth-bound passes
+// instead of leaving it idle between them.  Every sequence's arithmetic is
+// unchanged (a half is the same kernels over fewer problems), so the results
+// are bit-identical to one slice.
 static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const double* rhs, double* out0,
                              int32_t* info0, double* out1, int32_t* info1, double* norms0, double* norms1) {
   const int B = (int)h.batch, m = h.m, n = h.n;
   const int maxit = lsqr_maxiter(h);
-  const int V = nq * B;   // sequences
   const int nc = (int)h.cones.size() / 2;
   const int N = n + m + 1;
   const int RB = std::max(1, (m + SPLIT_ROWS - 1) / SPLIT_ROWS);
   const size_t M1 = (size_t)std::max(m, 1);
   // fused form: u_n of two sequences in the pass kernel's LDS, v'_n in dpiV's
   const bool fuse = h.split_fuse && nc > 0 && n <= SPLIT_FUSE_NMAX;
+  const int ns = fuse && B >= 2 ? 2 : 1;   // batch slices
   const int PL = 3 * RB + 3 * nc;
   const size_t per = fuse ? (size_t)6 * N + 3 * M1 + (size_t)2 * RB * n + PL
                           : (size_t)5 * N + 4 * M1 + (size_t)RB * n;
-  h.csplit.ensure((size_t)V * per * sizeof(double) + (size_t)2 * V * sizeof(LsqrState) + 64);
-  SplitWS ws;
-  FSplit fs;
-  double* base = h.csplit.as<double>();
-  LsqrState* st;
-  if (fuse) {
-    fs.x = base;
-    fs.w = fs.x + (size_t)V * N;
-    fs.u0 = fs.w + (size_t)V * N;
-    fs.u1 = fs.u0 + (size_t)V * N;
-    fs.v0 = fs.u1 + (size_t)V * N;
-    fs.v1 = fs.v0 + (size_t)V * N;
-    fs.Dv = fs.v1 + (size_t)V * N;
-    fs.tmpm = fs.Dv + (size_t)V * M1;
-    fs.yb = fs.tmpm + (size_t)V * M1;
-    fs.gpM = fs.yb + (size_t)V * M1;
-    fs.gpT = fs.gpM + (size_t)V * RB * n;
-    fs.part = fs.gpT + (size_t)V * RB * n;
-    fs.s0 = reinterpret_cast<LsqrState*>(base + (size_t)V * per);
-    fs.s1 = fs.s0 + V;
-    fs.N = N;
-    fs.m = m;
-    fs.n = n;
-    fs.RB = RB;
-    fs.B = B;
-    fs.nc = nc;
-    fs.PL = PL;
-    // the first Mᵀ·u runs the six-launch form's kernels on these buffers
-    // (out: v1, free until the first dpiU)
-    ws.x = fs.x;
-    ws.u = fs.u0;
-    ws.v = fs.v0;
-    ws.w = fs.w;
-    ws.out = fs.v1;
-    ws.Dv = fs.Dv;
-    ws.tmpm = fs.tmpm;
-    ws.yb = fs.yb;
-    ws.gpart = fs.gpT;
-    st = fs.s0;
-  } else {
-    ws.x = base;
-    ws.u = ws.x + (size_t)V * N;
-    ws.v = ws.u + (size_t)V * N;
-    ws.w = ws.v + (size_t)V * N;
-    ws.out = ws.w + (size_t)V * N;
-    ws.Dv = ws.out + (size_t)V * N;
-    ws.tmpm = ws.Dv + (size_t)V * M1;
-    ws.yb = ws.tmpm + (size_t)V * M1;
-    ws.gpart = ws.yb + (size_t)V * M1;
-    st = reinterpret_cast<LsqrState*>(base + (size_t)V * per);
-  }
-  ws.N = N;
-  ws.m = m;
-  ws.n = n;
-  ws.RB = RB;
-  ws.B = B;
-  int32_t* active = reinterpret_cast<int32_t*>(reinterpret_cast<LsqrState*>(base + (size_t)V * per) + 2 * V);
+  // one region per slice: vectors, then 2·V_s states, then the active counter
+  const int Bs0 = (B + ns - 1) / ns;
+  const size_t region = (((size_t)nq * Bs0 * per * sizeof(double) + (size_t)2 * nq * Bs0 * sizeof(LsqrState) + 64) +
+                         255) & ~(size_t)255;
+  h.csplit.ensure(ns * region);
+  h.psd_app.ensure(std::max<size_t>((size_t)nq * B * h.psd_big_len, 1) * sizeof(double));
   const size_t dl = dpi_lds_bytes(h.cones);
-  const double* vcone = h.vp.as<double>();
-  const double* P = h.dpi.as<double>();
   const ConeDesc* cd = h.cone_dev.as<ConeDesc>();
-  h.psd_app.ensure(std::max<size_t>((size_t)V * h.psd_big_len, 1) * sizeof(double));
-  double* gws = h.psd_app.as<double>();
-  const int32_t nact = V;
-  DOPT_CHECK_HIP(hipMemcpyAsync(active, &nact, sizeof(int32_t), hipMemcpyHostToDevice, h.stream));
-  int32_t left = V;
-  PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
-  auto pass = [&](int dir) {
-    hipLaunchKernelGGL(conic_split_pass_kernel<4>, dim3(RB, B), dim3(256), 0, h.stream, dir, h.cA, h.cb, ws, st, nq);
+  if (ns > 1) {
+    ensure_aux(h);
+    DOPT_CHECK_HIP(hipEventRecord(h.ev_fork, h.stream));   // aux after everything queued before the LSQR
+    DOPT_CHECK_HIP(hipStreamWaitEvent(h.aux, h.ev_fork, 0));
+  }
+  struct Slice {
+    int b0, Bs, V, par, left;
+    hipStream_t st;
+    SplitWS ws;
+    FSplit fs;
+    LsqrState* stv;
+    int32_t* active;
+    const double *A, *bv, *cv, *vcone, *P;
+    double* gws;
+  } sl[2];
+  for (int s = 0; s < ns; ++s) {
+    Slice& S = sl[s];
+    S.b0 = s * Bs0;
+    S.Bs = std::min(Bs0, B - S.b0);
+    S.V = nq * S.Bs;
+    S.par = 0;
+    S.left = S.V;
+    S.st = s ? h.aux : h.stream;
+    char* rbase = reinterpret_cast<char*>(h.csplit.p) + s * region;
+    double* base = reinterpret_cast<double*>(rbase);
+    const int V = S.V;
+    SplitWS& ws = S.ws;
+    FSplit& fs = S.fs;
+    if (fuse) {
+      fs.x = base;
+      fs.w = fs.x + (size_t)V * N;
+      fs.u0 = fs.w + (size_t)V * N;
+      fs.u1 = fs.u0 + (size_t)V * N;
+      fs.v0 = fs.u1 + (size_t)V * N;
+      fs.v1 = fs.v0 + (size_t)V * N;
+      fs.Dv = fs.v1 + (size_t)V * N;
+      fs.tmpm = fs.Dv + (size_t)V * M1;
+      fs.yb = fs.tmpm + (size_t)V * M1;
+      fs.gpM = fs.yb + (size_t)V * M1;
+      fs.gpT = fs.gpM + (size_t)V * RB * n;
+      fs.part = fs.gpT + (size_t)V * RB * n;
+      fs.s0 = reinterpret_cast<LsqrState*>(base + (size_t)V * per);
+      fs.s1 = fs.s0 + V;
+      fs.N = N;
+      fs.m = m;
+      fs.n = n;
+      fs.RB = RB;
+      fs.B = S.Bs;
+      fs.nc = nc;
+      fs.PL = PL;
+      // the first Mᵀ·u runs the six-launch form's kernels on these buffers
+      // (out: v1, free until the first dpiU)
+      ws.x = fs.x;
+      ws.u = fs.u0;
+      ws.v = fs.v0;
+      ws.w = fs.w;
+      ws.out = fs.v1;
+      ws.Dv = fs.Dv;
+      ws.tmpm = fs.tmpm;
+      ws.yb = fs.yb;
+      ws.gpart = fs.gpT;
+      S.stv = fs.s0;
+    } else {
+      ws.x = base;
+      ws.u = ws.x + (size_t)V * N;
+      ws.v = ws.u + (size_t)V * N;
+      ws.w = ws.v + (size_t)V * N;
+      ws.out = ws.w + (size_t)V * N;
+      ws.Dv = ws.out + (size_t)V * N;
+      ws.tmpm = ws.Dv + (size_t)V * M1;
+      ws.yb = ws.tmpm + (size_t)V * M1;
+      ws.gpart = ws.yb + (size_t)V * M1;
+      S.stv = reinterpret_cast<LsqrState*>(base + (size_t)V * per);
+    }
+    ws.N = N;
+    ws.m = m;
+    ws.n = n;
+    ws.RB = RB;
+    ws.B = S.Bs;
+    S.active = reinterpret_cast<int32_t*>(reinterpret_cast<LsqrState*>(base + (size_t)V * per) + 2 * V);
+    S.A = h.cA + (size_t)S.b0 * m * n;
+    S.bv = h.cb + (size_t)S.b0 * m;
+    S.cv = h.cc + (size_t)S.b0 * n;
+    S.vcone = h.vp.as<double>() + (size_t)S.b0 * m;
+    S.P = h.dpi.as<double>() + (size_t)S.b0 * h.dpi_len;
+    S.gws = h.psd_app.as<double>() + (size_t)nq * S.b0 * h.psd_big_len;
+  }
+  auto pass = [&](Slice& S, int dir) {
+    hipLaunchKernelGGL(conic_split_pass_kernel<4>, dim3(RB, S.Bs), dim3(256), 0, S.st, dir, S.A, S.bv, S.ws, S.stv,
+                       nq);
   };
-  auto passT = [&]() {
-    pass(1);
+  auto passT = [&](Slice& S) {
+    pass(S, 1);
     if (nc)
-      hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, V),
-                         dim3(CTPB), dl, h.stream, 1, cd, vcone, P, h.dpi_len, ws, st, gws, h.psd_big_len);
+      hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, S.V), dim3(CTPB), dl, S.st, 1, cd, S.vcone, S.P,
+                         h.dpi_len, S.ws, S.stv, S.gws, h.psd_big_len);
   };
-  hipLaunchKernelGGL(conic_split_init_kernel, dim3(V), dim3(CTPB), 0, h.stream, rhs, tol0, tol1, ws, st, active);
-  passT();
-  hipLaunchKernelGGL(conic_split_init2_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st, active,
-                     fuse ? fs.part + fs.PL - 2 * nc : nullptr, PL, nc);
+  PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
+  for (int s = 0; s < ns; ++s) {
+    Slice& S = sl[s];
+    const int32_t nact = S.V;
+    DOPT_CHECK_HIP(hipMemcpyAsync(S.active, &nact, sizeof(int32_t), hipMemcpyHostToDevice, S.st));
+    hipLaunchKernelGGL(conic_split_init_kernel, dim3(S.V), dim3(CTPB), 0, S.st, rhs, (size_t)B * N, S.b0, tol0,
+                       tol1, S.ws, S.stv, S.active);
+    passT(S);
+    hipLaunchKernelGGL(conic_split_init2_kernel, dim3(S.V), dim3(VT), 0, S.st, S.bv, S.cv, S.ws, S.stv, S.active,
+                       fuse ? S.fs.part + S.fs.PL - 2 * nc : nullptr, PL, nc);
+  }
   ccheck();
-  int par = 0;
   if (fuse) {
     const size_t dlv = ((dl + 15) & ~(size_t)15) + (size_t)n * sizeof(double);
     const int img = (int)(((dl + 15) & ~(size_t)15) / sizeof(double));
     const size_t dlp = (size_t)2 * n * sizeof(double);
-    auto dpiV = [&](int first) {
-      hipLaunchKernelGGL(conic_fsplit_dpiV_kernel, dim3(nc, V),
-                         dim3(CTPB), dlv, h.stream, cd, vcone, P, h.dpi_len, h.cc, fs, par, first, maxit, active, gws,
-                         h.psd_big_len, img);
+    auto dpiV = [&](Slice& S, int first) {
+      hipLaunchKernelGGL(conic_fsplit_dpiV_kernel, dim3(nc, S.V), dim3(CTPB), dlv, S.st, cd, S.vcone, S.P, h.dpi_len,
+                         S.cv, S.fs, S.par, first, maxit, S.active, S.gws, h.psd_big_len, img);
     };
-    dpiV(1);
-    for (int it = 0; it < maxit && left > 0;) {
-      for (int k = 0; k < SPLIT_CHUNK && it < maxit; ++k, ++it) {
-        hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 0>), dim3(RB, B), dim3(256), 0, h.stream, h.cA, h.cb, h.cc,
-                           fs, par, nq);
-        hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 1>), dim3(RB, B), dim3(256), dlp, h.stream, h.cA, h.cb, h.cc,
-                           fs, par, nq);
-        hipLaunchKernelGGL(conic_fsplit_dpiU_kernel,
-                           dim3(nc, V), dim3(CTPB), dl, h.stream, cd, vcone, P, h.dpi_len, fs, par, gws,
-                           h.psd_big_len);
-        dpiV(0);
-        par ^= 1;
+    auto iteration = [&](Slice& S, bool skew) {
+      hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 0>), dim3(RB, S.Bs), dim3(256), 0, S.st, S.A, S.bv, S.cv, S.fs,
+                         S.par, nq);
+      if (skew) {   // the second slice starts one launch behind the first
+        DOPT_CHECK_HIP(hipEventRecord(h.ev_join, S.st));
+        DOPT_CHECK_HIP(hipStreamWaitEvent(sl[1].st, h.ev_join, 0));
       }
+      hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 1>), dim3(RB, S.Bs), dim3(256), dlp, S.st, S.A, S.bv, S.cv,
+                         S.fs, S.par, nq);
+      hipLaunchKernelGGL(conic_fsplit_dpiU_kernel, dim3(nc, S.V), dim3(CTPB), dl, S.st, cd, S.vcone, S.P, h.dpi_len,
+                         S.fs, S.par, S.gws, h.psd_big_len);
+      dpiV(S, 0);
+      S.par ^= 1;
+    };
+    for (int s = 0; s < ns; ++s) dpiV(sl[s], 1);
+    bool first = ns > 1;
+    for (int it = 0; it < maxit;) {
+      bool any = false;
+      for (int s = 0; s < ns; ++s) any |= sl[s].left > 0;
+      if (!any) break;
+      int k = 0;
+      for (; k < SPLIT_CHUNK && it + k < maxit; ++k)
+        for (int s = 0; s < ns; ++s)
+          if (sl[s].left > 0) {
+            iteration(sl[s], first && s == 0);
+            first = false;
+          }
+      it += k;
       ccheck();
-      DOPT_CHECK_HIP(hipMemcpyAsync(&left, active, sizeof(int32_t), hipMemcpyDeviceToHost, h.stream));
-      DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+      for (int s = 0; s < ns; ++s)
+        if (sl[s].left > 0)
+          DOPT_CHECK_HIP(hipMemcpyAsync(&sl[s].left, sl[s].active, sizeof(int32_t), hipMemcpyDeviceToHost, sl[s].st));
+      for (int s = 0; s < ns; ++s) DOPT_CHECK_HIP(hipStreamSynchronize(sl[s].st));
     }
   } else {
-    for (int it = 0; it < maxit && left > 0;) {
+    Slice& S = sl[0];
+    for (int it = 0; it < maxit && S.left > 0;) {
       for (int k = 0; k < SPLIT_CHUNK && it < maxit; ++k, ++it) {
         if (nc)
-          hipLaunchKernelGGL(conic_split_dpi_kernel,
-                             dim3(nc, V), dim3(CTPB), dl, h.stream, 0, cd, vcone, P, h.dpi_len, ws, st, gws,
-                             h.psd_big_len);
-        pass(0);
-        hipLaunchKernelGGL(conic_split_upd_u_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st);
-        passT();
-        hipLaunchKernelGGL(conic_split_upd_v_kernel, dim3(V), dim3(VT), 0, h.stream, h.cb, h.cc, ws, st, maxit,
-                           active);
+          hipLaunchKernelGGL(conic_split_dpi_kernel, dim3(nc, S.V), dim3(CTPB), dl, S.st, 0, cd, S.vcone, S.P,
+                             h.dpi_len, S.ws, S.stv, S.gws, h.psd_big_len);
+        pass(S, 0);
+        hipLaunchKernelGGL(conic_split_upd_u_kernel, dim3(S.V), dim3(VT), 0, S.st, S.bv, S.cv, S.ws, S.stv);
+        passT(S);
+        hipLaunchKernelGGL(conic_split_upd_v_kernel, dim3(S.V), dim3(VT), 0, S.st, S.bv, S.cv, S.ws, S.stv, maxit,
+                           S.active);
       }
       ccheck();
-      DOPT_CHECK_HIP(hipMemcpyAsync(&left, active, sizeof(int32_t), hipMemcpyDeviceToHost, h.stream));
-      DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+      DOPT_CHECK_HIP(hipMemcpyAsync(&S.left, S.active, sizeof(int32_t), hipMemcpyDeviceToHost, S.st));
+      DOPT_CHECK_HIP(hipStreamSynchronize(S.st));
     }
   }
-  hipLaunchKernelGGL(conic_split_out_kernel, dim3(V), dim3(CTPB), 0, h.stream, ws,
-                     fuse ? (par ? fs.s1 : fs.s0) : st, out0, info0, out1, info1, norms0, norms1);
+  for (int s = 0; s < ns; ++s) {
+    Slice& S = sl[s];
+    hipLaunchKernelGGL(conic_split_out_kernel, dim3(S.V), dim3(CTPB), 0, S.st, S.ws,
+                       fuse ? (S.par ? S.fs.s1 : S.fs.s0) : S.stv, out0 + (size_t)S.b0 * N,
+                       info0 ? info0 + S.b0 : nullptr, out1 ? out1 + (size_t)S.b0 * N : nullptr,
+                       info1 ? info1 + S.b0 : nullptr, norms0 ? norms0 + (size_t)4 * S.b0 : nullptr,
+                       norms1 ? norms1 + (size_t)4 * S.b0 : nullptr, B);
+  }
+  if (ns > 1) {   // the handle's stream continues after both slices
+    DOPT_CHECK_HIP(hipEventRecord(h.ev_join, h.aux));
+    DOPT_CHECK_HIP(hipStreamWaitEvent(h.stream, h.ev_join, 0));
+  }
   ccheck();
 }
 

@@ -771,3 +771,29 @@ def test_capped_lsqr_istop7(ConicBatch, monkeypatch, shape, split):
     if log:
         with open(log, "a") as f:
             f.write(json.dumps(dict(test=f"capped LSQR: {name} (split={split})", ks=list(ks), worst=worst)) + "\n")
+
+
+def test_split_batch_slices_bitwise(SplitConicBatch):
+    """The fused split LSQR runs a batch as two slices on two streams (round 5):
+    a batch of 3 (slices of 2 and 1 problems) gives bit for bit the outputs and
+    iteration counts of each problem solved alone (batch 1, one slice)."""
+    from diffopt_amd.synthetic import conic_numpy
+    cones = [(4, 10), (4, 15), (1, 5)]
+    B, n = 3, 25
+    d = conic_numpy(B, n, cones, 13)
+    e = SplitConicBatch(B, n, cones)
+    e.set(d["A"], d["b"], d["c"], d["x"], d["s"], d["y"])
+    (out, fdx), (g, dA, db, dc) = e.forward_reverse(d["dx"], d["dA"], d["db"], d["dc"])
+    st = e.lsqr_stats()
+    e.close()
+    for b in range(B):
+        e1 = SplitConicBatch(1, n, cones)
+        e1.set(*[d[k][b:b + 1] for k in ("A", "b", "c", "x", "s", "y")])
+        (o1, f1), (g1, a1, b1, c1) = e1.forward_reverse(d["dx"][b:b + 1], d["dA"][b:b + 1], d["db"][b:b + 1],
+                                                        d["dc"][b:b + 1])
+        s1 = e1.lsqr_stats()
+        e1.close()
+        for x, y in [(out, o1), (fdx, f1), (g, g1), (dA, a1), (db, b1), (dc, c1)]:
+            np.testing.assert_array_equal(np.asarray(x)[b], np.asarray(y)[0])
+        for k in ("istop", "iterations", "fwd_istop", "fwd_iterations"):
+            assert st[k][b] == s1[k][0], (b, k)
