@@ -175,7 +175,11 @@ def run_nlp(args, world, rank, local_rank):
 
     def step():
         eng.factor()
-        eng.forward_reverse(dp_t, dx_t, dd_t)   # forward + reverse, one pass over the factors for both
+        if args.nlp_separate:   # the reference's two calls: forward_differentiate!, reverse_differentiate!
+            eng.forward(dp_t)
+            eng.reverse(dx_t, dd_t)
+        else:
+            eng.forward_reverse(dp_t, dx_t, dd_t)   # forward + reverse, one pass over the factors for both
 
     for _ in range(args.warmup):
         step()
@@ -219,7 +223,8 @@ def run_nlp(args, world, rank, local_rank):
         roof["avg_launch_ms"] = round(avg_s * 1e3, 4)
         roof["phases_ms_per_step"] = {k.replace("qp_", "nlp_"): v for k, v in breakdown.items()}
         line = {
-            "metric": "NLP KKT sensitivity solves/sec (fwd+rev)",
+            "metric": "NLP KKT sensitivity solves/sec (fwd+rev)"
+                      + (" [separate forward and reverse calls]" if args.nlp_separate else ""),
             "value": round(world * B * args.steps / elapsed, 1),
             "unit": "solves/s",
             "n_gpus": world,
@@ -550,6 +555,9 @@ def main():
     ap.add_argument("--conic-variant", choices=["bench", "wellcond"], default="bench",
                     help="config 4: the bench generator (LSQR stops at maxiter) or the converging variant")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--nlp-separate", action="store_true",
+                    help="config 6: time dopt_nlp_forward and dopt_nlp_reverse as two calls (the reference's "
+                         "pattern) instead of the fused dopt_nlp_forward_reverse")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--sync-allgather", action="store_true",
                     help="N > 1: blocking all-gather per step instead of the overlapped pipeline")

@@ -225,6 +225,7 @@ int dopt_qp_set(dopt_handle* h, const double* Q, const double* G, const double* 
     // pointers name: the handle holds no model until this call succeeds
     h->set = false;
     h->factored = false;
+    h->small_ready = false;
     h->Q = stage_in(*h, h->own_in[0], Q, B * n * n);
     h->G = m ? stage_in(*h, h->own_in[1], G, B * m * n) : nullptr;
     h->hv = m ? stage_in(*h, h->own_in[2], hv, B * m) : nullptr;
@@ -307,6 +308,7 @@ int dopt_qp_set_csc(dopt_handle* h,
     // handle holds no model until this call succeeds
     h->set = false;
     h->factored = false;
+    h->small_ready = false;
     // a throw after a queued copy out of the pinned buffer waits for it, so
     // the next call's memcpy into that buffer cannot race the DMA
     struct SyncOnThrow {
@@ -449,6 +451,13 @@ int dopt_qp_reverse(dopt_handle* h, const double* dl_dz, double* out) {
     const size_t B = h->batch, n = h->n, L = h->n + h->m + h->p;
     const double* d = stage_in(*h, h->tin[0], dl_dz, B * n);
     double* o = out_ptr(*h, h->tout[0], out, B * L);
+    // a model not yet factorised, batch of a few: the one-launch small path
+    // (qp_small.hip); anything it cannot take runs the batched route below
+    if (!h->factored && dopt::qp_small_eligible(*h) &&
+        dopt::qp_small_reverse(*h, d, o, [&] { copy_out(*h, out, o, B * L); })) {
+      h->last_time = tm.s();
+      return 0;
+    }
     dopt::qp_reverse(*h, d, o);
     copy_out(*h, out, o, B * L);
     const int rc = first_info(*h);
@@ -471,6 +480,15 @@ int dopt_qp_forward(dopt_handle* h, const double* dQ, const double* dq, const do
     const double* e = stage_in(*h, h->tin[5], dA, B * p * n);
     const double* f = stage_in(*h, h->tin[6], db, B * p);
     double* o = out_ptr(*h, h->tout[1], out, B * L);
+    if (!h->factored && h->small_ready) {   // the small path's factors (dopt_qp_reverse)
+      dopt::qp_small_forward(*h, dopt::FwdTangents{a, b, m ? c : nullptr, m ? d : nullptr, p ? e : nullptr,
+                                                   p ? f : nullptr},
+                             o);
+      copy_out(*h, out, o, B * L);
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+      h->last_time = tm.s();
+      return 0;
+    }
     dopt::qp_forward(*h, a, b, c, d, e, f, o);
     copy_out(*h, out, o, B * L);
     const int rc = first_info(*h);
@@ -827,7 +845,7 @@ int dopt_qp_get_kept(dopt_handle* h, int8_t* kept) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_QP) throw Error(-1, "QP only");
     if (!kept) throw Error(-1, "kept is required");
-    if (!h->factored) throw Error(-1, "no factorisation has run");
+    if (!h->factored && !h->small_ready) throw Error(-1, "no factorisation has run");
     const size_t B = h->batch, m = h->m;
     std::vector<int32_t> rpos(B * m);
     if (B * m)
@@ -852,7 +870,8 @@ int dopt_qp_get_lu_kind(dopt_handle* h, int8_t* kinds) {
       const int r = dopt::qp_route(mm.iterative, mm.nsys);
       kinds[i] = r == dopt::ROUTE_LSQR ? DOPT_LU_KIND_LSQR
                  : r == dopt::ROUTE_GENERIC ? DOPT_LU_KIND_PIVOT
-                 : mm.lu == dopt::LU_NOPIV ? DOPT_LU_KIND_NOPIV : DOPT_LU_KIND_PIVOT;
+                 : mm.lu == dopt::LU_NOPIV ? DOPT_LU_KIND_NOPIV
+                 : mm.lu == dopt::LU_SMALL ? DOPT_LU_KIND_SMALL : DOPT_LU_KIND_PIVOT;
     }
     return 0;
   });

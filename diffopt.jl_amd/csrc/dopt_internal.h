@@ -49,7 +49,7 @@ struct DevBuf {
 
 // Per-problem QP metadata (device, batch entries).
 // Factorisation kinds (QPMeta::lu).
-enum QPLu { LU_NONE = 0, LU_NOPIV = 1, LU_PIVOT = 2, LU_REJECT = 3, LU_GENERIC = 4 };
+enum QPLu { LU_NONE = 0, LU_NOPIV = 1, LU_PIVOT = 2, LU_REJECT = 3, LU_GENERIC = 4, LU_SMALL = 5 };
 // selection masks of the solve launches (bit k: solve problems with lu == k)
 constexpr int LU_SEL_NOPIV = 1 << LU_NOPIV;
 constexpr int LU_SEL_PIVOT = 1 << LU_PIVOT;
@@ -68,6 +68,8 @@ struct QPMeta {
 };
 
 constexpr int ASM_WPP = 16;          // assembly tile workgroups per problem (qp_assemble.hip)
+constexpr int SM_MAX = 128;          // small-problem path (qp_small.hip): largest reduced system held in LDS
+constexpr int SM_BATCH = 8;          // ... and the largest batch it takes (one model at a time: the Julia back-end)
 constexpr int BLOCKED_MAX = 4096;    // largest reduced system of the blocked route (no-pivot LU, blocked solves)
 constexpr int PIVOT_MAX = 1536;      // largest system of the partial-pivoting blocked LU (panel: 512 threads × 3 rows);
                                      // larger blocked problems the no-pivot LU rejects take the generic LU
@@ -176,6 +178,7 @@ struct Handle {
   bool has_lsqr = true;            // some problem takes the LSQR branch
   int32_t n_pivot = 0;             // problems factorised with partial pivoting (last factorisation)
   bool set = false, factored = false;
+  bool small_ready = false;        // the small path's factors are in K (qp_small.hip; dopt_qp_forward reuses them)
 
   // ---- CONIC ----
   const double *cA = nullptr, *cb = nullptr, *cc = nullptr;
@@ -300,6 +303,10 @@ struct PhaseTimer {
 
 // Launch helpers (defined in qp.hip / conic.hip)
 void qp_factor(Handle& h);
+// small-problem path (qp_small.hip)
+bool qp_small_eligible(const Handle& h);
+bool qp_small_reverse(Handle& h, const double* dl_dz, double* out, const std::function<void()>& copy);
+void qp_small_forward(Handle& h, const FwdTangents& T, double* out);
 void qp_reverse(Handle& h, const double* dl_dz, double* out);
 void csc_to_dense(Handle& h, const int64_t* colptr, const int64_t* rowval, const double* nzval,
                   int64_t nnz, int rows, int ncols, double* dense, int* err);

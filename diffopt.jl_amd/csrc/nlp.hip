@@ -1027,7 +1027,11 @@ void nlp_factor(Handle& h) {
   bool fast = false;
   try {
     factor_dense(h, [&h](const int32_t* pl, int count) { assemble(h, pl, count); }, &pre);
-    fast = early_check && h.lu_mode == 1 && h.n_pivot == 0 && h.blocked_npmax > 0 && h.meta_host;
+    // (a rejected problem too tall for the pivoting panel goes to the generic
+    // LU, counted in n_generic, not n_pivot: its factor was not seen by the
+    // early check — ADVICE r04)
+    fast = early_check && h.lu_mode == 1 && h.n_pivot == 0 && h.n_generic == 0 && h.blocked_npmax > 0 &&
+           h.meta_host;
   } catch (...) {
     h.lu_mode = lu_mode;
     throw;
@@ -1073,7 +1077,7 @@ void nlp_factor(Handle& h) {
   }
   // every factor no-pivot (none rejected, corrected or failed): the solves
   // skip the partial-pivoting kernels' launches
-  h.nlp_pivoted = h.n_pivot != 0 || std::any_of(h.nlp_corr.begin(), h.nlp_corr.end(), [](int32_t k) { return k != 0; });
+  h.nlp_pivoted = h.n_pivot != 0 || h.n_generic != 0 || std::any_of(h.nlp_corr.begin(), h.nlp_corr.end(), [](int32_t k) { return k != 0; });
   h.nfactored = true;
 }
 

@@ -942,6 +942,7 @@ static ReasmFn qp_reasm(Handle& h) {
 
 void qp_factor(Handle& h) {
   if (!h.set) throw Error(-1, "dopt_qp_factor: dopt_qp_set has not been called");
+  h.small_ready = false;   // K is overwritten
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
     prep_assemble(h, nullptr, (int)h.batch, h.lu_mode == 0, [&] { meta_copy(h); });

@@ -1,0 +1,616 @@
+// Small-problem drop-in path (round 5): the Julia back-end
+// (DiffOptMI355X.QPModel) differentiates one model at a time — dopt_qp_set_csc,
+// dopt_qp_reverse, dopt_qp_forward on a batch of one (test/moi_wrapper.jl:74-98,
+// test/jump.jl:603-621).  For such calls the batched route's dozen launches and
+// three host turnarounds cost more than the arithmetic.  Here a reduced system
+// of at most SM_MAX unknowns is prepared, assembled, factorised and solved by
+// ONE workgroup per problem, held in LDS, in one launch per direction:
+//
+//   qp_small_rev_kernel   s = Gz − h in the prepare kernel's (Julia's) order and
+//                         the kept rows (bit-exact with qp_prep_kernel); the
+//                         reduced KKT [Q, G_kᵀΛ_k, Aᵀ; G_k, D(s_k), 0; A, 0, 0]
+//                         (QuadraticProgram.jl:256-282) in LDS; the no-pivot LU
+//                         with the batched route's acceptance tests (|l| ≤
+//                         NOPIV_LMAX: UMFPACK's threshold test with the diagonal
+//                         as candidate; |u| ≤ NOPIV_GROWTH·max|K|); L and U to
+//                         the K slab for the forward call; the reverse solve
+//                         K x = [dl/dz; 0; 0] and the outputs, eliminated rows
+//                         recovered as x_λi = (0 − G_i·x_z)/s_i (:316-351)
+//   qp_small_fwd_kernel   the forward right-hand side (:429-433), Kᵀx = r by
+//                         Uᵀ then Lᵀ from the stored factors, the outputs,
+//                         eliminated rows x_λi = r_i/s_i (:357-446)
+//
+// A problem the path cannot take (the LSQR branch Q == 0, a reduced system
+// larger than SM_MAX, a rejected or singular pivot) raises the batch's flag and
+// the call runs the batched route instead, which also reports singularities in
+// the reference's coordinates.  Same semantics, different rounding: the
+// outputs agree with the batched route and the oracle to the parity bar.
+#include "dopt_internal.h"
+
+namespace dopt {
+
+namespace {
+
+constexpr int SM_T = 256;   // threads per workgroup (4 waves: one per SIMD)
+constexpr int SM_LD = SM_MAX + 1;
+constexpr int SM_G = 16;    // reverse LU: a 16 × 16 thread grid, each thread 8 × 8 entries (cyclic)
+
+__device__ __forceinline__ double sm_block_max(double v, double* red) {
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  double r = red[0];
+  for (int w = 1; w < SM_T / 64; ++w) r = fmax(r, red[w]);
+  return r;
+}
+
+// Both kernels' LDS: the factor image and the vectors.  Before the reverse
+// kernel's LU the image region holds the problem's Q, G and A (staged with
+// every load in flight, when they fit).
+struct SmallLds {
+  double S[SM_MAX * SM_LD];   // the L\U factors (row-major, padded rows)
+  double rowb[2][SM_MAX];     // reverse LU: step k's pivot row / column, double-buffered
+  double colb[2][SM_MAX];
+  double z[SM_MAX];           // z (rev) | scratch
+  double y[SM_MAX];           // the solve vector
+  double dinv[SM_MAX];        // 1 / diag(U)
+  double pivb[2];             // reverse LU: step k's pivot
+  double sk[SM_MAX];          // s and λ of the kept rows, compact
+  double lk[SM_MAX];
+  double red[SM_T / 64];
+  int kidx[SM_MAX];           // kept rows, ascending (at most SM_MAX − n − p of them)
+  int cnt[SM_T / 64 + 1];
+};
+
+// The problem's dense inputs as the reverse kernel reads them: staged in LDS
+// (STG) or in place (column-major both ways).
+template <bool STG>
+struct SmSrc {
+  const double *Q, *G, *A;
+};
+
+// Prepare (rev kernel): s, the kept set, rpos / kidx / s to global, the kept
+// rows' s and λ to LDS; returns nk, or −1 when the problem cannot take the
+// small path (workgroup-uniform).
+template <bool STG>
+__device__ __forceinline__ int sm_prepare(const QPIn& P, const SmSrc<STG>& X, int b, SmallLds& L, double* __restrict__ s_out,
+                          int32_t* __restrict__ kidx_g, int32_t* __restrict__ rpos_g) {
+  constexpr int NW = SM_T / 64;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int n = P.n, m = P.m;
+  int nz = 0;
+  for (int i = t; i < n * n; i += SM_T) nz |= X.Q[i] != 0.0;
+  if (!__syncthreads_or(nz)) return -1;   // norm(Q) ≈ 0: the LSQR branch
+  if (t == 0) L.cnt[NW] = 0;
+  __syncthreads();
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int i0 = 0; i0 < m; i0 += SM_T) {
+    const int i = i0 + t;
+    int keep = 0;
+    double si = 0.0, li = 0.0;
+    if (i < m) {
+      // Σ_j G_ij z_j in j order, no fma: qp_prep_kernel's (Julia's mul!)
+      // arithmetic
+      double acc = 0.0;
+#pragma unroll 8
+      for (int j = 0; j < n; ++j) acc = __dadd_rn(acc, __dmul_rn(X.G[i + (size_t)j * m], L.z[j]));
+      si = __dsub_rn(acc, P.h[(size_t)b * m + i]);
+      li = P.lam[(size_t)b * m + i];
+      s_out[(size_t)b * m + i] = si;
+      keep = !(li == 0.0 && si != 0.0);
+    }
+    const unsigned long long ball = __ballot(keep);
+    if (lane == 0) L.cnt[wv] = __popcll(ball);
+    __syncthreads();
+    int off = L.cnt[NW];
+    for (int w = 0; w < wv; ++w) off += L.cnt[w];
+    const int ci = off + __popcll(ball & lt);
+    if (i < m) {
+      if (keep && ci < SM_MAX) {
+        L.kidx[ci] = i;
+        L.sk[ci] = si;
+        L.lk[ci] = li;
+        kidx_g[(size_t)b * m + ci] = i;
+      }
+      rpos_g[(size_t)b * m + i] = keep ? ci : -1;
+    }
+    __syncthreads();
+    if (t == 0) {
+      int sum = 0;
+      for (int w = 0; w < NW; ++w) sum += L.cnt[w];
+      L.cnt[NW] += sum;
+    }
+    __syncthreads();
+  }
+  const int nk = L.cnt[NW];
+  return n + P.p + nk <= SM_MAX ? nk : -1;
+}
+
+// The reduced KKT [Q, G_kᵀΛ_k, Aᵀ; G_k, D(s_k), 0; A, 0, 0] into the thread's
+// registers, e[a][c] = K[ti + 16a][tj + 16c]: per entry an address, a
+// multiplier and a constant, then one unconditional load each; identity
+// padding past N.  Returns the thread's max |K|.
+template <bool STG>
+__device__ __forceinline__ double sm_assemble(const QPIn& P, const SmSrc<STG>& X, const SmallLds& L, int nk, int N,
+                                              int ti, int tj, double (&e)[8][8]) {
+  const int n = P.n, m = P.m, p = P.p;
+  double amax = 0.0;
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    if (a == 4) __builtin_amdgcn_sched_barrier(0);   // two rounds of 32 loads (register pressure)
+#pragma unroll
+    for (int c8 = 0; c8 < 8; ++c8) {
+      const int r = ti + SM_G * a, c = tj + SM_G * c8;
+      const double* q = X.Q;
+      double mul = 0.0, cv = r == c ? 1.0 : 0.0;
+      if (r < N && c < N) {
+        cv = 0.0;
+        mul = 1.0;
+        if (r < n) {
+          if (c < n) q = X.Q + r + (size_t)c * n;
+          else if (c < n + nk) { q = X.G + L.kidx[c - n] + (size_t)r * m; mul = L.lk[c - n]; }
+          else q = X.A + (c - n - nk) + (size_t)r * p;
+        } else if (r < n + nk) {
+          if (c < n) q = X.G + L.kidx[r - n] + (size_t)c * m;
+          else { mul = 0.0; cv = c == r ? L.sk[r - n] : 0.0; }
+        } else if (c < n) {
+          q = X.A + (r - n - nk) + (size_t)c * p;
+        } else {
+          mul = 0.0;
+        }
+      }
+      const double x = *q;
+      e[a][c8] = mul != 0.0 ? x * mul : cv;
+      if (r < N && c < N) amax = fmax(amax, fabs(e[a][c8]));
+    }
+  }
+  return amax;
+}
+
+// Right-looking no-pivot LU steps k = 16·KK … 16·KK + 15 (then KK + 1 …) on
+// the register tiles, with the batched route's acceptance tests as each entry
+// becomes final (|l| ≤ NOPIV_LMAX: UMFPACK's threshold test with the diagonal
+// as candidate; |u| ≤ bound = NOPIV_GROWTH·max|K|).  Step k: the owners of row
+// k write U's row k to the factor image and to the row buffer (zeros on and
+// before the diagonal, the pivot to its slot), the owners of column k write it
+// to the column buffer (zeros on and above the diagonal); one barrier
+// (buffers double-buffered); every thread scales its column-k entries (the
+// column's owners store them as L's column k) and applies the select-free
+// rank-1 fma to its live blocks — blocks a, c < KK are past (compile time),
+// blocks wholly in the padding are skipped by uniform branches.
+template <int KK>
+__device__ __forceinline__ void sm_lu_from(double (&e)[8][8], SmallLds& L, int N, int ti, int tj, double bound,
+                                           int& bad, double* stamp) {
+  if (SM_G * KK >= N) return;
+  double* S = L.S;
+  const int kend = N - SM_G * KK < SM_G ? N - SM_G * KK : SM_G;
+#ifdef SM_STAMPS
+  long long q_[4] = {0, 0, 0, 0}, c_ = clock64(), d_;
+#define SM_LAP(i) d_ = clock64(), q_[i] += d_ - c_, c_ = d_
+#else
+#define SM_LAP(i)
+#endif
+  for (int kr = 0; kr < kend; ++kr) {
+    const int k = SM_G * KK + kr, buf = k & 1;
+    SM_LAP(3);
+    if (ti == kr)
+#pragma unroll
+      for (int c8 = KK; c8 < 8; ++c8) {
+        const int c = tj + SM_G * c8;
+        const double v = e[KK][c8];
+        if (c >= k && c < N) S[k * SM_LD + c] = v;
+        L.rowb[buf][c] = c > k ? v : 0.0;
+        bad |= c > k && !(fabs(v) <= bound);
+#ifdef SM_DEBUG
+        if (c > k && !(fabs(v) <= bound)) printf("small: k %d U row entry c %d = %g\n", k, c, v);
+        if (c == k && (!(fabs(v) > 0.0) || !(fabs(v) <= bound))) printf("small: k %d pivot %g\n", k, v);
+#endif
+        if (c == k) {
+          L.pivb[buf] = v;
+          bad |= !(fabs(v) > 0.0) || !(fabs(v) <= bound);
+        }
+      }
+    if (tj == kr)
+#pragma unroll
+      for (int a = KK; a < 8; ++a) {
+        const int r = ti + SM_G * a;
+        L.colb[buf][r] = r > k ? e[a][KK] : 0.0;
+      }
+    SM_LAP(0);
+    __syncthreads();
+    SM_LAP(1);
+    const double rp = 1.0 / L.pivb[buf];
+    double l[8], u[8];
+#pragma unroll
+    for (int a = KK; a < 8; ++a) l[a] = L.colb[buf][ti + SM_G * a] * rp;
+#pragma unroll
+    for (int c8 = KK; c8 < 8; ++c8) u[c8] = L.rowb[buf][tj + SM_G * c8];
+    if (tj == kr)
+#pragma unroll
+      for (int a = KK; a < 8; ++a) {
+        const int r = ti + SM_G * a;
+        if (r > k && r < N) S[r * SM_LD + k] = l[a];
+        bad |= !(fabs(l[a]) <= NOPIV_LMAX);
+#ifdef SM_DEBUG
+        if (!(fabs(l[a]) <= NOPIV_LMAX)) printf("small: k %d l row %d = %g (piv %g)\n", k, r, l[a], L.pivb[buf]);
+#endif
+      }
+#pragma unroll
+    for (int a = KK; a < 8; ++a) {
+      if (SM_G * a >= N) continue;   // uniform
+#pragma unroll
+      for (int c8 = KK; c8 < 8; ++c8) {
+        if (SM_G * c8 >= N) continue;
+        e[a][c8] = fma(-l[a], u[c8], e[a][c8]);
+      }
+    }
+    SM_LAP(2);
+  }
+#ifdef SM_STAMPS
+  if (threadIdx.x == 0)
+    for (int i = 0; i < 4; ++i) stamp[i] += (double)q_[i];
+#endif
+  if constexpr (KK < 7) sm_lu_from<KK + 1>(e, L, N, ti, tj, bound, bad, stamp);
+}
+
+// One wave's triangular sweeps over the LDS factors (N ≤ 128: entry i of the
+// vector in lane i & 63, register i >> 6); step k's entry by v_readlane.
+__device__ __forceinline__ double sm_entry(double y0, double y1, int k) {
+  const double v = k < 64 ? y0 : y1;
+  return __longlong_as_double(((long long)__builtin_amdgcn_readlane((int)(__double_as_longlong(v) >> 32), k & 63)
+                               << 32) |
+                              (unsigned)__builtin_amdgcn_readlane((int)__double_as_longlong(v), k & 63));
+}
+// One sweep: step k (ascending when LOWER — the entries past k — descending
+// otherwise — the entries before k) takes entry k (× 1/d_k when DIAG, which
+// also stores it) and updates every other live entry i with its coefficient,
+// S[i][k] (column sweeps: L y = r, U x = y) or S[k][i] (TRANS: Uᵀ w = r,
+// Lᵀ x = w).  The coefficients of the next four steps are loaded while the
+// current four run, so the chain is readlane → fma only.
+template <bool LOWER, bool TRANS, bool DIAG>
+__device__ __forceinline__ void sm_sweep(const double* S, const double* dinv, int N, int lane, double& y0,
+                                         double& y1) {
+  const int i0 = lane, i1 = lane + 64;
+  auto coef = [&](int k, int i) {   // k clamped into the image (the tail's dead loads)
+    const int kc = k < 0 ? 0 : (k > SM_MAX - 1 ? SM_MAX - 1 : k);
+    return TRANS ? S[kc * SM_LD + i] : S[i * SM_LD + kc];
+  };
+  auto dget = [&](int k) { return DIAG ? dinv[k < 0 ? 0 : (k > SM_MAX - 1 ? SM_MAX - 1 : k)] : 1.0; };
+  const int st = LOWER ? 1 : -1;
+  int k = LOWER ? 0 : N - 1;
+  double c0[4], c1[4], dv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    c0[q] = coef(k + q * st, i0);
+    c1[q] = coef(k + q * st, i1);
+    dv[q] = dget(k + q * st);
+  }
+  for (int it = 0; it < N; it += 4) {
+    double n0[4], n1[4], nd[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      n0[q] = coef(k + (q + 4) * st, i0);
+      n1[q] = coef(k + (q + 4) * st, i1);
+      nd[q] = dget(k + (q + 4) * st);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (it + q < N) {   // uniform
+        const int kq = k + q * st;
+        double v = sm_entry(y0, y1, kq);
+        if (DIAG) {
+          v *= dv[q];
+          y0 = i0 == kq ? v : y0;
+          y1 = i1 == kq ? v : y1;
+        }
+        const bool u0 = LOWER ? (i0 > kq && i0 < N) : i0 < kq;
+        const bool u1 = LOWER ? (i1 > kq && i1 < N) : i1 < kq;
+        y0 = u0 ? fma(-c0[q], v, y0) : y0;
+        y1 = u1 ? fma(-c1[q], v, y1) : y1;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      c0[q] = n0[q];
+      c1[q] = n1[q];
+      dv[q] = nd[q];
+    }
+    k += 4 * st;
+  }
+}
+// the four solves over the LU image: L unit lower below the diagonal, U on and
+// above, dinv = 1/diag(U)
+__device__ __forceinline__ void sm_lsolve(const double* S, const double* dinv, int N, int lane, double& y0,
+                                          double& y1) {
+  sm_sweep<true, false, false>(S, dinv, N, lane, y0, y1);
+}
+__device__ __forceinline__ void sm_usolve(const double* S, const double* dinv, int N, int lane, double& y0,
+                                          double& y1) {
+  sm_sweep<false, false, true>(S, dinv, N, lane, y0, y1);
+}
+__device__ __forceinline__ void sm_utsolve(const double* S, const double* dinv, int N, int lane, double& y0,
+                                           double& y1) {
+  sm_sweep<true, true, true>(S, dinv, N, lane, y0, y1);
+}
+__device__ __forceinline__ void sm_ltsolve(const double* S, const double* dinv, int N, int lane, double& y0,
+                                           double& y1) {
+  sm_sweep<false, true, false>(S, dinv, N, lane, y0, y1);
+}
+
+#ifdef SM_STAMPS   // (tools/probe/small_probe.hip: thread 0's clock at phase marks, past the outputs)
+#define SM_STAMP(i) \
+  if (threadIdx.x == 0) out[P.n + P.m + P.p + (i)] = (double)clock64()
+#else
+#define SM_STAMP(i)
+#endif
+
+// The reverse kernel.  Q, G and A are staged in LDS when they fit (one round
+// of loads), s and the kept set follow, the reduced system goes to registers
+// (thread (ti, tj) = (t / 16, t % 16) holds rows ti + 16a and columns
+// tj + 16c, a, c < 8: cyclic, so the shrinking trailing block stays spread
+// over every thread), the LU writes the factors to the LDS image as they
+// become final, wave 0 solves, every thread writes outputs.
+template <bool STG>
+__device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restrict__ dl_dz, double* __restrict__ K,
+                                           int ld, int nmax, double* __restrict__ s_out,
+                                           int32_t* __restrict__ kidx_g, int32_t* __restrict__ rpos_g,
+                                           QPMeta* __restrict__ meta, double* __restrict__ out,
+                                           int32_t* __restrict__ flag, SmallLds& L) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int n = P.n, m = P.m, p = P.p;
+  const double* Qb = P.Q + (size_t)b * n * n;
+  const double* Gb = P.G + (size_t)b * m * n;
+  const double* Ab = P.A + (size_t)b * p * n;
+  SmSrc<STG> X;
+  SM_STAMP(0);
+  if constexpr (STG) {
+    double* Qs = L.S;
+    double* Gs = Qs + n * n;
+    double* As = Gs + (size_t)m * n;
+#pragma unroll 8
+    for (int i = t; i < n * n; i += SM_T) Qs[i] = Qb[i];
+#pragma unroll 8
+    for (int i = t; i < m * n; i += SM_T) Gs[i] = Gb[i];
+#pragma unroll 8
+    for (int i = t; i < p * n; i += SM_T) As[i] = Ab[i];
+    X.Q = Qs;
+    X.G = Gs;
+    X.A = As;
+  } else {
+    X.Q = Qb;
+    X.G = Gb;
+    X.A = Ab;
+  }
+  for (int j = t; j < n; j += SM_T) L.z[j] = P.z[(size_t)b * n + j];
+  __syncthreads();
+  SM_STAMP(1);
+  const int nk = sm_prepare<STG>(P, X, b, L, s_out, kidx_g, rpos_g);
+  SM_STAMP(2);
+  if (nk < 0) {   // workgroup-uniform
+#ifdef SM_DEBUG
+    if (t == 0) printf("small: prepare rejects (nk %d)\n", nk);
+#endif
+    if (t == 0) atomicOr(flag, 1);
+    return;
+  }
+  const int N = n + nk + p;
+  const int ti = t / SM_G, tj = t % SM_G;
+  double e[8][8];
+  const double amax = sm_assemble<STG>(P, X, L, nk, N, ti, tj, e);
+  const double bound = NOPIV_GROWTH * sm_block_max(amax, L.red);   // (its barriers end the staged reads)
+  SM_STAMP(3);
+#ifdef SM_DEBUG
+  if (t == 0) printf("small: e00 %g e01 %g e10 %g Q0 %g X.Q0 %g amax %g nk %d\n", e[0][0], e[0][1], e[1][0], Qb[0], X.Q[0], amax, nk);
+#endif
+  int bad = 0;
+  sm_lu_from<0>(e, L, N, ti, tj, bound, bad, out + n + m + p + 8);
+  SM_STAMP(4);
+#ifdef SM_DEBUG
+  if (bad) printf("small: t %d rejects (N %d bound %g piv0 %g)\n", t, N, bound, L.S[0]);
+#endif
+#ifdef SM_DUMP   // (tools/probe/small_probe.hip: the factors kept whatever the tests say)
+  if (__syncthreads_or(bad) && t == 0) atomicOr(flag, 1);
+#else
+  if (__syncthreads_or(bad)) {   // workgroup-uniform
+    if (t == 0) atomicOr(flag, 1);
+    return;
+  }
+#endif
+  double* S = L.S;
+  for (int r = t; r < N; r += SM_T) L.dinv[r] = 1.0 / S[r * SM_LD + r];
+  // the factors to the K slab (the forward call's)
+  double* Kb = K + (size_t)b * nmax * ld;
+  const int lane = t & 63, wv = t >> 6;
+  for (int r = wv; r < N; r += SM_T / 64)
+    for (int c = lane; c < N; c += 64) Kb[(size_t)r * ld + c] = S[r * SM_LD + c];
+  if (t == 0) {
+    QPMeta mm = {};
+    mm.nk = nk;
+    mm.nsys = N;
+    mm.iterative = 0;
+    mm.info = 0;
+    mm.lu = LU_SMALL;   // not the batched route's factors (h.factored stays false: its solves never read them)
+    meta[b] = mm;
+  }
+  __syncthreads();
+  SM_STAMP(5);
+  // reverse: K x = [dl/dz; 0; 0] — L y = r, then U x = y, by wave 0 alone
+  // with the vector in registers (entries lane and lane + 64): the pivot entry
+  // comes by v_readlane, no barrier per step
+  double* y = L.y;
+  if (wv == 0) {
+    const double* db = dl_dz + (size_t)b * n;
+    double y0 = lane < n ? db[lane] : 0.0, y1 = lane + 64 < n ? db[lane + 64] : 0.0;
+    sm_lsolve(S, L.dinv, N, lane, y0, y1);
+    sm_usolve(S, L.dinv, N, lane, y0, y1);
+    if (lane < N) y[lane] = y0;
+    if (lane + 64 < N) y[lane + 64] = y1;
+  }
+  __syncthreads();
+  SM_STAMP(6);
+  // outputs −[x_z | x_λ | x_ν]; eliminated rows x_λl = (0 − G_l·x_z)/s_l
+  double* ob = out + (size_t)b * (n + m + p);
+  const double* sb = s_out + (size_t)b * m;
+  const int32_t* rp = rpos_g + (size_t)b * m;
+  for (int i = t; i < n; i += SM_T) ob[i] = -y[i];
+  for (int e2 = t; e2 < p; e2 += SM_T) ob[n + m + e2] = -y[n + nk + e2];
+  for (int l = t; l < m; l += SM_T) {
+    const int kk = rp[l];
+    if (kk >= 0) {
+      ob[n + l] = -y[n + kk];
+    } else {
+      double acc = 0.0;
+#pragma unroll 8
+      for (int j = 0; j < n; ++j) acc = fma(Gb[l + (size_t)j * m], y[j], acc);
+      ob[n + l] = -((0.0 - acc) / sb[l]);
+    }
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(SM_T) void qp_small_rev_kernel(QPIn P, const double* __restrict__ dl_dz,
+                                                            double* __restrict__ K, int ld, int nmax,
+                                                            double* __restrict__ s_out, int32_t* __restrict__ kidx_g,
+                                                            int32_t* __restrict__ rpos_g, QPMeta* __restrict__ meta,
+                                                            double* __restrict__ out, int32_t* __restrict__ flag) {
+  __shared__ SmallLds L;
+  if ((P.n + P.m + P.p) * P.n <= SM_MAX * SM_LD)   // uniform: Q, G and A fit the image region
+    sm_reverse<true>(P, dl_dz, K, ld, nmax, s_out, kidx_g, rpos_g, meta, out, flag, L);
+  else
+    sm_reverse<false>(P, dl_dz, K, ld, nmax, s_out, kidx_g, rpos_g, meta, out, flag, L);
+}
+
+__global__ __launch_bounds__(SM_T) void qp_small_fwd_kernel(QPIn P, FwdTangents T, const double* __restrict__ K,
+                                                            int ld, int nmax, const double* __restrict__ s,
+                                                            const int32_t* __restrict__ rpos_g,
+                                                            const QPMeta* __restrict__ meta,
+                                                            double* __restrict__ out) {
+  __shared__ SmallLds L;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int n = P.n, m = P.m, p = P.p;
+  const QPMeta mm = meta[b];
+  const int nk = mm.nk, N = mm.nsys;
+  double* S = L.S;
+  const double* Kb = K + (size_t)b * nmax * ld;
+  const int lane = t & 63, wv = t >> 6;
+  for (int r = wv; r < N; r += SM_T / 64)
+    for (int c = lane; c < N; c += 64) S[r * SM_LD + c] = Kb[(size_t)r * ld + c];
+  for (int r = t; r < N; r += SM_T) L.dinv[r] = 1.0 / Kb[(size_t)r * ld + r];
+  // the full forward right-hand side r (QuadraticProgram.jl:429-433):
+  //   [dQ z + dq + dGᵀλ + dAᵀν; λ.*(dG z) − λ.*dh; dA z − db] — r1 and r3 in
+  // y (reduced positions), r2 kept in registers per row for the recovery
+  const double* zb = P.z + (size_t)b * n;
+  const double* lb = P.lam + (size_t)b * m;
+  const double* nb = P.nu + (size_t)b * p;
+  double* y = L.y;
+  for (int i = t; i < n; i += SM_T) {
+    double acc = 0.0;
+    if (T.dQ) {
+      const double* dQb = T.dQ + (size_t)b * n * n;
+#pragma unroll 8
+      for (int j = 0; j < n; ++j) acc = fma(dQb[i + (size_t)j * n], zb[j], acc);
+    }
+    if (T.dq) acc += T.dq[(size_t)b * n + i];
+    if (T.dG)
+#pragma unroll 8
+      for (int l = 0; l < m; ++l) acc = fma(T.dG[(size_t)b * m * n + l + (size_t)i * m], lb[l], acc);
+    if (T.dA)
+      for (int e = 0; e < p; ++e) acc = fma(T.dA[(size_t)b * p * n + e + (size_t)i * p], nb[e], acc);
+    y[i] = acc;
+  }
+  for (int e = t; e < p; e += SM_T) {
+    double az = 0.0;
+    if (T.dA)
+      for (int j = 0; j < n; ++j) az = fma(T.dA[(size_t)b * p * n + e + (size_t)j * p], zb[j], az);
+    y[n + nk + e] = az - (T.db ? T.db[(size_t)b * p + e] : 0.0);
+  }
+  auto r2 = [&](int l) {
+    double gz = 0.0;
+    if (T.dG)
+#pragma unroll 8
+      for (int j = 0; j < n; ++j) gz = fma(T.dG[(size_t)b * m * n + l + (size_t)j * m], zb[j], gz);
+    const double hh = T.dh ? T.dh[(size_t)b * m + l] : 0.0;
+    return lb[l] * gz - lb[l] * hh;
+  };
+  const int32_t* rp = rpos_g + (size_t)b * m;
+  for (int l = t; l < m; l += SM_T) {
+    const int kk = rp[l];
+    if (kk >= 0) y[n + kk] = r2(l);
+  }
+  __syncthreads();
+  // Kᵀ x = r: Uᵀ w = r, then Lᵀ x = w, by wave 0 (as the reverse kernel)
+  if (wv == 0) {
+    double y0 = lane < N ? y[lane] : 0.0, y1 = lane + 64 < N ? y[lane + 64] : 0.0;
+    sm_utsolve(S, L.dinv, N, lane, y0, y1);
+    sm_ltsolve(S, L.dinv, N, lane, y0, y1);
+    if (lane < N) y[lane] = y0;
+    if (lane + 64 < N) y[lane + 64] = y1;
+  }
+  __syncthreads();
+  double* ob = out + (size_t)b * (n + m + p);
+  const double* sb = s + (size_t)b * m;
+  for (int i = t; i < n; i += SM_T) ob[i] = -y[i];
+  for (int e = t; e < p; e += SM_T) ob[n + m + e] = -y[n + nk + e];
+  for (int l = t; l < m; l += SM_T) {
+    const int kk = rp[l];
+    ob[n + l] = kk >= 0 ? -y[n + kk] : -(r2(l) / sb[l]);
+  }
+}
+
+namespace {
+QPIn small_inputs(const Handle& h) {
+  static const double* dummy = nullptr;
+  (void)dummy;
+  QPIn P;
+  P.Q = h.Q;
+  P.G = h.G;
+  P.h = h.hv;
+  P.A = h.A;
+  P.z = h.z;
+  P.lam = h.lam;
+  P.nu = h.nu;
+  P.n = h.n;
+  P.m = h.m;
+  P.p = h.p;
+  return P;
+}
+}  // namespace
+
+bool qp_small_eligible(const Handle& h) {
+  return h.kind == DOPT_KIND_QP && h.lu_mode == 1 && h.batch >= 1 && h.batch <= SM_BATCH && h.n > 0 &&
+         h.n + h.p < SM_MAX && h.set;
+}
+
+// Reverse through the small path: true when every problem took it (the
+// outputs are queued on the handle's stream; `copy` — the host copy-out — is
+// queued before the flag's read-back so one synchronisation serves both).
+bool qp_small_reverse(Handle& h, const double* dl_dz, double* out, const std::function<void()>& copy) {
+  h.small_ready = false;
+  h.csc_err.ensure(sizeof(int));
+  int32_t* flag = h.csc_err.as<int32_t>();
+  DOPT_CHECK_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), h.stream));
+  hipLaunchKernelGGL(qp_small_rev_kernel, dim3((unsigned)h.batch), dim3(SM_T), 0, h.stream, small_inputs(h), dl_dz,
+                     h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(), h.kidx.as<int32_t>(),
+                     h.kidx.as<int32_t>() + (size_t)h.batch * h.m, h.meta.as<QPMeta>(), out, flag);
+  DOPT_CHECK_HIP(hipGetLastError());
+  copy();
+  int32_t hf = 0;
+  DOPT_CHECK_HIP(hipMemcpyAsync(&hf, flag, sizeof(int32_t), hipMemcpyDeviceToHost, h.stream));
+  DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+  h.small_ready = hf == 0;
+  return h.small_ready;
+}
+
+// Forward from the small path's factors (h.small_ready); the outputs are
+// queued on the handle's stream.
+void qp_small_forward(Handle& h, const FwdTangents& T, double* out) {
+  hipLaunchKernelGGL(qp_small_fwd_kernel, dim3((unsigned)h.batch), dim3(SM_T), 0, h.stream, small_inputs(h), T,
+                     h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(), h.kidx.as<int32_t>() + (size_t)h.batch * h.m,
+                     h.meta.as<QPMeta>(), out);
+  DOPT_CHECK_HIP(hipGetLastError());
+}
+
+}  // namespace dopt

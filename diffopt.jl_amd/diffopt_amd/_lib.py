@@ -102,7 +102,7 @@ def phase_mask(lib, names):
 
 
 ABI_VERSION = 2
-LU_KIND_LSQR, LU_KIND_NOPIV, LU_KIND_PIVOT = 0, 1, 2
+LU_KIND_LSQR, LU_KIND_NOPIV, LU_KIND_PIVOT, LU_KIND_SMALL = 0, 1, 2, 3
 
 
 class EngineUnavailable(RuntimeError):

@@ -322,7 +322,8 @@ class QPBatch:
 
     def lu_kind(self):
         """Per-problem factorisation kind of the last factorisation:
-        _lib.LU_KIND_LSQR / LU_KIND_NOPIV / LU_KIND_PIVOT."""
+        _lib.LU_KIND_LSQR / LU_KIND_NOPIV / LU_KIND_PIVOT, or LU_KIND_SMALL after a
+        reverse call the one-workgroup small path served (qp_small.hip)."""
         buf = np.zeros(self.batch, dtype=np.int8)
         _lib.check(self.lib.dopt_qp_get_lu_kind(self.h, buf.ctypes.data), self.h)
         return buf

@@ -364,6 +364,7 @@ int dopt_qp_get_kept(dopt_handle* h, int8_t* kept);
 #define DOPT_LU_KIND_LSQR 0      /* `iterative` branch (no factorisation)        */
 #define DOPT_LU_KIND_NOPIV 1     /* no-pivot LU passed the threshold test        */
 #define DOPT_LU_KIND_PIVOT 2     /* partial pivoting                             */
+#define DOPT_LU_KIND_SMALL 3     /* no-pivot LU of the one-workgroup small path  */
 int dopt_qp_get_lu_kind(dopt_handle* h, int8_t* kinds);
 /* per-problem flag: 1 when the last factorisation took the P-symmetric
  * no-pivot route (P = diag(1, λ_k, 1) makes P·K symmetric: lower trailing
