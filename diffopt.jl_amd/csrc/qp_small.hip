@@ -34,6 +34,7 @@ namespace {
 constexpr int SM_T = 256;   // threads per workgroup (4 waves: one per SIMD)
 constexpr int SM_LD = SM_MAX + 1;
 constexpr int SM_G = 16;    // reverse LU: a 16 × 16 thread grid, each thread 8 × 8 entries (cyclic)
+constexpr int SM_GB = 4;    // reverse LU: steps per elimination group (rank-4 updates)
 
 __device__ __forceinline__ double sm_block_max(double v, double* red) {
   for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
@@ -51,12 +52,12 @@ __device__ __forceinline__ double sm_block_max(double v, double* red) {
 // every load in flight, when they fit).
 struct SmallLds {
   double S[SM_MAX * SM_LD];   // the L\U factors (row-major, padded rows)
-  double rowb[2][SM_MAX];     // reverse LU: step k's pivot row / column, double-buffered
-  double colb[2][SM_MAX];
+  double rowb[2][SM_GB][SM_MAX];   // reverse LU: a group's rows / columns / diagonal block,
+  double colb[2][SM_GB][SM_MAX];   // double-buffered
+  double dblk[2][SM_GB * SM_GB];
   double z[SM_MAX];           // z (rev) | scratch
   double y[SM_MAX];           // the solve vector
   double dinv[SM_MAX];        // 1 / diag(U)
-  double pivb[2];             // reverse LU: step k's pivot
   double sk[SM_MAX];          // s and λ of the kept rows, compact
   double lk[SM_MAX];
   double red[SM_T / 64];
@@ -64,24 +65,30 @@ struct SmallLds {
   int cnt[SM_T / 64 + 1];
 };
 
-// The problem's dense inputs as the reverse kernel reads them: staged in LDS
-// (STG) or in place (column-major both ways).
-template <bool STG>
+// The problem's dense inputs (column-major) as the reverse kernel reads them:
+// in place, or (STG) staged in LDS at the front of the image region — Q at 0,
+// G at n², A at n² + mn — and then always addressed from the LDS array itself,
+// so every read is a plain LDS read.
 struct SmSrc {
   const double *Q, *G, *A;
 };
+template <bool STG>
+__device__ __forceinline__ double sm_src(const SmallLds& Ls, const SmSrc& Xs, int src, size_t idx, int nn, int mm) {
+  if constexpr (STG) return Ls.S[(src == 0 ? 0 : src == 1 ? (size_t)nn * nn : (size_t)nn * nn + (size_t)mm * nn) + idx];
+  else return (src == 0 ? Xs.Q : src == 1 ? Xs.G : Xs.A)[idx];
+}
 
 // Prepare (rev kernel): s, the kept set, rpos / kidx / s to global, the kept
 // rows' s and λ to LDS; returns nk, or −1 when the problem cannot take the
 // small path (workgroup-uniform).
 template <bool STG>
-__device__ __forceinline__ int sm_prepare(const QPIn& P, const SmSrc<STG>& X, int b, SmallLds& L, double* __restrict__ s_out,
+__device__ __forceinline__ int sm_prepare(const QPIn& P, const SmSrc& X, int b, SmallLds& L, double* __restrict__ s_out,
                           int32_t* __restrict__ kidx_g, int32_t* __restrict__ rpos_g) {
   constexpr int NW = SM_T / 64;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n = P.n, m = P.m;
   int nz = 0;
-  for (int i = t; i < n * n; i += SM_T) nz |= X.Q[i] != 0.0;
+  for (int i = t; i < n * n; i += SM_T) nz |= sm_src<STG>(L, X, 0, i, n, m) != 0.0;
   if (!__syncthreads_or(nz)) return -1;   // norm(Q) ≈ 0: the LSQR branch
   if (t == 0) L.cnt[NW] = 0;
   __syncthreads();
@@ -95,7 +102,7 @@ __device__ __forceinline__ int sm_prepare(const QPIn& P, const SmSrc<STG>& X, in
       // arithmetic
       double acc = 0.0;
 #pragma unroll 8
-      for (int j = 0; j < n; ++j) acc = __dadd_rn(acc, __dmul_rn(X.G[i + (size_t)j * m], L.z[j]));
+      for (int j = 0; j < n; ++j) acc = __dadd_rn(acc, __dmul_rn(sm_src<STG>(L, X, 1, i + (size_t)j * m, n, m), L.z[j]));
       si = __dsub_rn(acc, P.h[(size_t)b * m + i]);
       li = P.lam[(size_t)b * m + i];
       s_out[(size_t)b * m + i] = si;
@@ -133,7 +140,7 @@ __device__ __forceinline__ int sm_prepare(const QPIn& P, const SmSrc<STG>& X, in
 // multiplier and a constant, then one unconditional load each; identity
 // padding past N.  Returns the thread's max |K|.
 template <bool STG>
-__device__ __forceinline__ double sm_assemble(const QPIn& P, const SmSrc<STG>& X, const SmallLds& L, int nk, int N,
+__device__ __forceinline__ double sm_assemble(const QPIn& P, const SmSrc& X, const SmallLds& L, int nk, int N,
                                               int ti, int tj, double (&e)[8][8]) {
   const int n = P.n, m = P.m, p = P.p;
   double amax = 0.0;
@@ -143,25 +150,27 @@ __device__ __forceinline__ double sm_assemble(const QPIn& P, const SmSrc<STG>& X
 #pragma unroll
     for (int c8 = 0; c8 < 8; ++c8) {
       const int r = ti + SM_G * a, c = tj + SM_G * c8;
-      const double* q = X.Q;
+      int which = 0;
+      size_t off = 0;
       double mul = 0.0, cv = r == c ? 1.0 : 0.0;
       if (r < N && c < N) {
         cv = 0.0;
         mul = 1.0;
         if (r < n) {
-          if (c < n) q = X.Q + r + (size_t)c * n;
-          else if (c < n + nk) { q = X.G + L.kidx[c - n] + (size_t)r * m; mul = L.lk[c - n]; }
-          else q = X.A + (c - n - nk) + (size_t)r * p;
+          if (c < n) off = r + (size_t)c * n;
+          else if (c < n + nk) { which = 1; off = L.kidx[c - n] + (size_t)r * m; mul = L.lk[c - n]; }
+          else { which = 2; off = (c - n - nk) + (size_t)r * p; }
         } else if (r < n + nk) {
-          if (c < n) q = X.G + L.kidx[r - n] + (size_t)c * m;
+          if (c < n) { which = 1; off = L.kidx[r - n] + (size_t)c * m; }
           else { mul = 0.0; cv = c == r ? L.sk[r - n] : 0.0; }
         } else if (c < n) {
-          q = X.A + (r - n - nk) + (size_t)c * p;
+          which = 2;
+          off = (r - n - nk) + (size_t)c * p;
         } else {
           mul = 0.0;
         }
       }
-      const double x = *q;
+      const double x = sm_src<STG>(L, X, which, off, n, m);
       e[a][c8] = mul != 0.0 ? x * mul : cv;
       if (r < N && c < N) amax = fmax(amax, fabs(e[a][c8]));
     }
@@ -169,82 +178,146 @@ __device__ __forceinline__ double sm_assemble(const QPIn& P, const SmSrc<STG>& X
   return amax;
 }
 
-// Right-looking no-pivot LU steps k = 16·KK … 16·KK + 15 (then KK + 1 …) on
-// the register tiles, with the batched route's acceptance tests as each entry
-// becomes final (|l| ≤ NOPIV_LMAX: UMFPACK's threshold test with the diagonal
-// as candidate; |u| ≤ bound = NOPIV_GROWTH·max|K|).  Step k: the owners of row
-// k write U's row k to the factor image and to the row buffer (zeros on and
-// before the diagonal, the pivot to its slot), the owners of column k write it
-// to the column buffer (zeros on and above the diagonal); one barrier
-// (buffers double-buffered); every thread scales its column-k entries (the
-// column's owners store them as L's column k) and applies the select-free
-// rank-1 fma to its live blocks — blocks a, c < KK are past (compile time),
-// blocks wholly in the padding are skipped by uniform branches.
-template <int KK>
+// Right-looking no-pivot LU in groups of four steps (rank-4 updates, one
+// barrier per group) on the register tiles, with the batched route's
+// acceptance tests as each entry becomes final (|l| ≤ NOPIV_LMAX: UMFPACK's
+// threshold test with the diagonal as candidate; |u| ≤ bound =
+// NOPIV_GROWTH·max|K|).  Group k … k+3 (k = 16·KK + 4g):
+//   before the barrier, the wave holding rows k … k+3 (wave g: thread row
+//   class ti = t / 16) gathers the 4 × 4 diagonal block by v_readlane,
+//   factors it, and turns its rows into U's rows (L_D u = y, the earlier
+//   rows' entries by lane shuffles); it publishes them (zeros up to the
+//   group's last column), the block's factors and 1/diag(U_D), and stores
+//   them to the factor image with the tests; the owners of columns k … k+3
+//   publish them below the group's rows (zeros above);
+//   after it, every thread derives L's entries of its rows (l U_D = x; the
+//   columns' owners store them with the threshold test) and applies the
+//   rank-4 fma to its live blocks.
+// Blocks a, c < KK are past and blocks a, c ≥ NB = ⌈N / 16⌉ pure padding, both
+// compile-time (the kernel dispatches on NB); identity rows pad the system to
+// a multiple of four.
+template <int KK, int NB>
 __device__ __forceinline__ void sm_lu_from(double (&e)[8][8], SmallLds& L, int N, int ti, int tj, double bound,
                                            int& bad, double* stamp) {
-  if (SM_G * KK >= N) return;
+  if constexpr (KK >= NB) return;
   double* S = L.S;
-  const int kend = N - SM_G * KK < SM_G ? N - SM_G * KK : SM_G;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int NP = (N + SM_GB - 1) / SM_GB * SM_GB;
+  const int gend = (NP - SM_G * KK < SM_G ? NP - SM_G * KK : SM_G) / SM_GB;
 #ifdef SM_STAMPS
   long long q_[4] = {0, 0, 0, 0}, c_ = clock64(), d_;
 #define SM_LAP(i) d_ = clock64(), q_[i] += d_ - c_, c_ = d_
 #else
 #define SM_LAP(i)
 #endif
-  for (int kr = 0; kr < kend; ++kr) {
-    const int k = SM_G * KK + kr, buf = k & 1;
+  for (int g = 0; g < gend; ++g) {
+    const int k = SM_G * KK + SM_GB * g, k3 = k + SM_GB - 1, buf = g & 1;
+    const int jc = tj - SM_GB * g;   // position of the thread's column class in the group
+    const bool cown = jc >= 0 && jc < SM_GB;
     SM_LAP(3);
-    if (ti == kr)
+    if (wv == g) {   // the group's rows (uniform): lane = 16·jr + tj
+      const int jr = lane >> 4;
+      double d[SM_GB * SM_GB];
 #pragma unroll
-      for (int c8 = KK; c8 < 8; ++c8) {
-        const int c = tj + SM_G * c8;
-        const double v = e[KK][c8];
-        if (c >= k && c < N) S[k * SM_LD + c] = v;
-        L.rowb[buf][c] = c > k ? v : 0.0;
-        bad |= c > k && !(fabs(v) <= bound);
-#ifdef SM_DEBUG
-        if (c > k && !(fabs(v) <= bound)) printf("small: k %d U row entry c %d = %g\n", k, c, v);
-        if (c == k && (!(fabs(v) > 0.0) || !(fabs(v) <= bound))) printf("small: k %d pivot %g\n", k, v);
-#endif
-        if (c == k) {
-          L.pivb[buf] = v;
-          bad |= !(fabs(v) > 0.0) || !(fabs(v) <= bound);
+      for (int i = 0; i < SM_GB; ++i)
+#pragma unroll
+        for (int j = 0; j < SM_GB; ++j) {
+          const long long bits = __double_as_longlong(e[KK][KK]);
+          const int src = 16 * i + SM_GB * g + j;
+          d[i * SM_GB + j] = __longlong_as_double(
+              ((long long)__builtin_amdgcn_readlane((int)(bits >> 32), src) << 32) |
+              (unsigned)__builtin_amdgcn_readlane((int)bits, src));
+        }
+#pragma unroll
+      for (int q = 0; q < SM_GB; ++q) {
+        const double rq = 1.0 / d[q * SM_GB + q];
+#pragma unroll
+        for (int i = q + 1; i < SM_GB; ++i) {
+          d[i * SM_GB + q] *= rq;
+#pragma unroll
+          for (int j = q + 1; j < SM_GB; ++j) d[i * SM_GB + j] = fma(-d[i * SM_GB + q], d[q * SM_GB + j], d[i * SM_GB + j]);
         }
       }
-    if (tj == kr)
+      if (lane < SM_GB * SM_GB) {   // the block's factors: published, to the image, the tests
+        const int i = lane / SM_GB, j = lane % SM_GB;
+        double v = d[0];
 #pragma unroll
-      for (int a = KK; a < 8; ++a) {
+        for (int x = 1; x < SM_GB * SM_GB; ++x) v = lane == x ? d[x] : v;
+        L.dblk[buf][lane] = i == j ? 1.0 / v : v;   // 1/u_jj on the diagonal
+        if (k + i < N && k + j < N) {
+          S[(k + i) * SM_LD + k + j] = v;
+          bad |= i > j ? !(fabs(v) <= NOPIV_LMAX) : !(fabs(v) <= bound);
+          if (i == j) bad |= !(fabs(v) > 0.0);
+        }
+      }
+      double lrow[SM_GB - 1];   // L_D's row jr
+#pragma unroll
+      for (int q = 0; q < SM_GB - 1; ++q) {
+        double v = 0.0;
+#pragma unroll
+        for (int i = q + 1; i < SM_GB; ++i) v = jr == i ? d[i * SM_GB + q] : v;
+        lrow[q] = v;
+      }
+#pragma unroll
+      for (int c8 = KK; c8 < NB; ++c8) {
+        const int c = tj + SM_G * c8;
+        double v = e[KK][c8];   // row k + jr
+#pragma unroll
+        for (int q = 0; q < SM_GB - 1; ++q) {
+          const double uq = __shfl(v, 16 * q + tj);   // row k + q's entry, final
+          v = jr > q ? fma(-lrow[q], uq, v) : v;
+        }
+        L.rowb[buf][jr][c] = c > k3 ? v : 0.0;
+        if (c > k3 && c < N && k + jr < N) {
+          S[(k + jr) * SM_LD + c] = v;
+          bad |= !(fabs(v) <= bound);
+        }
+      }
+    }
+    if (cown)
+#pragma unroll
+      for (int a = KK; a < NB; ++a) {
         const int r = ti + SM_G * a;
-        L.colb[buf][r] = r > k ? e[a][KK] : 0.0;
+        L.colb[buf][jc][r] = r > k3 ? e[a][KK] : 0.0;
       }
     SM_LAP(0);
     __syncthreads();
     SM_LAP(1);
-    const double rp = 1.0 / L.pivb[buf];
-    double l[8], u[8];
+    // U_D's strict upper triangle and 1/diag(U_D)
+    double ud[SM_GB * SM_GB];
 #pragma unroll
-    for (int a = KK; a < 8; ++a) l[a] = L.colb[buf][ti + SM_G * a] * rp;
+    for (int i = 0; i < SM_GB * SM_GB; ++i)
+      if (i / SM_GB <= i % SM_GB) ud[i] = L.dblk[buf][i];
+    // L's entries of the thread's rows: l U_D = x, x = the rows' group columns
+    double l[8][SM_GB];
 #pragma unroll
-    for (int c8 = KK; c8 < 8; ++c8) u[c8] = L.rowb[buf][tj + SM_G * c8];
-    if (tj == kr)
+    for (int a = KK; a < NB; ++a) {
+      const int r = ti + SM_G * a;
 #pragma unroll
-      for (int a = KK; a < 8; ++a) {
-        const int r = ti + SM_G * a;
-        if (r > k && r < N) S[r * SM_LD + k] = l[a];
-        bad |= !(fabs(l[a]) <= NOPIV_LMAX);
-#ifdef SM_DEBUG
-        if (!(fabs(l[a]) <= NOPIV_LMAX)) printf("small: k %d l row %d = %g (piv %g)\n", k, r, l[a], L.pivb[buf]);
-#endif
+      for (int j = 0; j < SM_GB; ++j) {
+        double x = L.colb[buf][j][r];
+#pragma unroll
+        for (int q = 0; q < j; ++q) x = fma(-l[a][q], ud[q * SM_GB + j], x);
+        l[a][j] = x * ud[j * SM_GB + j];
       }
+      if (cown && r > k3 && r < N) {   // column k + jc of L: to the image, the threshold test
+        double v = l[a][0];
 #pragma unroll
-    for (int a = KK; a < 8; ++a) {
-      if (SM_G * a >= N) continue;   // uniform
-#pragma unroll
-      for (int c8 = KK; c8 < 8; ++c8) {
-        if (SM_G * c8 >= N) continue;
-        e[a][c8] = fma(-l[a], u[c8], e[a][c8]);
+        for (int j = 1; j < SM_GB; ++j) v = jc == j ? l[a][j] : v;
+        S[r * SM_LD + k + jc] = v;
+        bad |= !(fabs(v) <= NOPIV_LMAX);
       }
+    }
+#pragma unroll
+    for (int c8 = KK; c8 < NB; ++c8) {
+      const int c = tj + SM_G * c8;
+      double u[SM_GB];
+#pragma unroll
+      for (int j = 0; j < SM_GB; ++j) u[j] = L.rowb[buf][j][c];
+#pragma unroll
+      for (int a = KK; a < NB; ++a)
+#pragma unroll
+        for (int j = 0; j < SM_GB; ++j) e[a][c8] = fma(-l[a][j], u[j], e[a][c8]);
     }
     SM_LAP(2);
   }
@@ -252,7 +325,7 @@ __device__ __forceinline__ void sm_lu_from(double (&e)[8][8], SmallLds& L, int N
   if (threadIdx.x == 0)
     for (int i = 0; i < 4; ++i) stamp[i] += (double)q_[i];
 #endif
-  if constexpr (KK < 7) sm_lu_from<KK + 1>(e, L, N, ti, tj, bound, bad, stamp);
+  if constexpr (KK + 1 < NB) sm_lu_from<KK + 1, NB>(e, L, N, ti, tj, bound, bad, stamp);
 }
 
 // One wave's triangular sweeps over the LDS factors (N ≤ 128: entry i of the
@@ -363,25 +436,15 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
   const double* Qb = P.Q + (size_t)b * n * n;
   const double* Gb = P.G + (size_t)b * m * n;
   const double* Ab = P.A + (size_t)b * p * n;
-  SmSrc<STG> X;
+  const SmSrc X{Qb, Gb, Ab};
   SM_STAMP(0);
   if constexpr (STG) {
-    double* Qs = L.S;
-    double* Gs = Qs + n * n;
-    double* As = Gs + (size_t)m * n;
 #pragma unroll 8
-    for (int i = t; i < n * n; i += SM_T) Qs[i] = Qb[i];
+    for (int i = t; i < n * n; i += SM_T) L.S[i] = Qb[i];
 #pragma unroll 8
-    for (int i = t; i < m * n; i += SM_T) Gs[i] = Gb[i];
+    for (int i = t; i < m * n; i += SM_T) L.S[n * n + i] = Gb[i];
 #pragma unroll 8
-    for (int i = t; i < p * n; i += SM_T) As[i] = Ab[i];
-    X.Q = Qs;
-    X.G = Gs;
-    X.A = As;
-  } else {
-    X.Q = Qb;
-    X.G = Gb;
-    X.A = Ab;
+    for (int i = t; i < p * n; i += SM_T) L.S[n * n + m * n + i] = Ab[i];
   }
   for (int j = t; j < n; j += SM_T) L.z[j] = P.z[(size_t)b * n + j];
   __syncthreads();
@@ -402,10 +465,20 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
   const double bound = NOPIV_GROWTH * sm_block_max(amax, L.red);   // (its barriers end the staged reads)
   SM_STAMP(3);
 #ifdef SM_DEBUG
-  if (t == 0) printf("small: e00 %g e01 %g e10 %g Q0 %g X.Q0 %g amax %g nk %d\n", e[0][0], e[0][1], e[1][0], Qb[0], X.Q[0], amax, nk);
+  if (t == 0) printf("small: e00 %g e01 %g e10 %g Q0 %g amax %g nk %d\n", e[0][0], e[0][1], e[1][0], Qb[0], amax, nk);
 #endif
   int bad = 0;
-  sm_lu_from<0>(e, L, N, ti, tj, bound, bad, out + n + m + p + 8);
+  double* stamp = out + n + m + p + 8;   // (SM_STAMPS only)
+  switch ((N + SM_G - 1) / SM_G) {       // uniform
+    case 1: sm_lu_from<0, 1>(e, L, N, ti, tj, bound, bad, stamp); break;
+    case 2: sm_lu_from<0, 2>(e, L, N, ti, tj, bound, bad, stamp); break;
+    case 3: sm_lu_from<0, 3>(e, L, N, ti, tj, bound, bad, stamp); break;
+    case 4: sm_lu_from<0, 4>(e, L, N, ti, tj, bound, bad, stamp); break;
+    case 5: sm_lu_from<0, 5>(e, L, N, ti, tj, bound, bad, stamp); break;
+    case 6: sm_lu_from<0, 6>(e, L, N, ti, tj, bound, bad, stamp); break;
+    case 7: sm_lu_from<0, 7>(e, L, N, ti, tj, bound, bad, stamp); break;
+    default: sm_lu_from<0, 8>(e, L, N, ti, tj, bound, bad, stamp); break;
+  }
   SM_STAMP(4);
 #ifdef SM_DEBUG
   if (bad) printf("small: t %d rejects (N %d bound %g piv0 %g)\n", t, N, bound, L.S[0]);
