@@ -188,6 +188,7 @@ int dopt_destroy(dopt_handle* h) {
   if (h->meta_host) (void)hipHostFree(h->meta_host);
   if (h->pin) (void)hipHostFree(h->pin);
   if (h->meta_ev) (void)hipEventDestroy(h->meta_ev);
+  if (h->meta_fork) (void)hipEventDestroy(h->meta_fork);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;

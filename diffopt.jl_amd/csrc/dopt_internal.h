@@ -164,6 +164,7 @@ struct Handle {
   DevBuf mws;                // multi-RHS: per-workgroup vectors of tall systems (qp_multi.hip)
   QPMeta* meta_host = nullptr;     // pinned copy of `meta` (asynchronous read-back)
   hipEvent_t meta_ev = nullptr;    // recorded after the read-back copy
+  hipEvent_t meta_fork = nullptr;  // the LU's end on the handle's stream (the read-back on `aux` waits for it)
   // factorisation: 1 = no-pivot blocked LU with the threshold test and a
   // partial-pivoting re-factorisation of rejected problems (default);
   // 0 = partial pivoting for every problem (env DOPT_LU=0)
@@ -269,10 +270,14 @@ inline void ensure_aux(Handle& h) {
   DOPT_CHECK_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
   DOPT_CHECK_HIP(hipStreamCreateWithPriority(&h.aux, hipStreamNonBlocking, least));
   DOPT_CHECK_HIP(hipStreamCreateWithPriority(&h.crit, hipStreamNonBlocking, greatest));
-  DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_fork, hipEventDisableTiming));
-  DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_join, hipEventDisableTiming));
-  DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_qsym, hipEventDisableTiming));
-  DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_crit, hipEventDisableTiming));
+  // stream-to-stream dependencies on one device: a device-scope release is
+  // enough (the default system-scope fence writes the L2 back at every record)
+  const unsigned fl = hipEventDisableTiming | hipEventReleaseToDevice;
+  DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_fork, fl));
+  DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_join, fl));
+  DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_qsym, fl));
+  DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.ev_crit, fl));
+  DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.meta_fork, fl));
 }
 inline double* qsy_max(Handle& h) { return h.qsy.as<double>(); }
 inline int32_t* qsy_flag(Handle& h) { return reinterpret_cast<int32_t*>(h.qsy.as<double>() + h.batch); }

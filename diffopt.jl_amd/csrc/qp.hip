@@ -815,6 +815,21 @@ static void meta_copy(Handle& h) {
   DOPT_CHECK_HIP(hipEventRecord(h.meta_ev, h.stream));
 }
 
+// The same read-back on the second stream, forked from the handle's stream
+// by a device-scope event: the kernels queued next on the handle's stream (the
+// speculative solves after the LU) do not wait behind the copy.
+static void meta_copy_side(Handle& h) {
+  ensure_aux(h);
+  if (!h.meta_host) {
+    DOPT_CHECK_HIP(hipHostMalloc((void**)&h.meta_host, std::max<size_t>(h.batch, 1) * sizeof(QPMeta)));
+    DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.meta_ev, hipEventDisableTiming));
+  }
+  DOPT_CHECK_HIP(hipEventRecord(h.meta_fork, h.stream));
+  DOPT_CHECK_HIP(hipStreamWaitEvent(h.aux, h.meta_fork, 0));
+  DOPT_CHECK_HIP(hipMemcpyAsync(h.meta_host, h.meta.p, h.batch * sizeof(QPMeta), hipMemcpyDeviceToHost, h.aux));
+  DOPT_CHECK_HIP(hipEventRecord(h.meta_ev, h.aux));
+}
+
 // After the assembly: largest padded blocked system (sizes the blocked
 // launches), whether any problem needs the generic or the LSQR kernels.
 static void meta_sizes(Handle& h) {
@@ -890,7 +905,7 @@ static void factor_blocked(Handle& h, F&& spec, double* w0, double* w1, const Re
       qp_nopiv_factor(h, dinv_of(h), w0, w1);
     }
     if (pre_copy) (*pre_copy)();   // kernels whose metadata the read-back below should carry (NLP: the pivot check)
-    if (h.blocked_npmax) meta_copy(h);
+    if (h.blocked_npmax) meta_copy_side(h);
     spec();
     h.n_pivot = 0;
     if (h.blocked_npmax) {
@@ -1214,9 +1229,20 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     qp_blocked_solve2(h, dinv_of(h), rhs_of(h, 0), rhs_of(h, 1), x_of(h, 0), x_of(h, 1), sel, sw0, sw1);
   };
-  factor_blocked(h, [&] { solve2(h.lu_mode == 1 ? LU_SEL_NOPIV : LU_SEL_ALL, w0, w1); }, w0, w1, qp_reasm(h));
+  // with every problem on the no-pivot route the outputs are queued
+  // speculatively too, before the host reads the rejected list back; a
+  // fallback (partial pivoting, the generic LU) recomputes them all after
+  const bool spec_out = h.lu_mode == 1 && !h.has_generic && !h.has_lsqr;
+  h.n_generic = 0;   // (the speculative outputs must not run the previous factorisation's generic solves)
+  factor_blocked(
+      h,
+      [&] {
+        solve2(h.lu_mode == 1 ? LU_SEL_NOPIV : LU_SEL_ALL, w0, w1);
+        if (spec_out) finish_pair(h, out_rev, out_fwd);
+      },
+      w0, w1, qp_reasm(h));
   if (h.n_pivot > 0) solve2(LU_SEL_PIVOT, nullptr, nullptr);
-  finish_pair(h, out_rev, out_fwd);
+  if (!spec_out || h.n_pivot > 0 || h.n_generic > 0) finish_pair(h, out_rev, out_fwd);
   h.factored = true;   // the factors stay valid for later reverse / forward calls
   // the host already knows every info: the no-pivot LU accepted every blocked
   // problem (an accepted factor has no zero pivot) and no fallback or generic

@@ -569,9 +569,27 @@ __global__ __launch_bounds__(SM_T) void qp_small_fwd_kernel(QPIn P, FwdTangents 
   double* S = L.S;
   const double* Kb = K + (size_t)b * nmax * ld;
   const int lane = t & 63, wv = t >> 6;
-  for (int r = wv; r < N; r += SM_T / 64)
-    for (int c = lane; c < N; c += 64) S[r * SM_LD + c] = Kb[(size_t)r * ld + c];
-  for (int r = t; r < N; r += SM_T) L.dinv[r] = 1.0 / Kb[(size_t)r * ld + r];
+  // the factors into LDS: rows by wave, 8 rows × 2 column halves per round,
+  // all sixteen loads in flight before any store
+  for (int r0 = wv; r0 < N; r0 += 8 * (SM_T / 64)) {
+    double v[8][2];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int r = r0 + u * (SM_T / 64), c = lane + 64 * hh;
+        v[u][hh] = Kb[(size_t)(r < N ? r : 0) * ld + (c < N ? c : 0)];
+      }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int r = r0 + u * (SM_T / 64), c = lane + 64 * hh;
+        if (r < N && c < N) S[r * SM_LD + c] = v[u][hh];
+      }
+  }
+  __syncthreads();
+  for (int r = t; r < N; r += SM_T) L.dinv[r] = 1.0 / S[r * SM_LD + r];
   // the full forward right-hand side r (QuadraticProgram.jl:429-433):
   //   [dQ z + dq + dGᵀλ + dAᵀν; λ.*(dG z) − λ.*dh; dA z − db] — r1 and r3 in
   // y (reduced positions), r2 kept in registers per row for the recovery
