@@ -1249,7 +1249,8 @@ __global__ __launch_bounds__(CTPB) void conic_rev_out_kernel(
 // both live sequences of its problem (gemv_multi<2>, each product in the
 // single-sequence order: bit-identical to two separate runs).
 // ---------------------------------------------------------------------------
-constexpr int SPLIT_CHUNK = 8;
+constexpr int SPLIT_CHUNK = 8;        // iterations queued before the first convergence read-back ...
+constexpr int SPLIT_CHUNK_MAX = 64;   // ... doubling per read-back up to this (fused form)
 #ifndef DOPT_SPLIT_K
 #define DOPT_SPLIT_K 8
 #endif
@@ -2361,18 +2362,23 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
     };
     for (int s = 0; s < ns; ++s) dpiV(sl[s], 1);
     bool first = ns > 1;
+    // the host reads the active count back after 8, 16, 32, then every 64
+    // iterations (each read-back drains both streams; an iteration queued
+    // after convergence costs only its launches' early exits)
+    int chunk = SPLIT_CHUNK;
     for (int it = 0; it < maxit;) {
       bool any = false;
       for (int s = 0; s < ns; ++s) any |= sl[s].left > 0;
       if (!any) break;
       int k = 0;
-      for (; k < SPLIT_CHUNK && it + k < maxit; ++k)
+      for (; k < chunk && it + k < maxit; ++k)
         for (int s = 0; s < ns; ++s)
           if (sl[s].left > 0) {
             iteration(sl[s], first && s == 0);
             first = false;
           }
       it += k;
+      chunk = std::min(2 * chunk, SPLIT_CHUNK_MAX);
       ccheck();
       for (int s = 0; s < ns; ++s)
         if (sl[s].left > 0)
