@@ -142,3 +142,29 @@ def test_small_path_singular_reports_info(QPBatch):
     with pytest.raises(SingularException):
         e.reverse(d["dl_dz"])
     e.close()
+
+
+@pytest.mark.parametrize("n,m,p,phi", [(1, 1, 0, 0.0), (5, 3, 0, 0.5), (7, 0, 2, 0.0), (17, 9, 4, 0.4),
+                                       (33, 40, 15, 0.3), (64, 64, 0, 1.0), (96, 31, 31, 0.0)])
+def test_small_path_shapes(QPBatch, n, m, p, phi):
+    """Ragged shapes around the register tiles' 16-row blocks and the four-step
+    groups (N' = 1, not a multiple of 4 or 16, exactly 128, m = 0, p = 0),
+    with dense tangents so every forward RHS term is live; batch 2, both
+    directions against the oracle, and the path actually taken."""
+    from diffopt_amd.synthetic import qp_numpy
+    d = qp_numpy(2, n, m, p, phi, 1000 + n + m + p, dense_tangents=True)
+    e = QPBatch(2, n, m, p)
+    e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    rev = e.reverse(d["dl_dz"])
+    assert (e.lu_kind() == SMALL).all(), e.lu_kind()
+    fwd = e.forward(dQ=d["dQ"], dq=d["dq"], dG=d["dG"] if m else None, dh=d["dh"] if m else None,
+                    dA=d["dA"] if p else None, db=d["db"] if p else None)
+    e.close()
+    for b in range(2):
+        args = [d[k][b] for k in ("Q", "G", "h", "A", "z", "lam", "nu")]
+        ref_r = np.concatenate(oqp.reverse_differentiate(*args, d["dl_dz"][b]))
+        ref_f = np.concatenate(oqp.forward_differentiate(
+            *args, dQ=d["dQ"][b], dq=d["dq"][b], dG=d["dG"][b] if m else None, dh=d["dh"][b] if m else None,
+            dA=d["dA"][b] if p else None, db=d["db"][b] if p else None))
+        assert relfro(rev[b], ref_r) <= RTOL
+        assert relfro(fwd[b], ref_f) <= RTOL
