@@ -328,23 +328,22 @@ __device__ __forceinline__ void sm_lu_from(double (&e)[8][8], SmallLds& L, int N
   if constexpr (KK + 1 < NB) sm_lu_from<KK + 1, NB>(e, L, N, ti, tj, bound, bad, stamp);
 }
 
-// One wave's triangular sweeps over the LDS factors (N ≤ 128: entry i of the
-// vector in lane i & 63, register i >> 6); step k's entry by v_readlane.
-__device__ __forceinline__ double sm_entry(double y0, double y1, int k) {
-  const double v = k < 64 ? y0 : y1;
-  return __longlong_as_double(((long long)__builtin_amdgcn_readlane((int)(__double_as_longlong(v) >> 32), k & 63)
-                               << 32) |
-                              (unsigned)__builtin_amdgcn_readlane((int)__double_as_longlong(v), k & 63));
-}
-// One sweep: step k (ascending when LOWER — the entries past k — descending
-// otherwise — the entries before k) takes entry k (× 1/d_k when DIAG, which
-// also stores it) and updates every other live entry i with its coefficient,
+// One sweep over the LU image by one wave, vector entry i in lane i & 63,
+// register i >> 6: step k (ascending when LOWER — the entries past k —,
+// descending otherwise — the entries before k) takes entry k by v_readlane
+// (× 1/d_k when DIAG) and updates the live entries with their coefficients,
 // S[i][k] (column sweeps: L y = r, U x = y) or S[k][i] (TRANS: Uᵀ w = r,
-// Lᵀ x = w).  The coefficients of the next four steps are loaded while the
-// current four run, so the chain is readlane → fma only.
-template <bool LOWER, bool TRANS, bool DIAG>
-__device__ __forceinline__ void sm_sweep(const double* S, const double* dinv, int N, int lane, double& y0,
-                                         double& y1) {
+// Lᵀ x = w).  The steps run in two phases, k < 64 and k ≥ 64, so the pivot
+// entry's register is fixed per phase and one of the two registers needs no
+// mask at all (every lane of it is past / before k, or outside the system);
+// DIAG entries are divided at the end (a step never updates its own entry).
+// The next four steps' coefficients are loaded while the current four run.
+// M0 / M1: how step k updates register 0 / 1 — 0 not at all, 1 every lane,
+// 2 the lanes past (LOWER) / before k.
+template <bool LOWER, bool TRANS, bool DIAG, bool HI, int M0, int M1>
+__device__ __forceinline__ void sm_sweep_phase(const double* S, const double* dinv, int kfirst, int cnt, int lane,
+                                               double& y0, double& y1) {
+  if (cnt <= 0) return;
   const int i0 = lane, i1 = lane + 64;
   auto coef = [&](int k, int i) {   // k clamped into the image (the tail's dead loads)
     const int kc = k < 0 ? 0 : (k > SM_MAX - 1 ? SM_MAX - 1 : k);
@@ -352,45 +351,66 @@ __device__ __forceinline__ void sm_sweep(const double* S, const double* dinv, in
   };
   auto dget = [&](int k) { return DIAG ? dinv[k < 0 ? 0 : (k > SM_MAX - 1 ? SM_MAX - 1 : k)] : 1.0; };
   const int st = LOWER ? 1 : -1;
-  int k = LOWER ? 0 : N - 1;
+  int k = kfirst;
   double c0[4], c1[4], dv[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    c0[q] = coef(k + q * st, i0);
-    c1[q] = coef(k + q * st, i1);
+    if (M0) c0[q] = coef(k + q * st, i0);
+    if (M1) c1[q] = coef(k + q * st, i1);
     dv[q] = dget(k + q * st);
   }
-  for (int it = 0; it < N; it += 4) {
+  for (int it = 0; it < cnt; it += 4) {
     double n0[4], n1[4], nd[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      n0[q] = coef(k + (q + 4) * st, i0);
-      n1[q] = coef(k + (q + 4) * st, i1);
+      if (M0) n0[q] = coef(k + (q + 4) * st, i0);
+      if (M1) n1[q] = coef(k + (q + 4) * st, i1);
       nd[q] = dget(k + (q + 4) * st);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      if (it + q < N) {   // uniform
+      if (it + q < cnt) {   // uniform
         const int kq = k + q * st;
-        double v = sm_entry(y0, y1, kq);
-        if (DIAG) {
-          v *= dv[q];
-          y0 = i0 == kq ? v : y0;
-          y1 = i1 == kq ? v : y1;
-        }
-        const bool u0 = LOWER ? (i0 > kq && i0 < N) : i0 < kq;
-        const bool u1 = LOWER ? (i1 > kq && i1 < N) : i1 < kq;
-        y0 = u0 ? fma(-c0[q], v, y0) : y0;
-        y1 = u1 ? fma(-c1[q], v, y1) : y1;
+        const double src = HI ? y1 : y0;
+        double v = __longlong_as_double(
+            ((long long)__builtin_amdgcn_readlane((int)(__double_as_longlong(src) >> 32), kq & 63) << 32) |
+            (unsigned)__builtin_amdgcn_readlane((int)__double_as_longlong(src), kq & 63));
+        if (DIAG) v *= dv[q];
+        if (M0 == 1) y0 = fma(-c0[q], v, y0);
+        if (M0 == 2) y0 = (LOWER ? i0 > kq : i0 < kq) ? fma(-c0[q], v, y0) : y0;
+        if (M1 == 1) y1 = fma(-c1[q], v, y1);
+        if (M1 == 2) y1 = (LOWER ? i1 > kq : i1 < kq) ? fma(-c1[q], v, y1) : y1;
       }
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      c0[q] = n0[q];
-      c1[q] = n1[q];
+      if (M0) c0[q] = n0[q];
+      if (M1) c1[q] = n1[q];
       dv[q] = nd[q];
     }
     k += 4 * st;
+  }
+}
+// Lanes at or past N may hold anything: they are never read back (v_readlane
+// takes k < N only, the callers store entries < N only).
+template <bool LOWER, bool TRANS, bool DIAG>
+__device__ __forceinline__ void sm_sweep(const double* S, const double* dinv, int N, int lane, double& y0,
+                                         double& y1) {
+  const int lo = N < 64 ? N : 64;   // steps with k < 64
+  if (LOWER) {
+    if (N > 64) {
+      sm_sweep_phase<LOWER, TRANS, DIAG, false, 2, 1>(S, dinv, 0, lo, lane, y0, y1);
+      sm_sweep_phase<LOWER, TRANS, DIAG, true, 0, 2>(S, dinv, 64, N - 64, lane, y0, y1);
+    } else {
+      sm_sweep_phase<LOWER, TRANS, DIAG, false, 2, 0>(S, dinv, 0, lo, lane, y0, y1);
+    }
+  } else {
+    sm_sweep_phase<LOWER, TRANS, DIAG, true, 1, 2>(S, dinv, N - 1, N - 64, lane, y0, y1);
+    sm_sweep_phase<LOWER, TRANS, DIAG, false, 2, 0>(S, dinv, lo - 1, lo, lane, y0, y1);
+  }
+  if (DIAG) {
+    y0 *= dinv[lane];
+    y1 *= dinv[lane + 64];
   }
 }
 // the four solves over the LU image: L unit lower below the diagonal, U on and
