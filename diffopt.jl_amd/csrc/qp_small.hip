@@ -185,14 +185,15 @@ __device__ __forceinline__ double sm_assemble(const QPIn& P, const SmSrc& X, con
 // NOPIV_GROWTH·max|K|).  Group k … k+3 (k = 16·KK + 4g):
 //   before the barrier, the wave holding rows k … k+3 (wave g: thread row
 //   class ti = t / 16) gathers the 4 × 4 diagonal block by v_readlane,
-//   factors it, and turns its rows into U's rows (L_D u = y, the earlier
-//   rows' entries by lane shuffles); it publishes them (zeros up to the
-//   group's last column), the block's factors and 1/diag(U_D), and stores
-//   them to the factor image with the tests; the owners of columns k … k+3
-//   publish them below the group's rows (zeros above);
-//   after it, every thread derives L's entries of its rows (l U_D = x; the
-//   columns' owners store them with the threshold test) and applies the
-//   rank-4 fma to its live blocks.
+//   factors it, publishes the factors (1/u_jj on the diagonal) and its raw
+//   rows past the group's columns (zeros before), and stores the block to the
+//   factor image with the tests; the owners of columns k … k+3 publish them
+//   below the group's rows (zeros above);
+//   after it, every thread derives L's entries of its rows (l U_D = x) and
+//   U's entries of its columns (L_D u = y) — the owners store theirs to the
+//   image with the tests — and applies the rank-4 fma to its live blocks.
+//   (U's rows formed by the group's wave before the barrier, by lane
+//   shuffles, measured 117.5 k against 112.5 k cycles for config 1's LU.)
 // Blocks a, c < KK are past and blocks a, c ≥ NB = ⌈N / 16⌉ pure padding, both
 // compile-time (the kernel dispatches on NB); identity rows pad the system to
 // a multiple of four.
@@ -250,28 +251,10 @@ __device__ __forceinline__ void sm_lu_from(double (&e)[8][8], SmallLds& L, int N
           if (i == j) bad |= !(fabs(v) > 0.0);
         }
       }
-      double lrow[SM_GB - 1];   // L_D's row jr
 #pragma unroll
-      for (int q = 0; q < SM_GB - 1; ++q) {
-        double v = 0.0;
-#pragma unroll
-        for (int i = q + 1; i < SM_GB; ++i) v = jr == i ? d[i * SM_GB + q] : v;
-        lrow[q] = v;
-      }
-#pragma unroll
-      for (int c8 = KK; c8 < NB; ++c8) {
+      for (int c8 = KK; c8 < NB; ++c8) {   // the group's raw rows past its columns
         const int c = tj + SM_G * c8;
-        double v = e[KK][c8];   // row k + jr
-#pragma unroll
-        for (int q = 0; q < SM_GB - 1; ++q) {
-          const double uq = __shfl(v, 16 * q + tj);   // row k + q's entry, final
-          v = jr > q ? fma(-lrow[q], uq, v) : v;
-        }
-        L.rowb[buf][jr][c] = c > k3 ? v : 0.0;
-        if (c > k3 && c < N && k + jr < N) {
-          S[(k + jr) * SM_LD + c] = v;
-          bad |= !(fabs(v) <= bound);
-        }
+        L.rowb[buf][jr][c] = c > k3 ? e[KK][c8] : 0.0;
       }
     }
     if (cown)
@@ -283,11 +266,12 @@ __device__ __forceinline__ void sm_lu_from(double (&e)[8][8], SmallLds& L, int N
     SM_LAP(0);
     __syncthreads();
     SM_LAP(1);
-    // U_D's strict upper triangle and 1/diag(U_D)
+    // the diagonal block's factors: L_D strictly below, U_D strictly above,
+    // 1/diag(U_D) on the diagonal
     double ud[SM_GB * SM_GB];
 #pragma unroll
-    for (int i = 0; i < SM_GB * SM_GB; ++i)
-      if (i / SM_GB <= i % SM_GB) ud[i] = L.dblk[buf][i];
+    for (int i = 0; i < SM_GB * SM_GB; ++i) ud[i] = L.dblk[buf][i];
+    const int jr = ti - SM_GB * g;   // the thread's row class in the group (owners of U's rows: 0 … 3)
     // L's entries of the thread's rows: l U_D = x, x = the rows' group columns
     double l[8][SM_GB];
 #pragma unroll
@@ -311,9 +295,22 @@ __device__ __forceinline__ void sm_lu_from(double (&e)[8][8], SmallLds& L, int N
 #pragma unroll
     for (int c8 = KK; c8 < NB; ++c8) {
       const int c = tj + SM_G * c8;
+      // U's entries of the column: L_D u = y, y = the group rows' raw entries
       double u[SM_GB];
 #pragma unroll
-      for (int j = 0; j < SM_GB; ++j) u[j] = L.rowb[buf][j][c];
+      for (int j = 0; j < SM_GB; ++j) {
+        double y = L.rowb[buf][j][c];
+#pragma unroll
+        for (int q = 0; q < j; ++q) y = fma(-ud[j * SM_GB + q], u[q], y);
+        u[j] = y;
+      }
+      if (jr >= 0 && jr < SM_GB && c > k3 && c < N && k + jr < N) {   // row k + jr of U: image, growth test
+        double v = u[0];
+#pragma unroll
+        for (int j = 1; j < SM_GB; ++j) v = jr == j ? u[j] : v;
+        S[(k + jr) * SM_LD + c] = v;
+        bad |= !(fabs(v) <= bound);
+      }
 #pragma unroll
       for (int a = KK; a < NB; ++a)
 #pragma unroll
