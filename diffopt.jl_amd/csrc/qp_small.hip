@@ -26,6 +26,7 @@
 // the reference's coordinates.  Same semantics, different rounding: the
 // outputs agree with the batched route and the oracle to the parity bar.
 #include "dopt_internal.h"
+#include <type_traits>
 
 namespace dopt {
 
@@ -72,9 +73,12 @@ struct SmallLds {
 struct SmSrc {
   const double *Q, *G, *A;
 };
+// (offsets in 32 bits when staged: the stage holds at most SM_MAX·SM_LD doubles)
 template <bool STG>
-__device__ __forceinline__ double sm_src(const SmallLds& Ls, const SmSrc& Xs, int src, size_t idx, int nn, int mm) {
-  if constexpr (STG) return Ls.S[(src == 0 ? 0 : src == 1 ? (size_t)nn * nn : (size_t)nn * nn + (size_t)mm * nn) + idx];
+using SmOff = typename std::conditional<STG, int, size_t>::type;
+template <bool STG>
+__device__ __forceinline__ double sm_src(const SmallLds& Ls, const SmSrc& Xs, int src, SmOff<STG> idx, int nn, int mm) {
+  if constexpr (STG) return Ls.S[(src == 0 ? 0 : src == 1 ? nn * nn : nn * nn + mm * nn) + idx];
   else return (src == 0 ? Xs.Q : src == 1 ? Xs.G : Xs.A)[idx];
 }
 
@@ -102,7 +106,8 @@ __device__ __forceinline__ int sm_prepare(const QPIn& P, const SmSrc& X, int b, 
       // arithmetic
       double acc = 0.0;
 #pragma unroll 8
-      for (int j = 0; j < n; ++j) acc = __dadd_rn(acc, __dmul_rn(sm_src<STG>(L, X, 1, i + (size_t)j * m, n, m), L.z[j]));
+      for (int j = 0; j < n; ++j)
+        acc = __dadd_rn(acc, __dmul_rn(sm_src<STG>(L, X, 1, i + (SmOff<STG>)j * m, n, m), L.z[j]));
       si = __dsub_rn(acc, P.h[(size_t)b * m + i]);
       li = P.lam[(size_t)b * m + i];
       s_out[(size_t)b * m + i] = si;
@@ -151,21 +156,21 @@ __device__ __forceinline__ double sm_assemble(const QPIn& P, const SmSrc& X, con
     for (int c8 = 0; c8 < 8; ++c8) {
       const int r = ti + SM_G * a, c = tj + SM_G * c8;
       int which = 0;
-      size_t off = 0;
+      SmOff<STG> off = 0;
       double mul = 0.0, cv = r == c ? 1.0 : 0.0;
       if (r < N && c < N) {
         cv = 0.0;
         mul = 1.0;
         if (r < n) {
-          if (c < n) off = r + (size_t)c * n;
-          else if (c < n + nk) { which = 1; off = L.kidx[c - n] + (size_t)r * m; mul = L.lk[c - n]; }
-          else { which = 2; off = (c - n - nk) + (size_t)r * p; }
+          if (c < n) off = r + (SmOff<STG>)c * n;
+          else if (c < n + nk) { which = 1; off = L.kidx[c - n] + (SmOff<STG>)r * m; mul = L.lk[c - n]; }
+          else { which = 2; off = (c - n - nk) + (SmOff<STG>)r * p; }
         } else if (r < n + nk) {
-          if (c < n) { which = 1; off = L.kidx[r - n] + (size_t)c * m; }
+          if (c < n) { which = 1; off = L.kidx[r - n] + (SmOff<STG>)c * m; }
           else { mul = 0.0; cv = c == r ? L.sk[r - n] : 0.0; }
         } else if (c < n) {
           which = 2;
-          off = (r - n - nk) + (size_t)c * p;
+          off = (r - n - nk) + (SmOff<STG>)c * p;
         } else {
           mul = 0.0;
         }
