@@ -660,6 +660,7 @@ int dopt_nlp_set_kkt(dopt_handle* h, int32_t rows, int32_t num_w, int32_t num_co
       throw Error(-1, "dopt_nlp_set_kkt: bad sizes");
     if (!M) throw Error(-1, "M is required");
     h->nlp_kkt = true;
+    h->lhs_info.clear();   // (dopt_lhs_resolve: only after a dopt_lhs_solve of this matrix)
     h->nlp_rows = rows;
     h->nlp_num_w = num_w;
     h->nlp_ncons = num_cons;
@@ -800,6 +801,28 @@ int dopt_lhs_solve(dopt_handle* h, int32_t rows, const double* M, int32_t k, con
   if (rc) return rc;
   for (int32_t v : info)
     if (v > 0) return v;   // LHS \ RHS raises SingularException(info)
+  return 0;
+}
+
+int dopt_lhs_resolve(dopt_handle* h, int32_t k, const double* rhs, double* x, int32_t trans) {
+  if (!h) return -1;
+  std::vector<int32_t> info(h->batch, 0);
+  const int rc = guarded(h, [&]() {
+    if (k <= 0) throw Error(-1, "k must be positive");
+    if (!rhs || !x) throw Error(-1, "rhs and x are required");
+    Timer tm;
+    const size_t cnt = (size_t)k * h->batch * h->nlp_rows;
+    const double* r = stage_in(*h, h->tin[0], rhs, cnt);
+    double* o = out_ptr(*h, h->tout[0], x, cnt);
+    dopt::lhs_resolve(*h, k, r, o, trans != 0, info.data());
+    copy_out(*h, x, o, cnt);
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    h->last_time = tm.s();
+    return 0;
+  });
+  if (rc) return rc;
+  for (int32_t v : info)
+    if (v > 0) return v;
   return 0;
 }
 

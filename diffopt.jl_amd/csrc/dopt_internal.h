@@ -206,6 +206,7 @@ struct Handle {
   int32_t nlp_ncons = 0;           // constraint rows of M (KKT mode: as given)
   int32_t nlp_max_corr = 50;       // inertia corrections tried (0: a singular M is reported, dopt_lhs_solve)
   bool nlp_kkt = false;
+  std::vector<int32_t> lhs_info;   // dopt_lhs_solve: info of the last non-iterative factorisation (dopt_lhs_resolve)
   DevBuf nlp_map;                  // int32 index maps (nlp.hip NLPMap)
   const double* nin[12] = {};      // Hxx, Hxp, Jx, Jp, x, cval, crhs, y, xl, xu, yl, yu (KKT mode: nin[0] = M)
   DevBuf own_nin[12];
@@ -359,6 +360,7 @@ void factor_dense(Handle& h, const ReasmFn& reasm, const std::function<void()>* 
 double* dense_dinv(Handle& h);
 void lsqr_slabs(Handle& h, int trans, const double* rhs, double* x);
 void lhs_solve(Handle& h, int k, const double* rhs, double* x, bool iterative, int32_t* info);
+void lhs_resolve(Handle& h, int k, const double* rhs, double* x, bool trans, int32_t* info);
 void nlp_configure(Handle& h);
 void nlp_factor(Handle& h);
 void nlp_forward(Handle& h, const double* dp, double* dx, double* ddual);
@@ -366,7 +368,7 @@ void nlp_reverse(Handle& h, const double* dx, const double* ddual, double* dp);
 void nlp_forward_reverse(Handle& h, const double* dp, const double* dxs, const double* dds, double* dx,
                          double* ddual, double* dpo);
 void nlp_jacobian(Handle& h, double* ds);
-void nlp_kkt_solve(Handle& h, int k, const double* rhs, double* x);
+void nlp_kkt_solve(Handle& h, int k, const double* rhs, double* x, bool trans = false);
 void conic_factor(Handle& h);
 void conic_forward(Handle& h, const double* dA, const double* db, const double* dc,
                    double* out, double* out_dx);

@@ -1209,7 +1209,7 @@ void nlp_jacobian(Handle& h, double* ds) {
 // nlp_utilities.jl:436-442): x = K \ rhs for k right-hand sides per problem,
 // rhs / x seed-major with stride rows (k × B × rows); problems whose
 // inertia correction failed give zeros.
-void nlp_kkt_solve(Handle& h, int k, const double* rhs, double* x) {
+void nlp_kkt_solve(Handle& h, int k, const double* rhs, double* x, bool trans) {
   if (!h.nfactored) nlp_factor(h);
   if (k <= 0) throw Error(-1, "dopt_nlp_kkt_solve: k must be positive");
   const int B = (int)h.batch, R = h.nlp_rows;
@@ -1221,7 +1221,7 @@ void nlp_kkt_solve(Handle& h, int k, const double* rhs, double* x) {
   DOPT_CHECK_HIP(hipMemsetAsync(rk, 0, blk * k * sizeof(double), h.stream));
   DOPT_CHECK_HIP(hipMemcpy2DAsync(rk, h.nmax * sizeof(double), rhs, R * sizeof(double), R * sizeof(double),
                                   (size_t)k * B, hipMemcpyDeviceToDevice, h.stream));
-  solve_multi(h, 0, k, rk, xk);
+  solve_multi(h, trans ? 1 : 0, k, rk, xk);
   DOPT_CHECK_HIP(hipMemcpy2DAsync(x, R * sizeof(double), xk, h.nmax * sizeof(double), R * sizeof(double),
                                   (size_t)k * B, hipMemcpyDeviceToDevice, h.stream));
   // failed corrections: zeros
@@ -1229,6 +1229,17 @@ void nlp_kkt_solve(Handle& h, int k, const double* rhs, double* x) {
     if (h.nlp_corr[b] < 0)
       for (int j = 0; j < k; ++j)
         DOPT_CHECK_HIP(hipMemsetAsync(x + ((size_t)j * B + b) * R, 0, R * sizeof(double), h.stream));
+}
+
+// A further solve on the factorisation of the last non-iterative lhs_solve:
+// M x = rhs, or Mᵀ x = rhs (`trans`) — the plug point's LHS' call after its
+// LHS call (QuadraticProgram.jl:335, :438) without a second factorisation.
+// info as the factorising call reported it (Mᵀ is singular exactly when M is).
+void lhs_resolve(Handle& h, int k, const double* rhs, double* x, bool trans, int32_t* info) {
+  if (!h.nlp_kkt || !h.nfactored || h.lhs_info.size() != (size_t)h.batch)
+    throw Error(-1, "dopt_lhs_resolve: no factorisation from a non-iterative dopt_lhs_solve");
+  std::copy(h.lhs_info.begin(), h.lhs_info.end(), info);
+  nlp_kkt_solve(h, k, rhs, x, trans);
 }
 
 // The reference's QuadraticProgram.LinearAlgebraSolver plug point
@@ -1254,9 +1265,11 @@ void lhs_solve(Handle& h, int k, const double* rhs, double* x, bool iterative, i
     DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h.meta.p, B * sizeof(QPMeta), hipMemcpyDeviceToHost, h.stream));
     DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
     for (int b = 0; b < B; ++b) info[b] = h.nlp_corr[b] < 0 ? std::max(meta[b].info, 1) : 0;
-    nlp_kkt_solve(h, k, rhs, x);
+    h.lhs_info.assign(info, info + B);
+    nlp_kkt_solve(h, k, rhs, x, false);
     return;
   }
+  h.lhs_info.clear();
   // LSQR: M into the slabs, every problem on the `iterative` branch
   DOPT_CHECK_HIP(hipMemsetAsync(h.nlp_shift.p, 0, (size_t)B * sizeof(int32_t), h.stream));
   DOPT_CHECK_HIP(hipMemsetAsync(h.kamax.p, 0, (size_t)B * sizeof(double), h.stream));

@@ -55,6 +55,7 @@ SIGNATURES = {
     "dopt_conic_lsqr_norms": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_lhs_solve": (ctypes.c_int, [_h, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_int32]),
+    "dopt_lhs_resolve": (ctypes.c_int, [_h, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]),
     "dopt_qp_params_reverse": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64]
                                + [ctypes.c_void_p] * 5),
     "dopt_qp_params_forward": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64]

@@ -367,6 +367,8 @@ class MI355XSolver:
         self.device = device
         self._h = None
         self._key = None
+        self._fact = None      # (memory key of the array factorised last, the array)
+        self.resolves = 0      # calls served by dopt_lhs_resolve (introspection)
         self.lib = _lib.load()
 
     def close(self):
@@ -374,6 +376,7 @@ class MI355XSolver:
             self.lib.dopt_destroy(self._h)
             self._h = None
             self._key = None
+            self._fact = None
 
     def __del__(self):
         try:
@@ -413,11 +416,29 @@ class MI355XSolver:
             raise TypeError("RHS does not match LHS")
         k = Rk.shape[2]
         rhs = np.ascontiguousarray(np.transpose(Rk, (2, 0, 1)))   # seed-major (k, B, rows)
-        Mc = np.ascontiguousarray(np.swapaxes(M, 1, 2))            # column-major per problem
         out = np.empty_like(rhs)
         h = self._handle(B, rows)
-        rc = self.lib.dopt_lhs_solve(h, rows, Mc.ctypes.data, k, rhs.ctypes.data, out.ctypes.data,
-                                     int(bool(iterative)))
+        # the reference's second call per model passes LHS' (an adjoint of the
+        # LHS it just solved with: QuadraticProgram.jl:335, :438): an array
+        # that is exactly the transpose of the one factorised last (same
+        # memory, shape and strides reversed) is answered from those factors,
+        # once per factorisation; any other call factorises (the array may
+        # have changed in place since)
+        lhs = LHS if isinstance(LHS, np.ndarray) else None
+        key = None
+        if lhs is not None and lhs.ndim == 2:
+            key = (lhs.__array_interface__["data"][0], lhs.shape, lhs.strides)
+        reuse = (not iterative and key is not None and self._fact is not None
+                 and (key[0], key[1][::-1], key[2][::-1]) == self._fact[0])
+        if reuse:
+            rc = self.lib.dopt_lhs_resolve(h, k, rhs.ctypes.data, out.ctypes.data, 1)
+            self.resolves += 1
+            self._fact = None
+        else:
+            Mc = np.ascontiguousarray(np.swapaxes(M, 1, 2))        # column-major per problem
+            rc = self.lib.dopt_lhs_solve(h, rows, Mc.ctypes.data, k, rhs.ctypes.data, out.ctypes.data,
+                                         int(bool(iterative)))
+            self._fact = None if iterative or key is None else (key, lhs)   # (lhs kept alive)
         _lib.check(rc, h)
         X = np.transpose(out, (1, 2, 0))                           # (B, rows, k)
         if vec:

@@ -251,29 +251,48 @@ mutable struct MI355XSolver
     device::Int
     handle::Union{Nothing,Handle}
     rows::Int
+    last::Any          # the matrix whose factorisation the handle holds (by identity)
+    last_adj::Bool     # ... factorised as its adjoint
 end
-MI355XSolver(; device::Integer = 0) = MI355XSolver(device, nothing, 0)
+MI355XSolver(; device::Integer = 0) = MI355XSolver(device, nothing, 0, nothing, false)
 
 function _solver_handle!(s::MI355XSolver, rows::Int)
     if s.handle === nothing || s.rows != rows
         s.handle = Handle(rows, 0, 0; device = s.device, kind = KIND_NLP)
         s.rows = rows
+        s.last = nothing
     end
     return s.handle
 end
 
 function QP.solve_system(s::MI355XSolver, LHS, RHS, iterative)
     rows = size(LHS, 1)
-    # LHS, or LHS' materialised (column-major); a sparse LHS is densified here
-    # (the engine's dense LU: UMFPACK's sparsity is not exploited)
-    M = Matrix{Float64}(LHS)
     rhs = Vector{Float64}(RHS)
     x = Vector{Float64}(undef, rows)
     h = _solver_handle!(s, rows)
+    # the second call per model passes LHS' — an Adjoint wrapping the very
+    # LHS just factorised (:335 then :438): answered from those factors by a
+    # transposed solve (dopt_lhs_resolve), in either order
+    adj = LHS isa LinearAlgebra.Adjoint || LHS isa LinearAlgebra.Transpose
+    obj = adj ? parent(LHS) : LHS
+    if !iterative && s.last !== nothing && obj === s.last && adj != s.last_adj
+        GC.@preserve rhs x begin
+            rc = ccall((:dopt_lhs_resolve, LIB), Cint,
+                       (Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}, Int32), h.ptr, 1, rhs, x, 1)
+            s.last = nothing                 # one reuse per factorisation
+            _check(rc, h.ptr)                # the factorising call's info again
+        end
+        return x
+    end
+    # LHS, or LHS' materialised (column-major); a sparse LHS is densified here
+    # (the engine's dense LU: UMFPACK's sparsity is not exploited)
+    M = Matrix{Float64}(LHS)
     GC.@preserve M rhs x begin
         rc = ccall((:dopt_lhs_solve, LIB), Cint,
                    (Ptr{Cvoid}, Int32, Ptr{Float64}, Int32, Ptr{Float64}, Ptr{Float64}, Int32),
                    h.ptr, rows, M, 1, rhs, x, Int32(iterative))
+        s.last = iterative ? nothing : obj
+        s.last_adj = adj
         _check(rc, h.ptr)                    # rc > 0: SingularException(rc)
     end
     return x

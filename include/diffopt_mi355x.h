@@ -351,6 +351,14 @@ int dopt_nlp_kkt_solve(dopt_handle* h, int32_t k, const double* rhs, double* x);
  * iterative: LSQR with IterativeSolvers' defaults, as the reference. */
 int dopt_lhs_solve(dopt_handle* h, int32_t rows, const double* M, int32_t k, const double* rhs, double* x,
                    int32_t iterative);
+/* A further solve on the factorisation of the last non-iterative
+ * dopt_lhs_solve of this handle: M x = rhs (trans 0) or Mᵀ x = rhs (trans 1),
+ * same shapes; returns that call's info again (Mᵀ is singular exactly when M
+ * is).  The plug point's second call per model (`LHS'`, QuadraticProgram.jl:438,
+ * after `LHS` at :335) then costs the solves, not a second factorisation —
+ * the Julia shim takes it when the adjoint's parent is the matrix it last
+ * factorised.  < 0 if no such factorisation is held. */
+int dopt_lhs_resolve(dopt_handle* h, int32_t k, const double* rhs, double* x, int32_t trans);
 
 int dopt_get_info(dopt_handle* h, int32_t* info);
 /* per-problem `iterative` branch flags (QP; 1 = LSQR branch). */

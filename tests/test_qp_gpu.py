@@ -684,3 +684,42 @@ def test_left_looking_factors_serve_every_solve(QPBatch, monkeypatch, shape):
     r3, f3 = g.forward_reverse(d["dl_dz"], **fkw)
     assert relfro(r3, r1) <= 1e-9 and relfro(f3, f1) <= 1e-9
     g.close()
+
+
+def test_plug_point_adjoint_reuses_factors():
+    """MI355XSolver: the reference's second call per model passes LHS' (the
+    adjoint of the LHS just solved, QuadraticProgram.jl:335, :438); the solver
+    answers it from the same factorisation (dopt_lhs_resolve, transposed),
+    against numpy at 1e-10, in both orders, once per factorisation; the same
+    array twice, or a new array, is factorised again; a singular LHS' raises
+    as LHS did."""
+    from diffopt_amd import SingularException
+    from diffopt_amd.qp import MI355XSolver
+    rng = np.random.default_rng(5)
+    rows = 90
+    L = rng.standard_normal((rows, rows)) + rows ** 0.5 * np.eye(rows)
+    r = rng.standard_normal(rows)
+    s = MI355XSolver()
+    x = s.solve_system(L, r)
+    xt = s.solve_system(L.T, r)
+    assert s.resolves == 1
+    assert np.linalg.norm(x - np.linalg.solve(L, r)) <= 1e-10 * np.linalg.norm(x)
+    assert np.linalg.norm(xt - np.linalg.solve(L.T, r)) <= 1e-10 * np.linalg.norm(xt)
+    L2 = rng.standard_normal((rows, rows)) + rows ** 0.5 * np.eye(rows)
+    xt2 = s.solve_system(L2.T, r)          # a new array: factorised
+    x2 = s.solve_system(L2, r)             # then its parent: reused
+    assert s.resolves == 2
+    assert np.linalg.norm(x2 - np.linalg.solve(L2, r)) <= 1e-10 * np.linalg.norm(x2)
+    assert np.linalg.norm(xt2 - np.linalg.solve(L2.T, r)) <= 1e-10 * np.linalg.norm(xt2)
+    s.solve_system(L2, r)                  # one reuse per factorisation: factorised again
+    assert s.resolves == 2
+    s.solve_system(L2, r)                  # the same array twice: factorised again
+    assert s.resolves == 2
+    S = L.copy()
+    S[:, 3] = 0.0
+    with pytest.raises(SingularException):
+        s.solve_system(S, r)
+    with pytest.raises(SingularException):
+        s.solve_system(S.T, r)
+    assert s.resolves == 3
+    s.close()
