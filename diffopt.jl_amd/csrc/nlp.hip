@@ -1014,7 +1014,13 @@ void nlp_factor(Handle& h) {
   // wasted), so such systems go straight to partial pivoting — unless they
   // take the reduced route (R has no such rows; a problem kept on the full M
   // there is rejected by the no-pivot LU and re-factorised with pivoting).
-  const bool saddle_only = !h.nlp_kkt && h.nlp_ng + h.nlp_nl + h.nlp_nlo + h.nlp_nup == 0;
+  // The QP plug point (dopt_lhs_solve: KKT mode without inertia correction)
+  // gets the saddle-point KKT [Q, GᵀΛ, Aᵀ; G, D(s), 0; A, 0, 0], whose zero
+  // blocks fill with non-zero Schur complements in the natural order: the
+  // no-pivot LU first (config-1 shape 0.46 → 0.34 ms per model), partial
+  // pivoting for what its tests reject.
+  const bool saddle_only = (!h.nlp_kkt && h.nlp_ng + h.nlp_nl + h.nlp_nlo + h.nlp_nup == 0) ||
+                           (h.nlp_kkt && h.nlp_max_corr == 0);
   const int32_t lu_mode = h.lu_mode;
   if (!saddle_only && !reduced_on(h)) h.lu_mode = 0;
   // the singularity check rides on the LU's metadata read-back when the

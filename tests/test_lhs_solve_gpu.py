@@ -82,7 +82,10 @@ def test_cached_solver_handle():
         rhs = rng.standard_normal(L.shape[0])
         for M in (L, L.T):
             got = s.solve_system(M, rhs)
-            np.testing.assert_array_equal(got, solve_system(M, rhs))
+            if M is L:   # factorised here: the fresh-handle result exactly
+                np.testing.assert_array_equal(got, solve_system(M, rhs))
+            else:        # LHS': a transposed solve on L's factors (dopt_lhs_resolve)
+                np.testing.assert_allclose(got, solve_system(M, rhs), rtol=1e-12, atol=1e-14)
             np.testing.assert_allclose(got, np.linalg.solve(M, rhs), rtol=1e-10, atol=1e-12)
         if seed == 22:
             Z = L.copy()
