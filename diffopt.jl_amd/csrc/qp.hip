@@ -815,19 +815,21 @@ static void meta_copy(Handle& h) {
   DOPT_CHECK_HIP(hipEventRecord(h.meta_ev, h.stream));
 }
 
-// The same read-back on the second stream, forked from the handle's stream
-// by a device-scope event: the kernels queued next on the handle's stream (the
-// speculative solves after the LU) do not wait behind the copy.
+// The same read-back on a side stream, forked from the handle's stream by a
+// device-scope event: the kernels queued next on the handle's stream (the
+// assembly tiles after the prepare kernel, the speculative solves after the
+// LU) do not wait behind the copy.
 static void meta_copy_side(Handle& h) {
   ensure_aux(h);
   if (!h.meta_host) {
     DOPT_CHECK_HIP(hipHostMalloc((void**)&h.meta_host, std::max<size_t>(h.batch, 1) * sizeof(QPMeta)));
     DOPT_CHECK_HIP(hipEventCreateWithFlags(&h.meta_ev, hipEventDisableTiming));
   }
+  // (on `crit`: `aux` may still be running the Q symmetry check)
   DOPT_CHECK_HIP(hipEventRecord(h.meta_fork, h.stream));
-  DOPT_CHECK_HIP(hipStreamWaitEvent(h.aux, h.meta_fork, 0));
-  DOPT_CHECK_HIP(hipMemcpyAsync(h.meta_host, h.meta.p, h.batch * sizeof(QPMeta), hipMemcpyDeviceToHost, h.aux));
-  DOPT_CHECK_HIP(hipEventRecord(h.meta_ev, h.aux));
+  DOPT_CHECK_HIP(hipStreamWaitEvent(h.crit, h.meta_fork, 0));
+  DOPT_CHECK_HIP(hipMemcpyAsync(h.meta_host, h.meta.p, h.batch * sizeof(QPMeta), hipMemcpyDeviceToHost, h.crit));
+  DOPT_CHECK_HIP(hipEventRecord(h.meta_ev, h.crit));
 }
 
 // After the assembly: largest padded blocked system (sizes the blocked
@@ -960,7 +962,7 @@ void qp_factor(Handle& h) {
   h.small_ready = false;   // K is overwritten
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
-    prep_assemble(h, nullptr, (int)h.batch, h.lu_mode == 0, [&] { meta_copy(h); });
+    prep_assemble(h, nullptr, (int)h.batch, h.lu_mode == 0, [&] { meta_copy_side(h); });
   }
   meta_sizes(h);
   factor_blocked(h, [] {}, nullptr, nullptr, qp_reasm(h));
@@ -1208,7 +1210,7 @@ void qp_forward_reverse(Handle& h, const double* dl_dz, const double* dQ,
   const FwdTangents T = tangents(h, dQ, dq, dG, dh, dA, db);
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
-    prep_assemble(h, nullptr, (int)h.batch, h.lu_mode == 0, [&] { meta_copy(h); });
+    prep_assemble(h, nullptr, (int)h.batch, h.lu_mode == 0, [&] { meta_copy_side(h); });
   }
   // no-pivot LU: both right-hand sides ride along as a bordering column / row
   // and come out forward-swept (w0, w1, written by the RHS kernels next to
