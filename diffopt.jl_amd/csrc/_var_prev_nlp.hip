@@ -961,9 +961,7 @@ void nlp_configure(Handle& h) {
 // with partial-pivoting fallback), then for the singular problems
 // J_k = M + k·st·D, k = 1 … NLP_MAX_CORR, re-assembled and factorised with
 // partial pivoting until non-singular (NonLinearProgram.jl:356-381).
-static void nlp_factor_tail(Handle& h, bool fast);
-
-void nlp_factor(Handle& h, bool defer) {
+void nlp_factor(Handle& h) {
   if (!h.nset) throw Error(-1, "dopt_nlp_factor: the NLP point has not been set");
   const int B = (int)h.batch;
   DOPT_CHECK_HIP(hipMemsetAsync(h.nlp_shift.p, 0, (size_t)B * sizeof(int32_t), h.stream));
@@ -1032,17 +1030,9 @@ void nlp_factor(Handle& h, bool defer) {
     pivot_check(h, nullptr, B);
     early_check = true;
   };
-  bool fast = false, deferred = false;
+  bool fast = false;
   try {
-    factor_dense(h, [&h](const int32_t* pl, int count) { assemble(h, pl, count); }, &pre,
-                 defer ? &deferred : nullptr);
-    if (deferred) {   // the verdicts are read back by the next call that needs the factors (nlp_finish)
-      h.nlp_fast_ok = early_check && h.lu_mode == 1;
-      h.lu_mode = lu_mode;
-      h.nlp_pending = true;
-      h.nfactored = true;
-      return;
-    }
+    factor_dense(h, [&h](const int32_t* pl, int count) { assemble(h, pl, count); }, &pre);
     // (a rejected problem too tall for the pivoting panel goes to the generic
     // LU, counted in n_generic, not n_pivot: its factor was not seen by the
     // early check — ADVICE r04)
@@ -1053,31 +1043,6 @@ void nlp_factor(Handle& h, bool defer) {
     throw;
   }
   h.lu_mode = lu_mode;
-  nlp_factor_tail(h, fast);
-}
-
-// A deferred nlp_factor's second half (no-op otherwise): the LU's metadata
-// read-back, the rejected problems' fallbacks, the singularity verdicts and
-// the inertia corrections — what dopt_nlp_factor leaves for the next call.
-void nlp_finish(Handle& h) {
-  if (!h.nlp_pending) return;
-  h.nlp_pending = false;
-  factor_dense_finish(h, [&h](const int32_t* pl, int count) { assemble(h, pl, count); });
-  nlp_factor_tail(h, h.nlp_fast_ok && h.n_pivot == 0 && h.n_generic == 0 && h.blocked_npmax > 0 && h.meta_host);
-}
-
-// a set call drops a deferred factorisation (its inputs are replaced)
-void nlp_drop_pending(Handle& h) {
-  if (!h.nlp_pending) return;
-  DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
-  if (h.aux) DOPT_CHECK_HIP(hipStreamSynchronize(h.aux));
-  if (h.crit) DOPT_CHECK_HIP(hipStreamSynchronize(h.crit));
-  h.nlp_pending = false;
-  h.nfactored = false;
-}
-
-static void nlp_factor_tail(Handle& h, bool fast) {
-  const int B = (int)h.batch;
   std::vector<int32_t> all(B);
   for (int b = 0; b < B; ++b) all[b] = b;
   std::vector<int32_t> sing;
@@ -1126,7 +1091,6 @@ static int solve_sel(const Handle& h) { return h.nlp_pivoted ? LU_SEL_ALL : LU_S
 
 void nlp_forward(Handle& h, const double* dp, double* dx, double* ddual) {
   if (!h.nfactored) nlp_factor(h);
-  nlp_finish(h);
   if (h.nlp_kkt) throw Error(-1, "dopt_nlp_forward: the handle holds a KKT matrix (use dopt_nlp_kkt_solve)");
   const int B = (int)h.batch;
   double* rhs = h.rhs.as<double>();
@@ -1151,7 +1115,6 @@ void nlp_forward(Handle& h, const double* dp, double* dx, double* ddual) {
 
 void nlp_reverse(Handle& h, const double* dx, const double* ddual, double* dp) {
   if (!h.nfactored) nlp_factor(h);
-  nlp_finish(h);
   if (h.nlp_kkt) throw Error(-1, "dopt_nlp_reverse: the handle holds a KKT matrix (use dopt_nlp_kkt_solve)");
   const int B = (int)h.batch;
   double* rhs = h.rhs.as<double>() + (size_t)B * h.nmax;
@@ -1198,17 +1161,6 @@ void nlp_forward_reverse(Handle& h, const double* dp, const double* dxs, const d
     DOPT_CHECK_HIP(hipGetLastError());
     if (red) red_rhs(h, 0, 0, rf, t1);   // the pair: rr = rf + blk → t1 + blk
   }
-  // a deferred factorisation finishes here, its verdict read-back overlapped
-  // by the right-hand sides above (they do not read the factors); the
-  // reduction's right-hand sides depend on the corrections (red_use), so a
-  // corrected batch forms them again
-  if (h.nlp_pending) {
-    nlp_finish(h);
-    if (red && std::any_of(h.nlp_corr.begin(), h.nlp_corr.end(), [](int32_t k) { return k != 0; })) {
-      PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
-      red_rhs(h, 0, 0, rf, t1);
-    }
-  }
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     qp_blocked_solve_pair(h, dense_dinv(h), red ? t1 : rf, red ? t1 + blk : rr, red ? t2 : x, red ? t2 + blk : u,
@@ -1233,7 +1185,6 @@ static void solve_multi(Handle& h, int trans, int k, double* rk, double* xk) {
 
 void nlp_jacobian(Handle& h, double* ds) {
   if (!h.nfactored) nlp_factor(h);
-  nlp_finish(h);
   if (h.nlp_kkt) throw Error(-1, "dopt_nlp_jacobian: the handle holds a KKT matrix (use dopt_nlp_kkt_solve)");
   const int B = (int)h.batch, P = h.p;
   if (P == 0) return;
@@ -1266,7 +1217,6 @@ void nlp_jacobian(Handle& h, double* ds) {
 // inertia correction failed give zeros.
 void nlp_kkt_solve(Handle& h, int k, const double* rhs, double* x, bool trans) {
   if (!h.nfactored) nlp_factor(h);
-  nlp_finish(h);
   if (k <= 0) throw Error(-1, "dopt_nlp_kkt_solve: k must be positive");
   const int B = (int)h.batch, R = h.nlp_rows;
   const size_t blk = (size_t)B * h.nmax;

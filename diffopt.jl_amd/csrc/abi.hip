@@ -576,6 +576,7 @@ int dopt_nlp_set_structure(dopt_handle* h, const int32_t* con_kind, const int8_t
                            const int8_t* has_up, int32_t sense) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_set_structure on a non-NLP handle");
+    dopt::nlp_drop_pending(*h);   // a deferred factorisation of the old inputs
     if (sense != 1 && sense != -1) throw Error(-1, "sense must be +1 (MIN_SENSE) or -1 (MAX_SENSE)");
     const int n = h->n, c = h->m;
     if (c && !con_kind) throw Error(-1, "con_kind is required when the model has constraints");
@@ -634,6 +635,7 @@ int dopt_nlp_set(dopt_handle* h, const double* Hxx, const double* Hxp, const dou
                  const double* yu) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_set on a non-NLP handle");
+    dopt::nlp_drop_pending(*h);   // a deferred factorisation of the old inputs
     if (!h->nstruct || h->nlp_kkt) throw Error(-1, "dopt_nlp_set: call dopt_nlp_set_structure first");
     const size_t B = h->batch, n = h->n, c = h->m, P = h->p;
     if (!Hxx || !x) throw Error(-1, "Hxx and x are required");
@@ -656,6 +658,7 @@ int dopt_nlp_set(dopt_handle* h, const double* Hxx, const double* Hxp, const dou
 int dopt_nlp_set_kkt(dopt_handle* h, int32_t rows, int32_t num_w, int32_t num_cons, const double* M) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_set_kkt on a non-NLP handle");
+    dopt::nlp_drop_pending(*h);   // a deferred factorisation of the old inputs
     if (rows <= 0 || num_w < 0 || num_cons < 0 || num_w + num_cons > rows)
       throw Error(-1, "dopt_nlp_set_kkt: bad sizes");
     if (!M) throw Error(-1, "M is required");
@@ -681,7 +684,7 @@ int dopt_nlp_factor(dopt_handle* h) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_factor on a non-NLP handle");
     Timer tm;
-    dopt::nlp_factor(*h);
+    dopt::nlp_factor(*h, true);   // returns with the LU queued: the next call reads the verdicts back
     h->last_time = tm.s();
     return 0;
   });
@@ -830,6 +833,7 @@ int dopt_nlp_get_corrections(dopt_handle* h, int32_t* corr) {
   return guarded(h, [&]() {
     if (!corr) throw Error(-1, "corr is required");
     if (!h->nfactored) throw Error(-1, "dopt_nlp_get_corrections: not factorised");
+    dopt::nlp_finish(*h);
     std::copy(h->nlp_corr.begin(), h->nlp_corr.end(), corr);
     return 0;
   });
@@ -932,6 +936,7 @@ int dopt_get_system_size(dopt_handle* h, int32_t* sizes) {
     if (!sizes) throw Error(-1, "sizes is required");
     if (h->kind == DOPT_KIND_QP || h->kind == DOPT_KIND_NLP) {
       if (h->kind == DOPT_KIND_NLP && !h->nfactored) throw Error(-1, "no NLP factorisation has run");
+      if (h->kind == DOPT_KIND_NLP) dopt::nlp_finish(*h);
       std::vector<dopt::QPMeta> meta(h->batch);
       DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h->meta.p, h->batch * sizeof(dopt::QPMeta),
                                     hipMemcpyDeviceToHost, h->stream));

@@ -225,6 +225,8 @@ struct Handle {
   DevBuf nlp_t1, nlp_t2;           // reduced right-hand sides / solutions (max(2, P) × B × nmax)
   DevBuf nlp_msc;                  // per problem: max |M| of the full M (the reduced route's singularity scale)
   bool nstruct = false, nset = false, nfactored = false;
+  bool nlp_pending = false;        // dopt_nlp_factor returned with the LU queued; nlp_finish reads the verdicts
+  bool nlp_fast_ok = false;        // ... and the pivot check rode on its metadata read-back
 
   // scratch for host-mode tangents / outputs
   DevBuf tin[8], tout[6];
@@ -356,13 +358,20 @@ size_t dinv_stride(int nmax);
 using ReasmFn = std::function<void(const int32_t*, int)>;
 // pre_copy (optional): launched after the no-pivot LU, before its metadata
 // read-back (so the host's copy carries what it writes)
-void factor_dense(Handle& h, const ReasmFn& reasm, const std::function<void()>* pre_copy = nullptr);
+// deferred (optional): with every problem on the no-pivot blocked route the
+// call returns with the LU queued and its metadata read-back in flight
+// (*deferred = true); factor_dense_finish does the rest
+void factor_dense(Handle& h, const ReasmFn& reasm, const std::function<void()>* pre_copy = nullptr,
+                  bool* deferred = nullptr);
+void factor_dense_finish(Handle& h, const ReasmFn& reasm);
 double* dense_dinv(Handle& h);
 void lsqr_slabs(Handle& h, int trans, const double* rhs, double* x);
 void lhs_solve(Handle& h, int k, const double* rhs, double* x, bool iterative, int32_t* info);
 void lhs_resolve(Handle& h, int k, const double* rhs, double* x, bool trans, int32_t* info);
 void nlp_configure(Handle& h);
-void nlp_factor(Handle& h);
+void nlp_factor(Handle& h, bool defer = false);   // defer: dopt_nlp_factor (the rest in nlp_finish)
+void nlp_finish(Handle& h);
+void nlp_drop_pending(Handle& h);
 void nlp_forward(Handle& h, const double* dp, double* dx, double* ddual);
 void nlp_reverse(Handle& h, const double* dx, const double* ddual, double* dp);
 void nlp_forward_reverse(Handle& h, const double* dp, const double* dxs, const double* dds, double* dx,

@@ -891,9 +891,44 @@ static void generic_lu(Handle& h, const std::vector<int32_t>& list) {
 // (optional) is queued right after the no-pivot LU, before the host waits for
 // the rejected list: work that skips rejected problems (the solves of the
 // fused call).
+// After the no-pivot LU and its metadata read-back: the problems it rejected
+// (partial pivoting, re-assembled by `reasm`; those too tall for the pivoting
+// panel join `glist`), then the generic LU of `glist`.
+static void factor_blocked_rest(Handle& h, const ReasmFn& reasm, std::vector<int32_t>& glist, bool nopiv) {
+  auto np_of = [](const QPMeta& mm) { return (mm.nsys + 31) & ~31; };
+  if (nopiv && h.blocked_npmax) {
+    DOPT_CHECK_HIP(hipEventSynchronize(h.meta_ev));
+    bool any = false;
+    std::vector<int32_t> big;   // rejected problems too tall for the pivoting panel
+    for (int64_t b = 0; b < h.batch; ++b) {
+      const QPMeta& mm = h.meta_host[b];
+      if (mm.lu != LU_REJECT) continue;
+      if (np_of(mm) > PIVOT_MAX) big.push_back((int32_t)b);
+      else any = true;
+    }
+    if (any) {
+      PhaseTimer pt(h, DOPT_PHASE_QP_LU_PIVOT);
+      h.n_pivot = pivot_fallback(h, reasm);
+    }
+    if (!big.empty()) {
+      h.plist.ensure(big.size() * sizeof(int32_t));
+      DOPT_CHECK_HIP(hipMemcpyAsync(h.plist.p, big.data(), big.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                                    h.stream));
+      reasm(h.plist.as<int32_t>(), (int)big.size());
+      DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+      glist.insert(glist.end(), big.begin(), big.end());
+    }
+  }
+  h.n_generic = 0;
+  if (!glist.empty()) {   // timed as the fallback phase: qp_lu stays one launch sequence per factorisation
+    PhaseTimer pt(h, DOPT_PHASE_QP_LU_PIVOT);
+    generic_lu(h, glist);
+  }
+}
+
 template <class F>
 static void factor_blocked(Handle& h, F&& spec, double* w0, double* w1, const ReasmFn& reasm,
-                           const std::function<void()>* pre_copy = nullptr) {
+                           const std::function<void()>* pre_copy = nullptr, bool* deferred = nullptr) {
   auto np_of = [](const QPMeta& mm) { return (mm.nsys + 31) & ~31; };
   std::vector<int32_t> glist;   // problems for the generic LU
   if (h.has_generic)
@@ -901,6 +936,7 @@ static void factor_blocked(Handle& h, F&& spec, double* w0, double* w1, const Re
       const QPMeta& mm = h.meta_host[b];
       if (qp_route(mm.iterative, mm.nsys) == ROUTE_GENERIC) glist.push_back((int32_t)b);
     }
+  if (deferred) *deferred = false;
   if (h.lu_mode == 1) {
     {
       PhaseTimer pt(h, DOPT_PHASE_QP_LU);
@@ -910,29 +946,11 @@ static void factor_blocked(Handle& h, F&& spec, double* w0, double* w1, const Re
     if (h.blocked_npmax) meta_copy_side(h);
     spec();
     h.n_pivot = 0;
-    if (h.blocked_npmax) {
-      DOPT_CHECK_HIP(hipEventSynchronize(h.meta_ev));
-      bool any = false;
-      std::vector<int32_t> big;   // rejected problems too tall for the pivoting panel
-      for (int64_t b = 0; b < h.batch; ++b) {
-        const QPMeta& mm = h.meta_host[b];
-        if (mm.lu != LU_REJECT) continue;
-        if (np_of(mm) > PIVOT_MAX) big.push_back((int32_t)b);
-        else any = true;
-      }
-      if (any) {
-        PhaseTimer pt(h, DOPT_PHASE_QP_LU_PIVOT);
-        h.n_pivot = pivot_fallback(h, reasm);
-      }
-      if (!big.empty()) {
-        h.plist.ensure(big.size() * sizeof(int32_t));
-        DOPT_CHECK_HIP(hipMemcpyAsync(h.plist.p, big.data(), big.size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                                      h.stream));
-        reasm(h.plist.as<int32_t>(), (int)big.size());
-        DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
-        glist.insert(glist.end(), big.begin(), big.end());
-      }
+    if (deferred && h.blocked_npmax && glist.empty()) {   // the caller finishes later (factor_dense_finish)
+      *deferred = true;
+      return;
     }
+    factor_blocked_rest(h, reasm, glist, true);
   } else {
     {
       PhaseTimer pt(h, DOPT_PHASE_QP_LU_PIVOT);
@@ -945,11 +963,7 @@ static void factor_blocked(Handle& h, F&& spec, double* w0, double* w1, const Re
         const QPMeta& mm = h.meta_host[b];
         if (qp_route(mm.iterative, mm.nsys) == ROUTE_BLOCKED && np_of(mm) > PIVOT_MAX) glist.push_back((int32_t)b);
       }
-  }
-  h.n_generic = 0;
-  if (!glist.empty()) {   // timed as the fallback phase: qp_lu stays one launch sequence per factorisation
-    PhaseTimer pt(h, DOPT_PHASE_QP_LU_PIVOT);
-    generic_lu(h, glist);
+    factor_blocked_rest(h, reasm, glist, false);
   }
 }
 
@@ -972,10 +986,16 @@ void qp_factor(Handle& h) {
 // The blocked factorisation of a batch already assembled into K / meta by a
 // caller (the NLP back-end), with `reasm` re-assembling the problems the
 // no-pivot LU rejects.  Sizes from h.blocked_npmax; blocked route only.
-void factor_dense(Handle& h, const ReasmFn& reasm, const std::function<void()>* pre_copy) {
+void factor_dense(Handle& h, const ReasmFn& reasm, const std::function<void()>* pre_copy, bool* deferred) {
   h.has_generic = false;
   h.has_lsqr = false;
-  factor_blocked(h, [] {}, nullptr, nullptr, reasm, pre_copy);
+  factor_blocked(h, [] {}, nullptr, nullptr, reasm, pre_copy, deferred);
+}
+// The rest of a deferred factor_dense (no-pivot LU queued, its metadata
+// read-back in flight): the wait, then the rejected problems' fallbacks.
+void factor_dense_finish(Handle& h, const ReasmFn& reasm) {
+  std::vector<int32_t> glist;
+  factor_blocked_rest(h, reasm, glist, true);
 }
 
 double* dense_dinv(Handle& h) { return dinv_of(h); }

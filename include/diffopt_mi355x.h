@@ -310,7 +310,11 @@ int dopt_nlp_set(dopt_handle* h, const double* Hxx, const double* Hxp, const dou
                  const double* yu);
 /* LU of every problem's M with the reference's inertia correction
  * (M + k·1e-6·D, k ≤ 50); a problem whose correction fails gets ∂s = 0, as
- * in the reference (nlp_utilities.jl:436-439). */
+ * in the reference (nlp_utilities.jl:436-439).  Returns once the no-pivot LU
+ * is queued: the verdicts (fallbacks, corrections) are read back by the next
+ * call that needs the factors (forward / reverse / jacobian / kkt_solve /
+ * get_corrections / get_system_size), which then overlaps that wait with
+ * its own right-hand sides. */
 int dopt_nlp_factor(dopt_handle* h);
 /* dp[P] → dx[n], ddual[c + nlow + nup] (constraint duals, then the duals of
  * the primal lower and upper bounds in variable order): ∂s·Δp. */
