@@ -1124,9 +1124,20 @@ static void nlp_factor_tail(Handle& h, bool fast) {
 
 static int solve_sel(const Handle& h) { return h.nlp_pivoted ? LU_SEL_ALL : LU_SEL_NOPIV; }
 
+// a deferred factorisation finishes after the caller's right-hand sides are
+// queued (they do not read the factors); the reduction's sides depend on the
+// corrections, so a corrected batch forms them again (`redo`)
+static void nlp_finish_after_rhs(Handle& h, bool red, const std::function<void()>& redo) {
+  if (!h.nlp_pending) return;
+  nlp_finish(h);
+  if (red && std::any_of(h.nlp_corr.begin(), h.nlp_corr.end(), [](int32_t k) { return k != 0; })) {
+    PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
+    redo();
+  }
+}
+
 void nlp_forward(Handle& h, const double* dp, double* dx, double* ddual) {
   if (!h.nfactored) nlp_factor(h);
-  nlp_finish(h);
   if (h.nlp_kkt) throw Error(-1, "dopt_nlp_forward: the handle holds a KKT matrix (use dopt_nlp_kkt_solve)");
   const int B = (int)h.batch;
   double* rhs = h.rhs.as<double>();
@@ -1138,6 +1149,7 @@ void nlp_forward(Handle& h, const double* dp, double* dx, double* ddual) {
     DOPT_CHECK_HIP(hipGetLastError());
     if (red) red_rhs(h, 0, 1, rhs, red_t1(h, 1));
   }
+  nlp_finish_after_rhs(h, red, [&] { red_rhs(h, 0, 1, rhs, red_t1(h, 1)); });
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     qp_blocked_solve(h, dense_dinv(h), 0, red ? red_t1(h, 1) : rhs, red ? red_t2(h, 1) : x, solve_sel(h));
@@ -1151,7 +1163,6 @@ void nlp_forward(Handle& h, const double* dp, double* dx, double* ddual) {
 
 void nlp_reverse(Handle& h, const double* dx, const double* ddual, double* dp) {
   if (!h.nfactored) nlp_factor(h);
-  nlp_finish(h);
   if (h.nlp_kkt) throw Error(-1, "dopt_nlp_reverse: the handle holds a KKT matrix (use dopt_nlp_kkt_solve)");
   const int B = (int)h.batch;
   double* rhs = h.rhs.as<double>() + (size_t)B * h.nmax;
@@ -1163,6 +1174,7 @@ void nlp_reverse(Handle& h, const double* dx, const double* ddual, double* dp) {
     DOPT_CHECK_HIP(hipGetLastError());
     if (red) red_rhs(h, 1, 1, rhs, red_t1(h, 1));
   }
+  nlp_finish_after_rhs(h, red, [&] { red_rhs(h, 1, 1, rhs, red_t1(h, 1)); });
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     qp_blocked_solve(h, dense_dinv(h), 1, red ? red_t1(h, 1) : rhs, red ? red_t2(h, 1) : u, solve_sel(h));
@@ -1198,17 +1210,7 @@ void nlp_forward_reverse(Handle& h, const double* dp, const double* dxs, const d
     DOPT_CHECK_HIP(hipGetLastError());
     if (red) red_rhs(h, 0, 0, rf, t1);   // the pair: rr = rf + blk → t1 + blk
   }
-  // a deferred factorisation finishes here, its verdict read-back overlapped
-  // by the right-hand sides above (they do not read the factors); the
-  // reduction's right-hand sides depend on the corrections (red_use), so a
-  // corrected batch forms them again
-  if (h.nlp_pending) {
-    nlp_finish(h);
-    if (red && std::any_of(h.nlp_corr.begin(), h.nlp_corr.end(), [](int32_t k) { return k != 0; })) {
-      PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
-      red_rhs(h, 0, 0, rf, t1);
-    }
-  }
+  nlp_finish_after_rhs(h, red, [&] { red_rhs(h, 0, 0, rf, t1); });
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_SOLVE);
     qp_blocked_solve_pair(h, dense_dinv(h), red ? t1 : rf, red ? t1 + blk : rr, red ? t2 : x, red ? t2 + blk : u,
