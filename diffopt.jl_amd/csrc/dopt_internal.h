@@ -64,7 +64,8 @@ struct QPMeta {
   int32_t sym;       // 1: P·K is symmetric (P = diag(1, λ_k, 1): every kept λ finite and non-zero, Q
                      // symmetric) — the no-pivot LU computes only the lower trailing tiles and takes
                      // U12 from L21 (qp_nopiv.hip); 0: every tile
-  int32_t pad;
+  int32_t spec_miss; // NLP, speculative launch (nlp_red_prep_kernel): the problem is not reduced and P-symmetric;
+                     // the meta above is a placeholder of the reduced size and the factorisation is redone
 };
 
 constexpr int ASM_WPP = 16;          // assembly tile workgroups per problem (qp_assemble.hip)
@@ -227,6 +228,11 @@ struct Handle {
   bool nstruct = false, nset = false, nfactored = false;
   bool nlp_pending = false;        // dopt_nlp_factor returned with the LU queued; nlp_finish reads the verdicts
   bool nlp_fast_ok = false;        // ... and the pivot check rode on its metadata read-back
+  // the pending LU was launched on the guess "every problem reduced and
+  // P-symmetric" (no read-back before it); nlp_finish checks meta.spec_miss
+  bool nlp_spec = false;
+  bool nlp_spec_off = false;       // a guess on this handle missed: later factorisations read back first
+  bool nlp_spec_redo = false;      // nlp_finish re-factorised after a miss: the reduced sides are formed again
 
   // scratch for host-mode tangents / outputs
   DevBuf tin[8], tout[6];
@@ -369,7 +375,9 @@ void lsqr_slabs(Handle& h, int trans, const double* rhs, double* x);
 void lhs_solve(Handle& h, int k, const double* rhs, double* x, bool iterative, int32_t* info);
 void lhs_resolve(Handle& h, int k, const double* rhs, double* x, bool trans, int32_t* info);
 void nlp_configure(Handle& h);
-void nlp_factor(Handle& h, bool defer = false);   // defer: dopt_nlp_factor (the rest in nlp_finish)
+// defer: dopt_nlp_factor (the rest in nlp_finish); spec: the LU may be launched
+// before the prepare kernel's metadata is read back (nlp_finish checks it)
+void nlp_factor(Handle& h, bool defer = false, bool spec = true);
 void nlp_finish(Handle& h);
 void nlp_drop_pending(Handle& h);
 void nlp_forward(Handle& h, const double* dp, double* dx, double* ddual);

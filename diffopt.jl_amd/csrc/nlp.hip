@@ -45,11 +45,17 @@ __global__ __launch_bounds__(NT) void nlp_red_prep_kernel(NLPDims d, NLPMap mp, 
                                                           QPMeta* __restrict__ meta, double* __restrict__ kamax,
                                                           const int32_t* __restrict__ hasym,
                                                           const double* __restrict__ hmax,
-                                                          double* __restrict__ mscale) {
+                                                          double* __restrict__ mscale, int spec,
+                                                          int32_t* __restrict__ shift, double* __restrict__ scale,
+                                                          int rb) {
   __shared__ int bad;
   __shared__ double red[NT / 64], mred[NT / 64];
   const size_t b = blockIdx.x;
   const int t = threadIdx.x;
+  // the problem's inertia shift and pivot-check scale rows zeroed here (the
+  // assembly, when it runs, overwrites the scale): no fills before the LU
+  if (t == 0) shift[b] = 0;
+  for (int i = t; i < rb; i += NT) scale[b * rb + i] = 0.0;
   double* delta = R.delta + b * d.num_w;
   int32_t* kx = R.kx + b * d.num_w;
   if (t == 0) bad = 0;
@@ -147,6 +153,11 @@ __global__ __launch_bounds__(NT) void nlp_red_prep_kernel(NLPDims d, NLPMap mp, 
     mm.nsys = ok ? d.n + d.c : d.rows;
     mm.lu = LU_NONE;
     mm.sym = ok && hasym && !hasym[b];   // R symmetric: H exactly symmetric
+    if (spec && !mm.sym) {   // the launch guessed reduced and symmetric: a placeholder of R's size, flagged
+      mm.nsys = d.n + d.c;
+      mm.sym = 1;
+      mm.spec_miss = 1;
+    }
     meta[b] = mm;
   }
 }
@@ -963,12 +974,15 @@ void nlp_configure(Handle& h) {
 // partial pivoting until non-singular (NonLinearProgram.jl:356-381).
 static void nlp_factor_tail(Handle& h, bool fast);
 
-void nlp_factor(Handle& h, bool defer) {
+void nlp_factor(Handle& h, bool defer, bool spec_ok) {
   if (!h.nset) throw Error(-1, "dopt_nlp_factor: the NLP point has not been set");
   const int B = (int)h.batch;
-  DOPT_CHECK_HIP(hipMemsetAsync(h.nlp_shift.p, 0, (size_t)B * sizeof(int32_t), h.stream));
-  DOPT_CHECK_HIP(hipMemsetAsync(h.kamax.p, 0, (size_t)B * sizeof(double), h.stream));
+  if (!reduced_on(h)) {   // (the reduced route's prepare kernel sets both)
+    DOPT_CHECK_HIP(hipMemsetAsync(h.nlp_shift.p, 0, (size_t)B * sizeof(int32_t), h.stream));
+    DOPT_CHECK_HIP(hipMemsetAsync(h.kamax.p, 0, (size_t)B * sizeof(double), h.stream));
+  }
   h.nlp_left = false;
+  bool spec = false;
   {
     PhaseTimer pt(h, DOPT_PHASE_QP_ASSEMBLE);
     if (reduced_on(h)) {
@@ -988,24 +1002,36 @@ void nlp_factor(Handle& h, bool defer) {
         DOPT_CHECK_HIP(hipGetLastError());
         hasym = qsy_flag(h);
       }
+      // the left-looking route needs no assembly, so it can be launched on the
+      // guess that every problem is reduced and symmetric (the usual case)
+      // without waiting for the metadata: a problem that is not gets a
+      // placeholder of R's size and spec_miss, and nlp_finish redoes the
+      // factorisation from the read-back (config 6: ≈ 45 µs host turnaround
+      // before the LU)
+      spec = spec_ok && hasym && !h.nlp_spec_off;
       hipLaunchKernelGGL(nlp_red_prep_kernel, dim3(B), dim3(NT), 0, h.stream, dims(h), map_of(h), inputs(h),
                          red_of(h), h.meta.as<QPMeta>(), h.kamax.as<double>(), hasym,
-                         hasym ? (const double*)qsy_max(h) : nullptr, nlp_mscale(h));
+                         hasym ? (const double*)qsy_max(h) : nullptr, nlp_mscale(h), spec ? 1 : 0,
+                         h.nlp_shift.as<int32_t>(), h.nlp_scale.as<double>(), row_blocks(h));
       DOPT_CHECK_HIP(hipGetLastError());
-      // the factorised sizes (n + c, or the rows of M for a problem kept on
-      // the full route) size the LU and solve launches; every problem reduced
-      // and symmetric: the left-looking route
-      std::vector<QPMeta> mh(B);
-      DOPT_CHECK_HIP(hipMemcpyAsync(mh.data(), h.meta.p, B * sizeof(QPMeta), hipMemcpyDeviceToHost, h.stream));
-      DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
-      int npmax = 0;
-      for (const QPMeta& mm : mh) npmax = std::max(npmax, (mm.nsys + 31) & ~31);
-      h.blocked_npmax = npmax;
-      h.nlp_left = hasym && std::all_of(mh.begin(), mh.end(), [](const QPMeta& mm) { return mm.sym != 0; });
+      if (spec) {
+        const NLPDims d = dims(h);
+        h.blocked_npmax = (d.n + d.c + 31) & ~31;
+        h.nlp_left = true;
+      } else {
+        // the factorised sizes (n + c, or the rows of M for a problem kept on
+        // the full route) size the LU and solve launches; every problem
+        // reduced and symmetric: the left-looking route
+        std::vector<QPMeta> mh(B);
+        DOPT_CHECK_HIP(hipMemcpyAsync(mh.data(), h.meta.p, B * sizeof(QPMeta), hipMemcpyDeviceToHost, h.stream));
+        DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
+        int npmax = 0;
+        for (const QPMeta& mm : mh) npmax = std::max(npmax, (mm.nsys + 31) & ~31);
+        h.blocked_npmax = npmax;
+        h.nlp_left = hasym && std::all_of(mh.begin(), mh.end(), [](const QPMeta& mm) { return mm.sym != 0; });
+      }
     }
-    if (h.nlp_left)   // no assembly: the pivot check's scale is nlp_mscale alone
-      DOPT_CHECK_HIP(hipMemsetAsync(h.nlp_scale.p, 0, h.nlp_scale.bytes, h.stream));
-    else
+    if (!h.nlp_left)   // (none: the pivot check's scale is nlp_mscale alone, the zeroed rows)
       assemble(h, nullptr, B);
   }
   if (!reduced_on(h)) h.blocked_npmax = h.nmax;
@@ -1034,13 +1060,18 @@ void nlp_factor(Handle& h, bool defer) {
   };
   bool fast = false, deferred = false;
   try {
+    // (a speculative launch always defers: the guess is checked before any
+    // fallback reads the metadata)
     factor_dense(h, [&h](const int32_t* pl, int count) { assemble(h, pl, count); }, &pre,
-                 defer ? &deferred : nullptr);
+                 defer || spec ? &deferred : nullptr);
+    if (spec && !deferred) throw Error(-1, "dopt_nlp_factor: internal: speculative LU not deferred");
     if (deferred) {   // the verdicts are read back by the next call that needs the factors (nlp_finish)
       h.nlp_fast_ok = early_check && h.lu_mode == 1;
       h.lu_mode = lu_mode;
       h.nlp_pending = true;
+      h.nlp_spec = spec;
       h.nfactored = true;
+      if (!defer) nlp_finish(h);
       return;
     }
     // (a rejected problem too tall for the pivoting panel goes to the generic
@@ -1060,8 +1091,21 @@ void nlp_factor(Handle& h, bool defer) {
 // read-back, the rejected problems' fallbacks, the singularity verdicts and
 // the inertia corrections — what dopt_nlp_factor leaves for the next call.
 void nlp_finish(Handle& h) {
+  h.nlp_spec_redo = false;
   if (!h.nlp_pending) return;
   h.nlp_pending = false;
+  if (h.nlp_spec) {   // the guess (every problem reduced and symmetric) against the prepare kernel's verdicts
+    h.nlp_spec = false;
+    DOPT_CHECK_HIP(hipEventSynchronize(h.meta_ev));
+    bool miss = false;
+    for (int64_t b = 0; b < h.batch; ++b) miss |= h.meta_host[b].spec_miss != 0;
+    if (miss) {   // redone from the read-back (stream order: after the speculative LU)
+      h.nlp_spec_off = true;
+      nlp_factor(h, false, false);
+      h.nlp_spec_redo = true;
+      return;
+    }
+  }
   factor_dense_finish(h, [&h](const int32_t* pl, int count) { assemble(h, pl, count); });
   nlp_factor_tail(h, h.nlp_fast_ok && h.n_pivot == 0 && h.n_generic == 0 && h.blocked_npmax > 0 && h.meta_host);
 }
@@ -1073,6 +1117,7 @@ void nlp_drop_pending(Handle& h) {
   if (h.aux) DOPT_CHECK_HIP(hipStreamSynchronize(h.aux));
   if (h.crit) DOPT_CHECK_HIP(hipStreamSynchronize(h.crit));
   h.nlp_pending = false;
+  h.nlp_spec = false;
   h.nfactored = false;
 }
 
@@ -1126,11 +1171,13 @@ static int solve_sel(const Handle& h) { return h.nlp_pivoted ? LU_SEL_ALL : LU_S
 
 // a deferred factorisation finishes after the caller's right-hand sides are
 // queued (they do not read the factors); the reduction's sides depend on the
-// corrections, so a corrected batch forms them again (`redo`)
+// corrections and on the route, so a corrected batch, or one re-factorised
+// after a missed guess, forms them again (`redo`)
 static void nlp_finish_after_rhs(Handle& h, bool red, const std::function<void()>& redo) {
   if (!h.nlp_pending) return;
   nlp_finish(h);
-  if (red && std::any_of(h.nlp_corr.begin(), h.nlp_corr.end(), [](int32_t k) { return k != 0; })) {
+  if (red && (h.nlp_spec_redo ||
+              std::any_of(h.nlp_corr.begin(), h.nlp_corr.end(), [](int32_t k) { return k != 0; }))) {
     PhaseTimer pt(h, DOPT_PHASE_QP_RHS);
     redo();
   }

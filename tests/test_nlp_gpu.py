@@ -441,3 +441,51 @@ def test_forward_reverse_equals_separate_calls(case, lu_mode, monkeypatch):
         ox, od = onlp.forward(ds, L, dp[b])
         assert relfro(np.concatenate([gx[b], gd[b]]), np.concatenate([ox, od])) <= RTOL
         assert relfro(gp[b], onlp.reverse(ds, L, zx[b], zd[b])) <= RTOL
+
+
+# ---- the speculative LU launch (no metadata read-back before the LU) --------
+@pytest.mark.parametrize("call", ["forward_reverse", "forward", "reverse", "jacobian"])
+def test_speculative_launch_miss(call):
+    """dopt_nlp_factor launches the LU on the guess that every problem is
+    reduced and symmetric; a batch breaking it (problem 1 leaves the reduced
+    route) is re-factorised from the read-back by the next call, whose right-
+    hand sides were already queued — on a handle whose previous factorisation
+    guessed right, and again on the same handle (guessing now off).  Each call
+    matches a fresh engine's and the oracle."""
+    from diffopt_amd.synthetic import nlp_numpy
+    B, n, c, P = 4, 30, 18, 4
+    st, good, dp, dx, dd = nlp_numpy(B, n, c, P, 7400)
+    bad = {k: v.copy() for k, v in good.items()}
+    j = int(np.flatnonzero(st["has_low"])[0])
+    bad["xl"][1, j], bad["yl"][1, j] = bad["x"][1, j], 0.0
+    e = engine(st, good, B)
+    assert (e.system_size() == n + c).all()
+
+    def run(eng):
+        if call == "forward_reverse":
+            return eng.forward_reverse(dp, dx, dd)
+        if call == "forward":
+            return eng.forward(dp)
+        if call == "reverse":
+            return (eng.reverse(dx, dd),)
+        return (eng.jacobian(),)
+
+    for _ in range(2):
+        e.set(*[bad[k] for k in KEYS])
+        e.factor()
+        got = run(e)
+        assert e.system_size()[1] == e.layout()["rows"] and e.system_size()[0] == n + c
+        ref = engine(st, bad, B)
+        ref.system_size()
+        want = run(ref)
+        for g, w in zip(got, want):
+            np.testing.assert_allclose(g, w, rtol=0, atol=1e-12 * max(1.0, np.abs(w).max()))
+        ref.close()
+    ds, L, *_ = oracle_problem(st, bad, 1)
+    if call in ("forward", "forward_reverse"):
+        ox, od = onlp.forward(ds, L, dp[1])
+        assert relfro(np.concatenate([got[0][1], got[1][1]]), np.concatenate([ox, od])) <= RTOL
+    e.set(*[good[k] for k in KEYS])
+    e.factor()
+    check_against_oracle(e, st, good, dp, dx, dd, range(B))
+    e.close()
