@@ -1,5 +1,6 @@
 // C-ABI entry points (include/diffopt_mi355x.h).  Every function catches the
 // engine's exceptions and maps them onto the header's return-code contract.
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -170,7 +171,8 @@ int dopt_destroy(dopt_handle* h) {
   DevBuf* bufs[] = {&h->dinv, &h->plist, &h->lsqr_ws, &h->binv, &h->fwdw, &h->K, &h->ipiv, &h->s, &h->kidx, &h->meta, &h->rhs,
                     &h->x, &h->cone_dev, &h->vp, &h->dpi, &h->cwork, &h->cinfo, &h->cnorm, &h->csplit, &h->krhs, &h->kx,
                     &h->kfull, &h->kamax, &h->nlp_map, &h->nlp_shift, &h->nlp_scale, &h->kls, &h->gk, &h->glist,
-                    &h->mws, &h->qsy, &h->psd_eig, &h->psd_app, &h->ukp, &h->nlp_rd, &h->nlp_ri, &h->nlp_t1, &h->nlp_t2};
+                    &h->mws, &h->qsy, &h->psd_eig, &h->psd_app, &h->ukp, &h->nlp_rd, &h->nlp_ri, &h->nlp_t1, &h->nlp_t2,
+                    &h->nlp_msc, &h->pack, &h->tpack};
   for (auto* b : bufs) b->release();
   for (auto& b : h->own_nin) b.release();
   for (auto& b : h->own_in) b.release();
@@ -187,6 +189,7 @@ int dopt_destroy(dopt_handle* h) {
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->meta_host) (void)hipHostFree(h->meta_host);
   if (h->pin) (void)hipHostFree(h->pin);
+  if (h->pin_out) (void)hipHostFree(h->pin_out);
   if (h->meta_ev) (void)hipEventDestroy(h->meta_ev);
   if (h->meta_fork) (void)hipEventDestroy(h->meta_fork);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
@@ -256,12 +259,14 @@ static const int64_t* stage_in_i64(Handle& h, DevBuf& buf, const int64_t* src, s
 // device pointers returned in order (null stays null).  Larger inputs keep
 // one copy per array (a host memcpy of gigabytes costs more than it saves).
 constexpr size_t PACK_MAX = (size_t)8 << 20;
+constexpr size_t LHS_PACK_MAX = (size_t)1 << 20;   // dopt_lhs_solve: M and the sides (the host memcpy pays below)
 struct PackIn {
   const void* src;
   size_t bytes;
 };
-static bool pack_in(Handle& h, const PackIn* in, int k, const void** out) {
+static bool pack_in(Handle& h, const PackIn* in, int k, const void** out, DevBuf* dst = nullptr) {
   if (h.mem == DOPT_MEM_DEVICE) return false;
+  DevBuf& D = dst ? *dst : h.pack;
   size_t tot = 0;
   for (int i = 0; i < k; ++i) tot += (in[i].bytes + 15) & ~(size_t)15;
   if (tot == 0 || tot > PACK_MAX) return false;
@@ -274,7 +279,7 @@ static bool pack_in(Handle& h, const PackIn* in, int k, const void** out) {
   }
   // the previous call's copy out of the pinned buffer is complete: every
   // host-mode entry point synchronises before it returns
-  h.pack.ensure(tot);
+  D.ensure(tot);
   size_t off = 0;
   for (int i = 0; i < k; ++i) {
     if (!in[i].src) {
@@ -282,11 +287,29 @@ static bool pack_in(Handle& h, const PackIn* in, int k, const void** out) {
       continue;
     }
     std::memcpy(static_cast<char*>(h.pin) + off, in[i].src, in[i].bytes);
-    out[i] = static_cast<const char*>(h.pack.p) + off;
+    out[i] = static_cast<const char*>(D.p) + off;
     off += (in[i].bytes + 15) & ~(size_t)15;
   }
-  DOPT_CHECK_HIP(hipMemcpyAsync(h.pack.p, h.pin, off, hipMemcpyHostToDevice, h.stream));
+  DOPT_CHECK_HIP(hipMemcpyAsync(D.p, h.pin, off, hipMemcpyHostToDevice, h.stream));
   return true;
+}
+
+// Pinned staging pays from a handle's third small call on (its hipHostMalloc
+// costs more than the pageable copies of a call or two save: a handle per
+// model — LHS then LHS' — stays pageable).
+static bool pin_ok(Handle& h) { return h.mem != DOPT_MEM_DEVICE && (h.pin_out || ++h.io_calls >= 3); }
+
+// The small path's pinned read-back buffer (the previous call's copy into it
+// is complete: every entry point synchronises before it returns).
+static char* pin_out(Handle& h, size_t bytes) {
+  if (h.pin_out_bytes < bytes) {
+    if (h.pin_out) DOPT_CHECK_HIP(hipHostFree(h.pin_out));
+    h.pin_out = nullptr;
+    h.pin_out_bytes = 0;
+    DOPT_CHECK_HIP(hipHostMalloc(&h.pin_out, bytes, hipHostMallocDefault));
+    h.pin_out_bytes = bytes;
+  }
+  return static_cast<char*>(h.pin_out);
 }
 
 int dopt_qp_set_csc(dopt_handle* h,
@@ -450,15 +473,44 @@ int dopt_qp_reverse(dopt_handle* h, const double* dl_dz, double* out) {
     if (!dl_dz || !out) throw Error(-1, "dl_dz and out are required");
     Timer tm;
     const size_t B = h->batch, n = h->n, L = h->n + h->m + h->p;
-    const double* d = stage_in(*h, h->tin[0], dl_dz, B * n);
-    double* o = out_ptr(*h, h->tout[0], out, B * L);
+    const bool host = h->mem != DOPT_MEM_DEVICE;
+    const double* d = nullptr;
     // a model not yet factorised, batch of a few: the one-launch small path
-    // (qp_small.hip); anything it cannot take runs the batched route below
-    if (!h->factored && dopt::qp_small_eligible(*h) &&
-        dopt::qp_small_reverse(*h, d, o, [&] { copy_out(*h, out, o, B * L); })) {
-      h->last_time = tm.s();
-      return 0;
+    // (qp_small.hip), its traffic one copy each way in host mode (the seed
+    // through the pinned pack; the outputs with the per-problem flags after
+    // them); anything it cannot take runs the batched route below
+    if (!h->factored && dopt::qp_small_eligible(*h)) {
+      const size_t ob = B * L * sizeof(double), fb = B * sizeof(int32_t);
+      const bool pinned = pin_ok(*h);
+      std::vector<char> page;   // (a handle's first call: pageable)
+      if (host) {
+        const PackIn pi[1] = {{dl_dz, B * n * sizeof(double)}};
+        const void* pd[1];
+        d = pinned && pack_in(*h, pi, 1, pd, &h->tpack) ? static_cast<const double*>(pd[0])
+                                                        : stage_in(*h, h->tin[0], dl_dz, B * n);
+        h->tout[0].ensure(ob + fb);
+      } else {
+        d = dl_dz;
+        h->csc_err.ensure(fb);
+      }
+      double* o = host ? h->tout[0].as<double>() : out;
+      int32_t* flags = host ? reinterpret_cast<int32_t*>(h->tout[0].as<char>() + ob) : h->csc_err.as<int32_t>();
+      dopt::qp_small_reverse(*h, d, o, flags);
+      if (!pinned) page.resize(host ? ob + fb : fb);
+      char* pin = pinned ? pin_out(*h, host ? ob + fb : fb) : page.data();
+      DOPT_CHECK_HIP(hipMemcpyAsync(pin, host ? static_cast<const void*>(o) : static_cast<const void*>(flags),
+                                    host ? ob + fb : fb, hipMemcpyDeviceToHost, h->stream));
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+      const int32_t* hf = reinterpret_cast<const int32_t*>(pin + (host ? ob : 0));
+      h->small_ready = std::all_of(hf, hf + B, [](int32_t f) { return f == 0; });
+      if (h->small_ready) {
+        if (host) std::memcpy(out, pin, ob);
+        h->last_time = tm.s();
+        return 0;
+      }
     }
+    if (!d) d = stage_in(*h, h->tin[0], dl_dz, B * n);
+    double* o = out_ptr(*h, h->tout[0], out, B * L);
     dopt::qp_reverse(*h, d, o);
     copy_out(*h, out, o, B * L);
     const int rc = first_info(*h);
@@ -474,6 +526,27 @@ int dopt_qp_forward(dopt_handle* h, const double* dQ, const double* dq, const do
     if (!out) throw Error(-1, "out is required");
     Timer tm;
     const size_t B = h->batch, n = h->n, m = h->m, p = h->p, L = n + m + p;
+    if (!h->factored && h->small_ready && pin_ok(*h)) {   // the small path's factors (dopt_qp_reverse): one copy each way
+      const PackIn pi[6] = {{dQ, B * n * n * sizeof(double)}, {dq, B * n * sizeof(double)},
+                            {m ? dG : nullptr, B * m * n * sizeof(double)}, {m ? dh : nullptr, B * m * sizeof(double)},
+                            {p ? dA : nullptr, B * p * n * sizeof(double)}, {p ? db : nullptr, B * p * sizeof(double)}};
+      const void* pd[6];
+      if (pack_in(*h, pi, 6, pd, &h->tpack)) {
+        const size_t ob = B * L * sizeof(double);
+        h->tout[1].ensure(ob);
+        double* o = h->tout[1].as<double>();
+        dopt::qp_small_forward(*h, dopt::FwdTangents{static_cast<const double*>(pd[0]), static_cast<const double*>(pd[1]),
+                                                     static_cast<const double*>(pd[2]), static_cast<const double*>(pd[3]),
+                                                     static_cast<const double*>(pd[4]), static_cast<const double*>(pd[5])},
+                               o);
+        char* pin = pin_out(*h, ob);
+        DOPT_CHECK_HIP(hipMemcpyAsync(pin, o, ob, hipMemcpyDeviceToHost, h->stream));
+        DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+        std::memcpy(out, pin, ob);
+        h->last_time = tm.s();
+        return 0;
+      }
+    }
     const double* a = stage_in(*h, h->tin[1], dQ, B * n * n);
     const double* b = stage_in(*h, h->tin[2], dq, B * n);
     const double* c = stage_in(*h, h->tin[3], dG, B * m * n);
@@ -655,26 +728,33 @@ int dopt_nlp_set(dopt_handle* h, const double* Hxx, const double* Hxp, const dou
   });
 }
 
+// dopt_nlp_set_kkt's body; `Mdev`: M already on the device (dopt_lhs_solve's
+// packed copy), else M is staged as any input
+static void set_kkt(Handle& h, int32_t rows, int32_t num_w, int32_t num_cons, const double* M,
+                    const double* Mdev) {
+  if (h.kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_set_kkt on a non-NLP handle");
+  dopt::nlp_drop_pending(h);   // a deferred factorisation of the old inputs
+  if (rows <= 0 || num_w < 0 || num_cons < 0 || num_w + num_cons > rows)
+    throw Error(-1, "dopt_nlp_set_kkt: bad sizes");
+  if (!M) throw Error(-1, "M is required");
+  h.nlp_kkt = true;
+  h.lhs_info.clear();   // (dopt_lhs_resolve: only after a dopt_lhs_solve of this matrix)
+  h.nlp_rows = rows;
+  h.nlp_num_w = num_w;
+  h.nlp_ncons = num_cons;
+  h.nlp_ng = h.nlp_nl = h.nlp_nlo = h.nlp_nup = h.nlp_nlowp = h.nlp_nupp = 0;
+  dopt::nlp_configure(h);
+  h.nlp_map.ensure(4 * sizeof(int32_t));
+  for (auto& p : h.nin) p = nullptr;
+  h.nin[0] = Mdev ? Mdev : stage_in(h, h.own_nin[0], M, (size_t)h.batch * rows * rows);
+  h.nstruct = true;
+  h.nset = true;
+  h.nfactored = false;
+}
+
 int dopt_nlp_set_kkt(dopt_handle* h, int32_t rows, int32_t num_w, int32_t num_cons, const double* M) {
   return guarded(h, [&]() {
-    if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_set_kkt on a non-NLP handle");
-    dopt::nlp_drop_pending(*h);   // a deferred factorisation of the old inputs
-    if (rows <= 0 || num_w < 0 || num_cons < 0 || num_w + num_cons > rows)
-      throw Error(-1, "dopt_nlp_set_kkt: bad sizes");
-    if (!M) throw Error(-1, "M is required");
-    h->nlp_kkt = true;
-    h->lhs_info.clear();   // (dopt_lhs_resolve: only after a dopt_lhs_solve of this matrix)
-    h->nlp_rows = rows;
-    h->nlp_num_w = num_w;
-    h->nlp_ncons = num_cons;
-    h->nlp_ng = h->nlp_nl = h->nlp_nlo = h->nlp_nup = h->nlp_nlowp = h->nlp_nupp = 0;
-    dopt::nlp_configure(*h);
-    h->nlp_map.ensure(4 * sizeof(int32_t));
-    for (auto& p : h->nin) p = nullptr;
-    h->nin[0] = stage_in(*h, h->own_nin[0], M, (size_t)h->batch * rows * rows);
-    h->nstruct = true;
-    h->nset = true;
-    h->nfactored = false;
+    set_kkt(*h, rows, num_w, num_cons, M, nullptr);
     DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
     return 0;
   });
@@ -783,21 +863,32 @@ int dopt_nlp_kkt_solve(dopt_handle* h, int32_t k, const double* rhs, double* x) 
 int dopt_lhs_solve(dopt_handle* h, int32_t rows, const double* M, int32_t k, const double* rhs, double* x,
                    int32_t iterative) {
   if (!h) return -1;
-  {
-    const int rc = dopt_nlp_set_kkt(h, rows, rows, 0, M);
-    if (rc) return rc;
-  }
   std::vector<int32_t> info(h->batch, 0);
   const int rc = guarded(h, [&]() {
+    Timer tm;
+    // a small host-mode system (the Julia plug point's one model): M and the
+    // right-hand sides in one pinned copy, the solution back by one
+    const size_t mcnt = rows > 0 ? (size_t)h->batch * rows * rows : 0;
+    const size_t cnt = rows > 0 && k > 0 ? (size_t)k * h->batch * rows : 0;
+    const PackIn pi[2] = {{M, mcnt * sizeof(double)}, {rhs, cnt * sizeof(double)}};
+    const void* pd[2] = {nullptr, nullptr};
+    const bool small = (mcnt + cnt) * sizeof(double) <= LHS_PACK_MAX && M && rhs && x && cnt &&
+                       h->kind == DOPT_KIND_NLP && pin_ok(*h) && pack_in(*h, pi, 2, pd, &h->tpack);
+    set_kkt(*h, rows, rows, 0, M, small ? static_cast<const double*>(pd[0]) : nullptr);
     if (k <= 0) throw Error(-1, "k must be positive");
     if (!rhs || !x) throw Error(-1, "rhs and x are required");
-    Timer tm;
-    const size_t cnt = (size_t)k * h->batch * rows;
-    const double* r = stage_in(*h, h->tin[0], rhs, cnt);
+    const double* r = small ? static_cast<const double*>(pd[1]) : stage_in(*h, h->tin[0], rhs, cnt);
     double* o = out_ptr(*h, h->tout[0], x, cnt);
     dopt::lhs_solve(*h, k, r, o, iterative != 0, info.data());
-    copy_out(*h, x, o, cnt);
-    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    if (small) {
+      char* pin = pin_out(*h, cnt * sizeof(double));
+      DOPT_CHECK_HIP(hipMemcpyAsync(pin, o, cnt * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+      std::memcpy(x, pin, cnt * sizeof(double));
+    } else {
+      copy_out(*h, x, o, cnt);
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    }
     h->last_time = tm.s();
     return 0;
   });
@@ -815,11 +906,21 @@ int dopt_lhs_resolve(dopt_handle* h, int32_t k, const double* rhs, double* x, in
     if (!rhs || !x) throw Error(-1, "rhs and x are required");
     Timer tm;
     const size_t cnt = (size_t)k * h->batch * h->nlp_rows;
-    const double* r = stage_in(*h, h->tin[0], rhs, cnt);
+    const PackIn pi[1] = {{rhs, cnt * sizeof(double)}};
+    const void* pd[1] = {nullptr};
+    const bool small = cnt * sizeof(double) <= LHS_PACK_MAX && pin_ok(*h) && pack_in(*h, pi, 1, pd, &h->tpack);
+    const double* r = small ? static_cast<const double*>(pd[0]) : stage_in(*h, h->tin[0], rhs, cnt);
     double* o = out_ptr(*h, h->tout[0], x, cnt);
     dopt::lhs_resolve(*h, k, r, o, trans != 0, info.data());
-    copy_out(*h, x, o, cnt);
-    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    if (small) {   // (as dopt_lhs_solve: one pinned copy each way)
+      char* pin = pin_out(*h, cnt * sizeof(double));
+      DOPT_CHECK_HIP(hipMemcpyAsync(pin, o, cnt * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+      std::memcpy(x, pin, cnt * sizeof(double));
+    } else {
+      copy_out(*h, x, o, cnt);
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+    }
     h->last_time = tm.s();
     return 0;
   });

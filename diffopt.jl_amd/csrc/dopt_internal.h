@@ -139,6 +139,13 @@ struct Handle {
   void* pin = nullptr;
   size_t pin_bytes = 0;
   DevBuf pack;
+  // the small path's per-call traffic (abi.hip): the tangents packed like the
+  // inputs (into tpack: pack stays the inputs' home), the outputs and the
+  // per-problem flags read back by ONE copy into pin_out
+  DevBuf tpack;
+  void* pin_out = nullptr;
+  size_t pin_out_bytes = 0;
+  int io_calls = 0;          // small-path calls so far (abi.hip pin_ok: pinned from the third on)
   DevBuf csc_in[9], csc_in_val[3], csc_err;   // host-mode copies of CSC colptr / rowval / nzval
   int32_t nmax = 0, ld = 0;  // max system size, K row stride (doubles)
   DevBuf K, ipiv, s, kidx, meta, rhs, x;
@@ -319,7 +326,7 @@ struct PhaseTimer {
 void qp_factor(Handle& h);
 // small-problem path (qp_small.hip)
 bool qp_small_eligible(const Handle& h);
-bool qp_small_reverse(Handle& h, const double* dl_dz, double* out, const std::function<void()>& copy);
+void qp_small_reverse(Handle& h, const double* dl_dz, double* out, int32_t* flags);
 void qp_small_forward(Handle& h, const FwdTangents& T, double* out);
 void qp_reverse(Handle& h, const double* dl_dz, double* out);
 void csc_to_dense(Handle& h, const int64_t* colptr, const int64_t* rowval, const double* nzval,

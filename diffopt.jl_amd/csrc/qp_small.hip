@@ -21,7 +21,7 @@
 //                         eliminated rows x_λi = r_i/s_i (:357-446)
 //
 // A problem the path cannot take (the LSQR branch Q == 0, a reduced system
-// larger than SM_MAX, a rejected or singular pivot) raises the batch's flag and
+// larger than SM_MAX, a rejected or singular pivot) raises its problem's flag and
 // the call runs the batched route instead, which also reports singularities in
 // the reference's coordinates.  Same semantics, different rounding: the
 // outputs agree with the batched route and the oracle to the parity bar.
@@ -459,6 +459,7 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
   const double* Gb = P.G + (size_t)b * m * n;
   const double* Ab = P.A + (size_t)b * p * n;
   const SmSrc X{Qb, Gb, Ab};
+  if (t == 0) flag[b] = 0;   // (1 below when the problem leaves the path)
   SM_STAMP(0);
   if constexpr (STG) {
 #pragma unroll 8
@@ -477,7 +478,7 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
 #ifdef SM_DEBUG
     if (t == 0) printf("small: prepare rejects (nk %d)\n", nk);
 #endif
-    if (t == 0) atomicOr(flag, 1);
+    if (t == 0) flag[b] = 1;
     return;
   }
   const int N = n + nk + p;
@@ -506,10 +507,10 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
   if (bad) printf("small: t %d rejects (N %d bound %g piv0 %g)\n", t, N, bound, L.S[0]);
 #endif
 #ifdef SM_DUMP   // (tools/probe/small_probe.hip: the factors kept whatever the tests say)
-  if (__syncthreads_or(bad) && t == 0) atomicOr(flag, 1);
+  if (__syncthreads_or(bad) && t == 0) flag[b] = 1;
 #else
   if (__syncthreads_or(bad)) {   // workgroup-uniform
-    if (t == 0) atomicOr(flag, 1);
+    if (t == 0) flag[b] = 1;
     return;
   }
 #endif
@@ -697,24 +698,15 @@ bool qp_small_eligible(const Handle& h) {
          h.n + h.p < SM_MAX && h.set;
 }
 
-// Reverse through the small path: true when every problem took it (the
-// outputs are queued on the handle's stream; `copy` — the host copy-out — is
-// queued before the flag's read-back so one synchronisation serves both).
-bool qp_small_reverse(Handle& h, const double* dl_dz, double* out, const std::function<void()>& copy) {
+// Reverse through the small path, queued on the handle's stream: the outputs,
+// and flags[b] = 1 for each problem it could not take (0 otherwise) — the
+// caller reads them back (abi.hip: with the outputs, one copy).
+void qp_small_reverse(Handle& h, const double* dl_dz, double* out, int32_t* flags) {
   h.small_ready = false;
-  h.csc_err.ensure(sizeof(int));
-  int32_t* flag = h.csc_err.as<int32_t>();
-  DOPT_CHECK_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), h.stream));
   hipLaunchKernelGGL(qp_small_rev_kernel, dim3((unsigned)h.batch), dim3(SM_T), 0, h.stream, small_inputs(h), dl_dz,
                      h.K.as<double>(), h.ld, h.nmax, h.s.as<double>(), h.kidx.as<int32_t>(),
-                     h.kidx.as<int32_t>() + (size_t)h.batch * h.m, h.meta.as<QPMeta>(), out, flag);
+                     h.kidx.as<int32_t>() + (size_t)h.batch * h.m, h.meta.as<QPMeta>(), out, flags);
   DOPT_CHECK_HIP(hipGetLastError());
-  copy();
-  int32_t hf = 0;
-  DOPT_CHECK_HIP(hipMemcpyAsync(&hf, flag, sizeof(int32_t), hipMemcpyDeviceToHost, h.stream));
-  DOPT_CHECK_HIP(hipStreamSynchronize(h.stream));
-  h.small_ready = hf == 0;
-  return h.small_ready;
 }
 
 // Forward from the small path's factors (h.small_ready); the outputs are

@@ -71,7 +71,10 @@ def test_cached_solver_handle():
     (the reference calls solve_system with LHS, then LHS', per
     model, and loops models): the reverse / forward pair and a loop over
     models of two sizes on one solver give exactly the fresh-handle results,
-    and a singular system in between does not poison the cached handle."""
+    and a singular system in between does not poison the cached handle.  The
+    cached handle's later calls stage through one pinned copy each way (its
+    first, like every fresh handle's, through pageable copies): the
+    comparisons against fresh handles check the two against each other."""
     from diffopt_amd import _lib
     from diffopt_amd.qp import MI355XSolver, solve_system
     s = MI355XSolver()
@@ -94,3 +97,4 @@ def test_cached_solver_handle():
                 s.solve_system(Z, rhs)
     assert s._key == (1, L.shape[0])
     s.close()
+

@@ -168,3 +168,33 @@ def test_small_path_shapes(QPBatch, n, m, p, phi):
             dA=d["dA"][b] if p else None, db=d["db"][b] if p else None))
         assert relfro(rev[b], ref_r) <= RTOL
         assert relfro(fwd[b], ref_f) <= RTOL
+
+
+def test_small_path_reused_handle(QPBatch):
+    """One handle, successive models (the Julia QPModel's pattern): its first
+    two calls stage through pageable copies, the later ones through the pinned
+    pack and the single read-back of outputs and flags; every model matches a
+    fresh handle bit for bit, and a model the path cannot take (Q = 0) on the
+    pinned route still falls back to the batched route in the same call."""
+    n, m, p = 50, 80, 30
+    e = QPBatch(2, n, m, p)
+    for it in range(4):
+        d = _data(2, n, m, p, 0.2, 9100 + it)
+        if it == 3:
+            d["Q"][1] = 0.0
+        args = [d[k] for k in ("Q", "G", "h", "A", "z", "lam", "nu")]
+        e.set(*args)
+        rev = e.reverse(d["dl_dz"])
+        fwd = e.forward(dq=d["dq"], dh=d["dh"], db=d["db"])
+        assert (e.lu_kind() == SMALL).all() == (it < 3)
+        f = QPBatch(2, n, m, p)
+        f.set(*args)
+        np.testing.assert_array_equal(rev, f.reverse(d["dl_dz"]))
+        np.testing.assert_array_equal(fwd, f.forward(dq=d["dq"], dh=d["dh"], db=d["db"]))
+        f.close()
+        for b in range(2):
+            ref_r, ref_f = _oracle(d, b, p)
+            assert relfro(rev[b], ref_r) <= RTOL
+            if not (it == 3 and b == 1):   # (the LSQR branch's forward: as test_small_path_fallbacks, reverse only)
+                assert relfro(fwd[b], ref_f) <= RTOL
+    e.close()
