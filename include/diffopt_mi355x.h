@@ -314,7 +314,11 @@ int dopt_nlp_set(dopt_handle* h, const double* Hxx, const double* Hxp, const dou
  * is queued: the verdicts (fallbacks, corrections) are read back by the next
  * call that needs the factors (forward / reverse / jacobian / kkt_solve /
  * get_corrections / get_system_size), which then overlaps that wait with
- * its own right-hand sides. */
+ * its own right-hand sides.  On the reduced route the LU is launched without
+ * reading the sizes back first, on the guess that every problem is reduced
+ * and H symmetric; the next call redoes the factorisation when the guess
+ * missed, and the handle stops guessing after one miss.  Until that next
+ * call, device-mode inputs must stay unchanged (a fallback re-reads them). */
 int dopt_nlp_factor(dopt_handle* h);
 /* dp[P] → dx[n], ddual[c + nlow + nup] (constraint duals, then the duals of
  * the primal lower and upper bounds in variable order): ∂s·Δp. */
