@@ -119,13 +119,21 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
     if (const char* e = getenv("DOPT_LU")) h->lu_mode = atoi(e) != 0;
     if (const char* e = getenv("DOPT_SYM")) h->sym_mode = atoi(e) != 0;
     if (const char* e = getenv("DOPT_LEFT")) h->left_mode = atoi(e) != 0;
+    if (const char* e = getenv("DOPT_LFLAT")) h->lflat = atoi(e) != 0;
+    if (const char* e = getenv("DOPT_LSPLIT")) h->lsplit = atoi(e) != 0;
     if (const char* e = getenv("DOPT_NLP_REDUCE")) h->nlp_reduce = atoi(e) != 0;
     if (const char* e = getenv("DOPT_SPLIT_FUSE")) h->split_fuse = atoi(e) != 0;
     if (kind == DOPT_KIND_QP) {
       // largest supported system: the generic solve stages an nmax vector in
       // LDS (64 KB); the blocked route takes reduced systems up to BLOCKED_MAX
-      if ((int64_t)n + m + p > 8192)
-        throw Error(-1, "QP systems with n + m + p > 8192 are not supported");
+      // above the dense route's cap (8192: the generic solve stages an nmax
+      // vector in LDS) the handle takes the sparse route (sparse.hip): the MOI
+      // matrix form through dopt_qp_set_csc, the LSQR branch, no dense K
+      if ((int64_t)n + m + p > dopt::DENSE_QP_MAX) {
+        h->sparse = true;
+        h->kamax.ensure(sizeof(double));
+        return 0;
+      }
       // Systems are identity-padded to whole 32-column blocks (qp_assemble.hip),
       // so the per-problem stride / row stride are rounded up to 32.
       h->nmax = (int32_t)dopt::round_up(std::max(n + m + p, 1), 32);
@@ -172,7 +180,7 @@ int dopt_destroy(dopt_handle* h) {
                     &h->x, &h->cone_dev, &h->vp, &h->dpi, &h->cwork, &h->cinfo, &h->cnorm, &h->csplit, &h->krhs, &h->kx,
                     &h->kfull, &h->kamax, &h->nlp_map, &h->nlp_shift, &h->nlp_scale, &h->kls, &h->gk, &h->glist,
                     &h->mws, &h->qsy, &h->psd_eig, &h->psd_app, &h->ukp, &h->nlp_rd, &h->nlp_ri, &h->nlp_t1, &h->nlp_t2,
-                    &h->nlp_msc, &h->pack, &h->tpack};
+                    &h->nlp_msc, &h->pack, &h->tpack, &h->rpack, &h->xacc};
   for (auto* b : bufs) b->release();
   for (auto& b : h->own_nin) b.release();
   for (auto& b : h->own_in) b.release();
@@ -217,10 +225,22 @@ int dopt_set_memory(dopt_handle* h, int32_t mem) {
   });
 }
 
+int dopt_set_sparse(dopt_handle* h, int32_t on) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_set_sparse: QP handles only");
+    if (!on && (int64_t)h->n + h->m + h->p > dopt::DENSE_QP_MAX)
+      throw Error(-1, "dopt_set_sparse: n + m + p > 8192 has only the sparse route");
+    h->sparse = on != 0;
+    h->set = h->factored = h->small_ready = false;   // a model is set again under the new route
+    return 0;
+  });
+}
+
 int dopt_qp_set(dopt_handle* h, const double* Q, const double* G, const double* hv,
                 const double* A, const double* z, const double* lam, const double* nu) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_set on a non-QP handle");
+    if (h->sparse) throw Error(-1, "dopt_qp_set: a sparse-route handle takes the MOI matrix form (dopt_qp_set_csc)");
     const size_t B = h->batch, n = h->n, m = h->m, p = h->p;
     if (!Q || !z) throw Error(-1, "Q and z are required");
     if (m && (!G || !hv || !lam)) throw Error(-1, "G, h and lam are required when m > 0");
@@ -344,6 +364,38 @@ int dopt_qp_set_csc(dopt_handle* h,
     h->csc_err.ensure(sizeof(int));
     DOPT_CHECK_HIP(hipMemsetAsync(h->csc_err.p, 0, sizeof(int), h->stream));
     int* err = h->csc_err.as<int>();
+    if (h->sparse) {   // kept sparse (sparse.hip): G, A and their CSR copies; Q only tested for zero
+      const int64_t* cp[3];
+      const int64_t* rv[3];
+      const double* nz[3];
+      const int64_t nnz[3] = {Q_nnz, G_nnz, A_nnz};
+      const int64_t* icp[3] = {Q_colptr, G_colptr, A_colptr};
+      const int64_t* irv[3] = {Q_rowval, G_rowval, A_rowval};
+      const double* inz[3] = {Q_nzval, G_nzval, A_nzval};
+      const size_t rows[3] = {n, m, p};
+      for (int k = 0; k < 3; ++k) {
+        const bool on = rows[k] > 0;
+        cp[k] = on ? stage_in_i64(*h, h->csc_in[3 * k], icp[k], B * (n + 1)) : nullptr;
+        rv[k] = on && nnz[k] ? stage_in_i64(*h, h->csc_in[3 * k + 1], irv[k], (size_t)nnz[k]) : nullptr;
+        nz[k] = on && nnz[k] ? stage_in(*h, h->csc_in_val[k], inz[k], (size_t)nnz[k]) : nullptr;
+      }
+      dopt::sp_set_csc(*h, cp[0], rv[0], nz[0], nnz[0], cp[1], rv[1], nz[1], nnz[1], cp[2], rv[2], nz[2], nnz[2],
+                       err);
+      int herr = 0;
+      DOPT_CHECK_HIP(hipMemcpyAsync(&herr, err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+      if (herr & 3) throw Error(-1, (herr & 1) ? "CSC colptr is not monotone / out of range"
+                                               : "CSC rowval out of range");
+      h->sp_qnz = (herr & 4) != 0;
+      h->Q = h->G = h->A = nullptr;
+      h->hv = m ? stage_in(*h, h->own_in[2], hv, B * m) : nullptr;
+      h->z = stage_in(*h, h->own_in[4], z, B * n);
+      h->lam = m ? stage_in(*h, h->own_in[5], lam, B * m) : nullptr;
+      h->nu = p ? stage_in(*h, h->own_in[6], nu, B * p) : nullptr;
+      h->set = true;
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+      return 0;
+    }
     struct Mat { const int64_t *cp, *rv; const double* nz; int64_t nnz; size_t rows; int slot; };
     const Mat mats[3] = {{Q_colptr, Q_rowval, Q_nzval, Q_nnz, n, 0},
                          {G_colptr, G_rowval, G_nzval, G_nnz, m, 1},
@@ -406,6 +458,10 @@ int dopt_qp_set_csc(dopt_handle* h,
 int dopt_qp_factor(dopt_handle* h) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_factor on a non-QP handle");
+    if (h->sparse) {
+      dopt::sp_factor(*h);
+      return 0;
+    }
     dopt::qp_factor(*h);
     return first_info(*h);
   });
@@ -475,6 +531,15 @@ int dopt_qp_reverse(dopt_handle* h, const double* dl_dz, double* out) {
     const size_t B = h->batch, n = h->n, L = h->n + h->m + h->p;
     const bool host = h->mem != DOPT_MEM_DEVICE;
     const double* d = nullptr;
+    if (h->sparse) {   // sparse route: LSQR on the implicit LHS (no singular verdict)
+      d = stage_in(*h, h->tin[0], dl_dz, B * n);
+      double* o = out_ptr(*h, h->tout[0], out, B * L);
+      dopt::sp_reverse(*h, d, o);
+      copy_out(*h, out, o, B * L);
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+      h->last_time = tm.s();
+      return 0;
+    }
     // a model not yet factorised, batch of a few: the one-launch small path
     // (qp_small.hip), its traffic one copy each way in host mode (the seed
     // through the pinned pack; the outputs with the per-problem flags after
@@ -526,7 +591,7 @@ int dopt_qp_forward(dopt_handle* h, const double* dQ, const double* dq, const do
     if (!out) throw Error(-1, "out is required");
     Timer tm;
     const size_t B = h->batch, n = h->n, m = h->m, p = h->p, L = n + m + p;
-    if (!h->factored && h->small_ready && pin_ok(*h)) {   // the small path's factors (dopt_qp_reverse): one copy each way
+    if (!h->sparse && !h->factored && h->small_ready && pin_ok(*h)) {   // the small path's factors (dopt_qp_reverse): one copy each way
       const PackIn pi[6] = {{dQ, B * n * n * sizeof(double)}, {dq, B * n * sizeof(double)},
                             {m ? dG : nullptr, B * m * n * sizeof(double)}, {m ? dh : nullptr, B * m * sizeof(double)},
                             {p ? dA : nullptr, B * p * n * sizeof(double)}, {p ? db : nullptr, B * p * sizeof(double)}};
@@ -554,6 +619,14 @@ int dopt_qp_forward(dopt_handle* h, const double* dQ, const double* dq, const do
     const double* e = stage_in(*h, h->tin[5], dA, B * p * n);
     const double* f = stage_in(*h, h->tin[6], db, B * p);
     double* o = out_ptr(*h, h->tout[1], out, B * L);
+    if (h->sparse) {
+      dopt::sp_forward(*h, dopt::FwdTangents{a, b, m ? c : nullptr, m ? d : nullptr, p ? e : nullptr, p ? f : nullptr},
+                       o);
+      copy_out(*h, out, o, B * L);
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+      h->last_time = tm.s();
+      return 0;
+    }
     if (!h->factored && h->small_ready) {   // the small path's factors (dopt_qp_reverse)
       dopt::qp_small_forward(*h, dopt::FwdTangents{a, b, m ? c : nullptr, m ? d : nullptr, p ? e : nullptr,
                                                    p ? f : nullptr},
@@ -574,6 +647,7 @@ int dopt_qp_forward(dopt_handle* h, const double* dQ, const double* dq, const do
 int dopt_qp_reverse_k(dopt_handle* h, int32_t k, const double* dl_dz, double* out) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_reverse_k on a non-QP handle");
+    if (h->sparse) throw Error(-1, "multi-RHS calls need factors: not on the sparse (LSQR) route");
     if (!dl_dz || !out) throw Error(-1, "dl_dz and out are required");
     if (k <= 0) throw Error(-1, "k must be positive");
     Timer tm;
@@ -592,6 +666,7 @@ int dopt_qp_forward_k(dopt_handle* h, int32_t k, const double* dQ, const double*
                       const double* dh, const double* dA, const double* db, double* out) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_qp_forward_k on a non-QP handle");
+    if (h->sparse) throw Error(-1, "multi-RHS calls need factors: not on the sparse (LSQR) route");
     if (!out) throw Error(-1, "out is required");
     if (k <= 0) throw Error(-1, "k must be positive");
     Timer tm;
@@ -629,6 +704,17 @@ int dopt_qp_forward_reverse(dopt_handle* h, const double* dl_dz, const double* d
     const double* f = stage_in(*h, h->tin[6], db, B * p);
     double* o1 = out_ptr(*h, h->tout[0], out_rev, B * L);
     double* o2 = out_ptr(*h, h->tout[1], out_fwd, B * L);
+    if (h->sparse) {   // both LSQR runs in one launch; device mode returns stream-ordered
+      h->factored = false;
+      dopt::sp_forward_reverse(*h, r, dopt::FwdTangents{a, b, m ? c : nullptr, m ? d : nullptr, p ? e : nullptr,
+                                                        p ? f : nullptr},
+                               o1, o2);
+      copy_out(*h, out_rev, o1, B * L);
+      copy_out(*h, out_fwd, o2, B * L);
+      if (h->mem != DOPT_MEM_DEVICE) DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+      h->last_time = tm.s();
+      return 0;
+    }
     h->factored = false;  // one solve = factor + fwd + rev (the factors are kept for later calls)
     h->info_clear = false;
     dopt::qp_forward_reverse(*h, r, a, b, c, d, e, f, o1, o2);
@@ -698,6 +784,7 @@ int dopt_nlp_set_structure(dopt_handle* h, const int32_t* con_kind, const int8_t
     DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
     h->nstruct = true;
     h->nset = false;
+    h->nlp_spec_off = false;   // a new structure: the speculative LU launch is tried again
     return 0;
   });
 }
@@ -908,7 +995,9 @@ int dopt_lhs_resolve(dopt_handle* h, int32_t k, const double* rhs, double* x, in
     const size_t cnt = (size_t)k * h->batch * h->nlp_rows;
     const PackIn pi[1] = {{rhs, cnt * sizeof(double)}};
     const void* pd[1] = {nullptr};
-    const bool small = cnt * sizeof(double) <= LHS_PACK_MAX && pin_ok(*h) && pack_in(*h, pi, 1, pd, &h->tpack);
+    // (its own device buffer: tpack still holds M when dopt_lhs_solve packed it,
+    // and nin[0] points there for a later re-factorisation)
+    const bool small = cnt * sizeof(double) <= LHS_PACK_MAX && pin_ok(*h) && pack_in(*h, pi, 1, pd, &h->rpack);
     const double* r = small ? static_cast<const double*>(pd[0]) : stage_in(*h, h->tin[0], rhs, cnt);
     double* o = out_ptr(*h, h->tout[0], x, cnt);
     dopt::lhs_resolve(*h, k, r, o, trans != 0, info.data());
@@ -953,7 +1042,9 @@ int dopt_nlp_get_layout(dopt_handle* h, int32_t* layout) {
 int dopt_get_info(dopt_handle* h, int32_t* info) {
   return guarded(h, [&]() {
     if (!info) throw Error(-1, "info is required");
-    if (h->kind == DOPT_KIND_QP) {
+    if (h->kind == DOPT_KIND_QP && h->sparse) {   // LSQR only: never singular
+      std::fill(info, info + h->batch, 0);
+    } else if (h->kind == DOPT_KIND_QP) {
       std::vector<dopt::QPMeta> meta(h->batch);
       DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h->meta.p, h->batch * sizeof(dopt::QPMeta),
                                     hipMemcpyDeviceToHost, h->stream));
@@ -974,6 +1065,7 @@ int dopt_qp_get_kept(dopt_handle* h, int8_t* kept) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_QP) throw Error(-1, "QP only");
     if (!kept) throw Error(-1, "kept is required");
+    if (h->sparse) throw Error(-1, "the sparse route eliminates no rows (LSQR on the full LHS)");
     if (!h->factored && !h->small_ready) throw Error(-1, "no factorisation has run");
     const size_t B = h->batch, m = h->m;
     std::vector<int32_t> rpos(B * m);
@@ -990,6 +1082,16 @@ int dopt_qp_get_lu_kind(dopt_handle* h, int8_t* kinds) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_QP && h->kind != DOPT_KIND_NLP) throw Error(-1, "QP and NLP handles only");
     if (!kinds) throw Error(-1, "kinds is required");
+    if (h->kind == DOPT_KIND_NLP) {
+      // dopt_nlp_factor returns with the LU queued: the finish step (fallbacks,
+      // inertia corrections, a missed speculative launch) sets the final kinds
+      if (!h->nfactored) throw Error(-1, "no NLP factorisation has run");
+      dopt::nlp_finish(*h);
+    }
+    if (h->sparse) {   // every problem on the LSQR branch (dopt_qp_factor refuses any other)
+      std::fill(kinds, kinds + h->batch, (int8_t)DOPT_LU_KIND_LSQR);
+      return 0;
+    }
     std::vector<dopt::QPMeta> meta(h->batch);
     DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h->meta.p, h->batch * sizeof(dopt::QPMeta),
                                   hipMemcpyDeviceToHost, h->stream));
@@ -1023,6 +1125,11 @@ int dopt_get_iterative(dopt_handle* h, int8_t* flags) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_QP) throw Error(-1, "QP only");
     if (!flags) throw Error(-1, "flags is required");
+    if (h->sparse) {
+      if (!h->set) throw Error(-1, "no model is set");
+      std::fill(flags, flags + h->batch, (int8_t)(h->sp_qnz ? 0 : 1));
+      return 0;
+    }
     std::vector<dopt::QPMeta> meta(h->batch);
     DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h->meta.p, h->batch * sizeof(dopt::QPMeta),
                                   hipMemcpyDeviceToHost, h->stream));
@@ -1038,6 +1145,10 @@ int dopt_get_system_size(dopt_handle* h, int32_t* sizes) {
     if (h->kind == DOPT_KIND_QP || h->kind == DOPT_KIND_NLP) {
       if (h->kind == DOPT_KIND_NLP && !h->nfactored) throw Error(-1, "no NLP factorisation has run");
       if (h->kind == DOPT_KIND_NLP) dopt::nlp_finish(*h);
+      if (h->sparse) {   // the full LHS (nothing eliminated)
+        std::fill(sizes, sizes + h->batch, h->n + h->m + h->p);
+        return 0;
+      }
       std::vector<dopt::QPMeta> meta(h->batch);
       DOPT_CHECK_HIP(hipMemcpyAsync(meta.data(), h->meta.p, h->batch * sizeof(dopt::QPMeta),
                                     hipMemcpyDeviceToHost, h->stream));
@@ -1049,6 +1160,18 @@ int dopt_get_system_size(dopt_handle* h, int32_t* sizes) {
                                     h->batch * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
       DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
     }
+    return 0;
+  });
+}
+
+int dopt_qp_lsqr_stats(dopt_handle* h, int32_t* stats) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_QP || !h->sparse) throw Error(-1, "dopt_qp_lsqr_stats: sparse-route QP handles only");
+    if (!stats) throw Error(-1, "stats is required");
+    if (!h->sp_info.p) throw Error(-1, "no sparse solve has run");
+    DOPT_CHECK_HIP(hipMemcpyAsync(stats, h->sp_info.p, 4 * h->batch * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                  h->stream));
+    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
     return 0;
   });
 }

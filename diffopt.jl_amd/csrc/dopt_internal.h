@@ -71,6 +71,7 @@ struct QPMeta {
 constexpr int ASM_WPP = 16;          // assembly tile workgroups per problem (qp_assemble.hip)
 constexpr int SM_MAX = 128;          // small-problem path (qp_small.hip): largest reduced system held in LDS
 constexpr int SM_BATCH = 8;          // ... and the largest batch it takes (one model at a time: the Julia back-end)
+constexpr int DENSE_QP_MAX = 8192;   // largest n + m + p of the dense QP route (above: sparse.hip)
 constexpr int BLOCKED_MAX = 4096;    // largest reduced system of the blocked route (no-pivot LU, blocked solves)
 constexpr int PIVOT_MAX = 1536;      // largest system of the partial-pivoting blocked LU (panel: 512 threads × 3 rows);
                                      // larger blocked problems the no-pivot LU rejects take the generic LU
@@ -111,6 +112,14 @@ struct PScale {
     return in ? v : 1.0;
   }
 };
+// Sparse QP route (sparse.hip): one matrix of the batch kept in the MOI form
+// (CSC, 0-based) plus a CSR copy built on the device
+struct SpStore {
+  DevBuf cp, ri, rp, ci, rv;   // CSC colptr / rows, CSR rowptr / columns / values
+  const double* cv = nullptr;  // CSC values (staged or borrowed nzval)
+  int64_t nnz = 0;
+  int rows = 0;
+};
 // QP problem inputs / forward tangents as seen by the kernels (device pointers)
 struct QPIn {
   const double *Q, *G, *h, *A, *z, *lam, *nu;
@@ -143,6 +152,7 @@ struct Handle {
   // inputs (into tpack: pack stays the inputs' home), the outputs and the
   // per-problem flags read back by ONE copy into pin_out
   DevBuf tpack;
+  DevBuf rpack;              // dopt_lhs_resolve's right-hand sides (tpack may hold the plug point's M)
   void* pin_out = nullptr;
   size_t pin_out_bytes = 0;
   int io_calls = 0;          // small-path calls so far (abi.hip pin_ok: pinned from the third on)
@@ -162,6 +172,11 @@ struct Handle {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_qsym = nullptr, ev_crit = nullptr;
   hipStream_t crit = nullptr;      // high-priority stream of the right-looking LU's critical chain
   int32_t left_mode = 1;           // P-symmetric batches: left-looking LU (env DOPT_LEFT=0: right-looking)
+  int32_t lflat = 1;               // left-looking LU: the column tiles accumulate the diagonal blocks' updates
+                                   // and sweeps (flat chain; env DOPT_LFLAT=0: ldiag restages the strips)
+  int32_t lsplit = 0;              // left-looking LU: tile (J+1, J) on the stream, the column's other tiles on `aux`
+                                   // beside ldiag(J+1) (env DOPT_LSPLIT)
+  DevBuf xacc;                     // ... those accumulators, one 64 × 64 (ten 16 × 16 tiles) per problem and block
   DevBuf ukp;                      // left-looking LU: u_kk / p_k of every finished diagonal block (nmax per problem)
   bool ukp_valid = false;          // the last no-pivot factorisation was left-looking (ukp holds its u_kk / p_k)
   bool u_missing = false;          // ... and stored only L for its P-symmetric problems (U from L on demand)
@@ -188,6 +203,11 @@ struct Handle {
   int32_t n_pivot = 0;             // problems factorised with partial pivoting (last factorisation)
   bool set = false, factored = false;
   bool small_ready = false;        // the small path's factors are in K (qp_small.hip; dopt_qp_forward reuses them)
+  // sparse route (sparse.hip): n + m + p above the dense cap, or dopt_set_sparse
+  bool sparse = false;
+  bool sp_qnz = false;             // some problem's Q has a non-zero value (needs an LU this route lacks)
+  SpStore sp[2];                   // G, A
+  DevBuf sp_tmp, sp_sort, sp_s, sp_ws, sp_info, sp_rhs;
 
   // ---- CONIC ----
   const double *cA = nullptr, *cb = nullptr, *cc = nullptr;
@@ -381,6 +401,14 @@ double* dense_dinv(Handle& h);
 void lsqr_slabs(Handle& h, int trans, const double* rhs, double* x);
 void lhs_solve(Handle& h, int k, const double* rhs, double* x, bool iterative, int32_t* info);
 void lhs_resolve(Handle& h, int k, const double* rhs, double* x, bool trans, int32_t* info);
+// sparse QP route (sparse.hip)
+void sp_set_csc(Handle& h, const int64_t* Qcp, const int64_t* Qrv, const double* Qnz, int64_t Qnnz,
+                const int64_t* Gcp, const int64_t* Grv, const double* Gnz, int64_t Gnnz, const int64_t* Acp,
+                const int64_t* Arv, const double* Anz, int64_t Annz, int* err);
+void sp_factor(Handle& h);
+void sp_reverse(Handle& h, const double* dl_dz, double* out);
+void sp_forward(Handle& h, const FwdTangents& T, double* out);
+void sp_forward_reverse(Handle& h, const double* dl_dz, const FwdTangents& T, double* out_rev, double* out_fwd);
 void nlp_configure(Handle& h);
 // defer: dopt_nlp_factor (the rest in nlp_finish); spec: the LU may be launched
 // before the prepare kernel's metadata is read back (nlp_finish checks it)

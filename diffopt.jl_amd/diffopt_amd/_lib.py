@@ -11,8 +11,14 @@ import os
 LIB_NAME = "libdiffopt_mi355x.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # A/B builds of the same engine (tools/build_variant.sh): DOPT_LIB names one
-# in place of the default in-tree library (benchmarking only)
-LIB_PATH = os.environ.get("DOPT_LIB") or LIB_PATH
+# in place of the default in-tree library (benchmarking only).  The override is
+# announced on stderr and recorded in LIB_OVERRIDE, so a stale variant left in
+# the environment cannot silently stand in for the in-tree build.
+LIB_OVERRIDE = os.environ.get("DOPT_LIB") or None
+if LIB_OVERRIDE:
+    import sys
+    print(f"diffopt_amd: DOPT_LIB={LIB_OVERRIDE} replaces the in-tree {LIB_PATH}", file=sys.stderr)
+    LIB_PATH = LIB_OVERRIDE
 
 DOPT_KIND_QP = 0
 DOPT_KIND_CONIC = 1
@@ -39,6 +45,8 @@ SIGNATURES = {
     "dopt_set_memory": (ctypes.c_int, [_h, ctypes.c_int32]),
     "dopt_qp_set": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 7),
     "dopt_qp_factor": (ctypes.c_int, [_h]),
+    "dopt_set_sparse": (ctypes.c_int, [_h, ctypes.c_int32]),
+    "dopt_qp_lsqr_stats": (ctypes.c_int, [_h, ctypes.c_void_p]),
     "dopt_qp_reverse": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_void_p]),
     "dopt_qp_reverse_grads": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 7),
     "dopt_conic_set_csc": (ctypes.c_int, [_h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

@@ -44,7 +44,9 @@ def _check_out(o, shape, device):
 class QPBatch:
     """Batched QP sensitivity engine (C-ABI handle wrapper)."""
 
-    def __init__(self, batch, n, m, p=0, device=0):
+    DENSE_MAX = 8192   # n + m + p of the dense route; above it the handle is sparse (dopt_set_sparse)
+
+    def __init__(self, batch, n, m, p=0, device=0, sparse=False):
         self.lib = _lib.load()
         self.batch, self.n, self.m, self.p = int(batch), int(n), int(m), int(p)
         self.device = device
@@ -56,6 +58,17 @@ class QPBatch:
         self.h = h
         self._mem = None
         self._keep = None
+        # the sparse route (sparse.hip): automatic above the dense cap, opt-in below
+        self.sparse = bool(sparse) or self.L > self.DENSE_MAX
+        if sparse:
+            _lib.check(self.lib.dopt_set_sparse(self.h, 1), self.h)
+
+    def lsqr_stats(self):
+        """Sparse route: (B, 2, 2) int32 — [istop, iterations] of the last
+        reverse (index 0) and forward (index 1) LSQR runs per problem."""
+        out = np.zeros(4 * self.batch, dtype=np.int32)
+        _lib.check(self.lib.dopt_qp_lsqr_stats(self.h, out.ctypes.data), self.h)
+        return out.reshape(2, self.batch, 2).transpose(1, 0, 2)
 
     def close(self):
         if getattr(self, "h", None):
@@ -421,15 +434,17 @@ class MI355XSolver:
         # the reference's second call per model passes LHS' (an adjoint of the
         # LHS it just solved with: QuadraticProgram.jl:335, :438): an array
         # that is exactly the transpose of the one factorised last (same
-        # memory, shape and strides reversed) is answered from those factors,
-        # once per factorisation; any other call factorises (the array may
-        # have changed in place since)
+        # memory, shape and strides reversed) AND whose contents still equal
+        # the matrix factorised (a copy kept at that call: an edit in place
+        # between the two calls refactorises, as `\` would) is answered from
+        # those factors, once per factorisation; any other call factorises
         lhs = LHS if isinstance(LHS, np.ndarray) else None
         key = None
         if lhs is not None and lhs.ndim == 2:
             key = (lhs.__array_interface__["data"][0], lhs.shape, lhs.strides)
         reuse = (not iterative and key is not None and self._fact is not None
-                 and (key[0], key[1][::-1], key[2][::-1]) == self._fact[0])
+                 and (key[0], key[1][::-1], key[2][::-1]) == self._fact[0]
+                 and np.array_equal(lhs.T, self._fact[1]))
         if reuse:
             rc = self.lib.dopt_lhs_resolve(h, k, rhs.ctypes.data, out.ctypes.data, 1)
             self.resolves += 1
@@ -438,7 +453,8 @@ class MI355XSolver:
             Mc = np.ascontiguousarray(np.swapaxes(M, 1, 2))        # column-major per problem
             rc = self.lib.dopt_lhs_solve(h, rows, Mc.ctypes.data, k, rhs.ctypes.data, out.ctypes.data,
                                          int(bool(iterative)))
-            self._fact = None if iterative or key is None else (key, lhs)   # (lhs kept alive)
+            # (the contents factorised, for the reuse check above)
+            self._fact = None if iterative or key is None else (key, np.array(lhs, copy=True))
         _lib.check(rc, h)
         X = np.transpose(out, (1, 2, 0))                           # (B, rows, k)
         if vec:

@@ -328,3 +328,49 @@ def conic_numpy_wellcond(batch, n, cones, seed, f_interior=0.25, f_dual_interior
         out["db"].append(rng.standard_normal(m))
         out["dc"].append(rng.standard_normal(n))
     return {k: np.stack(v) for k, v in out.items()}
+
+
+def lp_sparse_numpy(batch, n, p, m_extra, k, seed):
+    """Seeded sparse LPs (Q = 0: the reference's LSQR branch) at a vertex, for
+    the sparse route (sparse.hip).  Per problem: n − p active inequality rows
+    and the p equality rows together form W = Π·(I + 0.3·R/√k) (R: k random
+    N(0,1) entries per row, Π a row permutation) — a well-conditioned square
+    matrix, so the full KKT LHS is nonsingular and LSQR converges well before
+    maxiter; m_extra inactive rows with k random entries each.  Active rows:
+    s = 0, λ ~ U(0.5, 1.5); inactive: λ = 0, s ~ −U(0.5, 1.5).  Returns dict of
+    lists: G, A (scipy CSC per problem), h, z, lam, nu, dl_dz, dq, dh, db
+    (stacked arrays), with m = n − p + m_extra."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    m = n - p + m_extra
+    out = {key: [] for key in ["G", "A", "h", "z", "lam", "nu", "dl_dz", "dq", "dh", "db"]}
+    for _ in range(batch):
+        rows = np.repeat(np.arange(n), k)
+        cols = rng.integers(0, n, size=n * k)
+        vals = 0.3 * rng.standard_normal(n * k) / math.sqrt(k)
+        W = (sp.identity(n, format="csr") + sp.csr_matrix((vals, (rows, cols)), shape=(n, n))).tocsr()
+        W = W[rng.permutation(n)]
+        Ga, A = W[: n - p], W[n - p:]
+        ri = np.repeat(np.arange(m_extra), k)
+        ci = rng.integers(0, n, size=m_extra * k)
+        Gi = sp.csr_matrix((rng.standard_normal(m_extra * k) / math.sqrt(k), (ri, ci)), shape=(m_extra, n))
+        G = sp.vstack([Ga, Gi]).tocsr()
+        perm = rng.permutation(m)
+        G = G[perm]
+        act = perm < n - p                       # row i of G is active iff it came from Ga
+        lam = np.where(act, rng.uniform(0.5, 1.5, size=m), 0.0)
+        s = np.where(act, 0.0, -rng.uniform(0.5, 1.5, size=m))
+        z = rng.standard_normal(n)
+        out["G"].append(sp.csc_matrix(G))
+        out["A"].append(sp.csc_matrix(A))
+        out["h"].append(G @ z - s)
+        out["z"].append(z)
+        out["lam"].append(lam)
+        out["nu"].append(rng.standard_normal(p))
+        out["dl_dz"].append(rng.standard_normal(n))
+        out["dq"].append(rng.standard_normal(n))
+        out["dh"].append(rng.standard_normal(m))
+        out["db"].append(rng.standard_normal(p))
+    for key in ["h", "z", "lam", "nu", "dl_dz", "dq", "dh", "db"]:
+        out[key] = np.stack(out[key])
+    return out

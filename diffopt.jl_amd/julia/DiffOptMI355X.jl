@@ -253,8 +253,9 @@ mutable struct MI355XSolver
     rows::Int
     last::Any          # the matrix whose factorisation the handle holds (by identity)
     last_adj::Bool     # ... factorised as its adjoint
+    last_M::Any        # ... and the contents factorised (the reuse checks them: an in-place edit refactorises)
 end
-MI355XSolver(; device::Integer = 0) = MI355XSolver(device, nothing, 0, nothing, false)
+MI355XSolver(; device::Integer = 0) = MI355XSolver(device, nothing, 0, nothing, false, nothing)
 
 function _solver_handle!(s::MI355XSolver, rows::Int)
     if s.handle === nothing || s.rows != rows
@@ -272,10 +273,14 @@ function QP.solve_system(s::MI355XSolver, LHS, RHS, iterative)
     h = _solver_handle!(s, rows)
     # the second call per model passes LHS' — an Adjoint wrapping the very
     # LHS just factorised (:335 then :438): answered from those factors by a
-    # transposed solve (dopt_lhs_resolve), in either order
+    # transposed solve (dopt_lhs_resolve), in either order — provided its
+    # contents are still the ones factorised (the reference never edits LHS
+    # between the two calls, but `\` has no such hazard: an edit in place
+    # falls through to a fresh factorisation)
     adj = LHS isa LinearAlgebra.Adjoint || LHS isa LinearAlgebra.Transpose
     obj = adj ? parent(LHS) : LHS
-    if !iterative && s.last !== nothing && obj === s.last && adj != s.last_adj
+    if !iterative && s.last !== nothing && obj === s.last && adj != s.last_adj &&
+       (s.last_adj ? transpose(obj) == s.last_M : obj == s.last_M)
         GC.@preserve rhs x begin
             rc = ccall((:dopt_lhs_resolve, LIB), Cint,
                        (Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}, Int32), h.ptr, 1, rhs, x, 1)
@@ -293,6 +298,7 @@ function QP.solve_system(s::MI355XSolver, LHS, RHS, iterative)
                    h.ptr, rows, M, 1, rhs, x, Int32(iterative))
         s.last = iterative ? nothing : obj
         s.last_adj = adj
+        s.last_M = iterative ? nothing : M
         _check(rc, h.ptr)                    # rc > 0: SingularException(rc)
     end
     return x

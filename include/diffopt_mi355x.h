@@ -64,7 +64,9 @@ typedef struct dopt_handle dopt_handle;
  * CONIC: n variables, m conic rows (A x + b ∈ K), p ignored.
  * Replaces: `MOI.instantiate(QuadraticProgram.Model)` / `ConicProgram.Model()`
  * (reference moi_wrapper.jl:605-617; QuadraticProgram.jl:107-120;
- * ConicProgram.jl:99-111). */
+ * ConicProgram.jl:99-111).
+ * A QP handle with n + m + p > 8192 takes the SPARSE route (see
+ * dopt_set_sparse): no dense KKT storage is allocated. */
 int dopt_create(dopt_handle** h, int device, int64_t batch, int32_t n,
                 int32_t m, int32_t p, int32_t kind);
 int dopt_destroy(dopt_handle* h);
@@ -87,6 +89,23 @@ int dopt_set_memory(dopt_handle* h, int32_t mem);
 int dopt_qp_set(dopt_handle* h, const double* Q, const double* G,
                 const double* hvec, const double* A, const double* z,
                 const double* lam, const double* nu);
+/* Sparse QP route (sparse.hip; on = 1).  The MOI matrix form stays sparse, as
+ * in the reference (`_gradient_cache` keeps SparseMatrixCSC,
+ * QuadraticProgram.jl:182-213): dopt_qp_set_csc keeps G and A as CSC plus a
+ * CSR copy built on the device, and every solve is `lsqr(LHS, RHS)` /
+ * `lsqr(LHS', RHS)` on the implicit full LHS (:486-492; IterativeSolvers 0.9
+ * defaults, maxiter = n + m + p) — no dense K, no size cap.  Only the LSQR
+ * branch exists on this route: dopt_qp_factor fails (−1, with a message) when
+ * any problem's Q has a non-zero value (`norm(Q) ≈ 0` false, :333), since that
+ * needs a sparse direct LU (UMFPACK in the reference).  Automatic for
+ * n + m + p > 8192 (the dense route's cap; on = 0 is then refused); opt-in
+ * below it (tests compare the two routes).  Resets the handle's model.  Not on
+ * this route: dopt_qp_set (dense inputs), the multi-RHS calls, the kept mask.
+ * Forward tangents dQ / dG / dA stay dense column-major arrays (NULL = zero). */
+int dopt_set_sparse(dopt_handle* h, int32_t on);
+/* LSQR statistics of the sparse route's last solves, 4·B int32: per problem
+ * [istop | iterations] of the reverse run, then of the forward run. */
+int dopt_qp_lsqr_stats(dopt_handle* h, int32_t* stats);
 /* Same as dopt_qp_set, with Q, G, A given in the MOI matrix form the
  * reference builds (`_gradient_cache`, QuadraticProgram.jl:182-213;
  * `sparse_array_representation`, utils.jl:46-69): Julia SparseMatrixCSC

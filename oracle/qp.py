@@ -172,3 +172,44 @@ def reverse_constraint_eq(z, nu, dz, dnu):
     ``dν_i`` (user-facing ``db = −dν``)."""
     dA = dnu[:, None] * z[None, :] + nu[:, None] * dz[None, :]
     return dA, dnu.copy()
+
+
+def create_LHS_sparse(z, lam, G, h, A, n):
+    """``create_LHS_matrix`` (QuadraticProgram.jl:256-282) with Q = 0 as the
+    reference builds it — a ``SparseMatrixCSC`` (scipy CSC here), never dense:
+    ``[0, GᵀD(λ), Aᵀ; G, D(Gz − h), 0; A, 0, 0]``.  G, A: scipy sparse."""
+    m = 0 if G is None else G.shape[0]
+    p = 0 if A is None else A.shape[0]
+    top = [sp.csc_matrix((n, n))]
+    if m:
+        s = G @ z - h
+        top.append(G.T @ sp.diags(lam))
+    if p:
+        top.append(A.T)
+    rows = [top]
+    if m:
+        rows.append([G, sp.diags(s)] + ([None] if p else []))
+    if p:
+        rows.append([A] + ([None] if m else []) + [None])
+    return sp.bmat(rows, format="csc")
+
+
+def lp_sparse_differentiate(G, h, A, z, lam, nu, dl_dz, dq=None, dh=None, db=None):
+    """Reverse and forward of the LSQR branch (Q = 0) on the sparse LHS:
+    ``−lsqr(LHS, [dl/dz; 0; 0])`` (:336-337) and ``−lsqr(LHS', RHS)`` with the
+    forward RHS of :429-433 for vector tangents (dQ = dG = dA = 0).  Returns
+    (reverse [dz|dλ|dν], forward [dz|dλ|dν], (it_rev, istop_rev), (it_fwd, istop_fwd))."""
+    from .lsqr import lsqr
+    n = z.shape[0]
+    m = 0 if G is None else G.shape[0]
+    p = 0 if A is None else A.shape[0]
+    L = create_LHS_sparse(z, lam, G, h, A, n)
+    N = n + m + p
+    r_rev = np.concatenate([dl_dz, np.zeros(m + p)])
+    r1 = np.zeros(n) if dq is None else np.array(dq, float)
+    r2 = np.zeros(m) if dh is None or not m else -lam * dh
+    r3 = np.zeros(p) if db is None or not p else -np.asarray(db, float)
+    r_fwd = np.concatenate([r1, r2, r3])
+    xr, itr, isr = lsqr(lambda v: L @ v, lambda u: L.T @ u, r_rev, N, return_info=True)
+    xf, itf, isf = lsqr(lambda v: L.T @ v, lambda u: L @ u, r_fwd, N, return_info=True)
+    return -xr, -xf, (itr, isr), (itf, isf)

@@ -98,3 +98,30 @@ def test_cached_solver_handle():
     assert s._key == (1, L.shape[0])
     s.close()
 
+
+def test_factor_reuse_sees_in_place_edit():
+    """the LHS' call is answered from the LHS call's
+    factors only while the matrix still holds the contents factorised.  An
+    edit in place between the two calls (same memory, so the transposed view
+    looks identical by address) must refactorise and give ``L'ᵀ \\ rhs`` of
+    the EDITED matrix, as the reference's ``LHS' \\ RHS`` does
+    (QuadraticProgram.jl:335, :438); an unedited pair still takes the reuse."""
+    from diffopt_amd.qp import MI355XSolver
+    s = MI355XSolver()
+    rng = np.random.default_rng(31)
+    _, _, LHS = _kkt(41)
+    L = np.array(LHS.todense() if hasattr(LHS, "todense") else LHS, dtype=np.float64, order="C")
+    rhs = rng.standard_normal(L.shape[0])
+    s.solve_system(L, rhs)
+    before = s.resolves
+    L[2, 2] += 0.5                        # edited in place: the factors are stale
+    L[5, 1] -= 0.25
+    got = s.solve_system(L.T, rhs)
+    assert s.resolves == before           # no reuse: refactorised
+    np.testing.assert_allclose(got, np.linalg.solve(L.T, rhs), rtol=1e-10, atol=1e-12)
+    # the unedited pair: reused once, and still exact
+    s.solve_system(L, rhs)
+    got2 = s.solve_system(L.T, rhs)
+    assert s.resolves == before + 1
+    np.testing.assert_allclose(got2, np.linalg.solve(L.T, rhs), rtol=1e-10, atol=1e-12)
+    s.close()

@@ -1,0 +1,17 @@
+# Round 6: the sparse route's and the plug point's tests, QP parity under the
+# split column schedule (DOPT_LSPLIT), then config 2 in all four flat / split
+# combinations (two rounds), and the split form's kernel trace
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+J=tools/gpu_job.sh
+TEST_PATHS="tests/test_sparse_gpu.py tests/test_lhs_solve_gpu.py" bash $J test && cp gpurun_out/test.log gpurun_out/test_sparse.log && \
+DOPT_LSPLIT=1 TEST_PATHS="tests/test_qp_gpu.py tests/test_nlp_gpu.py" bash $J test || exit 1
+for r in a b; do
+ DOPT_LFLAT=0 DOPT_LSPLIT=0 bash $J bench f0s0$r --no-cpu-baseline && \
+ DOPT_LFLAT=1 DOPT_LSPLIT=0 bash $J bench f1s0$r --no-cpu-baseline && \
+ DOPT_LFLAT=0 DOPT_LSPLIT=1 bash $J bench f0s1$r --no-cpu-baseline && \
+ DOPT_LFLAT=1 DOPT_LSPLIT=1 bash $J bench f1s1$r --no-cpu-baseline || exit 1
+done
+DOPT_LSPLIT=1 bash $J prof split --steps 20 --warmup 3 && \
+python3 tools/timeline.py gpurun_out/prof_split > gpurun_out/timeline_split.txt
