@@ -97,6 +97,21 @@ constexpr double NOPIV_LMAX = 10.0;
 // multiplier bound alone lets growth of order 11^k through).
 constexpr double NOPIV_GROWTH = 1e8;
 
+// x + y·z with the product and the sum rounded separately — Julia's sparse
+// `mul!` arithmetic (the reference's Gz − h), which the kept set must match bit
+// for bit.  __dadd_rn / __dmul_rn do NOT guarantee this: the HIP headers define
+// them as plain + and *, which HIP's default -ffp-contract=fast-honor-pragmas
+// fuses into v_fma_f64 (round 6: the prepare kernels' s was FMA-contracted).
+// The pragma marks these two operations non-contractable wherever inlined.
+__device__ __forceinline__ double add_mul_rn(double x, double y, double z) {
+#pragma clang fp contract(off)
+  return x + y * z;
+}
+__device__ __forceinline__ double sub_rn(double x, double y) {
+#pragma clang fp contract(off)
+  return x - y;
+}
+
 // P-symmetric no-pivot LU (QPMeta::sym): the row scale p_r of the reduced
 // system's row r — λ of a kept inequality row, 1 for the z and ν rows
 // (kl = the problem's compacted λ_k, null for non-QP systems).

@@ -183,8 +183,8 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
           }
 #pragma unroll
           for (int u = 0; u < PREP_U2; ++u) {
-            acc[0] = __dadd_rn(acc[0], __dmul_rn(cur[u].x, zs[j + u]));
-            acc[1] = __dadd_rn(acc[1], __dmul_rn(cur[u].y, zs[j + u]));
+            acc[0] = add_mul_rn(acc[0], cur[u].x, zs[j + u]);
+            acc[1] = add_mul_rn(acc[1], cur[u].y, zs[j + u]);
             gm[0] = fmax(gm[0], fabs(cur[u].x));
             gm[1] = fmax(gm[1], fabs(cur[u].y));
             bstore1(wr, so0 + (unsigned)(j + u) * mb, cur[u].x);
@@ -197,8 +197,8 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
         }
         for (; j < n; ++j) {
           const dv2 g2 = bload2(gr, lo + (unsigned)j * mb);
-          acc[0] = __dadd_rn(acc[0], __dmul_rn(g2.x, zs[j]));
-          acc[1] = __dadd_rn(acc[1], __dmul_rn(g2.y, zs[j]));
+          acc[0] = add_mul_rn(acc[0], g2.x, zs[j]);
+          acc[1] = add_mul_rn(acc[1], g2.y, zs[j]);
           gm[0] = fmax(gm[0], fabs(g2.x));
           gm[1] = fmax(gm[1], fabs(g2.y));
           bstore1(wr, so0 + (unsigned)j * mb, g2.x);
@@ -211,14 +211,14 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
           for (int u = 0; u < PREP_U; ++u) gv[u] = gp[(size_t)(j + u) * m];
 #pragma unroll
           for (int u = 0; u < PREP_U; ++u) {
-            acc[0] = __dadd_rn(acc[0], __dmul_rn(gv[u], zs[j + u]));
+            acc[0] = add_mul_rn(acc[0], gv[u], zs[j + u]);
             gm[0] = fmax(gm[0], fabs(gv[u]));
             if (spec[0]) gw0[(size_t)(j + u) * m] = gv[u];
           }
         }
         for (; j < n; ++j) {
           const double g = gp[(size_t)j * m];
-          acc[0] = __dadd_rn(acc[0], __dmul_rn(g, zs[j]));
+          acc[0] = add_mul_rn(acc[0], g, zs[j]);
           gm[0] = fmax(gm[0], fabs(g));
           if (spec[0]) gw0[(size_t)j * m] = g;
         }
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(PREP_MAXT, 3) void qp_prep_kernel(QPIn P, double* _
       keep[q] = 0;
       si[q] = 0.0;
       if (valid[q]) {
-        si[q] = __dsub_rn(acc[q], hb[i + q]);
+        si[q] = sub_rn(acc[q], hb[i + q]);
         s_out[(size_t)b * m + i + q] = si[q];
         keep[q] = iterative ? 1 : !(li[q] == 0.0 && si[q] != 0.0);
         if (keep[q] && !spec[q]) atomicAdd(&extra, 1);

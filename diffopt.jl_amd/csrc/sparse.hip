@@ -147,8 +147,8 @@ __global__ __launch_bounds__(SP_SETUP) void sp_slack_kernel(SpMat G, const doubl
     const int i = (int)(e - b * m);
     const double* zb = z + b * n;
     double acc = 0.0;
-    for (int64_t k = rp[i]; k < rp[i + 1]; ++k) acc = __dadd_rn(acc, __dmul_rn(G.rv[k], zb[G.ci[k]]));
-    s[e] = __dadd_rn(acc, -hv[e]);
+    for (int64_t k = rp[i]; k < rp[i + 1]; ++k) acc = add_mul_rn(acc, G.rv[k], zb[G.ci[k]]);
+    s[e] = sub_rn(acc, hv[e]);
   }
 }
 

@@ -723,3 +723,48 @@ def test_plug_point_adjoint_reuses_factors():
         s.solve_system(S.T, r)
     assert s.resolves == 3
     s.close()
+
+
+def _fma_exact(a, b, c):
+    """fma(a, b, c) correctly rounded (exact rational arithmetic)."""
+    from fractions import Fraction
+    return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+
+def test_weakly_active_rows_kept_bit_exact(QPBatch, lu_mode):
+    """Rows with λ_i = 0 whose h_i is G_i·z summed in Julia's sparse `mul!`
+    order (product and sum rounded separately) have s_i = (Gz − h)_i == 0
+    exactly: the reference keeps them (QuadraticProgram.jl:256-282 eliminates
+    nothing; the engine's exact elimination must keep exactly the rows with
+    s ≠ 0).  Such a row makes the KKT column of λ_i all zero, so the reference's
+    `LHS \\ RHS` raises SingularException — and so must the engine.  Round 6
+    found the prepare kernels' s FMA-contracted (HIP's `__dadd_rn(x,
+    __dmul_rn(a, b))` is plain `x + a*b` and fuses): with an FMA, s_i comes out
+    ≈ 1e-17 instead of 0 on these rows, the row is eliminated, and the kept
+    mask and the singular verdict both differ from the reference's."""
+    from diffopt_amd import _lib
+    d = _synthetic(2, 40, 60, 5, 0.3, 20251018)
+    B, n = d["z"].shape
+    m = d["lam"].shape[1]
+    teeth = 0
+    for b in range(B):
+        ina = np.flatnonzero(d["lam"][b] == 0)
+        gz = oqp.gz_minus_h(d["G"][b], d["z"][b], np.zeros(m))   # Julia-order G·z
+        d["h"][b, ina] = gz[ina]
+        for i in ina:   # the FMA form of the same sum: non-zero on most of these rows
+            acc = 0.0
+            for j in range(n):
+                acc = _fma_exact(d["G"][b, i, j], d["z"][b, j], acc)
+            teeth += (acc - gz[i]) != 0.0
+    assert teeth >= 2, "the construction must separate FMA from Julia-order sums"
+    e = QPBatch(B, n, m, 5)
+    e.set(d["Q"], d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+    info = e.factor(singular_ok=True)
+    assert info > 0                                       # singular, as `LHS \\ RHS`
+    kept = e.kept()
+    for b in range(B):
+        np.testing.assert_array_equal(kept[b], _oracle_kept(d, b))   # bit-exact index selection
+        L = oqp.create_LHS_matrix(d["z"][b], d["lam"][b], d["Q"][b], d["G"][b], d["h"][b], d["A"][b])
+        assert not np.all(np.any(L != 0, axis=0))          # the oracle's LHS has a zero column
+    with pytest.raises(_lib.SingularException):
+        e.reverse(d["dl_dz"])

@@ -1,12 +1,16 @@
-# Round 6: the sparse route's and the plug point's tests, QP parity under the
-# split column schedule (DOPT_LSPLIT), then config 2 in all four flat / split
-# combinations (two rounds), and the split form's kernel trace
+# Round 6: the small-path probe inlined / out of line, the
+# sparse route's, plug point's and QP tests (incl. the weakly-active rows),
+# QP / NLP parity under the split column schedule (DOPT_LSPLIT), then config 2
+# in all four flat / split combinations (two rounds) and the split kernel trace
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 J=tools/gpu_job.sh
-TEST_PATHS="tests/test_sparse_gpu.py tests/test_lhs_solve_gpu.py" bash $J test && cp gpurun_out/test.log gpurun_out/test_sparse.log && \
-DOPT_LSPLIT=1 TEST_PATHS="tests/test_qp_gpu.py tests/test_nlp_gpu.py" bash $J test || exit 1
+mkdir -p gpurun_out
+timeout -k 10 60 tools/probebin_r06/small_probe_inl > gpurun_out/probe_inl.txt 2>&1 && \
+timeout -k 10 60 tools/probebin_r06/small_probe_noinl > gpurun_out/probe_noinl.txt 2>&1 && \
+TEST_PATHS="tests/test_sparse_gpu.py tests/test_lhs_solve_gpu.py tests/test_qp_gpu.py tests/test_qp_small_gpu.py" bash $J test && cp gpurun_out/test.log gpurun_out/test_a.log && \
+DOPT_LSPLIT=1 TEST_PATHS="tests/test_qp_gpu.py tests/test_nlp_gpu.py tests/test_multi_rhs_gpu.py" bash $J test || exit 1
 for r in a b; do
  DOPT_LFLAT=0 DOPT_LSPLIT=0 bash $J bench f0s0$r --no-cpu-baseline && \
  DOPT_LFLAT=1 DOPT_LSPLIT=0 bash $J bench f1s0$r --no-cpu-baseline && \
