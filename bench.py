@@ -167,7 +167,9 @@ def run_nlp(args, world, rank, local_rank):
     from diffopt_amd.synthetic import SEED0, nlp_numpy
     st, pt, dp, dx, dd = nlp_numpy(B, n, c, P, SEED0 + args.config + 7919 * rank)
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")
-    eng = NLPBatch(B, n, c, P, device=local_rank)
+    # the deferred factor return (opt-in, dopt_nlp_set_deferred): the inputs are
+    # device tensors that stay untouched across the step, as its contract asks
+    eng = NLPBatch(B, n, c, P, device=local_rank, deferred=True)
     eng.set_structure(st["con_kind"], st["has_low"], st["has_up"], st["sense"])
     eng.set(*[t(pt[k]) for k in NLP_KEYS])
     dp_t, dx_t, dd_t = t(dp), t(dx), t(dd)
@@ -240,6 +242,7 @@ def run_nlp(args, world, rank, local_rank):
                        "problems_per_gpu": B, "n": n, "constraints": c, "params": P, "kkt_rows": rows,
                        "factorised_size_mean": round(float(sizes.mean()), 1),
                        "inertia_corrections": int((corr != 0).sum()),
+                       "deferred_factor": True,
                        "factorisation": {"no_pivot": int((kinds == 1).sum()),
                                          "partial_pivoting": int((kinds == 2).sum())},
                        "parallelism": f"batch-sharded x{world}"},

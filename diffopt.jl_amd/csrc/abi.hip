@@ -851,8 +851,20 @@ int dopt_nlp_factor(dopt_handle* h) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_factor on a non-NLP handle");
     Timer tm;
-    dopt::nlp_factor(*h, true);   // returns with the LU queued: the next call reads the verdicts back
+    dopt::nlp_factor(*h, true);   // queued; the verdicts are read back by nlp_finish
+    // synchronous at return unless the caller opted into the
+    // deferred form (dopt_nlp_set_deferred): then the next call finishes it
+    if (!h->nlp_defer) dopt::nlp_finish(*h);
     h->last_time = tm.s();
+    return 0;
+  });
+}
+
+int dopt_nlp_set_deferred(dopt_handle* h, int32_t on) {
+  return guarded(h, [&]() {
+    if (h->kind != DOPT_KIND_NLP) throw Error(-1, "dopt_nlp_set_deferred: NLP handles only");
+    if (!on && h->nlp_pending) dopt::nlp_finish(*h);   // nothing stays queued past the switch
+    h->nlp_defer = on != 0;
     return 0;
   });
 }

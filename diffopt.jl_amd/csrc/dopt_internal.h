@@ -268,6 +268,7 @@ struct Handle {
   DevBuf nlp_t1, nlp_t2;           // reduced right-hand sides / solutions (max(2, P) × B × nmax)
   DevBuf nlp_msc;                  // per problem: max |M| of the full M (the reduced route's singularity scale)
   bool nstruct = false, nset = false, nfactored = false;
+  bool nlp_defer = false;          // dopt_nlp_set_deferred: dopt_nlp_factor may return with the LU queued
   bool nlp_pending = false;        // dopt_nlp_factor returned with the LU queued; nlp_finish reads the verdicts
   bool nlp_fast_ok = false;        // ... and the pivot check rode on its metadata read-back
   // the pending LU was launched on the guess "every problem reduced and

@@ -76,6 +76,7 @@ SIGNATURES = {
                                               ctypes.c_int32]),
     "dopt_nlp_set": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 12),
     "dopt_nlp_factor": (ctypes.c_int, [_h]),
+    "dopt_nlp_set_deferred": (ctypes.c_int, [_h, ctypes.c_int32]),
     "dopt_nlp_forward": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 3),
     "dopt_nlp_reverse": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 3),
     "dopt_nlp_forward_reverse": (ctypes.c_int, [_h] + [ctypes.c_void_p] * 6),

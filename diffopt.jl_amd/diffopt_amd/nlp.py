@@ -34,7 +34,7 @@ class NLPBatch:
     """Batched NLP KKT sensitivity engine (C-ABI handle wrapper): ``n``
     primal variables, ``c`` NLP constraints, ``P`` parameters per problem."""
 
-    def __init__(self, batch, n, c, P, device=0):
+    def __init__(self, batch, n, c, P, device=0, deferred=False):
         self.lib = _lib.load()
         self.batch, self.n, self.c, self.P = int(batch), int(n), int(c), int(P)
         h = ctypes.c_void_p()
@@ -46,6 +46,9 @@ class NLPBatch:
         self._mem = None
         self._keep = None
         self._layout = None
+        # opt-in: factor() returns with the LU queued (dopt_nlp_set_deferred)
+        if deferred:
+            _lib.check(self.lib.dopt_nlp_set_deferred(self.h, 1), self.h)
 
     def close(self):
         if getattr(self, "h", None):

@@ -329,16 +329,25 @@ int dopt_nlp_set(dopt_handle* h, const double* Hxx, const double* Hxp, const dou
                  const double* yu);
 /* LU of every problem's M with the reference's inertia correction
  * (M + k·1e-6·D, k ≤ 50); a problem whose correction fails gets ∂s = 0, as
- * in the reference (nlp_utilities.jl:436-439).  Returns once the no-pivot LU
- * is queued: the verdicts (fallbacks, corrections) are read back by the next
- * call that needs the factors (forward / reverse / jacobian / kkt_solve /
- * get_corrections / get_system_size), which then overlaps that wait with
- * its own right-hand sides.  On the reduced route the LU is launched without
- * reading the sizes back first, on the guess that every problem is reduced
- * and H symmetric; the next call redoes the factorisation when the guess
- * missed, and the handle stops guessing after one miss.  Until that next
- * call, device-mode inputs must stay unchanged (a fallback re-reads them). */
+ * in the reference (nlp_utilities.jl:436-439).  Synchronous at return by
+ * default: every verdict (fallbacks, corrections, the factorisation of a
+ * missed speculative launch — below) is final when the call returns.  On the
+ * reduced route the LU is launched without reading the sizes back first, on
+ * the guess that every problem is reduced and H symmetric; the call redoes the
+ * factorisation when the guess missed (the handle then stops guessing until the
+ * next dopt_nlp_set_structure). */
 int dopt_nlp_factor(dopt_handle* h);
+/* Opt-in (on = 1): dopt_nlp_factor returns once the LU is QUEUED, and the
+ * next call that needs the factors (forward / reverse / forward_reverse /
+ * jacobian / kkt_solve / get_corrections / get_system_size / get_lu_kind)
+ * reads the verdicts back, overlapping that wait with its own right-hand sides
+ * (config 6: ≈ 3 % per step).  The price: until that next call the handle
+ * still needs its inputs — in device mode they must stay unchanged (a
+ * fallback or a missed speculative launch re-reads them; a change in between
+ * gives undefined results), and an argument error of the factorisation
+ * surfaces from that next call.  Host mode copies the inputs, so only the
+ * error timing differs there.  on = 0 finishes a pending factorisation. */
+int dopt_nlp_set_deferred(dopt_handle* h, int32_t on);
 /* dp[P] → dx[n], ddual[c + nlow + nup] (constraint duals, then the duals of
  * the primal lower and upper bounds in variable order): ∂s·Δp. */
 int dopt_nlp_forward(dopt_handle* h, const double* dp, double* dx, double* ddual);

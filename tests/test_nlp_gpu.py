@@ -444,8 +444,9 @@ def test_forward_reverse_equals_separate_calls(case, lu_mode, monkeypatch):
 
 
 # ---- the speculative LU launch (no metadata read-back before the LU) --------
+@pytest.mark.parametrize("deferred", [False, True], ids=["sync", "deferred"])
 @pytest.mark.parametrize("call", ["forward_reverse", "forward", "reverse", "jacobian"])
-def test_speculative_launch_miss(call):
+def test_speculative_launch_miss(call, deferred):
     """dopt_nlp_factor launches the LU on the guess that every problem is
     reduced and symmetric; a batch breaking it (problem 1 leaves the reduced
     route) is re-factorised from the read-back by the next call, whose right-
@@ -459,6 +460,8 @@ def test_speculative_launch_miss(call):
     j = int(np.flatnonzero(st["has_low"])[0])
     bad["xl"][1, j], bad["yl"][1, j] = bad["x"][1, j], 0.0
     e = engine(st, good, B)
+    if deferred:   # opt-in: factor() returns with the LU queued, the next call finishes it
+        e.lib.dopt_nlp_set_deferred(e.h, 1)
     assert (e.system_size() == n + c).all()
 
     def run(eng):
@@ -473,10 +476,14 @@ def test_speculative_launch_miss(call):
     for _ in range(2):
         e.set(*[bad[k] for k in KEYS])
         e.factor()
+        # read straight after factor (in the deferred form the
+        # finish step must run first — a missed guess changes the kinds / sizes)
+        kinds, sizes = e.lu_kind(), e.system_size()
         got = run(e)
         assert e.system_size()[1] == e.layout()["rows"] and e.system_size()[0] == n + c
         ref = engine(st, bad, B)
-        ref.system_size()
+        np.testing.assert_array_equal(kinds, ref.lu_kind())
+        np.testing.assert_array_equal(sizes, ref.system_size())
         want = run(ref)
         for g, w in zip(got, want):
             np.testing.assert_allclose(g, w, rtol=0, atol=1e-12 * max(1.0, np.abs(w).max()))
@@ -489,3 +496,44 @@ def test_speculative_launch_miss(call):
     e.factor()
     check_against_oracle(e, st, good, dp, dx, dd, range(B))
     e.close()
+
+
+def test_factor_contract_sync_and_deferred():
+    """dopt_nlp_factor is synchronous at return by
+    default (every verdict final, nothing queued — including the
+    re-factorisation of a missed speculative launch); the deferred return is
+    opt-in (dopt_nlp_set_deferred), documented in the header and INTEGRATION.md
+    as needing the device-mode inputs unchanged until the next call.  Problem 1
+    misses the speculative launch (it leaves the reduced route).  Both forms,
+    inputs left alone, give bit-identical outputs, corrections and kinds, and
+    match a fresh engine; switching the deferred form off finishes a pending
+    factorisation."""
+    import torch
+    from diffopt_amd.nlp import NLPBatch
+    from diffopt_amd.synthetic import nlp_numpy
+    B, n, c, P = 4, 30, 18, 4
+    st, pt, dp, dx, dd = nlp_numpy(B, n, c, P, 7401)
+    j = int(np.flatnonzero(st["has_low"])[0])
+    pt["xl"][1, j], pt["yl"][1, j] = pt["x"][1, j], 0.0
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")
+    outs = {}
+    for deferred in (False, True):
+        e = NLPBatch(B, n, c, P, deferred=deferred)
+        e.set_structure(st["con_kind"], st["has_low"], st["has_up"], st["sense"])
+        dev = {k: t(pt[k]) for k in KEYS}
+        e.set(*[dev[k] for k in KEYS])
+        e.factor()
+        if deferred:   # off again: the pending factorisation is finished by the switch itself
+            assert e.lib.dopt_nlp_set_deferred(e.h, 0) == 0
+            assert e.lib.dopt_nlp_set_deferred(e.h, 1) == 0
+        got = e.forward_reverse(t(dp), t(dx), t(dd))
+        torch.cuda.synchronize()
+        outs[deferred] = [g.cpu().numpy() for g in got] + [e.corrections(), e.lu_kind(), e.system_size()]
+        e.close()
+    for a, b in zip(outs[False], outs[True]):
+        np.testing.assert_array_equal(a, b)
+    ref = engine(st, pt, B)
+    want = ref.forward_reverse(dp, dx, dd)
+    for a, w in zip(outs[False], want):
+        np.testing.assert_allclose(a, w, rtol=0, atol=1e-12 * max(1.0, np.abs(w).max()))
+    ref.close()

@@ -4,7 +4,11 @@
 // the same reduced system, the first differing entries printed, and the
 // kernel's time.
 //   hipcc --offload-arch=gfx950 -O3 -DSM_DUMP tools/probe/small_probe.hip -o small_probe
+#ifdef SM_R05   // the round-5 source (its s = Gz − h through __dadd_rn / __dmul_rn)
+#include "../../diffopt.jl_amd/csrc/_var_qp_small_r05.hip"
+#else
 #include "../../diffopt.jl_amd/csrc/qp_small.hip"
+#endif
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>

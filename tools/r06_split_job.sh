@@ -7,9 +7,10 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 J=tools/gpu_job.sh
 mkdir -p gpurun_out
-timeout -k 10 60 tools/probebin_r06/small_probe_inl > gpurun_out/probe_inl.txt 2>&1 && \
-timeout -k 10 60 tools/probebin_r06/small_probe_noinl > gpurun_out/probe_noinl.txt 2>&1 && \
-TEST_PATHS="tests/test_sparse_gpu.py tests/test_lhs_solve_gpu.py tests/test_qp_gpu.py tests/test_qp_small_gpu.py" bash $J test && cp gpurun_out/test.log gpurun_out/test_a.log && \
+for v in inl noinl r05_inl r05_noinl; do
+  timeout -k 10 60 tools/probebin_r06/small_probe_$v > gpurun_out/probe_$v.txt 2>&1 || exit 1
+done
+TEST_PATHS="tests/test_sparse_gpu.py tests/test_lhs_solve_gpu.py tests/test_qp_gpu.py tests/test_qp_small_gpu.py tests/test_nlp_gpu.py" bash $J test && cp gpurun_out/test.log gpurun_out/test_a.log && \
 DOPT_LSPLIT=1 TEST_PATHS="tests/test_qp_gpu.py tests/test_nlp_gpu.py tests/test_multi_rhs_gpu.py" bash $J test || exit 1
 for r in a b; do
  DOPT_LFLAT=0 DOPT_LSPLIT=0 bash $J bench f0s0$r --no-cpu-baseline && \
