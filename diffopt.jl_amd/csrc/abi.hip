@@ -119,8 +119,6 @@ int dopt_create(dopt_handle** out, int device, int64_t batch, int32_t n, int32_t
     if (const char* e = getenv("DOPT_LU")) h->lu_mode = atoi(e) != 0;
     if (const char* e = getenv("DOPT_SYM")) h->sym_mode = atoi(e) != 0;
     if (const char* e = getenv("DOPT_LEFT")) h->left_mode = atoi(e) != 0;
-    if (const char* e = getenv("DOPT_LFLAT")) h->lflat = atoi(e) != 0;
-    if (const char* e = getenv("DOPT_LSPLIT")) h->lsplit = atoi(e) != 0;
     if (const char* e = getenv("DOPT_NLP_REDUCE")) h->nlp_reduce = atoi(e) != 0;
     if (const char* e = getenv("DOPT_SPLIT_FUSE")) h->split_fuse = atoi(e) != 0;
     if (kind == DOPT_KIND_QP) {
@@ -180,7 +178,7 @@ int dopt_destroy(dopt_handle* h) {
                     &h->x, &h->cone_dev, &h->vp, &h->dpi, &h->cwork, &h->cinfo, &h->cnorm, &h->csplit, &h->krhs, &h->kx,
                     &h->kfull, &h->kamax, &h->nlp_map, &h->nlp_shift, &h->nlp_scale, &h->kls, &h->gk, &h->glist,
                     &h->mws, &h->qsy, &h->psd_eig, &h->psd_app, &h->ukp, &h->nlp_rd, &h->nlp_ri, &h->nlp_t1, &h->nlp_t2,
-                    &h->nlp_msc, &h->pack, &h->tpack, &h->rpack, &h->xacc};
+                    &h->nlp_msc, &h->pack, &h->tpack, &h->rpack};
   for (auto* b : bufs) b->release();
   for (auto& b : h->own_nin) b.release();
   for (auto& b : h->own_in) b.release();

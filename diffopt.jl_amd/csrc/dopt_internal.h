@@ -187,11 +187,6 @@ struct Handle {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_qsym = nullptr, ev_crit = nullptr;
   hipStream_t crit = nullptr;      // high-priority stream of the right-looking LU's critical chain
   int32_t left_mode = 1;           // P-symmetric batches: left-looking LU (env DOPT_LEFT=0: right-looking)
-  int32_t lflat = 1;               // left-looking LU: the column tiles accumulate the diagonal blocks' updates
-                                   // and sweeps (flat chain; env DOPT_LFLAT=0: ldiag restages the strips)
-  int32_t lsplit = 0;              // left-looking LU: tile (J+1, J) on the stream, the column's other tiles on `aux`
-                                   // beside ldiag(J+1) (env DOPT_LSPLIT)
-  DevBuf xacc;                     // ... those accumulators, one 64 × 64 (ten 16 × 16 tiles) per problem and block
   DevBuf ukp;                      // left-looking LU: u_kk / p_k of every finished diagonal block (nmax per problem)
   bool ukp_valid = false;          // the last no-pivot factorisation was left-looking (ukp holds its u_kk / p_k)
   bool u_missing = false;          // ... and stored only L for its P-symmetric problems (U from L on demand)

@@ -1639,32 +1639,6 @@ __device__ __forceinline__ int lc_uoff(int j, int c) { return j * NB64 + (c ^ ((
 // and every output (K's U_ab / L_ba, dinv, the packed inverse, u_kk / p_k,
 // the fused forward sweeps) come from F, by the whole workgroup.
 // ---------------------------------------------------------------------------
-// ---------------------------------------------------------------------------
-// Flat diagonal chain (round 6, default; DOPT_LFLAT=0 restages the strips).
-// Column tile (I, J) also forms T = L(I, J)·D_J·L(I, J)ᵀ — the term block
-// column J contributes to the update of diagonal block I — and adds it to a
-// per-problem accumulator X_I (one tile per (I, J) per launch: no atomics, and
-// the k-order of the sum is the launch order), so nlu_ldiag_kernel reads one
-// 64 × 64 accumulator instead of restaging and multiplying the J row strips
-// L(J, <J) (≈ 10 µs per strip on the chain).  Likewise the fused call's
-// forward sweeps: the tile subtracts L(I, J)·y_J and p_I·L(I, J)·(u/p ∘ c′)_J
-// from block I of the two right-hand sides (y_J, c′_J are final once
-// ldiag(J) ran).  T is symmetric: its ten 16 × 16 tiles (r, c) below are
-// computed from the rows of L(I, J) the waves hold after the TRSM (wave w:
-// rows 16w..16w+15, the A operand straight from the registers), rows c
-// through LDS; stored lane-linear (tile q, register rr, lane: q·256 + rr·64
-// + lane) for one coalesced read per thread in ldiag.
-//   w0: (0,0) (0,1) (0,2)   w1: (1,1) (1,2) (1,3)   w2: (2,2) (2,3)   w3: (3,3) (3,0)
-// ---------------------------------------------------------------------------
-constexpr int XT = 10 * 256;   // doubles per accumulator (problem, diagonal block)
-__host__ __device__ constexpr int xt_slot(int w, int k) { return w < 2 ? 3 * w + k : 6 + 2 * (w - 2) + k; }
-__device__ __forceinline__ int xt_col(int w, int k) { return w == 3 && k == 1 ? 0 : w + k; }
-__device__ __forceinline__ int xt_row(int q) { return q < 6 ? q / 3 : 2 + (q - 6) / 2; }
-__device__ __forceinline__ int xt_colq(int q) { return xt_col(xt_row(q), q < 6 ? q % 3 : (q - 6) % 2); }
-// L(I, J) image for the products (row-major 64 × 64; the column's bits 1..4
-// XOR the row's low four: a half-wave's 32 reads hit 32 distinct bank pairs)
-__device__ __forceinline__ int lx_off(int r, int c) { return r * NB64 + (c ^ ((r & 15) << 1)); }
-
 constexpr int LX = NB64 * SLD;   // the extras past the 64 × SLD image
 static_assert(LX + 5 * 64 + 128 + 2 <= STEP_LDS, "ldl64_core extras must fit 40 KB");
 
@@ -1817,12 +1791,12 @@ __device__ __forceinline__ void ldl64_core(double* buf, double* __restrict__ Kb,
 // The diagonal step of block column J = c0 / 64 for problem b (S: the
 // workgroup's STEP_LDS doubles of LDS); nlu_ldiag_kernel runs it for a batch,
 // nlu_left_all_kernel inside its per-problem loop.
-template <class SRC, bool FLAT>
+template <class SRC>
 __device__ __forceinline__ void ldiag_body(
     double* S, int b, double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm,
     double* __restrict__ dinv, size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv,
     double* __restrict__ ukp, double* __restrict__ w0, double* __restrict__ w1, double* __restrict__ kamax,
-    const double* __restrict__ kls, int n, int m, const SRC& src, const double* __restrict__ xacc, int nbx) {
+    const double* __restrict__ kls, int n, int m, const SRC& src) {
   LD_MARK(0);
   const QPMeta mm = meta[b];
   const int Np = nlu_np(mm);
@@ -1866,7 +1840,7 @@ __device__ __forceinline__ void ldiag_body(
   const int tc2 = wv == 0 ? 1 : 2;                      // column of tile 2 (row 3; w0, w1 only)
   const bool dact = 16 * ra < Wv;                       // wave-uniform: tile 0 inside the block
   const bool bact = Wv > 48 && wv != 2;                 // the row-3 tiles inside the block
-  for (int k0 = 0; k0 < (FLAT ? 0 : c0); k0 += NB64) {
+  for (int k0 = 0; k0 < c0; k0 += NB64) {
     double dk[16];   // D_k, for the A operand
 #pragma unroll
     for (int s = 0; s < 16; ++s) dk[s] = ud[k0 + 4 * s + g];
@@ -1901,17 +1875,9 @@ __device__ __forceinline__ void ldiag_body(
       sweep += sm;
     }
   }
-  if (!FLAT) __syncthreads();   // the staging is consumed: S becomes the diagonal image
+  __syncthreads();   // the staging is consumed: S becomes the diagonal image
   LD_MARK(1);
-  // flat chain: X = the accumulator the column tiles filled (one coalesced
-  // load per thread per 16 × 16 tile, issued with the source loads below)
-  double xv[10];
-  if (FLAT && c0 > 0) {
-    const double* Xa = xacc + ((size_t)b * nbx + (c0 >> 6)) * XT;
-#pragma unroll
-    for (int q = 0; q < 10; ++q) xv[q] = Xa[q * 256 + t];
-  }
-  if (!FLAT && c0 > 0) {   // workgroup-uniform: X's tiles and their mirrors → S
+  if (c0 > 0) {   // workgroup-uniform: X's tiles and their mirrors → S
     auto put = [&](int r, int c, const d4n& x) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
@@ -1940,16 +1906,6 @@ __device__ __forceinline__ void ldiag_body(
   // a compiler-only fence: the loads stay issued here (sunk next to their
   // uses they would wait one by one); it emits no instruction
   asm volatile("" ::: "memory");
-  if (FLAT && c0 > 0) {   // thread t holds register wv of lane (g, l16) of every tile: entry (16r + g + 4wv, 16c + l16)
-#pragma unroll
-    for (int q = 0; q < 10; ++q) {
-      const int r = xt_row(q), c = xt_colq(q);
-      const int i = 16 * r + g + 4 * wv, j = 16 * c + l16;
-      S[i * SLD + j] = xv[q];
-      if (r != c) S[j * SLD + i] = xv[q];
-    }
-    __syncthreads();
-  }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int j = 16 * q + l16;
@@ -1964,7 +1920,7 @@ __device__ __forceinline__ void ldiag_body(
       S[i * SLD + j] = av[q][rr] - x * pj[q];
     }
   }
-  if (!FLAT && w0b && t < 2 * NB64) {   // block J of b / c minus the finished blocks' contributions (flat: lcol did)
+  if (w0b && t < 2 * NB64) {   // block J of b / c minus the finished blocks' contributions
     const int j = t & 63;
     if (j < Wv && c0 + j < mm.nsys) {
       if (t < NB64) w0b[c0 + j] -= sweep;
@@ -1979,15 +1935,15 @@ __device__ __forceinline__ void ldiag_body(
              Np, mm.nsys, binv + (size_t)b * BSTR, w0b, w1b, bound, ps, ud);
 }
 
-template <class SRC, bool FLAT>
+template <class SRC>
 __global__ __launch_bounds__(PNT) __attribute__((amdgpu_waves_per_eu(4))) void nlu_ldiag_kernel(
     double* __restrict__ K, int ld, int nmax, int32_t* __restrict__ perm, double* __restrict__ dinv,
     size_t dstride, QPMeta* __restrict__ meta, int c0, double* __restrict__ binv, double* __restrict__ ukp,
     double* __restrict__ w0, double* __restrict__ w1, double* __restrict__ kamax, const double* __restrict__ kls,
-    int n, int m, SRC src, int b0, const double* __restrict__ xacc, int nbx) {
+    int n, int m, SRC src, int b0) {
   __shared__ double S[STEP_LDS];
-  ldiag_body<SRC, FLAT>(S, b0 + (int)blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, c0, binv, ukp, w0, w1,
-                        kamax, kls, n, m, src, xacc, nbx);
+  ldiag_body<SRC>(S, b0 + (int)blockIdx.x, K, ld, nmax, perm, dinv, dstride, meta, c0, binv, ukp, w0, w1,
+                       kamax, kls, n, m, src);
 }
 
 // ---------------------------------------------------------------------------
@@ -2024,11 +1980,9 @@ constexpr int LC_DS = 2 * LC_STAGE;      // D slices of the two buffers (128 dou
 constexpr int LC_P = LC_DS + 256;        // p_j of block J
 constexpr int LC_UD = LC_P + NB64;       // u_jj / p_j of block J
 constexpr int LC_CODES = LC_UD + NB64;   // NLP: the tile's 128 index codes (int)
-constexpr int LC_Y = LC_CODES + 64;      // flat form, fused call: y_J and (u/p ∘ c′)_J, the finished sweep blocks
-constexpr int LC_LDS = LC_Y + 2 * NB64;
-static_assert(NB64 * NB64 <= LC_DS, "U_JJ⁻¹'s image (and the flat form's L(I, J) image) reuse the stage buffers");
+constexpr int LC_LDS = LC_CODES + 64;
+static_assert(NB64 * NB64 <= LC_DS, "U_JJ⁻¹'s image reuses the stage buffers");
 static_assert(LC_LDS * 8 <= 40 * 1024, "four workgroups per CU");
-
 
 
 template <class SRC> constexpr bool src_staged() { return false; }   // the tile's sources need its index codes
@@ -2064,16 +2018,15 @@ __device__ __forceinline__ int src_ref_tile(const NSrcB& v, const double* X, int
   return nlp_R_ref_lower(v.s->d, v.s->in, v.s->R, v.b, r, c, tc[ri], tc[64 + ci], p);
 }
 
-template <class SRC, bool FLAT>
+template <class SRC>
 __device__ __forceinline__ void lcol_body(double* X, int b, int it, double* __restrict__ K, int ld, int nmax,
                                           QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
                                           const double* __restrict__ ukp, int cnt,
                                           const double* __restrict__ kamax, const double* __restrict__ kls, int n,
-                                          int m, const SRC& src, double* __restrict__ xacc, int nbx,
-                                          double* __restrict__ w0, double* __restrict__ w1, int it0) {
+                                          int m, const SRC& src) {
   const QPMeta mm = meta[b];
   const int Np = nlu_np(mm);
-  const int r0 = c0 + NB64 + 64 * (it0 + it);   // first row of tile I
+  const int r0 = c0 + NB64 + 64 * it;   // first row of tile I
   if (mm.lu == LU_REJECT || it >= cnt || r0 >= Np) return;   // workgroup-uniform
   const int sw = min(NB64, Np - r0);   // 32 or 64 rows
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
@@ -2148,14 +2101,8 @@ __device__ __forceinline__ void lcol_body(double* X, int b, int it, double* __re
   asm volatile("" ::: "memory");
   const double pv = t < NB64 ? (inp ? rp : 1.0) : rp;   // p_j | u_jj / p_j of block J
   const double pr = inr ? rr_ : 1.0;                     // p_i of this lane's tile row (growth bound)
-  // flat form, fused call: the finished sweep blocks of column J (ldiag(J) wrote them)
-  double* w0b = FLAT && w0 ? w0 + (size_t)b * nmax : nullptr;
-  double* w1b = FLAT && w0 ? w1 + (size_t)b * nmax : nullptr;
-  double yv = 0.0;
-  if (w0b && t < 2 * NB64) yv = t < NB64 ? w0b[c0 + t] : w1b[c0 + t - NB64];
   src_stage_codes(src, sv, X, r0, c0);
   if (t < 2 * NB64) X[LC_P + t] = pv;   // LC_UD = LC_P + 64
-  if (w0b && t < 2 * NB64) X[LC_Y + t] = t < NB64 ? yv : yv * pv;   // y_J | (u/p)_J ∘ c′_J
   d4n acc[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = (d4n){0, 0, 0, 0};
@@ -2205,112 +2152,49 @@ __device__ __forceinline__ void lcol_body(double* X, int b, int it, double* __re
   }
   vm_drain();
   __syncthreads();
-  if (!FLAT && !wact) return;   // no barrier below (the flat form's waves all reach its two)
+  if (!wact) return;   // no barrier below
   // L(I, J)ᵀ block a = Σ_{c ≤ a} U⁻ᵀ(a, c)·Cᵀ(c, w): A operand U⁻¹[j][j'] (j = 16c + 4s + g,
   // j' = 16a + l16; zero below the diagonal), B operand Cᵀ's register s of block c
   d4n lt[4];
+  int over = 0;
+  const double bound = growth_bound(__hip_atomic_load(kamax + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 #pragma unroll
-  for (int a = 0; a < 4; ++a) lt[a] = (d4n){0, 0, 0, 0};
+  for (int a = 0; a < 4; ++a) {
+    lt[a] = (d4n){0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c <= a; ++c)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int j = 16 * c + 4 * s + g, jp = 16 * a + l16;
+        const double u = X[lc_uoff(j, jp)];
+        lt[a] = nmfma(c < a || j <= jp ? u : 0.0, acc[c][s], lt[a]);
+      }
+  }
   const int ri = 16 * wv + l16;
-  if (wact) {
-    int over = 0;
-    const double bound = growth_bound(__hip_atomic_load(kamax + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  double* krow = Kb + (size_t)(r0 + ri) * ld + c0;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
+  for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int c = 0; c <= a; ++c)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int j = 16 * c + 4 * s + g, jp = 16 * a + l16;
-          const double u = X[lc_uoff(j, jp)];
-          lt[a] = nmfma(c < a || j <= jp ? u : 0.0, acc[c][s], lt[a]);
-        }
+    for (int rr = 0; rr < 4; ++rr) {
+      const double l = lt[a][rr], uk = X[LC_UD + 16 * a + g + 4 * rr];
+      krow[16 * a + g + 4 * rr] = l;
+      // |l| ≤ NOPIV_LMAX, and U(J, I)[j'][i] = (u_j'j' / p_j')·l·p_i within the growth bound
+      over |= (int)!(fabs(l) <= NOPIV_LMAX) | (int)!(fabs(uk * l * pr) <= bound);
     }
-    double* krow = Kb + (size_t)(r0 + ri) * ld + c0;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const double l = lt[a][rr], uk = X[LC_UD + 16 * a + g + 4 * rr];
-        krow[16 * a + g + 4 * rr] = l;
-        // |l| ≤ NOPIV_LMAX, and U(J, I)[j'][i] = (u_j'j' / p_j')·l·p_i within the growth bound
-        over |= (int)!(fabs(l) <= NOPIV_LMAX) | (int)!(fabs(uk * l * pr) <= bound);
-      }
-    if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;   // every writer stores the same value
-  }
-  if constexpr (FLAT) {
-    // ---- this column's share of diagonal block I's update and sweeps (the
-    // flat chain, above).  The previous accumulator of block I is loaded
-    // first (none at J = 0), to overlap the image's barrier.
-    double* Xa = xacc + ((size_t)b * nbx + (r0 >> 6)) * XT;
-    const int nq = wv < 2 ? 3 : 2;
-    d4n tq[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      tq[k] = (d4n){0, 0, 0, 0};
-      if (c0 > 0 && k < nq)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) tq[k][rr] = Xa[xt_slot(wv, k) * 256 + rr * 64 + lane];
-    }
-    if (w0b) {   // the sweeps: row ri of L(I, J) against y_J and (u/p ∘ c′)_J (both in LDS)
-      double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int k = 16 * a + 4 * rr + g;
-          s0 = fma(lt[a][rr], X[LC_Y + k], s0);
-          s1 = fma(lt[a][rr], X[LC_Y + NB64 + k], s1);
-        }
-      // the four lanes of row ri (g = 0..3)
-      s0 += __shfl_xor(s0, 16);
-      s1 += __shfl_xor(s1, 16);
-      s0 += __shfl_xor(s0, 32);
-      s1 += __shfl_xor(s1, 32);
-      if (wact && g == 0 && ri < sw && r0 + ri < mm.nsys) {
-        w0b[r0 + ri] -= s0;
-        w1b[r0 + ri] -= pr * s1;
-      }
-    }
-    __syncthreads();   // every wave is past the TRSM: the stage buffers take L(I, J)
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) X[lx_off(ri, 16 * a + 4 * rr + g)] = lt[a][rr];
-    __syncthreads();
-    // tile (wv, c): A = rows 16wv.. of L·D (registers), B = rows 16c.. of L
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      if (k < nq) {   // wave-uniform
-        const int c = xt_col(wv, k);
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int kk = 16 * a + 4 * rr + g;
-            const double bo = c == wv ? lt[a][rr] : X[lx_off(16 * c + l16, kk)];
-            tq[k] = nmfma(lt[a][rr] * X[LC_UD + kk], bo, tq[k]);
-          }
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) Xa[xt_slot(wv, k) * 256 + rr * 64 + lane] = tq[k][rr];
-      }
-    }
-  }
+  if (__any(over) && lane == 0) meta[b].lu = LU_REJECT;   // every writer stores the same value
 }
 
-template <class SRC, bool FLAT>
+template <class SRC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void nlu_lcol_kernel(
     double* __restrict__ K, int ld, int nmax, QPMeta* __restrict__ meta, int c0, const double* __restrict__ binv,
     const double* __restrict__ ukp, int ntile, int total, const double* __restrict__ kamax,
-    const double* __restrict__ kls, int n, int m, SRC src, double* __restrict__ xacc, int nbx,
-    double* __restrict__ w0, double* __restrict__ w1, int it0) {
+    const double* __restrict__ kls, int n, int m, SRC src) {
   __shared__ double X[LC_LDS];   // one LDS object (a second one can make the compiler drain the DMA early)
   const int L = blockIdx.x;
   const int qx = total >> 3, rx = total & 7, xcd = L & 7, slot = L >> 3;
   const int logical = (xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx) + slot;
   const int bl = logical / ntile;
-  lcol_body<SRC, FLAT>(X, bl, logical - bl * ntile, K, ld, nmax, meta, c0, binv, ukp, ntile, kamax, kls, n, m, src,
-                       xacc, nbx, w0, w1, it0);
+  lcol_body<SRC>(X, bl, logical - bl * ntile, K, ld, nmax, meta, c0, binv, ukp, ntile, kamax, kls, n, m, src);
 }
 
 // U of the left-looking route's P-symmetric factors, materialised from L for
@@ -2380,63 +2264,18 @@ static void left_lu(Handle& h, const SRC& src, double* dinv, double* w0, double*
   double* ukp = h.ukp.as<double>();
   hipStream_t S = h.stream;
   auto binv_of = [&](int c0) { return h.binv.as<double>() + (size_t)((c0 / NB64) & 1) * B * BSTR; };
-  // flat chain: one accumulator per (problem, diagonal block); block 0's slot unused
-  const int nbx = (npmax + NB64 - 1) / NB64;
-  const bool flat = h.lflat && nbx > 1;
-  double* xacc = nullptr;
-  if (flat) {
-    h.xacc.ensure((size_t)B * nbx * XT * sizeof(double));
-    xacc = h.xacc.as<double>();
-  }
-  // split schedule (DOPT_LSPLIT): the column's subdiagonal tile (J+1, J) —
-  // all that ldiag(J+1) waits for — on the handle's stream, the column's other
-  // tiles on `aux`, beside ldiag(J+1); tile (J+2, J+1) then waits for them
-  const bool split = h.lsplit != 0;
-  if (split) ensure_aux(h);
-  hipStream_t T = split ? h.aux : S;
-  bool pending = false;   // T holds column tiles the next subdiagonal tile needs
-  auto lcol = [&](hipStream_t st, int c0, double* bv, int it0, int ntile) {
-    const long long tot = (long long)ntile * B;
-    if (tot > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
-    if (flat)
-      hipLaunchKernelGGL((nlu_lcol_kernel<SRC, true>), dim3((unsigned)tot), dim3(256), 0, st, K, h.ld, h.nmax, meta,
-                         c0, bv, ukp, ntile, (int)tot, kamax, kls, h.n, h.m, src, xacc, nbx, w0, w1, it0);
-    else
-      hipLaunchKernelGGL((nlu_lcol_kernel<SRC, false>), dim3((unsigned)tot), dim3(256), 0, st, K, h.ld, h.nmax, meta,
-                         c0, bv, ukp, ntile, (int)tot, kamax, kls, h.n, h.m, src, xacc, nbx, w0, w1, it0);
-    DOPT_CHECK_HIP(hipGetLastError());
-  };
   for (int c0 = 0; c0 < npmax; c0 += NB64) {
     double* bv = binv_of(c0);
-    if (flat)
-      hipLaunchKernelGGL((nlu_ldiag_kernel<SRC, true>), dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv,
-                         dstride, meta, c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src, 0, xacc, nbx);
-    else
-      hipLaunchKernelGGL((nlu_ldiag_kernel<SRC, false>), dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv,
-                         dstride, meta, c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src, 0, xacc, nbx);
+    hipLaunchKernelGGL((nlu_ldiag_kernel<SRC>), dim3(B), dim3(PNT), 0, S, K, h.ld, h.nmax, perm, dinv, dstride, meta,
+                       c0, bv, ukp, w0, w1, kamax, kls, h.n, h.m, src, 0);
     DOPT_CHECK_HIP(hipGetLastError());
     const int ntile = (npmax - c0 - NB64 + 63) / 64;
     if (ntile <= 0) break;
-    if (!split) {
-      lcol(S, c0, bv, 0, ntile);
-      continue;
-    }
-    if (pending) {   // the previous column's other tiles (tile (J+1, J) stages their rows)
-      DOPT_CHECK_HIP(hipEventRecord(h.ev_join, T));
-      DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_join, 0));
-      pending = false;
-    }
-    if (ntile > 1) {   // T: after ldiag(J) (and, in order, its own earlier tiles)
-      DOPT_CHECK_HIP(hipEventRecord(h.ev_fork, S));
-      DOPT_CHECK_HIP(hipStreamWaitEvent(T, h.ev_fork, 0));
-      lcol(T, c0, bv, 1, ntile - 1);
-      pending = true;
-    }
-    lcol(S, c0, bv, 0, 1);
-  }
-  if (pending) {
-    DOPT_CHECK_HIP(hipEventRecord(h.ev_join, T));
-    DOPT_CHECK_HIP(hipStreamWaitEvent(S, h.ev_join, 0));
+    const long long tot = (long long)ntile * B;
+    if (tot > 0x7fffffffLL) throw Error(-1, "no-pivot LU: grid too large");
+    hipLaunchKernelGGL((nlu_lcol_kernel<SRC>), dim3((unsigned)tot), dim3(256), 0, S, K, h.ld, h.nmax, meta, c0, bv,
+                       ukp, ntile, (int)tot, kamax, kls, h.n, h.m, src);
+    DOPT_CHECK_HIP(hipGetLastError());
   }
 }
 
