@@ -225,7 +225,12 @@ int dopt_set_memory(dopt_handle* h, int32_t mem) {
 
 int dopt_set_sparse(dopt_handle* h, int32_t on) {
   return guarded(h, [&]() {
-    if (h->kind != DOPT_KIND_QP) throw Error(-1, "dopt_set_sparse: QP handles only");
+    if (h->kind != DOPT_KIND_QP && h->kind != DOPT_KIND_CONIC) throw Error(-1, "dopt_set_sparse: QP and conic handles only");
+    if (h->kind == DOPT_KIND_CONIC) {   // A_moi kept sparse by dopt_conic_set_csc (the persistent LSQR on it)
+      h->sparse = on != 0;
+      h->cset = h->cfactored = false;
+      return 0;
+    }
     if (!on && (int64_t)h->n + h->m + h->p > dopt::DENSE_QP_MAX)
       throw Error(-1, "dopt_set_sparse: n + m + p > 8192 has only the sparse route");
     h->sparse = on != 0;
@@ -1267,6 +1272,7 @@ int dopt_conic_set(dopt_handle* h, const double* A, const double* b, const doubl
                    const int32_t* cone_desc, int32_t ncones) {
   return guarded(h, [&]() {
     if (h->kind != DOPT_KIND_CONIC) throw Error(-1, "dopt_conic_set on a non-conic handle");
+    if (h->sparse) throw Error(-1, "dopt_conic_set: a sparse-route handle takes the MOI matrix form (dopt_conic_set_csc)");
     if (!A) throw Error(-1, "A, b, c, x, s, y are required");
     conic_set_common(h, stage_in(*h, h->own_cin[0], A, (size_t)h->batch * h->m * h->n), b, c, x, s, y,
                      cone_desc, ncones);
@@ -1288,6 +1294,20 @@ int dopt_conic_set_csc(dopt_handle* h, const int64_t* A_colptr, const int64_t* A
     const int64_t* cp = stage_in_i64(*h, h->csc_in[0], A_colptr, B * (n + 1));
     const int64_t* rv = stage_in_i64(*h, h->csc_in[1], A_rowval, (size_t)A_nnz);
     const double* nz = stage_in(*h, h->csc_in_val[0], A_nzval, (size_t)A_nnz);
+    if (h->sparse) {   // A_moi kept sparse: CSC + its CSR copy (sparse.hip), no dense A
+      for (int k = 0; k < ncones && cone_desc; ++k)
+        if (cone_desc[2 * k] == DOPT_CONE_PSD_TRI && cone_desc[2 * k + 1] > 64 * 65 / 2)
+          throw Error(-1, "sparse conic route: PSD cones up to side 64 (their Dπ apply runs in LDS)");
+      h->cset = h->cfactored = false;
+      if (m) dopt::sp_stage(*h, 0, cp, rv ? rv : cp, nz, A_nnz, (int)m, h->csc_err.as<int>());
+      int herr = 0;
+      DOPT_CHECK_HIP(hipMemcpyAsync(&herr, h->csc_err.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+      if (herr) throw Error(-1, (herr & 1) ? "CSC colptr is not monotone / out of range"
+                                           : "CSC rowval out of range");
+      conic_set_common(h, nullptr, b, c, x, s, y, cone_desc, ncones);
+      return 0;
+    }
     DevBuf& d = h->own_cin[0];
     d.ensure(std::max<size_t>(B * m * n, 1) * sizeof(double));
     if (m) dopt::csc_to_dense(*h, cp, rv ? rv : cp, nz ? nz : d.as<double>(), A_nnz, (int)m, (int)n,

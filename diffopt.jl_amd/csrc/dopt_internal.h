@@ -417,6 +417,9 @@ void sp_set_csc(Handle& h, const int64_t* Qcp, const int64_t* Qrv, const double*
                 const int64_t* Gcp, const int64_t* Grv, const double* Gnz, int64_t Gnnz, const int64_t* Acp,
                 const int64_t* Arv, const double* Anz, int64_t Annz, int* err);
 void sp_factor(Handle& h);
+// one CSC matrix (rows × n) into h.sp[slot]: converted, validated, CSR copy built (the conic route's A_moi: slot 0)
+void sp_stage(Handle& h, int slot, const int64_t* colptr, const int64_t* rowval, const double* nzval, int64_t nnz,
+              int rows, int* err);
 void sp_reverse(Handle& h, const double* dl_dz, double* out);
 void sp_forward(Handle& h, const FwdTangents& T, double* out);
 void sp_forward_reverse(Handle& h, const double* dl_dz, const FwdTangents& T, double* out_rev, double* out_fwd);

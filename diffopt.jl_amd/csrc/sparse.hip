@@ -431,7 +431,7 @@ int grid1(int64_t work, int tpb) { return (int)std::max<int64_t>(1, std::min<int
 // ---------------------------------------------------------------------------
 // One matrix (slot 0: G, 1: A) of dopt_qp_set_csc: convert, validate, build
 // the CSR copy.  `err` collects the error bits on the device.
-static void sp_stage(Handle& h, int slot, const int64_t* colptr, const int64_t* rowval, const double* nzval,
+void sp_stage(Handle& h, int slot, const int64_t* colptr, const int64_t* rowval, const double* nzval,
                      int64_t nnz, int rows, int* err) {
   const int B = (int)h.batch, n = h.n;
   SpStore& st = h.sp[slot];

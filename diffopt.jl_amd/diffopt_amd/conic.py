@@ -25,7 +25,7 @@ ZEROS, NONNEG, NONPOS, SOC, PSD = (_lib.CONE_ZEROS, _lib.CONE_NONNEG, _lib.CONE_
 
 
 class ConicBatch:
-    def __init__(self, batch, n, cones, device=0):
+    def __init__(self, batch, n, cones, device=0, sparse=False):
         self.lib = _lib.load()
         self.cones = [(int(c), int(d)) for c, d in cones]
         self.batch, self.n = int(batch), int(n)
@@ -38,6 +38,10 @@ class ConicBatch:
         self.h = h
         self._mem = None
         self._keep = None
+        # the sparse route (dopt_set_sparse): set_csc keeps A_moi sparse, LSQR matrix-free on it
+        self.sparse = bool(sparse)
+        if sparse:
+            _lib.check(self.lib.dopt_set_sparse(self.h, 1), self.h)
 
     def close(self):
         if getattr(self, "h", None):

@@ -234,8 +234,24 @@ def nlp_numpy(batch, n, c, P, seed, frac_geq=0.4, frac_leq=0.3, frac_low=0.5, fr
         rng.standard_normal((batch, nd))
 
 
+def _sparse_wellcond(rng, m, n, k):
+    """A dense m × n array with ≈ k non-zeros per row and singular values
+    O(1): the rows of I + 0.3·R/√k (R: k N(0,1) entries per row) for min(m, n)
+    of them, k random N(0,1)/√k entries for the rest, rows permuted."""
+    import scipy.sparse as sp
+    q = min(m, n)
+    rows = np.repeat(np.arange(q), k)
+    W = sp.identity(n, format="csr")[:q] + sp.csr_matrix(
+        (0.3 * rng.standard_normal(q * k) / math.sqrt(k), (rows, rng.integers(0, n, size=q * k))), shape=(q, n))
+    if m > q:
+        ri = np.repeat(np.arange(m - q), k)
+        W = sp.vstack([W, sp.csr_matrix((rng.standard_normal((m - q) * k) / math.sqrt(k),
+                                         (ri, rng.integers(0, n, size=(m - q) * k))), shape=(m - q, n))])
+    return W.tocsr()[rng.permutation(m)].toarray()
+
+
 def conic_numpy_wellcond(batch, n, cones, seed, f_interior=0.25, f_dual_interior=0.25, sigma=(1.0, 2.0),
-                         pair_norm=0.25):
+                         pair_norm=0.25, sparse_k=None):
     """The converging variant of a conic shape: the same
     cone list, but an instance family on which the reference's LSQR converges
     (istop 1–2) well inside maxiter, so parity can be held to 1e-6 on every
@@ -313,11 +329,14 @@ def conic_numpy_wellcond(batch, n, cones, seed, f_interior=0.25, f_dual_interior
             else:
                 raise ValueError("conic_numpy_wellcond: cone code %d not generated" % code)
             o += dim
-        k = min(m, n)
-        U, _ = np.linalg.qr(rng.standard_normal((m, m)))
-        V, _ = np.linalg.qr(rng.standard_normal((n, n)))
-        sv = rng.uniform(sigma[0], sigma[1], k)
-        A = (U[:, :k] * sv) @ V[:, :k].T
+        if sparse_k:   # the sparse route's family: k entries per row, well conditioned
+            A = _sparse_wellcond(rng, m, n, sparse_k)
+        else:
+            k = min(m, n)
+            U, _ = np.linalg.qr(rng.standard_normal((m, m)))
+            V, _ = np.linalg.qr(rng.standard_normal((n, n)))
+            sv = rng.uniform(sigma[0], sigma[1], k)
+            A = (U[:, :k] * sv) @ V[:, :k].T
         x = rng.standard_normal(n) / math.sqrt(n)
         b = s - A @ x
         c = A.T @ (wts * y)

@@ -89,7 +89,12 @@ int dopt_set_memory(dopt_handle* h, int32_t mem);
 int dopt_qp_set(dopt_handle* h, const double* Q, const double* G,
                 const double* hvec, const double* A, const double* z,
                 const double* lam, const double* nu);
-/* Sparse QP route (sparse.hip; on = 1).  The MOI matrix form stays sparse, as
+/* Sparse route (sparse.hip; on = 1).  CONIC handles: dopt_conic_set_csc keeps
+ * A_moi as CSC plus a CSR copy (no dense m×n A) and every LSQR run applies M
+ * matrix-free from them (ConicProgram.jl:243-247, :323, :372), one workgroup per
+ * problem; PSD cones up to side 64; dopt_conic_set (dense) is refused; dense
+ * tangents / dA outputs stay optional dense arrays (NULL = skip).
+ * QP handles (the sparse QP route).  The MOI matrix form stays sparse, as
  * in the reference (`_gradient_cache` keeps SparseMatrixCSC,
  * QuadraticProgram.jl:182-213): dopt_qp_set_csc keeps G and A as CSC plus a
  * CSR copy built on the device, and every solve is `lsqr(LHS, RHS)` /

@@ -179,3 +179,103 @@ def test_sparse_route_refusals():
     G.indices[0] = m + 5
     with pytest.raises(_lib.EngineError, match="rowval"):
         e.set_csc([sp.csc_matrix((n, n))], [G], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+
+
+# ---------------------------------------------------------------------------
+# The conic back-end on the sparse route: A_moi kept sparse (dopt_set_sparse on
+# a conic handle + dopt_conic_set_csc), LSQR on the matrix-free M
+# (ConicProgram.jl:243-247, :323, :372) from its CSC / CSR arrays.
+# ---------------------------------------------------------------------------
+def _conic_run(d, cones, sparse, B):
+    import scipy.sparse as sp
+    from diffopt_amd.conic import ConicBatch
+    n = d["x"].shape[1]
+    e = ConicBatch(B, n, cones, sparse=sparse)
+    if sparse:
+        e.set_csc([sp.csc_matrix(a) for a in d["A"]], d["b"], d["c"], d["x"], d["s"], d["y"])
+    else:
+        e.set(d["A"], d["b"], d["c"], d["x"], d["s"], d["y"])
+    r = e.forward_reverse(d["dx"], d["dA"], d["db"], d["dc"])
+    st = e.lsqr_stats()
+    e.close()
+    return r, st
+
+
+def _conic_vs_oracle(d, cones, B, res, st):
+    from oracle import conic as ocn
+    from test_conic_gpu import _errors, _oracle_outputs
+    (out, fdx), (g, dA, db, dc) = res
+    worst = 0.0
+    for b in range(B):
+        cache = ocn.Cache(d["A"][b], d["b"][b], d["c"][b], d["x"][b], d["s"][b], d["y"][b], cones)
+        ref = _oracle_outputs(cache, d["dA"][b], d["db"][b], d["dc"][b], d["dx"][b])
+        fi, ri = ref["info"]
+        assert fi[1] in (1, 2) and ri[1] in (1, 2), (b, fi, ri)
+        assert st["fwd_istop"][b] in (1, 2) and st["istop"][b] in (1, 2), st
+        err = _errors(dict(fwd=out[b], dx=fdx[b], g=g[b], dA=dA[b], db=db[b], dc=dc[b]), ref, cache)
+        worst = max(worst, max(err.values()))
+    assert worst <= RTOL, worst
+    return worst
+
+
+CONIC_ALL5 = [("m69", 4, 60, [(0, 2), (1, 30), (2, 20), (3, 8), (4, 6), (4, 3)], 42),
+              ("m87", 4, 80, [(0, 5), (1, 20), (2, 10), (3, 10), (3, 6), (4, 15), (4, 21)], 41)]
+
+
+@pytest.mark.parametrize("shape", CONIC_ALL5, ids=[s[0] for s in CONIC_ALL5])
+def test_sparse_conic_all_cone_codes_vs_oracle(shape):
+    """Every cone code on the converging family (the dense route's
+    test_all_cone_codes_converging shapes), A_moi through the sparse route:
+    every output at 1e-6 with no relaxed bar, LSQR converged as the oracle's;
+    and equal to the dense persistent route's to 1e-9 (same LSQR, only the
+    products' summation order differs)."""
+    from diffopt_amd.synthetic import conic_numpy_wellcond
+    _, B, n, cones, seed = shape
+    d = conic_numpy_wellcond(B, n, cones, seed, pair_norm=1.0)
+    res, st = _conic_run(d, cones, True, B)
+    _conic_vs_oracle(d, cones, B, res, st)
+    import os
+    old = os.environ.get("DOPT_CONIC_SPLIT")
+    os.environ["DOPT_CONIC_SPLIT"] = "0"
+    try:
+        dres, _ = _conic_run(d, cones, False, B)
+    finally:
+        if old is None:
+            del os.environ["DOPT_CONIC_SPLIT"]
+        else:
+            os.environ["DOPT_CONIC_SPLIT"] = old
+    for a, b in zip(res[0] + res[1], dres[0] + dres[1]):
+        assert relfro(a, b) <= 1e-9
+
+
+def test_sparse_conic_sparse_pattern():
+    """A genuinely sparse A_moi (≈ 5 entries per row, m = 892 ≤ n = 900 — the
+    converging side of this family; every cone code): the sparse route against
+    the oracle (dense A in the oracle) at 1e-6, LSQR converged as the oracle's."""
+    from diffopt_amd.synthetic import conic_numpy_wellcond
+    cones = [(0, 10), (3, 20)] * 20 + [(1, 200)] + [(4, 21)] * 2 + [(2, 50)]
+    n = 900
+    d = conic_numpy_wellcond(2, n, cones, 77, pair_norm=1.0, sparse_k=5)
+    assert (d["A"] != 0).mean() < 0.02
+    res, st = _conic_run(d, cones, True, 2)
+    _conic_vs_oracle(d, cones, 2, res, st)
+
+
+def test_sparse_conic_refusals():
+    from diffopt_amd import _lib
+    from diffopt_amd.conic import ConicBatch
+    from diffopt_amd.synthetic import conic_numpy_wellcond
+    cones = [(3, 5), (1, 5)]
+    d = conic_numpy_wellcond(1, 8, cones, 5)
+    e = ConicBatch(1, 8, cones, sparse=True)
+    with pytest.raises(_lib.EngineError, match="dopt_conic_set_csc"):
+        e.set(d["A"], d["b"], d["c"], d["x"], d["s"], d["y"])
+    e.close()
+    big = [(4, 66 * 67 // 2)]
+    e = ConicBatch(1, 8, big, sparse=True)
+    import scipy.sparse as sp
+    m = big[0][1]
+    with pytest.raises(_lib.EngineError, match="side 64"):
+        e.set_csc(sp.csc_matrix((m, 8)), np.zeros((1, m)), np.zeros((1, 8)), np.zeros((1, 8)), np.zeros((1, m)),
+                  np.zeros((1, m)))
+    e.close()
