@@ -47,6 +47,13 @@ CONIC_CFG = {4: dict(batch=512), 5: dict(batch=16)}
 # about 600 rows
 NLP_CFG = {6: dict(batch=1024, n=200, c=100, P=20)}
 NLP_KEYS = ["Hxx", "Hxp", "Jx", "Jp", "x", "cval", "crhs", "y", "xl", "xu", "yl", "yu"]
+# the sparse route (sparse.hip, §8 beyond BASELINE — VERDICT r05 missing 2;
+# no published number): 7 — sparse LPs (Q = 0, the reference's LSQR branch)
+# above the dense route's n + m + p <= 8192 cap, ≈ 5 entries per row; 8 —
+# sparse conic programs (A_moi kept sparse, every cone code, m <= n)
+SPARSE_CFG = {7: dict(batch=256, n=4000, p=100, m_extra=1000, k=5),
+              8: dict(batch=256, n=3000, k=5,
+                      cones=[(0, 10), (3, 20)] * 50 + [(1, 1000)] + [(4, 21)] * 4 + [(2, 216)])}
 
 
 def host_cores():
@@ -473,6 +480,135 @@ def run_conic(args, world, rank, local_rank):
 
 
 
+def _sparse_cpu(cfg_id, seconds):
+    """CPU baseline of the sparse configs: the oracle's restatement (scipy CSC
+    LHS / matrix-free M + the IterativeSolvers LSQR restatement) on one core,
+    problems of the same generator until ≈ `seconds` have passed."""
+    import numpy as np
+    from diffopt_amd import synthetic as syn
+    from oracle import qp as oqp
+    c = SPARSE_CFG[cfg_id]
+    t0, done = time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds or done == 0:
+        if cfg_id == 7:
+            d = syn.lp_sparse_numpy(1, c["n"], c["p"], c["m_extra"], c["k"], 9000 + done)
+            oqp.lp_sparse_differentiate(d["G"][0], d["h"][0], d["A"][0], d["z"][0], d["lam"][0], d["nu"][0],
+                                        d["dl_dz"][0], d["dq"][0], d["dh"][0], d["db"][0])
+        else:
+            from oracle import conic as ocn
+            d = syn.conic_numpy_wellcond(1, c["n"], c["cones"], 9000 + done, pair_norm=1.0, sparse_k=c["k"])
+            cache = ocn.Cache(d["A"][0], d["b"][0], d["c"][0], d["x"][0], d["s"][0], d["y"][0], c["cones"])
+            ocn.forward_differentiate(cache, None, d["db"][0], d["dc"][0])
+            ocn.reverse_differentiate(cache, d["dx"][0])
+        done += 1
+    el = time.perf_counter() - t0
+    return dict(value=round(done / el, 3), unit="solves/s", cores=1, kind="port",
+                sample=f"{done} problems of the config's generator, one core, {el:.1f} s")
+
+
+def run_sparse(args, world, rank, local_rank):
+    """Configs 7 / 8: the sparse route (sparse.hip; conic.hip's sparse LSQR).
+    One step = forward + reverse of every problem, LSQR on the matrix-free KKT
+    LHS / M from the CSC and CSR copies.  Roofline: HBM, on the algorithmic
+    bytes of the LSQR iterations actually run (the entries once per product
+    role, index + value, the N-vectors) — DESIGN.md §4."""
+    import numpy as np
+    import torch
+    c = SPARSE_CFG[args.config]
+    B = args.batch or c["batch"]
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = _sparse_cpu(args.config, min(args.cpu_seconds, 20.0))
+    torch.cuda.set_device(local_rank)
+    from diffopt_amd import synthetic as syn
+    seed = SEED0_SPARSE + args.config + 7919 * rank
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")
+    if args.config == 7:
+        from diffopt_amd.qp import QPBatch
+        import scipy.sparse as sp
+        n, p = c["n"], c["p"]
+        d = syn.lp_sparse_numpy(B, n, p, c["m_extra"], c["k"], seed)
+        m = d["lam"].shape[1]
+        N = n + m + p
+        eng = QPBatch(B, n, m, p, device=local_rank)
+        eng.set_csc([sp.csc_matrix((n, n))] * B, d["G"], d["h"], d["A"], d["z"], d["lam"], d["nu"])
+        nnz = float(sum(g.nnz for g in d["G"]) + sum(a.nnz for a in d["A"])) / B
+        dl, dq, dh, db = t(d["dl_dz"]), t(d["dq"]), t(d["dh"]), t(d["db"])
+        step = lambda: eng.forward_reverse(dl, dq=dq, dh=dh, db=db)
+        phase = "qp_lsqr"
+        # per LSQR iteration: two products, each reading every entry of G and A
+        # in both of its LHS roles (CSC for the z rows, CSR for the λ / ν rows:
+        # 12 B index + value), s and λ, the operand and result vectors; then
+        # the LSQR vector updates (≈ 16 N-vector passes)
+        b_it = 2.0 * (12.0 * 2.0 * nnz + 16.0 * m + 16.0 * N) + 8.0 * 16.0 * N
+        workload = (f"config 7: sparse LP batch (Q = 0, LSQR branch) above the dense cap, n={n}, m={m}, p={p}, "
+                    f"~{c['k']} entries per row")
+    else:
+        from diffopt_amd.conic import ConicBatch
+        n, cones = c["n"], c["cones"]
+        d = syn.conic_numpy_wellcond(B, n, cones, seed, pair_norm=1.0, sparse_k=c["k"], sparse_out=True)
+        m = sum(dim for _, dim in cones)
+        N = n + m + 1
+        eng = ConicBatch(B, n, cones, device=local_rank, sparse=True)
+        eng.set_csc(d["A"], d["b"], d["c"], d["x"], d["s"], d["y"])
+        nnz = float(sum(a.nnz for a in d["A"])) / B
+        dx, db, dc = t(d["dx"]), t(d["db"]), t(d["dc"])
+        step = lambda: eng.forward_reverse(dx, db=db, dc=dc, want_dA=False)
+        phase = "conic_lsqr"
+        plen = 0
+        for code, dim in cones:
+            if code in (1, 2):
+                plen += dim
+            elif code == 3:
+                plen += 4
+            elif code == 4:
+                dd = int((math.isqrt(8 * dim + 1) - 1) // 2)
+                plen += 2 * dd * dd + 2
+        # two M / Mᵀ applies per iteration, each reading A_moi's entries as CSR
+        # (A·) and as CSC (Aᵀ·), plus Dπ's parameters and the N-vectors
+        b_it = 48.0 * nnz + 8.0 * (plen + 4 * (n + m))
+        workload = f"config 8: sparse conic batch (A_moi kept sparse, every cone code), n={n}, m={m}, ~{c['k']} per row"
+    del d
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if args.config == 7:
+        st = eng.lsqr_stats()
+        it_f, it_r = st[:, 1, 1].astype(np.float64), st[:, 0, 1].astype(np.float64)
+    else:
+        st = eng.lsqr_stats()
+        it_f, it_r = st["fwd_iterations"].astype(np.float64), st["iterations"].astype(np.float64)
+    eng.phase_times()
+    eng.set_profiling(True, phases=[phase])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    eng.set_profiling(False)
+    ms_tot, cnt = eng.phase_times()[phase]
+    if rank == 0:
+        avg_s = ms_tot / cnt / 1e3
+        per_step = b_it * float((it_f + it_r).sum())
+        achieved = per_step / (ms_tot / 1e3 / args.steps) / 1e9
+        roof = dict(bound="hbm", achieved=round(achieved, 1), peak=PEAK_HBM_GBS, unit="GB/s",
+                    frac=round(achieved / PEAK_HBM_GBS, 4), traffic=None, kernel=phase,
+                    avg_launch_ms=round(avg_s * 1e3, 4), bytes_per_iteration=b_it, nnz_per_problem=nnz,
+                    lsqr_iterations_mean={"forward": float(it_f.mean()), "reverse": float(it_r.mean())})
+        print(json.dumps({
+            "metric": "KKT sensitivity solves/sec (fwd+rev), sparse route",
+            "value": round(world * B * args.steps / elapsed, 3), "unit": "solves/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded, diffopt_amd.synthetic: lp_sparse_numpy / conic_numpy_wellcond sparse_k)",
+            "config": {"workload": workload, "problems_per_gpu": B, "N": N, "parallelism": f"batch-sharded x{world}"},
+            "roofline": roof, "cpu_baseline": cpu}), flush=True)
+
+
+SEED0_SPARSE = 20250307
+
+
 def _phase_breakdown(eng, step, nsteps, drain=None):
     """Per-phase GPU ms per step from an untimed pass with every phase's HIP
     events on, and the dominant phase.  The timed region then records events
@@ -547,7 +683,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=None, choices=sorted(QP_CFG) + sorted(CONIC_CFG) + sorted(NLP_CFG),
+    ap.add_argument("--config", type=int, default=None,
+                    choices=sorted(QP_CFG) + sorted(CONIC_CFG) + sorted(NLP_CFG) + sorted(SPARSE_CFG),
                     help="default: 2 at N = 1, 3 (the north_star headline) under torchrun")
     ap.add_argument("--lam-eps", type=float, default=0.0,
                     help="QP: inactive rows get λ = LAM_EPS instead of 0 (no exact elimination)")
@@ -575,6 +712,8 @@ def main():
         return run_conic(args, world, rank, local_rank)
     if args.config in NLP_CFG:
         return run_nlp(args, world, rank, local_rank)
+    if args.config in SPARSE_CFG:
+        return run_sparse(args, world, rank, local_rank)
     cfg = dict(QP_CFG[args.config])
     cfg["lam_eps"] = args.lam_eps
     if args.batch:
@@ -681,6 +820,19 @@ def main():
         roof["traffic"] = _load_pmc(pkey + "@lam" if args.lam_eps > 0 else pkey)
         roof["avg_launch_ms"] = round(avg_s * 1e3, 4)
         roof["phases_ms_per_step"] = breakdown   # untimed pass (_phase_breakdown)
+        # the whole step against SURVEY §8(d)'s roofline t_roof = max(B/BW, F/P):
+        # B = the algorithmic bytes of a solve (inputs once, both outputs),
+        # F = the flops the shipped algorithm does (N'³/3 on the P-symmetric
+        # route, 2N'³/3 otherwise; the reference's full-KKT LU beside it)
+        b_step = B * 8.0 * (n * n + m * n + p * n + 4 * L + m + n)
+        f_step = float(np.where(symr == 1, 1.0 / 3.0, 2.0 / 3.0) @ (Ns ** 3))
+        f_ref = B * (2.0 / 3.0 * L ** 3 + 4.0 * L ** 2 + 4.0 * m * n)
+        t_hbm, t_fp = b_step / (PEAK_HBM_GBS * 1e9), f_step / (PEAK_FP64_TFLOPS * 1e12)
+        ms_step = elapsed / args.steps
+        roof["step"] = dict(t_roof_ms=round(1e3 * max(t_hbm, t_fp), 4), hbm_ms=round(1e3 * t_hbm, 4),
+                            fp64_ms=round(1e3 * t_fp, 4), bytes=b_step, flops=f_step,
+                            frac=round(max(t_hbm, t_fp) / ms_step, 4),
+                            reference_flops=f_ref, fp64_ms_at_reference_flops=round(1e3 * f_ref / (PEAK_FP64_TFLOPS * 1e12), 4))
         value = world * B * args.steps / elapsed
         line = {
             "metric": "KKT sensitivity solves/sec (fwd+rev) on batched QPs",

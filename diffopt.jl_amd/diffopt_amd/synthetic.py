@@ -234,7 +234,7 @@ def nlp_numpy(batch, n, c, P, seed, frac_geq=0.4, frac_leq=0.3, frac_low=0.5, fr
         rng.standard_normal((batch, nd))
 
 
-def _sparse_wellcond(rng, m, n, k):
+def _sparse_wellcond(rng, m, n, k, dense=True):
     """A dense m × n array with ≈ k non-zeros per row and singular values
     O(1): the rows of I + 0.3·R/√k (R: k N(0,1) entries per row) for min(m, n)
     of them, k random N(0,1)/√k entries for the rest, rows permuted."""
@@ -247,11 +247,12 @@ def _sparse_wellcond(rng, m, n, k):
         ri = np.repeat(np.arange(m - q), k)
         W = sp.vstack([W, sp.csr_matrix((rng.standard_normal((m - q) * k) / math.sqrt(k),
                                          (ri, rng.integers(0, n, size=(m - q) * k))), shape=(m - q, n))])
-    return W.tocsr()[rng.permutation(m)].toarray()
+    W = W.tocsr()[rng.permutation(m)]
+    return W.toarray() if dense else W.tocsc()
 
 
 def conic_numpy_wellcond(batch, n, cones, seed, f_interior=0.25, f_dual_interior=0.25, sigma=(1.0, 2.0),
-                         pair_norm=0.25, sparse_k=None):
+                         pair_norm=0.25, sparse_k=None, sparse_out=False):
     """The converging variant of a conic shape: the same
     cone list, but an instance family on which the reference's LSQR converges
     (istop 1–2) well inside maxiter, so parity can be held to 1e-6 on every
@@ -330,7 +331,7 @@ def conic_numpy_wellcond(batch, n, cones, seed, f_interior=0.25, f_dual_interior
                 raise ValueError("conic_numpy_wellcond: cone code %d not generated" % code)
             o += dim
         if sparse_k:   # the sparse route's family: k entries per row, well conditioned
-            A = _sparse_wellcond(rng, m, n, sparse_k)
+            A = _sparse_wellcond(rng, m, n, sparse_k, dense=not sparse_out)
         else:
             k = min(m, n)
             U, _ = np.linalg.qr(rng.standard_normal((m, m)))
@@ -343,10 +344,11 @@ def conic_numpy_wellcond(batch, n, cones, seed, f_interior=0.25, f_dual_interior
         out["A"].append(A); out["b"].append(b); out["c"].append(c); out["x"].append(x)
         out["s"].append(s); out["y"].append(y)
         out["dx"].append(rng.standard_normal(n))
-        out["dA"].append(rng.standard_normal((m, n)))
+        if not sparse_out:   # (sparse_out: A stays a list of scipy CSC, no dense dA tangent)
+            out["dA"].append(rng.standard_normal((m, n)))
         out["db"].append(rng.standard_normal(m))
         out["dc"].append(rng.standard_normal(n))
-    return {k: np.stack(v) for k, v in out.items()}
+    return {k: (v if k == "A" and sparse_out else np.stack(v)) for k, v in out.items() if v}
 
 
 def lp_sparse_numpy(batch, n, p, m_extra, k, seed):
