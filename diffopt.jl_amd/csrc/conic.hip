@@ -677,24 +677,26 @@ struct DenseA {
     gemv_pair(A, m, m, n, x, w, y, g, ys);
   }
 };
+template <int G>   // lanes per output entry (sp_lanes)
 struct SparseA {
   const int64_t *cp, *rp;   // this problem's CSC colptr (n + 1) and CSR rowptr (m + 1): global offsets
   const int32_t *ri, *ci;   // CSC rows, CSR columns
   const double *cv, *rv;    // CSC / CSR values
   __device__ __forceinline__ void pair(int m, int n, const double* x, const double* w, double* y, double* g,
                                        double*) const {
-    const int t = threadIdx.x, grp = t >> 3, sub = t & 7;
-    for (int o = grp; o < m + n; o += CTPB / 8) {
+    const int t = threadIdx.x, grp = t / G, sub = t % G;
+    for (int o = grp; o < m + n; o += CTPB / G) {
       double acc = 0.0;
       if (o < m) {
-        for (int64_t k = rp[o] + sub; k < rp[o + 1]; k += 8) acc = fma(rv[k], x[ci[k]], acc);
+#pragma unroll 4
+        for (int64_t k = rp[o] + sub; k < rp[o + 1]; k += G) acc = fma(rv[k], x[ci[k]], acc);
       } else {
         const int j = o - m;
-        for (int64_t k = cp[j] + sub; k < cp[j + 1]; k += 8) acc = fma(cv[k], w[ri[k]], acc);
+#pragma unroll 4
+        for (int64_t k = cp[j] + sub; k < cp[j + 1]; k += G) acc = fma(cv[k], w[ri[k]], acc);
       }
-      acc += __shfl_xor(acc, 4);
-      acc += __shfl_xor(acc, 2);
-      acc += __shfl_xor(acc, 1);
+#pragma unroll
+      for (int s2 = G / 2; s2 > 0; s2 >>= 1) acc += __shfl_xor(acc, s2);
       if (sub == 0) {
         if (o < m) y[o] = acc;
         else g[o - m] = acc;
@@ -837,20 +839,32 @@ __device__ __forceinline__ void MT_apply2(const ConicProblem& pr, const ConeDesc
 // problem; vectors in a per-problem global workspace (L2-resident).
 // mode 0: forward (rhs built from tangents); mode 1: reverse.
 // SPARSE: A_moi kept sparse (SpConic: the batch's CSC / CSR arrays; the
-// products by SparseA), otherwise the dense A.
+// products by SparseA<SG>), otherwise the dense A.  gridDim.y = 2 (sparse
+// route): blockIdx.y = 1 runs a second, independent sequence of the same
+// problem (rhs2 / tol2 / xout2 / info2 / norms2, its own workspace) beside the
+// first — the forward and reverse runs of dopt_conic_forward_reverse.
 // ---------------------------------------------------------------------------
 struct SpConic {
   const int64_t *cp, *rp;
   const int32_t *ri, *ci;
   const double *cv, *rv;
 };
-template <bool SPARSE>
+template <bool SPARSE, int SG = 1>
 __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
     const ConeDesc* __restrict__ cones_g, int ncones, const double* __restrict__ A,
     const double* __restrict__ b, const double* __restrict__ c,
     const double* __restrict__ v, const double* __restrict__ P, int plen, int m, int n,
     const double* __restrict__ rhs, double rhs_zero_tol, double* __restrict__ work,
-    double* __restrict__ xout, int32_t* __restrict__ info, double* __restrict__ norms, int maxiter, SpConic sa) {
+    double* __restrict__ xout, int32_t* __restrict__ info, double* __restrict__ norms, int maxiter, SpConic sa,
+    const double* __restrict__ rhs2, double tol2, double* __restrict__ xout2, int32_t* __restrict__ info2,
+    double* __restrict__ norms2) {
+  if (blockIdx.y) {   // (uniform) the second sequence
+    rhs = rhs2;
+    rhs_zero_tol = tol2;
+    xout = xout2;
+    info = info2;
+    norms = norms2;
+  }
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ double red[4];
   __shared__ ConeDesc cones[128];
@@ -871,7 +885,7 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
   pr.m = m;
   pr.n = n;
   const size_t wl = (size_t)5 * N + 3 * (size_t)m + n;
-  double* x = work + (size_t)bidx * wl;
+  double* x = work + ((size_t)blockIdx.y * gridDim.x + bidx) * wl;
   double* u = x + N;
   double* vv = u + N;
   double* w = vv + N;
@@ -881,10 +895,10 @@ __global__ __launch_bounds__(CTPB) void conic_lsqr_kernel(
   double* s3 = s2 + m;    // m
   double* s4 = s3 + m;    // n
   const double* rb = rhs + (size_t)bidx * N;
-  using MAT = typename std::conditional<SPARSE, SparseA, DenseA>::type;
+  using MAT = typename std::conditional<SPARSE, SparseA<SG>, DenseA>::type;
   MAT mat;
   if constexpr (SPARSE)
-    mat = SparseA{sa.cp + (size_t)bidx * (n + 1), sa.rp + (size_t)bidx * (m + 1), sa.ri, sa.ci, sa.cv, sa.rv};
+    mat = SparseA<SG>{sa.cp + (size_t)bidx * (n + 1), sa.rp + (size_t)bidx * (m + 1), sa.ri, sa.ci, sa.cv, sa.rv};
   else
     mat = DenseA{pr.A};
   double bb = 0.0;
@@ -2490,17 +2504,26 @@ static SpConic sp_conic(const Handle& h) {
                  st.rv.as<double>()};
 }
 
-// one persistent LSQR sequence per problem on the sparse A_moi (rhs, out: N
-// per problem; info / norms at the given offsets)
-static void conic_lsqr_sparse(Handle& h, double tol, const double* rhs, double* out, int32_t* info, double* norms) {
+// nq (1 or 2) persistent LSQR sequences per problem on the sparse A_moi, side
+// by side in one launch (rhs, out: N per problem; info / norms at the given
+// offsets).  The caller sized cwork: nq·B·wl of workspace at its front, the
+// right-hand sides behind it.
+static void conic_lsqr_sparse(Handle& h, int nq, double tol, const double* rhs, double* out, int32_t* info,
+                              double* norms, double tol2 = 0.0, const double* rhs2 = nullptr, double* out2 = nullptr,
+                              int32_t* info2 = nullptr, double* norms2 = nullptr) {
   const int B = (int)h.batch, m = h.m, n = h.n;
   const int nc = (int)h.cones.size() / 2;
-  // (the caller sized cwork: B·wl of per-problem workspace at its front, the
-  // right-hand sides behind it)
+  const int G = sp_lanes(2.0 * (double)h.sp[0].nnz / std::max<double>(1.0, (double)B * (m + n)));
   PhaseTimer pt(h, DOPT_PHASE_CONIC_LSQR);
-  hipLaunchKernelGGL(conic_lsqr_kernel<true>, dim3(B), dim3(CTPB), dpi_lds_bytes(h.cones), h.stream,
-                     h.cone_dev.as<ConeDesc>(), nc, nullptr, h.cb, h.cc, h.vp.as<double>(), h.dpi.as<double>(),
-                     h.dpi_len, m, n, rhs, tol, h.cwork.as<double>(), out, info, norms, lsqr_maxiter(h), sp_conic(h));
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(B, nq), dim3(CTPB), dpi_lds_bytes(h.cones), h.stream, h.cone_dev.as<ConeDesc>(),
+                       nc, nullptr, h.cb, h.cc, h.vp.as<double>(), h.dpi.as<double>(), h.dpi_len, m, n, rhs, tol,
+                       h.cwork.as<double>(), out, info, norms, lsqr_maxiter(h), sp_conic(h), rhs2, tol2, out2, info2,
+                       norms2);
+  };
+  if (G == 1) go(conic_lsqr_kernel<true, 1>);
+  else if (G == 4) go(conic_lsqr_kernel<true, 4>);
+  else go(conic_lsqr_kernel<true, 16>);
   ccheck();
 }
 
@@ -2514,7 +2537,7 @@ static void conic_lsqr(Handle& h, double tol, double* out) {
   h.cnorm.ensure((size_t)8 * std::max(B, 1) * sizeof(double));
   double* rhs = h.cwork.as<double>() + (size_t)B * wl;
   if (h.sparse) {
-    conic_lsqr_sparse(h, tol, rhs, out, h.cinfo.as<int32_t>(), h.cnorm.as<double>());
+    conic_lsqr_sparse(h, 1, tol, rhs, out, h.cinfo.as<int32_t>(), h.cnorm.as<double>());
     return;
   }
   if (use_split(h)) {
@@ -2526,7 +2549,8 @@ static void conic_lsqr(Handle& h, double tol, double* out) {
   hipLaunchKernelGGL(conic_lsqr_kernel<false>, dim3(B), dim3(CTPB), dpi_lds_bytes(h.cones), h.stream,
                      h.cone_dev.as<ConeDesc>(), nc, h.cA, h.cb, h.cc, h.vp.as<double>(),
                      h.dpi.as<double>(), h.dpi_len, m, n, rhs, tol, h.cwork.as<double>(), out,
-                     h.cinfo.as<int32_t>(), h.cnorm.as<double>(), lsqr_maxiter(h), SpConic{});
+                     h.cinfo.as<int32_t>(), h.cnorm.as<double>(), lsqr_maxiter(h), SpConic{}, nullptr, 0.0, nullptr,
+                     nullptr, nullptr);
   ccheck();
 }
 
@@ -2602,10 +2626,9 @@ void conic_forward_reverse(Handle& h, const double* dA, const double* db, const 
     hipLaunchKernelGGL(conic_rev_rhs_kernel, dim3(B), dim3(CTPB), 0, h.stream, dx, h.cx, m, n, rhs_r);
     ccheck();
   }
-  if (h.sparse) {   // the two sequences one after the other (results equal the separate calls)
+  if (h.sparse) {   // the two sequences side by side in one launch (each equal to its separate call)
     int32_t* info = h.cinfo.as<int32_t>();
-    conic_lsqr_sparse(h, 0.0, rhs_f, out_f, info + 2 * B, nrm + 4 * (size_t)B);
-    conic_lsqr_sparse(h, 1e-4, rhs_r, out_g, info, nrm);
+    conic_lsqr_sparse(h, 2, 0.0, rhs_f, out_f, info + 2 * B, nrm + 4 * (size_t)B, 1e-4, rhs_r, out_g, info, nrm);
   } else if (use_split(h)) {
     int32_t* info = h.cinfo.as<int32_t>();
     conic_lsqr_split(h, 2, 0.0, 1e-4, rhs_f, out_f, info + 2 * B, out_g, info, nrm + 4 * (size_t)B, nrm);

@@ -412,6 +412,11 @@ double* dense_dinv(Handle& h);
 void lsqr_slabs(Handle& h, int trans, const double* rhs, double* x);
 void lhs_solve(Handle& h, int k, const double* rhs, double* x, bool iterative, int32_t* info);
 void lhs_resolve(Handle& h, int k, const double* rhs, double* x, bool trans, int32_t* info);
+// lanes per output entry of the sparse products (sparse.hip, conic.hip): one
+// lane per row up to ≈ 12 entries, 4 up to 48, 16 above
+inline int sp_lanes(double entries_per_output) {
+  return entries_per_output <= 12.0 ? 1 : entries_per_output <= 48.0 ? 4 : 16;
+}
 // sparse QP route (sparse.hip)
 void sp_set_csc(Handle& h, const int64_t* Qcp, const int64_t* Qrv, const double* Qnz, int64_t Qnnz,
                 const int64_t* Gcp, const int64_t* Grv, const double* Gnz, int64_t Gnnz, const int64_t* Acp,

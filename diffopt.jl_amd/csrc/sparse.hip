@@ -38,7 +38,10 @@ namespace dopt {
 namespace {
 
 constexpr int SP_TPB = 1024;   // LSQR workgroup (16 waves)
-constexpr int SP_G = 8;        // lanes per output entry of a product
+// lanes per output entry of a product: a template parameter chosen per batch
+// from the mean entries per output (sp_lanes): 1 for the usual few-per-row
+// sparsity (every lane its own row, the row's loads pipelined), 4 / 16 for
+// denser rows
 constexpr int SP_SETUP = 256;
 
 // One matrix of the batch (G or A, `rows` × n) in both forms, global offsets.
@@ -232,10 +235,10 @@ struct SpSys {
   int n, m, p;
 };
 
-__device__ __forceinline__ double grp_sum(double v) {   // over the 8 lanes of a group
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 1);
+template <int G>
+__device__ __forceinline__ double grp_sum(double v) {   // over the G lanes of a group
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
 
@@ -243,6 +246,7 @@ __device__ __forceinline__ double grp_sum(double v) {   // over the 8 lanes of a
 //   z rows:  Σ_i G_ij·(tr ? x_λi : λ_i x_λi) + Σ_k A_kj x_νk      (CSC columns)
 //   λ rows:  (tr ? λ_i : 1)·(G x_z)_i + s_i x_λi                    (CSR rows)
 //   ν rows:  (A x_z)_k                                             (CSR rows)
+template <int SP_G>
 __device__ void sp_matvec(const SpSys& S, size_t b, int tr, const double* __restrict__ x, double* __restrict__ out) {
   const int t = threadIdx.x, grp = t / SP_G, sub = t % SP_G, NG = SP_TPB / SP_G;
   const int n = S.n, m = S.m, p = S.p, L = n + m + p;
@@ -256,23 +260,27 @@ __device__ void sp_matvec(const SpSys& S, size_t b, int tr, const double* __rest
     double acc = 0.0;
     if (o < n) {
       if (m)
+#pragma unroll 4
         for (int64_t k = gcp[o] + sub; k < gcp[o + 1]; k += SP_G) {
           const int i = S.G.ri[k];
           const double xv = x[n + i];
           acc = fma(S.G.cv[k], tr ? xv : lam[i] * xv, acc);
         }
       if (p)
+#pragma unroll 4
         for (int64_t k = acp[o] + sub; k < acp[o + 1]; k += SP_G) acc = fma(S.A.cv[k], x[n + m + S.A.ri[k]], acc);
-      acc = grp_sum(acc);
+      acc = grp_sum<SP_G>(acc);
     } else if (o < n + m) {
       const int i = o - n;
+#pragma unroll 4
       for (int64_t k = grp_[i] + sub; k < grp_[i + 1]; k += SP_G) acc = fma(S.G.rv[k], x[S.G.ci[k]], acc);
-      acc = grp_sum(acc);
+      acc = grp_sum<SP_G>(acc);
       acc = fma(sl[i], x[o], tr ? lam[i] * acc : acc);
     } else {
       const int k0 = o - n - m;
+#pragma unroll 4
       for (int64_t k = arp[k0] + sub; k < arp[k0 + 1]; k += SP_G) acc = fma(S.A.rv[k], x[S.A.ci[k]], acc);
-      acc = grp_sum(acc);
+      acc = grp_sum<SP_G>(acc);
     }
     if (sub == 0) out[o] = acc;
   }
@@ -295,6 +303,7 @@ __device__ __forceinline__ double sp_block_sum(double v, double* red) {
 // blockIdx.x = problem, blockIdx.y = sequence q (0: reverse, LHS; 1: forward,
 // LHSᵀ — `dir` gives each sequence's operator, rhs / out / info per sequence);
 // out = −x (QuadraticProgram.jl:336-337, :437-438); info: [istop, iterations]
+template <int SP_G>
 __global__ __launch_bounds__(SP_TPB) void sp_lsqr_kernel(SpSys S, int B, int dir0, int dir1,
                                                          const double* __restrict__ rhs0,
                                                          const double* __restrict__ rhs1, double* __restrict__ out0,
@@ -325,7 +334,7 @@ __global__ __launch_bounds__(SP_TPB) void sp_lsqr_kernel(SpSys S, int B, int dir
   if (beta > 0.0) {
     for (int i = t; i < N; i += SP_TPB) u[i] /= beta;
     __syncthreads();
-    sp_matvec(S, b, !trans, u, v);   // v = Aᵀu
+    sp_matvec<SP_G>(S, b, !trans, u, v);   // v = Aᵀu
     double aa = 0.0;
     for (int i = t; i < N; i += SP_TPB) aa = fma(v[i], v[i], aa);
     double alpha = sqrt(sp_block_sum(aa, red));
@@ -343,7 +352,7 @@ __global__ __launch_bounds__(SP_TPB) void sp_lsqr_kernel(SpSys S, int B, int dir
       const int maxiter = N;
       while (it < maxiter) {
         ++it;
-        sp_matvec(S, b, trans, v, tmp);   // tmp = A v
+        sp_matvec<SP_G>(S, b, trans, v, tmp);   // tmp = A v
         double su = 0.0;
         for (int i = t; i < N; i += SP_TPB) {
           const double ui = tmp[i] - alpha * u[i];
@@ -355,7 +364,7 @@ __global__ __launch_bounds__(SP_TPB) void sp_lsqr_kernel(SpSys S, int B, int dir
           for (int i = t; i < N; i += SP_TPB) u[i] /= beta;
           __syncthreads();
           anorm = sqrt(anorm * anorm + alpha * alpha + beta * beta);
-          sp_matvec(S, b, !trans, u, tmp);   // tmp = Aᵀu
+          sp_matvec<SP_G>(S, b, !trans, u, tmp);   // tmp = Aᵀu
           double sv = 0.0;
           for (int i = t; i < N; i += SP_TPB) {
             const double vi = tmp[i] - beta * v[i];
@@ -546,9 +555,17 @@ static void sp_lsqr(Handle& h, int nq, int dir0, int dir1, const double* rhs0, c
   h.sp_ws.ensure((size_t)nq * B * 5 * N * sizeof(double));
   h.sp_info.ensure((size_t)4 * std::max(B, 1) * sizeof(int32_t));
   int32_t* info = h.sp_info.as<int32_t>();
+  // lanes per output: the mean entries per output of the LHS products
+  const double per = (2.0 * ((double)h.sp[0].nnz + (double)h.sp[1].nnz)) / std::max<double>(1.0, (double)B * N);
+  const int G = sp_lanes(per);
   PhaseTimer pt(h, DOPT_PHASE_QP_LSQR);
-  hipLaunchKernelGGL(sp_lsqr_kernel, dim3(B, nq), dim3(SP_TPB), 0, h.stream, sp_sys(h), B, dir0, dir1, rhs0, rhs1,
-                     out0, out1, h.sp_ws.as<double>(), info + (dir0 ? 2 * B : 0), info + 2 * B);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(B, nq), dim3(SP_TPB), 0, h.stream, sp_sys(h), B, dir0, dir1, rhs0, rhs1, out0,
+                       out1, h.sp_ws.as<double>(), info + (dir0 ? 2 * B : 0), info + 2 * B);
+  };
+  if (G == 1) go(sp_lsqr_kernel<1>);
+  else if (G == 4) go(sp_lsqr_kernel<4>);
+  else go(sp_lsqr_kernel<16>);
   DOPT_CHECK_HIP(hipGetLastError());
 }
 
