@@ -593,7 +593,8 @@ def run_sparse(args, world, rank, local_rank):
         per_step = b_it * float((it_f + it_r).sum())
         achieved = per_step / (ms_tot / 1e3 / args.steps) / 1e9
         roof = dict(bound="hbm", achieved=round(achieved, 1), peak=PEAK_HBM_GBS, unit="GB/s",
-                    frac=round(achieved / PEAK_HBM_GBS, 4), traffic=None, kernel=phase,
+                    frac=round(achieved / PEAK_HBM_GBS, 4), traffic=_load_pmc(f"{phase}@cfg{args.config}"),
+                    kernel=phase,
                     avg_launch_ms=round(avg_s * 1e3, 4), bytes_per_iteration=b_it, nnz_per_problem=nnz,
                     lsqr_iterations_mean={"forward": float(it_f.mean()), "reverse": float(it_r.mean())})
         print(json.dumps({

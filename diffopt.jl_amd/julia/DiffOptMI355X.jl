@@ -395,6 +395,12 @@ function _ensure!(m::ConicModel)
     if h === nothing || (h.n, h.m) != (n, mr)
         h = m.handle = Handle(n, mr, 0; device = m.device, kind = KIND_CONIC)
         m.staged = nothing
+        # a large, sparse A_moi stays sparse on the device (dopt_set_sparse: LSQR
+        # on the matrix-free M from its CSC / CSR, as the reference's own lsqr on
+        # a SparseMatrixCSC, ConicProgram.jl:323, :372) instead of an m×n dense copy
+        if mr * n > 4_000_000 && SparseArrays.nnz(Amoi) < 0.05 * mr * n && _sparse_cones_ok(desc)
+            _check(ccall((:dopt_set_sparse, LIB), Cint, (Ptr{Cvoid}, Int32), h.ptr, Int32(1)), h.ptr)
+        end
     end
     key = (Amoi, b, c, copy(inner.x), copy(inner.s), copy(inner.y), desc)
     m.staged !== nothing && isequal(m.staged, key) && return h
@@ -411,6 +417,9 @@ function _ensure!(m::ConicModel)
     m.staged = key
     return h
 end
+
+# the sparse conic route takes PSD cones up to side 64 (include/diffopt_mi355x.h)
+_sparse_cones_ok(desc) = all(k -> desc[2k-1] != 4 || desc[2k] <= 64 * 65 ÷ 2, 1:(length(desc) ÷ 2))
 
 # forward_differentiate! (ConicProgram.jl:257-334): the tangents gathered with
 # the reference's own `_fill` (dA, db in MOI layout), [du | dv | dw] from the

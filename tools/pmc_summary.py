@@ -26,7 +26,8 @@ KERNEL_PHASE = {
     "qp_fused_kernel": "qp_fused",
     "qp_factor_fast_kernel": "qp_lu",
     "qp_solve_fast_kernel": "qp_solve",
-    "conic_lsqr_kernel": "conic_lsqr",
+    "conic_lsqr_kernel": "conic_lsqr",     # (dense or, config 8, the sparse route's instantiation)
+    "sp_lsqr_kernel": "qp_lsqr",           # the sparse QP route (config 7)
     "conic_lsqr2_kernel": "conic_lsqr",     # co-iterated forward + reverse (one launch per call)
     "conic_cone_kernel": "conic_cone",
     "conic_split_pass_kernel": "conic_split_pass",

@@ -1,0 +1,13 @@
+# Round 6 evidence, part A: configs 3, 2 (--lam-eps) and 6 at head, each with
+# its PMC traffic (the stale `traffic` fields of VERDICT r05 weak 10)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+J=tools/gpu_job.sh
+bash $J bench cfg3 --config 3 --steps 5 --warmup 2 \
+ && PMC_SUFFIX=@cfg3 bash $J pmc cfg3 --config 3 --steps 2 --warmup 1 \
+ && bash $J prof cfg3 --config 3 --steps 3 --warmup 1 \
+ && bash $J bench cfg2lam --lam-eps 1e-9 --no-cpu-baseline \
+ && PMC_SUFFIX=@lam bash $J pmc cfg2lam --lam-eps 1e-9 --steps 3 --warmup 1 \
+ && bash $J bench cfg6 --config 6 --steps 10 --warmup 2 \
+ && PMC_SUFFIX=@cfg6 bash $J pmc cfg6 --config 6 --steps 3 --warmup 1 \
+ && bash $J pmc cfg2 --steps 5 --warmup 2
