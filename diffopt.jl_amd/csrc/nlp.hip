@@ -260,7 +260,9 @@ __global__ __launch_bounds__(NT) void nlp_assemble_kernel(NLPDims d, NLPMap mp, 
 // u_ii: the no-pivot LU does not store its 32×32 diagonal blocks back to K
 // (qp_nopiv.hip: the solves read only their inverses), so for LU_NOPIV
 // problems u_ii = 1 / (U⁻¹)_ii from the block's inverse in dinv (L⁻¹ | U⁻¹,
-// row-major 32×32 each); partial-pivoting problems keep U in K.
+// row-major 32×32 each) — or, for the left-looking route's P-symmetric
+// factors (`ukp` non-null; dinv then holds only L⁻¹), u_ii = ukp_i (u/p with
+// p = 1 here); partial-pivoting problems keep U in K.
 __global__ __launch_bounds__(NT) void nlp_pivot_check_kernel(const double* __restrict__ K, int ld, int nmax,
                                                              const int32_t* __restrict__ perm,
                                                              const double* __restrict__ dinv, size_t dstride,
@@ -268,7 +270,8 @@ __global__ __launch_bounds__(NT) void nlp_pivot_check_kernel(const double* __res
                                                              const double* __restrict__ partial, int nparts,
                                                              int rows, const int32_t* __restrict__ plist,
                                                              NLPRed Rd, const int32_t* __restrict__ shift,
-                                                             const double* __restrict__ mscale) {
+                                                             const double* __restrict__ mscale,
+                                                             const double* __restrict__ ukp) {
   __shared__ double sred[NT / 64];
   __shared__ int ired[NT / 64];
   const int b = plist ? plist[blockIdx.x] : (int)blockIdx.x;
@@ -292,9 +295,11 @@ __global__ __launch_bounds__(NT) void nlp_pivot_check_kernel(const double* __res
   int first = 0x7fffffff;
   const double* Db = dinv + (size_t)b * dstride;
   const bool nopiv = mm.lu == LU_NOPIV;
+  const bool left = nopiv && ukp && mm.sym;   // workgroup-uniform
   for (int i = threadIdx.x; i < rows; i += NT) {
-    const double u = nopiv ? 1.0 / Db[(size_t)(i >> 5) * (2 * 32 * 32) + 32 * 32 + (i & 31) * 33]
-                           : Kb[(size_t)pb[i] * ld + i];
+    const double u = left    ? ukp[(size_t)b * nmax + i]
+                     : nopiv ? 1.0 / Db[(size_t)(i >> 5) * (2 * 32 * 32) + 32 * 32 + (i & 31) * 33]
+                             : Kb[(size_t)pb[i] * ld + i];
     if (!(fabs(u) > tol) && i < first) first = i;   // NaN fails too
   }
   for (int o = 32; o > 0; o >>= 1) first = min(first, __shfl_xor(first, o));
@@ -924,7 +929,8 @@ void pivot_check(Handle& h, const int32_t* plist, int count) {
   hipLaunchKernelGGL(nlp_pivot_check_kernel, dim3(count), dim3(NT), 0, h.stream, h.K.as<double>(), h.ld, h.nmax,
                      h.ipiv.as<int32_t>(), dense_dinv(h), dinv_stride(h.nmax), h.meta.as<QPMeta>(),
                      h.nlp_scale.as<double>(), row_blocks(h),
-                     h.nlp_rows, plist, red_of(h), h.nlp_shift.as<int32_t>(), nlp_mscale(h));
+                     h.nlp_rows, plist, red_of(h), h.nlp_shift.as<int32_t>(), nlp_mscale(h),
+                     h.ukp_valid ? h.ukp.as<double>() : nullptr);
   DOPT_CHECK_HIP(hipGetLastError());
 }
 

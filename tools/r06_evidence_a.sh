@@ -3,7 +3,12 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 J=tools/gpu_job.sh
-bash $J bench cfg3 --config 3 --steps 5 --warmup 2 \
+TEST_PATHS="tests/test_qp_gpu.py tests/test_multi_rhs_gpu.py tests/test_nlp_gpu.py tests/test_lhs_solve_gpu.py tests/test_params_gpu.py" bash $J test \
+ && cp gpurun_out/test.log gpurun_out/test_uinv.log \
+ && bash $J bench cfg2 --no-cpu-baseline \
+ && bash $J prof cfg2 --steps 20 --warmup 3 \
+ && python3 tools/timeline.py gpurun_out/prof_cfg2 > gpurun_out/timeline_cfg2.txt \
+ && bash $J bench cfg3 --config 3 --steps 5 --warmup 2 \
  && PMC_SUFFIX=@cfg3 bash $J pmc cfg3 --config 3 --steps 2 --warmup 1 \
  && bash $J prof cfg3 --config 3 --steps 3 --warmup 1 \
  && bash $J bench cfg2lam --lam-eps 1e-9 --no-cpu-baseline \
