@@ -191,3 +191,33 @@ def test_structured_psd_matches_dense():
             w = rng.standard_normal(k)
             np.testing.assert_allclose(S @ w, Dd @ w, rtol=1e-12, atol=1e-13)
             np.testing.assert_allclose(S.T @ w, Dd.T @ w, rtol=1e-12, atol=1e-13)
+
+
+LP_FX = [f for f in _load("lp_fixtures.json") if not np.any(np.array(f["Q"], dtype=float))]
+
+
+@pytest.mark.parametrize("fx", LP_FX, ids=[f["name"] for f in LP_FX])
+def test_sparse_lp_oracle_matches_reference_fixture(fx):
+    """The sparse route's checker (oracle/qp.py lp_sparse_differentiate: the
+    reference's LHS built as a scipy CSC, never dense, + the LSQR restatement)
+    pinned by the reference's own LP fixtures (test/linear_program.jl), for
+    the fixtures whose forward tangents are vectors (dq, dh, db): its reverse
+    reproduces the reference's expected values at the fixture's tolerances and
+    both directions equal the dense oracle's to 1e-6."""
+    import scipy.sparse as sp
+    a, fw = qp_arrays(fx)
+    if any(k in fw and fw[k].size and np.any(fw[k]) for k in ("dQ", "dG", "dA")):
+        pytest.skip("matrix tangents: the sparse checker takes vector tangents only")
+    n, m, p = a["Q"].shape[0], a["G"].shape[0], a["A"].shape[0]
+    rev, fwd, _, _ = qp.lp_sparse_differentiate(sp.csc_matrix(a["G"]) if m else None, a["h"],
+                                                sp.csc_matrix(a["A"]) if p else None, a["z"], a["lam"], a["nu"],
+                                                a["dzb"], fw.get("dq"), fw.get("dh") if m else None,
+                                                fw.get("db") if p else None)
+    got = qp_outputs(a, fw, solve_rev=lambda: (rev[:n], rev[n:n + m], rev[n + m:]), solve_fwd=lambda: fwd[:n])
+    for k, v in fx["expect"].items():
+        exp = np.array(v, dtype=float).reshape(np.shape(got[k]))
+        np.testing.assert_allclose(got[k], exp, atol=fx["atol"], rtol=fx["rtol"], err_msg=k)
+    dz, dl, dn = qp.reverse_differentiate(a["Q"], a["G"], a["h"], a["A"], a["z"], a["lam"], a["nu"], a["dzb"])
+    fz, fl, fn = qp.forward_differentiate(a["Q"], a["G"], a["h"], a["A"], a["z"], a["lam"], a["nu"], **fw)
+    for got_v, ref in ((rev, np.concatenate([dz, dl, dn])), (fwd, np.concatenate([fz, fl, fn]))):
+        assert np.linalg.norm(got_v - ref) <= 1e-6 * max(np.linalg.norm(ref), 1e-300)
