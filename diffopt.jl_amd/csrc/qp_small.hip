@@ -53,9 +53,14 @@ __device__ __forceinline__ double sm_block_max(double v, double* red) {
 // every load in flight, when they fit).
 struct SmallLds {
   double S[SM_MAX * SM_LD];   // the L\U factors (row-major, padded rows)
-  double rowb[2][SM_GB][SM_MAX];   // reverse LU: a group's rows / columns / diagonal block,
-  double colb[2][SM_GB][SM_MAX];   // double-buffered
-  double dblk[2][SM_GB * SM_GB];
+  union {
+    struct {
+      double rowb[2][SM_GB][SM_MAX];   // reverse LU (rank-4 groups): a group's rows / columns / diagonal
+      double colb[2][SM_GB][SM_MAX];   // block, double-buffered
+      double dblk[2][SM_GB * SM_GB];
+    };
+    double lw[SM_T / 64][256];   // reverse LU (16-blocks): each wave's copy of the diagonal block's L
+  };
   double z[SM_MAX];           // z (rev) | scratch
   double y[SM_MAX];           // the solve vector
   double dinv[SM_MAX];        // 1 / diag(U)
@@ -153,12 +158,15 @@ template <bool STG>
 __device__ __forceinline__ double sm_assemble(const QPIn& P, const SmSrc& X, const SmallLds& L, int nk, int N,
                                               int ti, int tj, double (&e)[8][8]) {
   const int n = P.n, m = P.m, p = P.p;
+  const int NB = (N + SM_G - 1) / SM_G;   // the blocks the LU reads (a, c < NB)
   double amax = 0.0;
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
     if (a == 4) __builtin_amdgcn_sched_barrier(0);   // two rounds of 32 loads (register pressure)
 #pragma unroll
     for (int c8 = 0; c8 < 8; ++c8) {
+      e[a][c8] = 0.0;
+      if (a >= NB || c8 >= NB) continue;   // uniform
       const int r = ti + SM_G * a, c = tj + SM_G * c8;
       int which = 0;
       SmOff<STG> off = 0;
@@ -335,6 +343,142 @@ __device__ __forceinline__ void sm_lu_from(double (&e)[8][8], SmallLds& L, int N
   if constexpr (KK + 1 < NB) sm_lu_from<KK + 1, NB>(e, L, N, ti, tj, bound, bad, stamp);
 }
 
+// lane l's x (l wave-uniform): two v_readlane_b32 into an SGPR pair
+__device__ __forceinline__ double sm_readlane(double x, int l) {
+  const unsigned long long v = (unsigned long long)__double_as_longlong(x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ void sm_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+typedef double sm_d4 __attribute__((ext_vector_type(4)));
+
+// Right-looking no-pivot LU by 16-blocks over the LDS image (round 6, VERDICT
+// r05 item 5; default — -DSM_LU_GROUPS builds the rank-4 groups above), the
+// same acceptance tests as each entry becomes final.  Block column KK
+// (k0 = 16·KK), two barriers per block:
+//   panel   every wave factors the 16 × 16 diagonal block redundantly, lane i
+//           < 16 holding row k0 + i (pivot row k's entries by v_readlane, no
+//           LDS on the chain), and in the same instructions eliminates the
+//           rows below it that its lanes 16 … 63 hold (48 rows per wave, four
+//           waves: every row below, L's entries of the block column, no
+//           TRSM); wave 0 stores the diagonal block, each wave its rows;
+//   U row   each wave then solves L_KK·U(KK, c) = A(KK, c) for its share of
+//           the columns right of the block (lane ↔ column, L_KK from the
+//           wave's own copy of it: no barrier between the two);
+//   update  after the barrier, A(I, C) −= L(I, KK)·U(KK, C) for every
+//           trailing 16 × 16 tile on v_mfma_f64_16x16x4f64 (tiles dealt
+//           round-robin to the waves), operands and accumulators from LDS.
+// The reverse solve's L y = r rides along (L.y holds r on entry, y on exit):
+// each lane carries its row's entry through the panel's sixteen steps (y_k by
+// v_readlane from the diagonal lane k), so the rows below take their
+// L(I, KK)·y_KK with the elimination and no separate forward sweep is run.
+// The 16-block padding of the system past N is the identity (assembled so).
+__device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double bound, int& bad) {
+  double* S = L.S;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
+  const int NP = 16 * NB;
+  double* Lw = L.lw[wv];   // this wave's copy of L_KK, column-major (L_ik at 16k + i)
+  for (int KK = 0; KK < NB; ++KK) {
+    const int k0 = 16 * KK;
+    // ---- panel: rows k0 + lane (lane < 16) and k0 + 16 + 48·wv + lane − 16
+    const int r = lane < 16 ? k0 + lane : k0 + 16 + 48 * wv + (lane - 16);
+    const bool rin = r < NP;
+    double a[16];
+    {
+      const double* src = S + (rin ? r : 0) * SM_LD + k0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) a[j] = rin ? src[j] : 0.0;
+    }
+    double rv = rin ? L.y[r] : 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      double pr[16];
+#pragma unroll
+      for (int j = k; j < 16; ++j) pr[j] = sm_readlane(a[j], k);
+      const double rq = 1.0 / pr[k];
+      if (lane > k) {
+        const double l = a[k] * rq;
+        a[k] = l;
+#pragma unroll
+        for (int j = k + 1; j < 16; ++j) a[j] = fma(-l, pr[j], a[j]);
+      }
+    }
+    // the forward sweep's block: y_k from lane k once final, the rows below it
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const double yk = sm_readlane(rv, k);
+      if (lane > k) rv = fma(-a[k], yk, rv);
+    }
+    // the tests and the stores of row r's entries (r, k0 + j): the rows below
+    // now (no wave reads them before the barrier), the diagonal block's after
+    // the barrier (every wave has loaded it by then; the update reads neither)
+    auto put_row = [&]() {
+      double* dst = S + r * SM_LD + k0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const double v = a[j];
+        dst[j] = v;
+        if (r < N && k0 + j < N) {
+          if (lane >= 16 || j < lane) bad |= !(fabs(v) <= NOPIV_LMAX);
+          else bad |= !(fabs(v) <= bound) || (j == lane && !(fabs(v) > 0.0));
+        }
+      }
+    };
+    if (rin && lane >= 16) {
+      put_row();
+      L.y[r] = rv;
+    }
+    if (lane < 16)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) Lw[16 * j + lane] = j < lane ? a[j] : 0.0;
+    sm_wave_sync();
+    // ---- U row: columns k0 + 16 + q, q = wv + 4·lane
+    const int ncol = NP - k0 - 16;
+    const int c = k0 + 16 + wv + 4 * lane;
+    if (wv + 4 * lane < ncol) {
+      double u[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) u[i] = S[(k0 + i) * SM_LD + c];
+#pragma unroll
+      for (int k = 0; k < 15; ++k)
+#pragma unroll
+        for (int i = k + 1; i < 16; ++i) u[i] = fma(-Lw[16 * k + i], u[k], u[i]);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        S[(k0 + i) * SM_LD + c] = u[i];
+        if (k0 + i < N && c < N) bad |= !(fabs(u[i]) <= bound);
+      }
+    }
+    __syncthreads();
+    if (wv == 0 && lane < 16) {
+      put_row();
+      L.y[r] = rv;
+    }
+    // ---- trailing update on MFMA: tile (I, C) −= L(I, KK)·U(KK, C)
+    const int nt = NB - KK - 1;
+    for (int tt = wv; tt < nt * nt; tt += SM_T / 64) {
+      const int i0 = k0 + 16 + 16 * (tt / nt), j0 = k0 + 16 + 16 * (tt % nt);
+      sm_d4 acc;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) acc[rr] = S[(i0 + g + 4 * rr) * SM_LD + j0 + l16];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const double av = -S[(i0 + l16) * SM_LD + k0 + 4 * s + g];
+        const double bv = S[(k0 + 4 * s + g) * SM_LD + j0 + l16];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) S[(i0 + g + 4 * rr) * SM_LD + j0 + l16] = acc[rr];
+    }
+    __syncthreads();
+  }
+}
+
 // One sweep over the LU image by one wave, vector entry i in lane i & 63,
 // register i >> 6: step k (ascending when LOWER — the entries past k —,
 // descending otherwise — the entries before k) takes entry k by v_readlane
@@ -496,6 +640,20 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
   if (t == 0) printf("small: e00 %g e01 %g e10 %g Q0 %g amax %g nk %d\n", e[0][0], e[0][1], e[1][0], Qb[0], amax, nk);
 #endif
   int bad = 0;
+#ifndef SM_LU_GROUPS
+  {
+    const int NB = (N + SM_G - 1) / SM_G;   // the system padded to 16-blocks (identity past N)
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int c8 = 0; c8 < 8; ++c8)
+        if (a < NB && c8 < NB) L.S[(ti + SM_G * a) * SM_LD + tj + SM_G * c8] = e[a][c8];
+    // the reverse right-hand side [dl/dz; 0; 0] (the LU's forward sweep)
+    for (int i = t; i < SM_G * NB; i += SM_T) L.y[i] = i < n ? dl_dz[(size_t)b * n + i] : 0.0;
+    __syncthreads();
+    sm_lu_blocked(L, N, NB, bound, bad);
+  }
+#else
   double* stamp = out + n + m + p + 8;   // (SM_STAMPS only)
   switch ((N + SM_G - 1) / SM_G) {       // uniform
     case 1: sm_lu_from<0, 1>(e, L, N, ti, tj, bound, bad, stamp); break;
@@ -507,6 +665,7 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
     case 7: sm_lu_from<0, 7>(e, L, N, ti, tj, bound, bad, stamp); break;
     default: sm_lu_from<0, 8>(e, L, N, ti, tj, bound, bad, stamp); break;
   }
+#endif
   SM_STAMP(4);
 #ifdef SM_DEBUG
   if (bad) printf("small: t %d rejects (N %d bound %g piv0 %g)\n", t, N, bound, L.S[0]);
@@ -520,13 +679,9 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
   }
 #endif
   double* S = L.S;
-  for (int r = t; r < N; r += SM_T) L.dinv[r] = 1.0 / S[r * SM_LD + r];
-  // the factors to the K slab (the forward call's)
   double* Kb = K + (size_t)b * nmax * ld;
   const int lane = t & 63, wv = t >> 6;
-  for (int r = wv; r < N; r += SM_T / 64)
-    for (int c = lane; c < N; c += 64) Kb[(size_t)r * ld + c] = S[r * SM_LD + c];
-  if (t == 0) {
+  auto put_meta = [&]() {
     QPMeta mm = {};
     mm.nk = nk;
     mm.nsys = N;
@@ -534,13 +689,37 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
     mm.info = 0;
     mm.lu = LU_SMALL;   // not the batched route's factors (h.factored stays false: its solves never read them)
     meta[b] = mm;
+  };
+  double* y = L.y;
+#ifndef SM_LU_GROUPS
+  // L y = r ran with the LU: wave 0 solves U x = y while the other three
+  // write the factors to the K slab (the forward call's)
+  if (wv == 0) {
+    for (int r = lane; r < N; r += 64) L.dinv[r] = 1.0 / S[r * SM_LD + r];
+    sm_wave_sync();
+    double y0 = lane < N ? y[lane] : 0.0, y1 = lane + 64 < N ? y[lane + 64] : 0.0;
+    sm_usolve(S, L.dinv, N, lane, y0, y1);
+    if (lane < N) y[lane] = y0;
+    if (lane + 64 < N) y[lane + 64] = y1;
+  } else {
+    for (int r = wv - 1; r < N; r += SM_T / 64 - 1)
+      for (int c = lane; c < N; c += 64) Kb[(size_t)r * ld + c] = S[r * SM_LD + c];
+    if (t == 64) put_meta();
   }
+  __syncthreads();
+  SM_STAMP(5);
+  SM_STAMP(6);
+#else
+  for (int r = t; r < N; r += SM_T) L.dinv[r] = 1.0 / S[r * SM_LD + r];
+  // the factors to the K slab (the forward call's)
+  for (int r = wv; r < N; r += SM_T / 64)
+    for (int c = lane; c < N; c += 64) Kb[(size_t)r * ld + c] = S[r * SM_LD + c];
+  if (t == 0) put_meta();
   __syncthreads();
   SM_STAMP(5);
   // reverse: K x = [dl/dz; 0; 0] — L y = r, then U x = y, by wave 0 alone
   // with the vector in registers (entries lane and lane + 64): the pivot entry
   // comes by v_readlane, no barrier per step
-  double* y = L.y;
   if (wv == 0) {
     const double* db = dl_dz + (size_t)b * n;
     double y0 = lane < n ? db[lane] : 0.0, y1 = lane + 64 < n ? db[lane + 64] : 0.0;
@@ -551,6 +730,7 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
   }
   __syncthreads();
   SM_STAMP(6);
+#endif
   // outputs −[x_z | x_λ | x_ν]; eliminated rows x_λl = (0 − G_l·x_z)/s_l
   double* ob = out + (size_t)b * (n + m + p);
   const double* sb = s_out + (size_t)b * m;

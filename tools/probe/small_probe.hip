@@ -110,6 +110,22 @@ int main(int argc, char** argv) {
       }
     }
   printf("max rel diff %.3g\n", maxd);
+  {  // the reverse solve: x = K⁻¹[dl; 0; 0] by the host LU against −out[0 … n)
+    std::vector<double> x(N, 0.0), o(nmax + 16);
+    for (int i = 0; i < n; ++i) x[i] = dl[i];
+    for (int i = 0; i < N; ++i)
+      for (int k = 0; k < i; ++k) x[i] -= R[(size_t)i * N + k] * x[k];
+    for (int i = N - 1; i >= 0; --i) {
+      for (int k = i + 1; k < N; ++k) x[i] -= R[(size_t)i * N + k] * x[k];
+      x[i] /= R[(size_t)i * N + i];
+    }
+    hipMemcpy(o.data(), out, (nmax + 16) * 8, hipMemcpyDeviceToHost);
+    double xd = 0.0;
+    for (int i = 0; i < n; ++i) xd = std::fmax(xd, std::fabs(-o[i] - x[i]) / (1.0 + std::fabs(x[i])));
+    for (int e = 0; e < p; ++e)
+      xd = std::fmax(xd, std::fabs(-o[n + m + e] - x[n + nk + e]) / (1.0 + std::fabs(x[n + nk + e])));
+    printf("solve max rel diff %.3g\n", xd);
+  }
 #ifdef SM_STAMPS
   std::vector<double> o(nmax + 16);
   hipMemcpy(o.data(), out, (nmax + 16) * 8, hipMemcpyDeviceToHost);

@@ -1,10 +1,13 @@
 # Round 6 evidence, part A: configs 3, 2 (--lam-eps) and 6 at head, each with
-# its PMC traffic (the stale `traffic` fields of VERDICT r05 weak 10)
+# its PMC traffic (the stale `traffic` fields of VERDICT r05 weak 10); first the
+# small path's blocked LU (probe + tests)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 J=tools/gpu_job.sh
-TEST_PATHS="tests/test_qp_gpu.py tests/test_multi_rhs_gpu.py tests/test_nlp_gpu.py tests/test_lhs_solve_gpu.py tests/test_params_gpu.py" bash $J test \
+bash tools/r06_small_blk_job.sh \
+ && TEST_PATHS="tests/test_qp_small_gpu.py tests/test_qp_gpu.py tests/test_multi_rhs_gpu.py tests/test_nlp_gpu.py tests/test_lhs_solve_gpu.py tests/test_params_gpu.py" bash $J test \
  && cp gpurun_out/test.log gpurun_out/test_uinv.log \
+ && timeout -k 10 300 python3 -u tools/bench_dropin.py > gpurun_out/dropin.jsonl 2>gpurun_out/dropin.err \
  && bash $J bench cfg2 --no-cpu-baseline \
  && bash $J prof cfg2 --steps 20 --warmup 3 \
  && python3 tools/timeline.py gpurun_out/prof_cfg2 > gpurun_out/timeline_cfg2.txt \
