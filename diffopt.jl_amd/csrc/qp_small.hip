@@ -59,7 +59,12 @@ struct SmallLds {
       double colb[2][SM_GB][SM_MAX];   // block, double-buffered
       double dblk[2][SM_GB * SM_GB];
     };
-    double lw[SM_T / 64][256];   // reverse LU (16-blocks): each wave's copy of the diagonal block's L
+    struct {
+      double lw[SM_T / 64][256];   // reverse LU (16-blocks): each wave's copy of the diagonal block's L
+#ifdef SM_USWEEP_BLK
+      double uinv[SM_MAX / 16][16 * 17];   // ... and the diagonal blocks' U⁻¹ (rows padded to 17)
+#endif
+    };
   };
   double z[SM_MAX];           // z (rev) | scratch
   double y[SM_MAX];           // the solve vector
@@ -395,12 +400,24 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
       for (int j = 0; j < 16; ++j) a[j] = rin ? src[j] : 0.0;
     }
     double rv = rin ? L.y[r] : 0.0;
+#ifdef SM_USWEEP_BLK
+    // row `lane` of U_KK⁻¹ (lanes < 16), formed with the elimination: X·U = I
+    // row by row, U's row k being final (pr) at step k
+    double xi[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) xi[j] = j == lane ? 1.0 : 0.0;
+#endif
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       double pr[16];
 #pragma unroll
       for (int j = k; j < 16; ++j) pr[j] = sm_readlane(a[j], k);
       const double rq = 1.0 / pr[k];
+#ifdef SM_USWEEP_BLK
+      xi[k] *= rq;
+#pragma unroll
+      for (int j = k + 1; j < 16; ++j) xi[j] = fma(-xi[k], pr[j], xi[j]);
+#endif
       if (lane > k) {
         const double l = a[k] * rq;
         a[k] = l;
@@ -458,6 +475,10 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
     if (wv == 0 && lane < 16) {
       put_row();
       L.y[r] = rv;
+#ifdef SM_USWEEP_BLK
+#pragma unroll
+      for (int j = 0; j < 16; ++j) L.uinv[KK][lane * 17 + j] = xi[j];
+#endif
     }
     // ---- trailing update on MFMA: tile (I, C) −= L(I, KK)·U(KK, C)
     const int nt = NB - KK - 1;
@@ -582,6 +603,62 @@ __device__ __forceinline__ void sm_ltsolve(const double* S, const double* dinv, 
                                            double& y1) {
   sm_sweep<false, true, false>(S, dinv, N, lane, y0, y1);
 }
+#ifdef SM_USWEEP_BLK
+// U x = y by 16-blocks, backward, by one wave (entries lane / lane + 64):
+// x_K = U_KK⁻¹·y_K (the block's entries by v_readlane), then the rows above
+// take U(<K, K)·x_K — sixteen products per row, no step-by-step chain.
+__device__ __forceinline__ void sm_usolve_blk(const double* S, const double (*U)[16 * 17], int NB, int lane,
+                                              double& y0, double& y1) {
+  for (int KK = NB - 1; KK >= 0; --KK) {
+    const int k0 = 16 * KK, base = k0 & 63;
+    const bool hi = k0 >= 64;   // uniform
+    double yv[16];
+    {
+      const double src = hi ? y1 : y0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) yv[j] = sm_readlane(src, base + j);
+    }
+    const int i = lane - base;
+    const bool inb = i >= 0 && i < 16;
+    const double* ur = U[KK] + (inb ? i : 0) * 17;
+    double x0 = 0.0, x1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      x0 = fma(ur[j], yv[j], x0);
+      x1 = fma(ur[j + 1], yv[j + 1], x1);
+    }
+    if (inb) {
+      if (hi) y1 = x0 + x1;
+      else y0 = x0 + x1;
+    }
+    if (k0 == 0) break;
+    double xv[16];
+    {
+      const double src = hi ? y1 : y0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) xv[j] = sm_readlane(src, base + j);
+    }
+    const double* r0 = S + lane * SM_LD + k0;
+    double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      a0 = fma(r0[j], xv[j], a0);
+      a1 = fma(r0[j + 1], xv[j + 1], a1);
+    }
+    if (lane < k0) y0 -= a0 + a1;
+    if (k0 > 64) {
+      const double* r1 = S + (64 + lane) * SM_LD + k0;
+      double c0 = 0.0, c1 = 0.0;
+#pragma unroll
+      for (int j = 0; j < 16; j += 2) {
+        c0 = fma(r1[j], xv[j], c0);
+        c1 = fma(r1[j + 1], xv[j + 1], c1);
+      }
+      if (64 + lane < k0) y1 -= c0 + c1;
+    }
+  }
+}
+#endif
 
 #ifdef SM_STAMPS   // (tools/probe/small_probe.hip: thread 0's clock at phase marks, past the outputs)
 #define SM_STAMP(i) \
@@ -695,10 +772,14 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
   // L y = r ran with the LU: wave 0 solves U x = y while the other three
   // write the factors to the K slab (the forward call's)
   if (wv == 0) {
+    double y0 = lane < N ? y[lane] : 0.0, y1 = lane + 64 < N ? y[lane + 64] : 0.0;
+#ifdef SM_USWEEP_BLK
+    sm_usolve_blk(S, L.uinv, (N + SM_G - 1) / SM_G, lane, y0, y1);
+#else
     for (int r = lane; r < N; r += 64) L.dinv[r] = 1.0 / S[r * SM_LD + r];
     sm_wave_sync();
-    double y0 = lane < N ? y[lane] : 0.0, y1 = lane + 64 < N ? y[lane + 64] : 0.0;
     sm_usolve(S, L.dinv, N, lane, y0, y1);
+#endif
     if (lane < N) y[lane] = y0;
     if (lane + 64 < N) y[lane + 64] = y1;
   } else {
