@@ -195,6 +195,7 @@ int dopt_destroy(dopt_handle* h) {
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->meta_host) (void)hipHostFree(h->meta_host);
   if (h->pin) (void)hipHostFree(h->pin);
+  if (h->pin_ev) (void)hipEventDestroy(h->pin_ev);
   if (h->pin_out) (void)hipHostFree(h->pin_out);
   if (h->meta_ev) (void)hipEventDestroy(h->meta_ev);
   if (h->meta_fork) (void)hipEventDestroy(h->meta_fork);
@@ -289,6 +290,10 @@ struct PackIn {
 };
 static bool pack_in(Handle& h, const PackIn* in, int k, const void** out, DevBuf* dst = nullptr) {
   if (h.mem == DOPT_MEM_DEVICE) return false;
+  if (h.pin_pending) {   // a set_csc's copy out of the buffer may still be queued
+    DOPT_CHECK_HIP(hipEventSynchronize(h.pin_ev));
+    h.pin_pending = false;
+  }
   DevBuf& D = dst ? *dst : h.pack;
   size_t tot = 0;
   for (int i = 0; i < k; ++i) tot += (in[i].bytes + 15) & ~(size_t)15;
@@ -317,19 +322,46 @@ static bool pack_in(Handle& h, const PackIn* in, int k, const void** out, DevBuf
   return true;
 }
 
+// The checks csc_scatter_kernel makes, on the host (a small host-mode model:
+// cheaper than reading the device's verdict back): bit 1 a column range out of
+// order / bounds, bit 2 a row index out of range.
+static int host_csc_check(const int64_t* cp, const int64_t* rv, int64_t nnz, size_t rows, size_t ncols, size_t B) {
+  int err = 0;
+  for (size_t b = 0; b < B; ++b) {
+    const int64_t* c = cp + b * (ncols + 1);
+    for (size_t j = 0; j < ncols; ++j) {
+      const int64_t k0 = c[j] - 1, k1 = c[j + 1] - 1;
+      if (k0 < 0 || k1 < k0 || k1 > nnz) {
+        err |= 1;
+        continue;
+      }
+      for (int64_t k = k0; k < k1; ++k) {
+        const int64_t r = rv[k] - 1;
+        if (r < 0 || r >= (int64_t)rows) err |= 2;
+      }
+    }
+  }
+  return err;
+}
+
 // Pinned staging pays from a handle's third small call on (its hipHostMalloc
 // costs more than the pageable copies of a call or two save: a handle per
 // model — LHS then LHS' — stays pageable).
 static bool pin_ok(Handle& h) { return h.mem != DOPT_MEM_DEVICE && (h.pin_out || ++h.io_calls >= 3); }
 
-// The small path's pinned read-back buffer (the previous call's copy into it
-// is complete: every entry point synchronises before it returns).
+// The small path's pinned read-back buffer (the previous call's use of it is
+// complete: every entry point that uses it synchronises before it returns).
+// The small-path kernels read and write it in place, at pin_out_dev.
 static char* pin_out(Handle& h, size_t bytes) {
   if (h.pin_out_bytes < bytes) {
     if (h.pin_out) DOPT_CHECK_HIP(hipHostFree(h.pin_out));
     h.pin_out = nullptr;
+    h.pin_out_dev = nullptr;
     h.pin_out_bytes = 0;
     DOPT_CHECK_HIP(hipHostMalloc(&h.pin_out, bytes, hipHostMallocDefault));
+    void* dp = nullptr;
+    DOPT_CHECK_HIP(hipHostGetDevicePointer(&dp, h.pin_out, 0));
+    h.pin_out_dev = static_cast<char*>(dp);
     h.pin_out_bytes = bytes;
   }
   return static_cast<char*>(h.pin_out);
@@ -418,6 +450,17 @@ int dopt_qp_set_csc(dopt_handle* h,
     pin[10] = {z, B * n * sizeof(double)};
     pin[11] = {m ? lam : nullptr, m ? B * m * sizeof(double) : 0};
     pin[12] = {p ? nu : nullptr, p ? B * p * sizeof(double) : 0};
+    // a packed (small host-mode) model is validated here, so the call returns
+    // with its copy and scatter queued instead of reading the device's verdict
+    int hostv = -1;
+    size_t pbytes = 0;
+    for (const PackIn& q : pin) pbytes += q.bytes;
+    if (h->mem != DOPT_MEM_DEVICE && pbytes <= PACK_MAX / 2) {
+      hostv = 0;
+      for (int k = 0; k < 3; ++k)
+        if (mats[k].rows > 0) hostv |= host_csc_check(mats[k].cp, mats[k].rv, mats[k].nnz, mats[k].rows, n, B);
+      if (hostv) throw Error(-1, (hostv & 1) ? "CSC colptr is not monotone / out of range" : "CSC rowval out of range");
+    }
     const bool packed = pack_in(*h, pin, 13, pdev);
     for (int k = 0; k < 3; ++k) {
       const Mat& M = mats[k];
@@ -432,11 +475,14 @@ int dopt_qp_set_csc(dopt_handle* h,
                          d.as<double>(), err);
       dense[k] = d.as<double>();
     }
-    int herr = 0;
-    DOPT_CHECK_HIP(hipMemcpyAsync(&herr, err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
-    DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
-    if (herr) throw Error(-1, (herr & 1) ? "CSC colptr is not monotone / out of range"
-                                         : "CSC rowval out of range");
+    const bool async = packed && hostv == 0;
+    if (!async) {
+      int herr = 0;
+      DOPT_CHECK_HIP(hipMemcpyAsync(&herr, err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+      if (herr) throw Error(-1, (herr & 1) ? "CSC colptr is not monotone / out of range"
+                                           : "CSC rowval out of range");
+    }
     h->Q = dense[0];
     h->G = m ? dense[1] : nullptr;
     h->A = p ? dense[2] : nullptr;
@@ -453,6 +499,12 @@ int dopt_qp_set_csc(dopt_handle* h,
     }
     h->set = true;
     h->factored = false;
+    if (async) {   // the inputs are in the pinned buffer: nothing of the caller's is read later
+      if (!h->pin_ev) DOPT_CHECK_HIP(hipEventCreateWithFlags(&h->pin_ev, hipEventDisableTiming));
+      DOPT_CHECK_HIP(hipEventRecord(h->pin_ev, h->stream));
+      h->pin_pending = true;
+      return 0;
+    }
     DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
     return 0;
   });
@@ -544,37 +596,51 @@ int dopt_qp_reverse(dopt_handle* h, const double* dl_dz, double* out) {
       return 0;
     }
     // a model not yet factorised, batch of a few: the one-launch small path
-    // (qp_small.hip), its traffic one copy each way in host mode (the seed
-    // through the pinned pack; the outputs with the per-problem flags after
-    // them); anything it cannot take runs the batched route below
+    // (qp_small.hip); in host mode from a handle's third call on no copy at
+    // all — the kernel reads the seed from and writes the outputs and the
+    // per-problem flags to the pinned read-back buffer (the first calls: one
+    // copy each way); anything it cannot take runs the batched route below
     if (!h->factored && dopt::qp_small_eligible(*h)) {
       const size_t ob = B * L * sizeof(double), fb = B * sizeof(int32_t);
       const bool pinned = pin_ok(*h);
-      std::vector<char> page;   // (a handle's first call: pageable)
-      if (host) {
-        const PackIn pi[1] = {{dl_dz, B * n * sizeof(double)}};
-        const void* pd[1];
-        d = pinned && pack_in(*h, pi, 1, pd, &h->tpack) ? static_cast<const double*>(pd[0])
-                                                        : stage_in(*h, h->tin[0], dl_dz, B * n);
-        h->tout[0].ensure(ob + fb);
-      } else {
-        d = dl_dz;
-        h->csc_err.ensure(fb);
+      if (host && pinned) {
+        const size_t so = (ob + fb + 15) & ~(size_t)15;
+        char* pz = pin_out(*h, so + B * n * sizeof(double));
+        std::memcpy(pz + so, dl_dz, B * n * sizeof(double));
+        const int32_t* hf = reinterpret_cast<const int32_t*>(pz + ob);
+        char* pd = h->pin_out_dev;
+        dopt::qp_small_reverse(*h, reinterpret_cast<const double*>(pd + so), reinterpret_cast<double*>(pd),
+                               reinterpret_cast<int32_t*>(pd + ob));
+        DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+        h->small_ready = std::all_of(hf, hf + B, [](int32_t f) { return f == 0; });
+        if (h->small_ready) {
+          std::memcpy(out, pz, ob);
+          h->last_time = tm.s();
+          return 0;
+        }
       }
-      double* o = host ? h->tout[0].as<double>() : out;
-      int32_t* flags = host ? reinterpret_cast<int32_t*>(h->tout[0].as<char>() + ob) : h->csc_err.as<int32_t>();
-      dopt::qp_small_reverse(*h, d, o, flags);
-      if (!pinned) page.resize(host ? ob + fb : fb);
-      char* pin = pinned ? pin_out(*h, host ? ob + fb : fb) : page.data();
-      DOPT_CHECK_HIP(hipMemcpyAsync(pin, host ? static_cast<const void*>(o) : static_cast<const void*>(flags),
-                                    host ? ob + fb : fb, hipMemcpyDeviceToHost, h->stream));
-      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
-      const int32_t* hf = reinterpret_cast<const int32_t*>(pin + (host ? ob : 0));
-      h->small_ready = std::all_of(hf, hf + B, [](int32_t f) { return f == 0; });
-      if (h->small_ready) {
-        if (host) std::memcpy(out, pin, ob);
-        h->last_time = tm.s();
-        return 0;
+      if (!(host && pinned)) {   // a handle's first calls (pageable), device mode
+        if (host) {
+          d = stage_in(*h, h->tin[0], dl_dz, B * n);
+          h->tout[0].ensure(ob + fb);
+        } else {
+          d = dl_dz;
+          h->csc_err.ensure(fb);
+        }
+        double* o = host ? h->tout[0].as<double>() : out;
+        int32_t* flags = host ? reinterpret_cast<int32_t*>(h->tout[0].as<char>() + ob) : h->csc_err.as<int32_t>();
+        dopt::qp_small_reverse(*h, d, o, flags);
+        std::vector<char> page(host ? ob + fb : fb);
+        DOPT_CHECK_HIP(hipMemcpyAsync(page.data(), host ? static_cast<const void*>(o) : static_cast<const void*>(flags),
+                                      page.size(), hipMemcpyDeviceToHost, h->stream));
+        DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+        const int32_t* hf = reinterpret_cast<const int32_t*>(page.data() + (host ? ob : 0));
+        h->small_ready = std::all_of(hf, hf + B, [](int32_t f) { return f == 0; });
+        if (h->small_ready) {
+          if (host) std::memcpy(out, page.data(), ob);
+          h->last_time = tm.s();
+          return 0;
+        }
       }
     }
     if (!d) d = stage_in(*h, h->tin[0], dl_dz, B * n);
@@ -594,21 +660,19 @@ int dopt_qp_forward(dopt_handle* h, const double* dQ, const double* dq, const do
     if (!out) throw Error(-1, "out is required");
     Timer tm;
     const size_t B = h->batch, n = h->n, m = h->m, p = h->p, L = n + m + p;
-    if (!h->sparse && !h->factored && h->small_ready && pin_ok(*h)) {   // the small path's factors (dopt_qp_reverse): one copy each way
+    if (!h->sparse && !h->factored && h->small_ready && pin_ok(*h)) {   // the small path's factors (dopt_qp_reverse): one copy in
       const PackIn pi[6] = {{dQ, B * n * n * sizeof(double)}, {dq, B * n * sizeof(double)},
                             {m ? dG : nullptr, B * m * n * sizeof(double)}, {m ? dh : nullptr, B * m * sizeof(double)},
                             {p ? dA : nullptr, B * p * n * sizeof(double)}, {p ? db : nullptr, B * p * sizeof(double)}};
       const void* pd[6];
       if (pack_in(*h, pi, 6, pd, &h->tpack)) {
+        // the outputs straight into the pinned read-back buffer (no copy)
         const size_t ob = B * L * sizeof(double);
-        h->tout[1].ensure(ob);
-        double* o = h->tout[1].as<double>();
+        char* pin = pin_out(*h, ob);
         dopt::qp_small_forward(*h, dopt::FwdTangents{static_cast<const double*>(pd[0]), static_cast<const double*>(pd[1]),
                                                      static_cast<const double*>(pd[2]), static_cast<const double*>(pd[3]),
                                                      static_cast<const double*>(pd[4]), static_cast<const double*>(pd[5])},
-                               o);
-        char* pin = pin_out(*h, ob);
-        DOPT_CHECK_HIP(hipMemcpyAsync(pin, o, ob, hipMemcpyDeviceToHost, h->stream));
+                               reinterpret_cast<double*>(h->pin_out_dev));
         DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
         std::memcpy(out, pin, ob);
         h->last_time = tm.s();

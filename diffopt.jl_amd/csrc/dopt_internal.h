@@ -162,6 +162,11 @@ struct Handle {
   // copy (dopt_qp_set_csc of a batch-1 model: 13 copies → 1)
   void* pin = nullptr;
   size_t pin_bytes = 0;
+  // dopt_qp_set_csc of a small host-mode model returns with its copy out of
+  // `pin` queued (validated on the host, nothing to read back): the next
+  // pack waits for this event before it writes the buffer again
+  hipEvent_t pin_ev = nullptr;
+  bool pin_pending = false;
   DevBuf pack;
   // the small path's per-call traffic (abi.hip): the tangents packed like the
   // inputs (into tpack: pack stays the inputs' home), the outputs and the
@@ -169,6 +174,7 @@ struct Handle {
   DevBuf tpack;
   DevBuf rpack;              // dopt_lhs_resolve's right-hand sides (tpack may hold the plug point's M)
   void* pin_out = nullptr;
+  char* pin_out_dev = nullptr;   // its device address (the small path's kernels read / write it directly)
   size_t pin_out_bytes = 0;
   int io_calls = 0;          // small-path calls so far (abi.hip pin_ok: pinned from the third on)
   DevBuf csc_in[9], csc_in_val[3], csc_err;   // host-mode copies of CSC colptr / rowval / nzval

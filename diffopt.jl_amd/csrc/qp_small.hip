@@ -61,7 +61,7 @@ struct SmallLds {
     };
     struct {
       double lw[SM_T / 64][256];   // reverse LU (16-blocks): each wave's copy of the diagonal block's L
-#ifdef SM_USWEEP_BLK
+#ifndef SM_USWEEP_STEPS
       double uinv[SM_MAX / 16][16 * 17];   // ... and the diagonal blocks' U⁻¹ (rows padded to 17)
 #endif
     };
@@ -400,24 +400,12 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
       for (int j = 0; j < 16; ++j) a[j] = rin ? src[j] : 0.0;
     }
     double rv = rin ? L.y[r] : 0.0;
-#ifdef SM_USWEEP_BLK
-    // row `lane` of U_KK⁻¹ (lanes < 16), formed with the elimination: X·U = I
-    // row by row, U's row k being final (pr) at step k
-    double xi[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) xi[j] = j == lane ? 1.0 : 0.0;
-#endif
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       double pr[16];
 #pragma unroll
       for (int j = k; j < 16; ++j) pr[j] = sm_readlane(a[j], k);
       const double rq = 1.0 / pr[k];
-#ifdef SM_USWEEP_BLK
-      xi[k] *= rq;
-#pragma unroll
-      for (int j = k + 1; j < 16; ++j) xi[j] = fma(-xi[k], pr[j], xi[j]);
-#endif
       if (lane > k) {
         const double l = a[k] * rq;
         a[k] = l;
@@ -475,10 +463,6 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
     if (wv == 0 && lane < 16) {
       put_row();
       L.y[r] = rv;
-#ifdef SM_USWEEP_BLK
-#pragma unroll
-      for (int j = 0; j < 16; ++j) L.uinv[KK][lane * 17 + j] = xi[j];
-#endif
     }
     // ---- trailing update on MFMA: tile (I, C) −= L(I, KK)·U(KK, C)
     const int nt = NB - KK - 1;
@@ -603,62 +587,182 @@ __device__ __forceinline__ void sm_ltsolve(const double* S, const double* dinv, 
                                            double& y1) {
   sm_sweep<false, true, false>(S, dinv, N, lane, y0, y1);
 }
-#ifdef SM_USWEEP_BLK
+#ifndef SM_USWEEP_STEPS
+// The diagonal blocks' U_KK⁻¹ from the image into U (rows padded to 17):
+// waves 0 / 1, four 16-lane groups each, lane i row i of X (X·U = I).
+__device__ __forceinline__ void sm_uinv(const double* S, int NB, double (*U)[16 * 17]) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, i = lane & 15;
+  const int KK = 4 * wv + (lane >> 4);
+  if (wv >= 2 || KK >= NB) return;
+  const double* D = S + 16 * KK * SM_LD + 16 * KK;
+  double x[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) x[j] = j == i ? 1.0 : 0.0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    double acc = x[j];
+#pragma unroll
+    for (int q = 0; q < j; ++q) acc = fma(-x[q], D[q * SM_LD + j], acc);
+    x[j] = acc / D[j * SM_LD + j];
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) U[KK][i * 17 + j] = x[j];
+}
+
 // U x = y by 16-blocks, backward, by one wave (entries lane / lane + 64):
-// x_K = U_KK⁻¹·y_K (the block's entries by v_readlane), then the rows above
-// take U(<K, K)·x_K — sixteen products per row, no step-by-step chain.
+// x_K = U_KK⁻¹·y_K, then the rows above take U(<K, K)·x_K — sixteen products
+// per row, no step-by-step chain.  The block's entries reach every lane as LDS
+// broadcasts through `sc` (16 doubles; v_readlane here spilled 600 SGPRs).
 __device__ __forceinline__ void sm_usolve_blk(const double* S, const double (*U)[16 * 17], int NB, int lane,
-                                              double& y0, double& y1) {
+                                              double& y0, double& y1, double* sc) {
   for (int KK = NB - 1; KK >= 0; --KK) {
     const int k0 = 16 * KK, base = k0 & 63;
     const bool hi = k0 >= 64;   // uniform
-    double yv[16];
-    {
-      const double src = hi ? y1 : y0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) yv[j] = sm_readlane(src, base + j);
-    }
     const int i = lane - base;
     const bool inb = i >= 0 && i < 16;
+    if (inb) sc[i] = hi ? y1 : y0;
+    sm_wave_sync();
     const double* ur = U[KK] + (inb ? i : 0) * 17;
     double x0 = 0.0, x1 = 0.0;
 #pragma unroll
     for (int j = 0; j < 16; j += 2) {
-      x0 = fma(ur[j], yv[j], x0);
-      x1 = fma(ur[j + 1], yv[j + 1], x1);
+      x0 = fma(ur[j], sc[j], x0);
+      x1 = fma(ur[j + 1], sc[j + 1], x1);
     }
+    sm_wave_sync();
     if (inb) {
-      if (hi) y1 = x0 + x1;
-      else y0 = x0 + x1;
+      const double x = x0 + x1;
+      sc[i] = x;
+      if (hi) y1 = x;
+      else y0 = x;
     }
+    sm_wave_sync();
     if (k0 == 0) break;
-    double xv[16];
-    {
-      const double src = hi ? y1 : y0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) xv[j] = sm_readlane(src, base + j);
-    }
     const double* r0 = S + lane * SM_LD + k0;
-    double a0 = 0.0, a1 = 0.0;
+    const double* r1 = S + (64 + lane) * SM_LD + k0;
+    double a0 = 0.0, a1 = 0.0, c0 = 0.0, c1 = 0.0;
 #pragma unroll
     for (int j = 0; j < 16; j += 2) {
-      a0 = fma(r0[j], xv[j], a0);
-      a1 = fma(r0[j + 1], xv[j + 1], a1);
+      a0 = fma(r0[j], sc[j], a0);
+      a1 = fma(r0[j + 1], sc[j + 1], a1);
+      if (k0 > 64) {
+        c0 = fma(r1[j], sc[j], c0);
+        c1 = fma(r1[j + 1], sc[j + 1], c1);
+      }
     }
     if (lane < k0) y0 -= a0 + a1;
-    if (k0 > 64) {
-      const double* r1 = S + (64 + lane) * SM_LD + k0;
-      double c0 = 0.0, c1 = 0.0;
-#pragma unroll
-      for (int j = 0; j < 16; j += 2) {
-        c0 = fma(r1[j], xv[j], c0);
-        c1 = fma(r1[j + 1], xv[j + 1], c1);
-      }
-      if (64 + lane < k0) y1 -= c0 + c1;
-    }
+    if (64 + lane < k0) y1 -= c0 + c1;
+    sm_wave_sync();
   }
 }
 #endif
+
+// The forward kernel's diagonal-block inverses, in place: after this the
+// diagonal 16-blocks of the image hold L_KK⁻¹ strictly below the diagonal
+// (its unit diagonal implied) and U_KK⁻¹ on and above it.  Sixteen blocks at
+// once — four 16-lane groups per wave, waves 0 / 1 the U inverses (lane i: row
+// i of X, X·U = I), waves 2 / 3 the L inverses (lane i: column i of Y, L·Y =
+// I) — into registers, then stored after a barrier.
+__device__ __forceinline__ void sm_diag_inverses(double* S, int NB) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, i = lane & 15;
+  const int KK = 4 * (wv & 1) + (lane >> 4);
+  const bool act = KK < NB;
+  const int k0 = 16 * (act ? KK : 0);
+  const double* D = S + k0 * SM_LD + k0;
+  double x[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) x[j] = j == i ? 1.0 : 0.0;
+  if (wv < 2) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      double acc = x[j];
+#pragma unroll
+      for (int q = 0; q < j; ++q) acc = fma(-x[q], D[q * SM_LD + j], acc);
+      x[j] = acc / D[j * SM_LD + j];
+    }
+  } else {
+#pragma unroll
+    for (int r = 1; r < 16; ++r) {
+      double acc = x[r];
+#pragma unroll
+      for (int k = 0; k < r; ++k) acc = fma(-D[r * SM_LD + k], x[k], acc);
+      x[r] = acc;
+    }
+  }
+  __syncthreads();
+  if (act) {
+    double* W = S + k0 * SM_LD + k0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (wv < 2 && j >= i) W[i * SM_LD + j] = x[j];
+      if (wv >= 2 && j > i) W[j * SM_LD + i] = x[j];
+    }
+  }
+  __syncthreads();
+}
+
+// Kᵀx = r by 16-blocks with the in-place inverses, one wave (entries lane /
+// lane + 64): Uᵀ w = r forward, w_K = U_KK⁻ᵀ·r_K and the rows past the block
+// take U(K, >K)ᵀ·w_K; then Lᵀ x = w backward likewise — sixteen products per
+// row and block, no step-by-step chain.  NP = 16·NB rows (identity padding).
+__device__ __forceinline__ void sm_fwd_sweeps_blk(const double* S, int NB, int lane, double& y0, double& y1) {
+  const int NP = 16 * NB;
+  auto blk = [&](int k0, bool upper) {   // the block's solve with its inverse, in place
+    const int base = k0 & 63;
+    const bool hi = k0 >= 64;
+    double rv[16];
+    const double src = hi ? y1 : y0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) rv[j] = sm_readlane(src, base + j);
+    const int i = lane - base;
+    const bool inb = i >= 0 && i < 16;
+    const int ic = inb ? i : 0;
+    double w0 = 0.0, w1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      // (U_KK⁻¹)_{ji}, j ≤ i; or (L_KK⁻¹)_{ji}, j ≥ i, unit diagonal
+      const double sv = S[(k0 + j) * SM_LD + k0 + ic];
+      const double c = upper ? (j <= ic ? sv : 0.0) : (j == ic ? 1.0 : (j > ic ? sv : 0.0));
+      if (j & 1) w1 = fma(c, rv[j], w1);
+      else w0 = fma(c, rv[j], w0);
+    }
+    if (inb) {
+      if (hi) y1 = w0 + w1;
+      else y0 = w0 + w1;
+    }
+  };
+  auto rows = [&](int k0, bool after) {   // the other rows: r_i −= Σ_j S(k0 + j, i)·x_j
+    const int base = k0 & 63;
+    const bool hi = k0 >= 64;
+    double xv[16];
+    const double src = hi ? y1 : y0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) xv[j] = sm_readlane(src, base + j);
+    double a0 = 0.0, a1 = 0.0, c0 = 0.0, c1 = 0.0;
+    const bool two = NP > 64;   // uniform
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const double* row = S + (k0 + j) * SM_LD;
+      if (j & 1) a1 = fma(row[lane], xv[j], a1);
+      else a0 = fma(row[lane], xv[j], a0);
+      if (two) {
+        if (j & 1) c1 = fma(row[64 + lane], xv[j], c1);
+        else c0 = fma(row[64 + lane], xv[j], c0);
+      }
+    }
+    const int e = after ? k0 + 16 : k0;
+    if (after ? lane >= e : lane < e) y0 -= a0 + a1;
+    if (two && (after ? 64 + lane >= e : 64 + lane < e)) y1 -= c0 + c1;
+  };
+  for (int KK = 0; KK < NB; ++KK) {
+    blk(16 * KK, true);
+    if (KK + 1 < NB) rows(16 * KK, true);
+  }
+  for (int KK = NB - 1; KK >= 0; --KK) {
+    blk(16 * KK, false);
+    if (KK > 0) rows(16 * KK, false);
+  }
+}
 
 #ifdef SM_STAMPS   // (tools/probe/small_probe.hip: thread 0's clock at phase marks, past the outputs)
 #define SM_STAMP(i) \
@@ -771,10 +875,14 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
 #ifndef SM_LU_GROUPS
   // L y = r ran with the LU: wave 0 solves U x = y while the other three
   // write the factors to the K slab (the forward call's)
+#ifndef SM_USWEEP_STEPS
+  sm_uinv(S, (N + SM_G - 1) / SM_G, L.uinv);
+  __syncthreads();
+#endif
   if (wv == 0) {
     double y0 = lane < N ? y[lane] : 0.0, y1 = lane + 64 < N ? y[lane + 64] : 0.0;
-#ifdef SM_USWEEP_BLK
-    sm_usolve_blk(S, L.uinv, (N + SM_G - 1) / SM_G, lane, y0, y1);
+#ifndef SM_USWEEP_STEPS
+    sm_usolve_blk(S, L.uinv, (N + SM_G - 1) / SM_G, lane, y0, y1, L.dinv);
 #else
     for (int r = lane; r < N; r += 64) L.dinv[r] = 1.0 / S[r * SM_LD + r];
     sm_wave_sync();
@@ -860,7 +968,9 @@ __global__ __launch_bounds__(SM_T) void qp_small_fwd_kernel(QPIn P, FwdTangents 
   const int lane = t & 63, wv = t >> 6;
   // the factors into LDS: rows by wave, 8 rows × 2 column halves per round,
   // all sixteen loads in flight before any store
-  for (int r0 = wv; r0 < N; r0 += 8 * (SM_T / 64)) {
+  // (the 16-block padding past N as the identity)
+  const int NP = (N + SM_G - 1) / SM_G * SM_G;
+  for (int r0 = wv; r0 < NP; r0 += 8 * (SM_T / 64)) {
     double v[8][2];
 #pragma unroll
     for (int u = 0; u < 8; ++u)
@@ -874,11 +984,11 @@ __global__ __launch_bounds__(SM_T) void qp_small_fwd_kernel(QPIn P, FwdTangents 
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int r = r0 + u * (SM_T / 64), c = lane + 64 * hh;
-        if (r < N && c < N) S[r * SM_LD + c] = v[u][hh];
+        if (r < NP && c < NP) S[r * SM_LD + c] = r < N && c < N ? v[u][hh] : (r == c ? 1.0 : 0.0);
       }
   }
   __syncthreads();
-  for (int r = t; r < N; r += SM_T) L.dinv[r] = 1.0 / S[r * SM_LD + r];
+  sm_diag_inverses(S, NP / SM_G);
   // the full forward right-hand side r (QuadraticProgram.jl:429-433):
   //   [dQ z + dq + dGᵀλ + dAᵀν; λ.*(dG z) − λ.*dh; dA z − db] — r1 and r3 in
   // y (reduced positions), r2 kept in registers per row for the recovery
@@ -921,11 +1031,10 @@ __global__ __launch_bounds__(SM_T) void qp_small_fwd_kernel(QPIn P, FwdTangents 
     if (kk >= 0) y[n + kk] = r2(l);
   }
   __syncthreads();
-  // Kᵀ x = r: Uᵀ w = r, then Lᵀ x = w, by wave 0 (as the reverse kernel)
+  // Kᵀ x = r: Uᵀ w = r, then Lᵀ x = w, by wave 0, by 16-blocks
   if (wv == 0) {
     double y0 = lane < N ? y[lane] : 0.0, y1 = lane + 64 < N ? y[lane + 64] : 0.0;
-    sm_utsolve(S, L.dinv, N, lane, y0, y1);
-    sm_ltsolve(S, L.dinv, N, lane, y0, y1);
+    sm_fwd_sweeps_blk(S, NP / SM_G, lane, y0, y1);
     if (lane < N) y[lane] = y0;
     if (lane + 64 < N) y[lane + 64] = y1;
   }

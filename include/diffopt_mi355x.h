@@ -119,7 +119,11 @@ int dopt_qp_lsqr_stats(dopt_handle* h, int32_t* stats);
  * concatenated X_rowval / X_nzval of X_nnz entries; all three matrices have n
  * columns (Q n×n symmetrised, G m×n, A p×n).  The library densifies on the
  * device (zero fill + scatter); a malformed colptr / rowval returns −1.
- * Host mode copies the CSC arrays, device mode borrows them. */
+ * Host mode copies the CSC arrays, device mode borrows them.  A small
+ * host-mode model (its arrays packed into the handle's pinned buffer) is
+ * validated on the host and the call returns with the copy and the scatter
+ * queued on the handle's stream: the caller's arrays are already copied, and
+ * every later call on the handle is ordered after them. */
 int dopt_qp_set_csc(dopt_handle* h,
                     const int64_t* Q_colptr, const int64_t* Q_rowval, const double* Q_nzval, int64_t Q_nnz,
                     const int64_t* G_colptr, const int64_t* G_rowval, const double* G_nzval, int64_t G_nnz,

@@ -198,3 +198,47 @@ def test_small_path_reused_handle(QPBatch):
             if not (it == 3 and b == 1):   # (the LSQR branch's forward: as test_small_path_fallbacks, reverse only)
                 assert relfro(fwd[b], ref_f) <= RTOL
     e.close()
+
+
+def test_small_path_csc_handle_reuse(QPBatch):
+    """The Julia QPModel's exact sequence on one handle — dopt_qp_set_csc of
+    the MOI form, reverse, forward — for successive models: from the third
+    call on set_csc validates on the host and returns with its copy queued,
+    and the small kernels read the seed from / write the outputs into the
+    pinned read-back buffer in place.  Every model against the oracle; a set
+    overwritten before any call (the queued copy of the first waits before
+    the pinned buffer is written again) solves the second model; a malformed
+    CSC raises on the host and leaves no model; a good set afterwards works."""
+    import scipy.sparse as sp
+    from diffopt_amd import EngineError
+    n, m, p = 50, 80, 30
+    e = QPBatch(1, n, m, p)
+
+    def put(d):
+        e.set_csc([sp.csc_matrix(d["Q"][0])], [sp.csc_matrix(d["G"][0])], d["h"], [sp.csc_matrix(d["A"][0])],
+                  d["z"], d["lam"], d["nu"])
+
+    def check(d):
+        rev = e.reverse(d["dl_dz"])
+        assert (e.lu_kind() == SMALL).all()
+        fwd = e.forward(dq=d["dq"], dh=d["dh"], db=d["db"])
+        ref_r, ref_f = _oracle(d, 0, p)
+        assert relfro(rev[0], ref_r) <= RTOL and relfro(fwd[0], ref_f) <= RTOL
+
+    for it in range(5):
+        d = _data(1, n, m, p, 0.2, 9300 + it)
+        put(d)
+        check(d)
+    d1, d2 = _data(1, n, m, p, 0.2, 9400), _data(1, n, m, p, 0.2, 9401)
+    put(d1)
+    put(d2)               # no call between the two sets
+    check(d2)
+    bad = sp.csc_matrix(d1["G"][0])
+    bad.indices[0] = 999  # row index out of range
+    with pytest.raises(EngineError, match="rowval out of range"):
+        e.set_csc([sp.csc_matrix(d1["Q"][0])], [bad], d1["h"], [sp.csc_matrix(d1["A"][0])], d1["z"], d1["lam"], d1["nu"])
+    with pytest.raises(EngineError):
+        e.reverse(d1["dl_dz"])
+    put(d1)
+    check(d1)
+    e.close()
