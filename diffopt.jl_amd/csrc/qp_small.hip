@@ -383,8 +383,14 @@ typedef double sm_d4 __attribute__((ext_vector_type(4)));
 // v_readlane from the diagonal lane k), so the rows below take their
 // L(I, KK)·y_KK with the elimination and no separate forward sweep is run.
 // The 16-block padding of the system past N is the identity (assembled so).
-__device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double bound, int& bad) {
+__device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double bound, int& bad, double* stamp) {
   double* S = L.S;
+#ifdef SM_STAMPS
+  long long q_[4] = {0, 0, 0, 0}, c_ = clock64(), d_;
+#define SB_LAP(i) d_ = clock64(), q_[i] += d_ - c_, c_ = d_
+#else
+#define SB_LAP(i)
+#endif
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
   const int NP = 16 * NB;
   double* Lw = L.lw[wv];   // this wave's copy of L_KK, column-major (L_ik at 16k + i)
@@ -405,6 +411,17 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
       double pr[16];
 #pragma unroll
       for (int j = k; j < 16; ++j) pr[j] = sm_readlane(a[j], k);
+#ifdef SM_PANEL_RCP
+      // 1/u_kk by v_rcp_f64 and two Newton steps, the rows at or above k
+      // untouched by a zero multiplier (no branch on the chain)
+      double rq = __builtin_amdgcn_rcp(pr[k]);
+      rq = fma(fma(-pr[k], rq, 1.0), rq, rq);
+      rq = fma(fma(-pr[k], rq, 1.0), rq, rq);
+      const double l = lane > k ? a[k] * rq : 0.0;
+      a[k] = lane > k ? l : a[k];
+#pragma unroll
+      for (int j = k + 1; j < 16; ++j) a[j] = fma(-l, pr[j], a[j]);
+#else
       const double rq = 1.0 / pr[k];
       if (lane > k) {
         const double l = a[k] * rq;
@@ -412,6 +429,7 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
 #pragma unroll
         for (int j = k + 1; j < 16; ++j) a[j] = fma(-l, pr[j], a[j]);
       }
+#endif
     }
     // the forward sweep's block: y_k from lane k once final, the rows below it
 #pragma unroll
@@ -442,6 +460,7 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
 #pragma unroll
       for (int j = 0; j < 16; ++j) Lw[16 * j + lane] = j < lane ? a[j] : 0.0;
     sm_wave_sync();
+    SB_LAP(0);
     // ---- U row: columns k0 + 16 + q, q = wv + 4·lane
     const int ncol = NP - k0 - 16;
     const int c = k0 + 16 + wv + 4 * lane;
@@ -459,13 +478,49 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
         if (k0 + i < N && c < N) bad |= !(fabs(u[i]) <= bound);
       }
     }
+    SB_LAP(1);
     __syncthreads();
     if (wv == 0 && lane < 16) {
       put_row();
       L.y[r] = rv;
     }
+    SB_LAP(2);
     // ---- trailing update on MFMA: tile (I, C) −= L(I, KK)·U(KK, C)
     const int nt = NB - KK - 1;
+#ifdef SM_TRAIL2
+    // two tiles per wave at a time: two independent MFMA chains, every LDS
+    // operand of both loaded before the first MFMA
+    for (int tt = wv; tt < nt * nt; tt += 2 * (SM_T / 64)) {
+      const int tu = tt + SM_T / 64;
+      const bool two = tu < nt * nt;   // uniform
+      const int i0 = k0 + 16 + 16 * (tt / nt), j0 = k0 + 16 + 16 * (tt % nt);
+      const int i1 = k0 + 16 + 16 * ((two ? tu : tt) / nt), j1 = k0 + 16 + 16 * ((two ? tu : tt) % nt);
+      sm_d4 acc0, acc1;
+      double av0[4], bv0[4], av1[4], bv1[4];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        acc0[rr] = S[(i0 + g + 4 * rr) * SM_LD + j0 + l16];
+        acc1[rr] = S[(i1 + g + 4 * rr) * SM_LD + j1 + l16];
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        av0[s2] = -S[(i0 + l16) * SM_LD + k0 + 4 * s2 + g];
+        bv0[s2] = S[(k0 + 4 * s2 + g) * SM_LD + j0 + l16];
+        av1[s2] = -S[(i1 + l16) * SM_LD + k0 + 4 * s2 + g];
+        bv1[s2] = S[(k0 + 4 * s2 + g) * SM_LD + j1 + l16];
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av0[s2], bv0[s2], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av1[s2], bv1[s2], acc1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        S[(i0 + g + 4 * rr) * SM_LD + j0 + l16] = acc0[rr];
+        if (two) S[(i1 + g + 4 * rr) * SM_LD + j1 + l16] = acc1[rr];
+      }
+    }
+#else
     for (int tt = wv; tt < nt * nt; tt += SM_T / 64) {
       const int i0 = k0 + 16 + 16 * (tt / nt), j0 = k0 + 16 + 16 * (tt % nt);
       sm_d4 acc;
@@ -480,8 +535,15 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) S[(i0 + g + 4 * rr) * SM_LD + j0 + l16] = acc[rr];
     }
+#endif
     __syncthreads();
+    SB_LAP(3);
   }
+#ifdef SM_STAMPS
+  if (threadIdx.x == 0)
+    for (int i = 0; i < 4; ++i) stamp[i] += (double)q_[i];
+#endif
+#undef SB_LAP
 }
 
 // One sweep over the LU image by one wave, vector entry i in lane i & 63,
@@ -832,7 +894,7 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
     // the reverse right-hand side [dl/dz; 0; 0] (the LU's forward sweep)
     for (int i = t; i < SM_G * NB; i += SM_T) L.y[i] = i < n ? dl_dz[(size_t)b * n + i] : 0.0;
     __syncthreads();
-    sm_lu_blocked(L, N, NB, bound, bad);
+    sm_lu_blocked(L, N, NB, bound, bad, out + n + m + p + 8);
   }
 #else
   double* stamp = out + n + m + p + 8;   // (SM_STAMPS only)
@@ -879,6 +941,7 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
   sm_uinv(S, (N + SM_G - 1) / SM_G, L.uinv);
   __syncthreads();
 #endif
+  SM_STAMP(5);
   if (wv == 0) {
     double y0 = lane < N ? y[lane] : 0.0, y1 = lane + 64 < N ? y[lane + 64] : 0.0;
 #ifndef SM_USWEEP_STEPS
@@ -896,7 +959,6 @@ __device__ __forceinline__ void sm_reverse(const QPIn& P, const double* __restri
     if (t == 64) put_meta();
   }
   __syncthreads();
-  SM_STAMP(5);
   SM_STAMP(6);
 #else
   for (int r = t; r < N; r += SM_T) L.dinv[r] = 1.0 / S[r * SM_LD + r];

@@ -66,6 +66,10 @@ int main(int argc, char** argv) {
   hipMemcpy(&hf, flag, 4, hipMemcpyDeviceToHost);
   hipMemcpy(&hm, meta, sizeof(hm), hipMemcpyDeviceToHost);
   const int N = hm.nsys, nk = hm.nk;
+  if (hf && (N <= 0 || N > 128)) {   // the prepare kernel's rejection: no meta, no factors
+    printf("kernel %.1f us, flag %d (not taken: N' > 128 or Q = 0)\n", ms * 1e3, hf);
+    return 0;
+  }
   std::vector<double> Kg((size_t)nmax * ld);
   hipMemcpy(Kg.data(), K, Kg.size() * 8, hipMemcpyDeviceToHost);
   printf("kernel %.1f us, flag %d, N %d nk %d\n", ms * 1e3, hf, N, nk);
@@ -129,10 +133,15 @@ int main(int argc, char** argv) {
 #ifdef SM_STAMPS
   std::vector<double> o(nmax + 16);
   hipMemcpy(o.data(), out, (nmax + 16) * 8, hipMemcpyDeviceToHost);
-  const char* nm[] = {"stage", "prepare", "assemble+max", "LU", "dinv+K slab", "solves"};
+  const char* nm[] = {"stage", "prepare", "assemble+max", "LU", "dinv|U inverses", "K slab + U sweep|solves"};
   for (int i = 0; i < 6; ++i) printf("  %-14s %8.0f cycles\n", nm[i], o[nmax + 1 + i] - o[nmax + i]);
+#ifdef SM_LU_GROUPS
   const char* lp[] = {"publish", "barrier", "reads+update", "loop"};
   for (int i = 0; i < 4; ++i) printf("  LU %-12s %8.0f cycles/step (3 launches summed)\n", lp[i], o[nmax + 8 + i] / N / 3);
+#else
+  const char* lp[] = {"panel", "U rows", "barrier", "update+barrier"};
+  for (int i = 0; i < 4; ++i) printf("  LU %-14s %8.0f cycles per launch\n", lp[i], o[nmax + 8 + i] / 3);
+#endif
 #endif
   return 0;
 }
