@@ -603,6 +603,7 @@ int dopt_qp_reverse(dopt_handle* h, const double* dl_dz, double* out) {
     if (!h->factored && dopt::qp_small_eligible(*h)) {
       const size_t ob = B * L * sizeof(double), fb = B * sizeof(int32_t);
       const bool pinned = pin_ok(*h);
+#ifndef DOPT_SMALL_COPY   // (A/B: DOPT_SMALL_COPY builds the copy-in / copy-out form of round 5)
       if (host && pinned) {
         const size_t so = (ob + fb + 15) & ~(size_t)15;
         char* pz = pin_out(*h, so + B * n * sizeof(double));
@@ -619,6 +620,27 @@ int dopt_qp_reverse(dopt_handle* h, const double* dl_dz, double* out) {
           return 0;
         }
       }
+#else
+      if (host && pinned) {
+        const PackIn pi[1] = {{dl_dz, B * n * sizeof(double)}};
+        const void* pd[1];
+        if (pack_in(*h, pi, 1, pd, &h->tpack)) {
+          h->tout[0].ensure(ob + fb);
+          dopt::qp_small_reverse(*h, static_cast<const double*>(pd[0]), h->tout[0].as<double>(),
+                                 reinterpret_cast<int32_t*>(h->tout[0].as<char>() + ob));
+          char* pz = pin_out(*h, ob + fb);
+          DOPT_CHECK_HIP(hipMemcpyAsync(pz, h->tout[0].p, ob + fb, hipMemcpyDeviceToHost, h->stream));
+          DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+          const int32_t* hf = reinterpret_cast<const int32_t*>(pz + ob);
+          h->small_ready = std::all_of(hf, hf + B, [](int32_t f) { return f == 0; });
+          if (h->small_ready) {
+            std::memcpy(out, pz, ob);
+            h->last_time = tm.s();
+            return 0;
+          }
+        }
+      }
+#endif
       if (!(host && pinned)) {   // a handle's first calls (pageable), device mode
         if (host) {
           d = stage_in(*h, h->tin[0], dl_dz, B * n);
@@ -669,6 +691,18 @@ int dopt_qp_forward(dopt_handle* h, const double* dQ, const double* dq, const do
         // the outputs straight into the pinned read-back buffer (no copy)
         const size_t ob = B * L * sizeof(double);
         char* pin = pin_out(*h, ob);
+#ifdef DOPT_SMALL_COPY
+        h->tout[1].ensure(ob);
+        dopt::qp_small_forward(*h, dopt::FwdTangents{static_cast<const double*>(pd[0]), static_cast<const double*>(pd[1]),
+                                                     static_cast<const double*>(pd[2]), static_cast<const double*>(pd[3]),
+                                                     static_cast<const double*>(pd[4]), static_cast<const double*>(pd[5])},
+                               h->tout[1].as<double>());
+        DOPT_CHECK_HIP(hipMemcpyAsync(pin, h->tout[1].p, ob, hipMemcpyDeviceToHost, h->stream));
+        DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+        std::memcpy(out, pin, ob);
+        h->last_time = tm.s();
+        return 0;
+#endif
         dopt::qp_small_forward(*h, dopt::FwdTangents{static_cast<const double*>(pd[0]), static_cast<const double*>(pd[1]),
                                                      static_cast<const double*>(pd[2]), static_cast<const double*>(pd[3]),
                                                      static_cast<const double*>(pd[4]), static_cast<const double*>(pd[5])},

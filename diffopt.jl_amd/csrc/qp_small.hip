@@ -411,9 +411,10 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
       double pr[16];
 #pragma unroll
       for (int j = k; j < 16; ++j) pr[j] = sm_readlane(a[j], k);
-#ifdef SM_PANEL_RCP
       // 1/u_kk by v_rcp_f64 and two Newton steps, the rows at or above k
-      // untouched by a zero multiplier (no branch on the chain)
+      // untouched by a zero multiplier (no branch on the chain; the IEEE
+      // division and a branch measured 35.1 k against 29.9 k cycles per
+      // launch for the panels at config 1)
       double rq = __builtin_amdgcn_rcp(pr[k]);
       rq = fma(fma(-pr[k], rq, 1.0), rq, rq);
       rq = fma(fma(-pr[k], rq, 1.0), rq, rq);
@@ -421,15 +422,6 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
       a[k] = lane > k ? l : a[k];
 #pragma unroll
       for (int j = k + 1; j < 16; ++j) a[j] = fma(-l, pr[j], a[j]);
-#else
-      const double rq = 1.0 / pr[k];
-      if (lane > k) {
-        const double l = a[k] * rq;
-        a[k] = l;
-#pragma unroll
-        for (int j = k + 1; j < 16; ++j) a[j] = fma(-l, pr[j], a[j]);
-      }
-#endif
     }
     // the forward sweep's block: y_k from lane k once final, the rows below it
 #pragma unroll
@@ -461,10 +453,14 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
       for (int j = 0; j < 16; ++j) Lw[16 * j + lane] = j < lane ? a[j] : 0.0;
     sm_wave_sync();
     SB_LAP(0);
-    // ---- U row: columns k0 + 16 + q, q = wv + 4·lane
+    // ---- U row: columns k0 + 16 + q, each wave a contiguous quarter of them
+    // (lane ↔ column: conflict-free LDS rows; q = wv + 4·lane, eight lanes
+    // to a bank, measured 29 k cycles per launch for this phase)
     const int ncol = NP - k0 - 16;
-    const int c = k0 + 16 + wv + 4 * lane;
-    if (wv + 4 * lane < ncol) {
+    const int cpw = (ncol + SM_T / 64 - 1) / (SM_T / 64);
+    const int q = wv * cpw + lane;
+    const int c = k0 + 16 + q;
+    if (lane < cpw && q < ncol) {
       double u[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) u[i] = S[(k0 + i) * SM_LD + c];
@@ -487,40 +483,6 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
     SB_LAP(2);
     // ---- trailing update on MFMA: tile (I, C) −= L(I, KK)·U(KK, C)
     const int nt = NB - KK - 1;
-#ifdef SM_TRAIL2
-    // two tiles per wave at a time: two independent MFMA chains, every LDS
-    // operand of both loaded before the first MFMA
-    for (int tt = wv; tt < nt * nt; tt += 2 * (SM_T / 64)) {
-      const int tu = tt + SM_T / 64;
-      const bool two = tu < nt * nt;   // uniform
-      const int i0 = k0 + 16 + 16 * (tt / nt), j0 = k0 + 16 + 16 * (tt % nt);
-      const int i1 = k0 + 16 + 16 * ((two ? tu : tt) / nt), j1 = k0 + 16 + 16 * ((two ? tu : tt) % nt);
-      sm_d4 acc0, acc1;
-      double av0[4], bv0[4], av1[4], bv1[4];
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        acc0[rr] = S[(i0 + g + 4 * rr) * SM_LD + j0 + l16];
-        acc1[rr] = S[(i1 + g + 4 * rr) * SM_LD + j1 + l16];
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) {
-        av0[s2] = -S[(i0 + l16) * SM_LD + k0 + 4 * s2 + g];
-        bv0[s2] = S[(k0 + 4 * s2 + g) * SM_LD + j0 + l16];
-        av1[s2] = -S[(i1 + l16) * SM_LD + k0 + 4 * s2 + g];
-        bv1[s2] = S[(k0 + 4 * s2 + g) * SM_LD + j1 + l16];
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) {
-        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av0[s2], bv0[s2], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av1[s2], bv1[s2], acc1, 0, 0, 0);
-      }
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        S[(i0 + g + 4 * rr) * SM_LD + j0 + l16] = acc0[rr];
-        if (two) S[(i1 + g + 4 * rr) * SM_LD + j1 + l16] = acc1[rr];
-      }
-    }
-#else
     for (int tt = wv; tt < nt * nt; tt += SM_T / 64) {
       const int i0 = k0 + 16 + 16 * (tt / nt), j0 = k0 + 16 + 16 * (tt % nt);
       sm_d4 acc;
@@ -535,7 +497,6 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) S[(i0 + g + 4 * rr) * SM_LD + j0 + l16] = acc[rr];
     }
-#endif
     __syncthreads();
     SB_LAP(3);
   }
@@ -1050,7 +1011,11 @@ __global__ __launch_bounds__(SM_T) void qp_small_fwd_kernel(QPIn P, FwdTangents 
       }
   }
   __syncthreads();
+#ifdef SM_FWD_STEPS   // (A/B: the step-by-step sweeps of round 5)
+  for (int r = t; r < N; r += SM_T) L.dinv[r] = 1.0 / S[r * SM_LD + r];
+#else
   sm_diag_inverses(S, NP / SM_G);
+#endif
   // the full forward right-hand side r (QuadraticProgram.jl:429-433):
   //   [dQ z + dq + dGᵀλ + dAᵀν; λ.*(dG z) − λ.*dh; dA z − db] — r1 and r3 in
   // y (reduced positions), r2 kept in registers per row for the recovery
@@ -1096,7 +1061,12 @@ __global__ __launch_bounds__(SM_T) void qp_small_fwd_kernel(QPIn P, FwdTangents 
   // Kᵀ x = r: Uᵀ w = r, then Lᵀ x = w, by wave 0, by 16-blocks
   if (wv == 0) {
     double y0 = lane < N ? y[lane] : 0.0, y1 = lane + 64 < N ? y[lane + 64] : 0.0;
+#ifdef SM_FWD_STEPS
+    sm_utsolve(S, L.dinv, N, lane, y0, y1);
+    sm_ltsolve(S, L.dinv, N, lane, y0, y1);
+#else
     sm_fwd_sweeps_blk(S, NP / SM_G, lane, y0, y1);
+#endif
     if (lane < N) y[lane] = y0;
     if (lane + 64 < N) y[lane + 64] = y1;
   }
