@@ -355,6 +355,11 @@ __device__ __forceinline__ double sm_readlane(double x, int l) {
   const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+__device__ __forceinline__ double sm_rcp(double d) {   // v_rcp_f64 + two Newton steps
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(fma(-d, r, 1.0), r, r);
+  return fma(fma(-d, r, 1.0), r, r);
+}
 __device__ __forceinline__ void sm_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -461,13 +466,21 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
     const int q = wv * cpw + lane;
     const int c = k0 + 16 + q;
     if (lane < cpw && q < ncol) {
-      double u[16];
+      // every operand loaded before the first fma (a compiler-only fence
+      // keeps them issued together: left to the scheduler, each LDS read
+      // waited for alone before its fma, ≈ 5 k cycles per block)
+      double u[16], lv[120];
 #pragma unroll
       for (int i = 0; i < 16; ++i) u[i] = S[(k0 + i) * SM_LD + c];
 #pragma unroll
-      for (int k = 0; k < 15; ++k)
+      for (int k = 0, e = 0; k < 15; ++k)
 #pragma unroll
-        for (int i = k + 1; i < 16; ++i) u[i] = fma(-Lw[16 * k + i], u[k], u[i]);
+        for (int i = k + 1; i < 16; ++i, ++e) lv[e] = Lw[16 * k + i];
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int k = 0, e = 0; k < 15; ++k)
+#pragma unroll
+        for (int i = k + 1; i < 16; ++i, ++e) u[i] = fma(-lv[e], u[k], u[i]);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         S[(k0 + i) * SM_LD + c] = u[i];
@@ -618,15 +631,22 @@ __device__ __forceinline__ void sm_uinv(const double* S, int NB, double (*U)[16 
   const int KK = 4 * wv + (lane >> 4);
   if (wv >= 2 || KK >= NB) return;
   const double* D = S + 16 * KK * SM_LD + 16 * KK;
-  double x[16];
+  // U's 136 entries loaded before the chain (compiler-only fence), the
+  // reciprocals of its diagonal off the chain
+  double uv[136], x[16];
+#pragma unroll
+  for (int j = 0, e = 0; j < 16; ++j)
+#pragma unroll
+    for (int q = 0; q <= j; ++q, ++e) uv[e] = D[q * SM_LD + j];
+  asm volatile("" ::: "memory");
 #pragma unroll
   for (int j = 0; j < 16; ++j) x[j] = j == i ? 1.0 : 0.0;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
+  for (int j = 0, e = 0; j < 16; ++j) {
     double acc = x[j];
 #pragma unroll
-    for (int q = 0; q < j; ++q) acc = fma(-x[q], D[q * SM_LD + j], acc);
-    x[j] = acc / D[j * SM_LD + j];
+    for (int q = 0; q < j; ++q, ++e) acc = fma(-x[q], uv[e], acc);
+    x[j] = acc * sm_rcp(uv[e++]);
   }
 #pragma unroll
   for (int j = 0; j < 16; ++j) U[KK][i * 17 + j] = x[j];
@@ -692,23 +712,32 @@ __device__ __forceinline__ void sm_diag_inverses(double* S, int NB) {
   const bool act = KK < NB;
   const int k0 = 16 * (act ? KK : 0);
   const double* D = S + k0 * SM_LD + k0;
-  double x[16];
+  // the triangle's entries loaded before the chain (compiler-only fence):
+  // U's 136 (column j's rows q ≤ j) or L's 120 (row r's columns k < r)
+  double dv[136], x[16];
+  const bool up = wv < 2;   // uniform
+#pragma unroll
+  for (int j = 0, e = 0; j < 16; ++j)
+#pragma unroll
+    for (int q = 0; q <= j; ++q, ++e) dv[e] = up ? D[q * SM_LD + j] : (q < j ? D[j * SM_LD + q] : 1.0);
+  asm volatile("" ::: "memory");
 #pragma unroll
   for (int j = 0; j < 16; ++j) x[j] = j == i ? 1.0 : 0.0;
-  if (wv < 2) {
+  if (up) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0, e = 0; j < 16; ++j) {
       double acc = x[j];
 #pragma unroll
-      for (int q = 0; q < j; ++q) acc = fma(-x[q], D[q * SM_LD + j], acc);
-      x[j] = acc / D[j * SM_LD + j];
+      for (int q = 0; q < j; ++q, ++e) acc = fma(-x[q], dv[e], acc);
+      x[j] = acc * sm_rcp(dv[e++]);
     }
   } else {
 #pragma unroll
-    for (int r = 1; r < 16; ++r) {
+    for (int r = 0, e = 0; r < 16; ++r) {
       double acc = x[r];
 #pragma unroll
-      for (int k = 0; k < r; ++k) acc = fma(-D[r * SM_LD + k], x[k], acc);
+      for (int k = 0; k < r; ++k, ++e) acc = fma(-dv[e], x[k], acc);
+      ++e;   // (the unit diagonal)
       x[r] = acc;
     }
   }

@@ -15,7 +15,7 @@ done
 timeout -k 10 300 python -u -m pytest tests/test_qp_small_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread \
   > gpurun_out/test_small.log 2>&1 || exit 1
 for r in 1 2; do
-  for v in head copyio fwdsteps; do
+  for v in head fwdsteps; do
     lib=""; [ $v != head ] && lib=$V/libdiffopt_$v.so
     echo "== $v round $r" >> gpurun_out/small_ab.txt
     DOPT_LIB=$lib timeout -k 10 300 python3 -u tools/bench_dropin.py --reps 30 2>/dev/null | grep "config 1" >> gpurun_out/small_ab.txt || exit 1
