@@ -397,9 +397,9 @@ int dopt_qp_set_csc(dopt_handle* h,
       }
     } sync_on_throw{h->stream};
     h->csc_err.ensure(sizeof(int));
-    DOPT_CHECK_HIP(hipMemsetAsync(h->csc_err.p, 0, sizeof(int), h->stream));
     int* err = h->csc_err.as<int>();
     if (h->sparse) {   // kept sparse (sparse.hip): G, A and their CSR copies; Q only tested for zero
+      DOPT_CHECK_HIP(hipMemsetAsync(h->csc_err.p, 0, sizeof(int), h->stream));
       const int64_t* cp[3];
       const int64_t* rv[3];
       const double* nz[3];
@@ -462,7 +462,26 @@ int dopt_qp_set_csc(dopt_handle* h,
       if (hostv) throw Error(-1, (hostv & 1) ? "CSC colptr is not monotone / out of range" : "CSC rowval out of range");
     }
     const bool packed = pack_in(*h, pin, 13, pdev);
-    for (int k = 0; k < 3; ++k) {
+    const bool async = packed && hostv == 0;
+    if (async) {   // validated on the host: Q, G and A zero-filled and scattered by ONE launch
+      dopt::CscTriple T{};
+      for (int k = 0; k < 3; ++k) {
+        const Mat& M = mats[k];
+        if (M.rows == 0) continue;
+        DevBuf& d = h->own_in[M.slot];
+        d.ensure(B * M.rows * n * sizeof(double));
+        T.cp[k] = (const int64_t*)pdev[3 * k];
+        T.rv[k] = (const int64_t*)pdev[3 * k + 1];
+        T.nz[k] = (const double*)pdev[3 * k + 2];
+        T.dense[k] = d.as<double>();
+        T.rows[k] = (int)M.rows;
+        dense[k] = d.as<double>();
+      }
+      dopt::csc_to_dense3(*h, T);
+    } else {
+      DOPT_CHECK_HIP(hipMemsetAsync(h->csc_err.p, 0, sizeof(int), h->stream));
+    }
+    for (int k = 0; k < 3 && !async; ++k) {
       const Mat& M = mats[k];
       if (M.rows == 0) continue;
       const int64_t* cp = packed ? (const int64_t*)pdev[3 * k] : stage_in_i64(*h, h->csc_in[3 * k], M.cp, B * (n + 1));
@@ -475,7 +494,6 @@ int dopt_qp_set_csc(dopt_handle* h,
                          d.as<double>(), err);
       dense[k] = d.as<double>();
     }
-    const bool async = packed && hostv == 0;
     if (!async) {
       int herr = 0;
       DOPT_CHECK_HIP(hipMemcpyAsync(&herr, err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
@@ -682,6 +700,29 @@ int dopt_qp_forward(dopt_handle* h, const double* dQ, const double* dq, const do
     if (!out) throw Error(-1, "out is required");
     Timer tm;
     const size_t B = h->batch, n = h->n, m = h->m, p = h->p, L = n + m + p;
+#ifndef DOPT_SMALL_COPY
+    // the small path's factors with only vector tangents (dq, dh, db; the
+    // matrix ones zero): no copy at all — the kernel reads them from and
+    // writes its outputs into the pinned read-back buffer
+    if (!h->sparse && !h->factored && h->small_ready && pin_ok(*h) && !dQ && !(m && dG) && !(p && dA)) {
+      const size_t ob = B * L * sizeof(double), so = (ob + 15) & ~(size_t)15;
+      const size_t vq = B * n * sizeof(double), vh = B * m * sizeof(double), vb = B * p * sizeof(double);
+      const size_t oq = so, oh = oq + ((vq + 15) & ~(size_t)15), obb = oh + ((vh + 15) & ~(size_t)15);
+      char* pz = pin_out(*h, obb + vb + 16);
+      if (dq) std::memcpy(pz + oq, dq, vq);
+      if (m && dh) std::memcpy(pz + oh, dh, vh);
+      if (p && db) std::memcpy(pz + obb, db, vb);
+      char* pd = h->pin_out_dev;
+      dopt::qp_small_forward(*h, dopt::FwdTangents{nullptr, dq ? reinterpret_cast<const double*>(pd + oq) : nullptr,
+                                                   nullptr, m && dh ? reinterpret_cast<const double*>(pd + oh) : nullptr,
+                                                   nullptr, p && db ? reinterpret_cast<const double*>(pd + obb) : nullptr},
+                             reinterpret_cast<double*>(pd));
+      DOPT_CHECK_HIP(hipStreamSynchronize(h->stream));
+      std::memcpy(out, pz, ob);
+      h->last_time = tm.s();
+      return 0;
+    }
+#endif
     if (!h->sparse && !h->factored && h->small_ready && pin_ok(*h)) {   // the small path's factors (dopt_qp_reverse): one copy in
       const PackIn pi[6] = {{dQ, B * n * n * sizeof(double)}, {dq, B * n * sizeof(double)},
                             {m ? dG : nullptr, B * m * n * sizeof(double)}, {m ? dh : nullptr, B * m * sizeof(double)},

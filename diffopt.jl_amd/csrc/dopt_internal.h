@@ -366,6 +366,16 @@ bool qp_small_eligible(const Handle& h);
 void qp_small_reverse(Handle& h, const double* dl_dz, double* out, int32_t* flags);
 void qp_small_forward(Handle& h, const FwdTangents& T, double* out);
 void qp_reverse(Handle& h, const double* dl_dz, double* out);
+// Q, G and A of a host-validated small model in one launch (zero fill, then
+// scatter; no range checks: abi.hip's host_csc_check ran)
+struct CscTriple {
+  const int64_t* cp[3];
+  const int64_t* rv[3];
+  const double* nz[3];
+  double* dense[3];
+  int rows[3];
+};
+void csc_to_dense3(Handle& h, const CscTriple& T);
 void csc_to_dense(Handle& h, const int64_t* colptr, const int64_t* rowval, const double* nzval,
                   int64_t nnz, int rows, int ncols, double* dense, int* err);
 void qp_reverse_grads(Handle& h, const double* rev, double* dQ, double* dq, double* dG, double* gc,

@@ -717,6 +717,27 @@ void csc_to_dense(Handle& h, const int64_t* colptr, const int64_t* rowval, const
   DOPT_CHECK_HIP(hipGetLastError());
 }
 
+// grid (column j, matrix k, problem b): the column zero-filled, then its
+// entries scattered (the same workgroup: a barrier between the two)
+__global__ __launch_bounds__(TPB) void csc_scatter3_kernel(CscTriple T, int ncols) {
+  const int j = blockIdx.x, k = blockIdx.y, b = blockIdx.z;
+  const int rows = T.rows[k];
+  if (rows == 0) return;   // workgroup-uniform
+  double* col = T.dense[k] + ((size_t)b * ncols + j) * rows;
+  for (int i = threadIdx.x; i < rows; i += TPB) col[i] = 0.0;
+  __syncthreads();
+  const int64_t* cp = T.cp[k] + (size_t)b * (ncols + 1);
+  const int64_t k1 = cp[j + 1] - 1;
+  for (int64_t q = cp[j] - 1 + threadIdx.x; q < k1; q += TPB) col[T.rv[k][q] - 1] = T.nz[k][q];
+}
+
+void csc_to_dense3(Handle& h, const CscTriple& T) {
+  if (h.n == 0 || h.batch == 0) return;
+  hipLaunchKernelGGL(csc_scatter3_kernel, dim3((unsigned)h.n, 3, (unsigned)h.batch), dim3(TPB), 0, h.stream, T,
+                     (int)h.n);
+  DOPT_CHECK_HIP(hipGetLastError());
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------

@@ -164,6 +164,19 @@ __device__ __forceinline__ double sm_assemble(const QPIn& P, const SmSrc& X, con
                                               int ti, int tj, double (&e)[8][8]) {
   const int n = P.n, m = P.m, p = P.p;
   const int NB = (N + SM_G - 1) / SM_G;   // the blocks the LU reads (a, c < NB)
+  // the kept rows' indices, λ and s of the thread's rows and columns, loaded
+  // together first (each entry then needs one load, not two dependent ones)
+  int rk[8], ck[8];
+  double rs[8], cl[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int r = ti + SM_G * u - n, c = tj + SM_G * u - n;
+    const bool rin = r >= 0 && r < nk, cin = c >= 0 && c < nk;
+    rk[u] = L.kidx[rin ? r : 0];
+    rs[u] = L.sk[rin ? r : 0];
+    ck[u] = L.kidx[cin ? c : 0];
+    cl[u] = L.lk[cin ? c : 0];
+  }
   double amax = 0.0;
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
@@ -181,11 +194,11 @@ __device__ __forceinline__ double sm_assemble(const QPIn& P, const SmSrc& X, con
         mul = 1.0;
         if (r < n) {
           if (c < n) off = r + (SmOff<STG>)c * n;
-          else if (c < n + nk) { which = 1; off = L.kidx[c - n] + (SmOff<STG>)r * m; mul = L.lk[c - n]; }
+          else if (c < n + nk) { which = 1; off = ck[c8] + (SmOff<STG>)r * m; mul = cl[c8]; }
           else { which = 2; off = (c - n - nk) + (SmOff<STG>)r * p; }
         } else if (r < n + nk) {
-          if (c < n) { which = 1; off = L.kidx[r - n] + (SmOff<STG>)c * m; }
-          else { mul = 0.0; cv = c == r ? L.sk[r - n] : 0.0; }
+          if (c < n) { which = 1; off = rk[a] + (SmOff<STG>)c * m; }
+          else { mul = 0.0; cv = c == r ? rs[a] : 0.0; }
         } else if (c < n) {
           which = 2;
           off = (r - n - nk) + (SmOff<STG>)c * p;

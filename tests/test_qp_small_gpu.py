@@ -241,4 +241,16 @@ def test_small_path_csc_handle_reuse(QPBatch):
         e.reverse(d1["dl_dz"])
     put(d1)
     check(d1)
+    # matrix tangents on the pinned route (the packed copy in, not the
+    # vector-only zero-copy form)
+    rng = np.random.default_rng(9500)
+    dQ = rng.standard_normal((1, n, n))
+    dQ = dQ + dQ.transpose(0, 2, 1)
+    dG, dA = rng.standard_normal((1, m, n)), rng.standard_normal((1, p, n))
+    e.reverse(d1["dl_dz"])
+    fwd = e.forward(dQ=dQ, dq=d1["dq"], dG=dG, dh=d1["dh"], dA=dA, db=d1["db"])
+    args = [d1[k][0] for k in ("Q", "G", "h", "A", "z", "lam", "nu")]
+    ref = np.concatenate(oqp.forward_differentiate(*args, dQ=dQ[0], dq=d1["dq"][0], dG=dG[0], dh=d1["dh"][0],
+                                                   dA=dA[0], db=d1["db"][0]))
+    assert relfro(fwd[0], ref) <= RTOL
     e.close()

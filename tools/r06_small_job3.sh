@@ -12,7 +12,7 @@ for v in blk blk_st; do
   echo "== $v" >> gpurun_out/small_ab.txt
   timeout -k 10 60 tools/probebin_blk/small_probe_$v >> gpurun_out/small_ab.txt 2>&1 || exit 1
 done
-timeout -k 10 300 python -u -m pytest tests/test_qp_small_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread \
+timeout -k 10 300 python -u -m pytest tests/test_qp_small_gpu.py tests/test_qp_gpu.py tests/test_model_api_gpu.py tests/test_lhs_solve_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread \
   > gpurun_out/test_small.log 2>&1 || exit 1
 for r in 1 2; do
   for v in head fwdsteps; do
