@@ -526,9 +526,9 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
     __syncthreads();
     SB_LAP(3);
   }
-#ifdef SM_STAMPS
-  if (threadIdx.x == 0)
-    for (int i = 0; i < 4; ++i) stamp[i] += (double)q_[i];
+#ifdef SM_STAMPS   // each wave's lane 0: stamp[4·wave + phase]
+  if (lane == 0)
+    for (int i = 0; i < 4; ++i) stamp[4 * wv + i] += (double)q_[i];
 #endif
 #undef SB_LAP
 }
@@ -712,122 +712,6 @@ __device__ __forceinline__ void sm_usolve_blk(const double* S, const double (*U)
   }
 }
 #endif
-
-// The forward kernel's diagonal-block inverses, in place: after this the
-// diagonal 16-blocks of the image hold L_KK⁻¹ strictly below the diagonal
-// (its unit diagonal implied) and U_KK⁻¹ on and above it.  Sixteen blocks at
-// once — four 16-lane groups per wave, waves 0 / 1 the U inverses (lane i: row
-// i of X, X·U = I), waves 2 / 3 the L inverses (lane i: column i of Y, L·Y =
-// I) — into registers, then stored after a barrier.
-__device__ __forceinline__ void sm_diag_inverses(double* S, int NB) {
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, i = lane & 15;
-  const int KK = 4 * (wv & 1) + (lane >> 4);
-  const bool act = KK < NB;
-  const int k0 = 16 * (act ? KK : 0);
-  const double* D = S + k0 * SM_LD + k0;
-  // the triangle's entries loaded before the chain (compiler-only fence):
-  // U's 136 (column j's rows q ≤ j) or L's 120 (row r's columns k < r)
-  double dv[136], x[16];
-  const bool up = wv < 2;   // uniform
-#pragma unroll
-  for (int j = 0, e = 0; j < 16; ++j)
-#pragma unroll
-    for (int q = 0; q <= j; ++q, ++e) dv[e] = up ? D[q * SM_LD + j] : (q < j ? D[j * SM_LD + q] : 1.0);
-  asm volatile("" ::: "memory");
-#pragma unroll
-  for (int j = 0; j < 16; ++j) x[j] = j == i ? 1.0 : 0.0;
-  if (up) {
-#pragma unroll
-    for (int j = 0, e = 0; j < 16; ++j) {
-      double acc = x[j];
-#pragma unroll
-      for (int q = 0; q < j; ++q, ++e) acc = fma(-x[q], dv[e], acc);
-      x[j] = acc * sm_rcp(dv[e++]);
-    }
-  } else {
-#pragma unroll
-    for (int r = 0, e = 0; r < 16; ++r) {
-      double acc = x[r];
-#pragma unroll
-      for (int k = 0; k < r; ++k, ++e) acc = fma(-dv[e], x[k], acc);
-      ++e;   // (the unit diagonal)
-      x[r] = acc;
-    }
-  }
-  __syncthreads();
-  if (act) {
-    double* W = S + k0 * SM_LD + k0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      if (wv < 2 && j >= i) W[i * SM_LD + j] = x[j];
-      if (wv >= 2 && j > i) W[j * SM_LD + i] = x[j];
-    }
-  }
-  __syncthreads();
-}
-
-// Kᵀx = r by 16-blocks with the in-place inverses, one wave (entries lane /
-// lane + 64): Uᵀ w = r forward, w_K = U_KK⁻ᵀ·r_K and the rows past the block
-// take U(K, >K)ᵀ·w_K; then Lᵀ x = w backward likewise — sixteen products per
-// row and block, no step-by-step chain.  NP = 16·NB rows (identity padding).
-__device__ __forceinline__ void sm_fwd_sweeps_blk(const double* S, int NB, int lane, double& y0, double& y1) {
-  const int NP = 16 * NB;
-  auto blk = [&](int k0, bool upper) {   // the block's solve with its inverse, in place
-    const int base = k0 & 63;
-    const bool hi = k0 >= 64;
-    double rv[16];
-    const double src = hi ? y1 : y0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) rv[j] = sm_readlane(src, base + j);
-    const int i = lane - base;
-    const bool inb = i >= 0 && i < 16;
-    const int ic = inb ? i : 0;
-    double w0 = 0.0, w1 = 0.0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      // (U_KK⁻¹)_{ji}, j ≤ i; or (L_KK⁻¹)_{ji}, j ≥ i, unit diagonal
-      const double sv = S[(k0 + j) * SM_LD + k0 + ic];
-      const double c = upper ? (j <= ic ? sv : 0.0) : (j == ic ? 1.0 : (j > ic ? sv : 0.0));
-      if (j & 1) w1 = fma(c, rv[j], w1);
-      else w0 = fma(c, rv[j], w0);
-    }
-    if (inb) {
-      if (hi) y1 = w0 + w1;
-      else y0 = w0 + w1;
-    }
-  };
-  auto rows = [&](int k0, bool after) {   // the other rows: r_i −= Σ_j S(k0 + j, i)·x_j
-    const int base = k0 & 63;
-    const bool hi = k0 >= 64;
-    double xv[16];
-    const double src = hi ? y1 : y0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) xv[j] = sm_readlane(src, base + j);
-    double a0 = 0.0, a1 = 0.0, c0 = 0.0, c1 = 0.0;
-    const bool two = NP > 64;   // uniform
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const double* row = S + (k0 + j) * SM_LD;
-      if (j & 1) a1 = fma(row[lane], xv[j], a1);
-      else a0 = fma(row[lane], xv[j], a0);
-      if (two) {
-        if (j & 1) c1 = fma(row[64 + lane], xv[j], c1);
-        else c0 = fma(row[64 + lane], xv[j], c0);
-      }
-    }
-    const int e = after ? k0 + 16 : k0;
-    if (after ? lane >= e : lane < e) y0 -= a0 + a1;
-    if (two && (after ? 64 + lane >= e : 64 + lane < e)) y1 -= c0 + c1;
-  };
-  for (int KK = 0; KK < NB; ++KK) {
-    blk(16 * KK, true);
-    if (KK + 1 < NB) rows(16 * KK, true);
-  }
-  for (int KK = NB - 1; KK >= 0; --KK) {
-    blk(16 * KK, false);
-    if (KK > 0) rows(16 * KK, false);
-  }
-}
 
 #ifdef SM_STAMPS   // (tools/probe/small_probe.hip: thread 0's clock at phase marks, past the outputs)
 #define SM_STAMP(i) \
@@ -1033,9 +917,7 @@ __global__ __launch_bounds__(SM_T) void qp_small_fwd_kernel(QPIn P, FwdTangents 
   const int lane = t & 63, wv = t >> 6;
   // the factors into LDS: rows by wave, 8 rows × 2 column halves per round,
   // all sixteen loads in flight before any store
-  // (the 16-block padding past N as the identity)
-  const int NP = (N + SM_G - 1) / SM_G * SM_G;
-  for (int r0 = wv; r0 < NP; r0 += 8 * (SM_T / 64)) {
+  for (int r0 = wv; r0 < N; r0 += 8 * (SM_T / 64)) {
     double v[8][2];
 #pragma unroll
     for (int u = 0; u < 8; ++u)
@@ -1049,15 +931,11 @@ __global__ __launch_bounds__(SM_T) void qp_small_fwd_kernel(QPIn P, FwdTangents 
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int r = r0 + u * (SM_T / 64), c = lane + 64 * hh;
-        if (r < NP && c < NP) S[r * SM_LD + c] = r < N && c < N ? v[u][hh] : (r == c ? 1.0 : 0.0);
+        if (r < N && c < N) S[r * SM_LD + c] = v[u][hh];
       }
   }
   __syncthreads();
-#ifdef SM_FWD_STEPS   // (A/B: the step-by-step sweeps of round 5)
   for (int r = t; r < N; r += SM_T) L.dinv[r] = 1.0 / S[r * SM_LD + r];
-#else
-  sm_diag_inverses(S, NP / SM_G);
-#endif
   // the full forward right-hand side r (QuadraticProgram.jl:429-433):
   //   [dQ z + dq + dGᵀλ + dAᵀν; λ.*(dG z) − λ.*dh; dA z − db] — r1 and r3 in
   // y (reduced positions), r2 kept in registers per row for the recovery
@@ -1100,15 +978,13 @@ __global__ __launch_bounds__(SM_T) void qp_small_fwd_kernel(QPIn P, FwdTangents 
     if (kk >= 0) y[n + kk] = r2(l);
   }
   __syncthreads();
-  // Kᵀ x = r: Uᵀ w = r, then Lᵀ x = w, by wave 0, by 16-blocks
+  // Kᵀ x = r: Uᵀ w = r, then Lᵀ x = w, by wave 0 (as the reverse kernel)
   if (wv == 0) {
     double y0 = lane < N ? y[lane] : 0.0, y1 = lane + 64 < N ? y[lane + 64] : 0.0;
-#ifdef SM_FWD_STEPS
+    // (step by step: the 16-block form with the diagonal blocks' inverses
+    // formed here measured 6 µs slower per call, round 6)
     sm_utsolve(S, L.dinv, N, lane, y0, y1);
     sm_ltsolve(S, L.dinv, N, lane, y0, y1);
-#else
-    sm_fwd_sweeps_blk(S, NP / SM_G, lane, y0, y1);
-#endif
     if (lane < N) y[lane] = y0;
     if (lane + 64 < N) y[lane + 64] = y1;
   }

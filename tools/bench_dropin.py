@@ -7,6 +7,9 @@ same factorisation) and the narrow `LinearAlgebraSolver` plug point
 shapes, batch 1, host buffers, beside the oracle's single solve on one core
 (the reference algorithm: assemble the full KKT, SuperLU, refactorised per
 direction, QuadraticProgram.jl:316-446).  Prints one JSON line per case.
+The `qpmodel_*_ms` fields time the Python wrapper calls; `qpmodel_*_abi_ms`
+time the ABI calls alone with their arrays and pointers ready, as the Julia
+ccalls issue them (`qpmodel_set_csc_ms` is that already).
 
   python tools/bench_dropin.py [--reps 30]
 """
@@ -59,6 +62,9 @@ def main():
         e.reverse(d["dl_dz"][a.reps][None])
         t_first = time.perf_counter() - t_first
         t_set, t_rev, t_fwd, t_py = [], [], [], []
+        t_rev_abi, t_fwd_abi = [], []
+        lib = e.lib
+        out_r = np.empty((1, n + m + p)); out_f = np.empty((1, n + m + p))
         for r in range(a.reps):
             Q, G, h, A, z, lam, nu = prob(r)
             # the MOI matrix form as Julia holds it (CSC arrays built outside
@@ -75,6 +81,20 @@ def main():
             e.forward(dq=d["dq"][r][None], dh=d["dh"][r][None], db=d["db"][r][None] if p else None)
             t3 = time.perf_counter()
             t_set.append(t1 - t0); t_rev.append(t2 - t1); t_fwd.append(t3 - t2)
+            # the same two calls as the Julia ccalls issue them: arrays and
+            # pointers ready, the ABI call alone timed (set_csc above likewise)
+            e.set_csc_args(args)
+            dl = np.ascontiguousarray(d["dl_dz"][r][None])
+            vq, vh = np.ascontiguousarray(d["dq"][r][None]), np.ascontiguousarray(d["dh"][r][None])
+            vb = np.ascontiguousarray(d["db"][r][None]) if p else None
+            pv = [vq.ctypes.data, vh.ctypes.data, vb.ctypes.data if p else None]
+            t4 = time.perf_counter()
+            rc = lib.dopt_qp_reverse(e.h, dl.ctypes.data, out_r.ctypes.data)
+            t5 = time.perf_counter()
+            rc |= lib.dopt_qp_forward(e.h, None, pv[0], None, pv[1], None, pv[2], out_f.ctypes.data)
+            t6 = time.perf_counter()
+            assert rc == 0
+            t_rev_abi.append(t5 - t4); t_fwd_abi.append(t6 - t5)
         e.close()
         # the LinearAlgebraSolver plug point: LHS (reverse) and LHS' (forward)
         def plug(solver):
@@ -106,6 +126,9 @@ def main():
             qpmodel_reverse_ms=round(_med(t_rev), 3),
             qpmodel_forward_ms=round(_med(t_fwd), 3),
             qpmodel_model_ms=round(_med(np.add(np.add(t_set, t_rev), t_fwd)), 3),
+            qpmodel_reverse_abi_ms=round(_med(t_rev_abi), 3),
+            qpmodel_forward_abi_ms=round(_med(t_fwd_abi), 3),
+            qpmodel_model_abi_ms=round(_med(np.add(np.add(t_set, t_rev_abi), t_fwd_abi)), 3),
             plug_point_cached_handle_ms=round(_med(t_cached), 3),
             plug_point_handle_per_call_ms=round(_med(t_fresh), 3),
             reps=a.reps)), flush=True)

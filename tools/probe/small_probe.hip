@@ -42,12 +42,12 @@ int main(int argc, char** argv) {
   QPMeta* meta;
   hipMalloc(&K, (size_t)nmax * ld * 8);
   hipMalloc(&sout, m * 8);
-  hipMalloc(&out, (nmax + 16) * 8);
+  hipMalloc(&out, (nmax + 32) * 8);
   hipMalloc(&kidx, 2 * m * 4);
   hipMalloc(&flag, 4);
   hipMalloc(&meta, sizeof(QPMeta));
   hipMemset(flag, 0, 4);
-  hipMemset(out, 0, (nmax + 16) * 8);
+  hipMemset(out, 0, (nmax + 32) * 8);
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
@@ -115,7 +115,7 @@ int main(int argc, char** argv) {
     }
   printf("max rel diff %.3g\n", maxd);
   {  // the reverse solve: x = K⁻¹[dl; 0; 0] by the host LU against −out[0 … n)
-    std::vector<double> x(N, 0.0), o(nmax + 16);
+    std::vector<double> x(N, 0.0), o(nmax + 32);
     for (int i = 0; i < n; ++i) x[i] = dl[i];
     for (int i = 0; i < N; ++i)
       for (int k = 0; k < i; ++k) x[i] -= R[(size_t)i * N + k] * x[k];
@@ -123,7 +123,7 @@ int main(int argc, char** argv) {
       for (int k = i + 1; k < N; ++k) x[i] -= R[(size_t)i * N + k] * x[k];
       x[i] /= R[(size_t)i * N + i];
     }
-    hipMemcpy(o.data(), out, (nmax + 16) * 8, hipMemcpyDeviceToHost);
+    hipMemcpy(o.data(), out, (nmax + 32) * 8, hipMemcpyDeviceToHost);
     double xd = 0.0;
     for (int i = 0; i < n; ++i) xd = std::fmax(xd, std::fabs(-o[i] - x[i]) / (1.0 + std::fabs(x[i])));
     for (int e = 0; e < p; ++e)
@@ -131,8 +131,8 @@ int main(int argc, char** argv) {
     printf("solve max rel diff %.3g\n", xd);
   }
 #ifdef SM_STAMPS
-  std::vector<double> o(nmax + 16);
-  hipMemcpy(o.data(), out, (nmax + 16) * 8, hipMemcpyDeviceToHost);
+  std::vector<double> o(nmax + 32);
+  hipMemcpy(o.data(), out, (nmax + 32) * 8, hipMemcpyDeviceToHost);
   const char* nm[] = {"stage", "prepare", "assemble+max", "LU", "dinv|U inverses", "K slab + U sweep|solves"};
   for (int i = 0; i < 6; ++i) printf("  %-14s %8.0f cycles\n", nm[i], o[nmax + 1 + i] - o[nmax + i]);
 #ifdef SM_LU_GROUPS
@@ -140,7 +140,9 @@ int main(int argc, char** argv) {
   for (int i = 0; i < 4; ++i) printf("  LU %-12s %8.0f cycles/step (3 launches summed)\n", lp[i], o[nmax + 8 + i] / N / 3);
 #else
   const char* lp[] = {"panel", "U rows", "barrier", "update+barrier"};
-  for (int i = 0; i < 4; ++i) printf("  LU %-14s %8.0f cycles per launch\n", lp[i], o[nmax + 8 + i] / 3);
+  for (int i = 0; i < 4; ++i)
+    printf("  LU %-14s %8.0f %8.0f %8.0f %8.0f cycles per launch (waves 0-3)\n", lp[i], o[nmax + 8 + i] / 3,
+           o[nmax + 12 + i] / 3, o[nmax + 16 + i] / 3, o[nmax + 20 + i] / 3);
 #endif
 #endif
   return 0;
