@@ -412,6 +412,29 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = lane >> 4, l16 = lane & 15;
   const int NP = 16 * NB;
   double* Lw = L.lw[wv];   // this wave's copy of L_KK, column-major (L_ik at 16k + i)
+  // The diagonal block's factors and y entries go to the image one block
+  // late, from the last wave's registers (every wave holds the same values;
+  // that wave has the fewest rows below): block KK's rows and columns are
+  // read by no later step, and a store right after the block's first barrier
+  // sat on wave 0's path to its trailing tiles.
+  constexpr int PW = SM_T / 64 - 1;
+  double da[16], dy = 0.0;
+  int dk0 = -1;
+  auto put_diag = [&]() {
+    const int rr = dk0 + lane;
+    double* dst = S + rr * SM_LD + dk0;
+    int tb = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const double v = da[j];
+      dst[j] = v;
+      const double lim = j < lane ? NOPIV_LMAX : bound;
+      const int in = (int)(rr < N) & (int)(dk0 + j < N);
+      tb |= in & ((int)!(fabs(v) <= lim) | ((int)(j == lane) & (int)!(fabs(v) > 0.0)));
+    }
+    bad |= tb;
+    L.y[rr] = dy;
+  };
   for (int KK = 0; KK < NB; ++KK) {
     const int k0 = 16 * KK;
     // ---- panel: rows k0 + lane (lane < 16) and k0 + 16 + 48·wv + lane − 16
@@ -424,6 +447,7 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
       for (int j = 0; j < 16; ++j) a[j] = rin ? src[j] : 0.0;
     }
     double rv = rin ? L.y[r] : 0.0;
+    if (wv == PW && lane < 16 && dk0 >= 0) put_diag();   // block KK − 1's (see above)
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       double pr[16];
@@ -459,9 +483,9 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
       for (int j = 0; j < 16; ++j) {
         const double v = a[j];
         dst[j] = v;
-        const double lim = (lane >= 16) | (j < lane) ? NOPIV_LMAX : bound;
-        const bool in = (r < N) & (k0 + j < N);
-        tb |= in & (!(fabs(v) <= lim) | ((j == lane) & !(fabs(v) > 0.0)));
+        const double lim = ((int)(lane >= 16) | (int)(j < lane)) ? NOPIV_LMAX : bound;
+        const int in = (int)(r < N) & (int)(k0 + j < N);
+        tb |= in & ((int)!(fabs(v) <= lim) | ((int)(j == lane) & (int)!(fabs(v) > 0.0)));
       }
       bad |= tb;
     };
@@ -500,14 +524,16 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         S[(k0 + i) * SM_LD + c] = u[i];
-        bad |= (k0 + i < N) & (c < N) & !(fabs(u[i]) <= bound);
+        bad |= (int)(k0 + i < N) & (int)(c < N) & (int)!(fabs(u[i]) <= bound);
       }
     }
     SB_LAP(1);
     __syncthreads();
-    if (wv == 0 && lane < 16) {
-      put_row();
-      L.y[r] = rv;
+    if (wv == PW && lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) da[j] = a[j];
+      dy = rv;
+      dk0 = k0;
     }
     SB_LAP(2);
     // ---- trailing update on MFMA: tile (I, C) −= L(I, KK)·U(KK, C)
@@ -529,6 +555,7 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
     __syncthreads();
     SB_LAP(3);
   }
+  if (wv == PW && lane < 16 && dk0 >= 0) put_diag();   // the last block's (the caller's barrier follows)
 #ifdef SM_STAMPS   // each wave's lane 0: stamp[4·wave + phase]
   if (lane == 0)
     for (int i = 0; i < 4; ++i) stamp[4 * wv + i] += (double)q_[i];
