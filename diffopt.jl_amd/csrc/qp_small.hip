@@ -413,27 +413,27 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
   const int NP = 16 * NB;
   double* Lw = L.lw[wv];   // this wave's copy of L_KK, column-major (L_ik at 16k + i)
   // The diagonal block's factors and y entries go to the image one block
-  // late, from the last wave's registers (every wave holds the same values;
-  // that wave has the fewest rows below): block KK's rows and columns are
-  // read by no later step, and a store right after the block's first barrier
-  // sat on wave 0's path to its trailing tiles.
-  constexpr int PW = SM_T / 64 - 1;
-  double da[16], dy = 0.0;
+  // late, four columns per wave from its registers (every wave holds the
+  // whole block): block KK's rows and columns are read by no later step, and
+  // one wave storing all of it right after the block's first barrier sat on
+  // that wave's path to its trailing tiles.
+  double da[4], dy = 0.0;
   int dk0 = -1;
   auto put_diag = [&]() {
     const int rr = dk0 + lane;
-    double* dst = S + rr * SM_LD + dk0;
+    double* dst = S + rr * SM_LD + dk0 + 4 * wv;
     int tb = 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const double v = da[j];
-      dst[j] = v;
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = 4 * wv + jj;
+      const double v = da[jj];
+      dst[jj] = v;
       const double lim = j < lane ? NOPIV_LMAX : bound;
       const int in = (int)(rr < N) & (int)(dk0 + j < N);
       tb |= in & ((int)!(fabs(v) <= lim) | ((int)(j == lane) & (int)!(fabs(v) > 0.0)));
     }
     bad |= tb;
-    L.y[rr] = dy;
+    if (wv == 0) L.y[rr] = dy;
   };
   for (int KK = 0; KK < NB; ++KK) {
     const int k0 = 16 * KK;
@@ -447,7 +447,7 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
       for (int j = 0; j < 16; ++j) a[j] = rin ? src[j] : 0.0;
     }
     double rv = rin ? L.y[r] : 0.0;
-    if (wv == PW && lane < 16 && dk0 >= 0) put_diag();   // block KK − 1's (see above)
+    if (lane < 16 && dk0 >= 0) put_diag();   // block KK − 1's (see above)
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       double pr[16];
@@ -502,7 +502,11 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
     // (lane ↔ column: conflict-free LDS rows; q = wv + 4·lane, eight lanes
     // to a bank, measured 29 k cycles per launch for this phase)
     const int ncol = NP - k0 - 16;
+#ifdef SM_UROW_W2   // (A/B: 64 columns per wave, waves 0 / 1 only: a quarter of the L_KK broadcasts)
+    const int cpw = 64;
+#else
     const int cpw = (ncol + SM_T / 64 - 1) / (SM_T / 64);
+#endif
     const int q = wv * cpw + lane;
     const int c = k0 + 16 + q;
     if (lane < cpw && q < ncol) {
@@ -529,9 +533,10 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
     }
     SB_LAP(1);
     __syncthreads();
-    if (wv == PW && lane < 16) {
+    if (lane < 16) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) da[j] = a[j];
+      for (int jj = 0; jj < 4; ++jj)   // (selects: no run-time register index)
+        da[jj] = wv == 0 ? a[jj] : wv == 1 ? a[4 + jj] : wv == 2 ? a[8 + jj] : a[12 + jj];
       dy = rv;
       dk0 = k0;
     }
@@ -555,7 +560,7 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
     __syncthreads();
     SB_LAP(3);
   }
-  if (wv == PW && lane < 16 && dk0 >= 0) put_diag();   // the last block's (the caller's barrier follows)
+  if (lane < 16 && dk0 >= 0) put_diag();   // the last block's (the caller's barrier follows)
 #ifdef SM_STAMPS   // each wave's lane 0: stamp[4·wave + phase]
   if (lane == 0)
     for (int i = 0; i < 4; ++i) stamp[4 * wv + i] += (double)q_[i];
