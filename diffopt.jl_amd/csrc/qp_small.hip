@@ -185,27 +185,20 @@ __device__ __forceinline__ double sm_assemble(const QPIn& P, const SmSrc& X, con
     for (int c8 = 0; c8 < 8; ++c8) {
       e[a][c8] = 0.0;
       if (a >= NB || c8 >= NB) continue;   // uniform
+      // the entry's block by selects, no branch (the if / else tree of
+      // round 5 diverged within each wave: ≈ 8 000 instructions, 20 k cycles)
       const int r = ti + SM_G * a, c = tj + SM_G * c8;
-      int which = 0;
-      SmOff<STG> off = 0;
-      double mul = 0.0, cv = r == c ? 1.0 : 0.0;
-      if (r < N && c < N) {
-        cv = 0.0;
-        mul = 1.0;
-        if (r < n) {
-          if (c < n) off = r + (SmOff<STG>)c * n;
-          else if (c < n + nk) { which = 1; off = ck[c8] + (SmOff<STG>)r * m; mul = cl[c8]; }
-          else { which = 2; off = (c - n - nk) + (SmOff<STG>)r * p; }
-        } else if (r < n + nk) {
-          if (c < n) { which = 1; off = rk[a] + (SmOff<STG>)c * m; }
-          else { mul = 0.0; cv = c == r ? rs[a] : 0.0; }
-        } else if (c < n) {
-          which = 2;
-          off = (r - n - nk) + (SmOff<STG>)c * p;
-        } else {
-          mul = 0.0;
-        }
-      }
+      const bool rQ = r < n, rG = (r >= n) & (r < n + nk), rA = (r >= n + nk) & (r < N);
+      const bool cQ = c < n, cG = (c >= n) & (c < n + nk), cA = (c >= n + nk) & (c < N);
+      const bool qq = rQ & cQ, qg = rQ & cG, gq = rG & cQ, qa = rQ & cA, aq = rA & cQ;
+      // (masked sums: a select chain here was still compiled into branches)
+      const int which = (int)(qg | gq) + 2 * (int)(qa | aq);
+      const SmOff<STG> off = (SmOff<STG>)qq * (r + (SmOff<STG>)c * n) + (SmOff<STG>)qg * (ck[c8] + (SmOff<STG>)r * m) +
+                             (SmOff<STG>)gq * (rk[a] + (SmOff<STG>)c * m) +
+                             (SmOff<STG>)qa * ((c - n - nk) + (SmOff<STG>)r * p) +
+                             (SmOff<STG>)aq * ((r - n - nk) + (SmOff<STG>)c * p);
+      const double mul = qg ? cl[c8] : (double)(int)(qq | gq | qa | aq);
+      const double cv = r != c ? 0.0 : rG ? rs[a] : r >= N ? 1.0 : 0.0;   // D(s_k); identity padding
       const double x = sm_src<STG>(L, X, which, off, n, m);
       e[a][c8] = mul != 0.0 ? x * mul : cv;
       if (r < N && c < N) amax = fmax(amax, fabs(e[a][c8]));
@@ -502,7 +495,7 @@ __device__ __forceinline__ void sm_lu_blocked(SmallLds& L, int N, int NB, double
     // (lane ↔ column: conflict-free LDS rows; q = wv + 4·lane, eight lanes
     // to a bank, measured 29 k cycles per launch for this phase)
     const int ncol = NP - k0 - 16;
-#ifdef SM_UROW_W2   // (A/B: 64 columns per wave, waves 0 / 1 only: a quarter of the L_KK broadcasts)
+#ifndef SM_UROW_W4   // 64 columns per wave, waves 0 / 1 (a quarter of the L_KK broadcasts: U rows 20 k → 15 k cycles per launch at config 1)
     const int cpw = 64;
 #else
     const int cpw = (ncol + SM_T / 64 - 1) / (SM_T / 64);
