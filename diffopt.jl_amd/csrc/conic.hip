@@ -554,6 +554,22 @@ constexpr int PAIR_ROWS = 64 * PAIR_K;
 // NV = 1 summation order exactly (the column chunk NC only groups loads), so
 // the co-iterated sequences are bit-identical to separate ones.  NC = 2 for
 // NV = 2 keeps two waves per SIMD.  ys: NV·4·PAIR_ROWS doubles.
+#ifndef DOPT_A_NT
+#define DOPT_A_NT 1
+#endif
+// A_moi's loads in the sweeps: non-temporal by default (round 6).  A is
+// re-read every LSQR iteration but is larger than the 256 MB Infinity Cache
+// at the configs that stream it (config 4: 1 GB, config 5: 0.8 GB), so it
+// never hits there; loaded with the default policy it evicts the vectors,
+// partial sums and states every launch re-reads.  Measured (same box,
+// two rounds each): config 5 LSQR 142.5 → 135.5 ms per step (107 → 112
+// solves/s), config 4 513.3 → 490.6 ms (997 → 1 043 solves/s).
+// DOPT_A_NT=0 builds the default-policy form.
+__device__ __forceinline__ double a_load(const double* p) {
+  if (DOPT_A_NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+
 template <int NV, int PK = PAIR_K, int NC = (NV == 1 ? PAIR_NC : 2), int NW = 4>
 __device__ __forceinline__ void gemv_multi(const double* __restrict__ A, int ld, int m, int n,
                                            const double* const* x, const double* const* w, double* const* y,
@@ -586,7 +602,7 @@ __device__ __forceinline__ void gemv_multi(const double* __restrict__ A, int ld,
       for (int c = 0; c < NC; ++c) {
         const double* cc = Ar + (size_t)(j + NW * c) * ld;
 #pragma unroll
-        for (int k = 0; k < PK; ++k) a[c][k] = ok[k] ? cc[64 * k] : 0.0;
+        for (int k = 0; k < PK; ++k) a[c][k] = ok[k] ? a_load(cc + 64 * k) : 0.0;
       }
       double sc[NV][NC];
 #pragma unroll
@@ -619,7 +635,7 @@ __device__ __forceinline__ void gemv_multi(const double* __restrict__ A, int ld,
       const double* c0 = Ar + (size_t)j * ld;
       double a0[PK];
 #pragma unroll
-      for (int k = 0; k < PK; ++k) a0[k] = ok[k] ? c0[64 * k] : 0.0;
+      for (int k = 0; k < PK; ++k) a0[k] = ok[k] ? a_load(c0 + 64 * k) : 0.0;
 #pragma unroll
       for (int q = 0; q < NV; ++q) {
         const double x0 = x[q][j];

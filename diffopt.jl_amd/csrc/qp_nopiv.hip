@@ -178,7 +178,13 @@ __device__ __forceinline__ QSrcB qsrc(const QSrc& s, int b, const QPMeta& mm) {
 // sources, plain pointers become flat loads, which count against the LDS
 // counter too (every LDS wait then drained them)
 typedef const double __attribute__((address_space(1))) gdouble;
-__device__ __forceinline__ double gload(const double* base, int off) { return ((gdouble*)base)[off]; }
+#ifndef DOPT_SRC_NT
+#define DOPT_SRC_NT 0
+#endif
+__device__ __forceinline__ double gload(const double* base, int off) {
+  if (DOPT_SRC_NT) return __builtin_nontemporal_load(&((gdouble*)base)[off]);
+  return ((gdouble*)base)[off];
+}
 
 // K[r][c] of the reduced system [Q, G_kᵀΛ, Aᵀ; G_k, D(s_k), 0; A, 0, 0]
 // (identity padding past N).  Branch-free: the source address is selected
