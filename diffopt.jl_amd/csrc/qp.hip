@@ -497,6 +497,9 @@ __global__ __launch_bounds__(TPB) void qp_fwd_rhs_kernel(
 // grid 2B — workgroups b < B the reverse outputs (x, out), b ≥ B the forward
 // ones of problem b − B (x1, out1): the light forward recovery rides beside the
 // reverse one's G reads instead of a launch of its own
+#ifndef DOPT_QP_NT
+#define DOPT_QP_NT 0   // G's loads in the reverse outputs' recovery: non-temporal
+#endif
 __global__ __launch_bounds__(TPB) void qp_output_kernel(
     const double* __restrict__ x0, const double* __restrict__ G,
     const double* __restrict__ s, const int32_t* __restrict__ rpos,
@@ -535,7 +538,8 @@ __global__ __launch_bounds__(TPB) void qp_output_kernel(
     for (; j + 8 <= n; j += 8) {
       double gv[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) gv[u] = Gb[l + (size_t)(j + u) * m];
+      for (int u = 0; u < 8; ++u)
+        gv[u] = DOPT_QP_NT ? __builtin_nontemporal_load(&Gb[l + (size_t)(j + u) * m]) : Gb[l + (size_t)(j + u) * m];
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc = fma(gv[u], xz[j + u], acc);
     }

@@ -55,8 +55,12 @@ constexpr int BUF_FLAGS = 0x00020000;   // raw buffer resource, word 3 (gfx9 fam
 typedef double dv2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32v2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32v4 __attribute__((ext_vector_type(4)));
+#ifndef DOPT_QP_NT
+#define DOPT_QP_NT 0
+#endif
+// G's once-per-step stream: cache policy nt (aux bit 1) under DOPT_QP_NT
 __device__ __forceinline__ dv2 bload2(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  return __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, DOPT_QP_NT ? 2 : 0));
 }
 __device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, unsigned off, double x) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32v2, x), r, off, 0, 0);
