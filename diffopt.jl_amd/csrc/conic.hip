@@ -570,7 +570,10 @@ __device__ __forceinline__ double a_load(const double* p) {
   return *p;
 }
 
-template <int NV, int PK = PAIR_K, int NC = (NV == 1 ? PAIR_NC : 2), int NW = 4>
+#ifndef DOPT_PAIR_NC2
+#define DOPT_PAIR_NC2 3   // columns in flight per wave for two sequences (co-iterated; round 6: 3 → config 4 490.6 → 486.1 ms, 2 the round-4 default, 4: 487.8, 1: 558.4)
+#endif
+template <int NV, int PK = PAIR_K, int NC = (NV == 1 ? PAIR_NC : DOPT_PAIR_NC2), int NW = 4>
 __device__ __forceinline__ void gemv_multi(const double* __restrict__ A, int ld, int m, int n,
                                            const double* const* x, const double* const* w, double* const* y,
                                            double* const* g, double* __restrict__ ys) {
