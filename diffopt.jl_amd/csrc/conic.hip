@@ -1348,7 +1348,11 @@ constexpr int SPLIT_CHUNK_MAX = 64;   // ... doubling per read-back up to this (
 #endif
 constexpr int SPLIT_K = DOPT_SPLIT_K;            // rows per lane of a split row block
 constexpr int SPLIT_ROWS = 64 * SPLIT_K;
-constexpr int SPLIT_FUSE_NMAX = 4096;   // fused form: u_n / v'_n of a sequence in LDS
+constexpr int SPLIT_FUSE_NMAX = 4096;
+#ifndef DOPT_SPLIT_NC2
+#define DOPT_SPLIT_NC2 3   // round 6 (non-temporal A): 3 → config-5 LSQR 135.5 → 134.8 ms, 4: 135.0
+#endif
+constexpr int SPLIT_NC2 = DOPT_SPLIT_NC2;   // columns in flight per wave, two sequences (split passes)   // fused form: u_n / v'_n of a sequence in LDS
 
 struct LsqrState {
   double alpha, beta, rhobar, phibar, anorm, ddnorm, xxnorm, zz, sn2, cs2, bnorm;
@@ -1431,7 +1435,7 @@ __global__ __launch_bounds__(64 * NW) void conic_split_pass_kernel(
     yb[c] = ws.mvec(ws.yb, bv) + r0;
     gp[c] = ws.gpart + ((size_t)bv * ws.RB + rb) * n;
   }
-  if (cnt == 2) gemv_multi<2, SPLIT_K, 2, NW>(Ab, m, rows, n, src, wv, yb, gp, ys);
+  if (cnt == 2) gemv_multi<2, SPLIT_K, SPLIT_NC2, NW>(Ab, m, rows, n, src, wv, yb, gp, ys);
   else gemv_multi<1, SPLIT_K, PAIR_NC, NW>(Ab, m, rows, n, src, wv, yb, gp, ys);
   const double* bb = bvec + (size_t)b * m + r0;
   for (int c = 0; c < cnt; ++c) {
@@ -1999,7 +2003,7 @@ __global__ __launch_bounds__(64 * NW) void conic_fsplit_pass_kernel(
   if (nl == 0) return;
   // two columns in flight per wave for two sequences, PAIR_NC for one (four
   // for two measured no faster, round 4: 170.7 vs 168.0 ms at config 5)
-  if (nl == 2) gemv_multi<2, SPLIT_K, 2, NW>(Ab, m, rows, n, xs, wv, yv, gv, ys);
+  if (nl == 2) gemv_multi<2, SPLIT_K, SPLIT_NC2, NW>(Ab, m, rows, n, xs, wv, yv, gv, ys);
   else gemv_multi<1, SPLIT_K, PAIR_NC, NW>(Ab, m, rows, n, xs, wv, yv, gv, ys);
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   for (int c = 0; c < nl; ++c) {
