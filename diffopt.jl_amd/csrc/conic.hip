@@ -1840,12 +1840,15 @@ struct FSplit {
   __device__ double* U(int p, int bv) const { return (p ? u1 : u0) + (size_t)bv * N; }
   __device__ double* V(int p, int bv) const { return (p ? v1 : v0) + (size_t)bv * N; }
   __device__ LsqrState* S(int p) const { return p ? s1 : s0; }
-  // partial slots per sequence: Σu'² [RB] | Σb·Dv [RB] | Σb·u_m [RB] | Σv'² [nc] | Σw² [2][nc]
+  // partial slots per sequence: Σu'² [RB] | Σb·Dv [RB] | Σb·u_m [RB] | Σv'² [nc] | Σw² [2][nc] | n part [2][CTPB]
   __device__ double* P(int bv) const { return part + (size_t)bv * PL; }
   __device__ int oPbd() const { return RB; }
   __device__ int oPbu() const { return 2 * RB; }
   __device__ int oPv() const { return 3 * RB; }
   __device__ int oPw(int p) const { return 3 * RB + nc + p * nc; }
+  // per-thread partial sums of v′'s n part (Σ val², Σ c·u_n), CTPB each:
+  // dpiU's extra workgroup writes them, dpiV reads them
+  __device__ int oPn() const { return 3 * RB + 3 * nc; }
 };
 
 // K block sums at once (fixed order: every workgroup of a launch that reduces
@@ -2050,14 +2053,40 @@ __global__ __launch_bounds__(64 * NW) void conic_fsplit_pass_kernel(
 // dpiU: one cone per workgroup; v' = Dπᵀ(tmpm) + u_m − βv on the cone's rows
 __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiU_kernel(
     const ConeDesc* __restrict__ cones_g, const double* __restrict__ vcone, const double* __restrict__ P,
-    int plen, FSplit fs, int par, double* __restrict__ gws, int wlen) {
+    int plen, const double* __restrict__ cvec, FSplit fs, int par, double* __restrict__ gws, int wlen) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ double red[4];
   const int k = blockIdx.x, bv = blockIdx.y, t = threadIdx.x;
   const LsqrState& st = fs.S(par)[bv];
   if (st.done || st.skipT) return;
-  const ConeDesc cd = cones_g[k];
   const int n = fs.n, m = fs.m;
+  if (k == fs.nc) {
+    // the extra workgroup: v′ on the n part, (Σ_rb gpT) − c·u_end − β·v, into
+    // v's next buffer unnormalised (dpiV divides by α there, as it does the
+    // cones' rows), and each thread's two partial sums in the order dpiV
+    // formed them itself before (round 6: every cone workgroup of dpiV
+    // re-reduced the RB·n partials)
+    const int N = fs.N, RB = fs.RB;
+    const double beta = st.beta;
+    const double* vo = fs.V(par, bv);
+    double* vn = fs.V(par ^ 1, bv);
+    const double* un = fs.U(par ^ 1, bv);
+    const double* c = cvec + (size_t)fs.phys(bv) * n;
+    const double ue = un[N - 1];
+    double a0 = 0.0, a1 = 0.0;
+    for (int j = t; j < n; j += CTPB) {
+      const double cj = c[j];
+      const double val = (gsum32(fs.gpT + (size_t)bv * RB * n, RB, n, j) - cj * ue) - beta * vo[j];
+      vn[j] = val;
+      a0 = fma(val, val, a0);
+      a1 = fma(cj, un[j], a1);
+    }
+    double* Pq = fs.P(bv) + fs.oPn();
+    Pq[t] = a0;
+    Pq[CTPB + t] = a1;
+    return;
+  }
+  const ConeDesc cd = cones_g[k];
   const double* pv = vcone + (size_t)fs.phys(bv) * m;
   const double* pp = P + (size_t)fs.phys(bv) * plen;
   double* vn = fs.V(par ^ 1, bv);
@@ -2121,17 +2150,8 @@ __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiV_kernel(
     double* vl = lds + img;
     double dvs = 1.0, vend_n = 0.0;
     if (!st.skipT) {
-      const double* un = fs.U(par ^ 1, bv);
-      const double* c = cvec + (size_t)fs.phys(bv) * n;
-      const double ue = un[N - 1];
-      double acc[2] = {0.0, 0.0};
-      for (int j = t; j < n; j += CTPB) {
-        const double cj = c[j];
-        const double val = (gsum32(fs.gpT + (size_t)bv * RB * n, RB, n, j) - cj * ue) - beta * vo[j];
-        vl[j] = val;
-        acc[0] = fma(val, val, acc[0]);
-        acc[1] = fma(cj, un[j], acc[1]);
-      }
+      // v′'s n part and its partial sums: dpiU's extra workgroup
+      double acc[2] = {Pq[fs.oPn() + t], Pq[fs.oPn() + CTPB + t]};
       for (int r = t; r < fs.nc; r += CTPB) acc[0] += Pq[fs.oPv() + r];
       for (int r = t; r < RB; r += CTPB) acc[1] += Pq[fs.oPbu() + r];
       bsumk<CTPB, 2>(acc, red);
@@ -2177,7 +2197,7 @@ __global__ __launch_bounds__(CTPB) void conic_fsplit_dpiV_kernel(
     };
     rows(rlo, rhi, false);
     if (k == 0) {
-      rows(0, n, !st.skipT);
+      rows(0, n, false);   // (v′'s n part in vn, from dpiU's extra workgroup)
       if (t == 0) {   // the end
         const double wo = w[N - 1];
         vn[N - 1] = vend_n;
@@ -2314,7 +2334,7 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
   // fused form: u_n of two sequences in the pass kernel's LDS, v'_n in dpiV's
   const bool fuse = h.split_fuse && nc > 0 && n <= SPLIT_FUSE_NMAX;
   const int ns = fuse && B >= 2 ? 2 : 1;   // batch slices
-  const int PL = 3 * RB + 3 * nc;
+  const int PL = 3 * RB + 3 * nc + 2 * CTPB;
   const size_t per = fuse ? (size_t)6 * N + 3 * M1 + (size_t)2 * RB * n + PL
                           : (size_t)5 * N + 4 * M1 + (size_t)RB * n;
   // one region per slice: vectors, then 2·V_s states, then the active counter
@@ -2431,7 +2451,7 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
                        tol1, S.ws, S.stv, S.active);
     passT(S);
     hipLaunchKernelGGL(conic_split_init2_kernel, dim3(S.V), dim3(VT), 0, S.st, S.bv, S.cv, S.ws, S.stv, S.active,
-                       fuse ? S.fs.part + S.fs.PL - 2 * nc : nullptr, PL, nc);
+                       fuse ? S.fs.part + 3 * RB + nc : nullptr, PL, nc);
   }
   ccheck();
   if (fuse) {
@@ -2451,8 +2471,8 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
       }
       hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 1>), dim3(RB, S.Bs), dim3(256), dlp, S.st, S.A, S.bv, S.cv,
                          S.fs, S.par, nq);
-      hipLaunchKernelGGL(conic_fsplit_dpiU_kernel, dim3(nc, S.V), dim3(CTPB), dl, S.st, cd, S.vcone, S.P, h.dpi_len,
-                         S.fs, S.par, S.gws, h.psd_big_len);
+      hipLaunchKernelGGL(conic_fsplit_dpiU_kernel, dim3(nc + 1, S.V), dim3(CTPB), dl, S.st, cd, S.vcone, S.P,
+                         h.dpi_len, S.cv, S.fs, S.par, S.gws, h.psd_big_len);
       dpiV(S, 0);
       S.par ^= 1;
     };
