@@ -1832,7 +1832,7 @@ __global__ __launch_bounds__(CTPB) void conic_split_out_kernel(
 // of one launch.
 // ---------------------------------------------------------------------------
 struct FSplit {
-  double *x, *w, *Dv, *tmpm, *yb, *gpM, *gpT, *part;
+  double *x, *w, *Dv, *tmpm, *yb, *gpM, *gpT, *part, *ut;
   double *u0, *u1, *v0, *v1;
   LsqrState *s0, *s1;
   int N, m, n, RB, B, nc, PL;
@@ -1840,7 +1840,8 @@ struct FSplit {
   __device__ double* U(int p, int bv) const { return (p ? u1 : u0) + (size_t)bv * N; }
   __device__ double* V(int p, int bv) const { return (p ? v1 : v0) + (size_t)bv * N; }
   __device__ LsqrState* S(int p) const { return p ? s1 : s0; }
-  // partial slots per sequence: Σu'² [RB] | Σb·Dv [RB] | Σb·u_m [RB] | Σv'² [nc] | Σw² [2][nc] | n part [2][CTPB]
+  // partial slots per sequence: Σu'² [RB] | Σb·Dv [RB] | Σb·u_m [RB] | Σv'² [nc] | Σw² [2][nc] | v′ n part [2][CTPB]
+  // | u′ n part [2][CTPB]
   __device__ double* P(int bv) const { return part + (size_t)bv * PL; }
   __device__ int oPbd() const { return RB; }
   __device__ int oPbu() const { return 2 * RB; }
@@ -1849,6 +1850,9 @@ struct FSplit {
   // per-thread partial sums of v′'s n part (Σ val², Σ c·u_n), CTPB each:
   // dpiU's extra workgroup writes them, dpiV reads them
   __device__ int oPn() const { return 3 * RB + 3 * nc; }
+  // per-thread partial sums of u′'s n part (Σ val², Σ c·v_n), CTPB each:
+  // conic_fsplit_uprep_kernel writes them (u′_n itself in ut), pass T reads them
+  __device__ int oPu() const { return 3 * RB + 3 * nc + 2 * CTPB; }
 };
 
 // K block sums at once (fixed order: every workgroup of a launch that reduces
@@ -1944,24 +1948,21 @@ __global__ __launch_bounds__(64 * NW) void conic_fsplit_pass_kernel(
     nl = cnt;
   } else {
     // prologue: u' on the n part and the end, β, u = u'/β
-    const double* c = cvec + (size_t)b * n;
-    double al[2] = {0.0, 0.0}, ve[2] = {0.0, 0.0}, acc[4] = {0.0, 0.0, 0.0, 0.0};
+    double al[2] = {0.0, 0.0}, acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int ci = 0; ci < cnt; ++ci) al[ci] = S[sq[ci]].alpha;
+    // u′'s n part and its per-thread partial sums: conic_fsplit_uprep_kernel
+    // (once per sequence; every workgroup here re-reduced the RB·n partials
+    // before, round 6)
+    static_assert(TPB == CTPB, "uprep's partial sums are per CTPB thread");
     for (int ci = 0; ci < cnt; ++ci) {
-      al[ci] = S[sq[ci]].alpha;
-      ve[ci] = fs.V(par, sq[ci])[N - 1];
+      const double* Pu = fs.P(sq[ci]) + fs.oPu();
+      acc[2 * ci] = Pu[t];
+      acc[2 * ci + 1] = Pu[CTPB + t];
     }
     for (int j = t; j < n; j += TPB) {
-      const double cj = c[j];
 #pragma unroll
       for (int ci = 0; ci < 2; ++ci)
-        if (ci < cnt) {
-          const int bv = sq[ci];
-          const double g = gsum32(fs.gpM + (size_t)bv * RB * n, RB, n, j);
-          const double val = (-g + cj * ve[ci]) - al[ci] * fs.U(par, bv)[j];
-          ul[ci * n + j] = val;
-          acc[2 * ci] = fma(val, val, acc[2 * ci]);
-          acc[2 * ci + 1] = fma(cj, fs.V(par, bv)[j], acc[2 * ci + 1]);
-        }
+        if (ci < cnt) ul[ci * n + j] = fs.ut[(size_t)sq[ci] * n + j];
     }
     for (int ci = 0; ci < cnt; ++ci) {
       const double* Pq = fs.P(sq[ci]);
@@ -2048,6 +2049,35 @@ __global__ __launch_bounds__(64 * NW) void conic_fsplit_pass_kernel(
         Pq[fs.oPbu() + rb] = acc[2 * c];
       }
     }
+}
+
+// uprep (between pass M and pass T): u′ on the n part, −(Σ_rb gpM) + c·v_end −
+// α·u, into ut, and each thread's partial sums in the order pass T formed
+// them itself before (its prologue: Σ val², Σ c·v_n per thread of CTPB)
+__global__ __launch_bounds__(CTPB) void conic_fsplit_uprep_kernel(const double* __restrict__ cvec, FSplit fs,
+                                                                  int par) {
+  const int bv = blockIdx.x, t = threadIdx.x;
+  const LsqrState& st = fs.S(par)[bv];
+  if (st.done) return;
+  const int n = fs.n, N = fs.N, RB = fs.RB;
+  const double al = st.alpha;
+  const double* vv = fs.V(par, bv);
+  const double ve = vv[N - 1];
+  const double* uo = fs.U(par, bv);
+  const double* c = cvec + (size_t)fs.phys(bv) * n;
+  double* ut = fs.ut + (size_t)bv * n;
+  double a0 = 0.0, a1 = 0.0;
+  for (int j = t; j < n; j += CTPB) {
+    const double cj = c[j];
+    const double g = gsum32(fs.gpM + (size_t)bv * RB * n, RB, n, j);
+    const double val = (-g + cj * ve) - al * uo[j];
+    ut[j] = val;
+    a0 = fma(val, val, a0);
+    a1 = fma(cj, vv[j], a1);
+  }
+  double* Pu = fs.P(bv) + fs.oPu();
+  Pu[t] = a0;
+  Pu[CTPB + t] = a1;
 }
 
 // dpiU: one cone per workgroup; v' = Dπᵀ(tmpm) + u_m − βv on the cone's rows
@@ -2334,8 +2364,8 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
   // fused form: u_n of two sequences in the pass kernel's LDS, v'_n in dpiV's
   const bool fuse = h.split_fuse && nc > 0 && n <= SPLIT_FUSE_NMAX;
   const int ns = fuse && B >= 2 ? 2 : 1;   // batch slices
-  const int PL = 3 * RB + 3 * nc + 2 * CTPB;
-  const size_t per = fuse ? (size_t)6 * N + 3 * M1 + (size_t)2 * RB * n + PL
+  const int PL = 3 * RB + 3 * nc + 4 * CTPB;
+  const size_t per = fuse ? (size_t)6 * N + 3 * M1 + (size_t)2 * RB * n + PL + n
                           : (size_t)5 * N + 4 * M1 + (size_t)RB * n;
   // one region per slice: vectors, then 2·V_s states, then the active counter
   const int Bs0 = (B + ns - 1) / ns;
@@ -2386,6 +2416,7 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
       fs.gpM = fs.yb + (size_t)V * M1;
       fs.gpT = fs.gpM + (size_t)V * RB * n;
       fs.part = fs.gpT + (size_t)V * RB * n;
+      fs.ut = fs.part + (size_t)V * PL;
       fs.s0 = reinterpret_cast<LsqrState*>(base + (size_t)V * per);
       fs.s1 = fs.s0 + V;
       fs.N = N;
@@ -2469,6 +2500,7 @@ static void conic_lsqr_split(Handle& h, int nq, double tol0, double tol1, const 
         DOPT_CHECK_HIP(hipEventRecord(h.ev_join, S.st));
         DOPT_CHECK_HIP(hipStreamWaitEvent(sl[1].st, h.ev_join, 0));
       }
+      hipLaunchKernelGGL(conic_fsplit_uprep_kernel, dim3(S.V), dim3(CTPB), 0, S.st, S.cv, S.fs, S.par);
       hipLaunchKernelGGL((conic_fsplit_pass_kernel<4, 1>), dim3(RB, S.Bs), dim3(256), dlp, S.st, S.A, S.bv, S.cv,
                          S.fs, S.par, nq);
       hipLaunchKernelGGL(conic_fsplit_dpiU_kernel, dim3(nc + 1, S.V), dim3(CTPB), dl, S.st, cd, S.vcone, S.P,
